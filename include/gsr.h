@@ -1,0 +1,139 @@
+/*
+ * gsr.h -- C ABI of the MI355X-native differentiable Gaussian rasterizer
+ * (libgsr.so, built from splatam_amd/csrc/*.hip for gfx950).
+ *
+ * This is the drop-in boundary for the reference's torch extension `_C`
+ * (hessian-diff-gaussian-rasterization-w-depth/ext.cpp:15-18).  Every entry
+ * point takes plain device pointers, sizes and a hipStream_t (as void*); no
+ * torch types cross it.  The Python binding splatam_amd/_C.py (ctypes) is the
+ * ~100-line tensor -> pointer marshalling layer on top of it; INTEGRATION.md
+ * shows the binding a maintainer would add on the reference side.
+ *
+ * Conventions:
+ *   - every float array is float32, contiguous, on the device the stream belongs to;
+ *   - "absent" inputs (shs, colors_precomp, scales, rotations, cov3D_precomp)
+ *     are NULL pointers (the reference turns an empty tensor into nullptr);
+ *   - viewmatrix / projmatrix are the reference's column-major 4x4 (16 floats,
+ *     element (r,c) at index 4c+r), campos / bg are 3 floats, all on device;
+ *   - opaque state buffers are allocated through the caller's allocator
+ *     callback and must be passed back unchanged to gsr_backward;
+ *   - all work is enqueued on `stream`; gsr_forward synchronises the stream
+ *     once to read num_rendered (rasterizer_impl.cu:282 does the same);
+ *   - negative return values are errors; gsr_last_error() gives the message
+ *     (thread-local).  No global state: re-entrant across devices/threads.
+ */
+#ifndef GSR_H
+#define GSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_ABI_VERSION 1
+
+/* error codes */
+#define GSR_OK 0
+#define GSR_ERR_INVALID_ARG (-1)
+#define GSR_ERR_ALLOC (-2)
+#define GSR_ERR_HIP (-3)
+#define GSR_ERR_PREFILTERED (-4) /* auxiliary.h:154-160 traps; we report instead */
+
+/* buffer kinds handed to the allocator callback */
+#define GSR_BUF_GEOM 0    /* per-Gaussian state   (reference geomBuffer)    */
+#define GSR_BUF_BINNING 1 /* per-instance state   (reference binningBuffer) */
+#define GSR_BUF_IMAGE 2   /* per-pixel/tile state (reference imgBuffer)     */
+#define GSR_BUF_SCRATCH 3 /* backward scratch, released by the caller after gsr_backward */
+
+/* Returns a device pointer to at least `bytes` bytes (256-byte aligned), or
+ * NULL on failure.  Replaces resizeFunctional (rasterize_points.cu:27-33). */
+typedef void* (*gsr_alloc_fn)(void* ctx, int kind, size_t bytes);
+
+/* GaussianRasterizationSettings (hessian_diff_gaussian_rasterization_w_depth/__init__.py:140-151) */
+typedef struct gsr_settings {
+    int image_height;
+    int image_width;
+    float tan_fovx;
+    float tan_fovy;
+    const float* bg;          /* [3] */
+    float scale_modifier;
+    const float* viewmatrix;  /* [16] column-major */
+    const float* projmatrix;  /* [16] column-major */
+    int sh_degree;
+    const float* campos;      /* [3] */
+    int prefiltered;
+} gsr_settings;
+
+/* Per-Gaussian inputs (rasterize_points.cu:36-54 argument list) */
+typedef struct gsr_gaussians {
+    int P;                      /* number of Gaussians */
+    int M;                      /* SH coefficients per Gaussian (0 when shs == NULL) */
+    const float* means3D;       /* [P,3] */
+    const float* shs;           /* [P,M,3] or NULL */
+    const float* colors_precomp;/* [P,3]   or NULL */
+    const float* opacities;     /* [P,1] */
+    const float* scales;        /* [P,3]   or NULL */
+    const float* rotations;     /* [P,4]   or NULL (w,x,y,z; not normalised in-kernel) */
+    const float* cov3D_precomp; /* [P,6]   or NULL */
+} gsr_gaussians;
+
+/* Output of rasterize_gaussians_backward (rasterize_points.cu:195), all
+ * written in full by gsr_backward (no zero-initialisation needed). */
+typedef struct gsr_grads {
+    float* dmeans2D;    /* [P,3] (z component 0) */
+    float* dcolors;     /* [P,3] */
+    float* dopacity;    /* [P,1] */
+    float* dmeans3D;    /* [P,3] */
+    float* dcov3D;      /* [P,6] */
+    float* dsh;         /* [P,M,3] (NULL allowed when M == 0) */
+    float* dscales;     /* [P,3] */
+    float* drotations;  /* [P,4] */
+} gsr_grads;
+
+/* Forward rasterization.  Replaces CudaRasterizer::Rasterizer::forward
+ * (rasterizer_impl.cu:198-339) behind RasterizeGaussiansCUDA
+ * (rasterize_points.cu:35-115).  Writes out_color [3,H,W], out_depth [1,H,W]
+ * (median depth, 15 when T never crosses 0.5) and radii [P].  Returns
+ * num_rendered (>= 0) or a negative error code. */
+int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians,
+                float* out_color, float* out_depth, int* radii,
+                gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
+/* Backward.  Replaces CudaRasterizer::Rasterizer::backward
+ * (rasterizer_impl.cu:343-434) behind RasterizeGaussiansBackwardCUDA
+ * (rasterize_points.cu:117-196).  `power` is the vendored fork's
+ * backward_power (backward.cu:1093-1137): gradients are summed over
+ * (pixel, Gaussian) pairs of powf(per-pair gradient, power); power == 1 is the
+ * standard 3DGS backward.  H/W come from settings (the reference reads them
+ * from dL_dout_color).  Returns GSR_OK or a negative error code. */
+int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians,
+                 const int* radii, const float* dL_dout_color, int num_rendered,
+                 const void* geom_buffer, const void* binning_buffer, const void* image_buffer,
+                 int power, const gsr_grads* grads,
+                 gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
+/* Frustum test view_z > 0.001.  Replaces markVisible / checkFrustum
+ * (rasterize_points.cu:198-216, rasterizer_impl.cu:54-67,141-153).
+ * visible: [P] bytes (0/1, torch.bool layout). */
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix,
+                     const float* projmatrix, uint8_t* visible, void* stream);
+
+/* Byte sizes of the opaque buffers (for tests and pre-sizing). */
+size_t gsr_geom_buffer_bytes(int P);
+size_t gsr_binning_buffer_bytes(int num_rendered, int image_width, int image_height);
+size_t gsr_image_buffer_bytes(int image_width, int image_height);
+
+const char* gsr_last_error(void);
+int gsr_abi_version(void);
+
+/* Test hook (tests/test_gpu_kernels.py): wave64 transposed reduction of
+ * in_dev[64*9] (lane-major) into out_dev[9]; checks the permlane/DPP lane
+ * mapping the backward relies on. */
+int gsr_selftest_reduce9(const float* in_dev, float* out_dev, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_H */

@@ -1,0 +1,123 @@
+"""Parity harness: runs the same scene through the product rasterizer
+(splatam_amd, HIP) and through the CPU oracle, and compares.
+
+TEST INFRASTRUCTURE ONLY (used by tests/, __graft_entry__.smoke and bench.py's
+cpu_baseline).  The product path never imports this module.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import oracle
+
+GRAD_KEYS = ("dmeans2D", "dcolors", "dopacity", "dmeans3D", "dcov3D", "dsh", "dscales", "drot")
+
+
+def cov3d_from(scales, rotations, mod=1.0):
+    """Upper-triangle Sigma = R S^2 R^T (forward.cu:118-152) in float64 torch."""
+    q = rotations.double()
+    r, x, y, z = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    R = torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y),
+                     2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x),
+                     2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], 1).reshape(-1, 3, 3)
+    s = mod * scales.double()
+    S = R @ torch.diag_embed(s * s) @ R.transpose(1, 2)
+    return torch.stack([S[:, 0, 0], S[:, 0, 1], S[:, 0, 2], S[:, 1, 1], S[:, 1, 2], S[:, 2, 2]], 1).float()
+
+
+def run_oracle(scene, dL_dcolor=None, *, bg=(0.0, 0.0, 0.0), use_sh=False, use_cov=False, power=1,
+               mode=oracle.UPSTREAM, dtype=np.float32, scale_modifier=1.0, backward=True):
+    c = scene.cam
+    kw = dict(view=c.viewmatrix.numpy(), proj=c.projmatrix.numpy(), campos=c.campos.numpy(), tanfovx=c.tanfovx,
+              tanfovy=c.tanfovy, H=c.H, W=c.W, bg=np.asarray(bg, np.float32), scale_modifier=scale_modifier,
+              dtype=dtype)
+    if use_sh:
+        kw.update(shs=scene.shs.numpy(), sh_degree=scene.sh_degree)
+    else:
+        kw.update(colors=scene.colors.numpy())
+    if use_cov:
+        kw.update(cov3D=cov3d_from(scene.scales, scene.rotations, 1.0).numpy())
+    else:
+        kw.update(scales=scene.scales.numpy(), rotations=scene.rotations.numpy())
+    fr = oracle.forward(scene.means3D.numpy(), scene.opacities.numpy(), **kw)
+    grads = None
+    if backward:
+        if dL_dcolor is None:
+            dL_dcolor = np.ones((3, c.H, c.W), np.float32)
+        m = mode if power == 1 else oracle.FUSED
+        grads = oracle.backward(fr, np.asarray(dL_dcolor), power=power, mode=m)
+    return fr, grads
+
+
+def run_gpu(scene, dL_dcolor=None, *, device="cuda:0", bg=(0.0, 0.0, 0.0), use_sh=False, use_cov=False, power=1,
+            scale_modifier=1.0, backward=True):
+    """Runs the product rasterizer (splatam_amd.GaussianRasterizer) and returns numpy results."""
+    from splatam_amd.rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+    c = scene.cam
+    dev = torch.device(device)
+    st = GaussianRasterizationSettings(
+        image_height=c.H, image_width=c.W, tanfovx=c.tanfovx, tanfovy=c.tanfovy,
+        bg=torch.tensor(bg, dtype=torch.float32, device=dev), scale_modifier=scale_modifier,
+        viewmatrix=c.viewmatrix.to(dev), projmatrix=c.projmatrix.to(dev), sh_degree=scene.sh_degree if use_sh else 0,
+        campos=c.campos.to(dev), prefiltered=False)
+    leaf = lambda t: t.detach().to(dev).clone().requires_grad_(True)  # noqa: E731
+    means3D = leaf(scene.means3D)
+    means2D = torch.zeros_like(means3D, requires_grad=True)
+    opac = leaf(scene.opacities)
+    kw = {}
+    if use_sh:
+        kw["shs"] = leaf(scene.shs)
+    else:
+        kw["colors_precomp"] = leaf(scene.colors)
+    if use_cov:
+        kw["cov3D_precomp"] = leaf(cov3d_from(scene.scales, scene.rotations, 1.0))
+    else:
+        kw["scales"] = leaf(scene.scales)
+        kw["rotations"] = leaf(scene.rotations)
+    ras = GaussianRasterizer(st, backward_power=power)
+    color, radii, depth = ras(means3D=means3D, means2D=means2D, opacities=opac, **kw)
+    out = dict(color=color.detach().cpu().numpy(), depth=depth.detach().cpu().numpy(),
+               radii=radii.cpu().numpy())
+    if backward:
+        if dL_dcolor is None:
+            dL_dcolor = np.ones((3, c.H, c.W), np.float32)
+        color.backward(torch.as_tensor(np.asarray(dL_dcolor, np.float32), device=dev))
+        g = dict(dmeans3D=means3D.grad, dmeans2D=means2D.grad, dopacity=opac.grad)
+        if use_sh:
+            g["dsh"] = kw["shs"].grad
+        else:
+            g["dcolors"] = kw["colors_precomp"].grad
+        if use_cov:
+            g["dcov3D"] = kw["cov3D_precomp"].grad
+        else:
+            g["dscales"] = kw["scales"].grad
+            g["drot"] = kw["rotations"].grad
+        out["grads"] = {k: v.detach().cpu().numpy() for k, v in g.items()}
+    return out
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    nb = np.linalg.norm(b)
+    return float(np.linalg.norm(a - b) / nb) if nb > 0 else float(np.linalg.norm(a - b))
+
+
+def compare_forward(gpu, fr, *, atol=1e-4):
+    """SURVEY.md 8(c) forward criterion: |d| <= atol*max(1,|ref|) on >= 99.9 % of pixels."""
+    c = np.asarray(gpu["color"], np.float64)
+    r = fr.color.astype(np.float64)
+    bad = np.abs(c - r) > atol * np.maximum(1.0, np.abs(r))
+    pix_bad = bad.any(axis=0)
+    depth_match = float((np.asarray(gpu["depth"]) == fr.depth).mean())
+    return dict(frac_bad=float(pix_bad.mean()), max_abs=float(np.abs(c - r).max()),
+                radii_match=float((gpu["radii"] == fr.radii).mean()), depth_match=depth_match)
+
+
+def compare_grads(gpu_grads, ref_grads):
+    out = {}
+    for k, v in gpu_grads.items():
+        ref = ref_grads[k].reshape(v.shape)
+        out[k] = rel_l2(v, ref)
+    return out

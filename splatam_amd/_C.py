@@ -1,0 +1,179 @@
+"""Torch <-> C-ABI marshalling for libgsr.so: the drop-in for the reference's
+pybind11 extension ``_C`` (hessian-diff-gaussian-rasterization-w-depth/ext.cpp:15-18).
+
+Same three functions, same positional arguments, same return tuples as
+rasterize_points.cu:35-216.  Tensors are turned into raw device pointers
+(``.contiguous()`` float32, empty tensor -> NULL exactly like the reference's
+``data_ptr()`` of an empty tensor), the current torch stream of the Gaussians'
+device is passed down, and the opaque state buffers are allocated as uint8
+torch tensors through the C allocator callback (replacing
+``resizeFunctional``, rasterize_points.cu:27-33).
+
+There is no CPU fallback: if libgsr.so is missing or the tensors are not on a
+ROCm device, these functions raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import torch
+
+from ._lib import ALLOC_FN, GsrGaussians, GsrGrads, GsrSettings, lib
+
+_tls = threading.local()
+
+
+def _alloc(ctx, kind, nbytes):  # called from C, under the GIL
+    try:
+        t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=_tls.device)
+        _tls.buffers[int(kind)] = t
+        return t.data_ptr()
+    except Exception as exc:  # pragma: no cover - reported through the NULL return
+        _tls.alloc_error = exc
+        return None
+
+
+_ALLOC_CB = ALLOC_FN(_alloc)
+
+
+def _begin(device):
+    _tls.device = device
+    _tls.buffers = {}
+    _tls.alloc_error = None
+
+
+def _check(rc: int, what: str):
+    if rc < 0:
+        err = getattr(_tls, "alloc_error", None)
+        msg = lib.gsr_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what}: {msg}" + (f" ({err})" if err else ""))
+
+
+def _dev_f32(t: torch.Tensor, device, name: str) -> torch.Tensor | None:
+    """Contiguous float32 on `device`, or None for an empty tensor (-> NULL)."""
+    if t is None or t.numel() == 0:
+        return None
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name}: expected scalar type Float but found {t.dtype}")
+    if t.device != device:
+        t = t.to(device)
+    return t.contiguous()
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _settings(bg, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, scale_modifier, degree, prefiltered,
+              device):
+    keep = [_dev_f32(bg, device, "bg"), _dev_f32(viewmatrix, device, "viewmatrix"),
+            _dev_f32(projmatrix, device, "projmatrix"), _dev_f32(campos, device, "campos")]
+    s = GsrSettings(image_height=int(H), image_width=int(W), tan_fovx=float(tan_fovx), tan_fovy=float(tan_fovy),
+                    bg=_ptr(keep[0]), scale_modifier=float(scale_modifier), viewmatrix=_ptr(keep[1]),
+                    projmatrix=_ptr(keep[2]), sh_degree=int(degree), campos=_ptr(keep[3]),
+                    prefiltered=int(bool(prefiltered)))
+    return s, keep
+
+
+def _gaussians(means3D, sh, colors, opacity, scales, rotations, cov3D_precomp, device):
+    P = means3D.size(0)
+    M = sh.size(1) if (sh is not None and sh.numel() > 0 and sh.dim() >= 2 and sh.size(0) != 0) else 0
+    keep = [_dev_f32(means3D, device, "means3D"), _dev_f32(sh, device, "sh") if M else None,
+            _dev_f32(colors, device, "colors"), _dev_f32(opacity, device, "opacity"),
+            _dev_f32(scales, device, "scales"), _dev_f32(rotations, device, "rotations"),
+            _dev_f32(cov3D_precomp, device, "cov3D_precomp")]
+    g = GsrGaussians(P=P, M=M, means3D=_ptr(keep[0]), shs=_ptr(keep[1]), colors_precomp=_ptr(keep[2]),
+                     opacities=_ptr(keep[3]), scales=_ptr(keep[4]), rotations=_ptr(keep[5]),
+                     cov3D_precomp=_ptr(keep[6]))
+    return g, keep, M
+
+
+def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                        viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                        prefiltered):
+    """RasterizeGaussiansCUDA (rasterize_points.cu:35-115).
+
+    Returns (num_rendered, color[3,H,W], radii[P] int32, geomBuffer, binningBuffer, imgBuffer, depth[1,H,W]).
+    """
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    device = means3D.device
+    if device.type != "cuda":
+        raise RuntimeError("splatam_amd rasterizer runs on ROCm devices only (no CPU fallback); "
+                           f"means3D is on {device}")
+    P = means3D.size(0)
+    H, W = int(image_height), int(image_width)
+    f32 = dict(dtype=torch.float32, device=device)
+    if P == 0:
+        empty = torch.empty(0, dtype=torch.uint8, device=device)
+        return (0, torch.zeros(3, H, W, **f32), torch.zeros(0, dtype=torch.int32, device=device), empty,
+                empty.clone(), empty.clone(), torch.zeros(1, H, W, **f32))
+    with torch.cuda.device(device):
+        s, keep_s = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, scale_modifier,
+                              degree, prefiltered, device)
+        g, keep_g, _ = _gaussians(means3D, sh, colors, opacity, scales, rotations, cov3D_precomp, device)
+        out_color = torch.empty(3, H, W, **f32)
+        out_depth = torch.empty(1, H, W, **f32)
+        radii = torch.empty(P, dtype=torch.int32, device=device)
+        _begin(device)
+        n = lib.gsr_forward(ctypes.byref(s), ctypes.byref(g), out_color.data_ptr(), out_depth.data_ptr(),
+                            radii.data_ptr(), _ALLOC_CB, None, _stream(device))
+        _check(n, "rasterize_gaussians")
+        bufs = _tls.buffers
+        return (int(n), out_color, radii, bufs[0], bufs[1], bufs[2], out_depth)
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
+                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree,
+                                 campos, geomBuffer, R, binningBuffer, imageBuffer, power=1):
+    """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:117-196).
+
+    Returns (dmeans2D[P,3], dcolors[P,3], dopacity[P,1], dmeans3D[P,3], dcov3D[P,6], dsh[P,M,3],
+    dscales[P,3], drotations[P,4]).
+    """
+    device = means3D.device
+    P = means3D.size(0)
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    M = sh.size(1) if (sh is not None and sh.numel() > 0 and sh.size(0) != 0) else 0
+    f32 = dict(dtype=torch.float32, device=device)
+    out = [torch.empty(P, 3, **f32), torch.empty(P, 3, **f32), torch.empty(P, 1, **f32), torch.empty(P, 3, **f32),
+           torch.empty(P, 6, **f32), torch.empty(P, M, 3, **f32), torch.empty(P, 3, **f32), torch.empty(P, 4, **f32)]
+    if P == 0:
+        return tuple(out)
+    with torch.cuda.device(device):
+        s, keep_s = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, scale_modifier,
+                              degree, False, device)
+        # opacities are not an input of the backward (rasterize_points.cu:117-139): they live in geomBuffer
+        g, keep_g, _ = _gaussians(means3D, sh, colors, None, scales, rotations, cov3D_precomp, device)
+        dpix = _dev_f32(dL_dout_color, device, "dL_dout_color")
+        radii_c = radii.to(device=device, dtype=torch.int32).contiguous()
+        grads = GsrGrads(*[o.data_ptr() if o.numel() > 0 else None for o in out])
+        _begin(device)
+        rc = lib.gsr_backward(ctypes.byref(s), ctypes.byref(g), radii_c.data_ptr(), dpix.data_ptr(), int(R),
+                              geomBuffer.data_ptr(), binningBuffer.data_ptr() if binningBuffer.numel() else None,
+                              imageBuffer.data_ptr(), int(power), ctypes.byref(grads), _ALLOC_CB, None,
+                              _stream(device))
+        _check(rc, "rasterize_gaussians_backward")
+        _tls.buffers = {}  # scratch is released to torch's caching allocator (stream-ordered)
+        return tuple(out)
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    """markVisible (rasterize_points.cu:198-216): bool[P], view_z > 0.001."""
+    device = means3D.device
+    P = means3D.size(0)
+    present = torch.zeros(P, dtype=torch.bool, device=device)
+    if P == 0:
+        return present
+    with torch.cuda.device(device):
+        m = _dev_f32(means3D, device, "means3D")
+        v = _dev_f32(viewmatrix, device, "viewmatrix")
+        p = _dev_f32(projmatrix, device, "projmatrix")
+        rc = lib.gsr_mark_visible(P, m.data_ptr(), v.data_ptr(), p.data_ptr(), present.data_ptr(), _stream(device))
+        _check(rc, "mark_visible")
+    return present

@@ -1,0 +1,69 @@
+"""Loads libgsr.so (the C ABI of include/gsr.h) with ctypes.
+
+Fails loudly: there is no CPU or eager-PyTorch fallback for the rasterizer.
+Set GSR_LIB to load a library from another path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GSR_LIB", os.path.join(_HERE, "libgsr.so"))
+
+c_int, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+
+
+class GsrSettings(ctypes.Structure):
+    """gsr_settings (include/gsr.h)."""
+    _fields_ = [("image_height", c_int), ("image_width", c_int), ("tan_fovx", c_float), ("tan_fovy", c_float),
+                ("bg", c_void_p), ("scale_modifier", c_float), ("viewmatrix", c_void_p), ("projmatrix", c_void_p),
+                ("sh_degree", c_int), ("campos", c_void_p), ("prefiltered", c_int)]
+
+
+class GsrGaussians(ctypes.Structure):
+    """gsr_gaussians (include/gsr.h)."""
+    _fields_ = [("P", c_int), ("M", c_int), ("means3D", c_void_p), ("shs", c_void_p), ("colors_precomp", c_void_p),
+                ("opacities", c_void_p), ("scales", c_void_p), ("rotations", c_void_p), ("cov3D_precomp", c_void_p)]
+
+
+class GsrGrads(ctypes.Structure):
+    """gsr_grads (include/gsr.h)."""
+    _fields_ = [("dmeans2D", c_void_p), ("dcolors", c_void_p), ("dopacity", c_void_p), ("dmeans3D", c_void_p),
+                ("dcov3D", c_void_p), ("dsh", c_void_p), ("dscales", c_void_p), ("drotations", c_void_p)]
+
+
+ALLOC_FN = ctypes.CFUNCTYPE(c_void_p, c_void_p, c_int, c_size_t)
+
+# every symbol declared in include/gsr.h: (name, restype, argtypes)
+SIGNATURES = {
+    "gsr_forward": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p, c_void_p, c_void_p,
+                            ALLOC_FN, c_void_p, c_void_p]),
+    "gsr_backward": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p, c_void_p, c_int,
+                             c_void_p, c_void_p, c_void_p, c_int, ctypes.POINTER(GsrGrads), ALLOC_FN, c_void_p,
+                             c_void_p]),
+    "gsr_mark_visible": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gsr_geom_buffer_bytes": (c_size_t, [c_int]),
+    "gsr_binning_buffer_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "gsr_image_buffer_bytes": (c_size_t, [c_int, c_int]),
+    "gsr_last_error": (ctypes.c_char_p, []),
+    "gsr_abi_version": (c_int, []),
+    "gsr_selftest_reduce9": (c_int, [c_void_p, c_void_p, c_void_p]),
+}
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(f"libgsr.so not found at {path}: build it with `python -m splatam_amd.build` "
+                          "(no CPU fallback exists for the rasterizer)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.gsr_abi_version() != 1:
+        raise ImportError("libgsr.so ABI version mismatch")
+    return lib
+
+
+lib = load()

@@ -1,0 +1,242 @@
+// gsr_capi.hip -- extern "C" entry points of libgsr.so (see include/gsr.h).
+//
+// Host orchestration of one rasterization, the counterpart of
+// CudaRasterizer::Rasterizer::{forward,backward,markVisible}
+// (rasterizer_impl.cu:141-434).  Everything is enqueued on the caller's
+// stream; the only host synchronisation is the read-back of num_rendered
+// (the reference's cudaMemcpy at rasterizer_impl.cu:282), done through a
+// pinned per-thread staging word.
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/gsr.h"
+#include "gsr_common.h"
+
+using namespace gsr;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+    return fail(GSR_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+struct Pinned {
+    uint32_t* p = nullptr;
+    ~Pinned() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+thread_local Pinned g_pinned;
+
+Camera make_camera(const gsr_settings* s) {
+    Camera c;
+    c.W = s->image_width;
+    c.H = s->image_height;
+    c.tan_fovx = s->tan_fovx;
+    c.tan_fovy = s->tan_fovy;
+    c.focal_y = (float)c.H / (2.0f * s->tan_fovy);  // rasterizer_impl.cu:222-223
+    c.focal_x = (float)c.W / (2.0f * s->tan_fovx);
+    c.gx = (c.W + TILE_X - 1) / TILE_X;
+    c.gy = (c.H + TILE_Y - 1) / TILE_Y;
+    c.view = s->viewmatrix;
+    c.proj = s->projmatrix;
+    c.campos = s->campos;
+    c.bg = s->bg;
+    c.scale_modifier = s->scale_modifier;
+    c.sh_degree = s->sh_degree;
+    c.prefiltered = s->prefiltered;
+    return c;
+}
+
+GaussIn make_gauss(const gsr_gaussians* g) {
+    GaussIn o;
+    o.P = g->P;
+    o.M = g->shs ? g->M : 0;
+    o.means3D = g->means3D;
+    o.shs = (g->shs && g->M > 0) ? g->shs : nullptr;
+    o.colors = g->colors_precomp;
+    o.opacities = g->opacities;
+    o.scales = g->scales;
+    o.rotations = g->rotations;
+    o.cov3D = g->cov3D_precomp;
+    return o;
+}
+
+int validate(const gsr_settings* s, const gsr_gaussians* g, bool forward) {
+    if (!s || !g) return fail(GSR_ERR_INVALID_ARG, "null settings or gaussians");
+    if (g->P < 0) return fail(GSR_ERR_INVALID_ARG, "P must be >= 0");
+    if (s->image_width <= 0 || s->image_height <= 0) return fail(GSR_ERR_INVALID_ARG, "image size must be positive");
+    if (s->image_width > 16 * 65535 || s->image_height > 16 * 65535)
+        return fail(GSR_ERR_INVALID_ARG, "image too large for 16-bit tile coordinates");
+    if (g->P == 0) return GSR_OK;
+    if (!g->means3D) return fail(GSR_ERR_INVALID_ARG, "means3D is required");
+    if (forward && !g->opacities) return fail(GSR_ERR_INVALID_ARG, "opacities are required");
+    if (!s->viewmatrix || !s->projmatrix || !s->bg) return fail(GSR_ERR_INVALID_ARG, "camera matrices / bg missing");
+    const bool has_sh = g->shs && g->M > 0;
+    if (!g->colors_precomp && !has_sh)
+        return fail(GSR_ERR_INVALID_ARG, "Please provide excatly one of either SHs or precomputed colors!");
+    if (!g->colors_precomp && !s->campos) return fail(GSR_ERR_INVALID_ARG, "campos required for SH colours");
+    if (has_sh && (s->sh_degree < 0 || s->sh_degree > 3 || (s->sh_degree + 1) * (s->sh_degree + 1) > g->M))
+        return fail(GSR_ERR_INVALID_ARG, "sh_degree must be in [0,3] with (deg+1)^2 <= M");
+    const bool has_sr = g->scales && g->rotations;
+    if (!has_sr && !g->cov3D_precomp)
+        return fail(GSR_ERR_INVALID_ARG,
+                    "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    return GSR_OK;
+}
+
+void* obtain(gsr_alloc_fn alloc, void* ctx, int kind, size_t bytes) {
+    void* p = alloc(ctx, kind, bytes);
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gsr_abi_version(void) { return GSR_ABI_VERSION; }
+
+const char* gsr_last_error(void) { return g_last_error.c_str(); }
+
+size_t gsr_geom_buffer_bytes(int P) { return GeomLayout::make(P).total; }
+size_t gsr_binning_buffer_bytes(int num_rendered, int W, int H) { return BinLayout::make(num_rendered, W, H).total; }
+size_t gsr_image_buffer_bytes(int W, int H) { return ImgLayout::make(W, H).total; }
+
+int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, float* out_color, float* out_depth,
+                int* radii, gsr_alloc_fn alloc, void* alloc_ctx, void* stream_) {
+    int rc = validate(settings, gaussians, true);
+    if (rc != GSR_OK) return rc;
+    if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
+    if (!out_color || !out_depth) return fail(GSR_ERR_INVALID_ARG, "output image pointers required");
+    hipStream_t stream = (hipStream_t)stream_;
+    const Camera cam = make_camera(settings);
+    const GaussIn g = make_gauss(gaussians);
+    const int P = g.P, W = cam.W, H = cam.H;
+    const GeomLayout GL = GeomLayout::make(P);
+    const ImgLayout IL = ImgLayout::make(W, H);
+    void* geom = obtain(alloc, alloc_ctx, GSR_BUF_GEOM, GL.total);
+    void* img = obtain(alloc, alloc_ctx, GSR_BUF_IMAGE, IL.total);
+    if (!geom || !img) return fail(GSR_ERR_ALLOC, "allocator returned NULL (geom/image buffer)");
+    const GeomPtrs geo = GeomPtrs::at(geom, GL);
+    char* ib = (char*)img;
+    float* final_T = (float*)(ib + IL.final_T);
+    uint32_t* n_contrib = (uint32_t*)(ib + IL.n_contrib);
+    uint2* ranges = (uint2*)(ib + IL.ranges);
+    hipError_t e;
+    if (P > 0) {
+        if (!radii) return fail(GSR_ERR_INVALID_ARG, "radii output required");
+        if ((e = hipMemsetAsync(geo.counters, 0, 16, stream)) != hipSuccess) return hip_fail(e, "memset counters");
+        if ((e = launch_preprocess(cam, g, geo, radii, GL.nb, stream)) != hipSuccess) return hip_fail(e, "preprocess");
+        if ((e = launch_exclusive_scan(geo.blocksums, (uint32_t)GL.nb, geo.counters, stream)) != hipSuccess)
+            return hip_fail(e, "scan");
+        if (!g_pinned.p) {
+            if ((e = hipHostMalloc((void**)&g_pinned.p, 16, hipHostMallocDefault)) != hipSuccess)
+                return hip_fail(e, "hipHostMalloc");
+        }
+        if ((e = hipMemcpyAsync(g_pinned.p, geo.counters, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+            return hip_fail(e, "copy num_rendered");
+        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "sync num_rendered");
+    }
+    const uint32_t I = (P > 0) ? g_pinned.p[0] : 0u;
+    if (P > 0 && g_pinned.p[1] != 0)
+        return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (I > 0x7fffffffu) return fail(GSR_ERR_INVALID_ARG, "num_rendered overflows int32");
+    const BinLayout BL = BinLayout::make((int)I, W, H);
+    void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, BL.total);
+    if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
+    char* bb = (char*)bin;
+    uint64_t* keys[2] = {(uint64_t*)(bb + BL.keys[0]), (uint64_t*)(bb + BL.keys[1])};
+    uint32_t* vals[2] = {(uint32_t*)(bb + BL.vals[0]), (uint32_t*)(bb + BL.vals[1])};
+    uint32_t* gid = (uint32_t*)(bb + BL.gid);
+    uint32_t* point_list = (uint32_t*)(bb + BL.point_list);
+    uint32_t* hist = (uint32_t*)(bb + BL.hist);
+    if ((e = hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)cam.gx * cam.gy, stream)) != hipSuccess)
+        return hip_fail(e, "memset ranges");
+    if (I > 0) {
+        if ((e = launch_duplicate(cam, P, geo, keys[0], gid, GL.nb, stream)) != hipSuccess) return hip_fail(e, "duplicate");
+        if ((e = launch_radix_sort(keys, vals, hist, I, BL.nsb, BL.npass, stream)) != hipSuccess)
+            return hip_fail(e, "radix sort");
+        if ((e = launch_ranges(keys[BL.final_buf], vals[BL.final_buf], gid, point_list, ranges, I, stream)) !=
+            hipSuccess)
+            return hip_fail(e, "ranges");
+    }
+    if ((e = launch_render_fwd(cam, ranges, point_list, geo, nullptr, final_T, n_contrib, out_color, out_depth,
+                               stream)) != hipSuccess)
+        return hip_fail(e, "render");
+    return (int)I;
+}
+
+int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
+                 const float* dL_dout_color, int num_rendered, const void* geom_buffer, const void* binning_buffer,
+                 const void* image_buffer, int power, const gsr_grads* grads, gsr_alloc_fn alloc, void* alloc_ctx,
+                 void* stream_) {
+    int rc = validate(settings, gaussians, false);
+    if (rc != GSR_OK) return rc;
+    if (!grads) return fail(GSR_ERR_INVALID_ARG, "grads required");
+    if (num_rendered < 0) return fail(GSR_ERR_INVALID_ARG, "num_rendered must be >= 0");
+    if (power != 1) return fail(GSR_ERR_INVALID_ARG, "backward_power != 1 not supported by this build");
+    hipStream_t stream = (hipStream_t)stream_;
+    const Camera cam = make_camera(settings);
+    const GaussIn g = make_gauss(gaussians);
+    const int P = g.P;
+    if (P == 0) return GSR_OK;
+    if (!geom_buffer || !image_buffer || !radii || !dL_dout_color)
+        return fail(GSR_ERR_INVALID_ARG, "missing forward state");
+    const GeomLayout GL = GeomLayout::make(P);
+    const ImgLayout IL = ImgLayout::make(cam.W, cam.H);
+    const BinLayout BL = BinLayout::make(num_rendered, cam.W, cam.H);
+    const GeomPtrs geo = GeomPtrs::at(const_cast<void*>(geom_buffer), GL);
+    const char* ib = (const char*)image_buffer;
+    const float* final_T = (const float*)(ib + IL.final_T);
+    const uint32_t* n_contrib = (const uint32_t*)(ib + IL.n_contrib);
+    const uint2* ranges = (const uint2*)(ib + IL.ranges);
+    float4* inst = nullptr;
+    hipError_t e;
+    if (num_rendered > 0) {
+        if (!binning_buffer) return fail(GSR_ERR_INVALID_ARG, "missing binning buffer");
+        if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
+        inst = (float4*)obtain(alloc, alloc_ctx, GSR_BUF_SCRATCH, sizeof(float4) * INST_REC_F4 * (size_t)num_rendered);
+        if (!inst) return fail(GSR_ERR_ALLOC, "allocator returned NULL (backward scratch)");
+        const char* bb = (const char*)binning_buffer;
+        const uint32_t* perm = (const uint32_t*)(bb + BL.vals[BL.final_buf]);
+        const uint32_t* point_list = (const uint32_t*)(bb + BL.point_list);
+        if ((e = launch_render_bwd(cam, ranges, point_list, perm, geo, nullptr, final_T, n_contrib, dL_dout_color,
+                                   inst, stream)) != hipSuccess)
+            return hip_fail(e, "render backward");
+    }
+    GradsOut out{grads->dmeans2D, grads->dcolors, grads->dopacity, grads->dmeans3D,
+                 grads->dcov3D,   grads->dsh,     grads->dscales,  grads->drotations};
+    if (!out.dmeans2D || !out.dcolors || !out.dopacity || !out.dmeans3D || !out.dcov3D || !out.dscales || !out.drot)
+        return fail(GSR_ERR_INVALID_ARG, "gradient output pointers required");
+    if ((e = launch_gauss_bwd(cam, g, geo, radii, inst, out, stream)) != hipSuccess)
+        return hip_fail(e, "gaussian backward");
+    return GSR_OK;
+}
+
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* visible, void* stream) {
+    (void)projmatrix;
+    if (P < 0) return fail(GSR_ERR_INVALID_ARG, "P must be >= 0");
+    if (P == 0) return GSR_OK;
+    if (!means3D || !viewmatrix || !visible) return fail(GSR_ERR_INVALID_ARG, "null pointer");
+    hipError_t e = launch_mark_visible(P, means3D, viewmatrix, visible, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "mark_visible");
+    return GSR_OK;
+}
+
+// Test hook: validates the wave64 permlane/DPP reduction on the device.
+int gsr_selftest_reduce9(const float* in_dev, float* out_dev, void* stream) {
+    hipError_t e = launch_selftest_reduce9(in_dev, out_dev, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "selftest");
+    return GSR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,391 @@
+// gsr_common.h -- shared device math, buffer layouts and launch declarations
+// of the MI355X-native Gaussian rasterizer (gfx950 / CDNA4, wave64).
+//
+// Buffer layouts are computed on the host from (P, num_rendered, W, H) alone,
+// exactly like the reference re-derives its chunk pointers
+// (rasterizer_impl.cu:155-194, rasterizer_impl.h:21-73), so gsr_backward can
+// find every array again without any header read-back.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace gsr {
+
+constexpr int TILE_X = 16;  // config.h:16-17 (BLOCK_X/BLOCK_Y); parity needs 16x16 tiles
+constexpr int TILE_Y = 16;
+constexpr int TILE_PIX = TILE_X * TILE_Y;
+constexpr int PRE_BLOCK = 256;       // Gaussians per preprocess / duplicate workgroup
+constexpr int SORT_THREADS = 256;
+constexpr int SORT_ITEMS = 8;        // keys per thread per radix pass
+constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;
+constexpr int RADIX = 256;
+constexpr int RENDER_BATCH = 256;    // Gaussians staged in LDS per batch
+constexpr int INST_REC_F4 = 3;       // backward per-instance record: 3 x float4 (9 used floats)
+
+// ---------------------------------------------------------------- layouts --
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct GeomLayout {       // per-Gaussian state ("geomBuffer")
+    size_t rec_a;         // float4 [P]  (x, y, conic A, conic B)   pixel coordinates
+    size_t rec_b;         // float4 [P]  (conic C, opacity, depth, 0)
+    size_t rec_c;         // float4 [P]  (r, g, b, clamped bits)
+    size_t rect;          // uint2  [P]  tile rect (x0 | y0<<16, x1 | y1<<16)
+    size_t tiles;         // u32    [P]  tiles touched
+    size_t offsets;       // u32    [P]  exclusive instance offset
+    size_t blocksums;     // u32    [nb] per-workgroup tile sums -> exclusive scan
+    size_t counters;      // u32    [4]  [0]=num_rendered [1]=prefiltered violation
+    size_t total;
+    int nb;
+    static GeomLayout make(int P) {
+        GeomLayout L;
+        size_t o = 0, p = (size_t)(P > 0 ? P : 1);
+        L.nb = (P + PRE_BLOCK - 1) / PRE_BLOCK;
+        L.rec_a = o; o = align_up(o + 16 * p, 256);
+        L.rec_b = o; o = align_up(o + 16 * p, 256);
+        L.rec_c = o; o = align_up(o + 16 * p, 256);
+        L.rect = o; o = align_up(o + 8 * p, 256);
+        L.tiles = o; o = align_up(o + 4 * p, 256);
+        L.offsets = o; o = align_up(o + 4 * p, 256);
+        L.blocksums = o; o = align_up(o + 4 * (size_t)(L.nb > 0 ? L.nb : 1), 256);
+        L.counters = o; o = align_up(o + 16, 256);
+        L.total = o;
+        return L;
+    }
+};
+
+struct ImgLayout {        // per-pixel / per-tile state ("imgBuffer")
+    size_t final_T;       // f32   [N]
+    size_t n_contrib;     // u32   [N]
+    size_t ranges;        // uint2 [tiles]
+    size_t total;
+    static ImgLayout make(int W, int H) {
+        ImgLayout L;
+        size_t N = (size_t)W * H;
+        size_t T = (size_t)((W + TILE_X - 1) / TILE_X) * ((H + TILE_Y - 1) / TILE_Y);
+        size_t o = 0;
+        L.final_T = o; o = align_up(o + 4 * (N ? N : 1), 256);
+        L.n_contrib = o; o = align_up(o + 4 * (N ? N : 1), 256);
+        L.ranges = o; o = align_up(o + 8 * (T ? T : 1), 256);
+        L.total = o;
+        return L;
+    }
+};
+
+inline int higher_msb(uint32_t n) {  // rasterizer_impl.cu:35-50 (bits needed for tile ids)
+    int b = 0;
+    while (b < 32 && (n >> b) != 0) b++;
+    return b;
+}
+
+struct BinLayout {        // per-instance state ("binningBuffer")
+    size_t keys[2];       // u64 [I] ping-pong
+    size_t vals[2];       // u32 [I] ping-pong (values = unsorted instance index)
+    size_t gid;           // u32 [I] Gaussian id of each unsorted instance
+    size_t point_list;    // u32 [I] Gaussian ids in (tile, depth) order
+    size_t hist;          // u32 [RADIX * nsb]
+    size_t total;
+    int nsb;              // radix-sort workgroups
+    int npass;            // 8-bit LSD passes over bits [0, 32 + msb(tiles))
+    int final_buf;        // which ping-pong half holds the sorted keys/vals
+    static BinLayout make(int I, int W, int H) {
+        BinLayout L;
+        size_t n = (size_t)(I > 0 ? I : 1);
+        uint32_t tiles = (uint32_t)(((W + TILE_X - 1) / TILE_X) * ((H + TILE_Y - 1) / TILE_Y));
+        int bits = 32 + higher_msb(tiles);
+        L.npass = (bits + 7) / 8;
+        L.final_buf = L.npass & 1;
+        L.nsb = (int)((n + SORT_TILE - 1) / SORT_TILE);
+        size_t o = 0;
+        L.keys[0] = o; o = align_up(o + 8 * n, 256);
+        L.keys[1] = o; o = align_up(o + 8 * n, 256);
+        L.vals[0] = o; o = align_up(o + 4 * n, 256);
+        L.vals[1] = o; o = align_up(o + 4 * n, 256);
+        L.gid = o; o = align_up(o + 4 * n, 256);
+        L.point_list = o; o = align_up(o + 4 * n, 256);
+        L.hist = o; o = align_up(o + 4 * (size_t)RADIX * L.nsb, 256);
+        L.total = o;
+        return L;
+    }
+};
+
+// ------------------------------------------------------------ parameters --
+struct Camera {
+    int W, H;
+    float tan_fovx, tan_fovy, focal_x, focal_y;
+    int gx, gy;  // tile grid
+    const float* view;
+    const float* proj;
+    const float* campos;
+    const float* bg;
+    float scale_modifier;
+    int sh_degree;
+    int prefiltered;
+};
+
+struct GaussIn {
+    int P, M;
+    const float* means3D;
+    const float* shs;
+    const float* colors;
+    const float* opacities;
+    const float* scales;
+    const float* rotations;
+    const float* cov3D;
+};
+
+struct GeomPtrs {
+    float4* rec_a;
+    float4* rec_b;
+    float4* rec_c;
+    uint2* rect;
+    uint32_t* tiles;
+    uint32_t* offsets;
+    uint32_t* blocksums;
+    uint32_t* counters;
+    static GeomPtrs at(void* base, const GeomLayout& L) {
+        char* b = (char*)base;
+        return {(float4*)(b + L.rec_a), (float4*)(b + L.rec_b), (float4*)(b + L.rec_c), (uint2*)(b + L.rect),
+                (uint32_t*)(b + L.tiles), (uint32_t*)(b + L.offsets), (uint32_t*)(b + L.blocksums),
+                (uint32_t*)(b + L.counters)};
+    }
+};
+
+// ------------------------------------------------------------ device math --
+// The functions below restate forward.cu / backward.cu / auxiliary.h in
+// standard notation.  They keep the operation order of oracle/gsr_oracle.c and
+// disable FMA contraction so that preprocess outputs (radii, tile rects) are
+// bit-identical to the float32 oracle.
+
+__constant__ static const float kSH_C0 = 0.28209479177387814f;
+__constant__ static const float kSH_C1 = 0.4886025119029199f;
+__constant__ static const float kSH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                                             -1.0925484305920792f, 0.5462742152960396f};
+__constant__ static const float kSH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                                             0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
+                                             -0.5900435899266435f};
+
+__device__ __forceinline__ float3 xform4x3(float3 p, const float* m) {  // auxiliary.h:58-66
+#pragma clang fp contract(off)
+    return make_float3(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
+                       m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]);
+}
+
+__device__ __forceinline__ float4 xform4x4(float3 p, const float* m) {  // auxiliary.h:68-77
+#pragma clang fp contract(off)
+    return make_float4(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14], m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]);
+}
+
+__device__ __forceinline__ float ndc2pix(float v, int S) {  // auxiliary.h:41-44 (double literals)
+    return (float)((((double)v + 1.0) * S - 1.0) * 0.5);
+}
+
+__device__ __forceinline__ void get_rect(float px, float py, int r, int gx, int gy, int& x0, int& y0, int& x1,
+                                         int& y1) {  // auxiliary.h:46-56
+#pragma clang fp contract(off)
+    float fr = (float)r;
+    int a = (int)((px - fr) / (float)TILE_X);
+    int b = (int)((py - fr) / (float)TILE_Y);
+    float cx = px + fr; cx = cx + (float)TILE_X; cx = cx - 1.0f;
+    float cy = py + fr; cy = cy + (float)TILE_Y; cy = cy - 1.0f;
+    int c = (int)(cx / (float)TILE_X);
+    int d = (int)(cy / (float)TILE_Y);
+    a = max(a, 0); b = max(b, 0); c = max(c, 0); d = max(d, 0);
+    x0 = min(a, gx); y0 = min(b, gy); x1 = min(c, gx); y1 = min(d, gy);
+}
+
+// Sigma = R S^2 R^T, R from the un-normalised quaternion (forward.cu:118-152)
+__device__ __forceinline__ void rot_from_quat(float4 q, float R[3][3]) {
+#pragma clang fp contract(off)
+    float r = q.x, x = q.y, y = q.z, z = q.w;
+    R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y - r * z); R[0][2] = 2.f * (x * z + r * y);
+    R[1][0] = 2.f * (x * y + r * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z - r * x);
+    R[2][0] = 2.f * (x * z - r * y); R[2][1] = 2.f * (y * z + r * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
+}
+
+__device__ __forceinline__ void cov3d_fwd(float3 s3, float mod, float4 q, float cov[6]) {
+#pragma clang fp contract(off)
+    float R[3][3];
+    rot_from_quat(q, R);
+    float s[3] = {mod * s3.x, mod * s3.y, mod * s3.z};
+    float M[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+#pragma unroll
+        for (int i = 0; i < 3; i++) M[k][i] = s[k] * R[i][k];
+    float S[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) S[i][j] = M[0][i] * M[0][j] + M[1][i] * M[1][j] + M[2][i] * M[2][j];
+    cov[0] = S[0][0]; cov[1] = S[0][1]; cov[2] = S[0][2];
+    cov[3] = S[1][1]; cov[4] = S[1][2]; cov[5] = S[2][2];
+}
+
+struct Proj {
+    float tx, ty, tz, xmul, ymul;
+    float Mx[2][3];  // J V3
+    float a, b, c;   // cov2D (+0.3 low-pass on the diagonal)
+};
+
+// forward.cu:74-113 (EWA, with the +-1.3 tanfov clamp) in standard notation
+__device__ __forceinline__ void cov2d_fwd(float3 mean, float fx, float fy, float tanx, float tany, const float c3[6],
+                                          const float* view, Proj& o) {
+#pragma clang fp contract(off)
+    float3 t = xform4x3(mean, view);
+    float limx = 1.3f * tanx, limy = 1.3f * tany;
+    float txtz = t.x / t.z, tytz = t.y / t.z;
+    o.xmul = (txtz < -limx || txtz > limx) ? 0.f : 1.f;
+    o.ymul = (tytz < -limy || tytz > limy) ? 0.f : 1.f;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    o.tx = t.x; o.ty = t.y; o.tz = t.z;
+    float J00 = fx / t.z, J02 = -(fx * t.x) / (t.z * t.z);
+    float J11 = fy / t.z, J12 = -(fy * t.y) / (t.z * t.z);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        o.Mx[0][k] = J00 * view[4 * k + 0] + J02 * view[4 * k + 2];
+        o.Mx[1][k] = J11 * view[4 * k + 1] + J12 * view[4 * k + 2];
+    }
+    float S[3][3] = {{c3[0], c3[1], c3[2]}, {c3[1], c3[3], c3[4]}, {c3[2], c3[4], c3[5]}};
+    float u0[3], u1[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        u0[k] = S[k][0] * o.Mx[0][0] + S[k][1] * o.Mx[0][1] + S[k][2] * o.Mx[0][2];
+        u1[k] = S[k][0] * o.Mx[1][0] + S[k][1] * o.Mx[1][1] + S[k][2] * o.Mx[1][2];
+    }
+    float a = o.Mx[0][0] * u0[0] + o.Mx[0][1] * u0[1] + o.Mx[0][2] * u0[2];
+    float b = o.Mx[0][0] * u1[0] + o.Mx[0][1] * u1[1] + o.Mx[0][2] * u1[2];
+    float c = o.Mx[1][0] * u1[0] + o.Mx[1][1] * u1[1] + o.Mx[1][2] * u1[2];
+    o.a = a + 0.3f;
+    o.b = b;
+    o.c = c + 0.3f;
+}
+
+// forward.cu:20-71 (one channel at a time, same order as the oracle)
+__device__ __forceinline__ void sh_fwd(int deg, float3 pos, const float* campos, const float* sh, float rgb[3],
+                                       unsigned& clamped_bits) {
+#pragma clang fp contract(off)
+    float dx = pos.x - campos[0], dy = pos.y - campos[1], dz = pos.z - campos[2];
+    float len = sqrtf(dx * dx + dy * dy + dz * dz);
+    float x = dx / len, y = dy / len, z = dz / len;
+    clamped_bits = 0;
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+#define S(k) sh[3 * (k) + ch]
+        float res = kSH_C0 * S(0);
+        if (deg > 0) {
+            res = res - kSH_C1 * y * S(1) + kSH_C1 * z * S(2) - kSH_C1 * x * S(3);
+            if (deg > 1) {
+                float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+                res = res + (kSH_C2[0] * xy * S(4) + kSH_C2[1] * yz * S(5) + kSH_C2[2] * (2.f * zz - xx - yy) * S(6) +
+                             kSH_C2[3] * xz * S(7) + kSH_C2[4] * (xx - yy) * S(8));
+                if (deg > 2) {
+                    res = res + (kSH_C3[0] * y * (3.f * xx - yy) * S(9) + kSH_C3[1] * xy * z * S(10) +
+                                 kSH_C3[2] * y * (4.f * zz - xx - yy) * S(11) +
+                                 kSH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy) * S(12) +
+                                 kSH_C3[4] * x * (4.f * zz - xx - yy) * S(13) + kSH_C3[5] * z * (xx - yy) * S(14) +
+                                 kSH_C3[6] * x * (xx - 3.f * yy) * S(15));
+                }
+            }
+        }
+#undef S
+        res = res + 0.5f;
+        if (res < 0.f) clamped_bits |= 1u << ch;
+        rgb[ch] = fmaxf(res, 0.f);
+    }
+}
+
+// --------------------------------------------------------- wave64 helpers --
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// Sum over each 16-lane row; every lane of the row receives the row total.
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_mov<0x124>(v);  // row_ror:4
+    v += dpp_mov<0x128>(v);  // row_ror:8
+    return v;
+}
+
+// v_permlane32_swap: lanes 0-31 <- a(l)+a(l+32), lanes 32-63 <- b(l-32)+b(l)
+__device__ __forceinline__ float swapsum32(float a, float b) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// v_permlane16_swap: within each 32-lane half, row0 <- a.r0+a.r1, row1 <- b.r0+b.r1
+__device__ __forceinline__ float swapsum16(float a, float b) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Transposed wave reduction of 9 values: ~30 VALU instead of 9 full
+// butterflies.  On return, for row = lane/16:
+//   r0 row {0,1,2,3} holds the wave totals of v{0,2,1,3}
+//   r1 row {0,1,2,3} holds the wave totals of v{4,6,5,7}
+//   r8 row 0 holds the wave total of v8
+__device__ __forceinline__ void wave_reduce9(const float v[9], float& r0, float& r1, float& r8) {
+    float s01 = swapsum32(v[0], v[1]);
+    float s23 = swapsum32(v[2], v[3]);
+    float s45 = swapsum32(v[4], v[5]);
+    float s67 = swapsum32(v[6], v[7]);
+    float s8 = swapsum32(v[8], 0.f);
+    float t0 = swapsum16(s01, s23);
+    float t1 = swapsum16(s45, s67);
+    float t2 = swapsum16(s8, 0.f);
+    r0 = row16_sum(t0);
+    r1 = row16_sum(t1);
+    r8 = row16_sum(t2);
+}
+__device__ __forceinline__ int reduce9_slot_r0(int row) { return (row == 0) ? 0 : (row == 1 ? 2 : (row == 2 ? 1 : 3)); }
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Lanes of the wave whose 8-bit digit equals mine (valid lanes only).
+__device__ __forceinline__ uint64_t wave_match8(uint32_t d, bool valid) {
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+        uint64_t bal = __ballot(valid && ((d >> b) & 1u));
+        m &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    return m;
+}
+
+// ------------------------------------------------------- kernel launchers --
+hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, int nb, hipStream_t s);
+hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hipStream_t s);
+hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid, int nb,
+                            hipStream_t s);
+hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t n, int nsb, int npass,
+                             hipStream_t s);
+hipError_t launch_ranges(const uint64_t* keys, const uint32_t* vals, const uint32_t* gid, uint32_t* point_list,
+                         uint2* ranges, uint32_t n, hipStream_t s);
+hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
+                             const float* colors, float* final_T, uint32_t* n_contrib, float* out_color,
+                             float* out_depth, hipStream_t s);
+hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* vis, hipStream_t s);
+hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list,
+                             const uint32_t* perm, GeomPtrs geo, const float* colors, const float* final_T,
+                             const uint32_t* n_contrib, const float* dL_dpix, float4* inst, hipStream_t s);
+struct GradsOut {
+    float* dmeans2D;
+    float* dcolors;
+    float* dopacity;
+    float* dmeans3D;
+    float* dcov3D;
+    float* dsh;
+    float* dscales;
+    float* drot;
+};
+hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float4* inst,
+                            const GradsOut& out, hipStream_t s);
+hipError_t launch_selftest_reduce9(const float* in, float* out, hipStream_t s);
+
+}  // namespace gsr

@@ -1,0 +1,401 @@
+// gsr_forward.hip -- forward pipeline of the MI355X-native Gaussian rasterizer.
+//
+//   preprocess  (forward.cu:155-256)     one lane per Gaussian, writes 48-B render records
+//   scan        (rasterizer_impl.cu:277)  per-workgroup tile sums -> exclusive scan
+//   duplicate   (rasterizer_impl.cu:70-111) load-balanced: a workgroup emits the
+//               instances of its 256 Gaussians with consecutive lanes on consecutive
+//               instances (binary search in LDS), so writes are coalesced
+//   radix sort  (rasterizer_impl.cu:301-309) stable 8-bit LSD passes, wave64 ballot
+//               match ranking (no atomics), values = unsorted instance index
+//   ranges      (rasterizer_impl.cu:116-138) + point_list gather of Gaussian ids
+//   render      (forward.cu:261-393) 16x16 tile per 256-lane workgroup, 256-entry
+//               LDS batches, block-wide early exit
+#include "gsr_common.h"
+
+namespace gsr {
+
+// ------------------------------------------------------------- preprocess --
+__global__ void __launch_bounds__(PRE_BLOCK) preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * PRE_BLOCK + threadIdx.x;
+    uint32_t tiles = 0;
+    if (i < g.P) {
+        int radius = 0;
+        float3 p = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
+        float4 hom = xform4x4(p, cam.proj);
+        float pw = 1.0f / (hom.w + 0.0000001f);
+        float3 pv = xform4x3(p, cam.view);
+        bool ok = pv.z > 0.001f;  // auxiliary.h:154 (the 1.3 NDC test is commented out)
+        if (!ok && cam.prefiltered) atomicOr(&geo.counters[1], 1u);
+        float cov3[6];
+        Proj pj;
+        float det = 0.f;
+        if (ok) {
+            if (g.cov3D) {
+#pragma unroll
+                for (int k = 0; k < 6; k++) cov3[k] = g.cov3D[6 * i + k];
+            } else {
+                float3 s = make_float3(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2]);
+                float4 q = make_float4(g.rotations[4 * i], g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3]);
+                cov3d_fwd(s, cam.scale_modifier, q, cov3);
+            }
+            cov2d_fwd(p, cam.focal_x, cam.focal_y, cam.tan_fovx, cam.tan_fovy, cov3, cam.view, pj);
+            det = pj.a * pj.c - pj.b * pj.b;
+            ok = det != 0.0f;
+        }
+        if (ok) {
+            float det_inv = 1.f / det;
+            float ca = pj.c * det_inv, cb = -pj.b * det_inv, cc = pj.a * det_inv;
+            float mid = 0.5f * (pj.a + pj.c);
+            float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+            float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+            float rad = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+            float px = ndc2pix(hom.x * pw, cam.W), py = ndc2pix(hom.y * pw, cam.H);
+            int x0, y0, x1, y1;
+            get_rect(px, py, (int)rad, cam.gx, cam.gy, x0, y0, x1, y1);
+            tiles = (uint32_t)((x1 - x0) * (y1 - y0));
+            if (tiles != 0) {
+                float rgb[3];
+                unsigned clamped = 0;
+                if (g.colors) {
+                    rgb[0] = g.colors[3 * i]; rgb[1] = g.colors[3 * i + 1]; rgb[2] = g.colors[3 * i + 2];
+                } else {
+                    sh_fwd(cam.sh_degree, p, cam.campos, g.shs + (size_t)3 * g.M * i, rgb, clamped);
+                }
+                radius = (int)rad;
+                geo.rec_a[i] = make_float4(px, py, ca, cb);
+                geo.rec_b[i] = make_float4(cc, g.opacities[i], pv.z, 0.f);
+                geo.rec_c[i] = make_float4(rgb[0], rgb[1], rgb[2], __uint_as_float(clamped));
+                geo.rect[i] = make_uint2((uint32_t)x0 | ((uint32_t)y0 << 16), (uint32_t)x1 | ((uint32_t)y1 << 16));
+            }
+        }
+        radii[i] = radius;
+        geo.tiles[i] = tiles;
+    }
+    // workgroup sum of tiles touched (input of the two-level scan)
+    __shared__ uint32_t wsum[PRE_BLOCK / 64];
+    uint32_t v = tiles;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) geo.blocksums[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, int nb, hipStream_t s) {
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(preprocess_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, g, geo, radii);
+    return hipGetLastError();
+}
+
+// -------------------------------------------------------- exclusive scan --
+// One 1024-lane workgroup scans `n` u32 in place (exclusive) and writes the
+// grand total.  Used for the per-workgroup tile sums and radix histograms.
+constexpr int SCAN_THREADS = 1024;
+constexpr int SCAN_ITEMS = 4;
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = __lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__global__ void __launch_bounds__(SCAN_THREADS) exclusive_scan_kernel(uint32_t* data, uint32_t n, uint32_t* total) {
+    __shared__ uint32_t wsums[SCAN_THREADS / 64];
+    __shared__ uint32_t s_carry;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < n; base += SCAN_THREADS * SCAN_ITEMS) {
+        uint32_t x[SCAN_ITEMS], sum = 0;
+        const uint32_t i0 = base + (uint32_t)tid * SCAN_ITEMS;
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; k++) {
+            x[k] = (i0 + k < n) ? data[i0 + k] : 0u;
+            sum += x[k];
+        }
+        uint32_t incl = wave_incl_scan(sum);
+        if (lane == 63) wsums[w] = incl;
+        __syncthreads();
+        if (w == 0) {
+            uint32_t ws = (lane < SCAN_THREADS / 64) ? wsums[lane] : 0u;
+            uint32_t wi = wave_incl_scan(ws);
+            if (lane < SCAN_THREADS / 64) wsums[lane] = wi - ws;  // exclusive wave offsets
+        }
+        __syncthreads();
+        uint32_t carry = s_carry;
+        uint32_t run = carry + wsums[w] + incl - sum;
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; k++) {
+            if (i0 + k < n) data[i0 + k] = run;
+            run += x[k];
+        }
+        __syncthreads();
+        if (tid == SCAN_THREADS - 1) s_carry = run;
+        __syncthreads();
+    }
+    if (tid == 0 && total) *total = s_carry;
+}
+
+hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hipStream_t s) {
+    hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, data, n, total);
+    return hipGetLastError();
+}
+
+// -------------------------------------------------------------- duplicate --
+__global__ void __launch_bounds__(PRE_BLOCK)
+duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, uint32_t* __restrict__ gid) {
+    __shared__ uint32_t s_incl[PRE_BLOCK];   // inclusive scan of tiles touched
+    __shared__ uint32_t s_x0[PRE_BLOCK], s_y0[PRE_BLOCK], s_w[PRE_BLOCK], s_depth[PRE_BLOCK];
+    __shared__ uint32_t wsum[PRE_BLOCK / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int i = blockIdx.x * PRE_BLOCK + tid;
+    uint32_t t = (i < P) ? geo.tiles[i] : 0u;
+    uint32_t incl = wave_incl_scan(t);
+    if (lane == 63) wsum[w] = incl;
+    if (t) {
+        uint2 r = geo.rect[i];
+        s_x0[tid] = r.x & 0xFFFFu;
+        s_y0[tid] = r.x >> 16;
+        s_w[tid] = (r.y & 0xFFFFu) - (r.x & 0xFFFFu);
+        s_depth[tid] = __float_as_uint(geo.rec_b[i].z);
+    }
+    __syncthreads();
+    uint32_t woff = 0;
+    for (int k = 0; k < w; k++) woff += wsum[k];
+    incl += woff;
+    s_incl[tid] = incl;
+    const uint32_t base = geo.blocksums[blockIdx.x];  // exclusive scan of workgroup totals
+    if (i < P) geo.offsets[i] = base + incl - t;
+    __syncthreads();
+    const uint32_t total = s_incl[PRE_BLOCK - 1];
+    for (uint32_t e = tid; e < total; e += PRE_BLOCK) {
+        // owner j: first Gaussian whose inclusive sum exceeds e
+        int lo = 0, hi = PRE_BLOCK - 1;
+        while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (s_incl[mid] > e) hi = mid; else lo = mid + 1;
+        }
+        const uint32_t start = (lo == 0) ? 0u : s_incl[lo - 1];
+        const uint32_t local = e - start;
+        const uint32_t wdt = s_w[lo];
+        const uint32_t ty = s_y0[lo] + local / wdt;
+        const uint32_t tx = s_x0[lo] + local % wdt;
+        const uint32_t u = base + e;
+        keys[u] = ((uint64_t)(ty * (uint32_t)cam.gx + tx) << 32) | (uint64_t)s_depth[lo];
+        gid[u] = (uint32_t)(blockIdx.x * PRE_BLOCK + lo);
+    }
+}
+
+hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid, int nb,
+                            hipStream_t s) {
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(duplicate_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, keys, gid);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------- radix sort --
+// Each workgroup owns SORT_TILE consecutive keys; wave w owns the w-th quarter
+// in 8 slots of 64 lanes, so (wave, slot, lane) order == key order (stable).
+__global__ void __launch_bounds__(SORT_THREADS)
+radix_hist_kernel(const uint64_t* __restrict__ keys, uint32_t n, int shift, uint32_t* __restrict__ hist, int nsb) {
+    __shared__ uint32_t wcnt[SORT_THREADS / 64][RADIX];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int k = tid; k < (SORT_THREADS / 64) * RADIX; k += SORT_THREADS) (&wcnt[0][0])[k] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * SORT_TILE + w * (SORT_TILE / 4);
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int s = 0; s < SORT_ITEMS; s++) {
+        const uint32_t idx = base + s * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t d = valid ? (uint32_t)(keys[idx] >> shift) & (RADIX - 1) : 0u;
+        const uint64_t m = wave_match8(d, valid);
+        if (valid && (m & lt) == 0) wcnt[w][d] += (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < SORT_THREADS / 64; k++) c += wcnt[k][tid];
+    hist[(size_t)tid * nsb + blockIdx.x] = c;
+}
+
+__global__ void __launch_bounds__(SORT_THREADS)
+radix_scatter_kernel(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint64_t* __restrict__ kout,
+                     uint32_t* __restrict__ vout, uint32_t n, int shift, const uint32_t* __restrict__ hist, int nsb) {
+    __shared__ uint32_t wcnt[SORT_THREADS / 64][RADIX];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int k = tid; k < (SORT_THREADS / 64) * RADIX; k += SORT_THREADS) (&wcnt[0][0])[k] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * SORT_TILE + w * (SORT_TILE / 4);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t key[SORT_ITEMS];
+    uint32_t val[SORT_ITEMS], rank[SORT_ITEMS], dig[SORT_ITEMS];
+#pragma unroll
+    for (int s = 0; s < SORT_ITEMS; s++) {
+        const uint32_t idx = base + s * 64 + lane;
+        const bool valid = idx < n;
+        key[s] = valid ? kin[idx] : 0ull;
+        val[s] = valid ? (vin ? vin[idx] : idx) : 0u;
+        const uint32_t d = (uint32_t)(key[s] >> shift) & (RADIX - 1);
+        dig[s] = d;
+        const uint64_t m = wave_match8(d, valid);
+        uint32_t prev = 0;
+        if (valid) prev = wcnt[w][d];
+        rank[s] = prev + (uint32_t)__popcll(m & lt);
+        if (valid && (m & lt) == 0) wcnt[w][d] = prev + (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    {
+        const uint32_t c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid];
+        const uint32_t g = hist[(size_t)tid * nsb + blockIdx.x];
+        __syncthreads();
+        wcnt[0][tid] = g;
+        wcnt[1][tid] = g + c0;
+        wcnt[2][tid] = g + c0 + c1;
+        wcnt[3][tid] = g + c0 + c1 + c2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < SORT_ITEMS; s++) {
+        const uint32_t idx = base + s * 64 + lane;
+        if (idx < n) {
+            const uint32_t pos = wcnt[w][dig[s]] + rank[s];
+            kout[pos] = key[s];
+            vout[pos] = val[s];
+        }
+    }
+}
+
+hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t n, int nsb, int npass,
+                             hipStream_t s) {
+    for (int p = 0; p < npass; p++) {
+        const int in = p & 1, out = in ^ 1;
+        hipLaunchKernelGGL(radix_hist_kernel, dim3(nsb), dim3(SORT_THREADS), 0, s, keys[in], n, 8 * p, hist, nsb);
+        hipError_t e = launch_exclusive_scan(hist, (uint32_t)RADIX * nsb, nullptr, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(radix_scatter_kernel, dim3(nsb), dim3(SORT_THREADS), 0, s, keys[in],
+                           p == 0 ? (const uint32_t*)nullptr : vals[in], keys[out], vals[out], n, 8 * p, hist, nsb);
+    }
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------------- ranges --
+__global__ void ranges_kernel(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                              const uint32_t* __restrict__ gid, uint32_t* __restrict__ point_list,
+                              uint2* __restrict__ ranges, uint32_t n) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t tile = (uint32_t)(keys[k] >> 32);
+    if (k == 0) {
+        ranges[tile].x = 0;
+    } else {
+        const uint32_t prev = (uint32_t)(keys[k - 1] >> 32);
+        if (prev != tile) {
+            ranges[prev].y = k;
+            ranges[tile].x = k;
+        }
+    }
+    if (k == n - 1) ranges[tile].y = n;
+    point_list[k] = gid[vals[k]];
+}
+
+hipError_t launch_ranges(const uint64_t* keys, const uint32_t* vals, const uint32_t* gid, uint32_t* point_list,
+                         uint2* ranges, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(ranges_kernel, dim3((n + 255) / 256), dim3(256), 0, s, keys, vals, gid, point_list, ranges, n);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------- render (fwd) --
+__global__ void __launch_bounds__(TILE_PIX)
+render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
+                  const float4* __restrict__ rec_a, const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
+                  const float* __restrict__ colors, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
+                  float* __restrict__ out_color, float* __restrict__ out_depth) {
+    __shared__ float4 s_a[RENDER_BATCH];
+    __shared__ float4 s_b[RENDER_BATCH];
+    __shared__ float4 s_c[RENDER_BATCH];
+    const int tid = threadIdx.x;
+    const int tile = blockIdx.y * cam.gx + blockIdx.x;
+    const int px = blockIdx.x * TILE_X + (tid & (TILE_X - 1));
+    const int py = blockIdx.y * TILE_Y + (tid >> 4);
+    const bool inside = px < cam.W && py < cam.H;
+    const float pxf = (float)px, pyf = (float)py;
+    const uint2 range = ranges[tile];
+    bool done = !inside;
+    float T = 1.f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 15.0f;  // forward.cu:308 median-depth default
+    uint32_t contributor = 0, last = 0;
+    for (uint32_t start = range.x; start < range.y; start += RENDER_BATCH) {
+        if (__syncthreads_and(done)) break;  // forward.cu:314-316
+        const uint32_t k = start + tid;
+        if (k < range.y) {
+            const uint32_t gi = point_list[k];
+            s_a[tid] = rec_a[gi];
+            float4 b = rec_b[gi];
+            s_b[tid] = b;
+            float4 c = colors ? make_float4(colors[3 * gi], colors[3 * gi + 1], colors[3 * gi + 2], 0.f) : rec_c[gi];
+            s_c[tid] = c;
+        }
+        __syncthreads();
+        const int cnt = (int)min((uint32_t)RENDER_BATCH, range.y - start);
+        for (int j = 0; j < cnt && !done; j++) {
+            contributor++;
+            const float4 a = s_a[j];
+            const float4 b = s_b[j];
+            const float dx = a.x - pxf, dy = a.y - pyf;
+            const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+            if (power > 0.0f) continue;
+            const float alpha = fminf(0.99f, b.y * __expf(power));
+            if (alpha < 1.0f / 255.0f) continue;
+            const float test_T = T * (1.f - alpha);
+            if (test_T < 0.0001f) { done = true; continue; }
+            const float4 c = s_c[j];
+            const float w = alpha * T;
+            C0 += c.x * w; C1 += c.y * w; C2 += c.z * w;
+            if (T > 0.5f && test_T < 0.5f) D = b.z;  // median depth (forward.cu:368-372)
+            T = test_T;
+            last = contributor;
+        }
+        __syncthreads();
+    }
+    if (inside) {
+        const int pid = py * cam.W + px;
+        const int HW = cam.W * cam.H;
+        final_T[pid] = T;
+        n_contrib[pid] = last;
+        out_color[pid] = C0 + T * cam.bg[0];
+        out_color[HW + pid] = C1 + T * cam.bg[1];
+        out_color[2 * HW + pid] = C2 + T * cam.bg[2];
+        out_depth[pid] = D;
+    }
+}
+
+hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
+                             const float* colors, float* final_T, uint32_t* n_contrib, float* out_color,
+                             float* out_depth, hipStream_t s) {
+    hipLaunchKernelGGL(render_fwd_kernel, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list,
+                       geo.rec_a, geo.rec_b, geo.rec_c, colors, final_T, n_contrib, out_color, out_depth);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------- mark visible --
+__global__ void mark_visible_kernel(int P, const float* __restrict__ means3D, const float* __restrict__ view,
+                                    uint8_t* __restrict__ vis) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    vis[i] = xform4x3(p, view).z > 0.001f ? 1 : 0;
+}
+
+hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* vis, hipStream_t s) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(mark_visible_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, view, vis);
+    return hipGetLastError();
+}
+
+}  // namespace gsr
