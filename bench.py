@@ -1,0 +1,222 @@
+"""Headline benchmark: SplaTAM tracking iterations through the MI355X rasterizer.
+
+BASELINE.json metric "rasterize fwd+bwd frames/sec @640x480, 300k Gaussians;
+HBM GB/s vs peak" on config 3: 300k isotropic Gaussians, 640x480, full
+tracking-iteration loss (scripts/splatam.py:220-353 with tracking=True).
+One step = one frame = RGB render fwd+bwd + depth/silhouette ([z,1,z^2])
+render fwd+bwd + masked L1 loss + Adam step on the camera pose.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+one process per GPU; every rank tracks its own frame against the same
+Gaussian map (frame sharding); rank 0 broadcasts the canonical
+Gaussian set over RCCL every --bcast-every steps (inside the timed region).
+`value` = frames processed by all ranks / max-over-ranks wall time.
+
+The JSON line carries:
+  roofline      -- render-backward kernel: SURVEY.md 8(d) algorithmic bytes per
+                   launch (8*Tt + 40*I + 20*N + 44*P, measured I) over its
+                   average duration from hipEvents recorded around that kernel
+                   on its launch stream during the timed region;
+  cpu_baseline  -- rank 0 at N=1 only: the float32 C oracle (oracle/) on one
+                   frame of the same workload, single thread.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "rasterize fwd+bwd frames/sec @640×480, 300k Gaussians; HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK_TFLOPS = 157.3  # FP32 vector (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--bcast-every", type=int, default=40,
+                    help="broadcast the Gaussian map every k steps (Replica: 40 tracking iters/frame)")
+    ap.add_argument("--cpu-baseline", choices=("auto", "on", "off"), default="auto")
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def img_n_contrib_sum(img_buffer: torch.Tensor, W: int, H: int) -> int:
+    """Sum of per-pixel n_contrib (= pairs the backward evaluates); ImgLayout in csrc/gsr_common.h."""
+    N = W * H
+    off = (4 * N + 255) // 256 * 256
+    nc = img_buffer[off:off + 4 * N].view(torch.int32)
+    return int(nc.sum().item())
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from splatam_amd import profiling
+    from splatam_amd.scenes import CONFIGS, config_scene
+    from splatam_amd.slam import camera_settings, get_loss_tracking, init_tracking_params, transformed_params2rendervar, \
+        transformed_params2depthplussilhouette, transform_to_frame
+    from splatam_amd.rasterizer import GaussianRasterizer
+
+    cfg = CONFIGS[args.config]
+    scene = config_scene(args.config)
+    P, W, H = scene.P, scene.cam.W, scene.cam.H
+    params = init_tracking_params(scene, num_frames=max(world, 1), device=dev)
+    map_keys = ("means3D", "rgb_colors", "unnorm_rotations", "logit_opacities", "log_scales")
+    if world > 1:
+        for k in map_keys:
+            dist.broadcast(params[k], src=0)
+    frame = rank  # frame sharding: rank r tracks frame r
+    cam = camera_settings(scene.cam, dev)
+    w2c = torch.eye(4, device=dev)
+    # targets: renders at the unperturbed pose (ground truth of the synthetic frame)
+    with torch.no_grad():
+        gt = dict(params)
+        gt["cam_unnorm_rots"] = torch.zeros_like(params["cam_unnorm_rots"])
+        gt["cam_unnorm_rots"][0, 0] = 1.0
+        gt["cam_trans"] = torch.zeros_like(params["cam_trans"])
+        tg = transform_to_frame(gt, frame, False, False)
+        im, _, _ = GaussianRasterizer(cam)(**transformed_params2rendervar(gt, tg))
+        ds, _, _ = GaussianRasterizer(cam)(**transformed_params2depthplussilhouette(gt, w2c, tg))
+    curr = {"cam": cam, "w2c": w2c, "im": im.clone(), "depth": ds[0:1].clone()}
+    params["cam_unnorm_rots"].requires_grad_(True)
+    params["cam_trans"].requires_grad_(True)
+    opt = torch.optim.Adam([{"params": [params["cam_unnorm_rots"]], "lr": 0.0004},
+                            {"params": [params["cam_trans"]], "lr": 0.002}])  # configs/replica/splatam.py:71-80
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss, _, _ = get_loss_tracking(params, curr, frame)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    profiling.enable_timing(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        if world > 1 and args.bcast_every > 0 and i % args.bcast_every == 0:
+            with torch.no_grad():
+                for k in map_keys:
+                    dist.broadcast(params[k], src=0)
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    stages = profiling.read_timing()
+    profiling.enable_timing(False)
+    elapsed = torch.tensor([t1 - t0], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    frames = args.steps * world
+    value = frames / elapsed
+
+    # ---- roofline of the dominant kernel (render backward) ------------------
+    rb = stages["render_bwd"]
+    Tt = ((W + 15) // 16) * ((H + 15) // 16)
+    N = W * H
+    I_avg = rb["units"] / max(rb["launches"], 1)
+    bytes_per_launch = 8 * Tt + 40 * I_avg + 20 * N + 44 * P
+    dur_s = rb["avg_us"] * 1e-6
+    achieved = bytes_per_launch / dur_s / 1e9 if dur_s > 0 else 0.0
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "render_bwd_pmc.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"kernel": "render_bwd_kernel", "bound": "hbm", "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic, "alg_bytes_per_launch": int(bytes_per_launch), "avg_us": round(rb["avg_us"], 2),
+                "num_rendered_avg": int(I_avg)}
+
+    # ---- CPU baseline: the float32 C oracle on one frame (rank 0, N=1) ------
+    cpu = None
+    want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
+    if want_cpu and rank == 0:
+        import numpy as np
+        from oracle import oracle as orc
+        with torch.no_grad():
+            tg = transform_to_frame(params, frame, False, False)
+            rv = transformed_params2rendervar(params, tg)
+            dv = transformed_params2depthplussilhouette(params, w2c, tg)
+        c = scene.cam
+        common = dict(view=c.viewmatrix.numpy(), proj=c.projmatrix.numpy(), campos=c.campos.numpy(),
+                      tanfovx=c.tanfovx, tanfovy=c.tanfovy, H=H, W=W)
+        rng = np.random.RandomState(0)
+        t_cpu = time.perf_counter()
+        evals = contrib = 0
+        for r in (rv, dv):
+            fr = orc.forward(r["means3D"].cpu().numpy(), r["opacities"].cpu().numpy(),
+                             colors=r["colors_precomp"].cpu().numpy(), scales=r["scales"].cpu().numpy(),
+                             rotations=r["rotations"].cpu().numpy(), **common)
+            g = orc.backward(fr, rng.randn(3, H, W).astype(np.float32))
+            evals += g["pair_evals"]
+            contrib += g["pair_contrib"]
+        t_cpu = time.perf_counter() - t_cpu
+        cpu = {"value": round(1.0 / t_cpu, 5), "unit": "frames/s", "cores": 1, "kind": "port",
+               "sample": f"1 frame (RGB + depth/silhouette render fwd+bwd) of config {args.config} "
+                         f"({P} Gaussians, {W}x{H}) through oracle/gsr_oracle.c float32, 1 thread, "
+                         f"{t_cpu:.1f} s"}
+        # VALU view of the same kernel: F_eval=12 per evaluated pair, +45 per contributing pair
+        flops = 12 * evals / 2 + 45 * contrib / 2
+        roofline["valu"] = {"achieved_tflops": round(flops / dur_s / 1e12, 3) if dur_s > 0 else None,
+                            "peak_tflops": VALU_PEAK_TFLOPS,
+                            "frac": round(flops / dur_s / 1e12 / VALU_PEAK_TFLOPS, 4) if dur_s > 0 else None,
+                            "pairs_evaluated": int(evals / 2), "pairs_contributing": int(contrib / 2)}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (SURVEY.md 8(d) seeded scene; targets rendered at the unperturbed pose)",
+            "config": {"workload": f"config {args.config}: {P} isotropic Gaussians, {W}x{H}, SplaTAM tracking "
+                                   "iteration (RGB + depth/silhouette render fwd+bwd, masked L1, Adam on pose)",
+                       "gaussians": P, "width": W, "height": H, "frames_per_step_per_gpu": 1,
+                       "broadcast_every": args.bcast_every if world > 1 else None,
+                       "parallelism": f"frame-sharded x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items()},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

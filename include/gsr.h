@@ -128,6 +128,22 @@ size_t gsr_image_buffer_bytes(int image_width, int image_height);
 const char* gsr_last_error(void);
 int gsr_abi_version(void);
 
+/* Per-stage device timing (diagnostics, bench.py).  When enabled, every stage
+ * below is bracketed by hipEvents recorded on the launch stream; read returns
+ * accumulated milliseconds, launch counts and work units (P for per-Gaussian
+ * stages, num_rendered for per-instance stages) since the last enable.
+ * Process-wide (autograd runs backward on its own thread).  gsr_timing_read synchronises on the recorded events. */
+#define GSR_STAGE_PREPROCESS 0 /* preprocess + tile-count scan  */
+#define GSR_STAGE_DUPLICATE 1  /* duplicateWithKeys              */
+#define GSR_STAGE_SORT 2       /* radix sort (all passes)        */
+#define GSR_STAGE_RANGES 3     /* identifyTileRanges + id gather */
+#define GSR_STAGE_RENDER_FWD 4 /* renderCUDA forward             */
+#define GSR_STAGE_RENDER_BWD 5 /* render backward                */
+#define GSR_STAGE_GAUSS_BWD 6  /* per-Gaussian chain rule        */
+#define GSR_NUM_STAGES 7
+int gsr_timing_enable(int on);
+int gsr_timing_read(double* ms, long long* launches, long long* units, int n);
+
 /* Test hook (tests/test_gpu_kernels.py): wave64 transposed reduction of
  * in_dev[64*9] (lane-major) into out_dev[9]; checks the permlane/DPP lane
  * mapping the backward relies on. */

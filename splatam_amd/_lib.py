@@ -49,6 +49,8 @@ SIGNATURES = {
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_abi_version": (c_int, []),
     "gsr_selftest_reduce9": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "gsr_timing_enable": (c_int, [c_int]),
+    "gsr_timing_read": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
 }
 
 

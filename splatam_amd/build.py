@@ -29,7 +29,10 @@ def hipcc() -> str:
 
 
 def flags():
+    # -fno-slp-vectorize: keep f32 adds/muls single-issue; SLP packing into v_pk_*_f32
+    # splits every DPP-fused add into v_mov_b32_dpp + v_pk_add (cdna_hip_programming.md App. B).
     return ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-function",
+            "-fno-slp-vectorize",
             "-I", os.path.join(ROOT, "include"), "-I", CSRC]
 
 

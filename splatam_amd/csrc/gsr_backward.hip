@@ -17,24 +17,30 @@
 
 namespace gsr {
 
+constexpr int BWD_BATCH = 128;
+constexpr int BWD_GROUP = 4;
+
 __global__ void __launch_bounds__(TILE_PIX)
 render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                   const uint32_t* __restrict__ perm, const float4* __restrict__ rec_a,
                   const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
                   const float* __restrict__ final_T, const uint32_t* __restrict__ n_contrib,
                   const float* __restrict__ dL_dpix, float4* __restrict__ inst) {
-    __shared__ float4 s_a[RENDER_BATCH];
-    __shared__ float4 s_b[RENDER_BATCH];
-    __shared__ float4 s_c[RENDER_BATCH];
-    __shared__ uint32_t s_u[RENDER_BATCH];
-    __shared__ float s_acc[4 * RENDER_BATCH * 9];
+    __shared__ float4 s_a[BWD_BATCH];
+    __shared__ float4 s_b[BWD_BATCH];
+    __shared__ float4 s_c[BWD_BATCH];
+    __shared__ uint32_t s_u[BWD_BATCH];
+    __shared__ __attribute__((aligned(16))) float s_acc[4 * BWD_BATCH * 9];
     __shared__ uint32_t s_wmax[4];
+    __shared__ uint8_t s_mask[BWD_BATCH];
+    __shared__ __attribute__((aligned(16))) uint16_t s_list[4][BWD_BATCH + BWD_GROUP];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int tile = blockIdx.y * cam.gx + blockIdx.x;
     const int px = blockIdx.x * TILE_X + (tid & (TILE_X - 1));
     const int py = blockIdx.y * TILE_Y + (tid >> 4);
     const bool inside = px < cam.W && py < cam.H;
     const int pid = py * cam.W + px;
+    const float x0 = (float)(blockIdx.x * TILE_X), y0 = (float)(blockIdx.y * TILE_Y);
     const int HW = cam.W * cam.H;
     const uint2 range = ranges[tile];
     const float T_final = inside ? final_T[pid] : 0.f;
@@ -59,86 +65,123 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         inst[3 * u + 2] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const float bg_dot = cam.bg[0] * dp0 + cam.bg[1] * dp1 + cam.bg[2] * dp2;
-    const float ddelx = (float)(0.5 * cam.W), ddely = (float)(0.5 * cam.H);  // backward.cu:935-936
+    const bool bg_on = cam.bg[0] != 0.f || cam.bg[1] != 0.f || cam.bg[2] != 0.f;  // uniform
     const float pxf = (float)px, pyf = (float)py;
     float T = T_final;
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, lc0 = 0.f, lc1 = 0.f, lc2 = 0.f, last_alpha = 0.f;
     const int row = lane >> 4;
-    for (int hi = (int)bmax; hi > 0; hi -= RENDER_BATCH) {
-        const int cnt = min(RENDER_BATCH, hi);
+    // records of the first batch (back to front)
+    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa;
+    uint32_t pu = 0;
+    if (tid < min(BWD_BATCH, (int)bmax)) {
+        const uint32_t k = range.x + bmax - 1 - tid;
+        const uint32_t gi = point_list[k];
+        pu = perm[k]; pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
+    }
+    for (int hi = (int)bmax; hi > 0; hi -= BWD_BATCH) {
+        const int cnt = min(BWD_BATCH, hi);
         if (tid < cnt) {
-            const uint32_t k = range.x + (uint32_t)(hi - 1 - tid);
-            const uint32_t gi = point_list[k];
-            s_u[tid] = perm[k];
-            s_a[tid] = rec_a[gi];
-            s_b[tid] = rec_b[gi];
-            s_c[tid] = rec_c[gi];
+            s_u[tid] = pu;
+            s_a[tid] = pa;
+            s_b[tid] = pb;
+            s_c[tid] = pc;
+            s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
         }
-        for (int q = tid; q < 4 * RENDER_BATCH * 9 / 4; q += TILE_PIX)
+        for (int q = tid; q < 4 * BWD_BATCH * 9 / 4; q += TILE_PIX)
             reinterpret_cast<float4*>(s_acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         __syncthreads();
-        for (int j = 0; j < cnt; j++) {
-            const uint32_t pos = (uint32_t)(hi - 1 - j);  // position in the tile list
-            if (pos >= wmax) continue;                     // wave-uniform: no lane reaches it
-            float v[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            bool contrib = false;
-            if (pos < last) {
-                const float4 a = s_a[j];
-                const float4 b = s_b[j];
-                const float dx = a.x - pxf, dy = a.y - pyf;
-                const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-                const float G = __expf(power);
-                const float alpha = fminf(0.99f, b.y * G);
-                if (power <= 0.0f && alpha >= 1.0f / 255.0f) {
-                    contrib = true;
-                    const float4 c = s_c[j];
-                    T = T / (1.f - alpha);
-                    const float dchannel = alpha * T;
-                    acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-                    acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-                    acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
+        {   // prefetch the next batch
+            const int nhi = hi - BWD_BATCH;
+            if (tid < min(BWD_BATCH, nhi)) {
+                const uint32_t k = range.x + (uint32_t)(nhi - 1 - tid);
+                const uint32_t gi = point_list[k];
+                pu = perm[k]; pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
+            }
+        }
+        // entries j with pos = hi-1-j >= wmax lie behind every pixel of this wave
+        const int n = build_strip_list(s_mask, cnt, w, hi - (int)wmax, s_list[w]);
+        Group4 nxt;
+        if (n > 0) load_group4(s_list[w], 0, n, s_a, s_b, nxt);
+        for (int i = 0; i < n; i += BWD_GROUP) {
+            const Group4 cur = nxt;
+            if (i + BWD_GROUP < n) load_group4(s_list[w], i + BWD_GROUP, n, s_a, s_b, nxt);  // in flight during math
+            int j[BWD_GROUP];
+            float4 a[BWD_GROUP], b[BWD_GROUP];
+            bool ok[BWD_GROUP];
+            float dx[BWD_GROUP], dy[BWD_GROUP], G[BWD_GROUP], alpha[BWD_GROUP];
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < BWD_GROUP; k++) {
+                j[k] = cur.j[k];
+                a[k] = cur.a[k];
+                b[k] = cur.b[k];
+                dx[k] = a[k].x - pxf;
+                dy[k] = a[k].y - pyf;
+                const float power = -0.5f * (a[k].z * dx[k] * dx[k] + b[k].x * dy[k] * dy[k]) - a[k].w * dx[k] * dy[k];
+                G[k] = __expf(power);
+                alpha[k] = fminf(0.99f, b[k].y * G[k]);
+                const uint32_t pos = (uint32_t)(hi - 1 - j[k]);  // position in the tile list
+                ok[k] = cur.valid[k] && pos < last && power <= 0.0f && alpha[k] >= 1.0f / 255.0f;
+                any = any || ok[k];
+            }
+            if (__ballot(any) == 0ull) continue;
+            // Per pair: reduce (hx, hy, hx*dx, hx*dy, hy*dy, G*dL/dalpha, dchannel*dL/dpix[3]) with
+            // h = G * dL/dG.  gauss_bwd turns them into the reference's per-pair quantities
+            // (backward.cu:1020-1038): dmean2D = -ddel * (Q [hx, hy]), dconic = -0.5 * (hxx, hxy, hyy);
+            // both are linear in the sums, the conic Q being constant per Gaussian.
+            float v[BWD_GROUP * 9];
+#pragma unroll
+            for (int k = 0; k < BWD_GROUP; k++) {
+                const float4 c = s_c[j[k]];
+                const float inv = __builtin_amdgcn_rcpf(1.f - alpha[k]);  // v_rcp_f32 (~1 ulp)
+                const float Tn = T * inv;                                  // T / (1 - alpha), backward.cu:978
+                const float na0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
+                const float na1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
+                const float na2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
+                float dL_dalpha = ((c.x - na0) * dp0 + (c.y - na1) * dp1 + (c.z - na2) * dp2) * Tn;
+                if (bg_on) dL_dalpha += (-T_final * inv) * bg_dot;
+                const bool o_ = ok[k];
+                dL_dalpha = o_ ? dL_dalpha : 0.f;
+                const float Gz = o_ ? G[k] : 0.f;
+                const float dch = o_ ? alpha[k] * Tn : 0.f;
+                const float h = Gz * (b[k].y * dL_dalpha);
+                const float hx = h * dx[k], hy = h * dy[k];
+                float* vk = v + 9 * k;
+                vk[0] = hx;
+                vk[1] = hy;
+                vk[2] = hx * dx[k];
+                vk[3] = hx * dy[k];
+                vk[4] = hy * dy[k];
+                vk[5] = Gz * dL_dalpha;
+                vk[6] = dch * dp0;
+                vk[7] = dch * dp1;
+                vk[8] = dch * dp2;
+                if (o_) {
+                    T = Tn;
+                    acc0 = na0; acc1 = na1; acc2 = na2;
                     lc0 = c.x; lc1 = c.y; lc2 = c.z;
-                    float dL_dalpha = (c.x - acc0) * dp0 + (c.y - acc1) * dp1 + (c.z - acc2) * dp2;
-                    v[6] = dchannel * dp0;
-                    v[7] = dchannel * dp1;
-                    v[8] = dchannel * dp2;
-                    dL_dalpha *= T;
-                    last_alpha = alpha;
-                    dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-                    const float dL_dG = b.y * dL_dalpha;
-                    const float gdx = G * dx, gdy = G * dy;
-                    const float dG_ddelx = -gdx * a.z - gdy * a.w;
-                    const float dG_ddely = -gdy * b.x - gdx * a.w;
-                    v[0] = dL_dG * dG_ddelx * ddelx;
-                    v[1] = dL_dG * dG_ddely * ddely;
-                    v[2] = -0.5f * gdx * dx * dL_dG;
-                    v[3] = -0.5f * gdx * dy * dL_dG;
-                    v[4] = -0.5f * gdy * dy * dL_dG;
-                    v[5] = G * dL_dalpha;
+                    last_alpha = alpha[k];
                 }
             }
-            if (__ballot(contrib) == 0ull) continue;
-            float r0, r1, r8;
-            wave_reduce9(v, r0, r1, r8);
-            if ((lane & 15) == 0) {
-                float* dst = s_acc + (w * RENDER_BATCH + j) * 9;
-                const int sl = reduce9_slot_r0(row);
-                dst[sl] = r0;
-                dst[4 + sl] = r1;
-                if (row == 0) dst[8] = r8;
+            float r[9];
+            wave_reduce4x9(v, r);
+            if ((lane & 15) == 0 && i + row < n) {
+                float* dst = s_acc + (w * BWD_BATCH + j[row]) * 9;
+#pragma unroll
+                for (int m = 0; m < 9; m++) dst[m] = r[m];
             }
         }
         __syncthreads();
         if (tid < cnt) {
-            float s[9];
+            float sum[9];
 #pragma unroll
-            for (int q = 0; q < 9; q++)
-                s[q] = s_acc[(0 * RENDER_BATCH + tid) * 9 + q] + s_acc[(1 * RENDER_BATCH + tid) * 9 + q] +
-                       s_acc[(2 * RENDER_BATCH + tid) * 9 + q] + s_acc[(3 * RENDER_BATCH + tid) * 9 + q];
+            for (int m = 0; m < 9; m++)
+                sum[m] = s_acc[(0 * BWD_BATCH + tid) * 9 + m] + s_acc[(1 * BWD_BATCH + tid) * 9 + m] +
+                         s_acc[(2 * BWD_BATCH + tid) * 9 + m] + s_acc[(3 * BWD_BATCH + tid) * 9 + m];
             const uint32_t u = s_u[tid];
-            inst[3 * u] = make_float4(s[0], s[1], s[2], s[3]);
-            inst[3 * u + 1] = make_float4(s[4], s[5], s[6], s[7]);
-            inst[3 * u + 2] = make_float4(s[8], 0.f, 0.f, 0.f);
+            inst[3 * u] = make_float4(sum[0], sum[1], sum[2], sum[3]);
+            inst[3 * u + 1] = make_float4(sum[4], sum[5], sum[6], sum[7]);
+            inst[3 * u + 2] = make_float4(sum[8], 0.f, 0.f, 0.f);
         }
         __syncthreads();
     }
@@ -346,6 +389,16 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
             g2[4] += r1.x; g2[5] += r1.y; g2[6] += r1.z; g2[7] += r1.w;
             g2[8] += r2;
         }
+        // instance records hold (hx, hy, hxx, hxy, hyy, dopacity, dcolor) sums (render_bwd_kernel)
+        const float4 ra = geo.rec_a[i];
+        const float Cc = geo.rec_b[i].x;
+        const float ddelx = (float)(0.5 * cam.W), ddely = (float)(0.5 * cam.H);  // backward.cu:935-936
+        const float hx = g2[0], hy = g2[1];
+        g2[0] = -(ra.z * hx + ra.w * hy) * ddelx;
+        g2[1] = -(Cc * hy + ra.w * hx) * ddely;
+        g2[2] *= -0.5f;
+        g2[3] *= -0.5f;
+        g2[4] *= -0.5f;
         const unsigned clamped = __float_as_uint(geo.rec_c[i].w);
         gauss_chain(cam, g, i, g2, clamped, dmean, dcov, dscale, drot, dsh, nsh);
     }

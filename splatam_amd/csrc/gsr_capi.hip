@@ -8,7 +8,9 @@
 // pinned per-thread staging word.
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/gsr.h"
 #include "gsr_common.h"
@@ -98,6 +100,69 @@ void* obtain(gsr_alloc_fn alloc, void* ctx, int kind, size_t bytes) {
     return p;
 }
 
+// ---- optional per-stage timing with hipEvents on the launch stream --------
+struct TimedRec {
+    int stage;
+    long long units;
+    hipEvent_t a, b;
+};
+struct Timing {
+    bool on = false;
+    std::vector<TimedRec> recs;
+    std::vector<hipEvent_t> pool;
+    double ms[GSR_NUM_STAGES] = {};
+    long long launches[GSR_NUM_STAGES] = {};
+    long long units[GSR_NUM_STAGES] = {};
+    ~Timing() {
+        for (auto& r : recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+    hipEvent_t take() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+};
+// Global (not thread-local): torch runs autograd backward on its own thread.
+Timing g_timing;
+std::mutex g_timing_mu;
+
+struct StageTimer {  // brackets the launches of one stage
+    TimedRec rec{};
+    hipStream_t s;
+    bool on;
+    StageTimer(int stage, long long units, hipStream_t s_) : s(s_), on(g_timing.on) {
+        if (!on) return;
+        rec.stage = stage; rec.units = units;
+        {
+            std::lock_guard<std::mutex> lk(g_timing_mu);
+            rec.a = g_timing.take(); rec.b = g_timing.take();
+        }
+        (void)hipEventRecord(rec.a, s);
+    }
+    ~StageTimer() {
+        if (!on) return;
+        (void)hipEventRecord(rec.b, s);
+        std::lock_guard<std::mutex> lk(g_timing_mu);
+        g_timing.recs.push_back(rec);
+    }
+};
+
+void timing_drain() {  // caller holds g_timing_mu
+    for (auto& r : g_timing.recs) {
+        float ms = 0.f;
+        if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            g_timing.ms[r.stage] += ms;
+            g_timing.launches[r.stage] += 1;
+            g_timing.units[r.stage] += r.units;
+        }
+        g_timing.pool.push_back(r.a);
+        g_timing.pool.push_back(r.b);
+    }
+    g_timing.recs.clear();
+}
+
 }  // namespace
 
 extern "C" {
@@ -134,9 +199,12 @@ int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, fl
     if (P > 0) {
         if (!radii) return fail(GSR_ERR_INVALID_ARG, "radii output required");
         if ((e = hipMemsetAsync(geo.counters, 0, 16, stream)) != hipSuccess) return hip_fail(e, "memset counters");
-        if ((e = launch_preprocess(cam, g, geo, radii, GL.nb, stream)) != hipSuccess) return hip_fail(e, "preprocess");
-        if ((e = launch_exclusive_scan(geo.blocksums, (uint32_t)GL.nb, geo.counters, stream)) != hipSuccess)
-            return hip_fail(e, "scan");
+        {
+            StageTimer t(GSR_STAGE_PREPROCESS, P, stream);
+            if ((e = launch_preprocess(cam, g, geo, radii, GL.nb, stream)) != hipSuccess) return hip_fail(e, "preprocess");
+            if ((e = launch_exclusive_scan(geo.blocksums, (uint32_t)GL.nb, geo.counters, stream)) != hipSuccess)
+                return hip_fail(e, "scan");
+        }
         if (!g_pinned.p) {
             if ((e = hipHostMalloc((void**)&g_pinned.p, 16, hipHostMallocDefault)) != hipSuccess)
                 return hip_fail(e, "hipHostMalloc");
@@ -161,16 +229,29 @@ int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, fl
     if ((e = hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)cam.gx * cam.gy, stream)) != hipSuccess)
         return hip_fail(e, "memset ranges");
     if (I > 0) {
-        if ((e = launch_duplicate(cam, P, geo, keys[0], gid, GL.nb, stream)) != hipSuccess) return hip_fail(e, "duplicate");
-        if ((e = launch_radix_sort(keys, vals, hist, I, BL.nsb, BL.npass, stream)) != hipSuccess)
-            return hip_fail(e, "radix sort");
-        if ((e = launch_ranges(keys[BL.final_buf], vals[BL.final_buf], gid, point_list, ranges, I, stream)) !=
-            hipSuccess)
-            return hip_fail(e, "ranges");
+        {
+            StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
+            if ((e = launch_duplicate(cam, P, geo, keys[0], gid, GL.nb, stream)) != hipSuccess)
+                return hip_fail(e, "duplicate");
+        }
+        {
+            StageTimer t(GSR_STAGE_SORT, I, stream);
+            if ((e = launch_radix_sort(keys, vals, hist, I, BL.nsb, BL.npass, stream)) != hipSuccess)
+                return hip_fail(e, "radix sort");
+        }
+        {
+            StageTimer t(GSR_STAGE_RANGES, I, stream);
+            if ((e = launch_ranges(keys[BL.final_buf], vals[BL.final_buf], gid, point_list, ranges, I, stream)) !=
+                hipSuccess)
+                return hip_fail(e, "ranges");
+        }
     }
-    if ((e = launch_render_fwd(cam, ranges, point_list, geo, nullptr, final_T, n_contrib, out_color, out_depth,
-                               stream)) != hipSuccess)
-        return hip_fail(e, "render");
+    {
+        StageTimer t(GSR_STAGE_RENDER_FWD, I, stream);
+        if ((e = launch_render_fwd(cam, ranges, point_list, geo, nullptr, final_T, n_contrib, out_color, out_depth,
+                                   stream)) != hipSuccess)
+            return hip_fail(e, "render");
+    }
     return (int)I;
 }
 
@@ -208,6 +289,7 @@ int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, c
         const char* bb = (const char*)binning_buffer;
         const uint32_t* perm = (const uint32_t*)(bb + BL.vals[BL.final_buf]);
         const uint32_t* point_list = (const uint32_t*)(bb + BL.point_list);
+        StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream);
         if ((e = launch_render_bwd(cam, ranges, point_list, perm, geo, nullptr, final_T, n_contrib, dL_dout_color,
                                    inst, stream)) != hipSuccess)
             return hip_fail(e, "render backward");
@@ -216,8 +298,11 @@ int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, c
                  grads->dcov3D,   grads->dsh,     grads->dscales,  grads->drotations};
     if (!out.dmeans2D || !out.dcolors || !out.dopacity || !out.dmeans3D || !out.dcov3D || !out.dscales || !out.drot)
         return fail(GSR_ERR_INVALID_ARG, "gradient output pointers required");
-    if ((e = launch_gauss_bwd(cam, g, geo, radii, inst, out, stream)) != hipSuccess)
-        return hip_fail(e, "gaussian backward");
+    {
+        StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
+        if ((e = launch_gauss_bwd(cam, g, geo, radii, inst, out, stream)) != hipSuccess)
+            return hip_fail(e, "gaussian backward");
+    }
     return GSR_OK;
 }
 
@@ -230,6 +315,25 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
     hipError_t e = launch_mark_visible(P, means3D, viewmatrix, visible, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "mark_visible");
     return GSR_OK;
+}
+
+int gsr_timing_enable(int on) {
+    std::lock_guard<std::mutex> lk(g_timing_mu);
+    timing_drain();
+    g_timing.on = on != 0;
+    for (int i = 0; i < GSR_NUM_STAGES; i++) { g_timing.ms[i] = 0.0; g_timing.launches[i] = 0; g_timing.units[i] = 0; }
+    return GSR_OK;
+}
+
+int gsr_timing_read(double* ms, long long* launches, long long* units, int n) {
+    std::lock_guard<std::mutex> lk(g_timing_mu);
+    timing_drain();
+    for (int i = 0; i < n && i < GSR_NUM_STAGES; i++) {
+        if (ms) ms[i] = g_timing.ms[i];
+        if (launches) launches[i] = g_timing.launches[i];
+        if (units) units[i] = g_timing.units[i];
+    }
+    return GSR_NUM_STAGES;
 }
 
 // Test hook: validates the wave64 permlane/DPP reduction on the device.

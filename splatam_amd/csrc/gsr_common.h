@@ -84,7 +84,7 @@ struct BinLayout {        // per-instance state ("binningBuffer")
     size_t vals[2];       // u32 [I] ping-pong (values = unsorted instance index)
     size_t gid;           // u32 [I] Gaussian id of each unsorted instance
     size_t point_list;    // u32 [I] Gaussian ids in (tile, depth) order
-    size_t hist;          // u32 [RADIX * nsb]
+    size_t hist;          // u32 [RADIX * nsb] + [RADIX] digit totals
     size_t total;
     int nsb;              // radix-sort workgroups
     int npass;            // 8-bit LSD passes over bits [0, 32 + msb(tiles))
@@ -104,7 +104,7 @@ struct BinLayout {        // per-instance state ("binningBuffer")
         L.vals[1] = o; o = align_up(o + 4 * n, 256);
         L.gid = o; o = align_up(o + 4 * n, 256);
         L.point_list = o; o = align_up(o + 4 * n, 256);
-        L.hist = o; o = align_up(o + 4 * (size_t)RADIX * L.nsb, 256);
+        L.hist = o; o = align_up(o + 4 * ((size_t)RADIX * L.nsb + RADIX), 256);  // + digit totals
         L.total = o;
         return L;
     }
@@ -299,6 +299,51 @@ __device__ __forceinline__ void sh_fwd(int deg, float3 pos, const float* campos,
     }
 }
 
+// 4-bit mask of the 16x4-pixel wave strips of a tile (pixel centres x0..x0+15,
+// rows y0+4w..y0+4w+3) that a Gaussian can contribute to, i.e. where
+// o * exp(-0.5 d^T Q d) >= 1/255 (forward.cu:341-351).  The bound is
+// conservative: tau and the half-extents carry margins that exceed the float32
+// error of evaluating `power` (grows with the conic's eccentricity kappa), so
+// culling never changes a result.  Anything unusual (non-finite values,
+// non-positive-definite conic, extreme eccentricity) returns 0xF: no culling.
+__device__ __forceinline__ uint32_t strip_mask(float4 a, float4 b, float x0, float y0) {
+    const float A = a.z, B = a.w, C = b.x, o = b.y;
+    const float det = A * C - B * B;
+    if (!(det > 0.f) || !(A > 0.f) || !isfinite(det) || !isfinite(a.x) || !isfinite(a.y) || !isfinite(o))
+        return 0xFu;
+    const float kappa = A * C / det;  // 1 / (1 - rho^2) >= 1
+    if (!(kappa < 1e4f)) return 0xFu;
+    const float t = 255.f * o;
+    if (t < 0.999f) return 0u;  // alpha <= o < 1/255: never blended
+    const float tau = fmaxf(__logf(t), 0.f) * (1.001f + 4e-6f * kappa) + 1e-3f;
+    const float hx = sqrtf(2.f * tau * C / det) * 1.001f + 0.01f;
+    const float hy = sqrtf(2.f * tau * A / det) * 1.001f + 0.01f;
+    if (a.x + hx < x0 || a.x - hx > x0 + (float)(TILE_X - 1)) return 0u;
+    uint32_t m = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const float ylo = y0 + 4.f * w, yhi = ylo + 3.f;
+        if (a.y + hy >= ylo && a.y - hy <= yhi) m |= 1u << w;
+    }
+    return m;
+}
+
+// Ordered list of the batch entries whose strip mask has bit `w` (one wave
+// builds its own list; ballot + popcount compaction, order preserved).
+__device__ __forceinline__ int build_strip_list(const uint8_t* s_mask, int cnt, int w, int jmin, uint16_t* list) {
+    const int lane = __lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int n = 0;
+    for (int c = 0; c < cnt; c += 64) {
+        const int j = c + lane;
+        const bool bit = j < cnt && j >= jmin && ((s_mask[j] >> w) & 1u);
+        const uint64_t bal = __ballot(bit);
+        if (bit) list[n + __popcll(bal & lt)] = (uint16_t)j;
+        n += __popcll(bal);
+    }
+    return n;
+}
+
 // --------------------------------------------------------- wave64 helpers --
 template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float v) {
@@ -344,6 +389,59 @@ __device__ __forceinline__ void wave_reduce9(const float v[9], float& r0, float&
     r8 = row16_sum(t2);
 }
 __device__ __forceinline__ int reduce9_slot_r0(int row) { return (row == 0) ? 0 : (row == 1 ? 2 : (row == 2 ? 1 : 3)); }
+
+// One group of N consecutive entries of a wave's strip list, with the two
+// float4 records every evaluation needs (x, y, A, B / C, opacity, depth).
+template <int N>
+struct GroupN {
+    int j[N];
+    bool valid[N];
+    float4 a[N], b[N];
+};
+using Group4 = GroupN<4>;
+
+template <int N>
+__device__ __forceinline__ void load_group(const uint16_t* list, int i, int n, const float4* s_a, const float4* s_b,
+                                           GroupN<N>& g) {
+    static_assert(N == 2 || N == 4, "group of 2 or 4 list entries");
+    if constexpr (N == 4) {
+        const uint2 q = *reinterpret_cast<const uint2*>(&list[i]);
+        g.j[0] = (int)(q.x & 0xFFFFu);
+        g.j[1] = (int)(q.x >> 16);
+        g.j[2] = (int)(q.y & 0xFFFFu);
+        g.j[3] = (int)(q.y >> 16);
+    } else {
+        const uint32_t q = *reinterpret_cast<const uint32_t*>(&list[i]);
+        g.j[0] = (int)(q & 0xFFFFu);
+        g.j[1] = (int)(q >> 16);
+    }
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        g.valid[k] = i + k < n;
+        if (!g.valid[k]) g.j[k] = g.j[0];
+    }
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        g.a[k] = s_a[g.j[k]];
+        g.b[k] = s_b[g.j[k]];
+    }
+}
+__device__ __forceinline__ void load_group4(const uint16_t* list, int i, int n, const float4* s_a, const float4* s_b,
+                                            Group4& g) {
+    load_group<4>(list, i, n, s_a, s_b, g);
+}
+
+// Transposed reduction of 4 items x 9 values (v[item*9 + q]) over the 64 lanes:
+// 18 permlane32 + 9 permlane16 swaps and 36 DPP adds (~2.5 VALU per value).
+// On return row rho (= lane / 16) of r[q] holds, in all its 16 lanes, the wave
+// total of value q of item rho.
+__device__ __forceinline__ void wave_reduce4x9(const float (&v)[36], float (&r)[9]) {
+    float r1[18];
+#pragma unroll
+    for (int n = 0; n < 18; n++) r1[n] = swapsum32(v[n], v[n + 18]);
+#pragma unroll
+    for (int m = 0; m < 9; m++) r[m] = row16_sum(swapsum16(r1[m], r1[m + 9]));
+}
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 

@@ -10,6 +10,8 @@
 //   ranges      (rasterizer_impl.cu:116-138) + point_list gather of Gaussian ids
 //   render      (forward.cu:261-393) 16x16 tile per 256-lane workgroup, 256-entry
 //               LDS batches, block-wide early exit
+#include <cstdlib>
+
 #include "gsr_common.h"
 
 namespace gsr {
@@ -224,13 +226,48 @@ radix_hist_kernel(const uint64_t* __restrict__ keys, uint32_t n, int shift, uint
     hist[(size_t)tid * nsb + blockIdx.x] = c;
 }
 
+// Per-digit exclusive scan of the [digit][block] histogram rows: workgroup d
+// scans row d in place and writes the digit total (no single-workgroup
+// bottleneck over RADIX * nsb entries).
+__global__ void __launch_bounds__(256) radix_rowscan_kernel(uint32_t* __restrict__ hist, int nsb,
+                                                            uint32_t* __restrict__ digit_total) {
+    __shared__ uint32_t wsums[4];
+    __shared__ uint32_t s_carry;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t* row = hist + (size_t)blockIdx.x * nsb;
+    if (tid == 0) s_carry = 0;
+    __syncthreads();
+    for (int base = 0; base < nsb; base += 256) {
+        const int i = base + tid;
+        const uint32_t x = (i < nsb) ? row[i] : 0u;
+        const uint32_t incl = wave_incl_scan(x);
+        if (lane == 63) wsums[w] = incl;
+        __syncthreads();
+        uint32_t off = s_carry;
+        for (int k = 0; k < w; k++) off += wsums[k];
+        if (i < nsb) row[i] = off + incl - x;
+        __syncthreads();
+        if (tid == 255) s_carry = off + incl;
+        __syncthreads();
+    }
+    if (tid == 0) digit_total[blockIdx.x] = s_carry;
+}
+
 __global__ void __launch_bounds__(SORT_THREADS)
 radix_scatter_kernel(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint64_t* __restrict__ kout,
-                     uint32_t* __restrict__ vout, uint32_t n, int shift, const uint32_t* __restrict__ hist, int nsb) {
+                     uint32_t* __restrict__ vout, uint32_t n, int shift, const uint32_t* __restrict__ hist, int nsb,
+                     const uint32_t* __restrict__ digit_total) {
     __shared__ uint32_t wcnt[SORT_THREADS / 64][RADIX];
+    __shared__ uint32_t s_dsum[SORT_THREADS / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     for (int k = tid; k < (SORT_THREADS / 64) * RADIX; k += SORT_THREADS) (&wcnt[0][0])[k] = 0;
+    // exclusive scan of the 256 digit totals -> global base of each digit
+    const uint32_t dt = digit_total[tid];
+    const uint32_t dincl = wave_incl_scan(dt);
+    if (lane == 63) s_dsum[w] = dincl;
     __syncthreads();
+    uint32_t dbase = dincl - dt;
+    for (int k = 0; k < w; k++) dbase += s_dsum[k];
     const uint32_t base = blockIdx.x * SORT_TILE + w * (SORT_TILE / 4);
     const uint64_t lt = (1ull << lane) - 1ull;
     uint64_t key[SORT_ITEMS];
@@ -252,7 +289,7 @@ radix_scatter_kernel(const uint64_t* __restrict__ kin, const uint32_t* __restric
     __syncthreads();
     {
         const uint32_t c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid];
-        const uint32_t g = hist[(size_t)tid * nsb + blockIdx.x];
+        const uint32_t g = dbase + hist[(size_t)tid * nsb + blockIdx.x];
         __syncthreads();
         wcnt[0][tid] = g;
         wcnt[1][tid] = g + c0;
@@ -273,13 +310,14 @@ radix_scatter_kernel(const uint64_t* __restrict__ kin, const uint32_t* __restric
 
 hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t n, int nsb, int npass,
                              hipStream_t s) {
+    uint32_t* digit_total = hist + (size_t)RADIX * nsb;
     for (int p = 0; p < npass; p++) {
         const int in = p & 1, out = in ^ 1;
         hipLaunchKernelGGL(radix_hist_kernel, dim3(nsb), dim3(SORT_THREADS), 0, s, keys[in], n, 8 * p, hist, nsb);
-        hipError_t e = launch_exclusive_scan(hist, (uint32_t)RADIX * nsb, nullptr, s);
-        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(radix_rowscan_kernel, dim3(RADIX), dim3(256), 0, s, hist, nsb, digit_total);
         hipLaunchKernelGGL(radix_scatter_kernel, dim3(nsb), dim3(SORT_THREADS), 0, s, keys[in],
-                           p == 0 ? (const uint32_t*)nullptr : vals[in], keys[out], vals[out], n, 8 * p, hist, nsb);
+                           p == 0 ? (const uint32_t*)nullptr : vals[in], keys[out], vals[out], n, 8 * p, hist, nsb,
+                           digit_total);
     }
     return hipGetLastError();
 }
@@ -312,6 +350,13 @@ hipError_t launch_ranges(const uint64_t* keys, const uint32_t* vals, const uint3
 }
 
 // ----------------------------------------------------------- render (fwd) --
+// Per 256-entry batch every Gaussian gets a 4-bit mask of the wave strips its
+// contribution ellipse reaches (strip_mask); each wave then walks only its own
+// compacted list, 4 entries per step: the LDS reads and exp/alpha of the 4
+// entries are independent (ILP), the transmittance chain is then applied in
+// order with predicated (branch-free) updates.  The next batch's global
+// gathers are issued before the current batch is rasterised.
+template <int FWD_GROUP, bool PREFETCH>
 __global__ void __launch_bounds__(TILE_PIX)
 render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                   const float4* __restrict__ rec_a, const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
@@ -320,46 +365,80 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     __shared__ float4 s_a[RENDER_BATCH];
     __shared__ float4 s_b[RENDER_BATCH];
     __shared__ float4 s_c[RENDER_BATCH];
-    const int tid = threadIdx.x;
+    __shared__ uint8_t s_mask[RENDER_BATCH];
+    __shared__ __attribute__((aligned(16))) uint16_t s_list[4][RENDER_BATCH + 4];
+    const int tid = threadIdx.x, w = tid >> 6;
     const int tile = blockIdx.y * cam.gx + blockIdx.x;
     const int px = blockIdx.x * TILE_X + (tid & (TILE_X - 1));
     const int py = blockIdx.y * TILE_Y + (tid >> 4);
+    const float x0 = (float)(blockIdx.x * TILE_X), y0 = (float)(blockIdx.y * TILE_Y);
     const bool inside = px < cam.W && py < cam.H;
     const float pxf = (float)px, pyf = (float)py;
     const uint2 range = ranges[tile];
     bool done = !inside;
     float T = 1.f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 15.0f;  // forward.cu:308 median-depth default
-    uint32_t contributor = 0, last = 0;
+    uint32_t last = 0;
+    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa;
+    if (range.x + tid < range.y) {
+        const uint32_t gi = point_list[range.x + tid];
+        pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
+    }
     for (uint32_t start = range.x; start < range.y; start += RENDER_BATCH) {
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
-        const uint32_t k = start + tid;
-        if (k < range.y) {
-            const uint32_t gi = point_list[k];
-            s_a[tid] = rec_a[gi];
-            float4 b = rec_b[gi];
-            s_b[tid] = b;
-            float4 c = colors ? make_float4(colors[3 * gi], colors[3 * gi + 1], colors[3 * gi + 2], 0.f) : rec_c[gi];
-            s_c[tid] = c;
+        const int cnt = (int)min((uint32_t)RENDER_BATCH, range.y - start);
+        if (tid < cnt) {
+            s_a[tid] = pa;
+            s_b[tid] = pb;
+            s_c[tid] = pc;
+            s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
         }
         __syncthreads();
-        const int cnt = (int)min((uint32_t)RENDER_BATCH, range.y - start);
-        for (int j = 0; j < cnt && !done; j++) {
-            contributor++;
-            const float4 a = s_a[j];
-            const float4 b = s_b[j];
-            const float dx = a.x - pxf, dy = a.y - pyf;
-            const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-            if (power > 0.0f) continue;
-            const float alpha = fminf(0.99f, b.y * __expf(power));
-            if (alpha < 1.0f / 255.0f) continue;
-            const float test_T = T * (1.f - alpha);
-            if (test_T < 0.0001f) { done = true; continue; }
-            const float4 c = s_c[j];
-            const float w = alpha * T;
-            C0 += c.x * w; C1 += c.y * w; C2 += c.z * w;
-            if (T > 0.5f && test_T < 0.5f) D = b.z;  // median depth (forward.cu:368-372)
-            T = test_T;
-            last = contributor;
+        {   // prefetch the next batch while this one is rasterised
+            const uint32_t k = start + RENDER_BATCH + tid;
+            if (k < range.y) {
+                const uint32_t gi = point_list[k];
+                pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
+            }
+        }
+        const int n = build_strip_list(s_mask, cnt, w, 0, s_list[w]);
+        const uint32_t pos0 = start - range.x;
+        GroupN<FWD_GROUP> nxt;
+        if (PREFETCH && n > 0) load_group<FWD_GROUP>(s_list[w], 0, n, s_a, s_b, nxt);
+        for (int i = 0; i < n; i += FWD_GROUP) {
+            if (__ballot(!done) == 0ull) break;
+            GroupN<FWD_GROUP> cur;
+            if (PREFETCH) {
+                cur = nxt;
+                if (i + FWD_GROUP < n) load_group<FWD_GROUP>(s_list[w], i + FWD_GROUP, n, s_a, s_b, nxt);
+            } else {
+                load_group<FWD_GROUP>(s_list[w], i, n, s_a, s_b, cur);
+            }
+            float4 c[FWD_GROUP];
+#pragma unroll
+            for (int k = 0; k < FWD_GROUP; k++) c[k] = s_c[cur.j[k]];
+            float power[FWD_GROUP], alpha[FWD_GROUP];
+#pragma unroll
+            for (int k = 0; k < FWD_GROUP; k++) {
+                const float dx = cur.a[k].x - pxf, dy = cur.a[k].y - pyf;
+                power[k] = -0.5f * (cur.a[k].z * dx * dx + cur.b[k].x * dy * dy) - cur.a[k].w * dx * dy;
+                alpha[k] = fminf(0.99f, cur.b[k].y * __expf(power[k]));
+            }
+#pragma unroll
+            for (int k = 0; k < FWD_GROUP; k++) {
+                const bool ok = cur.valid[k] && !done && power[k] <= 0.0f && alpha[k] >= 1.0f / 255.0f;
+                const float test_T = T * (1.f - alpha[k]);
+                const bool term = ok && test_T < 0.0001f;
+                done = done || term;
+                const bool blend = ok && !term;
+                if (blend) {
+                    C0 += c[k].x * alpha[k] * T;
+                    C1 += c[k].y * alpha[k] * T;
+                    C2 += c[k].z * alpha[k] * T;
+                    if (T > 0.5f && test_T < 0.5f) D = cur.b[k].z;  // median depth (forward.cu:368-372)
+                    T = test_T;
+                    last = pos0 + (uint32_t)cur.j[k] + 1u;            // entries visited up to the last blend
+                }
+            }
         }
         __syncthreads();
     }
@@ -378,8 +457,16 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* colors, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_depth, hipStream_t s) {
-    hipLaunchKernelGGL(render_fwd_kernel, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list,
-                       geo.rec_a, geo.rec_b, geo.rec_c, colors, final_T, n_contrib, out_color, out_depth);
+    // GSR_FWD_VARIANT (tuning only): 0 = 4-entry groups, 1 = 4 + prefetch, 2 = 2-entry groups + prefetch
+    static const int variant = [] {
+        const char* e = getenv("GSR_FWD_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    auto k = render_fwd_kernel<4, false>;
+    if (variant == 1) k = render_fwd_kernel<4, true>;
+    if (variant == 2) k = render_fwd_kernel<2, true>;
+    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rec_a, geo.rec_b,
+                       geo.rec_c, colors, final_T, n_contrib, out_color, out_depth);
     return hipGetLastError();
 }
 

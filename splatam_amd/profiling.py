@@ -1,0 +1,23 @@
+"""Per-stage device timing of the rasterizer (hipEvents recorded by libgsr on
+the launch stream; see gsr_timing_* in include/gsr.h)."""
+from __future__ import annotations
+
+import ctypes
+
+from ._lib import lib
+
+STAGES = ("preprocess", "duplicate", "sort", "ranges", "render_fwd", "render_bwd", "gauss_bwd")
+
+
+def enable_timing(on: bool = True) -> None:
+    lib.gsr_timing_enable(1 if on else 0)
+
+
+def read_timing() -> dict:
+    n = len(STAGES)
+    ms = (ctypes.c_double * n)()
+    cnt = (ctypes.c_longlong * n)()
+    units = (ctypes.c_longlong * n)()
+    lib.gsr_timing_read(ms, cnt, units, n)
+    return {s: dict(ms=ms[i], launches=cnt[i], units=units[i],
+                    avg_us=(1000.0 * ms[i] / cnt[i]) if cnt[i] else 0.0) for i, s in enumerate(STAGES)}

@@ -1,0 +1,165 @@
+"""SplaTAM's caller glue around the rasterizer: the unchanged callers of the
+drop-in API, restated so the tracking / mapping iteration can be run and
+benchmarked without SplaTAM's dataset / wandb / cv2 dependencies.
+
+Follows utils/slam_helpers.py (transform_to_frame 252-304, rendervar builders
+124-139 / 234-249, get_depth_and_silhouette 196-213), utils/slam_external.py
+(build_rotation 25-42, calc_ssim 66-97) and scripts/splatam.py get_loss
+(220-353) with the Replica tracking config (configs/replica/splatam.py:59-70).
+Everything here is plain torch on the rasterizer's device; the rasterizer
+itself is splatam_amd.rasterizer (HIP).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+from .scenes import Scene
+
+
+def build_rotation(q):
+    """slam_external.py:25-42 (normalises q first)."""
+    q = q / torch.sqrt((q * q).sum(dim=1, keepdim=True))
+    r, x, y, z = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    R = torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y),
+                     2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x),
+                     2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], dim=1)
+    return R.reshape(-1, 3, 3)
+
+
+def quat_mult(q1, q2):
+    """slam_helpers.py quat_mult (Hamilton product, w first)."""
+    w1, x1, y1, z1 = q1.T
+    w2, x2, y2, z2 = q2.T
+    return torch.stack([w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2,
+                        w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+                        w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2,
+                        w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2]).T
+
+
+def transform_to_frame(params, time_idx, gaussians_grad, camera_grad):
+    """slam_helpers.py:252-304."""
+    rots = params["cam_unnorm_rots"][..., time_idx]
+    trans = params["cam_trans"][..., time_idx]
+    if not camera_grad:
+        rots, trans = rots.detach(), trans.detach()
+    cam_rot = F.normalize(rots)
+    dev = params["means3D"].device
+    rel_w2c = torch.eye(4, device=dev, dtype=torch.float32)
+    rel_w2c[:3, :3] = build_rotation(cam_rot)[0]
+    rel_w2c[:3, 3] = trans[0]
+    pts = params["means3D"] if gaussians_grad else params["means3D"].detach()
+    unnorm = params["unnorm_rotations"] if gaussians_grad else params["unnorm_rotations"].detach()
+    pts4 = torch.cat((pts, torch.ones(pts.shape[0], 1, device=dev)), dim=1)
+    out = {"means3D": (rel_w2c @ pts4.T).T[:, :3]}
+    if params["log_scales"].shape[1] == 1:
+        out["unnorm_rotations"] = unnorm
+    else:
+        out["unnorm_rotations"] = quat_mult(cam_rot, F.normalize(unnorm))
+    return out
+
+
+def _scales(params):
+    ls = params["log_scales"]
+    return torch.exp(torch.tile(ls, (1, 3)) if ls.shape[1] == 1 else ls)
+
+
+def get_depth_and_silhouette(pts_3D, w2c):
+    """slam_helpers.py:196-213: per-Gaussian colours [z, 1, z^2] for the depth/silhouette render."""
+    pts4 = torch.cat((pts_3D, torch.ones_like(pts_3D[:, :1])), dim=-1)
+    z = (w2c @ pts4.transpose(0, 1)).transpose(0, 1)[:, 2:3]
+    return torch.cat([z, torch.ones_like(z), z * z], dim=1)
+
+
+def transformed_params2rendervar(params, tg):
+    """slam_helpers.py:124-139."""
+    return {"means3D": tg["means3D"], "colors_precomp": params["rgb_colors"],
+            "rotations": F.normalize(tg["unnorm_rotations"]), "opacities": torch.sigmoid(params["logit_opacities"]),
+            "scales": _scales(params),
+            "means2D": torch.zeros_like(params["means3D"], requires_grad=True) + 0}
+
+
+def transformed_params2depthplussilhouette(params, w2c, tg):
+    """slam_helpers.py:234-249."""
+    return {"means3D": tg["means3D"], "colors_precomp": get_depth_and_silhouette(tg["means3D"], w2c),
+            "rotations": F.normalize(tg["unnorm_rotations"]), "opacities": torch.sigmoid(params["logit_opacities"]),
+            "scales": _scales(params),
+            "means2D": torch.zeros_like(params["means3D"], requires_grad=True) + 0}
+
+
+def camera_settings(cam, device) -> GaussianRasterizationSettings:
+    """setup_camera (recon_helpers.py:4-27) moved to `device`."""
+    return GaussianRasterizationSettings(
+        image_height=cam.H, image_width=cam.W, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+        bg=torch.zeros(3, dtype=torch.float32, device=device), scale_modifier=1.0,
+        viewmatrix=cam.viewmatrix.to(device), projmatrix=cam.projmatrix.to(device), sh_degree=0,
+        campos=cam.campos.to(device), prefiltered=False)
+
+
+@dataclass
+class TrackingConfig:
+    """configs/replica/splatam.py:59-70 (tracking block)."""
+    use_sil_for_loss: bool = True
+    sil_thres: float = 0.99
+    use_l1: bool = True
+    ignore_outlier_depth_loss: bool = False
+    w_im: float = 0.5
+    w_depth: float = 1.0
+
+
+def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = TrackingConfig()):
+    """scripts/splatam.py:220-353 with tracking=True: two renders (RGB, [z,1,z^2]), masked L1 sums."""
+    tg = transform_to_frame(params, iter_time_idx, gaussians_grad=False, camera_grad=True)
+    rendervar = transformed_params2rendervar(params, tg)
+    depth_sil_rendervar = transformed_params2depthplussilhouette(params, curr_data["w2c"], tg)
+    rendervar["means2D"].retain_grad()
+    im, radius, _ = GaussianRasterizer(raster_settings=curr_data["cam"])(**rendervar)
+    depth_sil, _, _ = GaussianRasterizer(raster_settings=curr_data["cam"])(**depth_sil_rendervar)
+    depth = depth_sil[0, :, :].unsqueeze(0)
+    silhouette = depth_sil[1, :, :]
+    presence_sil_mask = silhouette > cfg.sil_thres
+    depth_sq = depth_sil[2, :, :].unsqueeze(0)
+    uncertainty = (depth_sq - depth ** 2).detach()
+    nan_mask = (~torch.isnan(depth)) & (~torch.isnan(uncertainty))
+    mask = (curr_data["depth"] > 0) & nan_mask
+    if cfg.use_sil_for_loss:
+        mask = mask & presence_sil_mask
+    mask = mask.detach()
+    loss_depth = torch.abs(curr_data["depth"] - depth)[mask].sum()
+    color_mask = torch.tile(mask, (3, 1, 1)).detach()
+    loss_im = torch.abs(curr_data["im"] - im)[color_mask].sum()
+    loss = cfg.w_im * loss_im + cfg.w_depth * loss_depth
+    return loss, radius, rendervar["means2D"]
+
+
+def init_tracking_params(scene: Scene, num_frames: int, device, pose_noise=(0.5, 0.01), seed=0):
+    """SplaTAM parameter dict (scripts/splatam.py:103-172 layout) with iso log_scales [P,1],
+    plus per-frame camera poses perturbed from identity by `pose_noise` = (deg, m)."""
+    g = torch.Generator().manual_seed(seed + 1000)
+    P = scene.P
+    params = {
+        "means3D": scene.means3D.clone(),
+        "rgb_colors": scene.colors.clone(),
+        "unnorm_rotations": scene.rotations.clone(),
+        "logit_opacities": torch.logit(scene.opacities.clamp(1e-6, 1 - 1e-6)),
+        "log_scales": torch.log(scene.scales[:, :1]).clone(),
+    }
+    rots = torch.zeros(1, 4, num_frames)
+    rots[0, 0] = 1.0
+    trans = torch.zeros(1, 3, num_frames)
+    ang = torch.deg2rad(torch.tensor(pose_noise[0]))
+    for t in range(num_frames):
+        axis = torch.randn(3, generator=g)
+        axis = axis / axis.norm()
+        rots[0, 0, t] = torch.cos(ang / 2)
+        rots[0, 1:, t] = axis * torch.sin(ang / 2)
+        d = torch.randn(3, generator=g)
+        trans[0, :, t] = pose_noise[1] * d / d.norm()
+    params["cam_unnorm_rots"] = rots
+    params["cam_trans"] = trans
+    out = {k: v.to(device).float().contiguous() for k, v in params.items()}
+    assert out["means3D"].shape[0] == P
+    return out

@@ -1,0 +1,58 @@
+"""Rasterizer-only microbenchmark (no SplaTAM glue): K x (RGB fwd+bwd, depth/silhouette
+fwd+bwd) on one synthetic config; prints per-stage hipEvent timings as JSON.
+Used for kernel iteration and for rocprofv3 PMC passes."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from splatam_amd import profiling  # noqa: E402
+from splatam_amd.rasterizer import GaussianRasterizer  # noqa: E402
+from splatam_amd.scenes import config_scene  # noqa: E402
+from splatam_amd.slam import camera_settings  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    s = config_scene(a.config)
+    cam = camera_settings(s.cam, dev)
+    m3 = s.means3D.to(dev).requires_grad_(True)
+    sc = s.scales.to(dev)
+    ro = s.rotations.to(dev)
+    op = s.opacities.to(dev)
+    col = s.colors.to(dev)
+    ds = torch.cat([m3.detach()[:, 2:3], torch.ones_like(m3[:, :1]), m3.detach()[:, 2:3] ** 2], 1)
+    g = torch.randn(3, s.cam.H, s.cam.W, device=dev)
+    ras = GaussianRasterizer(cam)
+
+    def it():
+        for c in (col, ds):
+            m2 = torch.zeros_like(m3, requires_grad=True)
+            im, _, _ = ras(means3D=m3, means2D=m2, opacities=op, colors_precomp=c, scales=sc, rotations=ro)
+            im.backward(g)
+
+    for _ in range(a.warmup):
+        it()
+    torch.cuda.synchronize()
+    profiling.enable_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        it()
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    st = profiling.read_timing()
+    print(json.dumps({"frames_per_s": a.iters / t, "ms_per_frame": 1000 * t / a.iters,
+                      "stages_us": {k: round(v["avg_us"], 2) for k, v in st.items()}}))
+
+
+if __name__ == "__main__":
+    main()
