@@ -13,17 +13,19 @@
 //               order (deterministic, bitwise reproducible) and applies the
 //               per-Gaussian chain rule (backward.cu:144-274 cov2D,
 //               412-475 cov3D, 480-530 projection, 20-139 SH).
+#include <cstdlib>
+
 #include "gsr_common.h"
 
 namespace gsr {
 
 constexpr int BWD_BATCH = 128;
-constexpr int BWD_GROUP = 4;
 
+template <int BWD_GROUP, bool PREFETCH>
 __global__ void __launch_bounds__(TILE_PIX)
 render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
-                  const uint32_t* __restrict__ perm, const float4* __restrict__ rec_a,
-                  const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
+                  const uint2* __restrict__ rect, const uint32_t* __restrict__ offsets,
+                  const float4* __restrict__ rec_a, const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
                   const float* __restrict__ final_T, const uint32_t* __restrict__ n_contrib,
                   const float* __restrict__ dL_dpix, float4* __restrict__ inst) {
     __shared__ float4 s_a[BWD_BATCH];
@@ -33,7 +35,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     __shared__ __attribute__((aligned(16))) float s_acc[4 * BWD_BATCH * 9];
     __shared__ uint32_t s_wmax[4];
     __shared__ uint8_t s_mask[BWD_BATCH];
-    __shared__ __attribute__((aligned(16))) uint16_t s_list[4][BWD_BATCH + BWD_GROUP];
+    __shared__ __attribute__((aligned(16))) uint16_t s_list[4][BWD_BATCH + 4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int tile = blockIdx.y * cam.gx + blockIdx.x;
     const int px = blockIdx.x * TILE_X + (tid & (TILE_X - 1));
@@ -59,7 +61,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     const uint32_t bmax = max(max(s_wmax[0], s_wmax[1]), max(s_wmax[2], s_wmax[3]));
     // Instances behind every pixel's last contributor receive zero gradient.
     for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {
-        const uint32_t u = perm[k];
+        const uint32_t gk = point_list[k];
+        const uint32_t u = instance_slot(rect[gk], offsets[gk], blockIdx.x, blockIdx.y);
         inst[3 * u] = make_float4(0.f, 0.f, 0.f, 0.f);
         inst[3 * u + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
         inst[3 * u + 2] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -68,7 +71,9 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     const bool bg_on = cam.bg[0] != 0.f || cam.bg[1] != 0.f || cam.bg[2] != 0.f;  // uniform
     const float pxf = (float)px, pyf = (float)py;
     float T = T_final;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, lc0 = 0.f, lc1 = 0.f, lc2 = 0.f, last_alpha = 0.f;
+    // accum_rec / last_color of backward.cu:997-1001 enter only through their dot
+    // product with dL/dpixel, so the recurrence is carried on those dot products.
+    float acc_dot = 0.f, lc_dot = 0.f, last_alpha = 0.f;
     const int row = lane >> 4;
     // records of the first batch (back to front)
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa;
@@ -76,14 +81,15 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     if (tid < min(BWD_BATCH, (int)bmax)) {
         const uint32_t k = range.x + bmax - 1 - tid;
         const uint32_t gi = point_list[k];
-        pu = perm[k]; pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
+        pu = instance_slot(rect[gi], offsets[gi], blockIdx.x, blockIdx.y);
+        pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
     }
     for (int hi = (int)bmax; hi > 0; hi -= BWD_BATCH) {
         const int cnt = min(BWD_BATCH, hi);
         if (tid < cnt) {
             s_u[tid] = pu;
-            s_a[tid] = pa;
-            s_b[tid] = pb;
+            s_a[tid] = stage_a(pa);
+            s_b[tid] = stage_b(pb);
             s_c[tid] = pc;
             s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
         }
@@ -95,56 +101,58 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             if (tid < min(BWD_BATCH, nhi)) {
                 const uint32_t k = range.x + (uint32_t)(nhi - 1 - tid);
                 const uint32_t gi = point_list[k];
-                pu = perm[k]; pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
+                pu = instance_slot(rect[gi], offsets[gi], blockIdx.x, blockIdx.y);
+                pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
             }
         }
         // entries j with pos = hi-1-j >= wmax lie behind every pixel of this wave
         const int n = build_strip_list(s_mask, cnt, w, hi - (int)wmax, s_list[w]);
-        Group4 nxt;
-        if (n > 0) load_group4(s_list[w], 0, n, s_a, s_b, nxt);
+        GroupN<BWD_GROUP> nxt;
+        if (PREFETCH && n > 0) load_group<BWD_GROUP>(s_list[w], 0, n, s_a, s_b, nxt);
         for (int i = 0; i < n; i += BWD_GROUP) {
-            const Group4 cur = nxt;
-            if (i + BWD_GROUP < n) load_group4(s_list[w], i + BWD_GROUP, n, s_a, s_b, nxt);  // in flight during math
+            GroupN<BWD_GROUP> cur;
+            if (PREFETCH) {
+                cur = nxt;
+                if (i + BWD_GROUP < n) load_group<BWD_GROUP>(s_list[w], i + BWD_GROUP, n, s_a, s_b, nxt);
+            } else {
+                load_group<BWD_GROUP>(s_list[w], i, n, s_a, s_b, cur);
+            }
             int j[BWD_GROUP];
-            float4 a[BWD_GROUP], b[BWD_GROUP];
             bool ok[BWD_GROUP];
-            float dx[BWD_GROUP], dy[BWD_GROUP], G[BWD_GROUP], alpha[BWD_GROUP];
+            float dx[BWD_GROUP], dy[BWD_GROUP], G[BWD_GROUP], araw[BWD_GROUP], alpha[BWD_GROUP];
             bool any = false;
 #pragma unroll
             for (int k = 0; k < BWD_GROUP; k++) {
                 j[k] = cur.j[k];
-                a[k] = cur.a[k];
-                b[k] = cur.b[k];
-                dx[k] = a[k].x - pxf;
-                dy[k] = a[k].y - pyf;
-                const float power = -0.5f * (a[k].z * dx[k] * dx[k] + b[k].x * dy[k] * dy[k]) - a[k].w * dx[k] * dy[k];
-                G[k] = __expf(power);
-                alpha[k] = fminf(0.99f, b[k].y * G[k]);
+                dx[k] = cur.a[k].x - pxf;
+                dy[k] = cur.a[k].y - pyf;
+                const float p2 = eval_p2(cur.a[k], cur.b[k], dx[k], dy[k]);  // log2(e) * power
+                G[k] = __builtin_amdgcn_exp2f(fminf(p2, 0.f));                // finite for every lane
+                araw[k] = cur.b[k].y * G[k];
+                alpha[k] = fminf(0.99f, araw[k]);
                 const uint32_t pos = (uint32_t)(hi - 1 - j[k]);  // position in the tile list
-                ok[k] = cur.valid[k] && pos < last && power <= 0.0f && alpha[k] >= 1.0f / 255.0f;
+                ok[k] = cur.valid[k] && pos < last && p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;
                 any = any || ok[k];
             }
             if (__ballot(any) == 0ull) continue;
             // Per pair: reduce (hx, hy, hx*dx, hx*dy, hy*dy, G*dL/dalpha, dchannel*dL/dpix[3]) with
-            // h = G * dL/dG.  gauss_bwd turns them into the reference's per-pair quantities
-            // (backward.cu:1020-1038): dmean2D = -ddel * (Q [hx, hy]), dconic = -0.5 * (hxx, hxy, hyy);
-            // both are linear in the sums, the conic Q being constant per Gaussian.
+            // h = G * dL/dG = (o * G) * dL/dalpha.  gauss_bwd turns them into the reference's
+            // per-pair quantities (backward.cu:1020-1038): dmean2D = -ddel * (Q [hx, hy]),
+            // dconic = -0.5 * (hxx, hxy, hyy); both are linear in the sums (Q is per Gaussian).
             float v[BWD_GROUP * 9];
 #pragma unroll
             for (int k = 0; k < BWD_GROUP; k++) {
                 const float4 c = s_c[j[k]];
                 const float inv = __builtin_amdgcn_rcpf(1.f - alpha[k]);  // v_rcp_f32 (~1 ulp)
                 const float Tn = T * inv;                                  // T / (1 - alpha), backward.cu:978
-                const float na0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-                const float na1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-                const float na2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-                float dL_dalpha = ((c.x - na0) * dp0 + (c.y - na1) * dp1 + (c.z - na2) * dp2) * Tn;
+                const float cd = c.x * dp0 + c.y * dp1 + c.z * dp2;
+                const float na_dot = last_alpha * lc_dot + (1.f - last_alpha) * acc_dot;
+                float dL_dalpha = (cd - na_dot) * Tn;
                 if (bg_on) dL_dalpha += (-T_final * inv) * bg_dot;
                 const bool o_ = ok[k];
                 dL_dalpha = o_ ? dL_dalpha : 0.f;
-                const float Gz = o_ ? G[k] : 0.f;
                 const float dch = o_ ? alpha[k] * Tn : 0.f;
-                const float h = Gz * (b[k].y * dL_dalpha);
+                const float h = araw[k] * dL_dalpha;
                 const float hx = h * dx[k], hy = h * dy[k];
                 float* vk = v + 9 * k;
                 vk[0] = hx;
@@ -152,23 +160,35 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 vk[2] = hx * dx[k];
                 vk[3] = hx * dy[k];
                 vk[4] = hy * dy[k];
-                vk[5] = Gz * dL_dalpha;
+                vk[5] = G[k] * dL_dalpha;
                 vk[6] = dch * dp0;
                 vk[7] = dch * dp1;
                 vk[8] = dch * dp2;
                 if (o_) {
                     T = Tn;
-                    acc0 = na0; acc1 = na1; acc2 = na2;
-                    lc0 = c.x; lc1 = c.y; lc2 = c.z;
+                    acc_dot = na_dot;
+                    lc_dot = cd;
                     last_alpha = alpha[k];
                 }
             }
-            float r[9];
-            wave_reduce4x9(v, r);
-            if ((lane & 15) == 0 && i + row < n) {
-                float* dst = s_acc + (w * BWD_BATCH + j[row]) * 9;
+            if constexpr (BWD_GROUP == 4) {
+                float r[9];
+                wave_reduce4x9(v, r);
+                if ((lane & 15) == 0 && i + row < n) {
+                    float* dst = s_acc + (w * BWD_BATCH + j[row]) * 9;
 #pragma unroll
-                for (int m = 0; m < 9; m++) dst[m] = r[m];
+                    for (int m = 0; m < 9; m++) dst[m] = r[m];
+                }
+            } else {
+                float r[5];
+                wave_reduce2x9(v, r);
+                const int item = row >> 1, half = row & 1;
+                if ((lane & 15) == 0 && i + item < n) {
+                    float* dst = s_acc + (w * BWD_BATCH + j[item]) * 9 + 4 * half;
+#pragma unroll
+                    for (int m = 0; m < 4; m++) dst[m] = r[m];
+                    if (half == 0) dst[8] = r[4];
+                }
             }
         }
         __syncthreads();
@@ -187,11 +207,19 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     }
 }
 
-hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list,
-                             const uint32_t* perm, GeomPtrs geo, const float* colors, const float* final_T,
-                             const uint32_t* n_contrib, const float* dL_dpix, float4* inst, hipStream_t s) {
-    (void)colors;
-    hipLaunchKernelGGL(render_bwd_kernel, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, perm,
+hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
+                             const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, float4* inst,
+                             hipStream_t s) {
+    // GSR_BWD_VARIANT (tuning only): 1 = 4-entry groups (default), 0 = 4 + prefetch, 2 = 2 + prefetch, 3 = 2
+    static const int variant = [] {
+        const char* e = getenv("GSR_BWD_VARIANT");
+        return e ? atoi(e) : 1;
+    }();
+    auto k = render_bwd_kernel<4, false>;
+    if (variant == 0) k = render_bwd_kernel<4, true>;
+    if (variant == 2) k = render_bwd_kernel<2, true>;
+    if (variant == 3) k = render_bwd_kernel<2, false>;
+    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rect, geo.offsets,
                        geo.rec_a, geo.rec_b, geo.rec_c, final_T, n_contrib, dL_dpix, inst);
     return hipGetLastError();
 }

@@ -7,6 +7,7 @@
 // (the reference's cudaMemcpy at rasterizer_impl.cu:282), done through a
 // pinned per-thread staging word.
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -195,25 +196,35 @@ int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, fl
     float* final_T = (float*)(ib + IL.final_T);
     uint32_t* n_contrib = (uint32_t*)(ib + IL.n_contrib);
     uint2* ranges = (uint2*)(ib + IL.ranges);
+    uint32_t* tile_count = (uint32_t*)(ib + IL.tile_count);
+    const int ntiles = cam.gx * cam.gy;
+    uint32_t* cursor = tile_count + (size_t)ntiles * TILE_CTR_STRIDE;
     hipError_t e;
+    if ((e = hipMemsetAsync(tile_count, 0, 8 * (size_t)ntiles * TILE_CTR_STRIDE, stream)) != hipSuccess)
+        return hip_fail(e, "memset tile counts");
     if (P > 0) {
         if (!radii) return fail(GSR_ERR_INVALID_ARG, "radii output required");
         if ((e = hipMemsetAsync(geo.counters, 0, 16, stream)) != hipSuccess) return hip_fail(e, "memset counters");
         {
             StageTimer t(GSR_STAGE_PREPROCESS, P, stream);
-            if ((e = launch_preprocess(cam, g, geo, radii, GL.nb, stream)) != hipSuccess) return hip_fail(e, "preprocess");
-            if ((e = launch_exclusive_scan(geo.blocksums, (uint32_t)GL.nb, geo.counters, stream)) != hipSuccess)
+            if ((e = launch_preprocess(cam, g, geo, radii, tile_count, GL.nb, stream)) != hipSuccess)
+                return hip_fail(e, "preprocess");
+            if ((e = launch_scan_counts(geo, GL.nb, tile_count, ntiles, ranges, stream)) != hipSuccess)
                 return hip_fail(e, "scan");
         }
         if (!g_pinned.p) {
             if ((e = hipHostMalloc((void**)&g_pinned.p, 16, hipHostMallocDefault)) != hipSuccess)
                 return hip_fail(e, "hipHostMalloc");
         }
-        if ((e = hipMemcpyAsync(g_pinned.p, geo.counters, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+        if ((e = hipMemcpyAsync(g_pinned.p, geo.counters, 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
             return hip_fail(e, "copy num_rendered");
         if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "sync num_rendered");
+    } else {
+        if ((e = hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)ntiles, stream)) != hipSuccess)
+            return hip_fail(e, "memset ranges");
     }
     const uint32_t I = (P > 0) ? g_pinned.p[0] : 0u;
+    const uint32_t longest = (P > 0) ? g_pinned.p[2] : 0u;
     if (P > 0 && g_pinned.p[1] != 0)
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     if (I > 0x7fffffffu) return fail(GSR_ERR_INVALID_ARG, "num_rendered overflows int32");
@@ -226,9 +237,21 @@ int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, fl
     uint32_t* gid = (uint32_t*)(bb + BL.gid);
     uint32_t* point_list = (uint32_t*)(bb + BL.point_list);
     uint32_t* hist = (uint32_t*)(bb + BL.hist);
-    if ((e = hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)cam.gx * cam.gy, stream)) != hipSuccess)
-        return hip_fail(e, "memset ranges");
-    if (I > 0) {
+    static const bool force_radix = getenv("GSR_FORCE_RADIX") && atoi(getenv("GSR_FORCE_RADIX")) != 0;
+    if (I > 0 && longest <= (uint32_t)TILE_SORT_CAP && !force_radix) {
+        // bucket every instance into its tile, then sort each tile in LDS
+        {
+            StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
+            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, cursor, keys[0], GL.nb, stream)) != hipSuccess)
+                return hip_fail(e, "duplicate");
+        }
+        {
+            StageTimer t(GSR_STAGE_SORT, I, stream);
+            if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, stream)) != hipSuccess)
+                return hip_fail(e, "tile sort");
+        }
+    } else if (I > 0) {
+        // fallback for tiles longer than the LDS sort: global stable LSD radix sort of (tile, depth)
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
             if ((e = launch_duplicate(cam, P, geo, keys[0], gid, GL.nb, stream)) != hipSuccess)
@@ -241,9 +264,8 @@ int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, fl
         }
         {
             StageTimer t(GSR_STAGE_RANGES, I, stream);
-            if ((e = launch_ranges(keys[BL.final_buf], vals[BL.final_buf], gid, point_list, ranges, I, stream)) !=
-                hipSuccess)
-                return hip_fail(e, "ranges");
+            if ((e = launch_gather_ids(vals[BL.final_buf], gid, point_list, I, stream)) != hipSuccess)
+                return hip_fail(e, "gather ids");
         }
     }
     {
@@ -287,11 +309,10 @@ int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, c
         inst = (float4*)obtain(alloc, alloc_ctx, GSR_BUF_SCRATCH, sizeof(float4) * INST_REC_F4 * (size_t)num_rendered);
         if (!inst) return fail(GSR_ERR_ALLOC, "allocator returned NULL (backward scratch)");
         const char* bb = (const char*)binning_buffer;
-        const uint32_t* perm = (const uint32_t*)(bb + BL.vals[BL.final_buf]);
         const uint32_t* point_list = (const uint32_t*)(bb + BL.point_list);
         StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream);
-        if ((e = launch_render_bwd(cam, ranges, point_list, perm, geo, nullptr, final_T, n_contrib, dL_dout_color,
-                                   inst, stream)) != hipSuccess)
+        if ((e = launch_render_bwd(cam, ranges, point_list, geo, final_T, n_contrib, dL_dout_color, inst, stream)) !=
+            hipSuccess)
             return hip_fail(e, "render backward");
     }
     GradsOut out{grads->dmeans2D, grads->dcolors, grads->dopacity, grads->dmeans3D,

@@ -23,6 +23,7 @@ constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;
 constexpr int RADIX = 256;
 constexpr int RENDER_BATCH = 256;    // Gaussians staged in LDS per batch
 constexpr int INST_REC_F4 = 3;       // backward per-instance record: 3 x float4 (9 used floats)
+constexpr int TILE_CTR_STRIDE = 64;  // per-tile atomic counters one 256-B line apart (spread over L2 channels)
 
 // ---------------------------------------------------------------- layouts --
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -35,7 +36,7 @@ struct GeomLayout {       // per-Gaussian state ("geomBuffer")
     size_t tiles;         // u32    [P]  tiles touched
     size_t offsets;       // u32    [P]  exclusive instance offset
     size_t blocksums;     // u32    [nb] per-workgroup tile sums -> exclusive scan
-    size_t counters;      // u32    [4]  [0]=num_rendered [1]=prefiltered violation
+    size_t counters;      // u32    [4]  [0]=num_rendered [1]=prefiltered violation [2]=longest tile list
     size_t total;
     int nb;
     static GeomLayout make(int P) {
@@ -58,7 +59,8 @@ struct GeomLayout {       // per-Gaussian state ("geomBuffer")
 struct ImgLayout {        // per-pixel / per-tile state ("imgBuffer")
     size_t final_T;       // f32   [N]
     size_t n_contrib;     // u32   [N]
-    size_t ranges;        // uint2 [tiles]
+    size_t ranges;        // uint2 [tiles]  [start, end) of each tile's sorted list
+    size_t tile_count;    // u32   [2*tiles*TILE_CTR_STRIDE] instance counters, then bucket cursors (one memset)
     size_t total;
     static ImgLayout make(int W, int H) {
         ImgLayout L;
@@ -68,6 +70,7 @@ struct ImgLayout {        // per-pixel / per-tile state ("imgBuffer")
         L.final_T = o; o = align_up(o + 4 * (N ? N : 1), 256);
         L.n_contrib = o; o = align_up(o + 4 * (N ? N : 1), 256);
         L.ranges = o; o = align_up(o + 8 * (T ? T : 1), 256);
+        L.tile_count = o; o = align_up(o + 8 * (size_t)TILE_CTR_STRIDE * (T ? T : 1), 256);
         L.total = o;
         return L;
     }
@@ -79,12 +82,14 @@ inline int higher_msb(uint32_t n) {  // rasterizer_impl.cu:35-50 (bits needed fo
     return b;
 }
 
+constexpr int TILE_SORT_CAP = 4096;  // longest tile list sorted in LDS (32 KiB of u64 keys)
+
 struct BinLayout {        // per-instance state ("binningBuffer")
-    size_t keys[2];       // u64 [I] ping-pong
-    size_t vals[2];       // u32 [I] ping-pong (values = unsorted instance index)
-    size_t gid;           // u32 [I] Gaussian id of each unsorted instance
-    size_t point_list;    // u32 [I] Gaussian ids in (tile, depth) order
-    size_t hist;          // u32 [RADIX * nsb] + [RADIX] digit totals
+    size_t point_list;    // u32 [I] Gaussian ids in (tile, depth, id) order -- always at offset 0
+    size_t keys[2];       // u64 [I] bucketed (depth<<32 | id) keys / radix ping-pong (tile<<32 | depth)
+    size_t vals[2];       // u32 [I] radix ping-pong values (fallback path only)
+    size_t gid;           // u32 [I] Gaussian id of each unsorted instance (fallback path only)
+    size_t hist;          // u32 [RADIX * nsb] + [RADIX] digit totals (fallback path only)
     size_t total;
     int nsb;              // radix-sort workgroups
     int npass;            // 8-bit LSD passes over bits [0, 32 + msb(tiles))
@@ -98,12 +103,12 @@ struct BinLayout {        // per-instance state ("binningBuffer")
         L.final_buf = L.npass & 1;
         L.nsb = (int)((n + SORT_TILE - 1) / SORT_TILE);
         size_t o = 0;
+        L.point_list = o; o = align_up(o + 4 * n, 256);
         L.keys[0] = o; o = align_up(o + 8 * n, 256);
         L.keys[1] = o; o = align_up(o + 8 * n, 256);
         L.vals[0] = o; o = align_up(o + 4 * n, 256);
         L.vals[1] = o; o = align_up(o + 4 * n, 256);
         L.gid = o; o = align_up(o + 4 * n, 256);
-        L.point_list = o; o = align_up(o + 4 * n, 256);
         L.hist = o; o = align_up(o + 4 * ((size_t)RADIX * L.nsb + RADIX), 256);  // + digit totals
         L.total = o;
         return L;
@@ -299,6 +304,19 @@ __device__ __forceinline__ void sh_fwd(int deg, float3 pos, const float* campos,
     }
 }
 
+// LDS staging form of a render record: the conic is prescaled so that
+//   p2 = A' dx^2 + B' dx dy + C' dy^2 = log2(e) * power      (forward.cu:341)
+// feeds v_exp_f32 (exp2) directly.  Forward and backward stage the same values,
+// so both evaluate bit-identical alphas.
+constexpr float kLog2e = 1.4426950408889634f;
+__device__ __forceinline__ float4 stage_a(float4 a) {
+    return make_float4(a.x, a.y, -0.5f * kLog2e * a.z, -kLog2e * a.w);
+}
+__device__ __forceinline__ float4 stage_b(float4 b) { return make_float4(-0.5f * kLog2e * b.x, b.y, b.z, b.w); }
+__device__ __forceinline__ float eval_p2(float4 a, float4 b, float dx, float dy) {
+    return a.z * dx * dx + a.w * dx * dy + b.x * dy * dy;
+}
+
 // 4-bit mask of the 16x4-pixel wave strips of a tile (pixel centres x0..x0+15,
 // rows y0+4w..y0+4w+3) that a Gaussian can contribute to, i.e. where
 // o * exp(-0.5 d^T Q d) >= 1/255 (forward.cu:341-351).  The bound is
@@ -443,6 +461,18 @@ __device__ __forceinline__ void wave_reduce4x9(const float (&v)[36], float (&r)[
     for (int m = 0; m < 9; m++) r[m] = row16_sum(swapsum16(r1[m], r1[m + 9]));
 }
 
+// Same for 2 items x 9 values (v[item*9 + q]).  On return, for row rho:
+//   r[m] (m < 4) holds value q = m + 4*(rho & 1) of item rho >> 1,
+//   r[4] holds value 8 of item rho >> 1 in rows 0 and 2 (rows 1, 3: zero).
+__device__ __forceinline__ void wave_reduce2x9(const float (&v)[18], float (&r)[5]) {
+    float r1[9];
+#pragma unroll
+    for (int q = 0; q < 9; q++) r1[q] = swapsum32(v[q], v[q + 9]);
+#pragma unroll
+    for (int m = 0; m < 4; m++) r[m] = row16_sum(swapsum16(r1[m], r1[m + 4]));
+    r[4] = row16_sum(swapsum16(r1[8], 0.f));
+}
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // Lanes of the wave whose 8-bit digit equals mine (valid lanes only).
@@ -456,22 +486,36 @@ __device__ __forceinline__ uint64_t wave_match8(uint32_t d, bool valid) {
     return m;
 }
 
+// Unsorted instance slot of (Gaussian g, tile tx,ty): duplicateWithKeys order
+// (rasterizer_impl.cu:98-109) = offsets[g] + row-major index inside g's tile rect.
+__device__ __forceinline__ uint32_t instance_slot(uint2 rect, uint32_t off, uint32_t tx, uint32_t ty) {
+    const uint32_t x0 = rect.x & 0xFFFFu, y0 = rect.x >> 16, w = (rect.y & 0xFFFFu) - x0;
+    return off + (ty - y0) * w + (tx - x0);
+}
+
 // ------------------------------------------------------- kernel launchers --
-hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, int nb, hipStream_t s);
+hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* tile_count,
+                             int nb, hipStream_t s);
 hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hipStream_t s);
+hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int ntiles, uint2* ranges,
+                              hipStream_t s);
 hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid, int nb,
+                            hipStream_t s);
+hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
+                                   uint64_t* keys, int nb, hipStream_t s);
+hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint32_t* point_list,
                             hipStream_t s);
 hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t n, int nsb, int npass,
                              hipStream_t s);
-hipError_t launch_ranges(const uint64_t* keys, const uint32_t* vals, const uint32_t* gid, uint32_t* point_list,
-                         uint2* ranges, uint32_t n, hipStream_t s);
+hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t* point_list, uint32_t n,
+                             hipStream_t s);
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* colors, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_depth, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* vis, hipStream_t s);
-hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list,
-                             const uint32_t* perm, GeomPtrs geo, const float* colors, const float* final_T,
-                             const uint32_t* n_contrib, const float* dL_dpix, float4* inst, hipStream_t s);
+hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
+                             const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, float4* inst,
+                             hipStream_t s);
 struct GradsOut {
     float* dmeans2D;
     float* dcolors;

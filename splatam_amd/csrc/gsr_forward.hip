@@ -17,7 +17,8 @@
 namespace gsr {
 
 // ------------------------------------------------------------- preprocess --
-__global__ void __launch_bounds__(PRE_BLOCK) preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii) {
+__global__ void __launch_bounds__(PRE_BLOCK)
+preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __restrict__ tile_count) {
 #pragma clang fp contract(off)
     const int i = blockIdx.x * PRE_BLOCK + threadIdx.x;
     uint32_t tiles = 0;
@@ -69,6 +70,8 @@ __global__ void __launch_bounds__(PRE_BLOCK) preprocess_kernel(Camera cam, Gauss
                 geo.rec_b[i] = make_float4(cc, g.opacities[i], pv.z, 0.f);
                 geo.rec_c[i] = make_float4(rgb[0], rgb[1], rgb[2], __uint_as_float(clamped));
                 geo.rect[i] = make_uint2((uint32_t)x0 | ((uint32_t)y0 << 16), (uint32_t)x1 | ((uint32_t)y1 << 16));
+                for (int ty = y0; ty < y1; ty++)  // per-tile instance counts -> bucket ranges
+                    for (int tx = x0; tx < x1; tx++) atomicAdd(&tile_count[(ty * cam.gx + tx) * TILE_CTR_STRIDE], 1u);
             }
         }
         radii[i] = radius;
@@ -84,9 +87,10 @@ __global__ void __launch_bounds__(PRE_BLOCK) preprocess_kernel(Camera cam, Gauss
     if (threadIdx.x == 0) geo.blocksums[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
-hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, int nb, hipStream_t s) {
+hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* tile_count,
+                             int nb, hipStream_t s) {
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(preprocess_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, g, geo, radii);
+    hipLaunchKernelGGL(preprocess_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, g, geo, radii, tile_count);
     return hipGetLastError();
 }
 
@@ -148,6 +152,70 @@ hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hi
     return hipGetLastError();
 }
 
+// One workgroup: exclusive scan of the per-workgroup tile sums (instance
+// offsets, total = num_rendered) and of the per-tile instance counts, which
+// directly gives every tile's [start, end) in the tile-major sorted list
+// (identifyTileRanges, rasterizer_impl.cu:116-138, without reading keys).
+__global__ void __launch_bounds__(SCAN_THREADS)
+scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t* __restrict__ tile_count,
+                   uint32_t ntiles, uint2* __restrict__ ranges, uint32_t* __restrict__ counters) {
+    __shared__ uint32_t wsums[SCAN_THREADS / 64];
+    __shared__ uint32_t s_carry, s_max;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int pass = 0; pass < 2; pass++) {
+        const uint32_t n = pass == 0 ? nb : ntiles;
+        const uint32_t* src = pass == 0 ? blocksums : tile_count;
+        if (tid == 0) { s_carry = 0; s_max = 0; }
+        __syncthreads();
+        uint32_t vmax = 0;
+        for (uint32_t base = 0; base < n; base += SCAN_THREADS * SCAN_ITEMS) {
+            uint32_t x[SCAN_ITEMS], sum = 0;
+            const uint32_t i0 = base + (uint32_t)tid * SCAN_ITEMS;
+#pragma unroll
+            for (int k = 0; k < SCAN_ITEMS; k++) {
+                x[k] = (i0 + k < n) ? src[(size_t)(i0 + k) * (pass == 0 ? 1 : TILE_CTR_STRIDE)] : 0u;
+                sum += x[k];
+                vmax = max(vmax, x[k]);
+            }
+            uint32_t incl = wave_incl_scan(sum);
+            if (lane == 63) wsums[w] = incl;
+            __syncthreads();
+            if (w == 0) {
+                uint32_t ws = (lane < SCAN_THREADS / 64) ? wsums[lane] : 0u;
+                uint32_t wi = wave_incl_scan(ws);
+                if (lane < SCAN_THREADS / 64) wsums[lane] = wi - ws;
+            }
+            __syncthreads();
+            uint32_t run = s_carry + wsums[w] + incl - sum;
+#pragma unroll
+            for (int k = 0; k < SCAN_ITEMS; k++) {
+                if (i0 + k < n) {
+                    if (pass == 0) blocksums[i0 + k] = run;
+                    else ranges[i0 + k] = make_uint2(run, run + x[k]);
+                }
+                run += x[k];
+            }
+            __syncthreads();
+            if (tid == SCAN_THREADS - 1) s_carry = run;
+            __syncthreads();
+        }
+        atomicMax(&s_max, vmax);
+        __syncthreads();
+        if (tid == 0) {
+            if (pass == 0) counters[0] = s_carry;
+            else counters[2] = s_max;
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int ntiles, uint2* ranges,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, geo.blocksums, (uint32_t)nb, tile_count,
+                       (uint32_t)ntiles, ranges, geo.counters);
+    return hipGetLastError();
+}
+
 // -------------------------------------------------------------- duplicate --
 __global__ void __launch_bounds__(PRE_BLOCK)
 duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, uint32_t* __restrict__ gid) {
@@ -197,6 +265,103 @@ hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* ke
                             hipStream_t s) {
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(duplicate_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, keys, gid);
+    return hipGetLastError();
+}
+
+// Bucketed duplicate: every instance goes straight into its tile's bucket
+// (slot from a per-tile cursor), keyed (depth bits << 32 | Gaussian id).  The
+// order inside a bucket is arbitrary; tile_sort_kernel restores the reference
+// order (depth, then id: cub's stable LSD sort, rasterizer_impl.cu:304-309).
+__global__ void __launch_bounds__(PRE_BLOCK)
+duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict__ ranges,
+                        uint32_t* __restrict__ cursor, uint64_t* __restrict__ keys) {
+    __shared__ uint32_t s_incl[PRE_BLOCK];
+    __shared__ uint32_t s_x0[PRE_BLOCK], s_y0[PRE_BLOCK], s_w[PRE_BLOCK], s_depth[PRE_BLOCK];
+    __shared__ uint32_t wsum[PRE_BLOCK / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int i = blockIdx.x * PRE_BLOCK + tid;
+    uint32_t t = (i < P) ? geo.tiles[i] : 0u;
+    uint32_t incl = wave_incl_scan(t);
+    if (lane == 63) wsum[w] = incl;
+    if (t) {
+        uint2 r = geo.rect[i];
+        s_x0[tid] = r.x & 0xFFFFu;
+        s_y0[tid] = r.x >> 16;
+        s_w[tid] = (r.y & 0xFFFFu) - (r.x & 0xFFFFu);
+        s_depth[tid] = __float_as_uint(geo.rec_b[i].z);
+    }
+    __syncthreads();
+    uint32_t woff = 0;
+    for (int k = 0; k < w; k++) woff += wsum[k];
+    incl += woff;
+    s_incl[tid] = incl;
+    const uint32_t base = geo.blocksums[blockIdx.x];
+    if (i < P) geo.offsets[i] = base + incl - t;
+    __syncthreads();
+    const uint32_t total = s_incl[PRE_BLOCK - 1];
+    for (uint32_t e = tid; e < total; e += PRE_BLOCK) {
+        int lo = 0, hi = PRE_BLOCK - 1;
+        while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (s_incl[mid] > e) hi = mid; else lo = mid + 1;
+        }
+        const uint32_t local = e - ((lo == 0) ? 0u : s_incl[lo - 1]);
+        const uint32_t wdt = s_w[lo];
+        const uint32_t tile = (s_y0[lo] + local / wdt) * (uint32_t)cam.gx + s_x0[lo] + local % wdt;
+        const uint32_t pos = ranges[tile].x + atomicAdd(&cursor[tile * TILE_CTR_STRIDE], 1u);
+        keys[pos] = ((uint64_t)s_depth[lo] << 32) | (uint64_t)(blockIdx.x * PRE_BLOCK + lo);
+    }
+}
+
+hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
+                                   uint64_t* keys, int nb, hipStream_t s) {
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(duplicate_bucket_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, ranges, cursor, keys);
+    return hipGetLastError();
+}
+
+// One workgroup per tile: bitonic sort of the tile's bucket (<= TILE_SORT_CAP
+// u64 keys) in LDS, then the Gaussian ids are written in sorted order.  Keys
+// (depth bits, id) are unique inside a tile, so the order is a total order and
+// equals the reference's stable (tile, depth) radix order.
+constexpr int TILE_SORT_THREADS = 256;
+
+__global__ void __launch_bounds__(TILE_SORT_THREADS)
+tile_sort_kernel(const uint2* __restrict__ ranges, const uint64_t* __restrict__ keys,
+                 uint32_t* __restrict__ point_list) {
+    __shared__ uint64_t sk[TILE_SORT_CAP];
+    const int tid = threadIdx.x;
+    const uint2 range = ranges[blockIdx.x];
+    const uint32_t cnt = range.y - range.x;
+    if (cnt <= 1) {
+        if (cnt == 1 && tid == 0) point_list[range.x] = (uint32_t)keys[range.x];
+        return;
+    }
+    uint32_t n = 2;
+    while (n < cnt) n <<= 1;
+    for (uint32_t i = tid; i < n; i += TILE_SORT_THREADS) sk[i] = i < cnt ? keys[range.x + i] : ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= n; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = tid; i < n / 2; i += TILE_SORT_THREADS) {
+                const uint32_t lo = 2 * i - (i & (j - 1));
+                const uint32_t hi = lo + j;
+                const uint64_t a = sk[lo], b = sk[hi];
+                const bool up = (lo & k) == 0;
+                if ((a > b) == up) {
+                    sk[lo] = b;
+                    sk[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = tid; i < cnt; i += TILE_SORT_THREADS) point_list[range.x + i] = (uint32_t)sk[i];
+}
+
+hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint32_t* point_list,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(tile_sort_kernel, dim3(ntiles), dim3(TILE_SORT_THREADS), 0, s, ranges, keys, point_list);
     return hipGetLastError();
 }
 
@@ -322,30 +487,19 @@ hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* his
     return hipGetLastError();
 }
 
-// ----------------------------------------------------------------- ranges --
-__global__ void ranges_kernel(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-                              const uint32_t* __restrict__ gid, uint32_t* __restrict__ point_list,
-                              uint2* __restrict__ ranges, uint32_t n) {
+// ------------------------------------------------------- gather (fallback) --
+// Fallback path only: Gaussian ids of the radix-sorted instances (values are
+// unsorted instance indices).  Tile ranges already come from scan_counts_kernel.
+__global__ void gather_ids_kernel(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ gid,
+                                  uint32_t* __restrict__ point_list, uint32_t n) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const uint32_t tile = (uint32_t)(keys[k] >> 32);
-    if (k == 0) {
-        ranges[tile].x = 0;
-    } else {
-        const uint32_t prev = (uint32_t)(keys[k - 1] >> 32);
-        if (prev != tile) {
-            ranges[prev].y = k;
-            ranges[tile].x = k;
-        }
-    }
-    if (k == n - 1) ranges[tile].y = n;
-    point_list[k] = gid[vals[k]];
+    if (k < n) point_list[k] = gid[vals[k]];
 }
 
-hipError_t launch_ranges(const uint64_t* keys, const uint32_t* vals, const uint32_t* gid, uint32_t* point_list,
-                         uint2* ranges, uint32_t n, hipStream_t s) {
+hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t* point_list, uint32_t n,
+                             hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(ranges_kernel, dim3((n + 255) / 256), dim3(256), 0, s, keys, vals, gid, point_list, ranges, n);
+    hipLaunchKernelGGL(gather_ids_kernel, dim3((n + 255) / 256), dim3(256), 0, s, vals, gid, point_list, n);
     return hipGetLastError();
 }
 
@@ -387,8 +541,8 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
         const int cnt = (int)min((uint32_t)RENDER_BATCH, range.y - start);
         if (tid < cnt) {
-            s_a[tid] = pa;
-            s_b[tid] = pb;
+            s_a[tid] = stage_a(pa);
+            s_b[tid] = stage_b(pb);
             s_c[tid] = pc;
             s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
         }
@@ -420,8 +574,8 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
 #pragma unroll
             for (int k = 0; k < FWD_GROUP; k++) {
                 const float dx = cur.a[k].x - pxf, dy = cur.a[k].y - pyf;
-                power[k] = -0.5f * (cur.a[k].z * dx * dx + cur.b[k].x * dy * dy) - cur.a[k].w * dx * dy;
-                alpha[k] = fminf(0.99f, cur.b[k].y * __expf(power[k]));
+                power[k] = eval_p2(cur.a[k], cur.b[k], dx, dy);  // log2(e) * power
+                alpha[k] = fminf(0.99f, cur.b[k].y * __builtin_amdgcn_exp2f(fminf(power[k], 0.f)));
             }
 #pragma unroll
             for (int k = 0; k < FWD_GROUP; k++) {
