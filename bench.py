@@ -78,20 +78,17 @@ def main():
     torch.cuda.set_device(dev)
 
     from splatam_amd import profiling
-    from splatam_amd.scenes import CONFIGS, config_scene
+    from splatam_amd.scenes import config_scene
     from splatam_amd.slam import camera_settings, get_loss_tracking, init_tracking_params, transformed_params2rendervar, \
         transformed_params2depthplussilhouette, transform_to_frame
     from splatam_amd.rasterizer import GaussianRasterizer
 
-    cfg = CONFIGS[args.config]
+    from splatam_amd import dist as sd
     scene = config_scene(args.config)
     P, W, H = scene.P, scene.cam.W, scene.cam.H
     params = init_tracking_params(scene, num_frames=max(world, 1), device=dev)
-    map_keys = ("means3D", "rgb_colors", "unnorm_rotations", "logit_opacities", "log_scales")
-    if world > 1:
-        for k in map_keys:
-            dist.broadcast(params[k], src=0)
-    frame = rank  # frame sharding: rank r tracks frame r
+    sd.broadcast_map(params)                    # canonical Gaussian map from rank 0
+    frame = sd.frames_for_rank(world)[0] if world > 1 else 0  # frame sharding: rank r tracks frame r
     cam = camera_settings(scene.cam, dev)
     w2c = torch.eye(4, device=dev)
     # targets: renders at the unperturbed pose (ground truth of the synthetic frame)
@@ -126,9 +123,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         if world > 1 and args.bcast_every > 0 and i % args.bcast_every == 0:
-            with torch.no_grad():
-                for k in map_keys:
-                    dist.broadcast(params[k], src=0)
+            sd.broadcast_map(params)           # map update -> RCCL broadcast over xGMI
         step()
     torch.cuda.synchronize()
     if world > 1:
@@ -136,10 +131,7 @@ def main():
     t1 = time.perf_counter()
     stages = profiling.read_timing()
     profiling.enable_timing(False)
-    elapsed = torch.tensor([t1 - t0], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    elapsed = sd.max_over_ranks(t1 - t0, device=dev)
     frames = args.steps * world
     value = frames / elapsed
 

@@ -30,7 +30,7 @@ def run_oracle(scene, dL_dcolor=None, *, bg=(0.0, 0.0, 0.0), use_sh=False, use_c
                mode=oracle.UPSTREAM, dtype=np.float32, scale_modifier=1.0, backward=True):
     c = scene.cam
     kw = dict(view=c.viewmatrix.numpy(), proj=c.projmatrix.numpy(), campos=c.campos.numpy(), tanfovx=c.tanfovx,
-              tanfovy=c.tanfovy, H=c.H, W=c.W, bg=np.asarray(bg, np.float32), scale_modifier=scale_modifier,
+              tanfovy=c.tanfovy, H=c.H, W=c.W, bg=np.asarray(bg, dtype), scale_modifier=scale_modifier,
               dtype=dtype)
     if use_sh:
         kw.update(shs=scene.shs.numpy(), sh_degree=scene.sh_degree)

@@ -9,6 +9,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -31,13 +33,16 @@ int hip_fail(hipError_t e, const char* where) {
     return fail(GSR_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
 }
 
-struct Pinned {
+struct Pinned {  // per-thread staging of the device counters + the event after the scan
     uint32_t* p = nullptr;
+    hipEvent_t ev = nullptr;
     ~Pinned() {
         if (p) (void)hipHostFree(p);
+        if (ev) (void)hipEventDestroy(ev);
     }
 };
 thread_local Pinned g_pinned;
+std::atomic<double> g_inst_ratio{3.0};  // last num_rendered / P (binning capacity hint)
 
 Camera make_camera(const gsr_settings* s) {
     Camera c;
@@ -150,6 +155,13 @@ struct StageTimer {  // brackets the launches of one stage
     }
 };
 
+// The speculative launches learn their work units only after the host sync.
+void g_timing_units(int stage, long long units) {
+    std::lock_guard<std::mutex> lk(g_timing_mu);
+    for (auto it = g_timing.recs.rbegin(); it != g_timing.recs.rend(); ++it)
+        if (it->stage == stage) { it->units = units; break; }
+}
+
 void timing_drain() {  // caller holds g_timing_mu
     for (auto& r : g_timing.recs) {
         float ms = 0.f;
@@ -216,38 +228,97 @@ int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, fl
             if ((e = hipHostMalloc((void**)&g_pinned.p, 16, hipHostMallocDefault)) != hipSuccess)
                 return hip_fail(e, "hipHostMalloc");
         }
+        if (!g_pinned.ev && (e = hipEventCreateWithFlags(&g_pinned.ev, hipEventDisableTiming)) != hipSuccess)
+            return hip_fail(e, "hipEventCreate");
         if ((e = hipMemcpyAsync(g_pinned.p, geo.counters, 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
             return hip_fail(e, "copy num_rendered");
-        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "sync num_rendered");
+        if ((e = hipEventRecord(g_pinned.ev, stream)) != hipSuccess) return hip_fail(e, "record num_rendered");
     } else {
         if ((e = hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)ntiles, stream)) != hipSuccess)
             return hip_fail(e, "memset ranges");
     }
-    const uint32_t I = (P > 0) ? g_pinned.p[0] : 0u;
-    const uint32_t longest = (P > 0) ? g_pinned.p[2] : 0u;
-    if (P > 0 && g_pinned.p[1] != 0)
+    if (P == 0) {  // rasterize_points.cu:67-81: zero outputs, forward not run
+        void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, BinLayout::make(0, W, H).total);
+        if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
+        if ((e = hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess ||
+            (e = hipMemsetAsync(out_depth, 0, sizeof(float) * (size_t)W * H, stream)) != hipSuccess)
+            return hip_fail(e, "zero outputs");
+        return 0;
+    }
+    // Speculative binning + render: the binning buffer is sized from the last
+    // calls' instances-per-Gaussian ratio, so everything is enqueued before the
+    // host waits on num_rendered (the reference blocks right after the scan,
+    // rasterizer_impl.cu:282, leaving the GPU idle while it launches the rest).
+    static const bool force_radix = getenv("GSR_FORCE_RADIX") && atoi(getenv("GSR_FORCE_RADIX")) != 0;
+    const double ratio = g_inst_ratio.load(std::memory_order_relaxed);
+    const uint32_t cap = (uint32_t)std::min(2.0e9, std::max(1024.0, 1.5 * ratio * P));
+    auto bin_ptrs = [&](void* bin, const BinLayout& BL, uint64_t** keys, uint32_t** vals, uint32_t*& gid,
+                        uint32_t*& point_list, uint32_t*& hist) {
+        char* bb = (char*)bin;
+        keys[0] = (uint64_t*)(bb + BL.keys[0]);
+        keys[1] = (uint64_t*)(bb + BL.keys[1]);
+        vals[0] = (uint32_t*)(bb + BL.vals[0]);
+        vals[1] = (uint32_t*)(bb + BL.vals[1]);
+        gid = (uint32_t*)(bb + BL.gid);
+        point_list = (uint32_t*)(bb + BL.point_list);
+        hist = (uint32_t*)(bb + BL.hist);
+    };
+    uint64_t* keys[2];
+    uint32_t* vals[2];
+    uint32_t *gid, *point_list, *hist;
+    bool speculated = false;
+    if (!force_radix) {
+        const BinLayout SL = BinLayout::make((int)cap, W, H);
+        void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, SL.total);
+        if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
+        bin_ptrs(bin, SL, keys, vals, gid, point_list, hist);
+        const SpecGuard guard{geo.counters, cap, (uint32_t)TILE_SORT_CAP};
+        {
+            StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
+            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, cursor, keys[0], GL.nb, guard, stream)) != hipSuccess)
+                return hip_fail(e, "duplicate");
+        }
+        {
+            StageTimer t(GSR_STAGE_SORT, 0, stream);
+            if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, guard, stream)) != hipSuccess)
+                return hip_fail(e, "tile sort");
+        }
+        {
+            StageTimer t(GSR_STAGE_RENDER_FWD, 0, stream);
+            if ((e = launch_render_fwd(cam, ranges, point_list, geo, nullptr, final_T, n_contrib, out_color,
+                                       out_depth, guard, stream)) != hipSuccess)
+                return hip_fail(e, "render");
+        }
+        speculated = true;
+    }
+    if ((e = hipEventSynchronize(g_pinned.ev)) != hipSuccess) return hip_fail(e, "sync num_rendered");
+    const uint32_t I = g_pinned.p[0];
+    const uint32_t longest = g_pinned.p[2];
+    if (g_pinned.p[1] != 0)
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     if (I > 0x7fffffffu) return fail(GSR_ERR_INVALID_ARG, "num_rendered overflows int32");
+    g_inst_ratio.store(P > 0 ? std::max(0.05, (double)I / P) : 1.0, std::memory_order_relaxed);
+    const bool spec_ok = speculated && I <= cap && longest <= (uint32_t)TILE_SORT_CAP;
+    if (spec_ok) {
+        g_timing_units(GSR_STAGE_SORT, I);
+        g_timing_units(GSR_STAGE_RENDER_FWD, I);
+        return (int)I;
+    }
+    // exact re-launch (capacity overflow, a tile longer than the LDS sort, or forced radix)
     const BinLayout BL = BinLayout::make((int)I, W, H);
     void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, BL.total);
     if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
-    char* bb = (char*)bin;
-    uint64_t* keys[2] = {(uint64_t*)(bb + BL.keys[0]), (uint64_t*)(bb + BL.keys[1])};
-    uint32_t* vals[2] = {(uint32_t*)(bb + BL.vals[0]), (uint32_t*)(bb + BL.vals[1])};
-    uint32_t* gid = (uint32_t*)(bb + BL.gid);
-    uint32_t* point_list = (uint32_t*)(bb + BL.point_list);
-    uint32_t* hist = (uint32_t*)(bb + BL.hist);
-    static const bool force_radix = getenv("GSR_FORCE_RADIX") && atoi(getenv("GSR_FORCE_RADIX")) != 0;
+    bin_ptrs(bin, BL, keys, vals, gid, point_list, hist);
+    const SpecGuard none{geo.counters, 0xffffffffu, 0xffffffffu};
     if (I > 0 && longest <= (uint32_t)TILE_SORT_CAP && !force_radix) {
-        // bucket every instance into its tile, then sort each tile in LDS
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
-            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, cursor, keys[0], GL.nb, stream)) != hipSuccess)
+            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, cursor, keys[0], GL.nb, none, stream)) != hipSuccess)
                 return hip_fail(e, "duplicate");
         }
         {
             StageTimer t(GSR_STAGE_SORT, I, stream);
-            if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, stream)) != hipSuccess)
+            if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, none, stream)) != hipSuccess)
                 return hip_fail(e, "tile sort");
         }
     } else if (I > 0) {
@@ -271,7 +342,7 @@ int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, fl
     {
         StageTimer t(GSR_STAGE_RENDER_FWD, I, stream);
         if ((e = launch_render_fwd(cam, ranges, point_list, geo, nullptr, final_T, n_contrib, out_color, out_depth,
-                                   stream)) != hipSuccess)
+                                   none, stream)) != hipSuccess)
             return hip_fail(e, "render");
     }
     return (int)I;

@@ -473,6 +473,19 @@ __device__ __forceinline__ void wave_reduce2x9(const float (&v)[18], float (&r)[
     r[4] = row16_sum(swapsum16(r1[8], 0.f));
 }
 
+// Transposed reduction of N values (N a multiple of 4) over the 64 lanes.
+// On return row rho (= lane / 16) of r[m] (m < N/4) holds the wave total of
+// v[m + rho * N / 4] in all 16 lanes of the row.
+template <int N>
+__device__ __forceinline__ void wave_reduce_n(const float (&v)[N], float (&r)[N / 4]) {
+    static_assert(N % 4 == 0, "pad to a multiple of 4");
+    float r1[N / 2];
+#pragma unroll
+    for (int n = 0; n < N / 2; n++) r1[n] = swapsum32(v[n], v[n + N / 2]);
+#pragma unroll
+    for (int m = 0; m < N / 4; m++) r[m] = row16_sum(swapsum16(r1[m], r1[m + N / 4]));
+}
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // Lanes of the wave whose 8-bit digit equals mine (valid lanes only).
@@ -501,17 +514,27 @@ hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, 
                               hipStream_t s);
 hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid, int nb,
                             hipStream_t s);
+// Speculative launches: kernels exit early when the device-side counters show
+// num_rendered > cap_inst or a tile list longer than cap_tile (the host then
+// re-launches with an exact buffer).  Pass UINT32_MAX to disable the guard.
+struct SpecGuard {
+    const uint32_t* counters;  // GeomLayout counters: [0] num_rendered, [2] longest tile list
+    uint32_t cap_inst, cap_tile;
+    __device__ __forceinline__ bool overflow() const {
+        return counters[0] > cap_inst || counters[2] > cap_tile;
+    }
+};
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
-                                   uint64_t* keys, int nb, hipStream_t s);
+                                   uint64_t* keys, int nb, SpecGuard guard, hipStream_t s);
 hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint32_t* point_list,
-                            hipStream_t s);
+                            SpecGuard guard, hipStream_t s);
 hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t n, int nsb, int npass,
                              hipStream_t s);
 hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t* point_list, uint32_t n,
                              hipStream_t s);
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* colors, float* final_T, uint32_t* n_contrib, float* out_color,
-                             float* out_depth, hipStream_t s);
+                             float* out_depth, SpecGuard guard, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* vis, hipStream_t s);
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, float4* inst,
@@ -529,5 +552,16 @@ struct GradsOut {
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float4* inst,
                             const GradsOut& out, hipStream_t s);
 hipError_t launch_selftest_reduce9(const float* in, float* out, hipStream_t s);
+// backward_power != 1 (the vendored renderCUDAFused semantics, backward.cu:850-1140)
+constexpr int JAC_FLOATS = 80;  // per-Gaussian linear chain pack, see gsr_backward_power.hip
+int power_record_floats(int nsh);  // values stored per instance record
+hipError_t launch_gauss_jac(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, float* jac,
+                            hipStream_t s);
+hipError_t launch_render_bwd_power(const Camera& cam, const GaussIn& g, const uint2* ranges,
+                                   const uint32_t* point_list, GeomPtrs geo, const float* jac, const float* final_T,
+                                   const uint32_t* n_contrib, const float* dL_dpix, int power, float* rec,
+                                   hipStream_t s);
+hipError_t launch_gauss_bwd_power(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii,
+                                  const float* rec, const GradsOut& out, hipStream_t s);
 
 }  // namespace gsr

@@ -274,7 +274,8 @@ hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* ke
 // order (depth, then id: cub's stable LSD sort, rasterizer_impl.cu:304-309).
 __global__ void __launch_bounds__(PRE_BLOCK)
 duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict__ ranges,
-                        uint32_t* __restrict__ cursor, uint64_t* __restrict__ keys) {
+                        uint32_t* __restrict__ cursor, uint64_t* __restrict__ keys, SpecGuard guard) {
+    if (guard.overflow()) return;
     __shared__ uint32_t s_incl[PRE_BLOCK];
     __shared__ uint32_t s_x0[PRE_BLOCK], s_y0[PRE_BLOCK], s_w[PRE_BLOCK], s_depth[PRE_BLOCK];
     __shared__ uint32_t wsum[PRE_BLOCK / 64];
@@ -314,9 +315,10 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict
 }
 
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
-                                   uint64_t* keys, int nb, hipStream_t s) {
+                                   uint64_t* keys, int nb, SpecGuard guard, hipStream_t s) {
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(duplicate_bucket_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, ranges, cursor, keys);
+    hipLaunchKernelGGL(duplicate_bucket_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, ranges, cursor, keys,
+                       guard);
     return hipGetLastError();
 }
 
@@ -328,8 +330,9 @@ constexpr int TILE_SORT_THREADS = 256;
 
 __global__ void __launch_bounds__(TILE_SORT_THREADS)
 tile_sort_kernel(const uint2* __restrict__ ranges, const uint64_t* __restrict__ keys,
-                 uint32_t* __restrict__ point_list) {
+                 uint32_t* __restrict__ point_list, SpecGuard guard) {
     __shared__ uint64_t sk[TILE_SORT_CAP];
+    if (guard.overflow()) return;
     const int tid = threadIdx.x;
     const uint2 range = ranges[blockIdx.x];
     const uint32_t cnt = range.y - range.x;
@@ -360,8 +363,9 @@ tile_sort_kernel(const uint2* __restrict__ ranges, const uint64_t* __restrict__ 
 }
 
 hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint32_t* point_list,
-                            hipStream_t s) {
-    hipLaunchKernelGGL(tile_sort_kernel, dim3(ntiles), dim3(TILE_SORT_THREADS), 0, s, ranges, keys, point_list);
+                            SpecGuard guard, hipStream_t s) {
+    hipLaunchKernelGGL(tile_sort_kernel, dim3(ntiles), dim3(TILE_SORT_THREADS), 0, s, ranges, keys, point_list,
+                       guard);
     return hipGetLastError();
 }
 
@@ -515,7 +519,8 @@ __global__ void __launch_bounds__(TILE_PIX)
 render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                   const float4* __restrict__ rec_a, const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
                   const float* __restrict__ colors, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
-                  float* __restrict__ out_color, float* __restrict__ out_depth) {
+                  float* __restrict__ out_color, float* __restrict__ out_depth, SpecGuard guard) {
+    if (guard.overflow()) return;
     __shared__ float4 s_a[RENDER_BATCH];
     __shared__ float4 s_b[RENDER_BATCH];
     __shared__ float4 s_c[RENDER_BATCH];
@@ -610,7 +615,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
 
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* colors, float* final_T, uint32_t* n_contrib, float* out_color,
-                             float* out_depth, hipStream_t s) {
+                             float* out_depth, SpecGuard guard, hipStream_t s) {
     // GSR_FWD_VARIANT (tuning only): 0 = 4-entry groups, 1 = 4 + prefetch, 2 = 2-entry groups + prefetch
     static const int variant = [] {
         const char* e = getenv("GSR_FWD_VARIANT");
@@ -620,7 +625,7 @@ hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint3
     if (variant == 1) k = render_fwd_kernel<4, true>;
     if (variant == 2) k = render_fwd_kernel<2, true>;
     hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rec_a, geo.rec_b,
-                       geo.rec_c, colors, final_T, n_contrib, out_color, out_depth);
+                       geo.rec_c, colors, final_T, n_contrib, out_color, out_depth, guard);
     return hipGetLastError();
 }
 

@@ -40,8 +40,15 @@ def quat_mult(q1, q2):
                         w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2]).T
 
 
-def transform_to_frame(params, time_idx, gaussians_grad, camera_grad):
-    """slam_helpers.py:252-304."""
+def _affine(pts, R, t):
+    """pts @ R^T + t written elementwise: mathematically the reference's
+    (rel_w2c @ pts4.T).T[:, :3], but its backward w.r.t. (R, t) is a plain
+    reduction over the P points instead of a K=P GEMM (250 us on hipBLASLt)."""
+    return (pts.unsqueeze(1) * R.unsqueeze(0)).sum(-1) + t
+
+
+def transform_to_frame(params, time_idx, gaussians_grad, camera_grad, fast=True):
+    """slam_helpers.py:252-304 (fast=False: the literal matmul formulation)."""
     rots = params["cam_unnorm_rots"][..., time_idx]
     trans = params["cam_trans"][..., time_idx]
     if not camera_grad:
@@ -53,8 +60,11 @@ def transform_to_frame(params, time_idx, gaussians_grad, camera_grad):
     rel_w2c[:3, 3] = trans[0]
     pts = params["means3D"] if gaussians_grad else params["means3D"].detach()
     unnorm = params["unnorm_rotations"] if gaussians_grad else params["unnorm_rotations"].detach()
-    pts4 = torch.cat((pts, torch.ones(pts.shape[0], 1, device=dev)), dim=1)
-    out = {"means3D": (rel_w2c @ pts4.T).T[:, :3]}
+    if fast:
+        out = {"means3D": _affine(pts, rel_w2c[:3, :3], rel_w2c[:3, 3])}
+    else:
+        pts4 = torch.cat((pts, torch.ones(pts.shape[0], 1, device=dev)), dim=1)
+        out = {"means3D": (rel_w2c @ pts4.T).T[:, :3]}
     if params["log_scales"].shape[1] == 1:
         out["unnorm_rotations"] = unnorm
     else:
@@ -67,10 +77,13 @@ def _scales(params):
     return torch.exp(torch.tile(ls, (1, 3)) if ls.shape[1] == 1 else ls)
 
 
-def get_depth_and_silhouette(pts_3D, w2c):
+def get_depth_and_silhouette(pts_3D, w2c, fast=True):
     """slam_helpers.py:196-213: per-Gaussian colours [z, 1, z^2] for the depth/silhouette render."""
-    pts4 = torch.cat((pts_3D, torch.ones_like(pts_3D[:, :1])), dim=-1)
-    z = (w2c @ pts4.transpose(0, 1)).transpose(0, 1)[:, 2:3]
+    if fast:
+        z = (pts_3D * w2c[2, :3]).sum(-1, keepdim=True) + w2c[2, 3]
+    else:
+        pts4 = torch.cat((pts_3D, torch.ones_like(pts_3D[:, :1])), dim=-1)
+        z = (w2c @ pts4.transpose(0, 1)).transpose(0, 1)[:, 2:3]
     return torch.cat([z, torch.ones_like(z), z * z], dim=1)
 
 
@@ -82,9 +95,9 @@ def transformed_params2rendervar(params, tg):
             "means2D": torch.zeros_like(params["means3D"], requires_grad=True) + 0}
 
 
-def transformed_params2depthplussilhouette(params, w2c, tg):
+def transformed_params2depthplussilhouette(params, w2c, tg, fast=True):
     """slam_helpers.py:234-249."""
-    return {"means3D": tg["means3D"], "colors_precomp": get_depth_and_silhouette(tg["means3D"], w2c),
+    return {"means3D": tg["means3D"], "colors_precomp": get_depth_and_silhouette(tg["means3D"], w2c, fast),
             "rotations": F.normalize(tg["unnorm_rotations"]), "opacities": torch.sigmoid(params["logit_opacities"]),
             "scales": _scales(params),
             "means2D": torch.zeros_like(params["means3D"], requires_grad=True) + 0}
@@ -110,11 +123,17 @@ class TrackingConfig:
     w_depth: float = 1.0
 
 
-def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = TrackingConfig()):
-    """scripts/splatam.py:220-353 with tracking=True: two renders (RGB, [z,1,z^2]), masked L1 sums."""
-    tg = transform_to_frame(params, iter_time_idx, gaussians_grad=False, camera_grad=True)
+def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = TrackingConfig(), fast=True):
+    """scripts/splatam.py:220-353 with tracking=True: two renders (RGB, [z,1,z^2]), masked L1 sums.
+
+    fast=True evaluates the same loss without host synchronisation: boolean-mask
+    indexing `x[mask].sum()` becomes `where(mask, x, 0).sum()` (same value and
+    gradient, NaNs outside the mask excluded exactly as indexing excludes them),
+    and the pose transform avoids the K=P GEMM (see _affine).  fast=False is the
+    literal statement of the reference code."""
+    tg = transform_to_frame(params, iter_time_idx, gaussians_grad=False, camera_grad=True, fast=fast)
     rendervar = transformed_params2rendervar(params, tg)
-    depth_sil_rendervar = transformed_params2depthplussilhouette(params, curr_data["w2c"], tg)
+    depth_sil_rendervar = transformed_params2depthplussilhouette(params, curr_data["w2c"], tg, fast=fast)
     rendervar["means2D"].retain_grad()
     im, radius, _ = GaussianRasterizer(raster_settings=curr_data["cam"])(**rendervar)
     depth_sil, _, _ = GaussianRasterizer(raster_settings=curr_data["cam"])(**depth_sil_rendervar)
@@ -128,9 +147,14 @@ def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = Tr
     if cfg.use_sil_for_loss:
         mask = mask & presence_sil_mask
     mask = mask.detach()
-    loss_depth = torch.abs(curr_data["depth"] - depth)[mask].sum()
     color_mask = torch.tile(mask, (3, 1, 1)).detach()
-    loss_im = torch.abs(curr_data["im"] - im)[color_mask].sum()
+    if fast:
+        zero = torch.zeros((), device=depth.device, dtype=depth.dtype)
+        loss_depth = torch.where(mask, torch.abs(curr_data["depth"] - depth), zero).sum()
+        loss_im = torch.where(color_mask, torch.abs(curr_data["im"] - im), zero).sum()
+    else:
+        loss_depth = torch.abs(curr_data["depth"] - depth)[mask].sum()
+        loss_im = torch.abs(curr_data["im"] - im)[color_mask].sum()
     loss = cfg.w_im * loss_im + cfg.w_depth * loss_depth
     return loss, radius, rendervar["means2D"]
 

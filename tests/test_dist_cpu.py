@@ -1,0 +1,53 @@
+"""Frame-sharding orchestration (splatam_amd.dist) with world_size 2 on gloo (CPU)."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from splatam_amd import dist as sd
+    from splatam_amd.scenes import make_scene
+    from splatam_amd.slam import init_tracking_params
+    scene = make_scene(100, 32, 32, seed=rank)          # ranks start from different maps
+    params = init_tracking_params(scene, num_frames=4, device="cpu")
+    sent = sd.broadcast_map(params)
+    ref = init_tracking_params(make_scene(100, 32, 32, seed=0), num_frames=4, device="cpu")
+    same = all(torch.equal(params[k], ref[k]) for k in sd.MAP_KEYS)
+    frames = sd.frames_for_rank(5)
+    h = torch.full((100, 4), float(rank + 1))
+    sd.all_reduce_sum_(h)
+    t = sd.max_over_ranks(0.5 + rank)
+    q.put((rank, same, frames, float(h[0, 0]), t, sent))
+    dist.destroy_process_group()
+
+
+def test_frame_sharding_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, same0, f0, h0, t0, sent0), (r1, same1, f1, h1, t1, sent1) = res
+    assert same0 and same1                       # rank 1 received rank 0's map
+    assert f0 == [0, 2, 4] and f1 == [1, 3]      # disjoint, covering frames
+    assert h0 == h1 == 3.0                       # Fisher / Hessian merge
+    assert t0 == t1 == 1.5                       # max-over-ranks timing
+    assert sent0 == 100 * (3 + 3 + 4 + 1 + 1) * 4

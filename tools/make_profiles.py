@@ -1,0 +1,47 @@
+"""Turns a tools/profile_round.sh output directory into the committed
+profiles/ summaries: kernel stats CSV, per-kernel PMC traffic JSON and the bench line."""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def main(src, tag):
+    dst = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
+    os.makedirs(dst, exist_ok=True)
+    stats = glob.glob(f"{src}/trace/**/run_kernel_stats.csv", recursive=True)[0]
+    shutil.copy(stats, f"{dst}/{tag}_kernel_stats.csv")
+    rows = {r["Name"]: r for r in csv.DictReader(open(stats))}
+    pmc = defaultdict(lambda: defaultdict(list))
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        for f in glob.glob(f"{src}/pmc_{c}/**/run_counter_collection.csv", recursive=True):
+            for r in csv.DictReader(open(f)):
+                pmc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    summary = {}
+    for k, d in pmc.items():
+        fetch = sum(d["FETCH_SIZE"]) / max(len(d["FETCH_SIZE"]), 1)
+        write = sum(d["WRITE_SIZE"]) / max(len(d["WRITE_SIZE"]), 1)
+        summary[k] = {"FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write,
+                      "hbm_bytes_per_launch": int((fetch + write) * 1024),
+                      "avg_duration_ns_trace": float(rows[k]["AverageNs"]) if k in rows else None}
+    bench = None
+    for line in open(f"{src}/bench.log"):
+        if line.startswith("{"):
+            bench = json.loads(line)
+    out = {"tag": tag, "kernels": summary, "bench": bench,
+           "note": "FETCH_SIZE/WRITE_SIZE in KB per dispatch from separate rocprofv3 --pmc passes of "
+                   "bench.py; FETCH_SIZE is uncalibrated for gather patterns on gfx950 (MI355X_MICROARCH.md HBM)."}
+    json.dump(out, open(f"{dst}/{tag}_summary.json", "w"), indent=1)
+    rb = summary.get("render_bwd_kernel")
+    if rb:
+        json.dump({"kernel": "render_bwd_kernel", "hbm_bytes_per_launch": rb["hbm_bytes_per_launch"],
+                   "source": f"profiles/{tag}_summary.json"}, open(f"{dst}/render_bwd_pmc.json", "w"), indent=1)
+    shutil.copy(f"{src}/bench.log", f"{dst}/{tag}_bench.log")
+    print(json.dumps(out["kernels"], indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
