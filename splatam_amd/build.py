@@ -17,7 +17,7 @@ CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 OBJDIR = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libgsr.so")
-SOURCES = ["gsr_forward.hip", "gsr_backward.hip", "gsr_capi.hip"]
+SOURCES = ["gsr_forward.hip", "gsr_backward.hip", "gsr_backward_power.hip", "gsr_capi.hip"]
 ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
 
 
@@ -39,7 +39,7 @@ def flags():
 def _compile(src: str) -> str:
     obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
     srcp = os.path.join(CSRC, src)
-    deps = [srcp, os.path.join(CSRC, "gsr_common.h"), os.path.join(ROOT, "include", "gsr.h")]
+    deps = [srcp, os.path.join(ROOT, "include", "gsr.h")] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
     cmd = [hipcc(), *flags(), "-c", srcp, "-o", obj]

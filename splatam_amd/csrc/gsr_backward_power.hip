@@ -1,0 +1,357 @@
+// gsr_backward_power.hip -- backward with backward_power != 1 (SplaTAM's Fisher /
+// Hessian-diagonal scoring through the vendored fused kernel).
+//
+// Semantics (renderCUDAFused, backward.cu:850-1140; oracle/gsr_oracle.c mode
+// GSR_ORACLE_FUSED): every contributing (pixel, Gaussian) pair is pushed through
+// the whole per-Gaussian chain, each output component is raised to `power`
+// PER PAIR, and only then summed.  The power-1 pipeline may sum first and chain
+// once per Gaussian; here the nonlinearity forbids that, so:
+//
+//   gauss_jac         one lane per Gaussian: the chain is linear in the 9 per-pair
+//                     2D gradients (fixed clamp bits), so it is tabulated once per
+//                     Gaussian as an 80-float Jacobian pack (JAC_FLOATS):
+//                       [ 0..23] dmean3D  <- (dmean2D.xy, dconic.ABC, dRGB.rgb)  3x8
+//                       [24..41] dcov3D   <- dconic                            6x3
+//                       [42..50] dscale   <- dconic                            3x3
+//                       [51..62] drot     <- dconic                            4x3
+//                       [63..78] SH basis Y_k(dir) (dsh[k][c] = Y_k * dRGB_c)   16
+//   render_bwd_power  per tile, back to front (same recurrence and strip culling
+//                     as render_bwd_kernel); per pair it forms the NV = 22 + 3*nsh
+//                     output components from the staged pack (LDS broadcast
+//                     reads), applies powf per lane, reduces them across the wave
+//                     with the transposed permlane/DPP reduction and stores one
+//                     NV-float record per (tile, Gaussian) instance at its
+//                     unsorted slot;
+//   gauss_bwd_power   one lane per Gaussian: fixed-order sum of its records
+//                     straight into the output tensors (deterministic).
+//
+// Deliberate difference from the vendored kernel (documented in DESIGN.md):
+// SH gradients follow upstream (every coefficient, DC included, no pointer
+// offset), as in the power-1 path.
+#include <cstdlib>
+
+#include "gsr_chain.h"
+
+namespace gsr {
+
+template <int NSH>
+struct PowerShape {
+    static constexpr int NV = 22 + 3 * NSH;          // values per pair / record
+    static constexpr int NVP = (NV + 3) & ~3;        // padded to the reduction's multiple of 4
+    static constexpr int BATCH = NSH >= 9 ? 32 : 64;  // LDS: acc 4*BATCH*NVP floats
+};
+
+int power_record_floats(int nsh) {
+    switch (nsh) {
+        case 0: return PowerShape<0>::NVP;
+        case 1: return PowerShape<1>::NVP;
+        case 4: return PowerShape<4>::NVP;
+        case 9: return PowerShape<9>::NVP;
+        case 16: return PowerShape<16>::NVP;
+        default: return -1;
+    }
+}
+
+// --------------------------------------------------------- Jacobian pack --
+__global__ void __launch_bounds__(256)
+gauss_jac_kernel(Camera cam, GaussIn g, const int* __restrict__ radii, float* __restrict__ jac) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.P || radii[i] <= 0) return;
+    const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
+    float* J = jac + (size_t)JAC_FLOATS * i;
+    // column kk <- unit input g2[kin[kk]] (opacity, input 5, reaches no chained output)
+    for (int kk = 0; kk < 8; kk++) {
+        const int in = kk < 5 ? kk : kk + 1;
+        float g2[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        g2[in] = 1.f;
+        float dmean[3], dcov[6], dscale[3], drot[4], dsh[48];
+        gauss_chain(cam, g, i, g2, 0u, dmean, dcov, dscale, drot, dsh, nsh);
+        for (int r = 0; r < 3; r++) J[r * 8 + kk] = dmean[r];
+        if (in >= 2 && in <= 4) {
+            const int c = in - 2;
+            for (int r = 0; r < 6; r++) J[24 + 3 * r + c] = dcov[r];
+            for (int r = 0; r < 3; r++) J[42 + 3 * r + c] = dscale[r];
+            for (int r = 0; r < 4; r++) J[51 + 3 * r + c] = drot[r];
+        }
+        if (in == 6)
+            for (int k = 0; k < 16; k++) J[63 + k] = k < nsh ? dsh[3 * k] : 0.f;
+    }
+    J[79] = 0.f;
+}
+
+hipError_t launch_gauss_jac(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, float* jac,
+                            hipStream_t s) {
+    (void)geo;
+    if (g.P == 0) return hipSuccess;
+    hipLaunchKernelGGL(gauss_jac_kernel, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, radii, jac);
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------- render backward --
+__device__ __forceinline__ float pow_pair(float x, int p) { return p == 2 ? x * x : powf(x, (float)p); }
+
+template <int NSH>
+__global__ void __launch_bounds__(TILE_PIX)
+render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __restrict__ ranges,
+                        const uint32_t* __restrict__ point_list, const uint2* __restrict__ rect,
+                        const uint32_t* __restrict__ offsets, const float4* __restrict__ rec_a,
+                        const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
+                        const float4* __restrict__ jac, const float* __restrict__ final_T,
+                        const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
+                        float4* __restrict__ rec) {
+    constexpr int NV = PowerShape<NSH>::NV, NVP = PowerShape<NSH>::NVP, B = PowerShape<NSH>::BATCH;
+    constexpr int JF4 = JAC_FLOATS / 4;
+    __shared__ float4 s_a[B];
+    __shared__ float4 s_b[B];
+    __shared__ float4 s_c[B];
+    __shared__ float4 s_q[B];  // raw conic (A, B, C)
+    __shared__ uint32_t s_u[B];
+    __shared__ uint32_t s_g[B];
+    __shared__ float4 s_j[B * JF4];
+    __shared__ __attribute__((aligned(16))) float s_acc[4 * B * NVP];
+    __shared__ uint32_t s_wmax[4];
+    __shared__ uint8_t s_mask[B];
+    __shared__ __attribute__((aligned(16))) uint16_t s_list[4][B + 4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tile = blockIdx.y * cam.gx + blockIdx.x;
+    const int px = blockIdx.x * TILE_X + (tid & (TILE_X - 1));
+    const int py = blockIdx.y * TILE_Y + (tid >> 4);
+    const bool inside = px < cam.W && py < cam.H;
+    const int pid = py * cam.W + px;
+    const float x0 = (float)(blockIdx.x * TILE_X), y0 = (float)(blockIdx.y * TILE_Y);
+    const int HW = cam.W * cam.H;
+    const uint2 range = ranges[tile];
+    const float T_final = inside ? final_T[pid] : 0.f;
+    const uint32_t last = inside ? n_contrib[pid] : 0u;
+    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
+    if (inside) {
+        dp0 = dL_dpix[pid];
+        dp1 = dL_dpix[HW + pid];
+        dp2 = dL_dpix[2 * HW + pid];
+    }
+    uint32_t wmax = last;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o));
+    if (lane == 0) s_wmax[w] = wmax;
+    __syncthreads();
+    const uint32_t bmax = max(max(s_wmax[0], s_wmax[1]), max(s_wmax[2], s_wmax[3]));
+    for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {
+        const uint32_t gk = point_list[k];
+        const uint32_t u = instance_slot(rect[gk], offsets[gk], blockIdx.x, blockIdx.y);
+#pragma unroll
+        for (int m = 0; m < NVP / 4; m++) rec[(size_t)u * (NVP / 4) + m] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float bg_dot = cam.bg[0] * dp0 + cam.bg[1] * dp1 + cam.bg[2] * dp2;
+    const bool bg_on = cam.bg[0] != 0.f || cam.bg[1] != 0.f || cam.bg[2] != 0.f;
+    const float ddelx = (float)(0.5 * cam.W), ddely = (float)(0.5 * cam.H);  // backward.cu:935-936
+    const float pxf = (float)px, pyf = (float)py;
+    float T = T_final;
+    float acc_dot = 0.f, lc_dot = 0.f, last_alpha = 0.f;
+    const int row = lane >> 4;
+    for (int hi = (int)bmax; hi > 0; hi -= B) {
+        const int cnt = min(B, hi);
+        if (tid < cnt) {
+            const uint32_t gi = point_list[range.x + (uint32_t)(hi - 1 - tid)];
+            const float4 pa = rec_a[gi], pb = rec_b[gi];
+            s_g[tid] = gi;
+            s_u[tid] = instance_slot(rect[gi], offsets[gi], blockIdx.x, blockIdx.y);
+            s_a[tid] = stage_a(pa);
+            s_b[tid] = stage_b(pb);
+            s_c[tid] = rec_c[gi];
+            s_q[tid] = make_float4(pa.z, pa.w, pb.x, 0.f);
+            s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
+        }
+        for (int q = tid; q < 4 * B * NVP / 4; q += TILE_PIX)
+            reinterpret_cast<float4*>(s_acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        __syncthreads();
+        for (int q = tid; q < cnt * JF4; q += TILE_PIX) {
+            const int item = q / JF4, part = q - item * JF4;
+            s_j[q] = jac[(size_t)s_g[item] * JF4 + part];
+        }
+        __syncthreads();
+        const int n = build_strip_list(s_mask, cnt, w, hi - (int)wmax, s_list[w]);
+        for (int i = 0; i < n; i++) {
+            const int j = s_list[w][i];  // wave-uniform
+            const float4 a = s_a[j], b = s_b[j];
+            const float dx = a.x - pxf, dy = a.y - pyf;
+            const float p2 = eval_p2(a, b, dx, dy);
+            const float G = __builtin_amdgcn_exp2f(fminf(p2, 0.f));
+            const float araw = b.y * G;
+            const float alpha = fminf(0.99f, araw);
+            const uint32_t pos = (uint32_t)(hi - 1 - j);
+            const bool ok = pos < last && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+            if (__ballot(ok) == 0ull) continue;
+            const float4 c = s_c[j];
+            const float inv = __builtin_amdgcn_rcpf(1.f - alpha);
+            const float Tn = T * inv;
+            const float cd = c.x * dp0 + c.y * dp1 + c.z * dp2;
+            const float na_dot = last_alpha * lc_dot + (1.f - last_alpha) * acc_dot;
+            float dL_dalpha = (cd - na_dot) * Tn;
+            if (bg_on) dL_dalpha += (-T_final * inv) * bg_dot;
+            const float dch = alpha * Tn;
+            const float h = araw * dL_dalpha;  // G * dL/dG
+            const float hx = h * dx, hy = h * dy;
+            const float4 qc = s_q[j];
+            // per-pair quantities of backward.cu:1020-1038
+            float in8[8];
+            in8[0] = -(qc.x * hx + qc.y * hy) * ddelx;
+            in8[1] = -(qc.z * hy + qc.y * hx) * ddely;
+            in8[2] = -0.5f * hx * dx;
+            in8[3] = -0.5f * hx * dy;
+            in8[4] = -0.5f * hy * dy;
+            const float col0 = dch * dp0, col1 = dch * dp1, col2 = dch * dp2;
+            const unsigned clamped = __float_as_uint(c.w);
+            in8[5] = (clamped & 1u) ? 0.f : col0;
+            in8[6] = (clamped & 2u) ? 0.f : col1;
+            in8[7] = (clamped & 4u) ? 0.f : col2;
+            const float4* Jq = s_j + j * JF4;
+            float Jv[JAC_FLOATS];
+#pragma unroll
+            for (int m = 0; m < JF4; m++) {
+                const float4 t = Jq[m];
+                Jv[4 * m] = t.x; Jv[4 * m + 1] = t.y; Jv[4 * m + 2] = t.z; Jv[4 * m + 3] = t.w;
+            }
+            float v[NVP];
+            v[0] = in8[0];
+            v[1] = in8[1];
+            v[2] = col0;
+            v[3] = col1;
+            v[4] = col2;
+            v[5] = G * dL_dalpha;
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                float s = 0.f;
+#pragma unroll
+                for (int kk = 0; kk < 8; kk++) s += Jv[r * 8 + kk] * in8[kk];
+                v[6 + r] = s;
+            }
+#pragma unroll
+            for (int r = 0; r < 6; r++) v[9 + r] = Jv[24 + 3 * r] * in8[2] + Jv[25 + 3 * r] * in8[3] + Jv[26 + 3 * r] * in8[4];
+#pragma unroll
+            for (int r = 0; r < 3; r++) v[15 + r] = Jv[42 + 3 * r] * in8[2] + Jv[43 + 3 * r] * in8[3] + Jv[44 + 3 * r] * in8[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) v[18 + r] = Jv[51 + 3 * r] * in8[2] + Jv[52 + 3 * r] * in8[3] + Jv[53 + 3 * r] * in8[4];
+#pragma unroll
+            for (int k = 0; k < NSH; k++)
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) v[22 + 3 * k + ch] = Jv[63 + k] * in8[5 + ch];
+#pragma unroll
+            for (int m = 0; m < NVP; m++) {
+                float x = m < NV ? pow_pair(v[m], power) : 0.f;
+                if (!has_scales && m >= 15 && m < 22) x = 0.f;  // the reference skips scale/rot grads
+                v[m] = ok ? x : 0.f;
+            }
+            if (ok) {
+                T = Tn;
+                acc_dot = na_dot;
+                lc_dot = cd;
+                last_alpha = alpha;
+            }
+            float r[NVP / 4];
+            wave_reduce_n<NVP>(v, r);
+            if ((lane & 15) == 0) {
+                float* dst = s_acc + (w * B + j) * NVP + row * (NVP / 4);
+#pragma unroll
+                for (int m = 0; m < NVP / 4; m++) dst[m] = r[m];
+            }
+        }
+        __syncthreads();
+        for (int q = tid; q < cnt * (NVP / 4); q += TILE_PIX) {
+            const int item = q / (NVP / 4), m = q - item * (NVP / 4);
+            const float4* acc = reinterpret_cast<const float4*>(s_acc);
+            const float4 s0 = acc[(0 * B + item) * (NVP / 4) + m], s1 = acc[(1 * B + item) * (NVP / 4) + m];
+            const float4 s2 = acc[(2 * B + item) * (NVP / 4) + m], s3 = acc[(3 * B + item) * (NVP / 4) + m];
+            rec[(size_t)s_u[item] * (NVP / 4) + m] =
+                make_float4(s0.x + s1.x + s2.x + s3.x, s0.y + s1.y + s2.y + s3.y, s0.z + s1.z + s2.z + s3.z,
+                            s0.w + s1.w + s2.w + s3.w);
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_render_bwd_power(const Camera& cam, const GaussIn& g, const uint2* ranges,
+                                   const uint32_t* point_list, GeomPtrs geo, const float* jac, const float* final_T,
+                                   const uint32_t* n_contrib, const float* dL_dpix, int power, float* rec,
+                                   hipStream_t s) {
+    const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
+    const int has_scales = g.scales != nullptr;
+    const dim3 grid(cam.gx, cam.gy), block(TILE_PIX);
+#define GSR_LAUNCH_POWER(NSH_)                                                                                      \
+    hipLaunchKernelGGL(render_bwd_power_kernel<NSH_>, grid, block, 0, s, cam, has_scales, power, ranges, point_list, \
+                       geo.rect, geo.offsets, geo.rec_a, geo.rec_b, geo.rec_c, (const float4*)jac, final_T,        \
+                       n_contrib, dL_dpix, (float4*)rec)
+    switch (nsh) {
+        case 0: GSR_LAUNCH_POWER(0); break;
+        case 1: GSR_LAUNCH_POWER(1); break;
+        case 4: GSR_LAUNCH_POWER(4); break;
+        case 9: GSR_LAUNCH_POWER(9); break;
+        case 16: GSR_LAUNCH_POWER(16); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef GSR_LAUNCH_POWER
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------- per-Gaussian sums --
+template <int NSH>
+__global__ void __launch_bounds__(256)
+gauss_bwd_power_kernel(GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float4* __restrict__ rec,
+                       GradsOut out) {
+    constexpr int NVP = PowerShape<NSH>::NVP;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.P) return;
+    float s[NVP];
+#pragma unroll
+    for (int m = 0; m < NVP; m++) s[m] = 0.f;
+    if (radii[i] > 0) {
+        const uint32_t off = geo.offsets[i], cnt = geo.tiles[i];
+        for (uint32_t e = 0; e < cnt; e++) {
+            const float4* r = rec + (size_t)(off + e) * (NVP / 4);
+#pragma unroll
+            for (int m = 0; m < NVP / 4; m++) {
+                const float4 t = r[m];
+                s[4 * m] += t.x; s[4 * m + 1] += t.y; s[4 * m + 2] += t.z; s[4 * m + 3] += t.w;
+            }
+        }
+    }
+    out.dmeans2D[3 * i] = s[0];
+    out.dmeans2D[3 * i + 1] = s[1];
+    out.dmeans2D[3 * i + 2] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) out.dcolors[3 * i + k] = s[2 + k];
+    out.dopacity[i] = s[5];
+#pragma unroll
+    for (int k = 0; k < 3; k++) out.dmeans3D[3 * i + k] = s[6 + k];
+#pragma unroll
+    for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = s[9 + k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) out.dscales[3 * i + k] = s[15 + k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) out.drot[4 * i + k] = s[18 + k];
+    if (out.dsh && g.M > 0) {
+        float* d = out.dsh + (size_t)3 * g.M * i;
+#pragma unroll
+        for (int k = 0; k < 3 * NSH; k++)
+            if (k < 3 * g.M) d[k] = s[22 + k];
+        for (int k = 3 * NSH; k < 3 * g.M; k++) d[k] = 0.f;
+    }
+}
+
+hipError_t launch_gauss_bwd_power(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii,
+                                  const float* rec, const GradsOut& out, hipStream_t s) {
+    if (g.P == 0) return hipSuccess;
+    const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
+    const dim3 grid((g.P + 255) / 256), block(256);
+    const float4* r = (const float4*)rec;
+    switch (nsh) {
+        case 0: hipLaunchKernelGGL(gauss_bwd_power_kernel<0>, grid, block, 0, s, g, geo, radii, r, out); break;
+        case 1: hipLaunchKernelGGL(gauss_bwd_power_kernel<1>, grid, block, 0, s, g, geo, radii, r, out); break;
+        case 4: hipLaunchKernelGGL(gauss_bwd_power_kernel<4>, grid, block, 0, s, g, geo, radii, r, out); break;
+        case 9: hipLaunchKernelGGL(gauss_bwd_power_kernel<9>, grid, block, 0, s, g, geo, radii, r, out); break;
+        case 16: hipLaunchKernelGGL(gauss_bwd_power_kernel<16>, grid, block, 0, s, g, geo, radii, r, out); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace gsr

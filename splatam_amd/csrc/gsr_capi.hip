@@ -356,7 +356,6 @@ int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, c
     if (rc != GSR_OK) return rc;
     if (!grads) return fail(GSR_ERR_INVALID_ARG, "grads required");
     if (num_rendered < 0) return fail(GSR_ERR_INVALID_ARG, "num_rendered must be >= 0");
-    if (power != 1) return fail(GSR_ERR_INVALID_ARG, "backward_power != 1 not supported by this build");
     hipStream_t stream = (hipStream_t)stream_;
     const Camera cam = make_camera(settings);
     const GaussIn g = make_gauss(gaussians);
@@ -372,8 +371,42 @@ int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, c
     const float* final_T = (const float*)(ib + IL.final_T);
     const uint32_t* n_contrib = (const uint32_t*)(ib + IL.n_contrib);
     const uint2* ranges = (const uint2*)(ib + IL.ranges);
-    float4* inst = nullptr;
     hipError_t e;
+    GradsOut out{grads->dmeans2D, grads->dcolors, grads->dopacity, grads->dmeans3D,
+                 grads->dcov3D,   grads->dsh,     grads->dscales,  grads->drotations};
+    if (!out.dmeans2D || !out.dcolors || !out.dopacity || !out.dmeans3D || !out.dcov3D || !out.dscales || !out.drot)
+        return fail(GSR_ERR_INVALID_ARG, "gradient output pointers required");
+    if (power != 1) {
+        // per-pair powf before summation (renderCUDAFused, backward.cu:850-1140): gsr_backward_power.hip
+        const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
+        const int nvp = power_record_floats(nsh);
+        if (nvp < 0) return fail(GSR_ERR_INVALID_ARG, "unsupported sh_degree for backward_power != 1");
+        if (num_rendered > 0 && !binning_buffer) return fail(GSR_ERR_INVALID_ARG, "missing binning buffer");
+        if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
+        const size_t jac_bytes = (sizeof(float) * JAC_FLOATS * (size_t)P + 255) / 256 * 256;
+        const size_t rec_bytes = sizeof(float) * (size_t)nvp * (size_t)num_rendered;
+        char* scratch = (char*)obtain(alloc, alloc_ctx, GSR_BUF_SCRATCH, jac_bytes + rec_bytes);
+        if (!scratch) return fail(GSR_ERR_ALLOC, "allocator returned NULL (backward scratch)");
+        float* jac = (float*)scratch;
+        float* rec = (float*)(scratch + jac_bytes);
+        {
+            StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
+            if ((e = launch_gauss_jac(cam, g, geo, radii, jac, stream)) != hipSuccess)
+                return hip_fail(e, "gaussian jacobian");
+        }
+        if (num_rendered > 0) {
+            const uint32_t* point_list = (const uint32_t*)((const char*)binning_buffer + BL.point_list);
+            StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream);
+            if ((e = launch_render_bwd_power(cam, g, ranges, point_list, geo, jac, final_T, n_contrib, dL_dout_color,
+                                             power, rec, stream)) != hipSuccess)
+                return hip_fail(e, "render backward (power)");
+        }
+        StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
+        if ((e = launch_gauss_bwd_power(cam, g, geo, radii, rec, out, stream)) != hipSuccess)
+            return hip_fail(e, "gaussian backward (power)");
+        return GSR_OK;
+    }
+    float4* inst = nullptr;
     if (num_rendered > 0) {
         if (!binning_buffer) return fail(GSR_ERR_INVALID_ARG, "missing binning buffer");
         if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
@@ -386,10 +419,6 @@ int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, c
             hipSuccess)
             return hip_fail(e, "render backward");
     }
-    GradsOut out{grads->dmeans2D, grads->dcolors, grads->dopacity, grads->dmeans3D,
-                 grads->dcov3D,   grads->dsh,     grads->dscales,  grads->drotations};
-    if (!out.dmeans2D || !out.dcolors || !out.dopacity || !out.dmeans3D || !out.dcov3D || !out.dscales || !out.drot)
-        return fail(GSR_ERR_INVALID_ARG, "gradient output pointers required");
     {
         StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
         if ((e = launch_gauss_bwd(cam, g, geo, radii, inst, out, stream)) != hipSuccess)
