@@ -51,6 +51,16 @@ SIGNATURES = {
     "gsr_selftest_reduce9": (c_int, [c_void_p, c_void_p, c_void_p]),
     "gsr_timing_enable": (c_int, [c_int]),
     "gsr_timing_read": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
+    # include/gsr_glue.h: fused SplaTAM tracking glue
+    "gsr_track_scratch_floats": (c_int, [c_int]),
+    "gsr_track_transform_fwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                        c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gsr_track_transform_bwd": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "gsr_track_l1_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
+                                 ctypes.c_float, ctypes.c_float, c_void_p, c_void_p, c_void_p]),
+    "gsr_track_l1_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
+                                 ctypes.c_float, ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 

@@ -21,9 +21,10 @@
 using namespace gsr;
 
 namespace {
-
 thread_local std::string g_last_error;
+}  // namespace
 
+namespace gsr {
 int fail(int code, const std::string& msg) {
     g_last_error = msg;
     return code;
@@ -32,6 +33,9 @@ int fail(int code, const std::string& msg) {
 int hip_fail(hipError_t e, const char* where) {
     return fail(GSR_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
 }
+}  // namespace gsr
+
+namespace {
 
 struct Pinned {  // per-thread staging of the device counters + the event after the scan
     uint32_t* p = nullptr;

@@ -6,6 +6,7 @@
 // (rasterizer_impl.cu:155-194, rasterizer_impl.h:21-73), so gsr_backward can
 // find every array again without any header read-back.
 #pragma once
+#include <string>
 
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -552,6 +553,9 @@ struct GradsOut {
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float4* inst,
                             const GradsOut& out, hipStream_t s);
 hipError_t launch_selftest_reduce9(const float* in, float* out, hipStream_t s);
+// error reporting shared by the C entry points (gsr_last_error)
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* where);
 // backward_power != 1 (the vendored renderCUDAFused semantics, backward.cu:850-1140)
 constexpr int JAC_FLOATS = 80;  // per-Gaussian linear chain pack, see gsr_backward_power.hip
 int power_record_floats(int nsh);  // values stored per instance record

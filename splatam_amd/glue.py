@@ -1,0 +1,136 @@
+"""Fused SplaTAM tracking glue (include/gsr_glue.h, csrc/gsr_glue.hip).
+
+Autograd wrappers around the HIP glue kernels that replace, for the tracking
+iteration, the ~300 small torch kernels of
+
+* transform_to_frame(params, t, gaussians_grad=False, camera_grad=True)
+  (utils/slam_helpers.py:252-304) and the rendervar builders
+  (slam_helpers.py:124-139, 234-249) incl. get_depth_and_silhouette
+  (slam_helpers.py:196-213)  ->  ``track_transform``;
+* the tracking L1 terms of get_loss (scripts/splatam.py:262-296)  ->  ``tracking_l1``.
+
+Only the camera pose receives gradients from ``track_transform`` (the
+Gaussians are detached in tracking).  Like the rasterizer there is no CPU
+path: these raise on non-ROCm tensors.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import lib
+
+
+def _check(rc: int, what: str):
+    if rc < 0:
+        raise RuntimeError(f"{what}: {lib.gsr_last_error().decode(errors='replace')}")
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _f32c(t: torch.Tensor, name: str) -> torch.Tensor:
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name}: the fused glue runs on ROCm devices only (no CPU fallback)")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name}: expected float32, got {t.dtype}")
+    return t.contiguous()
+
+
+class _TrackTransform(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cam_rots, cam_trans, means_world, unnorm_rot, logit_opac, log_scales, w2c, time_idx):
+        cam_rots, cam_trans = _f32c(cam_rots, "cam_unnorm_rots"), _f32c(cam_trans, "cam_trans")
+        means_world, unnorm_rot = _f32c(means_world, "means3D"), _f32c(unnorm_rot, "unnorm_rotations")
+        logit_opac, log_scales, w2c = _f32c(logit_opac, "logit_opacities"), _f32c(log_scales, "log_scales"), \
+            _f32c(w2c, "w2c")
+        T = cam_rots.shape[-1]
+        if cam_rots.shape != (1, 4, T) or cam_trans.shape != (1, 3, T):
+            raise RuntimeError("cam_unnorm_rots / cam_trans must be (1,4,T) / (1,3,T)")
+        t = int(time_idx)
+        P = means_world.shape[0]
+        scols = log_scales.shape[1]
+        dev = means_world.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        means_cam = torch.empty(P, 3, **f32)
+        rot = torch.empty(P, 4, **f32)
+        dcol = torch.empty(P, 3, **f32)
+        opac = torch.empty(P, 1, **f32)
+        scales = torch.empty(P, 3, **f32)
+        rc = lib.gsr_track_transform_fwd(P, means_world.data_ptr(), unnorm_rot.data_ptr(), logit_opac.data_ptr(),
+                                         log_scales.data_ptr(), scols, cam_rots.data_ptr() + 4 * t,
+                                         cam_trans.data_ptr() + 4 * t, T, w2c.data_ptr(), means_cam.data_ptr(),
+                                         rot.data_ptr(), dcol.data_ptr(), opac.data_ptr(), scales.data_ptr(),
+                                         _stream(means_world))
+        _check(rc, "track_transform_fwd")
+        ctx.mark_non_differentiable(opac, scales)
+        ctx.save_for_backward(cam_rots, cam_trans, means_world, unnorm_rot, means_cam, w2c)
+        ctx.meta = (t, T, scols)
+        return means_cam, rot, dcol, opac, scales
+
+    @staticmethod
+    def backward(ctx, g_means, g_rot, g_dcol, _g_opac, _g_scales):
+        cam_rots, cam_trans, means_world, unnorm_rot, means_cam, w2c = ctx.saved_tensors
+        t, T, scols = ctx.meta
+        P = means_world.shape[0]
+        if g_means is None:
+            g_means = torch.zeros_like(means_cam)
+        g_means = g_means.contiguous()
+        g_rot = g_rot.contiguous() if (g_rot is not None and scols != 1) else None
+        g_dcol = g_dcol.contiguous() if g_dcol is not None else None
+        dq = torch.zeros_like(cam_rots)
+        dt = torch.zeros_like(cam_trans)
+        scratch = torch.empty(lib.gsr_track_scratch_floats(P), dtype=torch.float32, device=means_world.device)
+        rc = lib.gsr_track_transform_bwd(P, means_world.data_ptr(), unnorm_rot.data_ptr(), scols,
+                                         cam_rots.data_ptr() + 4 * t, means_cam.data_ptr(), w2c.data_ptr(),
+                                         g_means.data_ptr(), g_rot.data_ptr() if g_rot is not None else None,
+                                         g_dcol.data_ptr() if g_dcol is not None else None,
+                                         dq.data_ptr() + 4 * t, dt.data_ptr() + 4 * t, T, scratch.data_ptr(),
+                                         _stream(means_world))
+        _check(rc, "track_transform_bwd")
+        return dq, dt, None, None, None, None, None, None
+
+
+def track_transform(params: dict, time_idx: int, w2c: torch.Tensor):
+    """Returns (means3D_cam, rotations, depth_colors [z,1,z^2], opacities, scales) for the tracking
+    iteration; differentiable w.r.t. params['cam_unnorm_rots'] / params['cam_trans'] only."""
+    return _TrackTransform.apply(params["cam_unnorm_rots"], params["cam_trans"], params["means3D"].detach(),
+                                 params["unnorm_rotations"].detach(), params["logit_opacities"].detach(),
+                                 params["log_scales"].detach(), w2c, int(time_idx))
+
+
+class _TrackingL1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, im, depth_sil, gt_im, gt_depth, sil_thres, w_im, w_depth):
+        im, depth_sil = _f32c(im, "im"), _f32c(depth_sil, "depth_sil")
+        gt_im, gt_depth = _f32c(gt_im, "gt_im"), _f32c(gt_depth, "gt_depth")
+        _, H, W = im.shape
+        if depth_sil.shape != (3, H, W) or gt_im.shape != (3, H, W) or gt_depth.shape != (1, H, W):
+            raise RuntimeError("tracking_l1: expected im/depth_sil/gt_im [3,H,W] and gt_depth [1,H,W]")
+        loss = torch.empty((), dtype=torch.float32, device=im.device)
+        scratch = torch.empty(lib.gsr_track_scratch_floats(H * W), dtype=torch.float32, device=im.device)
+        rc = lib.gsr_track_l1_fwd(H, W, im.data_ptr(), depth_sil.data_ptr(), gt_im.data_ptr(), gt_depth.data_ptr(),
+                                  float(sil_thres), float(w_im), float(w_depth), loss.data_ptr(), scratch.data_ptr(),
+                                  _stream(im))
+        _check(rc, "track_l1_fwd")
+        ctx.save_for_backward(im, depth_sil, gt_im, gt_depth)
+        ctx.meta = (float(sil_thres), float(w_im), float(w_depth))
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        im, depth_sil, gt_im, gt_depth = ctx.saved_tensors
+        sil_thres, w_im, w_depth = ctx.meta
+        _, H, W = im.shape
+        g = g.contiguous()
+        dim = torch.empty_like(im)
+        dds = torch.empty_like(depth_sil)
+        rc = lib.gsr_track_l1_bwd(H, W, im.data_ptr(), depth_sil.data_ptr(), gt_im.data_ptr(), gt_depth.data_ptr(),
+                                  sil_thres, w_im, w_depth, g.data_ptr(), dim.data_ptr(), dds.data_ptr(), _stream(im))
+        _check(rc, "track_l1_bwd")
+        return dim, dds, None, None, None, None, None
+
+
+def tracking_l1(im, depth_sil, gt_im, gt_depth, sil_thres=0.99, w_im=0.5, w_depth=1.0):
+    """w_im * sum(mask*|gt_im - im|) + w_depth * sum(mask*|gt_depth - depth|) with SplaTAM's tracking mask."""
+    return _TrackingL1.apply(im, depth_sil, gt_im, gt_depth, sil_thres, w_im, w_depth)

@@ -123,14 +123,43 @@ class TrackingConfig:
     w_depth: float = 1.0
 
 
-def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = TrackingConfig(), fast=True):
+def fused_eligible(params, curr_data, cfg: TrackingConfig) -> bool:
+    """The fused HIP glue covers SplaTAM's tracking configuration: only the camera
+    pose needs gradients, L1 with the silhouette mask, no outlier-depth rejection."""
+    gauss_keys = ("means3D", "rgb_colors", "unnorm_rotations", "logit_opacities", "log_scales")
+    return (cfg.use_l1 and cfg.use_sil_for_loss and not cfg.ignore_outlier_depth_loss
+            and params["means3D"].is_cuda and not any(params[k].requires_grad for k in gauss_keys)
+            and curr_data["im"].dim() == 3 and curr_data["depth"].dim() == 3)
+
+
+def _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg: TrackingConfig):
+    from .glue import track_transform, tracking_l1
+    means, rots, dcol, opac, scales = track_transform(params, iter_time_idx, curr_data["w2c"])
+    P = means.shape[0]
+    means2D = torch.zeros(P, 3, device=means.device, requires_grad=True)
+    means2D_ds = torch.zeros(P, 3, device=means.device, requires_grad=True)
+    ras = GaussianRasterizer(raster_settings=curr_data["cam"])
+    im, radius, _ = ras(means3D=means, means2D=means2D, colors_precomp=params["rgb_colors"], opacities=opac,
+                        scales=scales, rotations=rots)
+    depth_sil, _, _ = ras(means3D=means, means2D=means2D_ds, colors_precomp=dcol, opacities=opac, scales=scales,
+                          rotations=rots)
+    loss = tracking_l1(im, depth_sil, curr_data["im"], curr_data["depth"], cfg.sil_thres, cfg.w_im, cfg.w_depth)
+    return loss, radius, means2D
+
+
+def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = TrackingConfig(), fast=True,
+                      fused=True):
     """scripts/splatam.py:220-353 with tracking=True: two renders (RGB, [z,1,z^2]), masked L1 sums.
 
+    fused=True (and fused_eligible): the pose transform / rendervar builders and
+    the masked L1 loss run as the HIP glue kernels of include/gsr_glue.h.
     fast=True evaluates the same loss without host synchronisation: boolean-mask
     indexing `x[mask].sum()` becomes `where(mask, x, 0).sum()` (same value and
     gradient, NaNs outside the mask excluded exactly as indexing excludes them),
     and the pose transform avoids the K=P GEMM (see _affine).  fast=False is the
     literal statement of the reference code."""
+    if fused and fast and fused_eligible(params, curr_data, cfg):
+        return _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg)
     tg = transform_to_frame(params, iter_time_idx, gaussians_grad=False, camera_grad=True, fast=fast)
     rendervar = transformed_params2rendervar(params, tg)
     depth_sil_rendervar = transformed_params2depthplussilhouette(params, curr_data["w2c"], tg, fast=fast)

@@ -1,5 +1,5 @@
 """CPU checks of the drop-in boundary: libgsr.so loads and exports every symbol
-include/gsr.h declares, the ctypes mirror matches the header, and the Python
+include/*.h declare, the ctypes mirror matches the header, and the Python
 wrapper hands `_C` exactly the argument lists the reference wrapper does
 (golden: tests/golden/abi_signature.json, captured from the reference)."""
 import ctypes
@@ -17,7 +17,8 @@ GOLDEN = os.path.join(ROOT, "tests", "golden", "abi_signature.json")
 
 
 def header_functions():
-    txt = open(HEADER).read()
+    import glob
+    txt = "\n".join(open(h).read() for h in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))))
     return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\*?\s+\**(gsr_[a-z_0-9]+)\s*\(", txt, re.M)))
 
 
@@ -35,7 +36,7 @@ def test_library_exports_every_header_symbol():
     assert len(fns) >= 10, fns
     missing = [f for f in fns if not hasattr(lib, f)]
     assert not missing, missing
-    assert set(fns) == set(_lib.SIGNATURES), "ctypes signature table out of sync with include/gsr.h"
+    assert set(fns) == set(_lib.SIGNATURES), "ctypes signature table out of sync with include/*.h"
     assert lib.gsr_abi_version() == 1
 
 
