@@ -114,6 +114,26 @@ int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians,
                  int power, const gsr_grads* grads,
                  gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
+/* Dual render: one rasterization composites a second colour set colors2
+ * [P,3] (precomputed) with the same alpha / transmittance, i.e. the two
+ * GaussianRasterizer calls SplaTAM makes per iteration on identical geometry
+ * (RGB and [z, 1, z^2], scripts/splatam.py:255,259), sharing preprocess,
+ * binning and the per-pair evaluation.  out_color and
+ * out_color2 are bitwise the images two gsr_forward calls would produce. */
+int gsr_forward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians,
+                     const float* colors2, float* out_color, float* out_color2, float* out_depth,
+                     int* radii, gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
+/* Backward of gsr_forward_dual (power 1): every geometric gradient in `grads`
+ * is the sum of the two renders' (as autograd would accumulate it over two
+ * calls), grads->dcolors is d/dcolors of the first set and dcolors2 [P,3]
+ * that of colors2. */
+int gsr_backward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians,
+                      const int* radii, const float* colors2, const float* dL_dout_color,
+                      const float* dL_dout_color2, int num_rendered, const void* geom_buffer,
+                      const void* binning_buffer, const void* image_buffer, const gsr_grads* grads,
+                      float* dcolors2, gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
 /* Frustum test view_z > 0.001.  Replaces markVisible / checkFrustum
  * (rasterize_points.cu:198-216, rasterizer_impl.cu:54-67,141-153).
  * visible: [P] bytes (0/1, torch.bool layout). */

@@ -163,6 +163,74 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         return tuple(out)
 
 
+def rasterize_gaussians_dual(background, means3D, colors, colors2, opacity, scales, rotations, scale_modifier,
+                             cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh,
+                             degree, campos, prefiltered):
+    """gsr_forward_dual: rasterize_gaussians with a second precomputed colour set
+    composited in the same pass.  Returns (num_rendered, color, color2, radii,
+    geomBuffer, binningBuffer, imgBuffer, depth)."""
+    device = means3D.device
+    if device.type != "cuda":
+        raise RuntimeError("splatam_amd rasterizer runs on ROCm devices only (no CPU fallback); "
+                           f"means3D is on {device}")
+    P = means3D.size(0)
+    H, W = int(image_height), int(image_width)
+    f32 = dict(dtype=torch.float32, device=device)
+    if colors2 is None or colors2.shape != (P, 3):
+        raise RuntimeError("colors2 must have dimensions (num_points, 3)")
+    with torch.cuda.device(device):
+        s, keep_s = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, scale_modifier,
+                              degree, prefiltered, device)
+        g, keep_g, _ = _gaussians(means3D, sh, colors, opacity, scales, rotations, cov3D_precomp, device)
+        c2 = _dev_f32(colors2, device, "colors2")
+        out_color = torch.empty(3, H, W, **f32)
+        out_color2 = torch.empty(3, H, W, **f32)
+        out_depth = torch.empty(1, H, W, **f32)
+        radii = torch.empty(P, dtype=torch.int32, device=device)
+        _begin(device)
+        n = lib.gsr_forward_dual(ctypes.byref(s), ctypes.byref(g), _ptr(c2), out_color.data_ptr(),
+                                 out_color2.data_ptr(), out_depth.data_ptr(), radii.data_ptr() if P else None,
+                                 _ALLOC_CB, None, _stream(device))
+        _check(n, "rasterize_gaussians_dual")
+        bufs = _tls.buffers
+        return (int(n), out_color, out_color2, radii, bufs[0], bufs[1], bufs[2], out_depth)
+
+
+def rasterize_gaussians_dual_backward(background, means3D, radii, colors, colors2, scales, rotations, scale_modifier,
+                                      cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
+                                      dL_dout_color2, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer):
+    """gsr_backward_dual.  Returns (dmeans2D, dcolors, dcolors2, dopacity, dmeans3D, dcov3D, dsh, dscales,
+    drotations); geometric gradients are the sums over both colour sets."""
+    device = means3D.device
+    P = means3D.size(0)
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    M = sh.size(1) if (sh is not None and sh.numel() > 0 and sh.size(0) != 0) else 0
+    f32 = dict(dtype=torch.float32, device=device)
+    out = [torch.empty(P, 3, **f32), torch.empty(P, 3, **f32), torch.empty(P, 1, **f32), torch.empty(P, 3, **f32),
+           torch.empty(P, 6, **f32), torch.empty(P, M, 3, **f32), torch.empty(P, 3, **f32), torch.empty(P, 4, **f32)]
+    dcolors2 = torch.empty(P, 3, **f32)
+    if P == 0:
+        return (out[0], out[1], dcolors2, *out[2:])
+    with torch.cuda.device(device):
+        s, keep_s = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, scale_modifier,
+                              degree, False, device)
+        g, keep_g, _ = _gaussians(means3D, sh, colors, None, scales, rotations, cov3D_precomp, device)
+        c2 = _dev_f32(colors2, device, "colors2")
+        dpix = _dev_f32(dL_dout_color, device, "dL_dout_color")
+        dpix2 = _dev_f32(dL_dout_color2, device, "dL_dout_color2")
+        radii_c = radii.to(device=device, dtype=torch.int32).contiguous()
+        grads = GsrGrads(*[o.data_ptr() if o.numel() > 0 else None for o in out])
+        _begin(device)
+        rc = lib.gsr_backward_dual(ctypes.byref(s), ctypes.byref(g), radii_c.data_ptr(), _ptr(c2), dpix.data_ptr(),
+                                   dpix2.data_ptr(), int(R), geomBuffer.data_ptr(),
+                                   binningBuffer.data_ptr() if binningBuffer.numel() else None,
+                                   imageBuffer.data_ptr(), ctypes.byref(grads), dcolors2.data_ptr(), _ALLOC_CB, None,
+                                   _stream(device))
+        _check(rc, "rasterize_gaussians_dual_backward")
+        _tls.buffers = {}
+        return (out[0], out[1], dcolors2, *out[2:])
+
+
 def mark_visible(means3D, viewmatrix, projmatrix):
     """markVisible (rasterize_points.cu:198-216): bool[P], view_z > 0.001."""
     device = means3D.device

@@ -21,18 +21,24 @@ namespace gsr {
 
 constexpr int BWD_BATCH = 128;
 
-template <int BWD_GROUP, bool PREFETCH>
+// DUAL: the pass also carries a second colour set (colors2, dL_dpix2) composited
+// with the same alpha / T (one dual forward): the per-pair dL/dalpha is the sum
+// of both renders' and each record holds 12 sums (the 9 below + dch * dL_dpix2).
+template <int BWD_GROUP, bool PREFETCH, bool DUAL>
 __global__ void __launch_bounds__(TILE_PIX)
 render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                   const uint2* __restrict__ rect, const uint32_t* __restrict__ offsets,
                   const float4* __restrict__ rec_a, const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
                   const float* __restrict__ final_T, const uint32_t* __restrict__ n_contrib,
-                  const float* __restrict__ dL_dpix, float4* __restrict__ inst) {
+                  const float* __restrict__ dL_dpix, const float* __restrict__ colors2,
+                  const float* __restrict__ dL_dpix2, float4* __restrict__ inst) {
+    constexpr int NV = DUAL ? 12 : 9;
     __shared__ float4 s_a[BWD_BATCH];
     __shared__ float4 s_b[BWD_BATCH];
     __shared__ float4 s_c[BWD_BATCH];
+    __shared__ float4 s_d[DUAL ? BWD_BATCH : 1];
     __shared__ uint32_t s_u[BWD_BATCH];
-    __shared__ __attribute__((aligned(16))) float s_acc[4 * BWD_BATCH * 9];
+    __shared__ __attribute__((aligned(16))) float s_acc[4 * BWD_BATCH * NV];
     __shared__ uint32_t s_wmax[4];
     __shared__ uint8_t s_mask[BWD_BATCH];
     __shared__ __attribute__((aligned(16))) uint16_t s_list[4][BWD_BATCH + 4];
@@ -47,11 +53,16 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     const uint2 range = ranges[tile];
     const float T_final = inside ? final_T[pid] : 0.f;
     const uint32_t last = inside ? n_contrib[pid] : 0u;
-    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
+    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f, dq0 = 0.f, dq1 = 0.f, dq2 = 0.f;
     if (inside) {
         dp0 = dL_dpix[pid];
         dp1 = dL_dpix[HW + pid];
         dp2 = dL_dpix[2 * HW + pid];
+        if (DUAL) {
+            dq0 = dL_dpix2[pid];
+            dq1 = dL_dpix2[HW + pid];
+            dq2 = dL_dpix2[2 * HW + pid];
+        }
     }
     uint32_t wmax = last;
 #pragma unroll
@@ -67,7 +78,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         inst[3 * u + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
         inst[3 * u + 2] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    const float bg_dot = cam.bg[0] * dp0 + cam.bg[1] * dp1 + cam.bg[2] * dp2;
+    float bg_dot = cam.bg[0] * dp0 + cam.bg[1] * dp1 + cam.bg[2] * dp2;
+    if (DUAL) bg_dot += cam.bg[0] * dq0 + cam.bg[1] * dq1 + cam.bg[2] * dq2;
     const bool bg_on = cam.bg[0] != 0.f || cam.bg[1] != 0.f || cam.bg[2] != 0.f;  // uniform
     const float pxf = (float)px, pyf = (float)py;
     float T = T_final;
@@ -76,13 +88,14 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     float acc_dot = 0.f, lc_dot = 0.f, last_alpha = 0.f;
     const int row = lane >> 4;
     // records of the first batch (back to front)
-    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa;
+    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
     uint32_t pu = 0;
     if (tid < min(BWD_BATCH, (int)bmax)) {
         const uint32_t k = range.x + bmax - 1 - tid;
         const uint32_t gi = point_list[k];
         pu = instance_slot(rect[gi], offsets[gi], blockIdx.x, blockIdx.y);
         pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
+        if (DUAL) pd = make_float4(colors2[3 * gi], colors2[3 * gi + 1], colors2[3 * gi + 2], 0.f);
     }
     for (int hi = (int)bmax; hi > 0; hi -= BWD_BATCH) {
         const int cnt = min(BWD_BATCH, hi);
@@ -91,9 +104,10 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             s_a[tid] = stage_a(pa);
             s_b[tid] = stage_b(pb);
             s_c[tid] = pc;
+            if (DUAL) s_d[tid] = pd;
             s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
         }
-        for (int q = tid; q < 4 * BWD_BATCH * 9 / 4; q += TILE_PIX)
+        for (int q = tid; q < 4 * BWD_BATCH * NV / 4; q += TILE_PIX)
             reinterpret_cast<float4*>(s_acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         __syncthreads();
         {   // prefetch the next batch
@@ -103,6 +117,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 const uint32_t gi = point_list[k];
                 pu = instance_slot(rect[gi], offsets[gi], blockIdx.x, blockIdx.y);
                 pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
+                if (DUAL) pd = make_float4(colors2[3 * gi], colors2[3 * gi + 1], colors2[3 * gi + 2], 0.f);
             }
         }
         // entries j with pos = hi-1-j >= wmax lie behind every pixel of this wave
@@ -139,13 +154,17 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             // h = G * dL/dG = (o * G) * dL/dalpha.  gauss_bwd turns them into the reference's
             // per-pair quantities (backward.cu:1020-1038): dmean2D = -ddel * (Q [hx, hy]),
             // dconic = -0.5 * (hxx, hxy, hyy); both are linear in the sums (Q is per Gaussian).
-            float v[BWD_GROUP * 9];
+            float v[BWD_GROUP * NV];
 #pragma unroll
             for (int k = 0; k < BWD_GROUP; k++) {
                 const float4 c = s_c[j[k]];
                 const float inv = __builtin_amdgcn_rcpf(1.f - alpha[k]);  // v_rcp_f32 (~1 ulp)
                 const float Tn = T * inv;                                  // T / (1 - alpha), backward.cu:978
-                const float cd = c.x * dp0 + c.y * dp1 + c.z * dp2;
+                float cd = c.x * dp0 + c.y * dp1 + c.z * dp2;
+                if (DUAL) {
+                    const float4 d2 = s_d[j[k]];
+                    cd += d2.x * dq0 + d2.y * dq1 + d2.z * dq2;
+                }
                 const float na_dot = last_alpha * lc_dot + (1.f - last_alpha) * acc_dot;
                 float dL_dalpha = (cd - na_dot) * Tn;
                 if (bg_on) dL_dalpha += (-T_final * inv) * bg_dot;
@@ -154,7 +173,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 const float dch = o_ ? alpha[k] * Tn : 0.f;
                 const float h = araw[k] * dL_dalpha;
                 const float hx = h * dx[k], hy = h * dy[k];
-                float* vk = v + 9 * k;
+                float* vk = v + NV * k;
                 vk[0] = hx;
                 vk[1] = hy;
                 vk[2] = hx * dx[k];
@@ -164,6 +183,11 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 vk[6] = dch * dp0;
                 vk[7] = dch * dp1;
                 vk[8] = dch * dp2;
+                if (DUAL) {
+                    vk[9] = dch * dq0;
+                    vk[10] = dch * dq1;
+                    vk[11] = dch * dq2;
+                }
                 if (o_) {
                     T = Tn;
                     acc_dot = na_dot;
@@ -172,12 +196,21 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 }
             }
             if constexpr (BWD_GROUP == 4) {
-                float r[9];
-                wave_reduce4x9(v, r);
+                float r[NV];
+                wave_reduce_n<4 * NV>(v, r);  // row rho holds item rho's NV sums
                 if ((lane & 15) == 0 && i + row < n) {
-                    float* dst = s_acc + (w * BWD_BATCH + j[row]) * 9;
+                    float* dst = s_acc + (w * BWD_BATCH + j[row]) * NV;
 #pragma unroll
-                    for (int m = 0; m < 9; m++) dst[m] = r[m];
+                    for (int m = 0; m < NV; m++) dst[m] = r[m];
+                }
+            } else if constexpr (DUAL) {
+                float r[6];
+                wave_reduce_n<24>(v, r);  // row rho: item rho >> 1, values 6 * (rho & 1) + m
+                const int item = row >> 1, half = row & 1;
+                if ((lane & 15) == 0 && i + item < n) {
+                    float* dst = s_acc + (w * BWD_BATCH + j[item]) * NV + 6 * half;
+#pragma unroll
+                    for (int m = 0; m < 6; m++) dst[m] = r[m];
                 }
             } else {
                 float r[5];
@@ -193,34 +226,36 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         }
         __syncthreads();
         if (tid < cnt) {
-            float sum[9];
+            float sum[12];
 #pragma unroll
-            for (int m = 0; m < 9; m++)
-                sum[m] = s_acc[(0 * BWD_BATCH + tid) * 9 + m] + s_acc[(1 * BWD_BATCH + tid) * 9 + m] +
-                         s_acc[(2 * BWD_BATCH + tid) * 9 + m] + s_acc[(3 * BWD_BATCH + tid) * 9 + m];
+            for (int m = 0; m < 12; m++)
+                sum[m] = m < NV ? s_acc[(0 * BWD_BATCH + tid) * NV + m] + s_acc[(1 * BWD_BATCH + tid) * NV + m] +
+                                      s_acc[(2 * BWD_BATCH + tid) * NV + m] + s_acc[(3 * BWD_BATCH + tid) * NV + m]
+                                : 0.f;
             const uint32_t u = s_u[tid];
             inst[3 * u] = make_float4(sum[0], sum[1], sum[2], sum[3]);
             inst[3 * u + 1] = make_float4(sum[4], sum[5], sum[6], sum[7]);
-            inst[3 * u + 2] = make_float4(sum[8], 0.f, 0.f, 0.f);
+            inst[3 * u + 2] = make_float4(sum[8], sum[9], sum[10], sum[11]);
         }
         __syncthreads();
     }
 }
 
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
-                             const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, float4* inst,
-                             hipStream_t s) {
+                             const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
+                             const float* colors2, const float* dL_dpix2, float4* inst, hipStream_t s) {
     // GSR_BWD_VARIANT (tuning only): 1 = 4-entry groups (default), 0 = 4 + prefetch, 2 = 2 + prefetch, 3 = 2
     static const int variant = [] {
         const char* e = getenv("GSR_BWD_VARIANT");
         return e ? atoi(e) : 1;
     }();
-    auto k = render_bwd_kernel<4, false>;
-    if (variant == 0) k = render_bwd_kernel<4, true>;
-    if (variant == 2) k = render_bwd_kernel<2, true>;
-    if (variant == 3) k = render_bwd_kernel<2, false>;
+    auto k = render_bwd_kernel<4, false, false>;
+    if (variant == 0) k = render_bwd_kernel<4, true, false>;
+    if (variant == 2) k = render_bwd_kernel<2, true, false>;
+    if (variant == 3) k = render_bwd_kernel<2, false, false>;
+    if (colors2) k = (variant == 3) ? render_bwd_kernel<2, false, true> : render_bwd_kernel<4, false, true>;
     hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rect, geo.offsets,
-                       geo.rec_a, geo.rec_b, geo.rec_c, final_T, n_contrib, dL_dpix, inst);
+                       geo.rec_a, geo.rec_b, geo.rec_c, final_T, n_contrib, dL_dpix, colors2, dL_dpix2, inst);
     return hipGetLastError();
 }
 
@@ -231,6 +266,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     if (i >= g.P) return;
     const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
     float g2[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float dcol2[3] = {0.f, 0.f, 0.f};
     float dmean[3] = {0.f, 0.f, 0.f}, dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dscale[3] = {0.f, 0.f, 0.f},
           drot[4] = {0.f, 0.f, 0.f, 0.f};
     float dsh[48];
@@ -241,10 +277,11 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         for (uint32_t e = 0; e < cnt; e++) {
             const float4 r0 = inst[3 * (off + e)];
             const float4 r1 = inst[3 * (off + e) + 1];
-            const float r2 = inst[3 * (off + e) + 2].x;
+            const float4 r2 = inst[3 * (off + e) + 2];
             g2[0] += r0.x; g2[1] += r0.y; g2[2] += r0.z; g2[3] += r0.w;
             g2[4] += r1.x; g2[5] += r1.y; g2[6] += r1.z; g2[7] += r1.w;
-            g2[8] += r2;
+            g2[8] += r2.x;
+            dcol2[0] += r2.y; dcol2[1] += r2.z; dcol2[2] += r2.w;
         }
         // instance records hold (hx, hy, hxx, hxy, hyy, dopacity, dcolor) sums (render_bwd_kernel)
         const float4 ra = geo.rec_a[i];
@@ -266,6 +303,11 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     out.dcolors[3 * i + 1] = g2[7];
     out.dcolors[3 * i + 2] = g2[8];
     out.dopacity[i] = g2[5];
+    if (out.dcolors2) {
+        out.dcolors2[3 * i] = dcol2[0];
+        out.dcolors2[3 * i + 1] = dcol2[1];
+        out.dcolors2[3 * i + 2] = dcol2[2];
+    }
 #pragma unroll
     for (int k = 0; k < 3; k++) out.dmeans3D[3 * i + k] = dmean[k];
 #pragma unroll

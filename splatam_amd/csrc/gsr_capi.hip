@@ -192,12 +192,16 @@ size_t gsr_geom_buffer_bytes(int P) { return GeomLayout::make(P).total; }
 size_t gsr_binning_buffer_bytes(int num_rendered, int W, int H) { return BinLayout::make(num_rendered, W, H).total; }
 size_t gsr_image_buffer_bytes(int W, int H) { return ImgLayout::make(W, H).total; }
 
-int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, float* out_color, float* out_depth,
-                int* radii, gsr_alloc_fn alloc, void* alloc_ctx, void* stream_) {
+// colors2 != NULL: dual render (second colour set composited in the same pass, out_color2)
+static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
+                        float* out_color, float* out_color2, float* out_depth, int* radii, gsr_alloc_fn alloc,
+                        void* alloc_ctx, void* stream_) {
     int rc = validate(settings, gaussians, true);
     if (rc != GSR_OK) return rc;
     if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
     if (!out_color || !out_depth) return fail(GSR_ERR_INVALID_ARG, "output image pointers required");
+    if (colors2 && !out_color2) return fail(GSR_ERR_INVALID_ARG, "out_color2 required with colors2");
+    if (colors2 && gaussians->P > 0 && !gaussians->means3D) return fail(GSR_ERR_INVALID_ARG, "means3D is required");
     hipStream_t stream = (hipStream_t)stream_;
     const Camera cam = make_camera(settings);
     const GaussIn g = make_gauss(gaussians);
@@ -245,7 +249,8 @@ int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, fl
         void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, BinLayout::make(0, W, H).total);
         if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
         if ((e = hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess ||
-            (e = hipMemsetAsync(out_depth, 0, sizeof(float) * (size_t)W * H, stream)) != hipSuccess)
+            (e = hipMemsetAsync(out_depth, 0, sizeof(float) * (size_t)W * H, stream)) != hipSuccess ||
+            (colors2 && (e = hipMemsetAsync(out_color2, 0, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess))
             return hip_fail(e, "zero outputs");
         return 0;
     }
@@ -289,8 +294,8 @@ int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, fl
         }
         {
             StageTimer t(GSR_STAGE_RENDER_FWD, 0, stream);
-            if ((e = launch_render_fwd(cam, ranges, point_list, geo, nullptr, final_T, n_contrib, out_color,
-                                       out_depth, guard, stream)) != hipSuccess)
+            if ((e = launch_render_fwd(cam, ranges, point_list, geo, colors2, final_T, n_contrib, out_color,
+                                       out_color2, out_depth, guard, stream)) != hipSuccess)
                 return hip_fail(e, "render");
         }
         speculated = true;
@@ -345,19 +350,24 @@ int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, fl
     }
     {
         StageTimer t(GSR_STAGE_RENDER_FWD, I, stream);
-        if ((e = launch_render_fwd(cam, ranges, point_list, geo, nullptr, final_T, n_contrib, out_color, out_depth,
+        if ((e = launch_render_fwd(cam, ranges, point_list, geo, colors2, final_T, n_contrib, out_color, out_color2,
+                                   out_depth,
                                    none, stream)) != hipSuccess)
             return hip_fail(e, "render");
     }
     return (int)I;
 }
 
-int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
-                 const float* dL_dout_color, int num_rendered, const void* geom_buffer, const void* binning_buffer,
-                 const void* image_buffer, int power, const gsr_grads* grads, gsr_alloc_fn alloc, void* alloc_ctx,
-                 void* stream_) {
+static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
+                         const float* dL_dout_color, const float* colors2, const float* dL_dout_color2,
+                         int num_rendered, const void* geom_buffer, const void* binning_buffer,
+                         const void* image_buffer, int power, const gsr_grads* grads, float* dcolors2,
+                         gsr_alloc_fn alloc, void* alloc_ctx, void* stream_) {
     int rc = validate(settings, gaussians, false);
     if (rc != GSR_OK) return rc;
+    if (colors2 && (!dL_dout_color2 || !dcolors2))
+        return fail(GSR_ERR_INVALID_ARG, "dual backward needs dL_dout_color2 and dcolors2");
+    if (colors2 && power != 1) return fail(GSR_ERR_INVALID_ARG, "dual render supports backward_power == 1 only");
     if (!grads) return fail(GSR_ERR_INVALID_ARG, "grads required");
     if (num_rendered < 0) return fail(GSR_ERR_INVALID_ARG, "num_rendered must be >= 0");
     hipStream_t stream = (hipStream_t)stream_;
@@ -419,10 +429,11 @@ int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, c
         const char* bb = (const char*)binning_buffer;
         const uint32_t* point_list = (const uint32_t*)(bb + BL.point_list);
         StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream);
-        if ((e = launch_render_bwd(cam, ranges, point_list, geo, final_T, n_contrib, dL_dout_color, inst, stream)) !=
-            hipSuccess)
+        if ((e = launch_render_bwd(cam, ranges, point_list, geo, final_T, n_contrib, dL_dout_color, colors2,
+                                   dL_dout_color2, inst, stream)) != hipSuccess)
             return hip_fail(e, "render backward");
     }
+    out.dcolors2 = dcolors2;
     {
         StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
         if ((e = launch_gauss_bwd(cam, g, geo, radii, inst, out, stream)) != hipSuccess)
@@ -466,6 +477,37 @@ int gsr_selftest_reduce9(const float* in_dev, float* out_dev, void* stream) {
     hipError_t e = launch_selftest_reduce9(in_dev, out_dev, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "selftest");
     return GSR_OK;
+}
+
+int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, float* out_color, float* out_depth,
+                int* radii, gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
+    return forward_impl(settings, gaussians, nullptr, out_color, nullptr, out_depth, radii, alloc, alloc_ctx, stream);
+}
+
+int gsr_forward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
+                     float* out_color, float* out_color2, float* out_depth, int* radii, gsr_alloc_fn alloc,
+                     void* alloc_ctx, void* stream) {
+    if (!colors2) return fail(GSR_ERR_INVALID_ARG, "colors2 required");
+    return forward_impl(settings, gaussians, colors2, out_color, out_color2, out_depth, radii, alloc, alloc_ctx,
+                        stream);
+}
+
+int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
+                 const float* dL_dout_color, int num_rendered, const void* geom_buffer, const void* binning_buffer,
+                 const void* image_buffer, int power, const gsr_grads* grads, gsr_alloc_fn alloc, void* alloc_ctx,
+                 void* stream) {
+    return backward_impl(settings, gaussians, radii, dL_dout_color, nullptr, nullptr, num_rendered, geom_buffer,
+                         binning_buffer, image_buffer, power, grads, nullptr, alloc, alloc_ctx, stream);
+}
+
+int gsr_backward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
+                      const float* colors2, const float* dL_dout_color, const float* dL_dout_color2,
+                      int num_rendered, const void* geom_buffer, const void* binning_buffer,
+                      const void* image_buffer, const gsr_grads* grads, float* dcolors2, gsr_alloc_fn alloc,
+                      void* alloc_ctx, void* stream) {
+    if (!colors2) return fail(GSR_ERR_INVALID_ARG, "colors2 required");
+    return backward_impl(settings, gaussians, radii, dL_dout_color, colors2, dL_dout_color2, num_rendered,
+                         geom_buffer, binning_buffer, image_buffer, 1, grads, dcolors2, alloc, alloc_ctx, stream);
 }
 
 }  // extern "C"

@@ -534,12 +534,12 @@ hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* his
 hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t* point_list, uint32_t n,
                              hipStream_t s);
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
-                             const float* colors, float* final_T, uint32_t* n_contrib, float* out_color,
-                             float* out_depth, SpecGuard guard, hipStream_t s);
+                             const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
+                             float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* vis, hipStream_t s);
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
-                             const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, float4* inst,
-                             hipStream_t s);
+                             const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
+                             const float* colors2, const float* dL_dpix2, float4* inst, hipStream_t s);
 struct GradsOut {
     float* dmeans2D;
     float* dcolors;
@@ -549,6 +549,7 @@ struct GradsOut {
     float* dsh;
     float* dscales;
     float* drot;
+    float* dcolors2;  // second colour set of a dual render (nullptr otherwise)
 };
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float4* inst,
                             const GradsOut& out, hipStream_t s);

@@ -514,16 +514,21 @@ hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t
 // entries are independent (ILP), the transmittance chain is then applied in
 // order with predicated (branch-free) updates.  The next batch's global
 // gathers are issued before the current batch is rasterised.
-template <int FWD_GROUP, bool PREFETCH>
+// DUAL: a second colour set (colors2, e.g. SplaTAM's [z, 1, z^2]) is composited
+// in the same pass -- same alpha / T / termination, so each output is bitwise
+// the image a separate call would produce.
+template <int FWD_GROUP, bool PREFETCH, bool DUAL>
 __global__ void __launch_bounds__(TILE_PIX)
 render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                   const float4* __restrict__ rec_a, const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
-                  const float* __restrict__ colors, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
-                  float* __restrict__ out_color, float* __restrict__ out_depth, SpecGuard guard) {
+                  const float* __restrict__ colors2, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
+                  float* __restrict__ out_color, float* __restrict__ out_color2, float* __restrict__ out_depth,
+                  SpecGuard guard) {
     if (guard.overflow()) return;
     __shared__ float4 s_a[RENDER_BATCH];
     __shared__ float4 s_b[RENDER_BATCH];
     __shared__ float4 s_c[RENDER_BATCH];
+    __shared__ float4 s_d[DUAL ? RENDER_BATCH : 1];
     __shared__ uint8_t s_mask[RENDER_BATCH];
     __shared__ __attribute__((aligned(16))) uint16_t s_list[4][RENDER_BATCH + 4];
     const int tid = threadIdx.x, w = tid >> 6;
@@ -536,11 +541,13 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     const uint2 range = ranges[tile];
     bool done = !inside;
     float T = 1.f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 15.0f;  // forward.cu:308 median-depth default
+    float C3 = 0.f, C4 = 0.f, C5 = 0.f;
     uint32_t last = 0;
-    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa;
+    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
     if (range.x + tid < range.y) {
         const uint32_t gi = point_list[range.x + tid];
         pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
+        if (DUAL) pd = make_float4(colors2[3 * gi], colors2[3 * gi + 1], colors2[3 * gi + 2], 0.f);
     }
     for (uint32_t start = range.x; start < range.y; start += RENDER_BATCH) {
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
@@ -549,6 +556,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             s_a[tid] = stage_a(pa);
             s_b[tid] = stage_b(pb);
             s_c[tid] = pc;
+            if (DUAL) s_d[tid] = pd;
             s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
         }
         __syncthreads();
@@ -557,6 +565,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             if (k < range.y) {
                 const uint32_t gi = point_list[k];
                 pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
+                if (DUAL) pd = make_float4(colors2[3 * gi], colors2[3 * gi + 1], colors2[3 * gi + 2], 0.f);
             }
         }
         const int n = build_strip_list(s_mask, cnt, w, 0, s_list[w]);
@@ -572,9 +581,12 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             } else {
                 load_group<FWD_GROUP>(s_list[w], i, n, s_a, s_b, cur);
             }
-            float4 c[FWD_GROUP];
+            float4 c[FWD_GROUP], d[FWD_GROUP];
 #pragma unroll
-            for (int k = 0; k < FWD_GROUP; k++) c[k] = s_c[cur.j[k]];
+            for (int k = 0; k < FWD_GROUP; k++) {
+                c[k] = s_c[cur.j[k]];
+                if (DUAL) d[k] = s_d[cur.j[k]];
+            }
             float power[FWD_GROUP], alpha[FWD_GROUP];
 #pragma unroll
             for (int k = 0; k < FWD_GROUP; k++) {
@@ -593,6 +605,11 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                     C0 += c[k].x * alpha[k] * T;
                     C1 += c[k].y * alpha[k] * T;
                     C2 += c[k].z * alpha[k] * T;
+                    if (DUAL) {
+                        C3 += d[k].x * alpha[k] * T;
+                        C4 += d[k].y * alpha[k] * T;
+                        C5 += d[k].z * alpha[k] * T;
+                    }
                     if (T > 0.5f && test_T < 0.5f) D = cur.b[k].z;  // median depth (forward.cu:368-372)
                     T = test_T;
                     last = pos0 + (uint32_t)cur.j[k] + 1u;            // entries visited up to the last blend
@@ -610,22 +627,28 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         out_color[HW + pid] = C1 + T * cam.bg[1];
         out_color[2 * HW + pid] = C2 + T * cam.bg[2];
         out_depth[pid] = D;
+        if (DUAL) {
+            out_color2[pid] = C3 + T * cam.bg[0];
+            out_color2[HW + pid] = C4 + T * cam.bg[1];
+            out_color2[2 * HW + pid] = C5 + T * cam.bg[2];
+        }
     }
 }
 
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
-                             const float* colors, float* final_T, uint32_t* n_contrib, float* out_color,
-                             float* out_depth, SpecGuard guard, hipStream_t s) {
+                             const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
+                             float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s) {
     // GSR_FWD_VARIANT (tuning only): 0 = 4-entry groups, 1 = 4 + prefetch, 2 = 2-entry groups + prefetch
     static const int variant = [] {
         const char* e = getenv("GSR_FWD_VARIANT");
         return e ? atoi(e) : 0;
     }();
-    auto k = render_fwd_kernel<4, false>;
-    if (variant == 1) k = render_fwd_kernel<4, true>;
-    if (variant == 2) k = render_fwd_kernel<2, true>;
+    auto k = render_fwd_kernel<4, false, false>;
+    if (variant == 1) k = render_fwd_kernel<4, true, false>;
+    if (variant == 2) k = render_fwd_kernel<2, true, false>;
+    if (colors2) k = render_fwd_kernel<4, false, true>;
     hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rec_a, geo.rec_b,
-                       geo.rec_c, colors, final_T, n_contrib, out_color, out_depth, guard);
+                       geo.rec_c, colors2, final_T, n_contrib, out_color, out_color2, out_depth, guard);
     return hipGetLastError();
 }
 

@@ -71,6 +71,55 @@ class _RasterizeGaussians(torch.autograd.Function):
                 grad_cov3Ds_precomp, None, None)
 
 
+def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations,
+                             cov3Ds_precomp, raster_settings):
+    """Two GaussianRasterizer calls on identical geometry fused into one
+    rasterization: SplaTAM renders RGB and the [z, 1, z^2]
+    depth/silhouette image from the same means / scales / rotations / opacities
+    and camera (scripts/splatam.py:255,259).  Returns (color, color2, radii,
+    depth); each image is bitwise what a separate call returns, and the gradients
+    of the shared inputs are the sums over both images, as autograd would
+    accumulate them over two calls (means2D receives that sum as well)."""
+    empty = torch.Tensor([])
+    return _RasterizeGaussiansDual.apply(means3D, means2D, empty if sh is None else sh,
+                                         empty if colors_precomp is None else colors_precomp, colors2, opacities,
+                                         empty if scales is None else scales,
+                                         empty if rotations is None else rotations,
+                                         empty if cov3Ds_precomp is None else cov3Ds_precomp, raster_settings)
+
+
+class _RasterizeGaussiansDual(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations, cov3Ds_precomp,
+                raster_settings):
+        s = raster_settings
+        num_rendered, color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth = _C.rasterize_gaussians_dual(
+            s.bg, means3D, colors_precomp, colors2, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
+            s.campos, s.prefiltered)
+        ctx.raster_settings = s
+        ctx.num_rendered = num_rendered
+        ctx.save_for_backward(colors_precomp, colors2, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
+                              geomBuffer, binningBuffer, imgBuffer)
+        ctx.mark_non_differentiable(radii, depth)
+        return color, color2, radii, depth
+
+    @staticmethod
+    def backward(ctx, grad_color, grad_color2, _grad_radii, _grad_depth):
+        s = ctx.raster_settings
+        (colors_precomp, colors2, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer,
+         imgBuffer) = ctx.saved_tensors
+        if grad_color is None:
+            grad_color = torch.zeros(3, s.image_height, s.image_width, device=means3D.device)
+        if grad_color2 is None:
+            grad_color2 = torch.zeros(3, s.image_height, s.image_width, device=means3D.device)
+        (g_m2, g_col, g_col2, g_op, g_m3, g_cov, g_sh, g_sc, g_rot) = _C.rasterize_gaussians_dual_backward(
+            s.bg, means3D, radii, colors_precomp, colors2, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_color, grad_color2, sh, s.sh_degree, s.campos,
+            geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer)
+        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None
+
+
 class GaussianRasterizer(nn.Module):
     """__init__.py:153-204.  ``backward_power`` is the fork's Fisher knob (1 = standard gradients)."""
 

@@ -16,7 +16,7 @@ from dataclasses import dataclass
 import torch
 import torch.nn.functional as F
 
-from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer, rasterize_gaussians_dual
 from .scenes import Scene
 
 
@@ -132,34 +132,39 @@ def fused_eligible(params, curr_data, cfg: TrackingConfig) -> bool:
             and curr_data["im"].dim() == 3 and curr_data["depth"].dim() == 3)
 
 
-def _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg: TrackingConfig):
+def _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg: TrackingConfig, dual=True):
     from .glue import track_transform, tracking_l1
     means, rots, dcol, opac, scales = track_transform(params, iter_time_idx, curr_data["w2c"])
     P = means.shape[0]
     means2D = torch.zeros(P, 3, device=means.device, requires_grad=True)
-    means2D_ds = torch.zeros(P, 3, device=means.device, requires_grad=True)
-    ras = GaussianRasterizer(raster_settings=curr_data["cam"])
-    im, radius, _ = ras(means3D=means, means2D=means2D, colors_precomp=params["rgb_colors"], opacities=opac,
-                        scales=scales, rotations=rots)
-    depth_sil, _, _ = ras(means3D=means, means2D=means2D_ds, colors_precomp=dcol, opacities=opac, scales=scales,
-                          rotations=rots)
+    if dual:  # both renders in one rasterization (means2D.grad then holds the sum over both images)
+        im, depth_sil, radius, _ = rasterize_gaussians_dual(means, means2D, None, params["rgb_colors"], dcol, opac,
+                                                            scales, rots, None, curr_data["cam"])
+    else:
+        means2D_ds = torch.zeros(P, 3, device=means.device, requires_grad=True)
+        ras = GaussianRasterizer(raster_settings=curr_data["cam"])
+        im, radius, _ = ras(means3D=means, means2D=means2D, colors_precomp=params["rgb_colors"], opacities=opac,
+                            scales=scales, rotations=rots)
+        depth_sil, _, _ = ras(means3D=means, means2D=means2D_ds, colors_precomp=dcol, opacities=opac, scales=scales,
+                              rotations=rots)
     loss = tracking_l1(im, depth_sil, curr_data["im"], curr_data["depth"], cfg.sil_thres, cfg.w_im, cfg.w_depth)
     return loss, radius, means2D
 
 
 def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = TrackingConfig(), fast=True,
-                      fused=True):
+                      fused=True, dual=True):
     """scripts/splatam.py:220-353 with tracking=True: two renders (RGB, [z,1,z^2]), masked L1 sums.
 
     fused=True (and fused_eligible): the pose transform / rendervar builders and
-    the masked L1 loss run as the HIP glue kernels of include/gsr_glue.h.
+    the masked L1 loss run as the HIP glue kernels of include/gsr_glue.h, and with
+    dual=True the two renders share one rasterization (gsr_forward_dual).
     fast=True evaluates the same loss without host synchronisation: boolean-mask
     indexing `x[mask].sum()` becomes `where(mask, x, 0).sum()` (same value and
     gradient, NaNs outside the mask excluded exactly as indexing excludes them),
     and the pose transform avoids the K=P GEMM (see _affine).  fast=False is the
     literal statement of the reference code."""
     if fused and fast and fused_eligible(params, curr_data, cfg):
-        return _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg)
+        return _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg, dual=dual)
     tg = transform_to_frame(params, iter_time_idx, gaussians_grad=False, camera_grad=True, fast=fast)
     rendervar = transformed_params2rendervar(params, tg)
     depth_sil_rendervar = transformed_params2depthplussilhouette(params, curr_data["w2c"], tg, fast=fast)
