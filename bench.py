@@ -4,7 +4,9 @@ BASELINE.json metric "rasterize fwd+bwd frames/sec @640x480, 300k Gaussians;
 HBM GB/s vs peak" on config 3: 300k isotropic Gaussians, 640x480, full
 tracking-iteration loss (scripts/splatam.py:220-353 with tracking=True).
 One step = one frame = RGB render fwd+bwd + depth/silhouette ([z,1,z^2])
-render fwd+bwd + masked L1 loss + Adam step on the camera pose.
+render fwd+bwd + masked L1 loss + Adam step on the camera pose.  The two renders
+share one dual rasterization (gsr_forward_dual) and the glue runs as the fused
+HIP kernels of include/gsr_glue.h (splatam_amd/slam.py get_loss_tracking).
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 one process per GPU; every rank tracks its own frame against the same
@@ -13,8 +15,9 @@ Gaussian set over RCCL every --bcast-every steps (inside the timed region).
 `value` = frames processed by all ranks / max-over-ranks wall time.
 
 The JSON line carries:
-  roofline      -- render-backward kernel: SURVEY.md 8(d) algorithmic bytes per
-                   launch (8*Tt + 40*I + 20*N + 44*P, measured I) over its
+  roofline      -- render-backward kernel (one dual launch per frame): SURVEY.md
+                   8(d) algorithmic bytes per launch extended to both colour sets
+                   (8*Tt + 52*I + 32*N + 56*P, measured I) over its
                    average duration from hipEvents recorded around that kernel
                    on its launch stream during the timed region;
   cpu_baseline  -- rank 0 at N=1 only: the float32 C oracle (oracle/) on one
@@ -140,7 +143,9 @@ def main():
     Tt = ((W + 15) // 16) * ((H + 15) // 16)
     N = W * H
     I_avg = rb["units"] / max(rb["launches"], 1)
-    bytes_per_launch = 8 * Tt + 40 * I_avg + 20 * N + 44 * P
+    # SURVEY.md 8(d) per-rasterization bytes 8*Tt + 40*I + 20*N + 44*P, for the dual launch
+    # (both colour sets): + colors2 gather 12*I, + dL_dpix2 12*N, + dcolors2 12*P
+    bytes_per_launch = 8 * Tt + 52 * I_avg + 32 * N + 56 * P
     dur_s = rb["avg_us"] * 1e-6
     achieved = bytes_per_launch / dur_s / 1e9 if dur_s > 0 else 0.0
     traffic = None
@@ -184,7 +189,9 @@ def main():
                          f"({P} Gaussians, {W}x{H}) through oracle/gsr_oracle.c float32, 1 thread, "
                          f"{t_cpu:.1f} s"}
         # VALU view of the same kernel: F_eval=12 per evaluated pair, +45 per contributing pair
-        flops = 12 * evals / 2 + 45 * contrib / 2
+        # for one colour set, +9 for the second set of the dual launch (dot product, 3 products, 3 sums);
+        # one dual launch evaluates each pair once for both renders (the oracle counts both renders)
+        flops = 12 * evals / 2 + 54 * contrib / 2
         roofline["valu"] = {"achieved_tflops": round(flops / dur_s / 1e12, 3) if dur_s > 0 else None,
                             "peak_tflops": VALU_PEAK_TFLOPS,
                             "frac": round(flops / dur_s / 1e12 / VALU_PEAK_TFLOPS, 4) if dur_s > 0 else None,

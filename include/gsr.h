@@ -79,8 +79,9 @@ typedef struct gsr_gaussians {
     const float* cov3D_precomp; /* [P,6]   or NULL */
 } gsr_gaussians;
 
-/* Output of rasterize_gaussians_backward (rasterize_points.cu:195), all
- * written in full by gsr_backward (no zero-initialisation needed). */
+/* Output of rasterize_gaussians_backward (rasterize_points.cu:195), each
+ * written in full by gsr_backward (no zero-initialisation needed); with
+ * power == 1 a NULL pointer (other than dmeans3D) skips that gradient. */
 typedef struct gsr_grads {
     float* dmeans2D;    /* [P,3] (z component 0) */
     float* dcolors;     /* [P,3] */
@@ -107,7 +108,10 @@ int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians,
  * backward_power (backward.cu:1093-1137): gradients are summed over
  * (pixel, Gaussian) pairs of powf(per-pair gradient, power); power == 1 is the
  * standard 3DGS backward.  H/W come from settings (the reference reads them
- * from dL_dout_color).  Returns GSR_OK or a negative error code. */
+ * from dL_dout_color).  With power == 1 every gradient pointer except
+ * dmeans3D may be NULL: that gradient is skipped, and render_bwd does not form
+ * the per-pair sums only it needs (dopacity, dcolors without SH).  Returns
+ * GSR_OK or a negative error code. */
 int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians,
                  const int* radii, const float* dL_dout_color, int num_rendered,
                  const void* geom_buffer, const void* binning_buffer, const void* image_buffer,
@@ -127,7 +131,7 @@ int gsr_forward_dual(const gsr_settings* settings, const gsr_gaussians* gaussian
 /* Backward of gsr_forward_dual (power 1): every geometric gradient in `grads`
  * is the sum of the two renders' (as autograd would accumulate it over two
  * calls), grads->dcolors is d/dcolors of the first set and dcolors2 [P,3]
- * that of colors2. */
+ * that of colors2 (NULL skips it, as for the pointers in `grads`). */
 int gsr_backward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians,
                       const int* radii, const float* colors2, const float* dL_dout_color,
                       const float* dL_dout_color2, int num_rendered, const void* geom_buffer,

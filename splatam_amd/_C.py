@@ -198,17 +198,23 @@ def rasterize_gaussians_dual(background, means3D, colors, colors2, opacity, scal
 
 def rasterize_gaussians_dual_backward(background, means3D, radii, colors, colors2, scales, rotations, scale_modifier,
                                       cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
-                                      dL_dout_color2, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer):
+                                      dL_dout_color2, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
+                                      needs=None):
     """gsr_backward_dual.  Returns (dmeans2D, dcolors, dcolors2, dopacity, dmeans3D, dcov3D, dsh, dscales,
-    drotations); geometric gradients are the sums over both colour sets."""
+    drotations); geometric gradients are the sums over both colour sets.  `needs` (9 bools in that
+    order, default all) skips the gradients nobody wants: they come back as None and the kernels do
+    not form their per-pair sums."""
     device = means3D.device
     P = means3D.size(0)
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     M = sh.size(1) if (sh is not None and sh.numel() > 0 and sh.size(0) != 0) else 0
     f32 = dict(dtype=torch.float32, device=device)
-    out = [torch.empty(P, 3, **f32), torch.empty(P, 3, **f32), torch.empty(P, 1, **f32), torch.empty(P, 3, **f32),
-           torch.empty(P, 6, **f32), torch.empty(P, M, 3, **f32), torch.empty(P, 3, **f32), torch.empty(P, 4, **f32)]
-    dcolors2 = torch.empty(P, 3, **f32)
+    needs = [True] * 9 if needs is None else list(needs)
+    needs[4] = True  # dmeans3D is always produced
+    shapes = [(P, 3), (P, 3), (P, 3), (P, 1), (P, 3), (P, 6), (P, M, 3), (P, 3), (P, 4)]
+    res = [torch.empty(*sh_, **f32) if nd else None for sh_, nd in zip(shapes, needs)]
+    out = [res[0], res[1], res[3], res[4], res[5], res[6], res[7], res[8]]
+    dcolors2 = res[2]
     if P == 0:
         return (out[0], out[1], dcolors2, *out[2:])
     with torch.cuda.device(device):
@@ -219,12 +225,13 @@ def rasterize_gaussians_dual_backward(background, means3D, radii, colors, colors
         dpix = _dev_f32(dL_dout_color, device, "dL_dout_color")
         dpix2 = _dev_f32(dL_dout_color2, device, "dL_dout_color2")
         radii_c = radii.to(device=device, dtype=torch.int32).contiguous()
-        grads = GsrGrads(*[o.data_ptr() if o.numel() > 0 else None for o in out])
+        grads = GsrGrads(*[o.data_ptr() if (o is not None and o.numel() > 0) else None for o in out])
         _begin(device)
         rc = lib.gsr_backward_dual(ctypes.byref(s), ctypes.byref(g), radii_c.data_ptr(), _ptr(c2), dpix.data_ptr(),
                                    dpix2.data_ptr(), int(R), geomBuffer.data_ptr(),
                                    binningBuffer.data_ptr() if binningBuffer.numel() else None,
-                                   imageBuffer.data_ptr(), ctypes.byref(grads), dcolors2.data_ptr(), _ALLOC_CB, None,
+                                   imageBuffer.data_ptr(), ctypes.byref(grads),
+                                   dcolors2.data_ptr() if dcolors2 is not None else None, _ALLOC_CB, None,
                                    _stream(device))
         _check(rc, "rasterize_gaussians_dual_backward")
         _tls.buffers = {}

@@ -23,8 +23,11 @@ constexpr int BWD_BATCH = 128;
 
 // DUAL: the pass also carries a second colour set (colors2, dL_dpix2) composited
 // with the same alpha / T (one dual forward): the per-pair dL/dalpha is the sum
-// of both renders' and each record holds 12 sums (the 9 below + dch * dL_dpix2).
-template <int BWD_GROUP, bool PREFETCH, bool DUAL>
+// of both renders'.  OPAC / COL1 / COL2: whether dL/dopacity, dL/dcolors and
+// dL/dcolors2 are wanted; absent ones are neither formed nor reduced (tracking
+// needs only the geometric sums and the depth colours).  Records always use the
+// fixed 12-slot layout [hx, hy, hxx, hxy, hyy | G dL/dalpha | dch dp(3) | dch dq(3)].
+template <int BWD_GROUP, bool PREFETCH, bool DUAL, bool OPAC = true, bool COL1 = true, bool COL2 = DUAL>
 __global__ void __launch_bounds__(TILE_PIX)
 render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                   const uint2* __restrict__ rect, const uint32_t* __restrict__ offsets,
@@ -32,7 +35,10 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                   const float* __restrict__ final_T, const uint32_t* __restrict__ n_contrib,
                   const float* __restrict__ dL_dpix, const float* __restrict__ colors2,
                   const float* __restrict__ dL_dpix2, float4* __restrict__ inst) {
-    constexpr int NV = DUAL ? 12 : 9;
+    static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
+    static_assert(BWD_GROUP == 4 || (OPAC && COL1), "2-entry groups only for the full value set");
+    constexpr int NV = 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? 3 : 0);
+    constexpr int O_OP = 5, O_C1 = 5 + (OPAC ? 1 : 0), O_C2 = O_C1 + (COL1 ? 3 : 0);
     __shared__ float4 s_a[BWD_BATCH];
     __shared__ float4 s_b[BWD_BATCH];
     __shared__ float4 s_c[BWD_BATCH];
@@ -179,14 +185,16 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 vk[2] = hx * dx[k];
                 vk[3] = hx * dy[k];
                 vk[4] = hy * dy[k];
-                vk[5] = G[k] * dL_dalpha;
-                vk[6] = dch * dp0;
-                vk[7] = dch * dp1;
-                vk[8] = dch * dp2;
-                if (DUAL) {
-                    vk[9] = dch * dq0;
-                    vk[10] = dch * dq1;
-                    vk[11] = dch * dq2;
+                if (OPAC) vk[O_OP] = G[k] * dL_dalpha;
+                if (COL1) {
+                    vk[O_C1] = dch * dp0;
+                    vk[O_C1 + 1] = dch * dp1;
+                    vk[O_C1 + 2] = dch * dp2;
+                }
+                if (COL2) {
+                    vk[O_C2] = dch * dq0;
+                    vk[O_C2 + 1] = dch * dq1;
+                    vk[O_C2 + 2] = dch * dq2;
                 }
                 if (o_) {
                     T = Tn;
@@ -203,15 +211,6 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
 #pragma unroll
                     for (int m = 0; m < NV; m++) dst[m] = r[m];
                 }
-            } else if constexpr (DUAL) {
-                float r[6];
-                wave_reduce_n<24>(v, r);  // row rho: item rho >> 1, values 6 * (rho & 1) + m
-                const int item = row >> 1, half = row & 1;
-                if ((lane & 15) == 0 && i + item < n) {
-                    float* dst = s_acc + (w * BWD_BATCH + j[item]) * NV + 6 * half;
-#pragma unroll
-                    for (int m = 0; m < 6; m++) dst[m] = r[m];
-                }
             } else {
                 float r[5];
                 wave_reduce2x9(v, r);
@@ -226,12 +225,20 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         }
         __syncthreads();
         if (tid < cnt) {
+            float c[NV];
+#pragma unroll
+            for (int m = 0; m < NV; m++)
+                c[m] = s_acc[(0 * BWD_BATCH + tid) * NV + m] + s_acc[(1 * BWD_BATCH + tid) * NV + m] +
+                       s_acc[(2 * BWD_BATCH + tid) * NV + m] + s_acc[(3 * BWD_BATCH + tid) * NV + m];
             float sum[12];
 #pragma unroll
-            for (int m = 0; m < 12; m++)
-                sum[m] = m < NV ? s_acc[(0 * BWD_BATCH + tid) * NV + m] + s_acc[(1 * BWD_BATCH + tid) * NV + m] +
-                                      s_acc[(2 * BWD_BATCH + tid) * NV + m] + s_acc[(3 * BWD_BATCH + tid) * NV + m]
-                                : 0.f;
+            for (int m = 0; m < 5; m++) sum[m] = c[m];
+            sum[5] = OPAC ? c[O_OP] : 0.f;
+#pragma unroll
+            for (int m = 0; m < 3; m++) {
+                sum[6 + m] = COL1 ? c[O_C1 + m] : 0.f;
+                sum[9 + m] = COL2 ? c[O_C2 + m] : 0.f;
+            }
             const uint32_t u = s_u[tid];
             inst[3 * u] = make_float4(sum[0], sum[1], sum[2], sum[3]);
             inst[3 * u + 1] = make_float4(sum[4], sum[5], sum[6], sum[7]);
@@ -241,19 +248,33 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     }
 }
 
+template <bool OPAC, bool COL1, bool COL2>
+static auto dual_variant() { return render_bwd_kernel<4, false, true, OPAC, COL1, COL2>; }
+
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
-                             const float* colors2, const float* dL_dpix2, float4* inst, hipStream_t s) {
+                             const float* colors2, const float* dL_dpix2, unsigned need, float4* inst,
+                             hipStream_t s) {
     // GSR_BWD_VARIANT (tuning only): 1 = 4-entry groups (default), 0 = 4 + prefetch, 2 = 2 + prefetch, 3 = 2
     static const int variant = [] {
         const char* e = getenv("GSR_BWD_VARIANT");
         return e ? atoi(e) : 1;
     }();
+    const bool op = need & NEED_OPACITY, c1 = need & NEED_COLORS, c2 = need & NEED_COLORS2;
     auto k = render_bwd_kernel<4, false, false>;
-    if (variant == 0) k = render_bwd_kernel<4, true, false>;
-    if (variant == 2) k = render_bwd_kernel<2, true, false>;
-    if (variant == 3) k = render_bwd_kernel<2, false, false>;
-    if (colors2) k = (variant == 3) ? render_bwd_kernel<2, false, true> : render_bwd_kernel<4, false, true>;
+    if (!colors2) {
+        if (variant == 0) k = render_bwd_kernel<4, true, false>;
+        if (variant == 2) k = render_bwd_kernel<2, true, false>;
+        if (variant == 3) k = render_bwd_kernel<2, false, false>;
+        if (!op || !c1) k = op ? render_bwd_kernel<4, false, false, true, false> :
+                            (c1 ? render_bwd_kernel<4, false, false, false, true> :
+                                  render_bwd_kernel<4, false, false, false, false>);
+    } else {
+        k = op ? (c1 ? (c2 ? dual_variant<1, 1, 1>() : dual_variant<1, 1, 0>())
+                     : (c2 ? dual_variant<1, 0, 1>() : dual_variant<1, 0, 0>()))
+               : (c1 ? (c2 ? dual_variant<0, 1, 1>() : dual_variant<0, 1, 0>())
+                     : (c2 ? dual_variant<0, 0, 1>() : dual_variant<0, 0, 0>()));
+    }
     hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rect, geo.offsets,
                        geo.rec_a, geo.rec_b, geo.rec_c, final_T, n_contrib, dL_dpix, colors2, dL_dpix2, inst);
     return hipGetLastError();
@@ -296,13 +317,17 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         const unsigned clamped = __float_as_uint(geo.rec_c[i].w);
         gauss_chain(cam, g, i, g2, clamped, dmean, dcov, dscale, drot, dsh, nsh);
     }
-    out.dmeans2D[3 * i] = g2[0];
-    out.dmeans2D[3 * i + 1] = g2[1];
-    out.dmeans2D[3 * i + 2] = 0.f;
-    out.dcolors[3 * i] = g2[6];
-    out.dcolors[3 * i + 1] = g2[7];
-    out.dcolors[3 * i + 2] = g2[8];
-    out.dopacity[i] = g2[5];
+    if (out.dmeans2D) {
+        out.dmeans2D[3 * i] = g2[0];
+        out.dmeans2D[3 * i + 1] = g2[1];
+        out.dmeans2D[3 * i + 2] = 0.f;
+    }
+    if (out.dcolors) {
+        out.dcolors[3 * i] = g2[6];
+        out.dcolors[3 * i + 1] = g2[7];
+        out.dcolors[3 * i + 2] = g2[8];
+    }
+    if (out.dopacity) out.dopacity[i] = g2[5];
     if (out.dcolors2) {
         out.dcolors2[3 * i] = dcol2[0];
         out.dcolors2[3 * i + 1] = dcol2[1];
@@ -310,12 +335,15 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     }
 #pragma unroll
     for (int k = 0; k < 3; k++) out.dmeans3D[3 * i + k] = dmean[k];
+    if (out.dcov3D)
 #pragma unroll
-    for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = dcov[k];
+        for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = dcov[k];
+    if (out.dscales)
 #pragma unroll
-    for (int k = 0; k < 3; k++) out.dscales[3 * i + k] = dscale[k];
+        for (int k = 0; k < 3; k++) out.dscales[3 * i + k] = dscale[k];
+    if (out.drot)
 #pragma unroll
-    for (int k = 0; k < 4; k++) out.drot[4 * i + k] = drot[k];
+        for (int k = 0; k < 4; k++) out.drot[4 * i + k] = drot[k];
     if (out.dsh && g.M > 0) {
         float* d = out.dsh + (size_t)3 * g.M * i;
 #pragma unroll

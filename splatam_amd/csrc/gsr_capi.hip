@@ -365,8 +365,7 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
                          gsr_alloc_fn alloc, void* alloc_ctx, void* stream_) {
     int rc = validate(settings, gaussians, false);
     if (rc != GSR_OK) return rc;
-    if (colors2 && (!dL_dout_color2 || !dcolors2))
-        return fail(GSR_ERR_INVALID_ARG, "dual backward needs dL_dout_color2 and dcolors2");
+    if (colors2 && !dL_dout_color2) return fail(GSR_ERR_INVALID_ARG, "dual backward needs dL_dout_color2");
     if (colors2 && power != 1) return fail(GSR_ERR_INVALID_ARG, "dual render supports backward_power == 1 only");
     if (!grads) return fail(GSR_ERR_INVALID_ARG, "grads required");
     if (num_rendered < 0) return fail(GSR_ERR_INVALID_ARG, "num_rendered must be >= 0");
@@ -388,9 +387,10 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     hipError_t e;
     GradsOut out{grads->dmeans2D, grads->dcolors, grads->dopacity, grads->dmeans3D,
                  grads->dcov3D,   grads->dsh,     grads->dscales,  grads->drotations};
-    if (!out.dmeans2D || !out.dcolors || !out.dopacity || !out.dmeans3D || !out.dcov3D || !out.dscales || !out.drot)
-        return fail(GSR_ERR_INVALID_ARG, "gradient output pointers required");
+    if (!out.dmeans3D) return fail(GSR_ERR_INVALID_ARG, "dmeans3D output pointer required");
     if (power != 1) {
+        if (!out.dmeans2D || !out.dcolors || !out.dopacity || !out.dcov3D || !out.dscales || !out.drot)
+            return fail(GSR_ERR_INVALID_ARG, "backward_power != 1 needs every gradient output pointer");
         // per-pair powf before summation (renderCUDAFused, backward.cu:850-1140): gsr_backward_power.hip
         const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
         const int nvp = power_record_floats(nsh);
@@ -429,8 +429,11 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
         const char* bb = (const char*)binning_buffer;
         const uint32_t* point_list = (const uint32_t*)(bb + BL.point_list);
         StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream);
+        // SH colours feed dL/dmeans3D through the view direction, so their sums are needed with SH
+        const unsigned need = (out.dopacity ? NEED_OPACITY : 0u) | ((out.dcolors || g.shs) ? NEED_COLORS : 0u) |
+                              (dcolors2 ? NEED_COLORS2 : 0u);
         if ((e = launch_render_bwd(cam, ranges, point_list, geo, final_T, n_contrib, dL_dout_color, colors2,
-                                   dL_dout_color2, inst, stream)) != hipSuccess)
+                                   dL_dout_color2, need, inst, stream)) != hipSuccess)
             return hip_fail(e, "render backward");
     }
     out.dcolors2 = dcolors2;

@@ -539,7 +539,10 @@ hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint3
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* vis, hipStream_t s);
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
-                             const float* colors2, const float* dL_dpix2, float4* inst, hipStream_t s);
+                             const float* colors2, const float* dL_dpix2, unsigned need, float4* inst,
+                             hipStream_t s);
+// which optional per-pair sums render_bwd forms (the geometric ones always)
+constexpr unsigned NEED_OPACITY = 1u, NEED_COLORS = 2u, NEED_COLORS2 = 4u;
 struct GradsOut {
     float* dmeans2D;
     float* dcolors;

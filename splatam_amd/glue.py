@@ -64,6 +64,8 @@ class _TrackTransform(torch.autograd.Function):
                                          _stream(means_world))
         _check(rc, "track_transform_fwd")
         ctx.mark_non_differentiable(opac, scales)
+        if scols == 1:
+            ctx.mark_non_differentiable(rot)  # isotropic maps: rotations do not depend on the pose
         ctx.save_for_backward(cam_rots, cam_trans, means_world, unnorm_rot, means_cam, w2c)
         ctx.meta = (t, T, scols)
         return means_cam, rot, dcol, opac, scales

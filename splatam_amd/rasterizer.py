@@ -113,10 +113,14 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
             grad_color = torch.zeros(3, s.image_height, s.image_width, device=means3D.device)
         if grad_color2 is None:
             grad_color2 = torch.zeros(3, s.image_height, s.image_width, device=means3D.device)
+        n = ctx.needs_input_grad  # (means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations, cov3D)
+        needs = (n[1], n[3], n[4], n[5], n[0], n[8], n[2], n[6], n[7])
         (g_m2, g_col, g_col2, g_op, g_m3, g_cov, g_sh, g_sc, g_rot) = _C.rasterize_gaussians_dual_backward(
             s.bg, means3D, radii, colors_precomp, colors2, scales, rotations, s.scale_modifier, cov3Ds_precomp,
             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_color, grad_color2, sh, s.sh_degree, s.campos,
-            geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer)
+            geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, needs=needs)
+        if not n[0]:
+            g_m3 = None
         return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None
 
 

@@ -220,3 +220,30 @@ def test_dual_render_matches_two_calls_and_oracle(cuda, aniso):
     for k, v in got.items():
         ref = ra[k].reshape(v.shape) + rb[k].reshape(v.shape)
         assert harness.rel_l2(v.detach().cpu().numpy(), ref) <= 1e-4, k
+
+
+def test_dual_render_skips_unneeded_gradients(cuda):
+    """Only means3D and colors2 require grad (SplaTAM tracking): the lean
+    backward variant gives bitwise the full variant's gradients for them."""
+    from splatam_amd.rasterizer import GaussianRasterizationSettings, rasterize_gaussians_dual
+    scene = make_scene(3000, 128, 96, seed=29, anisotropic=True)
+    c = scene.cam
+    st = GaussianRasterizationSettings(96, 128, c.tanfovx, c.tanfovy, torch.zeros(3, device=cuda), 1.0,
+                                       c.viewmatrix.to(cuda), c.projmatrix.to(cuda), 0, c.campos.to(cuda), False)
+    rs = np.random.RandomState(8)
+    g1 = torch.as_tensor(rs.randn(3, 96, 128).astype(np.float32), device=cuda)
+    g2 = torch.as_tensor(rs.randn(3, 96, 128).astype(np.float32), device=cuda)
+    z = scene.means3D[:, 2:3]
+    c2 = torch.cat([z, torch.ones_like(z), z * z], 1)
+    res = []
+    for lean in (False, True):
+        t = lambda x, rg: x.detach().to(cuda).clone().requires_grad_(rg)  # noqa: E731
+        m3, col2 = t(scene.means3D, True), t(c2, True)
+        op, col, sc, ro = (t(scene.opacities, not lean), t(scene.colors, not lean), t(scene.scales, not lean),
+                           t(scene.rotations, not lean))
+        m2 = torch.zeros_like(m3, requires_grad=not lean)
+        im, im2, _, _ = rasterize_gaussians_dual(m3, m2, None, col, col2, op, sc, ro, None, st)
+        ((im * g1).sum() + (im2 * g2).sum()).backward()
+        res.append((m3.grad.cpu(), col2.grad.cpu(), op.grad))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert res[1][2] is None
