@@ -106,8 +106,9 @@ def main():
     curr = {"cam": cam, "w2c": w2c, "im": im.clone(), "depth": ds[0:1].clone()}
     params["cam_unnorm_rots"].requires_grad_(True)
     params["cam_trans"].requires_grad_(True)
+    # configs/replica/splatam.py:71-80 tracking learning rates; torch's fused (single-kernel) Adam
     opt = torch.optim.Adam([{"params": [params["cam_unnorm_rots"]], "lr": 0.0004},
-                            {"params": [params["cam_trans"]], "lr": 0.002}])  # configs/replica/splatam.py:71-80
+                            {"params": [params["cam_trans"]], "lr": 0.002}], fused=True)
 
     def step():
         opt.zero_grad(set_to_none=True)

@@ -220,16 +220,30 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     const int ntiles = cam.gx * cam.gy;
     uint32_t* cursor = tile_count + (size_t)ntiles * TILE_CTR_STRIDE;
     hipError_t e;
-    if ((e = hipMemsetAsync(tile_count, 0, 8 * (size_t)ntiles * TILE_CTR_STRIDE, stream)) != hipSuccess)
+    // tile counts: per-workgroup LDS histograms + column scan (transient count matrix in SCRATCH),
+    // or global atomics on padded counters when the histogram does not fit in LDS
+    const bool lds_hist = ntiles <= MAX_LDS_TILES;
+    uint32_t* cmat = nullptr;
+    uint32_t* tile_tot = nullptr;
+    if (lds_hist && P > 0) {
+        cmat = (uint32_t*)obtain(alloc, alloc_ctx, GSR_BUF_SCRATCH, 4 * ((size_t)GL.nb * ntiles + ntiles));
+        if (!cmat) return fail(GSR_ERR_ALLOC, "allocator returned NULL (tile count matrix)");
+        tile_tot = cmat + (size_t)GL.nb * ntiles;
+    } else if ((e = hipMemsetAsync(tile_count, 0, 8 * (size_t)ntiles * TILE_CTR_STRIDE, stream)) != hipSuccess) {
         return hip_fail(e, "memset tile counts");
+    }
     if (P > 0) {
         if (!radii) return fail(GSR_ERR_INVALID_ARG, "radii output required");
         if ((e = hipMemsetAsync(geo.counters, 0, 16, stream)) != hipSuccess) return hip_fail(e, "memset counters");
         {
             StageTimer t(GSR_STAGE_PREPROCESS, P, stream);
-            if ((e = launch_preprocess(cam, g, geo, radii, tile_count, GL.nb, stream)) != hipSuccess)
+            if ((e = launch_preprocess(cam, g, geo, radii, lds_hist ? cmat : tile_count, lds_hist, ntiles, GL.nb,
+                                       stream)) != hipSuccess)
                 return hip_fail(e, "preprocess");
-            if ((e = launch_scan_counts(geo, GL.nb, tile_count, ntiles, ranges, stream)) != hipSuccess)
+            if (lds_hist && (e = launch_tile_colscan(cmat, GL.nb, ntiles, tile_tot, stream)) != hipSuccess)
+                return hip_fail(e, "tile count scan");
+            if ((e = launch_scan_counts(geo, GL.nb, lds_hist ? tile_tot : tile_count, lds_hist ? 1 : TILE_CTR_STRIDE,
+                                        ntiles, ranges, stream)) != hipSuccess)
                 return hip_fail(e, "scan");
         }
         if (!g_pinned.p) {
@@ -284,7 +298,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         const SpecGuard guard{geo.counters, cap, (uint32_t)TILE_SORT_CAP};
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
-            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, cursor, keys[0], GL.nb, guard, stream)) != hipSuccess)
+            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, lds_hist ? cmat : cursor, lds_hist, ntiles, keys[0],
+                                             GL.nb, guard, stream)) != hipSuccess)
                 return hip_fail(e, "duplicate");
         }
         {
@@ -322,7 +337,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     if (I > 0 && longest <= (uint32_t)TILE_SORT_CAP && !force_radix) {
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
-            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, cursor, keys[0], GL.nb, none, stream)) != hipSuccess)
+            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, lds_hist ? cmat : cursor, lds_hist, ntiles, keys[0],
+                                             GL.nb, none, stream)) != hipSuccess)
                 return hip_fail(e, "duplicate");
         }
         {

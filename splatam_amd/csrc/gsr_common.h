@@ -17,7 +17,8 @@ namespace gsr {
 constexpr int TILE_X = 16;  // config.h:16-17 (BLOCK_X/BLOCK_Y); parity needs 16x16 tiles
 constexpr int TILE_Y = 16;
 constexpr int TILE_PIX = TILE_X * TILE_Y;
-constexpr int PRE_BLOCK = 256;       // Gaussians per preprocess / duplicate workgroup
+constexpr int PRE_BLOCK = 1024;      // Gaussians per preprocess / duplicate workgroup (one count-matrix row)
+constexpr int MAX_LDS_TILES = 16384; // tile histogram in LDS up to 64 KB; global atomics beyond
 constexpr int SORT_THREADS = 256;
 constexpr int SORT_ITEMS = 8;        // keys per thread per radix pass
 constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;
@@ -508,11 +509,12 @@ __device__ __forceinline__ uint32_t instance_slot(uint2 rect, uint32_t off, uint
 }
 
 // ------------------------------------------------------- kernel launchers --
-hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* tile_count,
-                             int nb, hipStream_t s);
+hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* counts,
+                             bool lds_hist, int ntiles, int nb, hipStream_t s);
+hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, hipStream_t s);
 hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hipStream_t s);
-hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int ntiles, uint2* ranges,
-                              hipStream_t s);
+hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
+                              uint2* ranges, hipStream_t s);
 hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid, int nb,
                             hipStream_t s);
 // Speculative launches: kernels exit early when the device-side counters show
@@ -526,7 +528,7 @@ struct SpecGuard {
     }
 };
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
-                                   uint64_t* keys, int nb, SpecGuard guard, hipStream_t s);
+                                   bool lds_hist, int ntiles, uint64_t* keys, int nb, SpecGuard guard, hipStream_t s);
 hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint32_t* point_list,
                             SpecGuard guard, hipStream_t s);
 hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t n, int nsb, int npass,

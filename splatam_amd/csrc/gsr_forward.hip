@@ -17,9 +17,20 @@
 namespace gsr {
 
 // ------------------------------------------------------------- preprocess --
+// LDS_HIST: per-tile instance counts go to a workgroup histogram in LDS and
+// leave as one row of the [workgroup x tile] matrix `counts` (no global
+// atomics: ~680k scattered global atomics cost ~30 us on MI355X whatever their
+// contention, tools/micro/atomics.hip).  Otherwise: global atomics on padded
+// per-tile counters (fallback for > MAX_LDS_TILES tiles).
+template <bool LDS_HIST>
 __global__ void __launch_bounds__(PRE_BLOCK)
-preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __restrict__ tile_count) {
+preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __restrict__ counts, int ntiles) {
 #pragma clang fp contract(off)
+    extern __shared__ uint32_t s_hist[];
+    if (LDS_HIST) {
+        for (int t = threadIdx.x; t < ntiles; t += PRE_BLOCK) s_hist[t] = 0u;
+        __syncthreads();
+    }
     const int i = blockIdx.x * PRE_BLOCK + threadIdx.x;
     uint32_t tiles = 0;
     if (i < g.P) {
@@ -71,7 +82,10 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                 geo.rec_c[i] = make_float4(rgb[0], rgb[1], rgb[2], __uint_as_float(clamped));
                 geo.rect[i] = make_uint2((uint32_t)x0 | ((uint32_t)y0 << 16), (uint32_t)x1 | ((uint32_t)y1 << 16));
                 for (int ty = y0; ty < y1; ty++)  // per-tile instance counts -> bucket ranges
-                    for (int tx = x0; tx < x1; tx++) atomicAdd(&tile_count[(ty * cam.gx + tx) * TILE_CTR_STRIDE], 1u);
+                    for (int tx = x0; tx < x1; tx++) {
+                        if (LDS_HIST) atomicAdd(&s_hist[ty * cam.gx + tx], 1u);
+                        else atomicAdd(&counts[(ty * cam.gx + tx) * TILE_CTR_STRIDE], 1u);
+                    }
             }
         }
         radii[i] = radius;
@@ -84,13 +98,62 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
     __syncthreads();
-    if (threadIdx.x == 0) geo.blocksums[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (threadIdx.x == 0) {
+        uint32_t sum = 0;
+#pragma unroll
+        for (int k = 0; k < PRE_BLOCK / 64; k++) sum += wsum[k];
+        geo.blocksums[blockIdx.x] = sum;
+    }
+    if (LDS_HIST)
+        for (int t = threadIdx.x; t < ntiles; t += PRE_BLOCK) counts[(size_t)blockIdx.x * ntiles + t] = s_hist[t];
 }
 
-hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* tile_count,
-                             int nb, hipStream_t s) {
+hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* counts,
+                             bool lds_hist, int ntiles, int nb, hipStream_t s) {
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(preprocess_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, g, geo, radii, tile_count);
+    if (lds_hist)
+        hipLaunchKernelGGL(preprocess_kernel<true>, dim3(nb), dim3(PRE_BLOCK), sizeof(uint32_t) * ntiles, s, cam, g,
+                           geo, radii, counts, ntiles);
+    else
+        hipLaunchKernelGGL(preprocess_kernel<false>, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, g, geo, radii, counts,
+                           ntiles);
+    return hipGetLastError();
+}
+
+// Column scan of the [workgroup x tile] count matrix: in place, every entry
+// becomes the workgroup's offset inside its tile's bucket; tot[t] = tile total.
+// One workgroup per 64 tiles, 16 row segments each (coalesced across tiles).
+constexpr int CS_TILES = 64, CS_PARTS = 16;
+
+__global__ void __launch_bounds__(CS_TILES * CS_PARTS)
+tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t* __restrict__ tot) {
+    __shared__ uint32_t s_part[CS_PARTS][CS_TILES];
+    const int tl = threadIdx.x % CS_TILES, q = threadIdx.x / CS_TILES;
+    const int t = blockIdx.x * CS_TILES + tl;
+    const int rq = (nb + CS_PARTS - 1) / CS_PARTS;
+    const int b0 = min(nb, q * rq), b1 = min(nb, b0 + rq);
+    uint32_t sum = 0;
+    if (t < ntiles)
+#pragma unroll 4
+        for (int b = b0; b < b1; b++) sum += counts[(size_t)b * ntiles + t];
+    s_part[q][tl] = sum;
+    __syncthreads();
+    uint32_t run = 0;
+    for (int k = 0; k < q; k++) run += s_part[k][tl];
+    if (t < ntiles) {
+#pragma unroll 4
+        for (int b = b0; b < b1; b++) {
+            const uint32_t v = counts[(size_t)b * ntiles + t];
+            counts[(size_t)b * ntiles + t] = run;
+            run += v;
+        }
+        if (q == CS_PARTS - 1) tot[t] = run;
+    }
+}
+
+hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, hipStream_t s) {
+    hipLaunchKernelGGL(tile_colscan_kernel, dim3((ntiles + CS_TILES - 1) / CS_TILES), dim3(CS_TILES * CS_PARTS), 0, s,
+                       counts, nb, ntiles, tot);
     return hipGetLastError();
 }
 
@@ -158,7 +221,8 @@ hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hi
 // (identifyTileRanges, rasterizer_impl.cu:116-138, without reading keys).
 __global__ void __launch_bounds__(SCAN_THREADS)
 scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t* __restrict__ tile_count,
-                   uint32_t ntiles, uint2* __restrict__ ranges, uint32_t* __restrict__ counters) {
+                   uint32_t tile_stride, uint32_t ntiles, uint2* __restrict__ ranges,
+                   uint32_t* __restrict__ counters) {
     __shared__ uint32_t wsums[SCAN_THREADS / 64];
     __shared__ uint32_t s_carry, s_max;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -173,7 +237,7 @@ scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t
             const uint32_t i0 = base + (uint32_t)tid * SCAN_ITEMS;
 #pragma unroll
             for (int k = 0; k < SCAN_ITEMS; k++) {
-                x[k] = (i0 + k < n) ? src[(size_t)(i0 + k) * (pass == 0 ? 1 : TILE_CTR_STRIDE)] : 0u;
+                x[k] = (i0 + k < n) ? src[(size_t)(i0 + k) * (pass == 0 ? 1u : tile_stride)] : 0u;
                 sum += x[k];
                 vmax = max(vmax, x[k]);
             }
@@ -209,10 +273,10 @@ scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t
     }
 }
 
-hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int ntiles, uint2* ranges,
-                              hipStream_t s) {
+hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
+                              uint2* ranges, hipStream_t s) {
     hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, geo.blocksums, (uint32_t)nb, tile_count,
-                       (uint32_t)ntiles, ranges, geo.counters);
+                       (uint32_t)tile_stride, (uint32_t)ntiles, ranges, geo.counters);
     return hipGetLastError();
 }
 
@@ -272,10 +336,17 @@ hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* ke
 // (slot from a per-tile cursor), keyed (depth bits << 32 | Gaussian id).  The
 // order inside a bucket is arbitrary; tile_sort_kernel restores the reference
 // order (depth, then id: cub's stable LSD sort, rasterizer_impl.cu:304-309).
+template <bool LDS_HIST>
 __global__ void __launch_bounds__(PRE_BLOCK)
 duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict__ ranges,
-                        uint32_t* __restrict__ cursor, uint64_t* __restrict__ keys, SpecGuard guard) {
+                        uint32_t* __restrict__ cursor, int ntiles, uint64_t* __restrict__ keys, SpecGuard guard) {
     if (guard.overflow()) return;
+    // LDS_HIST: cursor = the column-scanned count matrix; this workgroup's
+    // instances of tile t go to ranges[t].x + cursor[block][t] + (LDS rank)
+    extern __shared__ uint32_t s_cur[];
+    if (LDS_HIST)
+        for (int t = threadIdx.x; t < ntiles; t += PRE_BLOCK)
+            s_cur[t] = ranges[t].x + cursor[(size_t)blockIdx.x * ntiles + t];
     __shared__ uint32_t s_incl[PRE_BLOCK];
     __shared__ uint32_t s_x0[PRE_BLOCK], s_y0[PRE_BLOCK], s_w[PRE_BLOCK], s_depth[PRE_BLOCK];
     __shared__ uint32_t wsum[PRE_BLOCK / 64];
@@ -309,16 +380,21 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict
         const uint32_t local = e - ((lo == 0) ? 0u : s_incl[lo - 1]);
         const uint32_t wdt = s_w[lo];
         const uint32_t tile = (s_y0[lo] + local / wdt) * (uint32_t)cam.gx + s_x0[lo] + local % wdt;
-        const uint32_t pos = ranges[tile].x + atomicAdd(&cursor[tile * TILE_CTR_STRIDE], 1u);
+        const uint32_t pos = LDS_HIST ? atomicAdd(&s_cur[tile], 1u)
+                                      : ranges[tile].x + atomicAdd(&cursor[tile * TILE_CTR_STRIDE], 1u);
         keys[pos] = ((uint64_t)s_depth[lo] << 32) | (uint64_t)(blockIdx.x * PRE_BLOCK + lo);
     }
 }
 
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
-                                   uint64_t* keys, int nb, SpecGuard guard, hipStream_t s) {
+                                   bool lds_hist, int ntiles, uint64_t* keys, int nb, SpecGuard guard, hipStream_t s) {
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(duplicate_bucket_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, ranges, cursor, keys,
-                       guard);
+    if (lds_hist)
+        hipLaunchKernelGGL(duplicate_bucket_kernel<true>, dim3(nb), dim3(PRE_BLOCK), sizeof(uint32_t) * ntiles, s, cam,
+                           P, geo, ranges, cursor, ntiles, keys, guard);
+    else
+        hipLaunchKernelGGL(duplicate_bucket_kernel<false>, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, ranges,
+                           cursor, ntiles, keys, guard);
     return hipGetLastError();
 }
 

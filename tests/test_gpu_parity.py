@@ -124,6 +124,7 @@ BIN_CASES = [
     dict(name="cfg1_like", P=4000, W=160, H=120, aniso=False),
     dict(name="aniso", P=3000, W=128, H=96, aniso=True),
     dict(name="long_lists", P=12000, W=48, H=32, aniso=False),   # > TILE_SORT_CAP -> radix fallback
+    dict(name="many_tiles", P=6000, W=2080, H=2080, aniso=True),  # > MAX_LDS_TILES -> global-atomic counts
 ]
 
 

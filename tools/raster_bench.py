@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from splatam_amd import profiling  # noqa: E402
-from splatam_amd.rasterizer import GaussianRasterizer  # noqa: E402
+from splatam_amd.rasterizer import GaussianRasterizer, rasterize_gaussians_dual  # noqa: E402
 from splatam_amd.scenes import config_scene  # noqa: E402
 from splatam_amd.slam import camera_settings  # noqa: E402
 
@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mode", choices=("dual_lean", "dual", "single"), default="dual_lean",
+                    help="dual_lean: one dual rasterization, grads for means3D + depth colours only (tracking)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     s = config_scene(a.config)
@@ -34,11 +36,21 @@ def main():
     g = torch.randn(3, s.cam.H, s.cam.W, device=dev)
     ras = GaussianRasterizer(cam)
 
+    full = a.mode != "dual_lean"
+    op.requires_grad_(full)
+    col.requires_grad_(full)
+    ds.requires_grad_(True)
+
     def it():
-        for c in (col, ds):
-            m2 = torch.zeros_like(m3, requires_grad=True)
-            im, _, _ = ras(means3D=m3, means2D=m2, opacities=op, colors_precomp=c, scales=sc, rotations=ro)
-            im.backward(g)
+        if a.mode == "single":
+            for c in (col, ds):
+                m2 = torch.zeros_like(m3, requires_grad=True)
+                im, _, _ = ras(means3D=m3, means2D=m2, opacities=op, colors_precomp=c, scales=sc, rotations=ro)
+                im.backward(g)
+        else:
+            m2 = torch.zeros_like(m3, requires_grad=full)
+            im, im2, _, _ = rasterize_gaussians_dual(m3, m2, None, col, ds, op, sc, ro, None, cam)
+            torch.autograd.backward([im, im2], [g, g])
 
     for _ in range(a.warmup):
         it()
