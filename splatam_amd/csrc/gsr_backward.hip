@@ -27,8 +27,16 @@ constexpr int BWD_BATCH = 128;
 // dL/dcolors2 are wanted; absent ones are neither formed nor reduced (tracking
 // needs only the geometric sums and the depth colours).  Records always use the
 // fixed 12-slot layout [hx, hy, hxx, hxy, hyy | G dL/dalpha | dch dp(3) | dch dq(3)].
-template <int BWD_GROUP, bool PREFETCH, bool DUAL, bool OPAC = true, bool COL1 = true, bool COL2 = DUAL>
-__global__ void __launch_bounds__(TILE_PIX)
+//
+// Per pixel the reference's back-to-front recurrence (backward.cu:966-1017)
+// is carried on dot products with dL/dpixel: the colour accumulated behind the
+// current Gaussian, accum_rec . dL/dpix, is one scalar A updated as
+// A <- A + alpha (c . dL/dpix - A) after each contributing Gaussian (the
+// reference's last_alpha / last_color / accum_rec update, one step earlier).
+// 5 workgroups per CU (<= 96 VGPRs): a 640x480 frame's 1200 tiles are all resident
+// at once, so there is no second dispatch round behind the slowest tiles
+template <bool DUAL, bool OPAC, bool COL1, bool COL2>
+__global__ void __launch_bounds__(TILE_PIX, 5)
 render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                   const uint2* __restrict__ rect, const uint32_t* __restrict__ offsets,
                   const float4* __restrict__ rec_a, const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
@@ -36,7 +44,6 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                   const float* __restrict__ dL_dpix, const float* __restrict__ colors2,
                   const float* __restrict__ dL_dpix2, float4* __restrict__ inst) {
     static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
-    static_assert(BWD_GROUP == 4 || (OPAC && COL1), "2-entry groups only for the full value set");
     constexpr int NV = 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? 3 : 0);
     constexpr int O_OP = 5, O_C1 = 5 + (OPAC ? 1 : 0), O_C2 = O_C1 + (COL1 ? 3 : 0);
     __shared__ float4 s_a[BWD_BATCH];
@@ -84,16 +91,15 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         inst[3 * u + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
         inst[3 * u + 2] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    // background term of dL/dalpha, -T_final / (1 - alpha) * (bg . dL/dpix) (backward.cu:1014):
+    // a per-pixel constant times 1 / (1 - alpha); exactly 0 when bg = 0
     float bg_dot = cam.bg[0] * dp0 + cam.bg[1] * dp1 + cam.bg[2] * dp2;
     if (DUAL) bg_dot += cam.bg[0] * dq0 + cam.bg[1] * dq1 + cam.bg[2] * dq2;
-    const bool bg_on = cam.bg[0] != 0.f || cam.bg[1] != 0.f || cam.bg[2] != 0.f;  // uniform
-    const float pxf = (float)px, pyf = (float)py;
-    float T = T_final;
-    // accum_rec / last_color of backward.cu:997-1001 enter only through their dot
-    // product with dL/dpixel, so the recurrence is carried on those dot products.
-    float acc_dot = 0.f, lc_dot = 0.f, last_alpha = 0.f;
+    const float Tbg = -T_final * bg_dot;
+    const v2f pix = v2f{(float)px, (float)py};
+    const v2f dp01 = v2f{dp0, dp1}, dq01 = v2f{dq0, dq1};
+    float T = T_final, A = 0.f;
     const int row = lane >> 4;
-    // records of the first batch (back to front)
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
     uint32_t pu = 0;
     if (tid < min(BWD_BATCH, (int)bmax)) {
@@ -107,8 +113,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         const int cnt = min(BWD_BATCH, hi);
         if (tid < cnt) {
             s_u[tid] = pu;
-            s_a[tid] = stage_a(pa);
-            s_b[tid] = stage_b(pb);
+            s_a[tid] = stage_a(pa, pb);
+            s_b[tid] = stage_b(pa, pb);
             s_c[tid] = pc;
             if (DUAL) s_d[tid] = pd;
             s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
@@ -128,99 +134,84 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         }
         // entries j with pos = hi-1-j >= wmax lie behind every pixel of this wave
         const int n = build_strip_list(s_mask, cnt, w, hi - (int)wmax, s_list[w]);
-        GroupN<BWD_GROUP> nxt;
-        if (PREFETCH && n > 0) load_group<BWD_GROUP>(s_list[w], 0, n, s_a, s_b, nxt);
-        for (int i = 0; i < n; i += BWD_GROUP) {
-            GroupN<BWD_GROUP> cur;
-            if (PREFETCH) {
-                cur = nxt;
-                if (i + BWD_GROUP < n) load_group<BWD_GROUP>(s_list[w], i + BWD_GROUP, n, s_a, s_b, nxt);
-            } else {
-                load_group<BWD_GROUP>(s_list[w], i, n, s_a, s_b, cur);
-            }
-            int j[BWD_GROUP];
-            bool ok[BWD_GROUP];
-            float dx[BWD_GROUP], dy[BWD_GROUP], G[BWD_GROUP], araw[BWD_GROUP], alpha[BWD_GROUP];
+        for (int i = 0; i < n; i += 4) {
+            const Group4 gq = load_group4(s_list[w], i, n);
+            v2f d[4];
+            float G[4], araw[4], alpha[4];
+            bool ok[4];
             bool any = false;
 #pragma unroll
-            for (int k = 0; k < BWD_GROUP; k++) {
-                j[k] = cur.j[k];
-                dx[k] = cur.a[k].x - pxf;
-                dy[k] = cur.a[k].y - pyf;
-                const float p2 = eval_p2(cur.a[k], cur.b[k], dx[k], dy[k]);  // log2(e) * power
-                G[k] = __builtin_amdgcn_exp2f(fminf(p2, 0.f));                // finite for every lane
-                araw[k] = cur.b[k].y * G[k];
+            for (int k = 0; k < 4; k++) {
+                const float4 a = s_a[gq.j[k]], b = s_b[gq.j[k]];
+                d[k] = pix_delta(a, pix);
+                const float p2 = eval_p2(a, b, d[k]);                       // log2(e) * power
+                G[k] = __builtin_amdgcn_exp2f(fminf(p2, 0.f));             // finite for every lane
+                araw[k] = b.y * G[k];
                 alpha[k] = fminf(0.99f, araw[k]);
-                const uint32_t pos = (uint32_t)(hi - 1 - j[k]);  // position in the tile list
-                ok[k] = cur.valid[k] && pos < last && p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;
+                const uint32_t pos = (uint32_t)(hi - 1 - gq.j[k]);         // position in the tile list
+                ok[k] = gq.valid[k] && pos < last && p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;
                 any = any || ok[k];
             }
             if (__ballot(any) == 0ull) continue;
-            // Per pair: reduce (hx, hy, hx*dx, hx*dy, hy*dy, G*dL/dalpha, dchannel*dL/dpix[3]) with
+            // serial part (in list order): T and A, then dL/dalpha and dchannel/dcolor
+            float dLa[4], dch[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float4 c = s_c[gq.j[k]];
+                float cd;
+                if (DUAL) {
+                    const float4 c2 = s_d[gq.j[k]];
+                    const v2f t = v2f{c.x, c.y} * dp01 + v2f{c2.x, c2.y} * dq01;
+                    cd = __builtin_fmaf(c.z, dp2, __builtin_fmaf(c2.z, dq2, t.x + t.y));
+                } else {
+                    const v2f t = v2f{c.x, c.y} * dp01;
+                    cd = __builtin_fmaf(c.z, dp2, t.x + t.y);
+                }
+                const float inv = __builtin_amdgcn_rcpf(1.f - alpha[k]);   // v_rcp_f32 (~1 ulp)
+                const float Tn = T * inv;                                   // T / (1 - alpha), backward.cu:978
+                const float e = cd - A;
+                const bool o = ok[k];
+                dLa[k] = o ? __builtin_fmaf(Tbg, inv, e * Tn) : 0.f;
+                dch[k] = o ? alpha[k] * Tn : 0.f;
+                T = o ? Tn : T;
+                A = o ? __builtin_fmaf(alpha[k], e, A) : A;
+            }
+            // Per pair: (hx, hy, hx*dx, hx*dy, hy*dy, G*dL/dalpha, dch*dL/dpix, dch*dL/dpix2) with
             // h = G * dL/dG = (o * G) * dL/dalpha.  gauss_bwd turns them into the reference's
             // per-pair quantities (backward.cu:1020-1038): dmean2D = -ddel * (Q [hx, hy]),
             // dconic = -0.5 * (hxx, hxy, hyy); both are linear in the sums (Q is per Gaussian).
-            float v[BWD_GROUP * NV];
+            float v[4 * NV];
 #pragma unroll
-            for (int k = 0; k < BWD_GROUP; k++) {
-                const float4 c = s_c[j[k]];
-                const float inv = __builtin_amdgcn_rcpf(1.f - alpha[k]);  // v_rcp_f32 (~1 ulp)
-                const float Tn = T * inv;                                  // T / (1 - alpha), backward.cu:978
-                float cd = c.x * dp0 + c.y * dp1 + c.z * dp2;
-                if (DUAL) {
-                    const float4 d2 = s_d[j[k]];
-                    cd += d2.x * dq0 + d2.y * dq1 + d2.z * dq2;
-                }
-                const float na_dot = last_alpha * lc_dot + (1.f - last_alpha) * acc_dot;
-                float dL_dalpha = (cd - na_dot) * Tn;
-                if (bg_on) dL_dalpha += (-T_final * inv) * bg_dot;
-                const bool o_ = ok[k];
-                dL_dalpha = o_ ? dL_dalpha : 0.f;
-                const float dch = o_ ? alpha[k] * Tn : 0.f;
-                const float h = araw[k] * dL_dalpha;
-                const float hx = h * dx[k], hy = h * dy[k];
+            for (int k = 0; k < 4; k++) {
                 float* vk = v + NV * k;
-                vk[0] = hx;
-                vk[1] = hy;
-                vk[2] = hx * dx[k];
-                vk[3] = hx * dy[k];
-                vk[4] = hy * dy[k];
-                if (OPAC) vk[O_OP] = G[k] * dL_dalpha;
+                const v2f hv = (araw[k] * dLa[k]) * d[k];   // (hx, hy)
+                const v2f hh = hv.x * d[k];                  // (hx dx, hx dy)
+                vk[0] = hv.x;
+                vk[1] = hv.y;
+                vk[2] = hh.x;
+                vk[3] = hh.y;
+                vk[4] = hv.y * d[k].y;
+                if (OPAC) vk[O_OP] = G[k] * dLa[k];
                 if (COL1) {
-                    vk[O_C1] = dch * dp0;
-                    vk[O_C1 + 1] = dch * dp1;
-                    vk[O_C1 + 2] = dch * dp2;
+                    const v2f t = dch[k] * dp01;
+                    vk[O_C1] = t.x;
+                    vk[O_C1 + 1] = t.y;
+                    vk[O_C1 + 2] = dch[k] * dp2;
                 }
                 if (COL2) {
-                    vk[O_C2] = dch * dq0;
-                    vk[O_C2 + 1] = dch * dq1;
-                    vk[O_C2 + 2] = dch * dq2;
-                }
-                if (o_) {
-                    T = Tn;
-                    acc_dot = na_dot;
-                    lc_dot = cd;
-                    last_alpha = alpha[k];
+                    const v2f t = dch[k] * dq01;
+                    vk[O_C2] = t.x;
+                    vk[O_C2 + 1] = t.y;
+                    vk[O_C2 + 2] = dch[k] * dq2;
                 }
             }
-            if constexpr (BWD_GROUP == 4) {
-                float r[NV];
-                wave_reduce_n<4 * NV>(v, r);  // row rho holds item rho's NV sums
-                if ((lane & 15) == 0 && i + row < n) {
-                    float* dst = s_acc + (w * BWD_BATCH + j[row]) * NV;
+            float r[NV];
+            wave_reduce_n<4 * NV>(v, r);  // row rho holds item rho's NV sums
+            if ((lane & 15) == 0 && i + row < n) {
+                const int jr = row == 0 ? gq.j[0] : (row == 1 ? gq.j[1] : (row == 2 ? gq.j[2] : gq.j[3]));
+                float* dst = s_acc + (w * BWD_BATCH + jr) * NV;
 #pragma unroll
-                    for (int m = 0; m < NV; m++) dst[m] = r[m];
-                }
-            } else {
-                float r[5];
-                wave_reduce2x9(v, r);
-                const int item = row >> 1, half = row & 1;
-                if ((lane & 15) == 0 && i + item < n) {
-                    float* dst = s_acc + (w * BWD_BATCH + j[item]) * 9 + 4 * half;
-#pragma unroll
-                    for (int m = 0; m < 4; m++) dst[m] = r[m];
-                    if (half == 0) dst[8] = r[4];
-                }
+                for (int m = 0; m < NV; m++) dst[m] = r[m];
             }
         }
         __syncthreads();
@@ -248,32 +239,23 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     }
 }
 
-template <bool OPAC, bool COL1, bool COL2>
-static auto dual_variant() { return render_bwd_kernel<4, false, true, OPAC, COL1, COL2>; }
+template <bool DUAL, bool OPAC, bool COL1, bool COL2>
+static auto bwd_variant() { return render_bwd_kernel<DUAL, OPAC, COL1, COL2>; }
 
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
                              const float* colors2, const float* dL_dpix2, unsigned need, float4* inst,
                              hipStream_t s) {
-    // GSR_BWD_VARIANT (tuning only): 1 = 4-entry groups (default), 0 = 4 + prefetch, 2 = 2 + prefetch, 3 = 2
-    static const int variant = [] {
-        const char* e = getenv("GSR_BWD_VARIANT");
-        return e ? atoi(e) : 1;
-    }();
-    const bool op = need & NEED_OPACITY, c1 = need & NEED_COLORS, c2 = need & NEED_COLORS2;
-    auto k = render_bwd_kernel<4, false, false>;
+    const bool op = need & NEED_OPACITY, c1 = need & NEED_COLORS, c2 = colors2 && (need & NEED_COLORS2);
+    auto k = bwd_variant<false, true, true, false>();
     if (!colors2) {
-        if (variant == 0) k = render_bwd_kernel<4, true, false>;
-        if (variant == 2) k = render_bwd_kernel<2, true, false>;
-        if (variant == 3) k = render_bwd_kernel<2, false, false>;
-        if (!op || !c1) k = op ? render_bwd_kernel<4, false, false, true, false> :
-                            (c1 ? render_bwd_kernel<4, false, false, false, true> :
-                                  render_bwd_kernel<4, false, false, false, false>);
+        k = op ? (c1 ? bwd_variant<false, 1, 1, 0>() : bwd_variant<false, 1, 0, 0>())
+               : (c1 ? bwd_variant<false, 0, 1, 0>() : bwd_variant<false, 0, 0, 0>());
     } else {
-        k = op ? (c1 ? (c2 ? dual_variant<1, 1, 1>() : dual_variant<1, 1, 0>())
-                     : (c2 ? dual_variant<1, 0, 1>() : dual_variant<1, 0, 0>()))
-               : (c1 ? (c2 ? dual_variant<0, 1, 1>() : dual_variant<0, 1, 0>())
-                     : (c2 ? dual_variant<0, 0, 1>() : dual_variant<0, 0, 0>()));
+        k = op ? (c1 ? (c2 ? bwd_variant<true, 1, 1, 1>() : bwd_variant<true, 1, 1, 0>())
+                     : (c2 ? bwd_variant<true, 1, 0, 1>() : bwd_variant<true, 1, 0, 0>()))
+               : (c1 ? (c2 ? bwd_variant<true, 0, 1, 1>() : bwd_variant<true, 0, 1, 0>())
+                     : (c2 ? bwd_variant<true, 0, 0, 1>() : bwd_variant<true, 0, 0, 0>()));
     }
     hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rect, geo.offsets,
                        geo.rec_a, geo.rec_b, geo.rec_c, final_T, n_contrib, dL_dpix, colors2, dL_dpix2, inst);

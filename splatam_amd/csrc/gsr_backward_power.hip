@@ -155,8 +155,8 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
             const float4 pa = rec_a[gi], pb = rec_b[gi];
             s_g[tid] = gi;
             s_u[tid] = instance_slot(rect[gi], offsets[gi], blockIdx.x, blockIdx.y);
-            s_a[tid] = stage_a(pa);
-            s_b[tid] = stage_b(pb);
+            s_a[tid] = stage_a(pa, pb);
+            s_b[tid] = stage_b(pa, pb);
             s_c[tid] = rec_c[gi];
             s_q[tid] = make_float4(pa.z, pa.w, pb.x, 0.f);
             s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
@@ -173,8 +173,9 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
         for (int i = 0; i < n; i++) {
             const int j = s_list[w][i];  // wave-uniform
             const float4 a = s_a[j], b = s_b[j];
-            const float dx = a.x - pxf, dy = a.y - pyf;
-            const float p2 = eval_p2(a, b, dx, dy);
+            const v2f dd = pix_delta(a, v2f{pxf, pyf});
+            const float dx = dd.x, dy = dd.y;
+            const float p2 = eval_p2(a, b, dd);
             const float G = __builtin_amdgcn_exp2f(fminf(p2, 0.f));
             const float araw = b.y * G;
             const float alpha = fminf(0.99f, araw);

@@ -306,17 +306,31 @@ __device__ __forceinline__ void sh_fwd(int deg, float3 pos, const float* campos,
     }
 }
 
-// LDS staging form of a render record: the conic is prescaled so that
+// LDS staging form of a render record (from the geom records ra = (x, y, A, B),
+// rb = (C, opacity, depth, -)): the conic is prescaled so that
 //   p2 = A' dx^2 + B' dx dy + C' dy^2 = log2(e) * power      (forward.cu:341)
-// feeds v_exp_f32 (exp2) directly.  Forward and backward stage the same values,
-// so both evaluate bit-identical alphas.
+// feeds v_exp_f32 (exp2) directly, and laid out as
+//   sa = (x, y, A', C'),  sb = (B', opacity, depth, -)
+// so (x, y) - pixel and (A', C') * (dx, dy) are packed-f32 pairs.  Forward and
+// backward stage the same values and evaluate p2 through the same contraction-
+// free sequence, so both see bit-identical alphas (the backward recovers T by
+// dividing by 1 - alpha and must take exactly the forward's decisions).
 constexpr float kLog2e = 1.4426950408889634f;
-__device__ __forceinline__ float4 stage_a(float4 a) {
-    return make_float4(a.x, a.y, -0.5f * kLog2e * a.z, -kLog2e * a.w);
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 stage_a(float4 ra, float4 rb) {
+    return make_float4(ra.x, ra.y, -0.5f * kLog2e * ra.z, -0.5f * kLog2e * rb.x);
 }
-__device__ __forceinline__ float4 stage_b(float4 b) { return make_float4(-0.5f * kLog2e * b.x, b.y, b.z, b.w); }
-__device__ __forceinline__ float eval_p2(float4 a, float4 b, float dx, float dy) {
-    return a.z * dx * dx + a.w * dx * dy + b.x * dy * dy;
+__device__ __forceinline__ float4 stage_b(float4 ra, float4 rb) {
+    return make_float4(-kLog2e * ra.w, rb.y, rb.z, 0.f);
+}
+__device__ __forceinline__ v2f pix_delta(float4 sa, v2f pix) {
+#pragma clang fp contract(off)
+    return v2f{sa.x, sa.y} - pix;
+}
+__device__ __forceinline__ float eval_p2(float4 sa, float4 sb, v2f d) {
+#pragma clang fp contract(off)
+    const v2f t = v2f{sa.z, sa.w} * d;  // (A' dx, C' dy)
+    return __builtin_fmaf(sb.x * d.x, d.y, __builtin_fmaf(t.x, d.x, t.y * d.y));
 }
 
 // 4-bit mask of the 16x4-pixel wave strips of a tile (pixel centres x0..x0+15,
@@ -410,45 +424,26 @@ __device__ __forceinline__ void wave_reduce9(const float v[9], float& r0, float&
 }
 __device__ __forceinline__ int reduce9_slot_r0(int row) { return (row == 0) ? 0 : (row == 1 ? 2 : (row == 2 ? 1 : 3)); }
 
-// One group of N consecutive entries of a wave's strip list, with the two
-// float4 records every evaluation needs (x, y, A, B / C, opacity, depth).
-template <int N>
-struct GroupN {
-    int j[N];
-    bool valid[N];
-    float4 a[N], b[N];
+// Four consecutive entries of a wave's strip list as wave-uniform (SGPR)
+// indices; entries past n repeat the first one and are flagged invalid.
+struct Group4 {
+    int j[4];
+    bool valid[4];
 };
-using Group4 = GroupN<4>;
-
-template <int N>
-__device__ __forceinline__ void load_group(const uint16_t* list, int i, int n, const float4* s_a, const float4* s_b,
-                                           GroupN<N>& g) {
-    static_assert(N == 2 || N == 4, "group of 2 or 4 list entries");
-    if constexpr (N == 4) {
-        const uint2 q = *reinterpret_cast<const uint2*>(&list[i]);
-        g.j[0] = (int)(q.x & 0xFFFFu);
-        g.j[1] = (int)(q.x >> 16);
-        g.j[2] = (int)(q.y & 0xFFFFu);
-        g.j[3] = (int)(q.y >> 16);
-    } else {
-        const uint32_t q = *reinterpret_cast<const uint32_t*>(&list[i]);
-        g.j[0] = (int)(q & 0xFFFFu);
-        g.j[1] = (int)(q >> 16);
-    }
+__device__ __forceinline__ Group4 load_group4(const uint16_t* list, int i, int n) {
+    const uint2 q = *reinterpret_cast<const uint2*>(&list[i]);
+    const uint32_t q0 = __builtin_amdgcn_readfirstlane(q.x), q1 = __builtin_amdgcn_readfirstlane(q.y);
+    Group4 g;
+    g.j[0] = (int)(q0 & 0xFFFFu);
+    g.j[1] = (int)(q0 >> 16);
+    g.j[2] = (int)(q1 & 0xFFFFu);
+    g.j[3] = (int)(q1 >> 16);
 #pragma unroll
-    for (int k = 0; k < N; k++) {
+    for (int k = 0; k < 4; k++) {
         g.valid[k] = i + k < n;
         if (!g.valid[k]) g.j[k] = g.j[0];
     }
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-        g.a[k] = s_a[g.j[k]];
-        g.b[k] = s_b[g.j[k]];
-    }
-}
-__device__ __forceinline__ void load_group4(const uint16_t* list, int i, int n, const float4* s_a, const float4* s_b,
-                                            Group4& g) {
-    load_group<4>(list, i, n, s_a, s_b, g);
+    return g;
 }
 
 // Transposed reduction of 4 items x 9 values (v[item*9 + q]) over the 64 lanes:

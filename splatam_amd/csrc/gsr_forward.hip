@@ -593,8 +593,8 @@ hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t
 // DUAL: a second colour set (colors2, e.g. SplaTAM's [z, 1, z^2]) is composited
 // in the same pass -- same alpha / T / termination, so each output is bitwise
 // the image a separate call would produce.
-template <int FWD_GROUP, bool PREFETCH, bool DUAL>
-__global__ void __launch_bounds__(TILE_PIX)
+template <bool DUAL>
+__global__ void __launch_bounds__(TILE_PIX, 5)
 render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                   const float4* __restrict__ rec_a, const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
                   const float* __restrict__ colors2, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
@@ -613,7 +613,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     const int py = blockIdx.y * TILE_Y + (tid >> 4);
     const float x0 = (float)(blockIdx.x * TILE_X), y0 = (float)(blockIdx.y * TILE_Y);
     const bool inside = px < cam.W && py < cam.H;
-    const float pxf = (float)px, pyf = (float)py;
+    const v2f pix = v2f{(float)px, (float)py};
     const uint2 range = ranges[tile];
     bool done = !inside;
     float T = 1.f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 15.0f;  // forward.cu:308 median-depth default
@@ -629,8 +629,8 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
         const int cnt = (int)min((uint32_t)RENDER_BATCH, range.y - start);
         if (tid < cnt) {
-            s_a[tid] = stage_a(pa);
-            s_b[tid] = stage_b(pb);
+            s_a[tid] = stage_a(pa, pb);
+            s_b[tid] = stage_b(pa, pb);
             s_c[tid] = pc;
             if (DUAL) s_d[tid] = pd;
             s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
@@ -646,49 +646,43 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         }
         const int n = build_strip_list(s_mask, cnt, w, 0, s_list[w]);
         const uint32_t pos0 = start - range.x;
-        GroupN<FWD_GROUP> nxt;
-        if (PREFETCH && n > 0) load_group<FWD_GROUP>(s_list[w], 0, n, s_a, s_b, nxt);
-        for (int i = 0; i < n; i += FWD_GROUP) {
+        for (int i = 0; i < n; i += 4) {
             if (__ballot(!done) == 0ull) break;
-            GroupN<FWD_GROUP> cur;
-            if (PREFETCH) {
-                cur = nxt;
-                if (i + FWD_GROUP < n) load_group<FWD_GROUP>(s_list[w], i + FWD_GROUP, n, s_a, s_b, nxt);
-            } else {
-                load_group<FWD_GROUP>(s_list[w], i, n, s_a, s_b, cur);
-            }
-            float4 c[FWD_GROUP], d[FWD_GROUP];
+            const Group4 gq = load_group4(s_list[w], i, n);
+            float alpha[4], depth[4];
+            bool ok[4];
 #pragma unroll
-            for (int k = 0; k < FWD_GROUP; k++) {
-                c[k] = s_c[cur.j[k]];
-                if (DUAL) d[k] = s_d[cur.j[k]];
-            }
-            float power[FWD_GROUP], alpha[FWD_GROUP];
-#pragma unroll
-            for (int k = 0; k < FWD_GROUP; k++) {
-                const float dx = cur.a[k].x - pxf, dy = cur.a[k].y - pyf;
-                power[k] = eval_p2(cur.a[k], cur.b[k], dx, dy);  // log2(e) * power
-                alpha[k] = fminf(0.99f, cur.b[k].y * __builtin_amdgcn_exp2f(fminf(power[k], 0.f)));
+            for (int k = 0; k < 4; k++) {
+                const float4 a = s_a[gq.j[k]], b = s_b[gq.j[k]];
+                const float p2 = eval_p2(a, b, pix_delta(a, pix));           // log2(e) * power
+                alpha[k] = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(fminf(p2, 0.f)));
+                depth[k] = b.z;
+                ok[k] = gq.valid[k] && p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;
             }
 #pragma unroll
-            for (int k = 0; k < FWD_GROUP; k++) {
-                const bool ok = cur.valid[k] && !done && power[k] <= 0.0f && alpha[k] >= 1.0f / 255.0f;
+            for (int k = 0; k < 4; k++) {
+                const bool okk = ok[k] && !done;
+                if (__ballot(okk) == 0ull) continue;  // no lane blends this Gaussian: skip its colours
                 const float test_T = T * (1.f - alpha[k]);
-                const bool term = ok && test_T < 0.0001f;
+                const bool term = okk && test_T < 0.0001f;
                 done = done || term;
-                const bool blend = ok && !term;
+                const bool blend = okk && !term;
+                const float4 c = s_c[gq.j[k]];
+                float4 c2;
+                if (DUAL) c2 = s_d[gq.j[k]];
                 if (blend) {
-                    C0 += c[k].x * alpha[k] * T;
-                    C1 += c[k].y * alpha[k] * T;
-                    C2 += c[k].z * alpha[k] * T;
+                    const float wgt = alpha[k] * T;
+                    C0 += c.x * wgt;
+                    C1 += c.y * wgt;
+                    C2 += c.z * wgt;
                     if (DUAL) {
-                        C3 += d[k].x * alpha[k] * T;
-                        C4 += d[k].y * alpha[k] * T;
-                        C5 += d[k].z * alpha[k] * T;
+                        C3 += c2.x * wgt;
+                        C4 += c2.y * wgt;
+                        C5 += c2.z * wgt;
                     }
-                    if (T > 0.5f && test_T < 0.5f) D = cur.b[k].z;  // median depth (forward.cu:368-372)
+                    if (T > 0.5f && test_T < 0.5f) D = depth[k];  // median depth (forward.cu:368-372)
                     T = test_T;
-                    last = pos0 + (uint32_t)cur.j[k] + 1u;            // entries visited up to the last blend
+                    last = pos0 + (uint32_t)gq.j[k] + 1u;          // entries visited up to the last blend
                 }
             }
         }
@@ -714,15 +708,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s) {
-    // GSR_FWD_VARIANT (tuning only): 0 = 4-entry groups, 1 = 4 + prefetch, 2 = 2-entry groups + prefetch
-    static const int variant = [] {
-        const char* e = getenv("GSR_FWD_VARIANT");
-        return e ? atoi(e) : 0;
-    }();
-    auto k = render_fwd_kernel<4, false, false>;
-    if (variant == 1) k = render_fwd_kernel<4, true, false>;
-    if (variant == 2) k = render_fwd_kernel<2, true, false>;
-    if (colors2) k = render_fwd_kernel<4, false, true>;
+    auto k = colors2 ? render_fwd_kernel<true> : render_fwd_kernel<false>;
     hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rec_a, geo.rec_b,
                        geo.rec_c, colors2, final_T, n_contrib, out_color, out_color2, out_depth, guard);
     return hipGetLastError();
