@@ -17,9 +17,10 @@ Gaussian set over RCCL every --bcast-every steps (inside the timed region).
 The JSON line carries:
   roofline      -- render-backward kernel (one dual launch per frame): SURVEY.md
                    8(d) algorithmic bytes per launch extended to both colour sets
-                   (8*Tt + 52*I + 32*N + 56*P, measured I) over its
-                   average duration from hipEvents recorded around that kernel
-                   on its launch stream during the timed region;
+                   (8*Tt + 52*I + 32*N + 56*P, measured I) over its average
+                   duration during the timed region, measured on its launch
+                   stream: device wall-clock stamps around every launch (graph
+                   mode; hipEvent records cannot be captured) or hipEvents (eager);
   cpu_baseline  -- rank 0 at N=1 only: the float32 C oracle (oracle/) on one
                    frame of the same workload, single thread.
 """
@@ -52,6 +53,8 @@ def parse():
     ap.add_argument("--bcast-every", type=int, default=40,
                     help="broadcast the Gaussian map every k steps (Replica: 40 tracking iters/frame)")
     ap.add_argument("--cpu-baseline", choices=("auto", "on", "off"), default="auto")
+    ap.add_argument("--graph", type=int, default=1, help="1: replay the tracking iterations as a HIP graph")
+    ap.add_argument("--iters-per-graph", type=int, default=20)
     return ap.parse_args()
 
 
@@ -117,33 +120,62 @@ def main():
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
-        step()
+    tracker = None
+    steps = args.steps
+    if args.graph:
+        # HIP graph of S tracking iterations (splatam_amd/tracker.py); warm-up and timed
+        # region are whole replays, so K is rounded up to a multiple of S
+        from splatam_amd.tracker import GraphTracker
+        S = max(1, min(args.iters_per_graph, args.steps))
+        steps = -(-args.steps // S) * S
+        tracker = GraphTracker(params, curr, frame, iters_per_graph=S, timing=True,
+                               warmup_iters=min(3, max(1, args.warmup)))
+        for _ in range(max(1, args.warmup // S)):
+            tracker.run()
+    else:
+        for _ in range(args.warmup):
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    profiling.enable_timing(True)
+    if tracker is None:
+        profiling.enable_timing(True)
+    else:  # reset the device-clock accumulators the captured stamps add to
+        profiling.enable_timing(clock_stages=("render_bwd",))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        if world > 1 and args.bcast_every > 0 and i % args.bcast_every == 0:
-            sd.broadcast_map(params)           # map update -> RCCL broadcast over xGMI
-        step()
+    if tracker is not None:
+        per_bcast = max(1, args.bcast_every // tracker.iters) if args.bcast_every > 0 else 0
+        for r in range(steps // tracker.iters):
+            if world > 1 and per_bcast and r % per_bcast == 0:
+                sd.broadcast_map(params)       # map update -> RCCL broadcast over xGMI
+            tracker.run()
+    else:
+        for i in range(steps):
+            if world > 1 and args.bcast_every > 0 and i % args.bcast_every == 0:
+                sd.broadcast_map(params)           # map update -> RCCL broadcast over xGMI
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     stages = profiling.read_timing()
     profiling.enable_timing(False)
+    if tracker is not None and tracker.overflowed():
+        raise SystemExit("binning capacity overflow during the timed replays: measurement invalid")
     elapsed = sd.max_over_ranks(t1 - t0, device=dev)
-    frames = args.steps * world
+    frames = steps * world
     value = frames / elapsed
 
     # ---- roofline of the dominant kernel (render backward) ------------------
     rb = stages["render_bwd"]
     Tt = ((W + 15) // 16) * ((H + 15) // 16)
     N = W * H
-    I_avg = rb["units"] / max(rb["launches"], 1)
+    if tracker is not None:  # static-mode launches report capacity as units; use the measured counters
+        nr = tracker.num_rendered()
+        I_avg = sum(nr) / len(nr)
+    else:
+        I_avg = rb["units"] / max(rb["launches"], 1)
     # SURVEY.md 8(d) per-rasterization bytes 8*Tt + 40*I + 20*N + 44*P, for the dual launch
     # (both colour sets): + colors2 gather 12*I, + dL_dpix2 12*N, + dcolors2 12*P
     bytes_per_launch = 8 * Tt + 52 * I_avg + 32 * N + 56 * P
@@ -159,7 +191,9 @@ def main():
     roofline = {"kernel": "render_bwd_kernel", "bound": "hbm", "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic, "alg_bytes_per_launch": int(bytes_per_launch), "avg_us": round(rb["avg_us"], 2),
-                "num_rendered_avg": int(I_avg)}
+                "num_rendered_avg": int(I_avg), "launches_timed": int(rb["launches"]),
+                "timing": "device wall_clock64 stamps around each launch (HIP graph)" if tracker is not None
+                else "hipEvents around each launch"}
 
     # ---- CPU baseline: the float32 C oracle on one frame (rank 0, N=1) ------
     cpu = None
@@ -200,9 +234,11 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "higher_is_better": True,
+            "metric": METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "execution": (f"HIP graph of {tracker.iters} tracking iterations, replayed; binning capacity "
+                          f"{tracker.capacity}, no overflow" if tracker is not None else "eager"),
             "data": "synthetic (SURVEY.md 8(d) seeded scene; targets rendered at the unperturbed pose)",
             "config": {"workload": f"config {args.config}: {P} isotropic Gaussians, {W}x{H}, SplaTAM tracking "
                                    "iteration (RGB + depth/silhouette render fwd+bwd, masked L1, Adam on pose)",

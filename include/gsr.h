@@ -128,6 +128,21 @@ int gsr_forward_dual(const gsr_settings* settings, const gsr_gaussians* gaussian
                      const float* colors2, float* out_color, float* out_color2, float* out_depth,
                      int* radii, gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
+/* Static-capacity, synchronisation-free gsr_forward_dual (capturable in a HIP
+ * graph).  The binning buffer holds `capacity` instances; nothing waits on the
+ * host.  The device counters are copied to `status` (device, 4 x u32:
+ * [0] num_rendered, [1] prefiltered violation, [2] longest tile list) when the
+ * stream reaches that point.  Outputs are valid iff status[0] <= capacity and
+ * status[2] <= 4096 (the LDS tile sort; longer lists need gsr_forward_dual);
+ * otherwise every kernel after the scan skipped its work (no out-of-bounds
+ * writes) and the call must be repeated with a larger capacity or in the
+ * synchronous mode.  Returns `capacity`: pass it as num_rendered to
+ * gsr_backward_dual (it sizes the buffer layouts). */
+int gsr_forward_dual_static(const gsr_settings* settings, const gsr_gaussians* gaussians,
+                            const float* colors2, int capacity, unsigned* status,
+                            float* out_color, float* out_color2, float* out_depth, int* radii,
+                            gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
 /* Backward of gsr_forward_dual (power 1): every geometric gradient in `grads`
  * is the sum of the two renders' (as autograd would accumulate it over two
  * calls), grads->dcolors is d/dcolors of the first set and dcolors2 [P,3]
@@ -165,6 +180,11 @@ int gsr_abi_version(void);
 #define GSR_STAGE_RENDER_BWD 5 /* render backward                */
 #define GSR_STAGE_GAUSS_BWD 6  /* per-Gaussian chain rule        */
 #define GSR_NUM_STAGES 7
+/* on: 0 off, 1 hipEvents around every stage (not usable under stream capture),
+ * GSR_TIMING_CLOCK | stage_mask: device-clock mode -- one-thread kernels read
+ * wall_clock64() before/after the stages in stage_mask (bit = stage id) and
+ * accumulate on the device, so captured HIP graphs accumulate over every replay. */
+#define GSR_TIMING_CLOCK 0x100
 int gsr_timing_enable(int on);
 int gsr_timing_read(double* ms, long long* launches, long long* units, int n);
 

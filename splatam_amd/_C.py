@@ -165,10 +165,12 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
 
 def rasterize_gaussians_dual(background, means3D, colors, colors2, opacity, scales, rotations, scale_modifier,
                              cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh,
-                             degree, campos, prefiltered):
+                             degree, campos, prefiltered, capacity=0, status=None):
     """gsr_forward_dual: rasterize_gaussians with a second precomputed colour set
     composited in the same pass.  Returns (num_rendered, color, color2, radii,
-    geomBuffer, binningBuffer, imgBuffer, depth)."""
+    geomBuffer, binningBuffer, imgBuffer, depth).  capacity > 0 selects
+    gsr_forward_dual_static (no host synchronisation; `status` is a device int32[4]
+    receiving the counters, and num_rendered is the capacity)."""
     device = means3D.device
     if device.type != "cuda":
         raise RuntimeError("splatam_amd rasterizer runs on ROCm devices only (no CPU fallback); "
@@ -188,9 +190,17 @@ def rasterize_gaussians_dual(background, means3D, colors, colors2, opacity, scal
         out_depth = torch.empty(1, H, W, **f32)
         radii = torch.empty(P, dtype=torch.int32, device=device)
         _begin(device)
-        n = lib.gsr_forward_dual(ctypes.byref(s), ctypes.byref(g), _ptr(c2), out_color.data_ptr(),
-                                 out_color2.data_ptr(), out_depth.data_ptr(), radii.data_ptr() if P else None,
-                                 _ALLOC_CB, None, _stream(device))
+        if capacity > 0:
+            if status is None or status.device != device or status.numel() < 4:
+                raise RuntimeError("static dual forward needs a device status tensor of 4 int32")
+            n = lib.gsr_forward_dual_static(ctypes.byref(s), ctypes.byref(g), _ptr(c2), int(capacity),
+                                            status.data_ptr(), out_color.data_ptr(), out_color2.data_ptr(),
+                                            out_depth.data_ptr(), radii.data_ptr() if P else None, _ALLOC_CB, None,
+                                            _stream(device))
+        else:
+            n = lib.gsr_forward_dual(ctypes.byref(s), ctypes.byref(g), _ptr(c2), out_color.data_ptr(),
+                                     out_color2.data_ptr(), out_depth.data_ptr(), radii.data_ptr() if P else None,
+                                     _ALLOC_CB, None, _stream(device))
         _check(n, "rasterize_gaussians_dual")
         bufs = _tls.buffers
         return (int(n), out_color, out_color2, radii, bufs[0], bufs[1], bufs[2], out_depth)

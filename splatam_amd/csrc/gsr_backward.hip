@@ -38,12 +38,12 @@ constexpr int BWD_BATCH = 128;
 template <bool DUAL, bool OPAC, bool COL1, bool COL2>
 __global__ void __launch_bounds__(TILE_PIX, 5)
 render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
-                  const uint2* __restrict__ rect, const uint32_t* __restrict__ offsets,
-                  const float4* __restrict__ rec_a, const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
-                  const float* __restrict__ final_T, const uint32_t* __restrict__ n_contrib,
-                  const float* __restrict__ dL_dpix, const float* __restrict__ colors2,
-                  const float* __restrict__ dL_dpix2, float4* __restrict__ inst) {
+                  const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
+                  const float* __restrict__ final_T,
+                  const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
+                  const float* __restrict__ dL_dpix2, float4* __restrict__ inst, BwdGuard guard) {
     static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
+    if (guard.overflow()) return;  // invalid forward state (static-mode overflow): touch nothing
     constexpr int NV = 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? 3 : 0);
     constexpr int O_OP = 5, O_C1 = 5 + (OPAC ? 1 : 0), O_C2 = O_C1 + (COL1 ? 3 : 0);
     __shared__ float4 s_a[BWD_BATCH];
@@ -86,7 +86,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     // Instances behind every pixel's last contributor receive zero gradient.
     for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {
         const uint32_t gk = point_list[k];
-        const uint32_t u = instance_slot(rect[gk], offsets[gk], blockIdx.x, blockIdx.y);
+        const RenderRec r = load_rr(rr, gk);
+        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), blockIdx.x, blockIdx.y);
         inst[3 * u] = make_float4(0.f, 0.f, 0.f, 0.f);
         inst[3 * u + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
         inst[3 * u + 2] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -103,11 +104,11 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
     uint32_t pu = 0;
     if (tid < min(BWD_BATCH, (int)bmax)) {
-        const uint32_t k = range.x + bmax - 1 - tid;
-        const uint32_t gi = point_list[k];
-        pu = instance_slot(rect[gi], offsets[gi], blockIdx.x, blockIdx.y);
-        pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
-        if (DUAL) pd = make_float4(colors2[3 * gi], colors2[3 * gi + 1], colors2[3 * gi + 2], 0.f);
+        const uint32_t gi = point_list[range.x + bmax - 1 - tid];
+        const RenderRec r = load_rr(rr, gi);
+        pu = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), blockIdx.x, blockIdx.y);
+        pa = r.q0; pb = r.q1; pc = r.q2;
+        if (DUAL) pd = r.q3;
     }
     for (int hi = (int)bmax; hi > 0; hi -= BWD_BATCH) {
         const int cnt = min(BWD_BATCH, hi);
@@ -125,11 +126,11 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         {   // prefetch the next batch
             const int nhi = hi - BWD_BATCH;
             if (tid < min(BWD_BATCH, nhi)) {
-                const uint32_t k = range.x + (uint32_t)(nhi - 1 - tid);
-                const uint32_t gi = point_list[k];
-                pu = instance_slot(rect[gi], offsets[gi], blockIdx.x, blockIdx.y);
-                pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
-                if (DUAL) pd = make_float4(colors2[3 * gi], colors2[3 * gi + 1], colors2[3 * gi + 2], 0.f);
+                const uint32_t gi = point_list[range.x + (uint32_t)(nhi - 1 - tid)];
+                const RenderRec r = load_rr(rr, gi);
+                pu = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), blockIdx.x, blockIdx.y);
+                pa = r.q0; pb = r.q1; pc = r.q2;
+                if (DUAL) pd = r.q3;
             }
         }
         // entries j with pos = hi-1-j >= wmax lie behind every pixel of this wave
@@ -245,7 +246,7 @@ static auto bwd_variant() { return render_bwd_kernel<DUAL, OPAC, COL1, COL2>; }
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
                              const float* colors2, const float* dL_dpix2, unsigned need, float4* inst,
-                             hipStream_t s) {
+                             BwdGuard guard, hipStream_t s) {
     const bool op = need & NEED_OPACITY, c1 = need & NEED_COLORS, c2 = colors2 && (need & NEED_COLORS2);
     auto k = bwd_variant<false, true, true, false>();
     if (!colors2) {
@@ -257,14 +258,14 @@ hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint3
                : (c1 ? (c2 ? bwd_variant<true, 0, 1, 1>() : bwd_variant<true, 0, 1, 0>())
                      : (c2 ? bwd_variant<true, 0, 0, 1>() : bwd_variant<true, 0, 0, 0>()));
     }
-    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rect, geo.offsets,
-                       geo.rec_a, geo.rec_b, geo.rec_c, final_T, n_contrib, dL_dpix, colors2, dL_dpix2, inst);
+    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rr, geo.blocksums,
+                       final_T, n_contrib, dL_dpix, dL_dpix2, inst, guard);
     return hipGetLastError();
 }
 
 __global__ void __launch_bounds__(256)
 gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float4* __restrict__ inst,
-                 GradsOut out) {
+                 GradsOut out, BwdGuard guard) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= g.P) return;
     const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
@@ -275,7 +276,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     float dsh[48];
 #pragma unroll
     for (int k = 0; k < 48; k++) dsh[k] = 0.f;
-    if (radii[i] > 0) {
+    if (radii[i] > 0 && !guard.overflow()) {  // overflow: zero gradients, no record reads
         const uint32_t off = geo.offsets[i], cnt = geo.tiles[i];
         for (uint32_t e = 0; e < cnt; e++) {
             const float4 r0 = inst[3 * (off + e)];
@@ -287,8 +288,9 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
             dcol2[0] += r2.y; dcol2[1] += r2.z; dcol2[2] += r2.w;
         }
         // instance records hold (hx, hy, hxx, hxy, hyy, dopacity, dcolor) sums (render_bwd_kernel)
-        const float4 ra = geo.rec_a[i];
-        const float Cc = geo.rec_b[i].x;
+        const float4* rri = geo.rr + (size_t)RR_F4 * i;
+        const float4 ra = rri[0];
+        const float Cc = rri[1].x;
         const float ddelx = (float)(0.5 * cam.W), ddely = (float)(0.5 * cam.H);  // backward.cu:935-936
         const float hx = g2[0], hy = g2[1];
         g2[0] = -(ra.z * hx + ra.w * hy) * ddelx;
@@ -296,7 +298,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         g2[2] *= -0.5f;
         g2[3] *= -0.5f;
         g2[4] *= -0.5f;
-        const unsigned clamped = __float_as_uint(geo.rec_c[i].w);
+        const unsigned clamped = geo.clamp[i];
         gauss_chain(cam, g, i, g2, clamped, dmean, dcov, dscale, drot, dsh, nsh);
     }
     if (out.dmeans2D) {
@@ -336,9 +338,10 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
 }
 
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float4* inst,
-                            const GradsOut& out, hipStream_t s) {
+                            const GradsOut& out, BwdGuard guard, hipStream_t s) {
     if (g.P == 0) return hipSuccess;
-    hipLaunchKernelGGL(gauss_bwd_kernel, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii, inst, out);
+    hipLaunchKernelGGL(gauss_bwd_kernel, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii, inst, out,
+                       guard);
     return hipGetLastError();
 }
 

@@ -93,12 +93,13 @@ __device__ __forceinline__ float pow_pair(float x, int p) { return p == 2 ? x * 
 template <int NSH>
 __global__ void __launch_bounds__(TILE_PIX)
 render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __restrict__ ranges,
-                        const uint32_t* __restrict__ point_list, const uint2* __restrict__ rect,
-                        const uint32_t* __restrict__ offsets, const float4* __restrict__ rec_a,
-                        const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
+                        const uint32_t* __restrict__ point_list, const float4* __restrict__ rr,
+                        const uint32_t* __restrict__ blocksums,
+                        const uint32_t* __restrict__ clamp_bits,
                         const float4* __restrict__ jac, const float* __restrict__ final_T,
                         const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
-                        float4* __restrict__ rec) {
+                        float4* __restrict__ rec, BwdGuard guard) {
+    if (guard.overflow()) return;
     constexpr int NV = PowerShape<NSH>::NV, NVP = PowerShape<NSH>::NVP, B = PowerShape<NSH>::BATCH;
     constexpr int JF4 = JAC_FLOATS / 4;
     __shared__ float4 s_a[B];
@@ -137,7 +138,8 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
     const uint32_t bmax = max(max(s_wmax[0], s_wmax[1]), max(s_wmax[2], s_wmax[3]));
     for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {
         const uint32_t gk = point_list[k];
-        const uint32_t u = instance_slot(rect[gk], offsets[gk], blockIdx.x, blockIdx.y);
+        const RenderRec r = load_rr(rr, gk);
+        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), blockIdx.x, blockIdx.y);
 #pragma unroll
         for (int m = 0; m < NVP / 4; m++) rec[(size_t)u * (NVP / 4) + m] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -152,12 +154,13 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
         const int cnt = min(B, hi);
         if (tid < cnt) {
             const uint32_t gi = point_list[range.x + (uint32_t)(hi - 1 - tid)];
-            const float4 pa = rec_a[gi], pb = rec_b[gi];
+            const RenderRec r = load_rr(rr, gi);
+            const float4 pa = r.q0, pb = r.q1;
             s_g[tid] = gi;
-            s_u[tid] = instance_slot(rect[gi], offsets[gi], blockIdx.x, blockIdx.y);
+            s_u[tid] = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), blockIdx.x, blockIdx.y);
             s_a[tid] = stage_a(pa, pb);
             s_b[tid] = stage_b(pa, pb);
-            s_c[tid] = rec_c[gi];
+            s_c[tid] = make_float4(r.q2.x, r.q2.y, r.q2.z, __uint_as_float(clamp_bits[gi]));
             s_q[tid] = make_float4(pa.z, pa.w, pb.x, 0.f);
             s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
         }
@@ -273,14 +276,14 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
 hipError_t launch_render_bwd_power(const Camera& cam, const GaussIn& g, const uint2* ranges,
                                    const uint32_t* point_list, GeomPtrs geo, const float* jac, const float* final_T,
                                    const uint32_t* n_contrib, const float* dL_dpix, int power, float* rec,
-                                   hipStream_t s) {
+                                   BwdGuard guard, hipStream_t s) {
     const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
     const int has_scales = g.scales != nullptr;
     const dim3 grid(cam.gx, cam.gy), block(TILE_PIX);
 #define GSR_LAUNCH_POWER(NSH_)                                                                                      \
     hipLaunchKernelGGL(render_bwd_power_kernel<NSH_>, grid, block, 0, s, cam, has_scales, power, ranges, point_list, \
-                       geo.rect, geo.offsets, geo.rec_a, geo.rec_b, geo.rec_c, (const float4*)jac, final_T,        \
-                       n_contrib, dL_dpix, (float4*)rec)
+                       geo.rr, geo.blocksums, geo.clamp, (const float4*)jac, final_T,                                              \
+                       n_contrib, dL_dpix, (float4*)rec, guard)
     switch (nsh) {
         case 0: GSR_LAUNCH_POWER(0); break;
         case 1: GSR_LAUNCH_POWER(1); break;
@@ -297,14 +300,14 @@ hipError_t launch_render_bwd_power(const Camera& cam, const GaussIn& g, const ui
 template <int NSH>
 __global__ void __launch_bounds__(256)
 gauss_bwd_power_kernel(GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float4* __restrict__ rec,
-                       GradsOut out) {
+                       GradsOut out, BwdGuard guard) {
     constexpr int NVP = PowerShape<NSH>::NVP;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= g.P) return;
     float s[NVP];
 #pragma unroll
     for (int m = 0; m < NVP; m++) s[m] = 0.f;
-    if (radii[i] > 0) {
+    if (radii[i] > 0 && !guard.overflow()) {
         const uint32_t off = geo.offsets[i], cnt = geo.tiles[i];
         for (uint32_t e = 0; e < cnt; e++) {
             const float4* r = rec + (size_t)(off + e) * (NVP / 4);
@@ -339,17 +342,17 @@ gauss_bwd_power_kernel(GaussIn g, GeomPtrs geo, const int* __restrict__ radii, c
 }
 
 hipError_t launch_gauss_bwd_power(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii,
-                                  const float* rec, const GradsOut& out, hipStream_t s) {
+                                  const float* rec, const GradsOut& out, BwdGuard guard, hipStream_t s) {
     if (g.P == 0) return hipSuccess;
     const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
     const dim3 grid((g.P + 255) / 256), block(256);
     const float4* r = (const float4*)rec;
     switch (nsh) {
-        case 0: hipLaunchKernelGGL(gauss_bwd_power_kernel<0>, grid, block, 0, s, g, geo, radii, r, out); break;
-        case 1: hipLaunchKernelGGL(gauss_bwd_power_kernel<1>, grid, block, 0, s, g, geo, radii, r, out); break;
-        case 4: hipLaunchKernelGGL(gauss_bwd_power_kernel<4>, grid, block, 0, s, g, geo, radii, r, out); break;
-        case 9: hipLaunchKernelGGL(gauss_bwd_power_kernel<9>, grid, block, 0, s, g, geo, radii, r, out); break;
-        case 16: hipLaunchKernelGGL(gauss_bwd_power_kernel<16>, grid, block, 0, s, g, geo, radii, r, out); break;
+        case 0: hipLaunchKernelGGL(gauss_bwd_power_kernel<0>, grid, block, 0, s, g, geo, radii, r, out, guard); break;
+        case 1: hipLaunchKernelGGL(gauss_bwd_power_kernel<1>, grid, block, 0, s, g, geo, radii, r, out, guard); break;
+        case 4: hipLaunchKernelGGL(gauss_bwd_power_kernel<4>, grid, block, 0, s, g, geo, radii, r, out, guard); break;
+        case 9: hipLaunchKernelGGL(gauss_bwd_power_kernel<9>, grid, block, 0, s, g, geo, radii, r, out, guard); break;
+        case 16: hipLaunchKernelGGL(gauss_bwd_power_kernel<16>, grid, block, 0, s, g, geo, radii, r, out, guard); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -79,6 +79,7 @@ GaussIn make_gauss(const gsr_gaussians* g) {
     o.scales = g->scales;
     o.rotations = g->rotations;
     o.cov3D = g->cov3D_precomp;
+    o.colors2 = nullptr;
     return o;
 }
 
@@ -118,6 +119,11 @@ struct TimedRec {
 };
 struct Timing {
     bool on = false;
+    // device-clock mode (graph-capturable): stamp kernels around the stages in `mask`
+    // accumulate wall_clock64() ticks on the device: [start, sum, count, -] per stage
+    bool clock = false;
+    unsigned mask = 0;
+    unsigned long long* dclock = nullptr;
     std::vector<TimedRec> recs;
     std::vector<hipEvent_t> pool;
     double ms[GSR_NUM_STAGES] = {};
@@ -138,22 +144,48 @@ struct Timing {
 Timing g_timing;
 std::mutex g_timing_mu;
 
+__global__ void stamp_begin_kernel(unsigned long long* c) { c[0] = wall_clock64(); }
+__global__ void stamp_end_kernel(unsigned long long* c) {
+    c[1] += wall_clock64() - c[0];
+    c[2] += 1;
+}
+
+// Inside a stream capture an event record is only an internal dependency unless
+// it is external: then it becomes a graph node re-recorded at every replay, so the
+// stage times read after replays are those of the last replay.
+hipError_t record_event(hipEvent_t e, hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive)
+        return hipEventRecordWithFlags(e, s, hipEventRecordExternal);
+    return hipEventRecord(e, s);
+}
+
 struct StageTimer {  // brackets the launches of one stage
     TimedRec rec{};
     hipStream_t s;
     bool on;
+    unsigned long long* dc = nullptr;
     StageTimer(int stage, long long units, hipStream_t s_) : s(s_), on(g_timing.on) {
         if (!on) return;
+        if (g_timing.clock) {
+            on = false;
+            if ((g_timing.mask >> stage) & 1u) {
+                dc = g_timing.dclock + 4 * stage;
+                hipLaunchKernelGGL(stamp_begin_kernel, dim3(1), dim3(1), 0, s, dc);
+            }
+            return;
+        }
         rec.stage = stage; rec.units = units;
         {
             std::lock_guard<std::mutex> lk(g_timing_mu);
             rec.a = g_timing.take(); rec.b = g_timing.take();
         }
-        (void)hipEventRecord(rec.a, s);
+        (void)record_event(rec.a, s);
     }
     ~StageTimer() {
+        if (dc) hipLaunchKernelGGL(stamp_end_kernel, dim3(1), dim3(1), 0, s, dc);
         if (!on) return;
-        (void)hipEventRecord(rec.b, s);
+        (void)record_event(rec.b, s);
         std::lock_guard<std::mutex> lk(g_timing_mu);
         g_timing.recs.push_back(rec);
     }
@@ -178,6 +210,7 @@ void timing_drain() {  // caller holds g_timing_mu
         g_timing.pool.push_back(r.b);
     }
     g_timing.recs.clear();
+    (void)hipGetLastError();  // an event that was never recorded must not leave a sticky error for torch
 }
 
 }  // namespace
@@ -193,9 +226,12 @@ size_t gsr_binning_buffer_bytes(int num_rendered, int W, int H) { return BinLayo
 size_t gsr_image_buffer_bytes(int W, int H) { return ImgLayout::make(W, H).total; }
 
 // colors2 != NULL: dual render (second colour set composited in the same pass, out_color2)
+// capacity > 0: static mode -- binning buffer of `capacity` instances, no host
+// synchronisation at all (graph-capturable); the device counters are copied to
+// `status` and the call returns `capacity` (the layout size for the backward).
 static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
                         float* out_color, float* out_color2, float* out_depth, int* radii, gsr_alloc_fn alloc,
-                        void* alloc_ctx, void* stream_) {
+                        void* alloc_ctx, void* stream_, int capacity = 0, uint32_t* status = nullptr) {
     int rc = validate(settings, gaussians, true);
     if (rc != GSR_OK) return rc;
     if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
@@ -204,7 +240,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     if (colors2 && gaussians->P > 0 && !gaussians->means3D) return fail(GSR_ERR_INVALID_ARG, "means3D is required");
     hipStream_t stream = (hipStream_t)stream_;
     const Camera cam = make_camera(settings);
-    const GaussIn g = make_gauss(gaussians);
+    GaussIn g = make_gauss(gaussians);
+    g.colors2 = colors2;  // packed into the render records by preprocess (dual render)
     const int P = g.P, W = cam.W, H = cam.H;
     const GeomLayout GL = GeomLayout::make(P);
     const ImgLayout IL = ImgLayout::make(W, H);
@@ -246,20 +283,23 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
                                         ntiles, ranges, stream)) != hipSuccess)
                 return hip_fail(e, "scan");
         }
-        if (!g_pinned.p) {
-            if ((e = hipHostMalloc((void**)&g_pinned.p, 16, hipHostMallocDefault)) != hipSuccess)
-                return hip_fail(e, "hipHostMalloc");
+        if (capacity <= 0) {
+            if (!g_pinned.p) {
+                if ((e = hipHostMalloc((void**)&g_pinned.p, 16, hipHostMallocDefault)) != hipSuccess)
+                    return hip_fail(e, "hipHostMalloc");
+            }
+            if (!g_pinned.ev && (e = hipEventCreateWithFlags(&g_pinned.ev, hipEventDisableTiming)) != hipSuccess)
+                return hip_fail(e, "hipEventCreate");
+            if ((e = hipMemcpyAsync(g_pinned.p, geo.counters, 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+                return hip_fail(e, "copy num_rendered");
+            if ((e = hipEventRecord(g_pinned.ev, stream)) != hipSuccess) return hip_fail(e, "record num_rendered");
         }
-        if (!g_pinned.ev && (e = hipEventCreateWithFlags(&g_pinned.ev, hipEventDisableTiming)) != hipSuccess)
-            return hip_fail(e, "hipEventCreate");
-        if ((e = hipMemcpyAsync(g_pinned.p, geo.counters, 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-            return hip_fail(e, "copy num_rendered");
-        if ((e = hipEventRecord(g_pinned.ev, stream)) != hipSuccess) return hip_fail(e, "record num_rendered");
     } else {
         if ((e = hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)ntiles, stream)) != hipSuccess)
             return hip_fail(e, "memset ranges");
     }
     if (P == 0) {  // rasterize_points.cu:67-81: zero outputs, forward not run
+        if (capacity > 0 && (e = hipMemsetAsync(status, 0, 16, stream)) != hipSuccess) return hip_fail(e, "status");
         void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, BinLayout::make(0, W, H).total);
         if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
         if ((e = hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess ||
@@ -272,9 +312,11 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     // calls' instances-per-Gaussian ratio, so everything is enqueued before the
     // host waits on num_rendered (the reference blocks right after the scan,
     // rasterizer_impl.cu:282, leaving the GPU idle while it launches the rest).
-    static const bool force_radix = getenv("GSR_FORCE_RADIX") && atoi(getenv("GSR_FORCE_RADIX")) != 0;
+    static const bool force_radix_env = getenv("GSR_FORCE_RADIX") && atoi(getenv("GSR_FORCE_RADIX")) != 0;
+    const bool force_radix = force_radix_env && capacity <= 0;
     const double ratio = g_inst_ratio.load(std::memory_order_relaxed);
-    const uint32_t cap = (uint32_t)std::min(2.0e9, std::max(1024.0, 1.5 * ratio * P));
+    const uint32_t cap = capacity > 0 ? (uint32_t)capacity
+                                      : (uint32_t)std::min(2.0e9, std::max(1024.0, 1.5 * ratio * P));
     auto bin_ptrs = [&](void* bin, const BinLayout& BL, uint64_t** keys, uint32_t** vals, uint32_t*& gid,
                         uint32_t*& point_list, uint32_t*& hist) {
         char* bb = (char*)bin;
@@ -315,6 +357,11 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         }
         speculated = true;
     }
+    if (capacity > 0) {  // static mode: report, never wait (an overflow shows in status, outputs invalid)
+        if ((e = hipMemcpyAsync(status, geo.counters, 16, hipMemcpyDeviceToDevice, stream)) != hipSuccess)
+            return hip_fail(e, "copy status");
+        return (int)cap;
+    }
     if ((e = hipEventSynchronize(g_pinned.ev)) != hipSuccess) return hip_fail(e, "sync num_rendered");
     const uint32_t I = g_pinned.p[0];
     const uint32_t longest = g_pinned.p[2];
@@ -348,6 +395,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         }
     } else if (I > 0) {
         // fallback for tiles longer than the LDS sort: global stable LSD radix sort of (tile, depth)
+        if ((e = hipMemsetD32Async((hipDeviceptr_t)(geo.counters + 3), 0xffffffffu, 1, stream)) != hipSuccess)
+            return hip_fail(e, "sort path flag");
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
             if ((e = launch_duplicate(cam, P, geo, keys[0], gid, GL.nb, stream)) != hipSuccess)
@@ -428,11 +477,13 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
             const uint32_t* point_list = (const uint32_t*)((const char*)binning_buffer + BL.point_list);
             StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream);
             if ((e = launch_render_bwd_power(cam, g, ranges, point_list, geo, jac, final_T, n_contrib, dL_dout_color,
-                                             power, rec, stream)) != hipSuccess)
+                                             power, rec, BwdGuard{geo.counters, (uint32_t)num_rendered}, stream)) !=
+                hipSuccess)
                 return hip_fail(e, "render backward (power)");
         }
         StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
-        if ((e = launch_gauss_bwd_power(cam, g, geo, radii, rec, out, stream)) != hipSuccess)
+        if ((e = launch_gauss_bwd_power(cam, g, geo, radii, rec, out, BwdGuard{geo.counters, (uint32_t)num_rendered},
+                                        stream)) != hipSuccess)
             return hip_fail(e, "gaussian backward (power)");
         return GSR_OK;
     }
@@ -449,13 +500,15 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
         const unsigned need = (out.dopacity ? NEED_OPACITY : 0u) | ((out.dcolors || g.shs) ? NEED_COLORS : 0u) |
                               (dcolors2 ? NEED_COLORS2 : 0u);
         if ((e = launch_render_bwd(cam, ranges, point_list, geo, final_T, n_contrib, dL_dout_color, colors2,
-                                   dL_dout_color2, need, inst, stream)) != hipSuccess)
+                                   dL_dout_color2, need, inst, BwdGuard{geo.counters, (uint32_t)num_rendered},
+                                   stream)) != hipSuccess)
             return hip_fail(e, "render backward");
     }
     out.dcolors2 = dcolors2;
     {
         StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
-        if ((e = launch_gauss_bwd(cam, g, geo, radii, inst, out, stream)) != hipSuccess)
+        if ((e = launch_gauss_bwd(cam, g, geo, radii, inst, out, BwdGuard{geo.counters, (uint32_t)num_rendered},
+                                  stream)) != hipSuccess)
             return hip_fail(e, "gaussian backward");
     }
     return GSR_OK;
@@ -476,13 +529,37 @@ int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_timing_mu);
     timing_drain();
     g_timing.on = on != 0;
+    g_timing.clock = on >= GSR_TIMING_CLOCK;
+    g_timing.mask = (unsigned)on & 0xFFu;
     for (int i = 0; i < GSR_NUM_STAGES; i++) { g_timing.ms[i] = 0.0; g_timing.launches[i] = 0; g_timing.units[i] = 0; }
+    if (g_timing.clock) {
+        hipError_t e;
+        if (!g_timing.dclock &&
+            (e = hipMalloc((void**)&g_timing.dclock, 4 * sizeof(unsigned long long) * GSR_NUM_STAGES)) != hipSuccess)
+            return hip_fail(e, "timing clock buffer");
+        if ((e = hipMemset(g_timing.dclock, 0, 4 * sizeof(unsigned long long) * GSR_NUM_STAGES)) != hipSuccess)
+            return hip_fail(e, "timing clock reset");
+    }
     return GSR_OK;
 }
 
 int gsr_timing_read(double* ms, long long* launches, long long* units, int n) {
     std::lock_guard<std::mutex> lk(g_timing_mu);
     timing_drain();
+    if (g_timing.clock && g_timing.dclock) {
+        unsigned long long h[4 * GSR_NUM_STAGES];
+        int dev = 0, khz = 0;
+        hipError_t e;
+        if ((e = hipMemcpy(h, g_timing.dclock, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "timing clock read");
+        if ((e = hipGetDevice(&dev)) != hipSuccess ||
+            (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev)) != hipSuccess || khz <= 0)
+            return fail(GSR_ERR_HIP, "wall clock rate unavailable");
+        for (int i = 0; i < GSR_NUM_STAGES; i++) {
+            g_timing.ms[i] = (double)h[4 * i + 1] / (double)khz;
+            g_timing.launches[i] = (long long)h[4 * i + 2];
+        }
+    }
     for (int i = 0; i < n && i < GSR_NUM_STAGES; i++) {
         if (ms) ms[i] = g_timing.ms[i];
         if (launches) launches[i] = g_timing.launches[i];
@@ -509,6 +586,15 @@ int gsr_forward_dual(const gsr_settings* settings, const gsr_gaussians* gaussian
     if (!colors2) return fail(GSR_ERR_INVALID_ARG, "colors2 required");
     return forward_impl(settings, gaussians, colors2, out_color, out_color2, out_depth, radii, alloc, alloc_ctx,
                         stream);
+}
+
+int gsr_forward_dual_static(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
+                            int capacity, unsigned* status, float* out_color, float* out_color2, float* out_depth,
+                            int* radii, gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
+    if (!colors2) return fail(GSR_ERR_INVALID_ARG, "colors2 required");
+    if (capacity <= 0 || !status) return fail(GSR_ERR_INVALID_ARG, "static mode needs capacity > 0 and status");
+    return forward_impl(settings, gaussians, colors2, out_color, out_color2, out_depth, radii, alloc, alloc_ctx,
+                        stream, capacity, status);
 }
 
 int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,

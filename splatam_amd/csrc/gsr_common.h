@@ -30,13 +30,19 @@ constexpr int TILE_CTR_STRIDE = 64;  // per-tile atomic counters one 256-B line 
 // ---------------------------------------------------------------- layouts --
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// One 64-byte render record per Gaussian (four float4, one cache-line fetch per
+// gather in the render kernels; the SoA form cost ~6 line fetches per instance):
+//   q0 = (x, y, conic A, conic B)     pixel coordinates
+//   q1 = (conic C, opacity, depth, workgroup-local instance offset bits)
+//   q2 = (r, g, b, tile rect lo bits)   rect lo = x0 | y0 << 16
+//   q3 = (colors2 r, g, b, tile rect hi bits)   rect hi = x1 | y1 << 16; colors2 = 0 unless dual
+constexpr int RR_F4 = 4;
 struct GeomLayout {       // per-Gaussian state ("geomBuffer")
-    size_t rec_a;         // float4 [P]  (x, y, conic A, conic B)   pixel coordinates
-    size_t rec_b;         // float4 [P]  (conic C, opacity, depth, 0)
-    size_t rec_c;         // float4 [P]  (r, g, b, clamped bits)
-    size_t rect;          // uint2  [P]  tile rect (x0 | y0<<16, x1 | y1<<16)
+    size_t rr;            // float4 [P][4] render records
+    size_t clamp;         // u32    [P]  SH clamp bits (r, g, b)
+    size_t bin;           // uint4  [P]  (rect lo, rect hi, depth bits, tiles) for duplicate
     size_t tiles;         // u32    [P]  tiles touched
-    size_t offsets;       // u32    [P]  exclusive instance offset
+    size_t offsets;       // u32    [P]  exclusive instance offset (also in q1.w)
     size_t blocksums;     // u32    [nb] per-workgroup tile sums -> exclusive scan
     size_t counters;      // u32    [4]  [0]=num_rendered [1]=prefiltered violation [2]=longest tile list
     size_t total;
@@ -45,10 +51,9 @@ struct GeomLayout {       // per-Gaussian state ("geomBuffer")
         GeomLayout L;
         size_t o = 0, p = (size_t)(P > 0 ? P : 1);
         L.nb = (P + PRE_BLOCK - 1) / PRE_BLOCK;
-        L.rec_a = o; o = align_up(o + 16 * p, 256);
-        L.rec_b = o; o = align_up(o + 16 * p, 256);
-        L.rec_c = o; o = align_up(o + 16 * p, 256);
-        L.rect = o; o = align_up(o + 8 * p, 256);
+        L.rr = o; o = align_up(o + 16 * RR_F4 * p, 256);
+        L.clamp = o; o = align_up(o + 4 * p, 256);
+        L.bin = o; o = align_up(o + 16 * p, 256);
         L.tiles = o; o = align_up(o + 4 * p, 256);
         L.offsets = o; o = align_up(o + 4 * p, 256);
         L.blocksums = o; o = align_up(o + 4 * (size_t)(L.nb > 0 ? L.nb : 1), 256);
@@ -140,24 +145,40 @@ struct GaussIn {
     const float* scales;
     const float* rotations;
     const float* cov3D;
+    const float* colors2;  // second precomputed colour set of a dual render (else nullptr)
 };
 
 struct GeomPtrs {
-    float4* rec_a;
-    float4* rec_b;
-    float4* rec_c;
-    uint2* rect;
+    float4* rr;
+    uint32_t* clamp;
+    uint4* bin;
     uint32_t* tiles;
     uint32_t* offsets;
     uint32_t* blocksums;
     uint32_t* counters;
     static GeomPtrs at(void* base, const GeomLayout& L) {
         char* b = (char*)base;
-        return {(float4*)(b + L.rec_a), (float4*)(b + L.rec_b), (float4*)(b + L.rec_c), (uint2*)(b + L.rect),
-                (uint32_t*)(b + L.tiles), (uint32_t*)(b + L.offsets), (uint32_t*)(b + L.blocksums),
-                (uint32_t*)(b + L.counters)};
+        return {(float4*)(b + L.rr), (uint32_t*)(b + L.clamp), (uint4*)(b + L.bin), (uint32_t*)(b + L.tiles),
+                (uint32_t*)(b + L.offsets),
+                (uint32_t*)(b + L.blocksums), (uint32_t*)(b + L.counters)};
     }
 };
+
+// Render record accessors
+struct RenderRec {
+    float4 q0, q1, q2, q3;
+};
+__device__ __forceinline__ RenderRec load_rr(const float4* __restrict__ rr, uint32_t i) {
+    const float4* r = rr + (size_t)RR_F4 * i;
+    return {r[0], r[1], r[2], r[3]};
+}
+__device__ __forceinline__ uint2 rr_rect(const RenderRec& r) {
+    return make_uint2(__float_as_uint(r.q2.w), __float_as_uint(r.q3.w));
+}
+// instance offset of Gaussian i: scanned workgroup base + workgroup-local part (q1.w)
+__device__ __forceinline__ uint32_t rr_offset(const RenderRec& r, const uint32_t* blocksums, uint32_t i) {
+    return blocksums[i / PRE_BLOCK] + __float_as_uint(r.q1.w);
+}
 
 // ------------------------------------------------------------ device math --
 // The functions below restate forward.cu / backward.cu / auxiliary.h in
@@ -483,6 +504,17 @@ __device__ __forceinline__ void wave_reduce_n(const float (&v)[N], float (&r)[N 
     for (int m = 0; m < N / 4; m++) r[m] = row16_sum(swapsum16(r1[m], r1[m + N / 4]));
 }
 
+// inclusive scan over the 64 lanes
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = __lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // Lanes of the wave whose 8-bit digit equals mine (valid lanes only).
@@ -522,6 +554,19 @@ struct SpecGuard {
         return counters[0] > cap_inst || counters[2] > cap_tile;
     }
 };
+// Backward-side check that the forward state is valid for a binning layout of
+// `cap_inst` instances: counters[3] holds the longest tile list the sort path
+// that produced point_list handles (TILE_SORT_CAP for the LDS tile sort,
+// 0xffffffff for the radix fallback), set by the forward.  Only a static-mode
+// forward can leave it failing; the backward kernels then do no work (no
+// out-of-bounds access) and the gradients are zero.
+struct BwdGuard {
+    const uint32_t* counters;
+    uint32_t cap_inst;
+    __device__ __forceinline__ bool overflow() const {
+        return counters[0] > cap_inst || counters[2] > counters[3];
+    }
+};
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
                                    bool lds_hist, int ntiles, uint64_t* keys, int nb, SpecGuard guard, hipStream_t s);
 hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint32_t* point_list,
@@ -536,7 +581,7 @@ hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint3
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* vis, hipStream_t s);
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
-                             const float* colors2, const float* dL_dpix2, unsigned need, float4* inst,
+                             const float* colors2, const float* dL_dpix2, unsigned need, float4* inst, BwdGuard guard,
                              hipStream_t s);
 // which optional per-pair sums render_bwd forms (the geometric ones always)
 constexpr unsigned NEED_OPACITY = 1u, NEED_COLORS = 2u, NEED_COLORS2 = 4u;
@@ -552,7 +597,7 @@ struct GradsOut {
     float* dcolors2;  // second colour set of a dual render (nullptr otherwise)
 };
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float4* inst,
-                            const GradsOut& out, hipStream_t s);
+                            const GradsOut& out, BwdGuard guard, hipStream_t s);
 hipError_t launch_selftest_reduce9(const float* in, float* out, hipStream_t s);
 // error reporting shared by the C entry points (gsr_last_error)
 int fail(int code, const std::string& msg);
@@ -565,8 +610,8 @@ hipError_t launch_gauss_jac(const Camera& cam, const GaussIn& g, GeomPtrs geo, c
 hipError_t launch_render_bwd_power(const Camera& cam, const GaussIn& g, const uint2* ranges,
                                    const uint32_t* point_list, GeomPtrs geo, const float* jac, const float* final_T,
                                    const uint32_t* n_contrib, const float* dL_dpix, int power, float* rec,
-                                   hipStream_t s);
+                                   BwdGuard guard, hipStream_t s);
 hipError_t launch_gauss_bwd_power(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii,
-                                  const float* rec, const GradsOut& out, hipStream_t s);
+                                  const float* rec, const GradsOut& out, BwdGuard guard, hipStream_t s);
 
 }  // namespace gsr

@@ -33,6 +33,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     }
     const int i = blockIdx.x * PRE_BLOCK + threadIdx.x;
     uint32_t tiles = 0;
+    float4 q1;
     if (i < g.P) {
         int radius = 0;
         float3 p = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
@@ -77,10 +78,18 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                     sh_fwd(cam.sh_degree, p, cam.campos, g.shs + (size_t)3 * g.M * i, rgb, clamped);
                 }
                 radius = (int)rad;
-                geo.rec_a[i] = make_float4(px, py, ca, cb);
-                geo.rec_b[i] = make_float4(cc, g.opacities[i], pv.z, 0.f);
-                geo.rec_c[i] = make_float4(rgb[0], rgb[1], rgb[2], __uint_as_float(clamped));
-                geo.rect[i] = make_uint2((uint32_t)x0 | ((uint32_t)y0 << 16), (uint32_t)x1 | ((uint32_t)y1 << 16));
+                float c2[3] = {0.f, 0.f, 0.f};
+                if (g.colors2) {
+                    c2[0] = g.colors2[3 * i]; c2[1] = g.colors2[3 * i + 1]; c2[2] = g.colors2[3 * i + 2];
+                }
+                const uint32_t rlo = (uint32_t)x0 | ((uint32_t)y0 << 16), rhi = (uint32_t)x1 | ((uint32_t)y1 << 16);
+                float4* rr = geo.rr + (size_t)RR_F4 * i;
+                rr[0] = make_float4(px, py, ca, cb);
+                rr[2] = make_float4(rgb[0], rgb[1], rgb[2], __uint_as_float(rlo));
+                rr[3] = make_float4(c2[0], c2[1], c2[2], __uint_as_float(rhi));
+                q1 = make_float4(cc, g.opacities[i], pv.z, 0.f);  // .w: workgroup-local instance offset, below
+                geo.bin[i] = make_uint4(rlo, rhi, __float_as_uint(pv.z), tiles);
+                geo.clamp[i] = clamped;
                 for (int ty = y0; ty < y1; ty++)  // per-tile instance counts -> bucket ranges
                     for (int tx = x0; tx < x1; tx++) {
                         if (LDS_HIST) atomicAdd(&s_hist[ty * cam.gx + tx], 1u);
@@ -90,20 +99,23 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
         }
         radii[i] = radius;
         geo.tiles[i] = tiles;
+        if (tiles == 0) geo.bin[i] = make_uint4(0u, 0u, 0u, 0u);
     }
-    // workgroup sum of tiles touched (input of the two-level scan)
+    // workgroup scan of tiles touched: the local instance offset goes into the render
+    // record (q1.w; the render kernels add the scanned workgroup base, blocksums[i >> 10]),
+    // the workgroup total into blocksums (input of the two-level scan)
     __shared__ uint32_t wsum[PRE_BLOCK / 64];
-    uint32_t v = tiles;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t incl = wave_incl_scan(tiles);
+    if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t sum = 0;
-#pragma unroll
-        for (int k = 0; k < PRE_BLOCK / 64; k++) sum += wsum[k];
-        geo.blocksums[blockIdx.x] = sum;
+    uint32_t woff = 0;
+    for (int k = 0; k < wv; k++) woff += wsum[k];
+    if (tiles) {
+        q1.w = __uint_as_float(woff + incl - tiles);
+        geo.rr[(size_t)RR_F4 * i + 1] = q1;
     }
+    if (threadIdx.x == PRE_BLOCK - 1) geo.blocksums[blockIdx.x] = woff + incl;
     if (LDS_HIST)
         for (int t = threadIdx.x; t < ntiles; t += PRE_BLOCK) counts[(size_t)blockIdx.x * ntiles + t] = s_hist[t];
 }
@@ -163,15 +175,6 @@ hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* t
 constexpr int SCAN_THREADS = 1024;
 constexpr int SCAN_ITEMS = 4;
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const int lane = __lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = __shfl_up(v, o);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
 
 __global__ void __launch_bounds__(SCAN_THREADS) exclusive_scan_kernel(uint32_t* data, uint32_t n, uint32_t* total) {
     __shared__ uint32_t wsums[SCAN_THREADS / 64];
@@ -222,7 +225,7 @@ hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hi
 __global__ void __launch_bounds__(SCAN_THREADS)
 scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t* __restrict__ tile_count,
                    uint32_t tile_stride, uint32_t ntiles, uint2* __restrict__ ranges,
-                   uint32_t* __restrict__ counters) {
+                   uint32_t* __restrict__ counters, uint32_t sort_cap) {
     __shared__ uint32_t wsums[SCAN_THREADS / 64];
     __shared__ uint32_t s_carry, s_max;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -266,8 +269,12 @@ scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t
         atomicMax(&s_max, vmax);
         __syncthreads();
         if (tid == 0) {
-            if (pass == 0) counters[0] = s_carry;
-            else counters[2] = s_max;
+            if (pass == 0) {
+                counters[0] = s_carry;
+            } else {
+                counters[2] = s_max;
+                counters[3] = sort_cap;  // longest list the tile sort will handle (BwdGuard)
+            }
         }
         __syncthreads();
     }
@@ -276,7 +283,7 @@ scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t
 hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
                               uint2* ranges, hipStream_t s) {
     hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, geo.blocksums, (uint32_t)nb, tile_count,
-                       (uint32_t)tile_stride, (uint32_t)ntiles, ranges, geo.counters);
+                       (uint32_t)tile_stride, (uint32_t)ntiles, ranges, geo.counters, (uint32_t)TILE_SORT_CAP);
     return hipGetLastError();
 }
 
@@ -292,11 +299,11 @@ duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, u
     uint32_t incl = wave_incl_scan(t);
     if (lane == 63) wsum[w] = incl;
     if (t) {
-        uint2 r = geo.rect[i];
+        const uint4 r = geo.bin[i];  // (rect lo, rect hi, depth bits, tiles)
         s_x0[tid] = r.x & 0xFFFFu;
         s_y0[tid] = r.x >> 16;
         s_w[tid] = (r.y & 0xFFFFu) - (r.x & 0xFFFFu);
-        s_depth[tid] = __float_as_uint(geo.rec_b[i].z);
+        s_depth[tid] = r.z;
     }
     __syncthreads();
     uint32_t woff = 0;
@@ -356,11 +363,11 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict
     uint32_t incl = wave_incl_scan(t);
     if (lane == 63) wsum[w] = incl;
     if (t) {
-        uint2 r = geo.rect[i];
+        const uint4 r = geo.bin[i];  // (rect lo, rect hi, depth bits, tiles)
         s_x0[tid] = r.x & 0xFFFFu;
         s_y0[tid] = r.x >> 16;
         s_w[tid] = (r.y & 0xFFFFu) - (r.x & 0xFFFFu);
-        s_depth[tid] = __float_as_uint(geo.rec_b[i].z);
+        s_depth[tid] = r.z;
     }
     __syncthreads();
     uint32_t woff = 0;
@@ -596,8 +603,7 @@ hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t
 template <bool DUAL>
 __global__ void __launch_bounds__(TILE_PIX, 5)
 render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
-                  const float4* __restrict__ rec_a, const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
-                  const float* __restrict__ colors2, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
+                  const float4* __restrict__ rr, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                   float* __restrict__ out_color, float* __restrict__ out_color2, float* __restrict__ out_depth,
                   SpecGuard guard) {
     if (guard.overflow()) return;
@@ -621,9 +627,9 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     uint32_t last = 0;
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
     if (range.x + tid < range.y) {
-        const uint32_t gi = point_list[range.x + tid];
-        pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
-        if (DUAL) pd = make_float4(colors2[3 * gi], colors2[3 * gi + 1], colors2[3 * gi + 2], 0.f);
+        const RenderRec r = load_rr(rr, point_list[range.x + tid]);
+        pa = r.q0; pb = r.q1; pc = r.q2;
+        if (DUAL) pd = r.q3;
     }
     for (uint32_t start = range.x; start < range.y; start += RENDER_BATCH) {
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
@@ -639,9 +645,9 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         {   // prefetch the next batch while this one is rasterised
             const uint32_t k = start + RENDER_BATCH + tid;
             if (k < range.y) {
-                const uint32_t gi = point_list[k];
-                pa = rec_a[gi]; pb = rec_b[gi]; pc = rec_c[gi];
-                if (DUAL) pd = make_float4(colors2[3 * gi], colors2[3 * gi + 1], colors2[3 * gi + 2], 0.f);
+                const RenderRec r = load_rr(rr, point_list[k]);
+                pa = r.q0; pb = r.q1; pc = r.q2;
+                if (DUAL) pd = r.q3;
             }
         }
         const int n = build_strip_list(s_mask, cnt, w, 0, s_list[w]);
@@ -709,8 +715,8 @@ hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint3
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s) {
     auto k = colors2 ? render_fwd_kernel<true> : render_fwd_kernel<false>;
-    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rec_a, geo.rec_b,
-                       geo.rec_c, colors2, final_T, n_contrib, out_color, out_color2, out_depth, guard);
+    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rr, final_T,
+                       n_contrib, out_color, out_color2, out_depth, guard);
     return hipGetLastError();
 }
 

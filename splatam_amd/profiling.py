@@ -9,8 +9,20 @@ from ._lib import lib
 STAGES = ("preprocess", "duplicate", "sort", "ranges", "render_fwd", "render_bwd", "gauss_bwd")
 
 
-def enable_timing(on: bool = True) -> None:
-    lib.gsr_timing_enable(1 if on else 0)
+GSR_TIMING_CLOCK = 0x100
+
+
+def enable_timing(on: bool = True, clock_stages=None) -> None:
+    """on: hipEvents around every stage.  clock_stages (names): device-clock
+    stamps around those stages only -- works inside captured HIP graphs and
+    accumulates over every replay."""
+    if clock_stages:
+        mask = 0
+        for name in clock_stages:
+            mask |= 1 << STAGES.index(name)
+        lib.gsr_timing_enable(GSR_TIMING_CLOCK | mask)
+    else:
+        lib.gsr_timing_enable(1 if on else 0)
 
 
 def read_timing() -> dict:

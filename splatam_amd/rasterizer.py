@@ -72,31 +72,34 @@ class _RasterizeGaussians(torch.autograd.Function):
 
 
 def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations,
-                             cov3Ds_precomp, raster_settings):
+                             cov3Ds_precomp, raster_settings, capacity=0, status=None):
     """Two GaussianRasterizer calls on identical geometry fused into one
     rasterization: SplaTAM renders RGB and the [z, 1, z^2]
     depth/silhouette image from the same means / scales / rotations / opacities
     and camera (scripts/splatam.py:255,259).  Returns (color, color2, radii,
     depth); each image is bitwise what a separate call returns, and the gradients
     of the shared inputs are the sums over both images, as autograd would
-    accumulate them over two calls (means2D receives that sum as well)."""
+    accumulate them over two calls (means2D receives that sum as well).
+    capacity > 0: synchronisation-free static mode (gsr_forward_dual_static),
+    for HIP-graph capture; check `status` (device int32[4]) afterwards."""
     empty = torch.Tensor([])
     return _RasterizeGaussiansDual.apply(means3D, means2D, empty if sh is None else sh,
                                          empty if colors_precomp is None else colors_precomp, colors2, opacities,
                                          empty if scales is None else scales,
                                          empty if rotations is None else rotations,
-                                         empty if cov3Ds_precomp is None else cov3Ds_precomp, raster_settings)
+                                         empty if cov3Ds_precomp is None else cov3Ds_precomp, raster_settings,
+                                         capacity, status)
 
 
 class _RasterizeGaussiansDual(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings):
+                raster_settings, capacity, status):
         s = raster_settings
         num_rendered, color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth = _C.rasterize_gaussians_dual(
             s.bg, means3D, colors_precomp, colors2, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
-            s.campos, s.prefiltered)
+            s.campos, s.prefiltered, capacity=capacity, status=status)
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
         ctx.save_for_backward(colors_precomp, colors2, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
@@ -121,7 +124,7 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
             geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, needs=needs)
         if not n[0]:
             g_m3 = None
-        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None
+        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None, None, None
 
 
 class GaussianRasterizer(nn.Module):

@@ -132,14 +132,15 @@ def fused_eligible(params, curr_data, cfg: TrackingConfig) -> bool:
             and curr_data["im"].dim() == 3 and curr_data["depth"].dim() == 3)
 
 
-def _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg: TrackingConfig, dual=True):
+def _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg: TrackingConfig, dual=True, capacity=0,
+                             status=None):
     from .glue import track_transform, tracking_l1
     means, rots, dcol, opac, scales = track_transform(params, iter_time_idx, curr_data["w2c"])
     P = means.shape[0]
     means2D = torch.zeros(P, 3, device=means.device, requires_grad=True)
     if dual:  # both renders in one rasterization (means2D.grad then holds the sum over both images)
         im, depth_sil, radius, _ = rasterize_gaussians_dual(means, means2D, None, params["rgb_colors"], dcol, opac,
-                                                            scales, rots, None, curr_data["cam"])
+                                                            scales, rots, None, curr_data["cam"], capacity, status)
     else:
         means2D_ds = torch.zeros(P, 3, device=means.device, requires_grad=True)
         ras = GaussianRasterizer(raster_settings=curr_data["cam"])

@@ -1,0 +1,99 @@
+"""SplaTAM tracking iterations replayed as one HIP graph.
+
+scripts/splatam.py tracks every frame with a fixed number of iterations
+(configs/replica/splatam.py:59: 40) of get_loss(tracking=True) + backward +
+Adam on the camera pose.  Each iteration is ~15 kernel launches whose host
+cost (Python, autograd, ctypes) exceeds their GPU time once the rasterizer is
+fast, so the iterations are captured once into a torch.cuda.CUDAGraph
+(hipGraph) and replayed: the host issues one launch per `iters_per_graph`
+iterations.
+
+Capture requires a forward that never waits on the host: the dual forward runs
+in its static mode (gsr_forward_dual_static) with a binning capacity taken
+from an eager probe of the same frame times `headroom`.  Every captured
+iteration copies its binning counters into its own row of `status`;
+`overflowed()` reads them (one host sync) and reports whether any iteration
+exceeded the capacity (its outputs would then be invalid -- rebuild the
+tracker with more headroom and re-run the frame).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _C
+from .layout import views
+from .rasterizer import GaussianRasterizationSettings
+from .slam import TrackingConfig, _get_loss_tracking_fused, fused_eligible
+
+TILE_SORT_CAP = 4096  # longest tile list the static mode handles (LDS tile sort)
+
+
+def probe_num_rendered(params, curr_data, time_idx) -> tuple[int, int]:
+    """(num_rendered, longest tile list) of the frame at the current pose (eager, synchronous)."""
+    from .glue import track_transform
+    cam: GaussianRasterizationSettings = curr_data["cam"]
+    with torch.no_grad():
+        means, rots, dcol, opac, scales = track_transform(params, time_idx, curr_data["w2c"])
+        out = _C.rasterize_gaussians_dual(cam.bg, means, params["rgb_colors"], dcol, opac, scales, rots,
+                                          cam.scale_modifier, torch.Tensor([]), cam.viewmatrix, cam.projmatrix,
+                                          cam.tanfovx, cam.tanfovy, cam.image_height, cam.image_width,
+                                          torch.Tensor([]), cam.sh_degree, cam.campos, cam.prefiltered)
+        n, img, binning = out[0], out[6], out[5]
+        r = views(img, binning, cam.image_width, cam.image_height, n)["ranges"]
+        longest = int((r[:, 1] - r[:, 0]).max().item()) if r.numel() else 0
+    return int(n), longest
+
+
+class GraphTracker:
+    def __init__(self, params: dict, curr_data: dict, time_idx: int, iters_per_graph: int = 20,
+                 cfg: TrackingConfig = TrackingConfig(), lrs=(0.0004, 0.002), headroom: float = 1.5,
+                 warmup_iters: int = 3, min_extra: int = 65536, timing: bool = False):
+        if not fused_eligible(params, curr_data, cfg):
+            raise RuntimeError("GraphTracker needs the fused tracking configuration (only the pose requires grad)")
+        self.params, self.curr, self.t, self.cfg = params, curr_data, time_idx, cfg
+        dev = params["means3D"].device
+        n, longest = probe_num_rendered(params, curr_data, time_idx)
+        if longest > TILE_SORT_CAP:
+            raise RuntimeError(f"a tile list of {longest} > {TILE_SORT_CAP}: use the eager (synchronous) path")
+        self.capacity = max(1, int(headroom * n) + int(min_extra))
+        self.iters = int(iters_per_graph)
+        self.status = torch.zeros(self.iters, 4, dtype=torch.int32, device=dev)
+        rots, trans = params["cam_unnorm_rots"], params["cam_trans"]
+        if not (rots.is_leaf and trans.is_leaf and rots.requires_grad and trans.requires_grad):
+            raise RuntimeError("cam_unnorm_rots / cam_trans must be leaf tensors requiring grad")
+        self.opt = torch.optim.Adam([{"params": [rots], "lr": lrs[0]}, {"params": [trans], "lr": lrs[1]}],
+                                    fused=True, capturable=True)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # warm-up iterations (real tracking iterations) outside the capture
+            for _ in range(max(1, warmup_iters)):
+                self._iteration(0)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        if timing:  # device-clock stamps around render_bwd become graph nodes (accumulate over replays)
+            from . import profiling
+            torch.cuda.synchronize(dev)
+            profiling.enable_timing(clock_stages=("render_bwd",))
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            for k in range(self.iters):
+                self.loss = self._iteration(k)
+
+    def _iteration(self, k: int):
+        self.opt.zero_grad(set_to_none=False)
+        loss, _, _ = _get_loss_tracking_fused(self.params, self.curr, self.t, self.cfg, dual=True,
+                                              capacity=self.capacity, status=self.status[k])
+        loss.backward()
+        self.opt.step()
+        return loss.detach()
+
+    def run(self):
+        """Enqueue `iters_per_graph` tracking iterations (one graph launch, no host sync)."""
+        self.graph.replay()
+
+    def overflowed(self) -> bool:
+        """True if any iteration of the last replay exceeded the binning capacity (one host sync)."""
+        st = self.status.cpu()
+        return bool((st[:, 0] > self.capacity).any() or (st[:, 2] > TILE_SORT_CAP).any() or (st[:, 1] != 0).any())
+
+    def num_rendered(self) -> list[int]:
+        return [int(x) for x in self.status[:, 0].cpu()]
