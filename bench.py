@@ -162,7 +162,8 @@ def main():
     stages = profiling.read_timing()
     profiling.enable_timing(False)
     if tracker is not None and tracker.overflowed():
-        raise SystemExit("binning capacity overflow during the timed replays: measurement invalid")
+        raise SystemExit(f"binning capacity overflow during the timed replays (capacity {tracker.capacity}, "
+                         f"status rows {tracker.status.cpu().tolist()}): measurement invalid")
     elapsed = sd.max_over_ranks(t1 - t0, device=dev)
     frames = steps * world
     value = frames / elapsed

@@ -144,6 +144,12 @@ struct Timing {
 Timing g_timing;
 std::mutex g_timing_mu;
 
+// 4-word counter copies / resets as kernels: plain kernel nodes when captured in a
+// HIP graph (small memcpy / memset nodes misbehaved on re-replay here)
+__global__ void copy4_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src) {
+    if (threadIdx.x < 4) dst[threadIdx.x] = src ? src[threadIdx.x] : 0u;
+}
+
 __global__ void stamp_begin_kernel(unsigned long long* c) { c[0] = wall_clock64(); }
 __global__ void stamp_end_kernel(unsigned long long* c) {
     c[1] += wall_clock64() - c[0];
@@ -271,7 +277,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     }
     if (P > 0) {
         if (!radii) return fail(GSR_ERR_INVALID_ARG, "radii output required");
-        if ((e = hipMemsetAsync(geo.counters, 0, 16, stream)) != hipSuccess) return hip_fail(e, "memset counters");
+        hipLaunchKernelGGL(copy4_kernel, dim3(1), dim3(64), 0, stream, geo.counters, (const uint32_t*)nullptr);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "reset counters");
         {
             StageTimer t(GSR_STAGE_PREPROCESS, P, stream);
             if ((e = launch_preprocess(cam, g, geo, radii, lds_hist ? cmat : tile_count, lds_hist, ntiles, GL.nb,
@@ -299,7 +306,10 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
             return hip_fail(e, "memset ranges");
     }
     if (P == 0) {  // rasterize_points.cu:67-81: zero outputs, forward not run
-        if (capacity > 0 && (e = hipMemsetAsync(status, 0, 16, stream)) != hipSuccess) return hip_fail(e, "status");
+        if (capacity > 0) {
+            hipLaunchKernelGGL(copy4_kernel, dim3(1), dim3(64), 0, stream, status, (const uint32_t*)nullptr);
+            if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "status");
+        }
         void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, BinLayout::make(0, W, H).total);
         if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
         if ((e = hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess ||
@@ -358,8 +368,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         speculated = true;
     }
     if (capacity > 0) {  // static mode: report, never wait (an overflow shows in status, outputs invalid)
-        if ((e = hipMemcpyAsync(status, geo.counters, 16, hipMemcpyDeviceToDevice, stream)) != hipSuccess)
-            return hip_fail(e, "copy status");
+        hipLaunchKernelGGL(copy4_kernel, dim3(1), dim3(64), 0, stream, status, (const uint32_t*)geo.counters);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "copy status");
         return (int)cap;
     }
     if ((e = hipEventSynchronize(g_pinned.ev)) != hipSuccess) return hip_fail(e, "sync num_rendered");

@@ -74,7 +74,8 @@ class GraphTracker:
             torch.cuda.synchronize(dev)
             profiling.enable_timing(clock_stages=("render_bwd",))
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        self.stream = side
+        with torch.cuda.graph(self.graph, stream=side):  # capture on the warm-up stream (autograd nodes live there)
             for k in range(self.iters):
                 self.loss = self._iteration(k)
 
