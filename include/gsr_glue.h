@@ -57,6 +57,19 @@ int gsr_track_transform_bwd(int P, const float* means_world, const float* unnorm
                             const float* dL_dmeans_cam, const float* dL_drot, const float* dL_ddepth_colors,
                             float* dL_dcam_q, float* dL_dcam_t, int q_stride, float* scratch, void* stream);
 
+/* gsr_track_transform_bwd with the optimizer step fused in:
+ * instead of writing the pose gradient, applies torch.optim.Adam (no weight
+ * decay, no amsgrad; the tracking optimizer of scripts/splatam.py) to the
+ * frame's pose column in place: cam_q (4 values) / cam_t (3 values) at stride
+ * q_stride.  adam_state: device, 15 floats [m_q 4, v_q 4, m_t 3, v_t 3, step],
+ * zero-initialised by the caller per frame (SplaTAM re-creates the optimizer per
+ * frame). */
+int gsr_track_transform_bwd_adam(int P, const float* means_world, const float* unnorm_rot, int scale_cols,
+                                 float* cam_q, float* cam_t, int q_stride, const float* means_cam,
+                                 const float* w2c, const float* dL_dmeans_cam, const float* dL_drot,
+                                 const float* dL_ddepth_colors, float lr_q, float lr_t, float beta1,
+                                 float beta2, float eps, float* adam_state, float* scratch, void* stream);
+
 /* im [3,H,W], depth_sil [3,H,W] (depth, silhouette, depth^2), gt_im [3,H,W], gt_depth [1,H,W].
  * loss: 1 float (device).  scratch: gsr_track_scratch_floats(H*W) floats. */
 int gsr_track_l1_fwd(int H, int W, const float* im, const float* depth_sil, const float* gt_im,

@@ -65,6 +65,10 @@ SIGNATURES = {
                                         c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gsr_track_transform_bwd": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "gsr_track_transform_bwd_adam": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                             c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.c_float,
+                                             ctypes.c_float, ctypes.c_float, ctypes.c_float, c_void_p, c_void_p,
+                                             c_void_p]),
     "gsr_track_l1_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
                                  ctypes.c_float, ctypes.c_float, c_void_p, c_void_p, c_void_p]),
     "gsr_track_l1_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,

@@ -149,6 +149,17 @@ std::mutex g_timing_mu;
 __global__ void copy4_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src) {
     if (threadIdx.x < 4) dst[threadIdx.x] = src ? src[threadIdx.x] : 0u;
 }
+__global__ void zero_words_kernel(uint32_t* __restrict__ p, size_t n) {
+    for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) p[k] = 0u;
+}
+// zero-fill as a kernel (a memset node in a captured graph was not re-executed on replay)
+hipError_t zero_async(void* p, size_t bytes, hipStream_t s) {
+    const size_t n = bytes / 4;
+    if (n == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<size_t>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(zero_words_kernel, dim3(blocks), dim3(256), 0, s, (uint32_t*)p, n);
+    return hipGetLastError();
+}
 
 __global__ void stamp_begin_kernel(unsigned long long* c) { c[0] = wall_clock64(); }
 __global__ void stamp_end_kernel(unsigned long long* c) {
@@ -272,13 +283,11 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         cmat = (uint32_t*)obtain(alloc, alloc_ctx, GSR_BUF_SCRATCH, 4 * ((size_t)GL.nb * ntiles + ntiles));
         if (!cmat) return fail(GSR_ERR_ALLOC, "allocator returned NULL (tile count matrix)");
         tile_tot = cmat + (size_t)GL.nb * ntiles;
-    } else if ((e = hipMemsetAsync(tile_count, 0, 8 * (size_t)ntiles * TILE_CTR_STRIDE, stream)) != hipSuccess) {
+    } else if ((e = zero_async(tile_count, 8 * (size_t)ntiles * TILE_CTR_STRIDE, stream)) != hipSuccess) {
         return hip_fail(e, "memset tile counts");
     }
     if (P > 0) {
         if (!radii) return fail(GSR_ERR_INVALID_ARG, "radii output required");
-        hipLaunchKernelGGL(copy4_kernel, dim3(1), dim3(64), 0, stream, geo.counters, (const uint32_t*)nullptr);
-        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "reset counters");
         {
             StageTimer t(GSR_STAGE_PREPROCESS, P, stream);
             if ((e = launch_preprocess(cam, g, geo, radii, lds_hist ? cmat : tile_count, lds_hist, ntiles, GL.nb,
@@ -287,7 +296,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
             if (lds_hist && (e = launch_tile_colscan(cmat, GL.nb, ntiles, tile_tot, stream)) != hipSuccess)
                 return hip_fail(e, "tile count scan");
             if ((e = launch_scan_counts(geo, GL.nb, lds_hist ? tile_tot : tile_count, lds_hist ? 1 : TILE_CTR_STRIDE,
-                                        ntiles, ranges, stream)) != hipSuccess)
+                                        ntiles, ranges, capacity > 0 ? status : nullptr, stream)) != hipSuccess)
                 return hip_fail(e, "scan");
         }
         if (capacity <= 0) {
@@ -302,7 +311,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
             if ((e = hipEventRecord(g_pinned.ev, stream)) != hipSuccess) return hip_fail(e, "record num_rendered");
         }
     } else {
-        if ((e = hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)ntiles, stream)) != hipSuccess)
+        if ((e = zero_async(ranges, sizeof(uint2) * (size_t)ntiles, stream)) != hipSuccess)
             return hip_fail(e, "memset ranges");
     }
     if (P == 0) {  // rasterize_points.cu:67-81: zero outputs, forward not run
@@ -312,9 +321,9 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         }
         void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, BinLayout::make(0, W, H).total);
         if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
-        if ((e = hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess ||
-            (e = hipMemsetAsync(out_depth, 0, sizeof(float) * (size_t)W * H, stream)) != hipSuccess ||
-            (colors2 && (e = hipMemsetAsync(out_color2, 0, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess))
+        if ((e = zero_async(out_color, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess ||
+            (e = zero_async(out_depth, sizeof(float) * (size_t)W * H, stream)) != hipSuccess ||
+            (colors2 && (e = zero_async(out_color2, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess))
             return hip_fail(e, "zero outputs");
         return 0;
     }
@@ -368,8 +377,6 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         speculated = true;
     }
     if (capacity > 0) {  // static mode: report, never wait (an overflow shows in status, outputs invalid)
-        hipLaunchKernelGGL(copy4_kernel, dim3(1), dim3(64), 0, stream, status, (const uint32_t*)geo.counters);
-        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "copy status");
         return (int)cap;
     }
     if ((e = hipEventSynchronize(g_pinned.ev)) != hipSuccess) return hip_fail(e, "sync num_rendered");

@@ -541,7 +541,7 @@ hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, 
 hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, hipStream_t s);
 hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hipStream_t s);
 hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
-                              uint2* ranges, hipStream_t s);
+                              uint2* ranges, uint32_t* status, hipStream_t s);
 hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid, int nb,
                             hipStream_t s);
 // Speculative launches: kernels exit early when the device-side counters show

@@ -33,6 +33,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     }
     const int i = blockIdx.x * PRE_BLOCK + threadIdx.x;
     uint32_t tiles = 0;
+    bool violation = false;  // prefiltered set but the point is culled (auxiliary.h:154-160)
     float4 q1;
     if (i < g.P) {
         int radius = 0;
@@ -41,7 +42,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
         float pw = 1.0f / (hom.w + 0.0000001f);
         float3 pv = xform4x3(p, cam.view);
         bool ok = pv.z > 0.001f;  // auxiliary.h:154 (the 1.3 NDC test is commented out)
-        if (!ok && cam.prefiltered) atomicOr(&geo.counters[1], 1u);
+        if (!ok && cam.prefiltered) violation = true;
         float cov3[6];
         Proj pj;
         float det = 0.f;
@@ -115,7 +116,9 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
         q1.w = __uint_as_float(woff + incl - tiles);
         geo.rr[(size_t)RR_F4 * i + 1] = q1;
     }
-    if (threadIdx.x == PRE_BLOCK - 1) geo.blocksums[blockIdx.x] = woff + incl;
+    // top bit: prefiltered violation anywhere in the workgroup (folded into counters[1] by the scan)
+    const bool viol = __syncthreads_or(violation);
+    if (threadIdx.x == PRE_BLOCK - 1) geo.blocksums[blockIdx.x] = (woff + incl) | (viol ? 0x80000000u : 0u);
     if (LDS_HIST)
         for (int t = threadIdx.x; t < ntiles; t += PRE_BLOCK) counts[(size_t)blockIdx.x * ntiles + t] = s_hist[t];
 }
@@ -225,22 +228,30 @@ hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hi
 __global__ void __launch_bounds__(SCAN_THREADS)
 scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t* __restrict__ tile_count,
                    uint32_t tile_stride, uint32_t ntiles, uint2* __restrict__ ranges,
-                   uint32_t* __restrict__ counters, uint32_t sort_cap) {
+                   uint32_t* __restrict__ counters, uint32_t sort_cap, uint32_t* __restrict__ status) {
+    // Writes all four counters (no reset needed): [0] num_rendered, [1] prefiltered violation
+    // (top bits of the workgroup sums), [2] longest tile list, [3] sort_cap; and a copy to
+    // `status` (static mode).
     __shared__ uint32_t wsums[SCAN_THREADS / 64];
-    __shared__ uint32_t s_carry, s_max;
+    __shared__ uint32_t s_carry, s_max, s_viol;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) s_viol = 0;
     for (int pass = 0; pass < 2; pass++) {
         const uint32_t n = pass == 0 ? nb : ntiles;
         const uint32_t* src = pass == 0 ? blocksums : tile_count;
         if (tid == 0) { s_carry = 0; s_max = 0; }
         __syncthreads();
-        uint32_t vmax = 0;
+        uint32_t vmax = 0, viol = 0;
         for (uint32_t base = 0; base < n; base += SCAN_THREADS * SCAN_ITEMS) {
             uint32_t x[SCAN_ITEMS], sum = 0;
             const uint32_t i0 = base + (uint32_t)tid * SCAN_ITEMS;
 #pragma unroll
             for (int k = 0; k < SCAN_ITEMS; k++) {
                 x[k] = (i0 + k < n) ? src[(size_t)(i0 + k) * (pass == 0 ? 1u : tile_stride)] : 0u;
+                if (pass == 0) {  // workgroup sums carry the prefiltered-violation flag in bit 31
+                    viol |= x[k] >> 31;
+                    x[k] &= 0x7fffffffu;
+                }
                 sum += x[k];
                 vmax = max(vmax, x[k]);
             }
@@ -267,13 +278,17 @@ scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t
             __syncthreads();
         }
         atomicMax(&s_max, vmax);
+        if (viol) atomicOr(&s_viol, 1u);
         __syncthreads();
         if (tid == 0) {
             if (pass == 0) {
                 counters[0] = s_carry;
+                counters[1] = s_viol;
+                if (status) { status[0] = s_carry; status[1] = s_viol; }
             } else {
                 counters[2] = s_max;
                 counters[3] = sort_cap;  // longest list the tile sort will handle (BwdGuard)
+                if (status) { status[2] = s_max; status[3] = sort_cap; }
             }
         }
         __syncthreads();
@@ -281,9 +296,10 @@ scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t
 }
 
 hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
-                              uint2* ranges, hipStream_t s) {
+                              uint2* ranges, uint32_t* status, hipStream_t s) {
     hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, geo.blocksums, (uint32_t)nb, tile_count,
-                       (uint32_t)tile_stride, (uint32_t)ntiles, ranges, geo.counters, (uint32_t)TILE_SORT_CAP);
+                       (uint32_t)tile_stride, (uint32_t)ntiles, ranges, geo.counters, (uint32_t)TILE_SORT_CAP,
+                       status);
     return hipGetLastError();
 }
 

@@ -168,8 +168,26 @@ track_transform_part_kernel(int P, const float* __restrict__ mw, const float* __
     block_sum<POSE_PARTS>(v, s_red, part + POSE_PARTS * blockIdx.x);
 }
 
+struct PoseAdam {  // torch.optim.Adam (no weight decay, no amsgrad) on the frame's pose column
+    float lr_q, lr_t, beta1, beta2, eps;
+    float* state;     // device: m_q[4], v_q[4], m_t[3], v_t[3], step
+    float* q;         // the frame's quaternion column (stride qs), updated in place
+    float* t;         // the frame's translation column (stride qs)
+};
+
+// exp_avg = b1 m + (1-b1) g; exp_avg_sq = b2 v + (1-b2) g^2;
+// p -= lr / (1 - b1^s) * m / (sqrt(v) / sqrt(1 - b2^s) + eps)
+__device__ __forceinline__ void adam_update(float& p, float g, float& m, float& v, float lr, const PoseAdam& a,
+                                            float bc1, float bc2_sqrt) {
+    m = a.beta1 * m + (1.f - a.beta1) * g;
+    v = a.beta2 * v + (1.f - a.beta2) * g * g;
+    const float denom = sqrtf(v) / bc2_sqrt + a.eps;
+    p -= (lr / bc1) * (m / denom);
+}
+
 __global__ void __launch_bounds__(GLUE_BLOCK)
-track_transform_fin_kernel(int nblocks, const float* __restrict__ part, const float* __restrict__ cq, int qs, float* __restrict__ dq, float* __restrict__ dt) {
+track_transform_fin_kernel(int nblocks, const float* __restrict__ part, const float* __restrict__ cq, int qs,
+                           float* __restrict__ dq, float* __restrict__ dt, PoseAdam adam) {
     __shared__ float s_red[4 * POSE_PARTS];
     __shared__ float s_tot[POSE_PARTS];
     float v[POSE_PARTS];
@@ -196,6 +214,16 @@ track_transform_fin_kernel(int nblocks, const float* __restrict__ part, const fl
     float4 dc = normalize4_bwd(make_float4(ps.n[0], ps.n[1], ps.n[2], ps.n[3]), ps.cn, dn);
     dc.x += S[12]; dc.y += S[13]; dc.z += S[14]; dc.w += S[15];
     const float4 g = normalize4_bwd(make_float4(ps.c[0], ps.c[1], ps.c[2], ps.c[3]), ps.qn, dc);
+    if (adam.state) {  // optimizer step fused here: the pose gradient never leaves the kernel
+        float* st = adam.state;
+        const float step = st[14] + 1.f;
+        st[14] = step;
+        const float bc1 = 1.f - powf(adam.beta1, step), bc2_sqrt = sqrtf(1.f - powf(adam.beta2, step));
+        const float gq[4] = {g.x, g.y, g.z, g.w};
+        for (int k = 0; k < 4; k++) adam_update(adam.q[k * qs], gq[k], st[k], st[4 + k], adam.lr_q, adam, bc1, bc2_sqrt);
+        for (int k = 0; k < 3; k++) adam_update(adam.t[k * qs], S[k], st[8 + k], st[11 + k], adam.lr_t, adam, bc1, bc2_sqrt);
+        return;
+    }
     dq[0] = g.x; dq[qs] = g.y; dq[2 * qs] = g.z; dq[3 * qs] = g.w;
     dt[0] = S[0]; dt[qs] = S[1]; dt[2 * qs] = S[2];
 }
@@ -295,9 +323,29 @@ int gsr_track_transform_bwd(int P, const float* means_world, const float* unnorm
     hipLaunchKernelGGL(track_transform_part_kernel, dim3(nb), dim3(GLUE_BLOCK), 0, s, P, means_world, unnorm_rot,
                        scale_cols, cam_q, q_stride, means_cam, w2c, dL_dmeans_cam, dL_drot, dL_ddepth_colors, scratch);
     hipLaunchKernelGGL(track_transform_fin_kernel, dim3(1), dim3(GLUE_BLOCK), 0, s, nb, scratch, cam_q, q_stride,
-                       dL_dcam_q, dL_dcam_t);
+                       dL_dcam_q, dL_dcam_t, PoseAdam{0.f, 0.f, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr});
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GSR_OK : hip_fail(e, "track_transform_bwd");
+}
+
+int gsr_track_transform_bwd_adam(int P, const float* means_world, const float* unnorm_rot, int scale_cols,
+                                 float* cam_q, float* cam_t, int q_stride, const float* means_cam, const float* w2c,
+                                 const float* dL_dmeans_cam, const float* dL_drot, const float* dL_ddepth_colors,
+                                 float lr_q, float lr_t, float beta1, float beta2, float eps, float* adam_state,
+                                 float* scratch, void* stream) {
+    if (P < 0 || (scale_cols != 1 && scale_cols != 3) || q_stride < 1)
+        return fail(GSR_ERR_INVALID_ARG, "track_transform_bwd_adam: bad sizes");
+    if (!cam_q || !cam_t || !adam_state || !scratch || !w2c ||
+        (P > 0 && (!means_world || !means_cam || !dL_dmeans_cam || !unnorm_rot)))
+        return fail(GSR_ERR_INVALID_ARG, "track_transform_bwd_adam: null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = blocks_for(P);
+    hipLaunchKernelGGL(track_transform_part_kernel, dim3(nb), dim3(GLUE_BLOCK), 0, s, P, means_world, unnorm_rot,
+                       scale_cols, cam_q, q_stride, means_cam, w2c, dL_dmeans_cam, dL_drot, dL_ddepth_colors, scratch);
+    hipLaunchKernelGGL(track_transform_fin_kernel, dim3(1), dim3(GLUE_BLOCK), 0, s, nb, scratch, cam_q, q_stride,
+                       nullptr, nullptr, PoseAdam{lr_q, lr_t, beta1, beta2, eps, adam_state, cam_q, cam_t});
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? GSR_OK : hip_fail(e, "track_transform_bwd_adam");
 }
 
 int gsr_track_l1_fwd(int H, int W, const float* im, const float* depth_sil, const float* gt_im,

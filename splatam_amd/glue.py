@@ -37,9 +37,22 @@ def _f32c(t: torch.Tensor, name: str) -> torch.Tensor:
     return t.contiguous()
 
 
+class PoseAdam:
+    """torch.optim.Adam (no weight decay / amsgrad) state for one frame's pose,
+    stepped inside the transform backward (gsr_track_transform_bwd_adam)."""
+
+    def __init__(self, device, lr_q=0.0004, lr_t=0.002, betas=(0.9, 0.999), eps=1e-8):
+        self.lr_q, self.lr_t, self.betas, self.eps = float(lr_q), float(lr_t), betas, float(eps)
+        self.state = torch.zeros(15, dtype=torch.float32, device=device)
+
+    def reset(self):
+        self.state.zero_()
+
+
 class _TrackTransform(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, cam_rots, cam_trans, means_world, unnorm_rot, logit_opac, log_scales, w2c, time_idx):
+    def forward(ctx, cam_rots, cam_trans, means_world, unnorm_rot, logit_opac, log_scales, w2c, time_idx,
+                pose_adam=None):
         cam_rots, cam_trans = _f32c(cam_rots, "cam_unnorm_rots"), _f32c(cam_trans, "cam_trans")
         means_world, unnorm_rot = _f32c(means_world, "means3D"), _f32c(unnorm_rot, "unnorm_rotations")
         logit_opac, log_scales, w2c = _f32c(logit_opac, "logit_opacities"), _f32c(log_scales, "log_scales"), \
@@ -63,11 +76,13 @@ class _TrackTransform(torch.autograd.Function):
                                          rot.data_ptr(), dcol.data_ptr(), opac.data_ptr(), scales.data_ptr(),
                                          _stream(means_world))
         _check(rc, "track_transform_fwd")
+        ctx.set_materialize_grads(False)  # no zero-filled grads for unused outputs
         ctx.mark_non_differentiable(opac, scales)
         if scols == 1:
             ctx.mark_non_differentiable(rot)  # isotropic maps: rotations do not depend on the pose
         ctx.save_for_backward(cam_rots, cam_trans, means_world, unnorm_rot, means_cam, w2c)
         ctx.meta = (t, T, scols)
+        ctx.pose_adam = pose_adam
         return means_cam, rot, dcol, opac, scales
 
     @staticmethod
@@ -75,11 +90,25 @@ class _TrackTransform(torch.autograd.Function):
         cam_rots, cam_trans, means_world, unnorm_rot, means_cam, w2c = ctx.saved_tensors
         t, T, scols = ctx.meta
         P = means_world.shape[0]
+        none = (None,) * 9
+        if g_means is None and g_dcol is None and g_rot is None:
+            return none
         if g_means is None:
             g_means = torch.zeros_like(means_cam)
         g_means = g_means.contiguous()
         g_rot = g_rot.contiguous() if (g_rot is not None and scols != 1) else None
         g_dcol = g_dcol.contiguous() if g_dcol is not None else None
+        opt = ctx.pose_adam
+        if opt is not None:  # optimizer step fused into the backward: the pose is updated in place
+            scratch = torch.empty(lib.gsr_track_scratch_floats(P), dtype=torch.float32, device=means_world.device)
+            rc = lib.gsr_track_transform_bwd_adam(
+                P, means_world.data_ptr(), unnorm_rot.data_ptr(), scols, cam_rots.data_ptr() + 4 * t,
+                cam_trans.data_ptr() + 4 * t, T, means_cam.data_ptr(), w2c.data_ptr(), g_means.data_ptr(),
+                g_rot.data_ptr() if g_rot is not None else None, g_dcol.data_ptr() if g_dcol is not None else None,
+                opt.lr_q, opt.lr_t, float(opt.betas[0]), float(opt.betas[1]), opt.eps, opt.state.data_ptr(),
+                scratch.data_ptr(), _stream(means_world))
+            _check(rc, "track_transform_bwd_adam")
+            return none
         dq = torch.zeros_like(cam_rots)
         dt = torch.zeros_like(cam_trans)
         scratch = torch.empty(lib.gsr_track_scratch_floats(P), dtype=torch.float32, device=means_world.device)
@@ -90,15 +119,17 @@ class _TrackTransform(torch.autograd.Function):
                                          dq.data_ptr() + 4 * t, dt.data_ptr() + 4 * t, T, scratch.data_ptr(),
                                          _stream(means_world))
         _check(rc, "track_transform_bwd")
-        return dq, dt, None, None, None, None, None, None
+        return dq, dt, None, None, None, None, None, None, None
 
 
-def track_transform(params: dict, time_idx: int, w2c: torch.Tensor):
+def track_transform(params: dict, time_idx: int, w2c: torch.Tensor, pose_adam: PoseAdam | None = None):
     """Returns (means3D_cam, rotations, depth_colors [z,1,z^2], opacities, scales) for the tracking
-    iteration; differentiable w.r.t. params['cam_unnorm_rots'] / params['cam_trans'] only."""
+    iteration; differentiable w.r.t. params['cam_unnorm_rots'] / params['cam_trans'] only.  With
+    pose_adam, the backward applies the Adam step to the frame's pose in place instead of
+    returning its gradient (no .grad, no optimizer kernels)."""
     return _TrackTransform.apply(params["cam_unnorm_rots"], params["cam_trans"], params["means3D"].detach(),
                                  params["unnorm_rotations"].detach(), params["logit_opacities"].detach(),
-                                 params["log_scales"].detach(), w2c, int(time_idx))
+                                 params["log_scales"].detach(), w2c, int(time_idx), pose_adam)
 
 
 class _TrackingL1(torch.autograd.Function):

@@ -105,6 +105,7 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
         ctx.save_for_backward(colors_precomp, colors2, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
                               geomBuffer, binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii, depth)
+        ctx.set_materialize_grads(False)  # radii / depth never carry gradients: no zero fills
         return color, color2, radii, depth
 
     @staticmethod

@@ -133,11 +133,13 @@ def fused_eligible(params, curr_data, cfg: TrackingConfig) -> bool:
 
 
 def _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg: TrackingConfig, dual=True, capacity=0,
-                             status=None):
+                             status=None, pose_adam=None, means2D=None):
+    """means2D: optional caller-owned [P,3] tensor (the tracker passes a static one without grad)."""
     from .glue import track_transform, tracking_l1
-    means, rots, dcol, opac, scales = track_transform(params, iter_time_idx, curr_data["w2c"])
+    means, rots, dcol, opac, scales = track_transform(params, iter_time_idx, curr_data["w2c"], pose_adam)
     P = means.shape[0]
-    means2D = torch.zeros(P, 3, device=means.device, requires_grad=True)
+    if means2D is None:
+        means2D = torch.zeros(P, 3, device=means.device, requires_grad=True)
     if dual:  # both renders in one rasterization (means2D.grad then holds the sum over both images)
         im, depth_sil, radius, _ = rasterize_gaussians_dual(means, means2D, None, params["rgb_colors"], dcol, opac,
                                                             scales, rots, None, curr_data["cam"], capacity, status)

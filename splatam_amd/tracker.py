@@ -8,7 +8,9 @@ fast, so the iterations are captured once into a torch.cuda.CUDAGraph
 (hipGraph) and replayed: the host issues one launch per `iters_per_graph`
 iterations.
 
-Capture requires a forward that never waits on the host: the dual forward runs
+The pose optimizer (torch.optim.Adam semantics) runs inside the transform
+backward (gsr_track_transform_bwd_adam), so an iteration is the loss forward
+and backward only.  Capture requires a forward that never waits on the host: the dual forward runs
 in its static mode (gsr_forward_dual_static) with a binning capacity taken
 from an eager probe of the same frame times `headroom`.  Every captured
 iteration copies its binning counters into its own row of `status`;
@@ -61,8 +63,12 @@ class GraphTracker:
         rots, trans = params["cam_unnorm_rots"], params["cam_trans"]
         if not (rots.is_leaf and trans.is_leaf and rots.requires_grad and trans.requires_grad):
             raise RuntimeError("cam_unnorm_rots / cam_trans must be leaf tensors requiring grad")
-        self.opt = torch.optim.Adam([{"params": [rots], "lr": lrs[0]}, {"params": [trans], "lr": lrs[1]}],
-                                    fused=True, capturable=True)
+        # Adam on the pose fused into the transform backward (gsr_track_transform_bwd_adam): the
+        # iteration is loss forward + backward only -- no .grad, zero_grad or optimizer kernels
+        from .glue import PoseAdam
+        self.adam = PoseAdam(dev, lr_q=lrs[0], lr_t=lrs[1])
+        self.seed = torch.ones((), dtype=torch.float32, device=dev)          # static loss-gradient seed
+        self.means2D = torch.zeros(params["means3D"].shape[0], 3, device=dev)  # no grad: tracking ignores it
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm-up iterations (real tracking iterations) outside the capture
@@ -80,11 +86,10 @@ class GraphTracker:
                 self.loss = self._iteration(k)
 
     def _iteration(self, k: int):
-        self.opt.zero_grad(set_to_none=False)
         loss, _, _ = _get_loss_tracking_fused(self.params, self.curr, self.t, self.cfg, dual=True,
-                                              capacity=self.capacity, status=self.status[k])
-        loss.backward()
-        self.opt.step()
+                                              capacity=self.capacity, status=self.status[k], pose_adam=self.adam,
+                                              means2D=self.means2D)
+        torch.autograd.backward(loss, self.seed)
         return loss.detach()
 
     def run(self):

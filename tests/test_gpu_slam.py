@@ -94,8 +94,9 @@ def _pose_leaves(params):
 
 
 def test_graph_tracker_matches_eager_iterations(cuda):
-    """HIP-graph replay (static-capacity forward, capturable fused Adam) follows the
-    same pose trajectory as the same number of eager fused iterations."""
+    """HIP-graph replay (static-capacity forward, pose Adam fused into the transform
+    backward) follows the pose trajectory of the same number of eager iterations
+    with torch.optim.Adam (float rounding of the Adam update differs: 1e-6 abs)."""
     from splatam_amd.tracker import GraphTracker
     params, curr = _setup(cuda, False)
     S, W = 6, 2
@@ -113,8 +114,8 @@ def test_graph_tracker_matches_eager_iterations(cuda):
     torch.cuda.synchronize()
     assert not tr.overflowed()
     assert min(tr.num_rendered()) > 0
-    torch.testing.assert_close(pg["cam_unnorm_rots"].detach(), pe["cam_unnorm_rots"].detach(), rtol=1e-5, atol=1e-7)
-    torch.testing.assert_close(pg["cam_trans"].detach(), pe["cam_trans"].detach(), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(pg["cam_unnorm_rots"].detach(), pe["cam_unnorm_rots"].detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(pg["cam_trans"].detach(), pe["cam_trans"].detach(), rtol=1e-5, atol=1e-6)
     assert float(tr.loss) > 0.0
 
 
