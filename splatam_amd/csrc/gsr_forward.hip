@@ -427,42 +427,120 @@ hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const
 // equals the reference's stable (tile, depth) radix order.
 constexpr int TILE_SORT_THREADS = 256;
 
+// Bitonic network over n = 256 * E keys (E per thread, blocked: thread t holds
+// indices [t*E, t*E+E)).  Element i pairs with i ^ j, ascending iff (i & k) == 0.
+// Partner in the same thread (j < E): register compare-exchange; in the same
+// wave (j < 64 E): lane shuffle (lane ^ j/E, same slot); otherwise through LDS.
+// For n = 1024 only 3 of the 55 stages need barriers (the LDS version had 55).
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int E, int J>
+__device__ __forceinline__ void bitonic_reg_stage(uint64_t (&v)[E], uint32_t base, uint32_t k) {
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        if (e & J) continue;
+        const bool up = ((base + (uint32_t)e) & k) == 0;
+        const uint64_t a = v[e], b = v[e + J];
+        const bool sw = (b < a) == up;  // one 64-bit compare, then two selects per word
+        v[e] = sw ? b : a;
+        v[e + J] = sw ? a : b;
+    }
+}
+
+// keep the smaller of (mine, partner) iff keep_min: one 64-bit compare + 2 selects
+__device__ __forceinline__ uint64_t bitonic_pick(uint64_t v, uint64_t o, bool keep_min) {
+    return ((o < v) == keep_min) ? o : v;
+}
+
+template <int E>
+__device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, uint32_t* __restrict__ dst,
+                               uint64_t* sk) {
+    constexpr uint32_t n = 256u * E;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t base = tid * E;
+    uint64_t v[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) v[e] = base + e < cnt ? src[base + e] : ~0ull;
+    for (uint32_t k = 2; k <= n; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            if (j >= (uint32_t)E) {
+                // j >= E, so k > j covers only thread-index bits: direction and side are the
+                // same for all E slots of a thread
+                const bool up = (base & k) == 0, keep_min = ((base & j) == 0) == up;
+                if (j >= 64u * E) {  // partner in another wave
+#pragma unroll
+                    for (int e = 0; e < E; e++) sk[base + e] = v[e];
+                    __syncthreads();
+#pragma unroll
+                    for (int e = 0; e < E; e++) v[e] = bitonic_pick(v[e], sk[(base + e) ^ j], keep_min);
+                    __syncthreads();
+                } else {  // partner lane ^ j/E, same slot
+                    const int m = (int)(j / E);
+#pragma unroll
+                    for (int e = 0; e < E; e++) v[e] = bitonic_pick(v[e], shfl_xor_u64(v[e], m), keep_min);
+                }
+            } else {  // partner in this thread
+                if (E > 2 && j == 2) bitonic_reg_stage<E, (E > 2 ? 2 : 1)>(v, base, k);
+                else if (E > 1 && j == 1) bitonic_reg_stage<E, 1>(v, base, k);
+            }
+        }
+    }
+    (void)lane;
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if (base + e < cnt) dst[base + e] = (uint32_t)v[e];
+}
+
 __global__ void __launch_bounds__(TILE_SORT_THREADS)
 tile_sort_kernel(const uint2* __restrict__ ranges, const uint64_t* __restrict__ keys,
                  uint32_t* __restrict__ point_list, SpecGuard guard) {
     __shared__ uint64_t sk[TILE_SORT_CAP];
     if (guard.overflow()) return;
-    const int tid = threadIdx.x;
     const uint2 range = ranges[blockIdx.x];
     const uint32_t cnt = range.y - range.x;
     if (cnt <= 1) {
-        if (cnt == 1 && tid == 0) point_list[range.x] = (uint32_t)keys[range.x];
+        if (cnt == 1 && threadIdx.x == 0) point_list[range.x] = (uint32_t)keys[range.x];
         return;
     }
-    uint32_t n = 2;
-    while (n < cnt) n <<= 1;
-    for (uint32_t i = tid; i < n; i += TILE_SORT_THREADS) sk[i] = i < cnt ? keys[range.x + i] : ~0ull;
-    __syncthreads();
-    for (uint32_t k = 2; k <= n; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = tid; i < n / 2; i += TILE_SORT_THREADS) {
-                const uint32_t lo = 2 * i - (i & (j - 1));
-                const uint32_t hi = lo + j;
-                const uint64_t a = sk[lo], b = sk[hi];
-                const bool up = (lo & k) == 0;
-                if ((a > b) == up) {
-                    sk[lo] = b;
-                    sk[hi] = a;
+    const uint64_t* src = keys + range.x;
+    uint32_t* dst = point_list + range.x;
+    if (cnt <= 256) {
+        tile_sort_regs<1>(src, cnt, dst, sk);
+    } else if (cnt <= 512) {
+        tile_sort_regs<2>(src, cnt, dst, sk);
+    } else if (cnt <= 1024) {
+        tile_sort_regs<4>(src, cnt, dst, sk);
+    } else {
+        // long lists (<= TILE_SORT_CAP): the same network entirely through LDS -- more keys
+        // per thread in registers would raise the whole kernel's VGPR count (occupancy 5 -> 3)
+        uint32_t n = 2048;
+        while (n < cnt) n <<= 1;
+        for (uint32_t i = threadIdx.x; i < n; i += TILE_SORT_THREADS) sk[i] = i < cnt ? src[i] : ~0ull;
+        __syncthreads();
+        for (uint32_t k = 2; k <= n; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = threadIdx.x; i < n / 2; i += TILE_SORT_THREADS) {
+                    const uint32_t lo = 2 * i - (i & (j - 1)), hi = lo + j;
+                    const uint64_t a = sk[lo], b = sk[hi];
+                    if ((a > b) == ((lo & k) == 0)) {
+                        sk[lo] = b;
+                        sk[hi] = a;
+                    }
                 }
+                __syncthreads();
             }
-            __syncthreads();
         }
+        for (uint32_t i = threadIdx.x; i < cnt; i += TILE_SORT_THREADS) dst[i] = (uint32_t)sk[i];
     }
-    for (uint32_t i = tid; i < cnt; i += TILE_SORT_THREADS) point_list[range.x + i] = (uint32_t)sk[i];
 }
 
 hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint32_t* point_list,
                             SpecGuard guard, hipStream_t s) {
+    static_assert(TILE_SORT_THREADS == 256 && TILE_SORT_CAP <= 4096, "tile_sort_regs assumes 256 x E; sk holds the cap");
     hipLaunchKernelGGL(tile_sort_kernel, dim3(ntiles), dim3(TILE_SORT_THREADS), 0, s, ranges, keys, point_list,
                        guard);
     return hipGetLastError();
