@@ -146,12 +146,17 @@ int gsr_forward_dual_static(const gsr_settings* settings, const gsr_gaussians* g
 /* Backward of gsr_forward_dual (power 1): every geometric gradient in `grads`
  * is the sum of the two renders' (as autograd would accumulate it over two
  * calls), grads->dcolors is d/dcolors of the first set and dcolors2 [P,3]
- * that of colors2 (NULL skips it, as for the pointers in `grads`). */
+ * that of colors2 (NULL skips it, as for the pointers in `grads`).
+ * dl2_channels: 3, or 1 when the caller guarantees channels 1 and 2 of
+ * dL_dout_color2 are zero (SplaTAM tracking differentiates only the depth of
+ * the [depth, silhouette, depth^2] render); those channels are then not read
+ * and dcolors2[:,1:] is written as zero. */
 int gsr_backward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians,
                       const int* radii, const float* colors2, const float* dL_dout_color,
                       const float* dL_dout_color2, int num_rendered, const void* geom_buffer,
                       const void* binning_buffer, const void* image_buffer, const gsr_grads* grads,
-                      float* dcolors2, gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+                      float* dcolors2, int dl2_channels, gsr_alloc_fn alloc, void* alloc_ctx,
+                      void* stream);
 
 /* Frustum test view_z > 0.001.  Replaces markVisible / checkFrustum
  * (rasterize_points.cu:198-216, rasterizer_impl.cu:54-67,141-153).

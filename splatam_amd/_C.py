@@ -209,11 +209,12 @@ def rasterize_gaussians_dual(background, means3D, colors, colors2, opacity, scal
 def rasterize_gaussians_dual_backward(background, means3D, radii, colors, colors2, scales, rotations, scale_modifier,
                                       cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
                                       dL_dout_color2, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
-                                      needs=None):
+                                      needs=None, dl2_channels=3):
     """gsr_backward_dual.  Returns (dmeans2D, dcolors, dcolors2, dopacity, dmeans3D, dcov3D, dsh, dscales,
     drotations); geometric gradients are the sums over both colour sets.  `needs` (9 bools in that
     order, default all) skips the gradients nobody wants: they come back as None and the kernels do
-    not form their per-pair sums."""
+    not form their per-pair sums.  dl2_channels=1 promises dL_dout_color2[1:] == 0 (only the depth
+    channel is differentiated): those channels are not read and dcolors2[:, 1:] comes back zero."""
     device = means3D.device
     P = means3D.size(0)
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
@@ -241,7 +242,8 @@ def rasterize_gaussians_dual_backward(background, means3D, radii, colors, colors
                                    dpix2.data_ptr(), int(R), geomBuffer.data_ptr(),
                                    binningBuffer.data_ptr() if binningBuffer.numel() else None,
                                    imageBuffer.data_ptr(), ctypes.byref(grads),
-                                   dcolors2.data_ptr() if dcolors2 is not None else None, _ALLOC_CB, None,
+                                   dcolors2.data_ptr() if dcolors2 is not None else None, int(dl2_channels),
+                                   _ALLOC_CB, None,
                                    _stream(device))
         _check(rc, "rasterize_gaussians_dual_backward")
         _tls.buffers = {}

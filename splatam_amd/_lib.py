@@ -49,7 +49,7 @@ SIGNATURES = {
                                         c_void_p]),
     "gsr_backward_dual": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, ctypes.POINTER(GsrGrads),
-                                  c_void_p, ALLOC_FN, c_void_p, c_void_p]),
+                                  c_void_p, c_int, ALLOC_FN, c_void_p, c_void_p]),
     "gsr_mark_visible": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gsr_geom_buffer_bytes": (c_size_t, [c_int]),
     "gsr_binning_buffer_bytes": (c_size_t, [c_int, c_int, c_int]),

@@ -35,7 +35,10 @@ constexpr int BWD_BATCH = 128;
 // reference's last_alpha / last_color / accum_rec update, one step earlier).
 // 5 workgroups per CU (<= 96 VGPRs): a 640x480 frame's 1200 tiles are all resident
 // at once, so there is no second dispatch round behind the slowest tiles
-template <bool DUAL, bool OPAC, bool COL1, bool COL2>
+// Q2: how many leading channels of dL_dpix2 may be non-zero (3, or 1 when the caller
+// promises the rest are zero -- SplaTAM's tracking loss differentiates only the depth
+// channel of the [depth, silhouette, depth^2] image).
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3>
 __global__ void __launch_bounds__(TILE_PIX, 5)
 render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                   const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
@@ -44,7 +47,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                   const float* __restrict__ dL_dpix2, float4* __restrict__ inst, BwdGuard guard) {
     static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
     if (guard.overflow()) return;  // invalid forward state (static-mode overflow): touch nothing
-    constexpr int NV = 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? 3 : 0);
+    static_assert(Q2 == 1 || Q2 == 3, "Q2 is 1 or 3 channels");
+    constexpr int NV = 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2 : 0);
     constexpr int O_OP = 5, O_C1 = 5 + (OPAC ? 1 : 0), O_C2 = O_C1 + (COL1 ? 3 : 0);
     __shared__ float4 s_a[BWD_BATCH];
     __shared__ float4 s_b[BWD_BATCH];
@@ -73,8 +77,10 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         dp2 = dL_dpix[2 * HW + pid];
         if (DUAL) {
             dq0 = dL_dpix2[pid];
-            dq1 = dL_dpix2[HW + pid];
-            dq2 = dL_dpix2[2 * HW + pid];
+            if (Q2 == 3) {
+                dq1 = dL_dpix2[HW + pid];
+                dq2 = dL_dpix2[2 * HW + pid];
+            }
         }
     }
     uint32_t wmax = last;
@@ -160,7 +166,11 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             for (int k = 0; k < 4; k++) {
                 const float4 c = s_c[gq.j[k]];
                 float cd;
-                if (DUAL) {
+                if (DUAL && Q2 == 1) {
+                    const float c2x = s_d[gq.j[k]].x;
+                    const v2f t = v2f{c.x, c.y} * dp01;
+                    cd = __builtin_fmaf(c.z, dp2, __builtin_fmaf(c2x, dq0, t.x + t.y));
+                } else if (DUAL) {
                     const float4 c2 = s_d[gq.j[k]];
                     const v2f t = v2f{c.x, c.y} * dp01 + v2f{c2.x, c2.y} * dq01;
                     cd = __builtin_fmaf(c.z, dp2, __builtin_fmaf(c2.z, dq2, t.x + t.y));
@@ -199,7 +209,9 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                     vk[O_C1 + 1] = t.y;
                     vk[O_C1 + 2] = dch[k] * dp2;
                 }
-                if (COL2) {
+                if (COL2 && Q2 == 1) {
+                    vk[O_C2] = dch[k] * dq0;
+                } else if (COL2) {
                     const v2f t = dch[k] * dq01;
                     vk[O_C2] = t.x;
                     vk[O_C2 + 1] = t.y;
@@ -229,7 +241,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
 #pragma unroll
             for (int m = 0; m < 3; m++) {
                 sum[6 + m] = COL1 ? c[O_C1 + m] : 0.f;
-                sum[9 + m] = COL2 ? c[O_C2 + m] : 0.f;
+                sum[9 + m] = (COL2 && m < Q2) ? c[O_C2 + m] : 0.f;
             }
             const uint32_t u = s_u[tid];
             inst[3 * u] = make_float4(sum[0], sum[1], sum[2], sum[3]);
@@ -240,18 +252,21 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     }
 }
 
-template <bool DUAL, bool OPAC, bool COL1, bool COL2>
-static auto bwd_variant() { return render_bwd_kernel<DUAL, OPAC, COL1, COL2>; }
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3>
+static auto bwd_variant() { return render_bwd_kernel<DUAL, OPAC, COL1, COL2, Q2>; }
 
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
                              const float* colors2, const float* dL_dpix2, unsigned need, float4* inst,
                              BwdGuard guard, hipStream_t s) {
     const bool op = need & NEED_OPACITY, c1 = need & NEED_COLORS, c2 = colors2 && (need & NEED_COLORS2);
+    const bool q1 = need & NEED_DL2_CH0_ONLY;
     auto k = bwd_variant<false, true, true, false>();
     if (!colors2) {
         k = op ? (c1 ? bwd_variant<false, 1, 1, 0>() : bwd_variant<false, 1, 0, 0>())
                : (c1 ? bwd_variant<false, 0, 1, 0>() : bwd_variant<false, 0, 0, 0>());
+    } else if (q1 && !op && !c1) {  // SplaTAM tracking: depth-channel gradient only
+        k = c2 ? bwd_variant<true, 0, 0, 1, 1>() : bwd_variant<true, 0, 0, 0, 1>();
     } else {
         k = op ? (c1 ? (c2 ? bwd_variant<true, 1, 1, 1>() : bwd_variant<true, 1, 1, 0>())
                      : (c2 ? bwd_variant<true, 1, 0, 1>() : bwd_variant<true, 1, 0, 0>()))

@@ -444,8 +444,9 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
                          const float* dL_dout_color, const float* colors2, const float* dL_dout_color2,
                          int num_rendered, const void* geom_buffer, const void* binning_buffer,
                          const void* image_buffer, int power, const gsr_grads* grads, float* dcolors2,
-                         gsr_alloc_fn alloc, void* alloc_ctx, void* stream_) {
+                         int dl2_channels, gsr_alloc_fn alloc, void* alloc_ctx, void* stream_) {
     int rc = validate(settings, gaussians, false);
+    if (dl2_channels != 1 && dl2_channels != 3) return fail(GSR_ERR_INVALID_ARG, "dl2_channels must be 1 or 3");
     if (rc != GSR_OK) return rc;
     if (colors2 && !dL_dout_color2) return fail(GSR_ERR_INVALID_ARG, "dual backward needs dL_dout_color2");
     if (colors2 && power != 1) return fail(GSR_ERR_INVALID_ARG, "dual render supports backward_power == 1 only");
@@ -515,7 +516,7 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
         StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream);
         // SH colours feed dL/dmeans3D through the view direction, so their sums are needed with SH
         const unsigned need = (out.dopacity ? NEED_OPACITY : 0u) | ((out.dcolors || g.shs) ? NEED_COLORS : 0u) |
-                              (dcolors2 ? NEED_COLORS2 : 0u);
+                              (dcolors2 ? NEED_COLORS2 : 0u) | (dl2_channels == 1 ? NEED_DL2_CH0_ONLY : 0u);
         if ((e = launch_render_bwd(cam, ranges, point_list, geo, final_T, n_contrib, dL_dout_color, colors2,
                                    dL_dout_color2, need, inst, BwdGuard{geo.counters, (uint32_t)num_rendered},
                                    stream)) != hipSuccess)
@@ -619,17 +620,18 @@ int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, c
                  const void* image_buffer, int power, const gsr_grads* grads, gsr_alloc_fn alloc, void* alloc_ctx,
                  void* stream) {
     return backward_impl(settings, gaussians, radii, dL_dout_color, nullptr, nullptr, num_rendered, geom_buffer,
-                         binning_buffer, image_buffer, power, grads, nullptr, alloc, alloc_ctx, stream);
+                         binning_buffer, image_buffer, power, grads, nullptr, 3, alloc, alloc_ctx, stream);
 }
 
 int gsr_backward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
                       const float* colors2, const float* dL_dout_color, const float* dL_dout_color2,
                       int num_rendered, const void* geom_buffer, const void* binning_buffer,
-                      const void* image_buffer, const gsr_grads* grads, float* dcolors2, gsr_alloc_fn alloc,
-                      void* alloc_ctx, void* stream) {
+                      const void* image_buffer, const gsr_grads* grads, float* dcolors2, int dl2_channels,
+                      gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
     if (!colors2) return fail(GSR_ERR_INVALID_ARG, "colors2 required");
     return backward_impl(settings, gaussians, radii, dL_dout_color, colors2, dL_dout_color2, num_rendered,
-                         geom_buffer, binning_buffer, image_buffer, 1, grads, dcolors2, alloc, alloc_ctx, stream);
+                         geom_buffer, binning_buffer, image_buffer, 1, grads, dcolors2, dl2_channels, alloc, alloc_ctx,
+                         stream);
 }
 
 }  // extern "C"

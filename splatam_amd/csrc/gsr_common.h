@@ -585,6 +585,7 @@ hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint3
                              hipStream_t s);
 // which optional per-pair sums render_bwd forms (the geometric ones always)
 constexpr unsigned NEED_OPACITY = 1u, NEED_COLORS = 2u, NEED_COLORS2 = 4u;
+constexpr unsigned NEED_DL2_CH0_ONLY = 8u;  // dL_dpix2 channels 1, 2 are promised zero
 struct GradsOut {
     float* dmeans2D;
     float* dcolors;

@@ -72,7 +72,7 @@ class _RasterizeGaussians(torch.autograd.Function):
 
 
 def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations,
-                             cov3Ds_precomp, raster_settings, capacity=0, status=None):
+                             cov3Ds_precomp, raster_settings, capacity=0, status=None, grad2_channels=3):
     """Two GaussianRasterizer calls on identical geometry fused into one
     rasterization: SplaTAM renders RGB and the [z, 1, z^2]
     depth/silhouette image from the same means / scales / rotations / opacities
@@ -81,20 +81,23 @@ def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opac
     of the shared inputs are the sums over both images, as autograd would
     accumulate them over two calls (means2D receives that sum as well).
     capacity > 0: synchronisation-free static mode (gsr_forward_dual_static),
-    for HIP-graph capture; check `status` (device int32[4]) afterwards."""
+    for HIP-graph capture; check `status` (device int32[4]) afterwards.
+    grad2_channels=1: the caller's loss reads only channel 0 of color2 (SplaTAM
+    tracking uses the depth, not the silhouette or depth^2, in its loss), so the
+    backward skips the other two channels; their incoming gradient must be zero."""
     empty = torch.Tensor([])
     return _RasterizeGaussiansDual.apply(means3D, means2D, empty if sh is None else sh,
                                          empty if colors_precomp is None else colors_precomp, colors2, opacities,
                                          empty if scales is None else scales,
                                          empty if rotations is None else rotations,
                                          empty if cov3Ds_precomp is None else cov3Ds_precomp, raster_settings,
-                                         capacity, status)
+                                         capacity, status, grad2_channels)
 
 
 class _RasterizeGaussiansDual(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings, capacity, status):
+                raster_settings, capacity, status, grad2_channels):
         s = raster_settings
         num_rendered, color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth = _C.rasterize_gaussians_dual(
             s.bg, means3D, colors_precomp, colors2, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
@@ -102,6 +105,7 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
             s.campos, s.prefiltered, capacity=capacity, status=status)
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
+        ctx.grad2_channels = grad2_channels
         ctx.save_for_backward(colors_precomp, colors2, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
                               geomBuffer, binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii, depth)
@@ -122,10 +126,11 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
         (g_m2, g_col, g_col2, g_op, g_m3, g_cov, g_sh, g_sc, g_rot) = _C.rasterize_gaussians_dual_backward(
             s.bg, means3D, radii, colors_precomp, colors2, scales, rotations, s.scale_modifier, cov3Ds_precomp,
             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_color, grad_color2, sh, s.sh_degree, s.campos,
-            geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, needs=needs)
+            geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, needs=needs,
+            dl2_channels=ctx.grad2_channels if grad_color2 is not None else 3)
         if not n[0]:
             g_m3 = None
-        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None, None, None
+        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None, None, None, None
 
 
 class GaussianRasterizer(nn.Module):

@@ -142,7 +142,8 @@ def _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg: TrackingConf
         means2D = torch.zeros(P, 3, device=means.device, requires_grad=True)
     if dual:  # both renders in one rasterization (means2D.grad then holds the sum over both images)
         im, depth_sil, radius, _ = rasterize_gaussians_dual(means, means2D, None, params["rgb_colors"], dcol, opac,
-                                                            scales, rots, None, curr_data["cam"], capacity, status)
+                                                            scales, rots, None, curr_data["cam"], capacity, status,
+                                                            grad2_channels=1)  # the L1 loss reads depth only
     else:
         means2D_ds = torch.zeros(P, 3, device=means.device, requires_grad=True)
         ras = GaussianRasterizer(raster_settings=curr_data["cam"])

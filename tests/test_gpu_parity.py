@@ -248,3 +248,37 @@ def test_dual_render_skips_unneeded_gradients(cuda):
         res.append((m3.grad.cpu(), col2.grad.cpu(), op.grad))
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
     assert res[1][2] is None
+
+
+def test_dual_render_depth_channel_only_gradient(cuda):
+    """grad2_channels=1 (SplaTAM tracking: the loss reads only the depth channel
+    of the depth/silhouette render) matches the 3-channel backward when the
+    incoming gradient of channels 1, 2 is zero; dcolors2[:, 1:] is exactly 0."""
+    from splatam_amd.rasterizer import GaussianRasterizationSettings, rasterize_gaussians_dual
+    scene = make_scene(3000, 128, 96, seed=31, anisotropic=False)
+    c = scene.cam
+    st = GaussianRasterizationSettings(96, 128, c.tanfovx, c.tanfovy, torch.zeros(3, device=cuda), 1.0,
+                                       c.viewmatrix.to(cuda), c.projmatrix.to(cuda), 0, c.campos.to(cuda), False)
+    rs = np.random.RandomState(9)
+    g1 = torch.as_tensor(rs.randn(3, 96, 128).astype(np.float32), device=cuda)
+    g2 = torch.zeros(3, 96, 128, device=cuda)
+    g2[0] = torch.as_tensor(rs.randn(96, 128).astype(np.float32), device=cuda)
+    z = scene.means3D[:, 2:3]
+    c2 = torch.cat([z, torch.ones_like(z), z * z], 1)
+    res = []
+    for ch in (3, 1):
+        t = lambda x, rg: x.detach().to(cuda).clone().requires_grad_(rg)  # noqa: E731
+        m3, col2 = t(scene.means3D, True), t(c2, True)
+        op, col, sc, ro = (t(scene.opacities, False), t(scene.colors, False), t(scene.scales, False),
+                           t(scene.rotations, False))
+        m2 = torch.zeros_like(m3)
+        im, im2, _, _ = rasterize_gaussians_dual(m3, m2, None, col, col2, op, sc, ro, None, st, grad2_channels=ch)
+        ((im * g1).sum() + (im2 * g2).sum()).backward()
+        res.append((m3.grad.cpu().numpy(), col2.grad.cpu().numpy()))
+    (m3_full, c2_full), (m3_lean, c2_lean) = res
+    # tolerance: the lean variant drops two exact-zero FMAs from the per-pair colour
+    # dot product, which reorders one rounding step (fp32, relative L2 1e-5)
+    assert harness.rel_l2(m3_lean, m3_full) <= 1e-5
+    assert harness.rel_l2(c2_lean[:, 0], c2_full[:, 0]) <= 1e-5
+    assert np.all(c2_lean[:, 1:] == 0)
+    assert np.abs(c2_full[:, 0]).sum() > 0

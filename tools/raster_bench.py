@@ -22,7 +22,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", choices=("dual_lean", "dual", "single"), default="dual_lean",
-                    help="dual_lean: one dual rasterization, grads for means3D + depth colours only (tracking)")
+                    help="dual_lean: one dual rasterization, grads for means3D + depth colours only, depth "
+                         "channel of the second image differentiated (tracking)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     s = config_scene(a.config)
@@ -34,6 +35,10 @@ def main():
     col = s.colors.to(dev)
     ds = torch.cat([m3.detach()[:, 2:3], torch.ones_like(m3[:, :1]), m3.detach()[:, 2:3] ** 2], 1)
     g = torch.randn(3, s.cam.H, s.cam.W, device=dev)
+    g2 = g.clone()
+    lean = a.mode == "dual_lean"
+    if lean:
+        g2[1:] = 0
     ras = GaussianRasterizer(cam)
 
     full = a.mode != "dual_lean"
@@ -49,8 +54,9 @@ def main():
                 im.backward(g)
         else:
             m2 = torch.zeros_like(m3, requires_grad=full)
-            im, im2, _, _ = rasterize_gaussians_dual(m3, m2, None, col, ds, op, sc, ro, None, cam)
-            torch.autograd.backward([im, im2], [g, g])
+            im, im2, _, _ = rasterize_gaussians_dual(m3, m2, None, col, ds, op, sc, ro, None, cam,
+                                                     grad2_channels=1 if lean else 3)
+            torch.autograd.backward([im, im2], [g, g2])
 
     for _ in range(a.warmup):
         it()
