@@ -61,8 +61,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     __shared__ __attribute__((aligned(16))) uint16_t s_list[4][BWD_BATCH + 4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int tile = blockIdx.y * cam.gx + blockIdx.x;
-    const int px = blockIdx.x * TILE_X + (tid & (TILE_X - 1));
-    const int py = blockIdx.y * TILE_Y + (tid >> 4);
+    const int px = blockIdx.x * TILE_X + tile_px(tid);
+    const int py = blockIdx.y * TILE_Y + tile_py(tid);
     const bool inside = px < cam.W && py < cam.H;
     const int pid = py * cam.W + px;
     const float x0 = (float)(blockIdx.x * TILE_X), y0 = (float)(blockIdx.y * TILE_Y);
@@ -124,7 +124,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             s_b[tid] = stage_b(pa, pb);
             s_c[tid] = pc;
             if (DUAL) s_d[tid] = pd;
-            s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
+            s_mask[tid] = (uint8_t)quad_mask(pa, pb, x0, y0);
         }
         for (int q = tid; q < 4 * BWD_BATCH * NV / 4; q += TILE_PIX)
             reinterpret_cast<float4*>(s_acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -140,7 +140,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             }
         }
         // entries j with pos = hi-1-j >= wmax lie behind every pixel of this wave
-        const int n = build_strip_list(s_mask, cnt, w, hi - (int)wmax, s_list[w]);
+        const int n = build_wave_list(s_mask, cnt, w, hi - (int)wmax, s_list[w]);
         for (int i = 0; i < n; i += 4) {
             const Group4 gq = load_group4(s_list[w], i, n);
             v2f d[4];

@@ -15,7 +15,7 @@
 //                       [42..50] dscale   <- dconic                            3x3
 //                       [51..62] drot     <- dconic                            4x3
 //                       [63..78] SH basis Y_k(dir) (dsh[k][c] = Y_k * dRGB_c)   16
-//   render_bwd_power  per tile, back to front (same recurrence and strip culling
+//   render_bwd_power  per tile, back to front (same recurrence and quadrant culling
 //                     as render_bwd_kernel); per pair it forms the NV = 22 + 3*nsh
 //                     output components from the staged pack (LDS broadcast
 //                     reads), applies powf per lane, reduces them across the wave
@@ -115,8 +115,8 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
     __shared__ __attribute__((aligned(16))) uint16_t s_list[4][B + 4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int tile = blockIdx.y * cam.gx + blockIdx.x;
-    const int px = blockIdx.x * TILE_X + (tid & (TILE_X - 1));
-    const int py = blockIdx.y * TILE_Y + (tid >> 4);
+    const int px = blockIdx.x * TILE_X + tile_px(tid);
+    const int py = blockIdx.y * TILE_Y + tile_py(tid);
     const bool inside = px < cam.W && py < cam.H;
     const int pid = py * cam.W + px;
     const float x0 = (float)(blockIdx.x * TILE_X), y0 = (float)(blockIdx.y * TILE_Y);
@@ -162,7 +162,7 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
             s_b[tid] = stage_b(pa, pb);
             s_c[tid] = make_float4(r.q2.x, r.q2.y, r.q2.z, __uint_as_float(clamp_bits[gi]));
             s_q[tid] = make_float4(pa.z, pa.w, pb.x, 0.f);
-            s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
+            s_mask[tid] = (uint8_t)quad_mask(pa, pb, x0, y0);
         }
         for (int q = tid; q < 4 * B * NVP / 4; q += TILE_PIX)
             reinterpret_cast<float4*>(s_acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -172,7 +172,7 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
             s_j[q] = jac[(size_t)s_g[item] * JF4 + part];
         }
         __syncthreads();
-        const int n = build_strip_list(s_mask, cnt, w, hi - (int)wmax, s_list[w]);
+        const int n = build_wave_list(s_mask, cnt, w, hi - (int)wmax, s_list[w]);
         for (int i = 0; i < n; i++) {
             const int j = s_list[w][i];  // wave-uniform
             const float4 a = s_a[j], b = s_b[j];

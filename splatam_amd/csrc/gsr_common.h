@@ -354,14 +354,21 @@ __device__ __forceinline__ float eval_p2(float4 sa, float4 sb, v2f d) {
     return __builtin_fmaf(sb.x * d.x, d.y, __builtin_fmaf(t.x, d.x, t.y * d.y));
 }
 
-// 4-bit mask of the 16x4-pixel wave strips of a tile (pixel centres x0..x0+15,
-// rows y0+4w..y0+4w+3) that a Gaussian can contribute to, i.e. where
+// Pixel of thread tid within its 16x16 tile: wave w covers the 8x8 quadrant
+// (w & 1, w >> 1), lanes row-major inside it.  Square wave footprints cull
+// round Gaussians tighter than 16x4 strips (14% fewer pixel-pair evaluations
+// on the config-3 frame, tools/tile_balance.py).
+__device__ __forceinline__ int tile_px(int tid) { return 8 * ((tid >> 6) & 1) + (tid & 7); }
+__device__ __forceinline__ int tile_py(int tid) { return 8 * (tid >> 7) + ((tid >> 3) & 7); }
+
+// 4-bit mask of the 8x8-pixel wave quadrants of a tile (bit w: pixel centres
+// x0+8(w&1) .. +7, y0+8(w>>1) .. +7) that a Gaussian can contribute to, i.e. where
 // o * exp(-0.5 d^T Q d) >= 1/255 (forward.cu:341-351).  The bound is
 // conservative: tau and the half-extents carry margins that exceed the float32
 // error of evaluating `power` (grows with the conic's eccentricity kappa), so
 // culling never changes a result.  Anything unusual (non-finite values,
 // non-positive-definite conic, extreme eccentricity) returns 0xF: no culling.
-__device__ __forceinline__ uint32_t strip_mask(float4 a, float4 b, float x0, float y0) {
+__device__ __forceinline__ uint32_t quad_mask(float4 a, float4 b, float x0, float y0) {
     const float A = a.z, B = a.w, C = b.x, o = b.y;
     const float det = A * C - B * B;
     if (!(det > 0.f) || !(A > 0.f) || !isfinite(det) || !isfinite(a.x) || !isfinite(a.y) || !isfinite(o))
@@ -373,19 +380,16 @@ __device__ __forceinline__ uint32_t strip_mask(float4 a, float4 b, float x0, flo
     const float tau = fmaxf(__logf(t), 0.f) * (1.001f + 4e-6f * kappa) + 1e-3f;
     const float hx = sqrtf(2.f * tau * C / det) * 1.001f + 0.01f;
     const float hy = sqrtf(2.f * tau * A / det) * 1.001f + 0.01f;
-    if (a.x + hx < x0 || a.x - hx > x0 + (float)(TILE_X - 1)) return 0u;
-    uint32_t m = 0;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        const float ylo = y0 + 4.f * w, yhi = ylo + 3.f;
-        if (a.y + hy >= ylo && a.y - hy <= yhi) m |= 1u << w;
-    }
-    return m;
+    const float xl = a.x - hx, xh = a.x + hx, yl = a.y - hy, yh = a.y + hy;
+    const uint32_t mx = (xh >= x0 && xl <= x0 + 7.f ? 1u : 0u) | (xh >= x0 + 8.f && xl <= x0 + 15.f ? 2u : 0u);
+    const uint32_t my = (yh >= y0 && yl <= y0 + 7.f ? 1u : 0u) | (yh >= y0 + 8.f && yl <= y0 + 15.f ? 2u : 0u);
+    // bit w = x half (w & 1) and y half (w >> 1)
+    return (mx * (my & 1u)) | ((mx * (my >> 1)) << 2);
 }
 
-// Ordered list of the batch entries whose strip mask has bit `w` (one wave
+// Ordered list of the batch entries whose quadrant mask has bit `w` (one wave
 // builds its own list; ballot + popcount compaction, order preserved).
-__device__ __forceinline__ int build_strip_list(const uint8_t* s_mask, int cnt, int w, int jmin, uint16_t* list) {
+__device__ __forceinline__ int build_wave_list(const uint8_t* s_mask, int cnt, int w, int jmin, uint16_t* list) {
     const int lane = __lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
     int n = 0;
@@ -445,7 +449,7 @@ __device__ __forceinline__ void wave_reduce9(const float v[9], float& r0, float&
 }
 __device__ __forceinline__ int reduce9_slot_r0(int row) { return (row == 0) ? 0 : (row == 1 ? 2 : (row == 2 ? 1 : 3)); }
 
-// Four consecutive entries of a wave's strip list as wave-uniform (SGPR)
+// Four consecutive entries of a wave's quadrant list as wave-uniform (SGPR)
 // indices; entries past n repeat the first one and are flagged invalid.
 struct Group4 {
     int j[4];

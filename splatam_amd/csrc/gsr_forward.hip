@@ -685,8 +685,8 @@ hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t
 }
 
 // ----------------------------------------------------------- render (fwd) --
-// Per 256-entry batch every Gaussian gets a 4-bit mask of the wave strips its
-// contribution ellipse reaches (strip_mask); each wave then walks only its own
+// Per 256-entry batch every Gaussian gets a 4-bit mask of the 8x8 wave quadrants its
+// contribution ellipse reaches (quad_mask); each wave then walks only its own
 // compacted list, 4 entries per step: the LDS reads and exp/alpha of the 4
 // entries are independent (ILP), the transmittance chain is then applied in
 // order with predicated (branch-free) updates.  The next batch's global
@@ -709,8 +709,8 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     __shared__ __attribute__((aligned(16))) uint16_t s_list[4][RENDER_BATCH + 4];
     const int tid = threadIdx.x, w = tid >> 6;
     const int tile = blockIdx.y * cam.gx + blockIdx.x;
-    const int px = blockIdx.x * TILE_X + (tid & (TILE_X - 1));
-    const int py = blockIdx.y * TILE_Y + (tid >> 4);
+    const int px = blockIdx.x * TILE_X + tile_px(tid);
+    const int py = blockIdx.y * TILE_Y + tile_py(tid);
     const float x0 = (float)(blockIdx.x * TILE_X), y0 = (float)(blockIdx.y * TILE_Y);
     const bool inside = px < cam.W && py < cam.H;
     const v2f pix = v2f{(float)px, (float)py};
@@ -733,7 +733,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             s_b[tid] = stage_b(pa, pb);
             s_c[tid] = pc;
             if (DUAL) s_d[tid] = pd;
-            s_mask[tid] = (uint8_t)strip_mask(pa, pb, x0, y0);
+            s_mask[tid] = (uint8_t)quad_mask(pa, pb, x0, y0);
         }
         __syncthreads();
         {   // prefetch the next batch while this one is rasterised
@@ -744,7 +744,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 if (DUAL) pd = r.q3;
             }
         }
-        const int n = build_strip_list(s_mask, cnt, w, 0, s_list[w]);
+        const int n = build_wave_list(s_mask, cnt, w, 0, s_list[w]);
         const uint32_t pos0 = start - range.x;
         for (int i = 0; i < n; i += 4) {
             if (__ballot(!done) == 0ull) break;

@@ -23,6 +23,76 @@ def stats(name, a):
           f"max/mean {a.max() / max(a.mean(), 1e-9):5.2f}")
 
 
+def instance_culling(geom, v, W, H, R, P):
+    """Per (tile, Gaussian) instance: does any pixel of the tile (of each 4-row
+    strip) reach alpha >= 1/255 inside power <= 0?  Same math as the render
+    kernels (exp of the conic power, min(0.99, o * G))."""
+    rr = geom[:16 * 4 * P].view(torch.float32).reshape(P, 16)
+    x, y, A, B, C, o = rr[:, 0], rr[:, 1], rr[:, 2], rr[:, 3], rr[:, 4], rr[:, 5]
+    rng = v["ranges"].long()
+    T = rng.shape[0]
+    gx = (W + 15) // 16
+    tile_of = torch.repeat_interleave(torch.arange(T, device=rng.device), (rng[:, 1] - rng[:, 0]).clamp(min=0))
+    gid = v["point_list"].long()[:R]
+    assert tile_of.numel() == R
+    ty, tx = tile_of // gx, tile_of % gx
+    ly, lx = torch.meshgrid(torch.arange(16, device=rng.device), torch.arange(16, device=rng.device), indexing="ij")
+    any_tile = torch.zeros(R, dtype=torch.bool, device=rng.device)
+    strips = torch.zeros(R, 4, dtype=torch.bool, device=rng.device)
+    for c0 in range(0, R, 65536):
+        sl = slice(c0, min(R, c0 + 65536))
+        g = gid[sl]
+        px = (tx[sl] * 16)[:, None, None] + lx[None]
+        py = (ty[sl] * 16)[:, None, None] + ly[None]
+        dx = x[g][:, None, None] - px
+        dy = y[g][:, None, None] - py
+        pw = -0.5 * (A[g][:, None, None] * dx * dx + C[g][:, None, None] * dy * dy) - B[g][:, None, None] * dx * dy
+        al = torch.clamp(o[g][:, None, None] * torch.exp(pw), max=0.99)
+        ok = (pw <= 0) & (al >= 1.0 / 255.0) & (px < W) & (py < H)
+        strips[sl] = ok.reshape(-1, 4, 64).any(2)
+        any_tile[sl] = strips[sl].any(1)
+    # strip_mask (gsr_common.h): the alpha ellipse's axis-aligned box against each strip
+    det = A * C - B * B
+    kappa = A * C / det
+    tau = torch.log(torch.clamp(255.0 * o, min=1.0)) * (1.001 + 4e-6 * kappa) + 1e-3
+    hx = torch.sqrt(2 * tau * C / det) * 1.001 + 0.01
+    hy = torch.sqrt(2 * tau * A / det) * 1.001 + 0.01
+    g = gid
+    x0 = (tx * 16).float()
+    y0 = (ty * 16).float()
+    inx = (x[g] + hx[g] >= x0) & (x[g] - hx[g] <= x0 + 15) & (255.0 * o[g] >= 0.999)
+    aabb = torch.stack([inx & (y[g] + hy[g] >= y0 + 4 * w) & (y[g] - hy[g] <= y0 + 4 * w + 3) for w in range(4)], 1)
+    # intra-tile wave imbalance of render_bwd: per 128-entry batch the workgroup waits for the
+    # wave with the longest strip list (groups of 4), so cost ~ sum over batches of max_w
+    lens = (rng[:, 1] - rng[:, 0]).clamp(min=0)
+    pos = torch.arange(R, device=rng.device) - rng[tile_of, 0]
+    from_back = lens[tile_of] - 1 - pos
+    batch = from_back // 128
+    nb = int(batch.max()) + 1 if R else 1
+    key = tile_of * nb + batch
+    cnt = torch.zeros(T * nb, 4, device=rng.device)
+    cnt.index_add_(0, key, aabb.float())
+    grp = torch.ceil(cnt / 4)
+    max_sum, mean_sum = float(grp.max(1).values.sum()), float(grp.mean(1).sum())
+    res = {}
+    for (sw, sh) in ((16, 4), (8, 8), (16, 8), (8, 16), (16, 16), (8, 4), (4, 4)):
+        hits = []
+        for oy in range(0, 16, sh):
+            for ox in range(0, 16, sw):
+                hits.append(inx.new_ones(()) & (x[g] + hx[g] >= x0 + ox) & (x[g] - hx[g] <= x0 + ox + sw - 1) &
+                            (y[g] + hy[g] >= y0 + oy) & (y[g] - hy[g] <= y0 + oy + sh - 1) &
+                            (255.0 * o[g] >= 0.999))
+        hits = torch.stack(hits, 1).float()
+        res[f"AABB pass, {sw}x{sh} sub-rects: px-evals/instance"] = float(hits.sum(1).mean() * sw * sh)
+    res["bwd wave groups: sum max_w / sum mean_w"] = max_sum / max(mean_sum, 1)
+    return {**res,
+            "instances contributing (any pixel)": float(any_tile.float().mean()),
+            "instances passing strip AABB": float(aabb.any(1).float().mean()),
+            "strip pairs passing AABB / all strips": float(aabb.float().mean()),
+            "strip pairs contributing / all strips": float(strips.float().mean()),
+            "strip pairs / contributing instance": float(strips.float().sum() / any_tile.float().sum().clamp(min=1))}
+
+
 def main():
     dev = torch.device("cuda:0")
     s = config_scene(int(sys.argv[1]) if len(sys.argv) > 1 else 3)
@@ -41,6 +111,7 @@ def main():
         torch.cuda.synchronize()
         rng = v["ranges"].cpu().numpy().astype(np.int64)
         nc = v["n_contrib"].cpu().numpy().reshape(H, W).astype(np.int64)
+        cull = instance_culling(out[3], v, W, H, R, s.P)
     gx, gy = (W + 15) // 16, (H + 15) // 16
     ncp = np.zeros((gy * 16, gx * 16), np.int64)
     ncp[:H, :W] = nc
@@ -54,6 +125,8 @@ def main():
     order = np.sort(bmax)[::-1]
     print("top-16 bwd trip counts", order[:16].tolist())
     print("trip/list ratio mean", float((bmax / np.maximum(length, 1)).mean()))
+    for k, val in cull.items():
+        print(f"{k:34s} {val:.4f}")
 
 
 if __name__ == "__main__":
