@@ -355,31 +355,70 @@ __device__ __forceinline__ float eval_p2(float4 sa, float4 sb, v2f d) {
 }
 
 // Pixel of thread tid within its 16x16 tile: wave w covers the 8x8 quadrant
-// (w & 1, w >> 1), lanes row-major inside it.  Square wave footprints cull
-// round Gaussians tighter than 16x4 strips (14% fewer pixel-pair evaluations
-// on the config-3 frame, tools/tile_balance.py).
-__device__ __forceinline__ int tile_px(int tid) { return 8 * ((tid >> 6) & 1) + (tid & 7); }
-__device__ __forceinline__ int tile_py(int tid) { return 8 * (tid >> 7) + ((tid >> 3) & 7); }
+// (w & 1, w >> 1); inside it, 16-lane row r covers the 4x4 block (r & 1, r >> 1),
+// lanes row-major.  Tile block b = 4w + r is at block column 2(w & 1) + (r & 1),
+// block row 2(w >> 1) + (r >> 1).  Small square footprints cull round Gaussians
+// tightly (pixel-pair evaluations per instance on the config-3 frame, AABB cull:
+// 16x4 strips 105, 8x8 quadrants 90, 4x4 blocks 48; tools/tile_balance.py).
+__device__ __forceinline__ int tile_px(int tid) { return 8 * ((tid >> 6) & 1) + 4 * ((tid >> 4) & 1) + (tid & 3); }
+__device__ __forceinline__ int tile_py(int tid) { return 8 * (tid >> 7) + 4 * ((tid >> 5) & 1) + ((tid >> 2) & 3); }
 
-// 4-bit mask of the 8x8-pixel wave quadrants of a tile (bit w: pixel centres
-// x0+8(w&1) .. +7, y0+8(w>>1) .. +7) that a Gaussian can contribute to, i.e. where
-// o * exp(-0.5 d^T Q d) >= 1/255 (forward.cu:341-351).  The bound is
-// conservative: tau and the half-extents carry margins that exceed the float32
-// error of evaluating `power` (grows with the conic's eccentricity kappa), so
-// culling never changes a result.  Anything unusual (non-finite values,
-// non-positive-definite conic, extreme eccentricity) returns 0xF: no culling.
-__device__ __forceinline__ uint32_t quad_mask(float4 a, float4 b, float x0, float y0) {
+// Ellipse half-extents of the region where o * exp(-0.5 d^T Q d) >= 1/255
+// (forward.cu:341-351), with margins that exceed the float32 error of
+// evaluating `power` (grows with the conic's eccentricity kappa), so culling
+// never changes a result.  Returns false for anything unusual (non-finite
+// values, non-positive-definite conic, extreme eccentricity): no culling.
+// Sets never = true when alpha <= o < 1/255 (never blended).
+__device__ __forceinline__ bool alpha_extent(float4 a, float4 b, float& hx, float& hy, bool& never) {
     const float A = a.z, B = a.w, C = b.x, o = b.y;
     const float det = A * C - B * B;
+    never = false;
     if (!(det > 0.f) || !(A > 0.f) || !isfinite(det) || !isfinite(a.x) || !isfinite(a.y) || !isfinite(o))
-        return 0xFu;
+        return false;
     const float kappa = A * C / det;  // 1 / (1 - rho^2) >= 1
-    if (!(kappa < 1e4f)) return 0xFu;
+    if (!(kappa < 1e4f)) return false;
     const float t = 255.f * o;
-    if (t < 0.999f) return 0u;  // alpha <= o < 1/255: never blended
+    if (t < 0.999f) {
+        never = true;
+        return true;
+    }
     const float tau = fmaxf(__logf(t), 0.f) * (1.001f + 4e-6f * kappa) + 1e-3f;
-    const float hx = sqrtf(2.f * tau * C / det) * 1.001f + 0.01f;
-    const float hy = sqrtf(2.f * tau * A / det) * 1.001f + 0.01f;
+    hx = sqrtf(2.f * tau * C / det) * 1.001f + 0.01f;
+    hy = sqrtf(2.f * tau * A / det) * 1.001f + 0.01f;
+    return true;
+}
+
+// 16-bit mask of the 4x4-pixel blocks of a tile (bit 4w + r, layout of
+// tile_px / tile_py) that a Gaussian can contribute to.
+__device__ __forceinline__ uint32_t block_mask(float4 a, float4 b, float x0, float y0) {
+    float hx = 0.f, hy = 0.f;
+    bool never;
+    if (!alpha_extent(a, b, hx, hy, never)) return 0xFFFFu;
+    if (never) return 0u;
+    const float xl = a.x - hx, xh = a.x + hx, yl = a.y - hy, yh = a.y + hy;
+    uint32_t mx = 0, my = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        mx |= (xh >= x0 + 4.f * c && xl <= x0 + 4.f * c + 3.f) ? 1u << c : 0u;
+        my |= (yh >= y0 + 4.f * c && yl <= y0 + 4.f * c + 3.f) ? 1u << c : 0u;
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int bi = 0; bi < 16; bi++) {
+        const int w = bi >> 2, r = bi & 3;
+        const int cx = 2 * (w & 1) + (r & 1), cy = 2 * (w >> 1) + (r >> 1);
+        m |= ((mx >> cx) & (my >> cy) & 1u) << bi;
+    }
+    return m;
+}
+
+// 4-bit mask of the 8x8-pixel wave quadrants of a tile (bit w: pixel centres
+// x0+8(w&1) .. +7, y0+8(w>>1) .. +7) that a Gaussian can contribute to.
+__device__ __forceinline__ uint32_t quad_mask(float4 a, float4 b, float x0, float y0) {
+    float hx = 0.f, hy = 0.f;
+    bool never;
+    if (!alpha_extent(a, b, hx, hy, never)) return 0xFu;
+    if (never) return 0u;
     const float xl = a.x - hx, xh = a.x + hx, yl = a.y - hy, yh = a.y + hy;
     const uint32_t mx = (xh >= x0 && xl <= x0 + 7.f ? 1u : 0u) | (xh >= x0 + 8.f && xl <= x0 + 15.f ? 2u : 0u);
     const uint32_t my = (yh >= y0 && yl <= y0 + 7.f ? 1u : 0u) | (yh >= y0 + 8.f && yl <= y0 + 15.f ? 2u : 0u);
@@ -401,6 +440,49 @@ __device__ __forceinline__ int build_wave_list(const uint8_t* s_mask, int cnt, i
         n += __popcll(bal);
     }
     return n;
+}
+
+// The four ordered lists of a wave's 16-lane rows: list[r] gets the batch
+// entries whose 16-bit block mask has bit 4w + r (ballot + popcount
+// compaction, order preserved).  n[r] = length of list r (wave-uniform).
+__device__ __forceinline__ void build_row_lists(const uint16_t* s_mask, int cnt, int w, int jmin, uint16_t* list,
+                                                int stride, int (&n)[4]) {
+    const int lane = __lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < 4; r++) n[r] = 0;
+    for (int c = 0; c < cnt; c += 64) {
+        const int j = c + lane;
+        const uint32_t m = (j < cnt && j >= jmin) ? ((uint32_t)s_mask[j] >> (4 * w)) & 0xFu : 0u;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const bool bit = (m >> r) & 1u;
+            const uint64_t bal = __ballot(bit);
+            if (bit) list[r * stride + n[r] + __popcll(bal & lt)] = (uint16_t)j;
+            n[r] += __popcll(bal);
+        }
+    }
+}
+
+// Four consecutive entries of this lane's row list (per-lane, VGPR); entries
+// past the row's length are invalid and point at entry 0 (always staged).
+struct RowGroup4 {
+    int j[4];
+    bool valid[4];
+};
+__device__ __forceinline__ RowGroup4 load_row_group4(const uint16_t* row_list, int i, int n) {
+    const uint2 q = *reinterpret_cast<const uint2*>(&row_list[i]);
+    RowGroup4 g;
+    g.j[0] = (int)(q.x & 0xFFFFu);
+    g.j[1] = (int)(q.x >> 16);
+    g.j[2] = (int)(q.y & 0xFFFFu);
+    g.j[3] = (int)(q.y >> 16);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        g.valid[k] = i + k < n;
+        if (!g.valid[k]) g.j[k] = 0;
+    }
+    return g;
 }
 
 // --------------------------------------------------------- wave64 helpers --

@@ -685,9 +685,10 @@ hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t
 }
 
 // ----------------------------------------------------------- render (fwd) --
-// Per 256-entry batch every Gaussian gets a 4-bit mask of the 8x8 wave quadrants its
-// contribution ellipse reaches (quad_mask); each wave then walks only its own
-// compacted list, 4 entries per step: the LDS reads and exp/alpha of the 4
+// Per 256-entry batch every Gaussian gets a 16-bit mask of the 4x4-pixel blocks
+// its contribution ellipse reaches (block_mask); each 16-lane row (one block)
+// then walks only its own compacted list, 4 entries per step (the four rows of
+// a wave walk different lists in lockstep): the LDS reads and exp/alpha of the 4
 // entries are independent (ILP), the transmittance chain is then applied in
 // order with predicated (branch-free) updates.  The next batch's global
 // gathers are issued before the current batch is rasterised.
@@ -705,9 +706,10 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     __shared__ float4 s_b[RENDER_BATCH];
     __shared__ float4 s_c[RENDER_BATCH];
     __shared__ float4 s_d[DUAL ? RENDER_BATCH : 1];
-    __shared__ uint8_t s_mask[RENDER_BATCH];
-    __shared__ __attribute__((aligned(16))) uint16_t s_list[4][RENDER_BATCH + 4];
-    const int tid = threadIdx.x, w = tid >> 6;
+    __shared__ uint16_t s_mask[RENDER_BATCH];
+    constexpr int LS = RENDER_BATCH + 4;  // row-list stride (u16)
+    __shared__ __attribute__((aligned(16))) uint16_t s_list[16 * LS];
+    const int tid = threadIdx.x, w = tid >> 6, row = (tid >> 4) & 3;
     const int tile = blockIdx.y * cam.gx + blockIdx.x;
     const int px = blockIdx.x * TILE_X + tile_px(tid);
     const int py = blockIdx.y * TILE_Y + tile_py(tid);
@@ -733,7 +735,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             s_b[tid] = stage_b(pa, pb);
             s_c[tid] = pc;
             if (DUAL) s_d[tid] = pd;
-            s_mask[tid] = (uint8_t)quad_mask(pa, pb, x0, y0);
+            s_mask[tid] = (uint16_t)block_mask(pa, pb, x0, y0);
         }
         __syncthreads();
         {   // prefetch the next batch while this one is rasterised
@@ -744,11 +746,15 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 if (DUAL) pd = r.q3;
             }
         }
-        const int n = build_wave_list(s_mask, cnt, w, 0, s_list[w]);
+        int nr[4];
+        build_row_lists(s_mask, cnt, w, 0, s_list + 4 * w * LS, LS, nr);
+        const int n = max(max(nr[0], nr[1]), max(nr[2], nr[3]));
+        const int nmine = row == 0 ? nr[0] : (row == 1 ? nr[1] : (row == 2 ? nr[2] : nr[3]));
+        const uint16_t* my_list = s_list + (4 * w + row) * LS;
         const uint32_t pos0 = start - range.x;
         for (int i = 0; i < n; i += 4) {
             if (__ballot(!done) == 0ull) break;
-            const Group4 gq = load_group4(s_list[w], i, n);
+            const RowGroup4 gq = load_row_group4(my_list, i, nmine);
             float alpha[4], depth[4];
             bool ok[4];
 #pragma unroll
