@@ -2,11 +2,12 @@
 //
 // power == 1 (the standard 3DGS backward; SplaTAM's tracking/mapping path):
 //   render_bwd  (backward.cu:586-748 semantics) one 16x16 tile per workgroup,
-//               back-to-front over LDS batches.  Per (wave, Gaussian) the 9
-//               per-pair 2D gradients are summed across the 64 lanes with a
-//               transposed permlane/DPP reduction (~30 VALU), the 4 wave
-//               partials are summed through LDS, and ONE plain 48-B record per
-//               (tile, Gaussian) instance is stored at its unsorted position.
+//               back-to-front over LDS batches; each 16-lane row walks the list
+//               of its 4x4-pixel block.  The per-pair 2D gradient terms are
+//               summed across the row with a transposed DPP reduction, the 16
+//               block partials are added through LDS in a fixed order, and ONE
+//               plain 48-B record per (tile, Gaussian) instance is stored at
+//               its unsorted position.
 //               No global atomics at all: the reference issues ~25 float
 //               atomics per contributing pair (backward.cu:1093-1137).
 //   gauss_bwd   one lane per Gaussian: sums its instance records in a fixed
@@ -19,7 +20,9 @@
 
 namespace gsr {
 
-constexpr int BWD_BATCH = 128;
+// Gaussians staged per batch: the per-row partial sums take 16 x batch x NV floats of LDS
+template <int NV>
+constexpr int bwd_batch() { return NV <= 6 ? 64 : 32; }
 
 // DUAL: the pass also carries a second colour set (colors2, dL_dpix2) composited
 // with the same alpha / T (one dual forward): the per-pair dL/dalpha is the sum
@@ -27,19 +30,34 @@ constexpr int BWD_BATCH = 128;
 // dL/dcolors2 are wanted; absent ones are neither formed nor reduced (tracking
 // needs only the geometric sums and the depth colours).  Records always use the
 // fixed 12-slot layout [hx, hy, hxx, hxy, hyy | G dL/dalpha | dch dp(3) | dch dq(3)].
+// Q2: how many leading channels of dL_dpix2 may be non-zero (3, or 1 when the caller
+// promises the rest are zero -- SplaTAM's tracking loss differentiates only the depth
+// channel of the [depth, silhouette, depth^2] image).
 //
 // Per pixel the reference's back-to-front recurrence (backward.cu:966-1017)
 // is carried on dot products with dL/dpixel: the colour accumulated behind the
 // current Gaussian, accum_rec . dL/dpix, is one scalar A updated as
 // A <- A + alpha (c . dL/dpix - A) after each contributing Gaussian (the
 // reference's last_alpha / last_color / accum_rec update, one step earlier).
+//
+// Work split: each 16-lane row owns a 4x4-pixel block and walks its own list of
+// the batch entries whose contribution ellipse reaches the block (block_mask),
+// 4 entries per step; the per-pair products are summed over the row with the
+// transposed in-row reduction (row_reduce) into a per-(block, entry) LDS slot,
+// and after the batch one thread per entry adds its (at most 16) block slots
+// in block order (deterministic) and stores ONE 48-B record per (tile,
+// Gaussian) instance at its unsorted position.
 // 5 workgroups per CU (<= 96 VGPRs): a 640x480 frame's 1200 tiles are all resident
-// at once, so there is no second dispatch round behind the slowest tiles
-// Q2: how many leading channels of dL_dpix2 may be non-zero (3, or 1 when the caller
-// promises the rest are zero -- SplaTAM's tracking loss differentiates only the depth
-// channel of the [depth, silhouette, depth^2] image).
+// at once, so there is no second dispatch round behind the slowest tiles.
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2>
+constexpr int bwd_nv() { return 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2 : 0); }
+// the wide dual variants (mapping-style: colour gradients of both sets) need more
+// than 96 VGPRs: 4 waves per SIMD instead of spilling
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2>
+constexpr int bwd_waves() { return (DUAL && bwd_nv<DUAL, OPAC, COL1, COL2, Q2>() >= 8) ? 4 : 5; }
+
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3>
-__global__ void __launch_bounds__(TILE_PIX, 5)
+__global__ void __launch_bounds__(TILE_PIX, (bwd_waves<DUAL, OPAC, COL1, COL2, Q2>()))
 render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                   const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
                   const float* __restrict__ final_T,
@@ -48,18 +66,21 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
     if (guard.overflow()) return;  // invalid forward state (static-mode overflow): touch nothing
     static_assert(Q2 == 1 || Q2 == 3, "Q2 is 1 or 3 channels");
-    constexpr int NV = 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2 : 0);
+    constexpr int NV = bwd_nv<DUAL, OPAC, COL1, COL2, Q2>();
     constexpr int O_OP = 5, O_C1 = 5 + (OPAC ? 1 : 0), O_C2 = O_C1 + (COL1 ? 3 : 0);
-    __shared__ float4 s_a[BWD_BATCH];
-    __shared__ float4 s_b[BWD_BATCH];
-    __shared__ float4 s_c[BWD_BATCH];
-    __shared__ float4 s_d[DUAL ? BWD_BATCH : 1];
-    __shared__ uint32_t s_u[BWD_BATCH];
-    __shared__ __attribute__((aligned(16))) float s_acc[4 * BWD_BATCH * NV];
-    __shared__ uint32_t s_wmax[4];
-    __shared__ uint8_t s_mask[BWD_BATCH];
-    __shared__ __attribute__((aligned(16))) uint16_t s_list[4][BWD_BATCH + 4];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int BB = bwd_batch<NV>();
+    constexpr int LS = BB + 4;  // row-list stride (u16)
+    using RRd = RowReduce<NV>;
+    __shared__ float4 s_a[BB];
+    __shared__ float4 s_b[BB];
+    __shared__ float4 s_c[BB];
+    __shared__ float4 s_d[DUAL ? BB : 1];
+    __shared__ uint32_t s_u[BB];
+    __shared__ uint16_t s_mask[BB];
+    __shared__ __attribute__((aligned(16))) float s_acc[16 * BB * NV];
+    __shared__ uint32_t s_rmax[16];
+    __shared__ __attribute__((aligned(16))) uint16_t s_list[16 * LS];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, row = (tid >> 4) & 3;
     const int tile = blockIdx.y * cam.gx + blockIdx.x;
     const int px = blockIdx.x * TILE_X + tile_px(tid);
     const int py = blockIdx.y * TILE_Y + tile_py(tid);
@@ -83,12 +104,16 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             }
         }
     }
-    uint32_t wmax = last;
+    // per-block (row) maximum of the pixels' last contributor
+    uint32_t rmax = last;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o));
-    if (lane == 0) s_wmax[w] = wmax;
+    for (int o = 8; o > 0; o >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, o));
+    if ((lane & 15) == 0) s_rmax[4 * w + row] = rmax;
     __syncthreads();
-    const uint32_t bmax = max(max(s_wmax[0], s_wmax[1]), max(s_wmax[2], s_wmax[3]));
+    uint32_t bmax = 0;
+#pragma unroll
+    for (int b = 0; b < 16; b++) bmax = max(bmax, s_rmax[b]);
+    const int rm[4] = {(int)s_rmax[4 * w], (int)s_rmax[4 * w + 1], (int)s_rmax[4 * w + 2], (int)s_rmax[4 * w + 3]};
     // Instances behind every pixel's last contributor receive zero gradient.
     for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {
         const uint32_t gk = point_list[k];
@@ -106,32 +131,35 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     const v2f pix = v2f{(float)px, (float)py};
     const v2f dp01 = v2f{dp0, dp1}, dq01 = v2f{dq0, dq1};
     float T = T_final, A = 0.f;
-    const int row = lane >> 4;
+    const int my_e = row_entry(lane), my_m0 = row_m0<NV>(lane);
+    const bool writer = (lane & RRd::WRITER_MASK) == 0;
+    float* acc_row = s_acc + (4 * w + row) * BB * NV;
+    const uint16_t* my_list = s_list + (4 * w + row) * LS;
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
     uint32_t pu = 0;
-    if (tid < min(BWD_BATCH, (int)bmax)) {
+    if (tid < min(BB, (int)bmax)) {
         const uint32_t gi = point_list[range.x + bmax - 1 - tid];
         const RenderRec r = load_rr(rr, gi);
         pu = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), blockIdx.x, blockIdx.y);
         pa = r.q0; pb = r.q1; pc = r.q2;
         if (DUAL) pd = r.q3;
     }
-    for (int hi = (int)bmax; hi > 0; hi -= BWD_BATCH) {
-        const int cnt = min(BWD_BATCH, hi);
+    for (int hi = (int)bmax; hi > 0; hi -= BB) {
+        const int cnt = min(BB, hi);
         if (tid < cnt) {
             s_u[tid] = pu;
             s_a[tid] = stage_a(pa, pb);
             s_b[tid] = stage_b(pa, pb);
             s_c[tid] = pc;
             if (DUAL) s_d[tid] = pd;
-            s_mask[tid] = (uint8_t)quad_mask(pa, pb, x0, y0);
+            s_mask[tid] = (uint16_t)block_mask(pa, pb, x0, y0);
         }
-        for (int q = tid; q < 4 * BWD_BATCH * NV / 4; q += TILE_PIX)
+        for (int q = tid; q < 16 * BB * NV / 4; q += TILE_PIX)
             reinterpret_cast<float4*>(s_acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         __syncthreads();
         {   // prefetch the next batch
-            const int nhi = hi - BWD_BATCH;
-            if (tid < min(BWD_BATCH, nhi)) {
+            const int nhi = hi - BB;
+            if (tid < min(BB, nhi)) {
                 const uint32_t gi = point_list[range.x + (uint32_t)(nhi - 1 - tid)];
                 const RenderRec r = load_rr(rr, gi);
                 pu = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), blockIdx.x, blockIdx.y);
@@ -139,10 +167,14 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 if (DUAL) pd = r.q3;
             }
         }
-        // entries j with pos = hi-1-j >= wmax lie behind every pixel of this wave
-        const int n = build_wave_list(s_mask, cnt, w, hi - (int)wmax, s_list[w]);
+        // entries j with pos = hi-1-j >= rmax lie behind every pixel of the block
+        const int jmin[4] = {hi - rm[0], hi - rm[1], hi - rm[2], hi - rm[3]};
+        int nr[4];
+        build_row_lists(s_mask, cnt, w, jmin, s_list + 4 * w * LS, LS, nr);
+        const int n = max(max(nr[0], nr[1]), max(nr[2], nr[3]));
+        const int nmine = row == 0 ? nr[0] : (row == 1 ? nr[1] : (row == 2 ? nr[2] : nr[3]));
         for (int i = 0; i < n; i += 4) {
-            const Group4 gq = load_group4(s_list[w], i, n);
+            const RowGroup4 gq = load_row_group4(my_list, i, nmine);
             v2f d[4];
             float G[4], araw[4], alpha[4];
             bool ok[4];
@@ -159,7 +191,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 ok[k] = gq.valid[k] && pos < last && p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;
                 any = any || ok[k];
             }
-            if (__ballot(any) == 0ull) continue;
+            if (__ballot(any) == 0ull) continue;  // slots stay zero
             // serial part (in list order): T and A, then dL/dalpha and dchannel/dcolor
             float dLa[4], dch[4];
 #pragma unroll
@@ -218,22 +250,28 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                     vk[O_C2 + 2] = dch[k] * dq2;
                 }
             }
-            float r[NV];
-            wave_reduce_n<4 * NV>(v, r);  // row rho holds item rho's NV sums
-            if ((lane & 15) == 0 && i + row < n) {
-                const int jr = row == 0 ? gq.j[0] : (row == 1 ? gq.j[1] : (row == 2 ? gq.j[2] : gq.j[3]));
-                float* dst = s_acc + (w * BWD_BATCH + jr) * NV;
+            float r[RRd::R];
+            row_reduce<NV>(v, r, lane);  // lane class (my_e, my_m0) holds its slice of the row totals
+            const int je = my_e == 0 ? gq.j[0] : (my_e == 1 ? gq.j[1] : (my_e == 2 ? gq.j[2] : gq.j[3]));
+            const bool ve = my_e == 0 ? gq.valid[0] : (my_e == 1 ? gq.valid[1] : (my_e == 2 ? gq.valid[2] : gq.valid[3]));
+            if (writer && ve) {
+                float* dst = acc_row + je * NV + my_m0;
 #pragma unroll
-                for (int m = 0; m < NV; m++) dst[m] = r[m];
+                for (int m = 0; m < RRd::R; m++) dst[m] = r[m];
             }
         }
         __syncthreads();
         if (tid < cnt) {
             float c[NV];
 #pragma unroll
-            for (int m = 0; m < NV; m++)
-                c[m] = s_acc[(0 * BWD_BATCH + tid) * NV + m] + s_acc[(1 * BWD_BATCH + tid) * NV + m] +
-                       s_acc[(2 * BWD_BATCH + tid) * NV + m] + s_acc[(3 * BWD_BATCH + tid) * NV + m];
+            for (int m = 0; m < NV; m++) c[m] = 0.f;
+            const uint32_t mask = s_mask[tid];
+            for (int b = 0; b < 16; b++) {  // fixed block order: deterministic
+                if (!((mask >> b) & 1u)) continue;
+                const float* src = s_acc + (b * BB + tid) * NV;
+#pragma unroll
+                for (int m = 0; m < NV; m++) c[m] += src[m];
+            }
             float sum[12];
 #pragma unroll
             for (int m = 0; m < 5; m++) sum[m] = c[m];

@@ -444,19 +444,20 @@ __device__ __forceinline__ int build_wave_list(const uint8_t* s_mask, int cnt, i
 
 // The four ordered lists of a wave's 16-lane rows: list[r] gets the batch
 // entries whose 16-bit block mask has bit 4w + r (ballot + popcount
-// compaction, order preserved).  n[r] = length of list r (wave-uniform).
-__device__ __forceinline__ void build_row_lists(const uint16_t* s_mask, int cnt, int w, int jmin, uint16_t* list,
-                                                int stride, int (&n)[4]) {
+// compaction, order preserved), skipping entries j < jmin[r].  n[r] = length of
+// list r (wave-uniform).
+__device__ __forceinline__ void build_row_lists(const uint16_t* s_mask, int cnt, int w, const int (&jmin)[4],
+                                                uint16_t* list, int stride, int (&n)[4]) {
     const int lane = __lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int r = 0; r < 4; r++) n[r] = 0;
     for (int c = 0; c < cnt; c += 64) {
         const int j = c + lane;
-        const uint32_t m = (j < cnt && j >= jmin) ? ((uint32_t)s_mask[j] >> (4 * w)) & 0xFu : 0u;
+        const uint32_t m = j < cnt ? ((uint32_t)s_mask[j] >> (4 * w)) & 0xFu : 0u;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            const bool bit = (m >> r) & 1u;
+            const bool bit = ((m >> r) & 1u) && j >= jmin[r];
             const uint64_t bal = __ballot(bit);
             if (bit) list[r * stride + n[r] + __popcll(bal & lt)] = (uint16_t)j;
             n[r] += __popcll(bal);
@@ -580,6 +581,70 @@ __device__ __forceinline__ void wave_reduce2x9(const float (&v)[18], float (&r)[
 // Transposed reduction of N values (N a multiple of 4) over the 64 lanes.
 // On return row rho (= lane / 16) of r[m] (m < N/4) holds the wave total of
 // v[m + rho * N / 4] in all 16 lanes of the row.
+// Sums over each 16-lane row of 4 entries x NV values (v[e * NV + m], entry-major),
+// transposed: a step pairs every lane with a partner differing in one lane class
+// bit; the lane keeps one half of its values and adds the partner's copy of that
+// half (2 selects + 1 DPP add per kept value), so each step halves what a lane
+// holds.  Partners: row_ror:8 (lane ^ 8), row_half_mirror (i <-> 7 - i, which
+// flips class bit 4), quad_perm [2,3,0,1] (^ 2), quad_perm [1,0,3,2] (^ 1).  The
+// first two steps split the entries: lane class e = 2 (lane>>3 & 1) + (lane>>2 & 1)
+// ends up with NV values of entry e; further transposed steps split m while the
+// count stays even, plain DPP adds finish the rest.  Cost ~2.8 VALU per value
+// against 4 for four plain DPP steps per value.
+template <int NV>
+struct RowReduce {
+    static constexpr int V = 4 * NV;
+    static constexpr int S = (V / 4) % 2 ? 2 : ((V / 8) % 2 ? 3 : 4);  // transposed steps (>= 2)
+    static constexpr int R = V >> S;                                     // values per lane at the end
+    // lanes that hold (and write) distinct results: class bits of the plain steps are 0
+    static constexpr int WRITER_MASK = S == 2 ? 3 : (S == 3 ? 1 : 0);
+};
+
+template <int N, int CTRL>
+__device__ __forceinline__ void row_tstep(const float* c, float* out, bool hi) {
+#pragma unroll
+    for (int i = 0; i < N / 2; i++) {
+        const float keep = hi ? c[i + N / 2] : c[i];
+        const float send = hi ? c[i] : c[i + N / 2];
+        out[i] = keep + dpp_mov<CTRL>(send);
+    }
+}
+
+// r[i] = row total of value (entry row_entry(lane), m = row_m0<NV>(lane) + i)
+template <int NV>
+__device__ __forceinline__ void row_reduce(const float (&v)[4 * NV], float (&r)[RowReduce<NV>::R], int lane) {
+    using RR = RowReduce<NV>;
+    constexpr int V = RR::V;
+    float a[V / 2], b[V / 4];
+    row_tstep<V, 0x128>(v, a, lane & 8);        // row_ror:8
+    row_tstep<V / 2, 0x141>(a, b, lane & 4);    // row_half_mirror
+    if constexpr (RR::S == 2) {
+#pragma unroll
+        for (int i = 0; i < RR::R; i++) {
+            float t = b[i] + dpp_mov<0x4E>(b[i]);
+            r[i] = t + dpp_mov<0xB1>(t);
+        }
+    } else if constexpr (RR::S == 3) {
+        float c[V / 8];
+        row_tstep<V / 4, 0x4E>(b, c, lane & 2);
+#pragma unroll
+        for (int i = 0; i < RR::R; i++) r[i] = c[i] + dpp_mov<0xB1>(c[i]);
+    } else {
+        float c[V / 8];
+        row_tstep<V / 4, 0x4E>(b, c, lane & 2);
+        row_tstep<V / 8, 0xB1>(c, r, lane & 1);
+    }
+}
+__device__ __forceinline__ int row_entry(int lane) { return 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1); }
+template <int NV>
+__device__ __forceinline__ int row_m0(int lane) {
+    using RR = RowReduce<NV>;
+    int m0 = 0;
+    if (RR::S >= 3 && (lane & 2)) m0 += NV / 2;
+    if (RR::S >= 4 && (lane & 1)) m0 += NV / 4;
+    return m0;
+}
+
 template <int N>
 __device__ __forceinline__ void wave_reduce_n(const float (&v)[N], float (&r)[N / 4]) {
     static_assert(N % 4 == 0, "pad to a multiple of 4");

@@ -747,7 +747,8 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             }
         }
         int nr[4];
-        build_row_lists(s_mask, cnt, w, 0, s_list + 4 * w * LS, LS, nr);
+        const int jmin0[4] = {0, 0, 0, 0};
+        build_row_lists(s_mask, cnt, w, jmin0, s_list + 4 * w * LS, LS, nr);
         const int n = max(max(nr[0], nr[1]), max(nr[2], nr[3]));
         const int nmine = row == 0 ? nr[0] : (row == 1 ? nr[1] : (row == 2 ? nr[2] : nr[3]));
         const uint16_t* my_list = s_list + (4 * w + row) * LS;

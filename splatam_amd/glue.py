@@ -77,9 +77,11 @@ class _TrackTransform(torch.autograd.Function):
                                          _stream(means_world))
         _check(rc, "track_transform_fwd")
         ctx.set_materialize_grads(False)  # no zero-filled grads for unused outputs
-        ctx.mark_non_differentiable(opac, scales)
-        if scols == 1:
-            ctx.mark_non_differentiable(rot)  # isotropic maps: rotations do not depend on the pose
+        # one call: a second mark_non_differentiable replaces the first set
+        if scols == 1:  # isotropic maps: rotations do not depend on the pose either
+            ctx.mark_non_differentiable(opac, scales, rot)
+        else:
+            ctx.mark_non_differentiable(opac, scales)
         ctx.save_for_backward(cam_rots, cam_trans, means_world, unnorm_rot, means_cam, w2c)
         ctx.meta = (t, T, scols)
         ctx.pose_adam = pose_adam

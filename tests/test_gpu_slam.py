@@ -126,3 +126,21 @@ def test_graph_tracker_reports_overflow(cuda):
     tr.run()
     torch.cuda.synchronize()
     assert tr.overflowed()
+
+
+@pytest.mark.parametrize("scale_cols", [1, 3])
+def test_track_transform_marks_gaussian_outputs_non_differentiable(cuda, scale_cols):
+    """Only the pose is differentiated in tracking: opacities and scales (and the
+    rotations of an isotropic map) carry no gradient, so the rasterizer backward
+    picks its lean variant (no dL/dopacity sums, depth-channel-only colours2)."""
+    from splatam_amd.glue import track_transform
+    params, curr = _setup(cuda, False)
+    p = dict(params)
+    if scale_cols == 3:
+        p["log_scales"] = params["log_scales"].repeat(1, 3).contiguous()
+    p["cam_unnorm_rots"] = params["cam_unnorm_rots"].detach().clone().requires_grad_(True)
+    p["cam_trans"] = params["cam_trans"].detach().clone().requires_grad_(True)
+    means, rots, dcol, opac, scales = track_transform(p, 1, curr["w2c"])
+    assert means.requires_grad and dcol.requires_grad
+    assert not opac.requires_grad and not scales.requires_grad
+    assert rots.requires_grad == (scale_cols == 3)
