@@ -20,6 +20,52 @@
 
 namespace gsr {
 
+// Per-pair geometric terms (hx, hy, hx dx, hx dy, hy dy[, G dL/dalpha]) with
+// h = G * dL/dG = (o * G) * dL/dalpha.
+template <bool OPAC>
+__device__ __forceinline__ void pair_geom(float* vk, float araw, float dLa, float G, v2f d) {
+    const v2f hv = (araw * dLa) * d;  // (hx, hy)
+    const v2f hh = hv.x * d;          // (hx dx, hx dy)
+    vk[0] = hv.x;
+    vk[1] = hv.y;
+    vk[2] = hh.x;
+    vk[3] = hh.y;
+    vk[4] = hv.y * d.y;
+    if (OPAC) vk[5] = G * dLa;
+}
+// Per-pair colour terms dch * dL/dpix (COL1, 3) and dch * dL/dpix2 (COL2, Q2 channels).
+template <bool COL1, bool COL2, int Q2>
+__device__ __forceinline__ void pair_colours(float* vk, float dch, v2f dp01, float dp2, float dq0, v2f dq01,
+                                             float dq2) {
+    if (COL1) {
+        const v2f t = dch * dp01;
+        vk[0] = t.x;
+        vk[1] = t.y;
+        vk[2] = dch * dp2;
+    }
+    float* v2 = vk + (COL1 ? 3 : 0);
+    if (COL2 && Q2 == 1) {
+        v2[0] = dch * dq0;
+    } else if (COL2) {
+        const v2f t = dch * dq01;
+        v2[0] = t.x;
+        v2[1] = t.y;
+        v2[2] = dch * dq2;
+    }
+}
+// Row totals of 4 entries x N values (entry-major) -> the LDS slots of this
+// lane's entry: dst points at the entry's slot (+ the pass's value offset).
+template <int N>
+__device__ __forceinline__ void reduce_store(const float (&v)[4 * N], int lane, float* dst, bool store) {
+    float r[RowReduce<N>::R];
+    row_reduce<N>(v, r, lane);
+    if (store && (lane & RowReduce<N>::WRITER_MASK) == 0) {
+        float* p = dst + row_m0<N>(lane);
+#pragma unroll
+        for (int m = 0; m < RowReduce<N>::R; m++) p[m] = r[m];
+    }
+}
+
 // Gaussians staged per batch: the per-row partial sums take 16 x batch x NV floats of LDS
 template <int NV>
 constexpr int bwd_batch() { return NV <= 6 ? 64 : 32; }
@@ -51,10 +97,9 @@ constexpr int bwd_batch() { return NV <= 6 ? 64 : 32; }
 // at once, so there is no second dispatch round behind the slowest tiles.
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2>
 constexpr int bwd_nv() { return 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2 : 0); }
-// the wide dual variants (mapping-style: colour gradients of both sets) need more
-// than 96 VGPRs: 4 waves per SIMD instead of spilling
+// 5 waves per SIMD for every variant (the wide ones reduce in two passes to fit 96 VGPRs)
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2>
-constexpr int bwd_waves() { return (DUAL && bwd_nv<DUAL, OPAC, COL1, COL2, Q2>() >= 8) ? 4 : 5; }
+constexpr int bwd_waves() { return 5; }
 
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3>
 __global__ void __launch_bounds__(TILE_PIX, (bwd_waves<DUAL, OPAC, COL1, COL2, Q2>()))
@@ -70,7 +115,6 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     constexpr int O_OP = 5, O_C1 = 5 + (OPAC ? 1 : 0), O_C2 = O_C1 + (COL1 ? 3 : 0);
     constexpr int BB = bwd_batch<NV>();
     constexpr int LS = BB + 4;  // row-list stride (u16)
-    using RRd = RowReduce<NV>;
     __shared__ float4 s_a[BB];
     __shared__ float4 s_b[BB];
     __shared__ float4 s_c[BB];
@@ -131,8 +175,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     const v2f pix = v2f{(float)px, (float)py};
     const v2f dp01 = v2f{dp0, dp1}, dq01 = v2f{dq0, dq1};
     float T = T_final, A = 0.f;
-    const int my_e = row_entry(lane), my_m0 = row_m0<NV>(lane);
-    const bool writer = (lane & RRd::WRITER_MASK) == 0;
+    const int my_e = row_entry(lane);
     float* acc_row = s_acc + (4 * w + row) * BB * NV;
     const uint16_t* my_list = s_list + (4 * w + row) * LS;
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
@@ -223,41 +266,35 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             // h = G * dL/dG = (o * G) * dL/dalpha.  gauss_bwd turns them into the reference's
             // per-pair quantities (backward.cu:1020-1038): dmean2D = -ddel * (Q [hx, hy]),
             // dconic = -0.5 * (hxx, hxy, hyy); both are linear in the sums (Q is per Gaussian).
-            float v[4 * NV];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                float* vk = v + NV * k;
-                const v2f hv = (araw[k] * dLa[k]) * d[k];   // (hx, hy)
-                const v2f hh = hv.x * d[k];                  // (hx dx, hx dy)
-                vk[0] = hv.x;
-                vk[1] = hv.y;
-                vk[2] = hh.x;
-                vk[3] = hh.y;
-                vk[4] = hv.y * d[k].y;
-                if (OPAC) vk[O_OP] = G[k] * dLa[k];
-                if (COL1) {
-                    const v2f t = dch[k] * dp01;
-                    vk[O_C1] = t.x;
-                    vk[O_C1 + 1] = t.y;
-                    vk[O_C1 + 2] = dch[k] * dp2;
-                }
-                if (COL2 && Q2 == 1) {
-                    vk[O_C2] = dch[k] * dq0;
-                } else if (COL2) {
-                    const v2f t = dch[k] * dq01;
-                    vk[O_C2] = t.x;
-                    vk[O_C2 + 1] = t.y;
-                    vk[O_C2 + 2] = dch[k] * dq2;
-                }
-            }
-            float r[RRd::R];
-            row_reduce<NV>(v, r, lane);  // lane class (my_e, my_m0) holds its slice of the row totals
             const int je = my_e == 0 ? gq.j[0] : (my_e == 1 ? gq.j[1] : (my_e == 2 ? gq.j[2] : gq.j[3]));
             const bool ve = my_e == 0 ? gq.valid[0] : (my_e == 1 ? gq.valid[1] : (my_e == 2 ? gq.valid[2] : gq.valid[3]));
-            if (writer && ve) {
-                float* dst = acc_row + je * NV + my_m0;
+            float* dst = acc_row + je * NV;
+            if constexpr (NV <= 6) {  // one reduction over all values
+                float v[4 * NV];
 #pragma unroll
-                for (int m = 0; m < RRd::R; m++) dst[m] = r[m];
+                for (int k = 0; k < 4; k++) {
+                    pair_geom<OPAC>(v + NV * k, araw[k], dLa[k], G[k], d[k]);
+                    pair_colours<COL1, COL2, Q2>(v + NV * k + O_C1, dch[k], dp01, dp2, dq0, dq01, dq2);
+                }
+                reduce_store<NV>(v, lane, dst, ve);
+            } else {  // wide variants: geometric, then opacity + colour sums (register pressure)
+                constexpr int NB = NV - 5;
+                {
+                    float v[4 * 5];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) pair_geom<false>(v + 5 * k, araw[k], dLa[k], G[k], d[k]);
+                    reduce_store<5>(v, lane, dst, ve);
+                }
+                {
+                    float v[4 * NB];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        if (OPAC) v[NB * k] = G[k] * dLa[k];
+                        pair_colours<COL1, COL2, Q2>(v + NB * k + (OPAC ? 1 : 0), dch[k], dp01, dp2, dq0, dq01,
+                                                     dq2);
+                    }
+                    reduce_store<NB>(v, lane, dst + 5, ve);
+                }
             }
         }
         __syncthreads();
