@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=("auto", "on", "off"), default="auto")
     ap.add_argument("--graph", type=int, default=1, help="1: replay the tracking iterations as a HIP graph")
     ap.add_argument("--iters-per-graph", type=int, default=20)
+    ap.add_argument("--timing", type=int, default=1,
+                    help="0: no device-clock timing of render_bwd in the graph (A/B check; no roofline)")
     return ap.parse_args()
 
 
@@ -128,7 +130,7 @@ def main():
         from splatam_amd.tracker import GraphTracker
         S = max(1, min(args.iters_per_graph, args.steps))
         steps = -(-args.steps // S) * S
-        tracker = GraphTracker(params, curr, frame, iters_per_graph=S, timing=True,
+        tracker = GraphTracker(params, curr, frame, iters_per_graph=S, timing=bool(args.timing),
                                warmup_iters=min(3, max(1, args.warmup)))
         for _ in range(max(1, args.warmup // S)):
             tracker.run()
@@ -193,7 +195,7 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic, "alg_bytes_per_launch": int(bytes_per_launch), "avg_us": round(rb["avg_us"], 2),
                 "num_rendered_avg": int(I_avg), "launches_timed": int(rb["launches"]),
-                "timing": "device wall_clock64 stamps around each launch (HIP graph)" if tracker is not None
+                "timing": "in-kernel wall_clock64 (first workgroup start to last workgroup end) of every launch in the timed HIP-graph replays" if tracker is not None
                 else "hipEvents around each launch"}
 
     # ---- CPU baseline: the float32 C oracle on one frame (rank 0, N=1) ------

@@ -186,9 +186,12 @@ int gsr_abi_version(void);
 #define GSR_STAGE_GAUSS_BWD 6  /* per-Gaussian chain rule        */
 #define GSR_NUM_STAGES 7
 /* on: 0 off, 1 hipEvents around every stage (not usable under stream capture),
- * GSR_TIMING_CLOCK | stage_mask: device-clock mode -- one-thread kernels read
- * wall_clock64() before/after the stages in stage_mask (bit = stage id) and
- * accumulate on the device, so captured HIP graphs accumulate over every replay. */
+ * GSR_TIMING_CLOCK | stage_mask: device-clock mode -- the stages in stage_mask
+ * (bit = stage id) are timed with wall_clock64() on the device and accumulated
+ * there, so captured HIP graphs accumulate over every replay.  The render
+ * stages stamp themselves inside the kernel (first workgroup start -> last
+ * workgroup end, no extra launches); other stages get one-thread stamp kernels
+ * before/after their launches. */
 #define GSR_TIMING_CLOCK 0x100
 int gsr_timing_enable(int on);
 int gsr_timing_read(double* ms, long long* launches, long long* units, int n);

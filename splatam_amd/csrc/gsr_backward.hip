@@ -107,9 +107,14 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                   const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
                   const float* __restrict__ final_T,
                   const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
-                  const float* __restrict__ dL_dpix2, float4* __restrict__ inst, BwdGuard guard) {
+                  const float* __restrict__ dL_dpix2, float4* __restrict__ inst, BwdGuard guard,
+                  unsigned long long* clk) {
     static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
-    if (guard.overflow()) return;  // invalid forward state (static-mode overflow): touch nothing
+    kclock_begin(clk);
+    if (guard.overflow()) {  // invalid forward state (static-mode overflow): touch nothing
+        kclock_end(clk);
+        return;
+    }
     static_assert(Q2 == 1 || Q2 == 3, "Q2 is 1 or 3 channels");
     constexpr int NV = bwd_nv<DUAL, OPAC, COL1, COL2, Q2>();
     constexpr int O_OP = 5, O_C1 = 5 + (OPAC ? 1 : 0), O_C2 = O_C1 + (COL1 ? 3 : 0);
@@ -325,6 +330,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         }
         __syncthreads();
     }
+    kclock_end(clk);
 }
 
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3>
@@ -333,7 +339,7 @@ static auto bwd_variant() { return render_bwd_kernel<DUAL, OPAC, COL1, COL2, Q2>
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
                              const float* colors2, const float* dL_dpix2, unsigned need, float4* inst,
-                             BwdGuard guard, hipStream_t s) {
+                             BwdGuard guard, hipStream_t s, unsigned long long* clk) {
     const bool op = need & NEED_OPACITY, c1 = need & NEED_COLORS, c2 = colors2 && (need & NEED_COLORS2);
     const bool q1 = need & NEED_DL2_CH0_ONLY;
     auto k = bwd_variant<false, true, true, false>();
@@ -349,7 +355,7 @@ hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint3
                      : (c2 ? bwd_variant<true, 0, 0, 1>() : bwd_variant<true, 0, 0, 0>()));
     }
     hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rr, geo.blocksums,
-                       final_T, n_contrib, dL_dpix, dL_dpix2, inst, guard);
+                       final_T, n_contrib, dL_dpix, dL_dpix2, inst, guard, clk);
     return hipGetLastError();
 }
 

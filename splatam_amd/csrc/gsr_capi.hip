@@ -161,6 +161,8 @@ hipError_t zero_async(void* p, size_t bytes, hipStream_t s) {
     return hipGetLastError();
 }
 
+size_t kclock_bytes() { return (size_t)KCLOCK_WORDS * sizeof(unsigned long long) * GSR_NUM_STAGES; }
+
 __global__ void stamp_begin_kernel(unsigned long long* c) { c[0] = wall_clock64(); }
 __global__ void stamp_end_kernel(unsigned long long* c) {
     c[1] += wall_clock64() - c[0];
@@ -182,13 +184,20 @@ struct StageTimer {  // brackets the launches of one stage
     hipStream_t s;
     bool on;
     unsigned long long* dc = nullptr;
-    StageTimer(int stage, long long units, hipStream_t s_) : s(s_), on(g_timing.on) {
+    unsigned long long* kc = nullptr;  // in-kernel clock slot (stages whose kernel stamps itself)
+    // in_kernel: the stage is one launch that takes kclock() and stamps itself
+    // (kclock_begin / kclock_end), so no stamp kernels are added around it
+    StageTimer(int stage, long long units, hipStream_t s_, bool in_kernel = false) : s(s_), on(g_timing.on) {
         if (!on) return;
         if (g_timing.clock) {
             on = false;
             if ((g_timing.mask >> stage) & 1u) {
-                dc = g_timing.dclock + 4 * stage;
-                hipLaunchKernelGGL(stamp_begin_kernel, dim3(1), dim3(1), 0, s, dc);
+                if (in_kernel) {
+                    kc = g_timing.dclock + (size_t)KCLOCK_WORDS * stage;
+                } else {
+                    dc = g_timing.dclock + (size_t)KCLOCK_WORDS * stage;
+                    hipLaunchKernelGGL(stamp_begin_kernel, dim3(1), dim3(1), 0, s, dc);
+                }
             }
             return;
         }
@@ -199,6 +208,7 @@ struct StageTimer {  // brackets the launches of one stage
         }
         (void)record_event(rec.a, s);
     }
+    unsigned long long* kclock() const { return kc; }
     ~StageTimer() {
         if (dc) hipLaunchKernelGGL(stamp_end_kernel, dim3(1), dim3(1), 0, s, dc);
         if (!on) return;
@@ -369,9 +379,9 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
                 return hip_fail(e, "tile sort");
         }
         {
-            StageTimer t(GSR_STAGE_RENDER_FWD, 0, stream);
+            StageTimer t(GSR_STAGE_RENDER_FWD, 0, stream, true);
             if ((e = launch_render_fwd(cam, ranges, point_list, geo, colors2, final_T, n_contrib, out_color,
-                                       out_color2, out_depth, guard, stream)) != hipSuccess)
+                                       out_color2, out_depth, guard, stream, t.kclock())) != hipSuccess)
                 return hip_fail(e, "render");
         }
         speculated = true;
@@ -431,10 +441,9 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         }
     }
     {
-        StageTimer t(GSR_STAGE_RENDER_FWD, I, stream);
+        StageTimer t(GSR_STAGE_RENDER_FWD, I, stream, true);
         if ((e = launch_render_fwd(cam, ranges, point_list, geo, colors2, final_T, n_contrib, out_color, out_color2,
-                                   out_depth,
-                                   none, stream)) != hipSuccess)
+                                   out_depth, none, stream, t.kclock())) != hipSuccess)
             return hip_fail(e, "render");
     }
     return (int)I;
@@ -513,13 +522,13 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
         if (!inst) return fail(GSR_ERR_ALLOC, "allocator returned NULL (backward scratch)");
         const char* bb = (const char*)binning_buffer;
         const uint32_t* point_list = (const uint32_t*)(bb + BL.point_list);
-        StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream);
+        StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream, true);
         // SH colours feed dL/dmeans3D through the view direction, so their sums are needed with SH
         const unsigned need = (out.dopacity ? NEED_OPACITY : 0u) | ((out.dcolors || g.shs) ? NEED_COLORS : 0u) |
                               (dcolors2 ? NEED_COLORS2 : 0u) | (dl2_channels == 1 ? NEED_DL2_CH0_ONLY : 0u);
         if ((e = launch_render_bwd(cam, ranges, point_list, geo, final_T, n_contrib, dL_dout_color, colors2,
                                    dL_dout_color2, need, inst, BwdGuard{geo.counters, (uint32_t)num_rendered},
-                                   stream)) != hipSuccess)
+                                   stream, t.kclock())) != hipSuccess)
             return hip_fail(e, "render backward");
     }
     out.dcolors2 = dcolors2;
@@ -553,9 +562,9 @@ int gsr_timing_enable(int on) {
     if (g_timing.clock) {
         hipError_t e;
         if (!g_timing.dclock &&
-            (e = hipMalloc((void**)&g_timing.dclock, 4 * sizeof(unsigned long long) * GSR_NUM_STAGES)) != hipSuccess)
+            (e = hipMalloc((void**)&g_timing.dclock, kclock_bytes())) != hipSuccess)
             return hip_fail(e, "timing clock buffer");
-        if ((e = hipMemset(g_timing.dclock, 0, 4 * sizeof(unsigned long long) * GSR_NUM_STAGES)) != hipSuccess)
+        if ((e = hipMemset(g_timing.dclock, 0, kclock_bytes())) != hipSuccess)
             return hip_fail(e, "timing clock reset");
     }
     return GSR_OK;
@@ -565,17 +574,17 @@ int gsr_timing_read(double* ms, long long* launches, long long* units, int n) {
     std::lock_guard<std::mutex> lk(g_timing_mu);
     timing_drain();
     if (g_timing.clock && g_timing.dclock) {
-        unsigned long long h[4 * GSR_NUM_STAGES];
+        std::vector<unsigned long long> h((size_t)KCLOCK_WORDS * GSR_NUM_STAGES);
         int dev = 0, khz = 0;
         hipError_t e;
-        if ((e = hipMemcpy(h, g_timing.dclock, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess)
+        if ((e = hipMemcpy(h.data(), g_timing.dclock, kclock_bytes(), hipMemcpyDeviceToHost)) != hipSuccess)
             return hip_fail(e, "timing clock read");
         if ((e = hipGetDevice(&dev)) != hipSuccess ||
             (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev)) != hipSuccess || khz <= 0)
             return fail(GSR_ERR_HIP, "wall clock rate unavailable");
         for (int i = 0; i < GSR_NUM_STAGES; i++) {
-            g_timing.ms[i] = (double)h[4 * i + 1] / (double)khz;
-            g_timing.launches[i] = (long long)h[4 * i + 2];
+            g_timing.ms[i] = (double)h[(size_t)KCLOCK_WORDS * i + 1] / (double)khz;
+            g_timing.launches[i] = (long long)h[(size_t)KCLOCK_WORDS * i + 2];
         }
     }
     for (int i = 0; i < n && i < GSR_NUM_STAGES; i++) {

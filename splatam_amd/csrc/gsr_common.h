@@ -486,6 +486,46 @@ __device__ __forceinline__ RowGroup4 load_row_group4(const uint16_t* row_list, i
     return g;
 }
 
+// In-kernel device-clock timing of one launch (graph-capturable, no extra
+// kernels): clk = [start, sum of durations, launches, groups done, then 16 group
+// counters KCLOCK_GROUP_STRIDE words apart].  The first workgroup stamps the
+// start; workgroups count themselves done in 16 counters on separate cache lines
+// (one counter for all 1200 workgroups serialised ~10 us of same-address
+// atomics at the end of the launch), the last of each group counts the group,
+// and the last group adds (now - start) and resets the counters for the next
+// launch.  wall_clock64 runs at 100 MHz.
+constexpr int KCLOCK_GROUP_STRIDE = 32;  // u64 words (256 B)
+constexpr int KCLOCK_WORDS = 4 + 16 * KCLOCK_GROUP_STRIDE;
+__device__ __forceinline__ void kclock_begin(unsigned long long* clk) {
+    if (clk && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        __hip_atomic_store(&clk[0], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Relaxed agent-scope atomics throughout: a release/acquire fence per workgroup
+// costs an L2 writeback each on this multi-XCD part (~4% of the tracking step).
+// Only workgroup 0 (the one that stamped the start) releases, and only the last
+// one acquires.
+__device__ __forceinline__ void kclock_end(unsigned long long* clk) {  // every thread of the block calls this
+    if (!clk) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x, g = b & 15u;
+        const unsigned ngroups = nb < 16u ? nb : 16u;
+        const unsigned gsize = nb / 16u + (g < nb % 16u ? 1u : 0u);
+        unsigned long long* gc = clk + 4 + g * KCLOCK_GROUP_STRIDE;
+        if (b == 0) __atomic_thread_fence(__ATOMIC_RELEASE);
+        if (__hip_atomic_fetch_add(gc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+            __hip_atomic_store(gc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_fetch_add(&clk[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1) {
+                __atomic_thread_fence(__ATOMIC_ACQUIRE);
+                const unsigned long long t0 = __hip_atomic_load(&clk[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                clk[1] += wall_clock64() - t0;
+                clk[2] += 1;
+                __hip_atomic_store(&clk[3], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
 // --------------------------------------------------------- wave64 helpers --
 template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float v) {
@@ -728,12 +768,13 @@ hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t
                              hipStream_t s);
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
-                             float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s);
+                             float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
+                             unsigned long long* clk = nullptr);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* vis, hipStream_t s);
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
                              const float* colors2, const float* dL_dpix2, unsigned need, float4* inst, BwdGuard guard,
-                             hipStream_t s);
+                             hipStream_t s, unsigned long long* clk = nullptr);
 // which optional per-pair sums render_bwd forms (the geometric ones always)
 constexpr unsigned NEED_OPACITY = 1u, NEED_COLORS = 2u, NEED_COLORS2 = 4u;
 constexpr unsigned NEED_DL2_CH0_ONLY = 8u;  // dL_dpix2 channels 1, 2 are promised zero

@@ -700,8 +700,12 @@ __global__ void __launch_bounds__(TILE_PIX, 5)
 render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                   const float4* __restrict__ rr, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                   float* __restrict__ out_color, float* __restrict__ out_color2, float* __restrict__ out_depth,
-                  SpecGuard guard) {
-    if (guard.overflow()) return;
+                  SpecGuard guard, unsigned long long* clk) {
+    kclock_begin(clk);
+    if (guard.overflow()) {
+        kclock_end(clk);
+        return;
+    }
     __shared__ float4 s_a[RENDER_BATCH];
     __shared__ float4 s_b[RENDER_BATCH];
     __shared__ float4 s_c[RENDER_BATCH];
@@ -810,14 +814,16 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             out_color2[2 * HW + pid] = C5 + T * cam.bg[2];
         }
     }
+    kclock_end(clk);
 }
 
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
-                             float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s) {
+                             float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
+                             unsigned long long* clk) {
     auto k = colors2 ? render_fwd_kernel<true> : render_fwd_kernel<false>;
     hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rr, final_T,
-                       n_contrib, out_color, out_color2, out_depth, guard);
+                       n_contrib, out_color, out_color2, out_depth, guard, clk);
     return hipGetLastError();
 }
 

@@ -108,8 +108,8 @@ def camera_settings(cam, device) -> GaussianRasterizationSettings:
     return GaussianRasterizationSettings(
         image_height=cam.H, image_width=cam.W, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
         bg=torch.zeros(3, dtype=torch.float32, device=device), scale_modifier=1.0,
-        viewmatrix=cam.viewmatrix.to(device), projmatrix=cam.projmatrix.to(device), sh_degree=0,
-        campos=cam.campos.to(device), prefiltered=False)
+        viewmatrix=cam.viewmatrix.to(device).contiguous(), projmatrix=cam.projmatrix.to(device).contiguous(),
+        sh_degree=0, campos=cam.campos.to(device).contiguous(), prefiltered=False)  # contiguous: no per-call copy
 
 
 @dataclass
