@@ -97,9 +97,11 @@ constexpr int bwd_batch() { return NV <= 6 ? 64 : 32; }
 // at once, so there is no second dispatch round behind the slowest tiles.
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2>
 constexpr int bwd_nv() { return 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2 : 0); }
-// 5 waves per SIMD for every variant (the wide ones reduce in two passes to fit 96 VGPRs)
+// 5 waves per SIMD (96 VGPRs; the wide variants reduce in two passes to fit), except
+// the dual variants with a 3-channel second gradient (mapping-style), which spill
+// at 96 VGPRs and run at 4
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2>
-constexpr int bwd_waves() { return 5; }
+constexpr int bwd_waves() { return (DUAL && Q2 == 3) ? 4 : 5; }
 
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3>
 __global__ void __launch_bounds__(TILE_PIX, (bwd_waves<DUAL, OPAC, COL1, COL2, Q2>()))
@@ -120,13 +122,16 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     constexpr int O_OP = 5, O_C1 = 5 + (OPAC ? 1 : 0), O_C2 = O_C1 + (COL1 ? 3 : 0);
     constexpr int BB = bwd_batch<NV>();
     constexpr int LS = BB + 4;  // row-list stride (u16)
-    __shared__ float4 s_a[BB];
-    __shared__ float4 s_b[BB];
-    __shared__ float4 s_c[BB];
-    __shared__ float4 s_d[DUAL ? BB : 1];
+    // entry BB is a dummy (opacity 0, never blends) that pads the row lists; its
+    // per-block slots absorb the pad entries' (zero) sums
+    constexpr int SL = BB + 1;  // per-block slot count
+    __shared__ float4 s_a[SL];
+    __shared__ float4 s_b[SL];
+    __shared__ float4 s_c[SL];
+    __shared__ float4 s_d[DUAL ? SL : 1];
     __shared__ uint32_t s_u[BB];
     __shared__ uint16_t s_mask[BB];
-    __shared__ __attribute__((aligned(16))) float s_acc[16 * BB * NV];
+    __shared__ __attribute__((aligned(16))) float s_acc[16 * SL * NV];
     __shared__ uint32_t s_rmax[16];
     __shared__ __attribute__((aligned(16))) uint16_t s_list[16 * LS];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, row = (tid >> 4) & 3;
@@ -181,48 +186,49 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     const v2f dp01 = v2f{dp0, dp1}, dq01 = v2f{dq0, dq1};
     float T = T_final, A = 0.f;
     const int my_e = row_entry(lane);
-    float* acc_row = s_acc + (4 * w + row) * BB * NV;
+    float* acc_row = s_acc + (4 * w + row) * SL * NV;
     const uint16_t* my_list = s_list + (4 * w + row) * LS;
+    if (tid == 0) {
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        s_a[BB] = z;
+        s_b[BB] = z;
+        s_c[BB] = z;
+        if (DUAL) s_d[BB] = z;
+    }
+    // Batch staging: thread t < batch holds entry t's render record (already in its
+    // LDS form) for the next batch while the current one is rasterised.
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
     uint32_t pu = 0;
-    if (tid < min(BB, (int)bmax)) {
-        const uint32_t gi = point_list[range.x + bmax - 1 - tid];
-        const RenderRec r = load_rr(rr, gi);
-        pu = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), blockIdx.x, blockIdx.y);
-        pa = r.q0; pb = r.q1; pc = r.q2;
-        if (DUAL) pd = r.q3;
-    }
+    auto fetch = [&](int hi_) {
+        if (tid < min(BB, hi_)) {
+            const uint32_t gi = point_list[range.x + (uint32_t)(hi_ - 1 - tid)];
+            const RenderRec r = load_rr(rr, gi);
+            pu = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), blockIdx.x, blockIdx.y);
+            pa = r.q0; pb = r.q1; pc = r.q2;
+            if (DUAL) pd = r.q3;
+        }
+    };
+    fetch((int)bmax);
     for (int hi = (int)bmax; hi > 0; hi -= BB) {
         const int cnt = min(BB, hi);
         if (tid < cnt) {
             s_u[tid] = pu;
-            s_a[tid] = stage_a(pa, pb);
-            s_b[tid] = stage_b(pa, pb);
+            s_a[tid] = pa;
+            s_b[tid] = pb;
             s_c[tid] = pc;
             if (DUAL) s_d[tid] = pd;
             s_mask[tid] = (uint16_t)block_mask(pa, pb, x0, y0);
         }
-        for (int q = tid; q < 16 * BB * NV / 4; q += TILE_PIX)
+        for (int q = tid; q < 16 * SL * NV / 4; q += TILE_PIX)
             reinterpret_cast<float4*>(s_acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         __syncthreads();
-        {   // prefetch the next batch
-            const int nhi = hi - BB;
-            if (tid < min(BB, nhi)) {
-                const uint32_t gi = point_list[range.x + (uint32_t)(nhi - 1 - tid)];
-                const RenderRec r = load_rr(rr, gi);
-                pu = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), blockIdx.x, blockIdx.y);
-                pa = r.q0; pb = r.q1; pc = r.q2;
-                if (DUAL) pd = r.q3;
-            }
-        }
+        fetch(hi - BB);  // prefetch the next batch
         // entries j with pos = hi-1-j >= rmax lie behind every pixel of the block
         const int jmin[4] = {hi - rm[0], hi - rm[1], hi - rm[2], hi - rm[3]};
-        int nr[4];
-        build_row_lists(s_mask, cnt, w, jmin, s_list + 4 * w * LS, LS, nr);
-        const int n = max(max(nr[0], nr[1]), max(nr[2], nr[3]));
-        const int nmine = row == 0 ? nr[0] : (row == 1 ? nr[1] : (row == 2 ? nr[2] : nr[3]));
+        const int n = build_row_lists(s_mask, cnt, w, jmin, s_list + 4 * w * LS, LS, (uint16_t)BB);
+        const int jlo = hi - (int)last;  // pos = hi-1-j < last  <=>  j >= jlo
         for (int i = 0; i < n; i += 4) {
-            const RowGroup4 gq = load_row_group4(my_list, i, nmine);
+            const RowGroup4 gq = load_row_group4(my_list, i);
             v2f d[4];
             float G[4], araw[4], alpha[4];
             bool ok[4];
@@ -235,8 +241,11 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 G[k] = __builtin_amdgcn_exp2f(fminf(p2, 0.f));             // finite for every lane
                 araw[k] = b.y * G[k];
                 alpha[k] = fminf(0.99f, araw[k]);
-                const uint32_t pos = (uint32_t)(hi - 1 - gq.j[k]);         // position in the tile list
-                ok[k] = gq.valid[k] && pos < last && p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;
+                // position in the tile list before the pixel's last contributor; the pad entry
+                // has alpha 0.  Non-contributing pairs continue with alpha 0: T and A then pass
+                // through unchanged (1 / (1 - 0) == 1 exactly) and only dL/dalpha needs a mask.
+                ok[k] = gq.j[k] >= jlo && p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;
+                alpha[k] = ok[k] ? alpha[k] : 0.f;
                 any = any || ok[k];
             }
             if (__ballot(any) == 0ull) continue;  // slots stay zero
@@ -263,16 +272,15 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 const float e = cd - A;
                 const bool o = ok[k];
                 dLa[k] = o ? __builtin_fmaf(Tbg, inv, e * Tn) : 0.f;
-                dch[k] = o ? alpha[k] * Tn : 0.f;
-                T = o ? Tn : T;
-                A = o ? __builtin_fmaf(alpha[k], e, A) : A;
+                dch[k] = alpha[k] * Tn;                 // 0 when masked
+                T = o ? Tn : T;                         // (select: keeps T exact whatever rcp(1) returns)
+                A = __builtin_fmaf(alpha[k], e, A);     // unchanged when masked
             }
             // Per pair: (hx, hy, hx*dx, hx*dy, hy*dy, G*dL/dalpha, dch*dL/dpix, dch*dL/dpix2) with
             // h = G * dL/dG = (o * G) * dL/dalpha.  gauss_bwd turns them into the reference's
             // per-pair quantities (backward.cu:1020-1038): dmean2D = -ddel * (Q [hx, hy]),
             // dconic = -0.5 * (hxx, hxy, hyy); both are linear in the sums (Q is per Gaussian).
             const int je = my_e == 0 ? gq.j[0] : (my_e == 1 ? gq.j[1] : (my_e == 2 ? gq.j[2] : gq.j[3]));
-            const bool ve = my_e == 0 ? gq.valid[0] : (my_e == 1 ? gq.valid[1] : (my_e == 2 ? gq.valid[2] : gq.valid[3]));
             float* dst = acc_row + je * NV;
             if constexpr (NV <= 6) {  // one reduction over all values
                 float v[4 * NV];
@@ -281,14 +289,14 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                     pair_geom<OPAC>(v + NV * k, araw[k], dLa[k], G[k], d[k]);
                     pair_colours<COL1, COL2, Q2>(v + NV * k + O_C1, dch[k], dp01, dp2, dq0, dq01, dq2);
                 }
-                reduce_store<NV>(v, lane, dst, ve);
+                reduce_store<NV>(v, lane, dst, true);
             } else {  // wide variants: geometric, then opacity + colour sums (register pressure)
                 constexpr int NB = NV - 5;
                 {
                     float v[4 * 5];
 #pragma unroll
                     for (int k = 0; k < 4; k++) pair_geom<false>(v + 5 * k, araw[k], dLa[k], G[k], d[k]);
-                    reduce_store<5>(v, lane, dst, ve);
+                    reduce_store<5>(v, lane, dst, true);
                 }
                 {
                     float v[4 * NB];
@@ -298,7 +306,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                         pair_colours<COL1, COL2, Q2>(v + NB * k + (OPAC ? 1 : 0), dch[k], dp01, dp2, dq0, dq01,
                                                      dq2);
                     }
-                    reduce_store<NB>(v, lane, dst + 5, ve);
+                    reduce_store<NB>(v, lane, dst + 5, true);
                 }
             }
         }
@@ -310,7 +318,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             const uint32_t mask = s_mask[tid];
             for (int b = 0; b < 16; b++) {  // fixed block order: deterministic
                 if (!((mask >> b) & 1u)) continue;
-                const float* src = s_acc + (b * BB + tid) * NV;
+                const float* src = s_acc + (b * SL + tid) * NV;
 #pragma unroll
                 for (int m = 0; m < NV; m++) c[m] += src[m];
             }
@@ -383,14 +391,15 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
             g2[8] += r2.x;
             dcol2[0] += r2.y; dcol2[1] += r2.z; dcol2[2] += r2.w;
         }
-        // instance records hold (hx, hy, hxx, hxy, hyy, dopacity, dcolor) sums (render_bwd_kernel)
-        const float4* rri = geo.rr + (size_t)RR_F4 * i;
-        const float4 ra = rri[0];
-        const float Cc = rri[1].x;
+        // instance records hold (hx, hy, hxx, hxy, hyy, dopacity, dcolor) sums (render_bwd_kernel);
+        // the conic is recomputed exactly as preprocess computed it (the render record keeps
+        // only its exp2-scaled form)
+        float ca, cb, cc;
+        gaussian_conic(cam, g, i, ca, cb, cc);
         const float ddelx = (float)(0.5 * cam.W), ddely = (float)(0.5 * cam.H);  // backward.cu:935-936
         const float hx = g2[0], hy = g2[1];
-        g2[0] = -(ra.z * hx + ra.w * hy) * ddelx;
-        g2[1] = -(Cc * hy + ra.w * hx) * ddely;
+        g2[0] = -(ca * hx + cb * hy) * ddelx;
+        g2[1] = -(cc * hy + cb * hx) * ddely;
         g2[2] *= -0.5f;
         g2[3] *= -0.5f;
         g2[4] *= -0.5f;

@@ -9,7 +9,7 @@
 //
 //   gauss_jac         one lane per Gaussian: the chain is linear in the 9 per-pair
 //                     2D gradients (fixed clamp bits), so it is tabulated once per
-//                     Gaussian as an 80-float Jacobian pack (JAC_FLOATS):
+//                     Gaussian as an 84-float Jacobian pack (JAC_FLOATS; [80..82] the conic):
 //                       [ 0..23] dmean3D  <- (dmean2D.xy, dconic.ABC, dRGB.rgb)  3x8
 //                       [24..41] dcov3D   <- dconic                            6x3
 //                       [42..50] dscale   <- dconic                            3x3
@@ -77,6 +77,8 @@ gauss_jac_kernel(Camera cam, GaussIn g, const int* __restrict__ radii, float* __
             for (int k = 0; k < 16; k++) J[63 + k] = k < nsh ? dsh[3 * k] : 0.f;
     }
     J[79] = 0.f;
+    gaussian_conic(cam, g, i, J[JAC_CONIC], J[JAC_CONIC + 1], J[JAC_CONIC + 2]);  // as preprocess computed it
+    J[JAC_CONIC + 3] = 0.f;
 }
 
 hipError_t launch_gauss_jac(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, float* jac,
@@ -105,7 +107,6 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
     __shared__ float4 s_a[B];
     __shared__ float4 s_b[B];
     __shared__ float4 s_c[B];
-    __shared__ float4 s_q[B];  // raw conic (A, B, C)
     __shared__ uint32_t s_u[B];
     __shared__ uint32_t s_g[B];
     __shared__ float4 s_j[B * JF4];
@@ -158,10 +159,9 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
             const float4 pa = r.q0, pb = r.q1;
             s_g[tid] = gi;
             s_u[tid] = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), blockIdx.x, blockIdx.y);
-            s_a[tid] = stage_a(pa, pb);
-            s_b[tid] = stage_b(pa, pb);
+            s_a[tid] = pa;
+            s_b[tid] = pb;
             s_c[tid] = make_float4(r.q2.x, r.q2.y, r.q2.z, __uint_as_float(clamp_bits[gi]));
-            s_q[tid] = make_float4(pa.z, pa.w, pb.x, 0.f);
             s_mask[tid] = (uint8_t)quad_mask(pa, pb, x0, y0);
         }
         for (int q = tid; q < 4 * B * NVP / 4; q += TILE_PIX)
@@ -195,11 +195,17 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
             const float dch = alpha * Tn;
             const float h = araw * dL_dalpha;  // G * dL/dG
             const float hx = h * dx, hy = h * dy;
-            const float4 qc = s_q[j];
+            const float4* Jq = s_j + j * JF4;
+            float Jv[JAC_FLOATS];
+#pragma unroll
+            for (int m = 0; m < JF4; m++) {
+                const float4 t = Jq[m];
+                Jv[4 * m] = t.x; Jv[4 * m + 1] = t.y; Jv[4 * m + 2] = t.z; Jv[4 * m + 3] = t.w;
+            }
             // per-pair quantities of backward.cu:1020-1038
             float in8[8];
-            in8[0] = -(qc.x * hx + qc.y * hy) * ddelx;
-            in8[1] = -(qc.z * hy + qc.y * hx) * ddely;
+            in8[0] = -(Jv[JAC_CONIC] * hx + Jv[JAC_CONIC + 1] * hy) * ddelx;
+            in8[1] = -(Jv[JAC_CONIC + 2] * hy + Jv[JAC_CONIC + 1] * hx) * ddely;
             in8[2] = -0.5f * hx * dx;
             in8[3] = -0.5f * hx * dy;
             in8[4] = -0.5f * hy * dy;
@@ -208,13 +214,6 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
             in8[5] = (clamped & 1u) ? 0.f : col0;
             in8[6] = (clamped & 2u) ? 0.f : col1;
             in8[7] = (clamped & 4u) ? 0.f : col2;
-            const float4* Jq = s_j + j * JF4;
-            float Jv[JAC_FLOATS];
-#pragma unroll
-            for (int m = 0; m < JF4; m++) {
-                const float4 t = Jq[m];
-                Jv[4 * m] = t.x; Jv[4 * m + 1] = t.y; Jv[4 * m + 2] = t.z; Jv[4 * m + 3] = t.w;
-            }
             float v[NVP];
             v[0] = in8[0];
             v[1] = in8[1];

@@ -5,6 +5,23 @@
 
 namespace gsr {
 
+// Conic of Gaussian i as preprocess computed it (same helpers, same inputs).
+__device__ inline void gaussian_conic(const Camera& cam, const GaussIn& g, int i, float& ca, float& cb, float& cc) {
+    const float3 m = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
+    float c3[6];
+    if (g.cov3D) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) c3[k] = g.cov3D[6 * i + k];
+    } else {
+        float3 s = make_float3(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2]);
+        float4 q = make_float4(g.rotations[4 * i], g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3]);
+        cov3d_fwd(s, cam.scale_modifier, q, c3);
+    }
+    Proj pj;
+    cov2d_fwd(m, cam.focal_x, cam.focal_y, cam.tan_fovx, cam.tan_fovy, c3, cam.view, pj);
+    (void)conic_of(pj, ca, cb, cc);
+}
+
 // ------------------------------------------------------ per-Gaussian chain --
 // g2: [0..1] dL/dmean2D (NDC units), [2..4] dL/dconic (A, B/2, C), [5] dL/dopacity,
 // [6..8] dL/dcolor.  Outputs: dmean3D[3], dcov3D[6], dscale[3], drot[4], dsh[3*nsh].

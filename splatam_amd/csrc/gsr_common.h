@@ -31,9 +31,10 @@ constexpr int TILE_CTR_STRIDE = 64;  // per-tile atomic counters one 256-B line 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // One 64-byte render record per Gaussian (four float4, one cache-line fetch per
-// gather in the render kernels; the SoA form cost ~6 line fetches per instance):
-//   q0 = (x, y, conic A, conic B)     pixel coordinates
-//   q1 = (conic C, opacity, depth, workgroup-local instance offset bits)
+// gather in the render kernels; the SoA form cost ~6 line fetches per instance),
+// stored in the form the render loops evaluate (copied to LDS as is):
+//   q0 = (x, y, K_AC * conic A, K_AC * conic C)   pixel coordinates; K_AC = -log2(e)/2
+//   q1 = (K_B * conic B, opacity, depth, workgroup-local instance offset bits); K_B = -log2(e)
 //   q2 = (r, g, b, tile rect lo bits)   rect lo = x0 | y0 << 16
 //   q3 = (colors2 r, g, b, tile rect hi bits)   rect hi = x1 | y1 << 16; colors2 = 0 unless dual
 constexpr int RR_F4 = 4;
@@ -293,6 +294,19 @@ __device__ __forceinline__ void cov2d_fwd(float3 mean, float fx, float fy, float
     o.c = c + 0.3f;
 }
 
+// conic = inverse of the (dilated) 2D covariance (forward.cu:219-224), shared by
+// preprocess and the backward (which recomputes it rather than storing it):
+// one contraction-free sequence, so both get the same bits.  Returns det.
+__device__ __forceinline__ float conic_of(const Proj& pj, float& ca, float& cb, float& cc) {
+#pragma clang fp contract(off)
+    const float det = pj.a * pj.c - pj.b * pj.b;
+    const float det_inv = 1.f / det;
+    ca = pj.c * det_inv;
+    cb = -pj.b * det_inv;
+    cc = pj.a * det_inv;
+    return det;
+}
+
 // forward.cu:20-71 (one channel at a time, same order as the oracle)
 __device__ __forceinline__ void sh_fwd(int deg, float3 pos, const float* campos, const float* sh, float rgb[3],
                                        unsigned& clamped_bits) {
@@ -327,23 +341,19 @@ __device__ __forceinline__ void sh_fwd(int deg, float3 pos, const float* campos,
     }
 }
 
-// LDS staging form of a render record (from the geom records ra = (x, y, A, B),
-// rb = (C, opacity, depth, -)): the conic is prescaled so that
+// Render-record form of the conic (written by preprocess, staged to LDS as is):
+// prescaled so that
 //   p2 = A' dx^2 + B' dx dy + C' dy^2 = log2(e) * power      (forward.cu:341)
-// feeds v_exp_f32 (exp2) directly, and laid out as
-//   sa = (x, y, A', C'),  sb = (B', opacity, depth, -)
+// feeds v_exp_f32 (exp2) directly, laid out as
+//   sa = q0 = (x, y, A', C'),  sb = q1 = (B', opacity, depth, -)
 // so (x, y) - pixel and (A', C') * (dx, dy) are packed-f32 pairs.  Forward and
-// backward stage the same values and evaluate p2 through the same contraction-
+// backward read the same values and evaluate p2 through the same contraction-
 // free sequence, so both see bit-identical alphas (the backward recovers T by
 // dividing by 1 - alpha and must take exactly the forward's decisions).
 constexpr float kLog2e = 1.4426950408889634f;
 typedef float v2f __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float4 stage_a(float4 ra, float4 rb) {
-    return make_float4(ra.x, ra.y, -0.5f * kLog2e * ra.z, -0.5f * kLog2e * rb.x);
-}
-__device__ __forceinline__ float4 stage_b(float4 ra, float4 rb) {
-    return make_float4(-kLog2e * ra.w, rb.y, rb.z, 0.f);
-}
+constexpr float K_AC = -0.5f * kLog2e;  // render-record scale of conic A and C
+constexpr float K_B = -kLog2e;          // render-record scale of conic B
 __device__ __forceinline__ v2f pix_delta(float4 sa, v2f pix) {
 #pragma clang fp contract(off)
     return v2f{sa.x, sa.y} - pix;
@@ -370,7 +380,9 @@ __device__ __forceinline__ int tile_py(int tid) { return 8 * (tid >> 7) + 4 * ((
 // values, non-positive-definite conic, extreme eccentricity): no culling.
 // Sets never = true when alpha <= o < 1/255 (never blended).
 __device__ __forceinline__ bool alpha_extent(float4 a, float4 b, float& hx, float& hy, bool& never) {
-    const float A = a.z, B = a.w, C = b.x, o = b.y;
+    // conic from the render-record scaling (a few ulp off the preprocess values; the
+    // margins below are orders of magnitude larger)
+    const float A = a.z * (1.f / K_AC), B = b.x * (1.f / K_B), C = a.w * (1.f / K_AC), o = b.y;
     const float det = A * C - B * B;
     never = false;
     if (!(det > 0.f) || !(A > 0.f) || !isfinite(det) || !isfinite(a.x) || !isfinite(a.y) || !isfinite(o))
@@ -444,17 +456,19 @@ __device__ __forceinline__ int build_wave_list(const uint8_t* s_mask, int cnt, i
 
 // The four ordered lists of a wave's 16-lane rows: list[r] gets the batch
 // entries whose 16-bit block mask has bit 4w + r (ballot + popcount
-// compaction, order preserved), skipping entries j < jmin[r].  n[r] = length of
-// list r (wave-uniform).
-__device__ __forceinline__ void build_row_lists(const uint16_t* s_mask, int cnt, int w, const int (&jmin)[4],
-                                                uint16_t* list, int stride, int (&n)[4]) {
+// compaction, order preserved), skipping entries j < jmin[r].  Every list is
+// then padded with `pad` (the index of a staged dummy entry that never blends)
+// up to the returned length: the longest list rounded up to 4, so the rows of
+// a wave step through their lists in lockstep with no validity tests.
+template <typename MaskOf>
+__device__ __forceinline__ int build_row_lists_by(MaskOf mask_of, int cnt, int w, const int (&jmin)[4],
+                                                  uint16_t* list, int stride, uint16_t pad) {
     const int lane = __lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int r = 0; r < 4; r++) n[r] = 0;
+    int n[4] = {0, 0, 0, 0};
     for (int c = 0; c < cnt; c += 64) {
         const int j = c + lane;
-        const uint32_t m = j < cnt ? ((uint32_t)s_mask[j] >> (4 * w)) & 0xFu : 0u;
+        const uint32_t m = j < cnt ? (mask_of(j) >> (4 * w)) & 0xFu : 0u;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const bool bit = ((m >> r) & 1u) && j >= jmin[r];
@@ -463,26 +477,28 @@ __device__ __forceinline__ void build_row_lists(const uint16_t* s_mask, int cnt,
             n[r] += __popcll(bal);
         }
     }
+    const int len = (max(max(n[0], n[1]), max(n[2], n[3])) + 3) & ~3;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+        for (int p = n[r] + lane; p < len; p += 64) list[r * stride + p] = pad;
+    return len;
+}
+__device__ __forceinline__ int build_row_lists(const uint16_t* s_mask, int cnt, int w, const int (&jmin)[4],
+                                               uint16_t* list, int stride, uint16_t pad) {
+    return build_row_lists_by([&](int j) { return (uint32_t)s_mask[j]; }, cnt, w, jmin, list, stride, pad);
 }
 
-// Four consecutive entries of this lane's row list (per-lane, VGPR); entries
-// past the row's length are invalid and point at entry 0 (always staged).
+// Four consecutive entries of this lane's (padded) row list, per lane (VGPR).
 struct RowGroup4 {
     int j[4];
-    bool valid[4];
 };
-__device__ __forceinline__ RowGroup4 load_row_group4(const uint16_t* row_list, int i, int n) {
+__device__ __forceinline__ RowGroup4 load_row_group4(const uint16_t* row_list, int i) {
     const uint2 q = *reinterpret_cast<const uint2*>(&row_list[i]);
     RowGroup4 g;
     g.j[0] = (int)(q.x & 0xFFFFu);
     g.j[1] = (int)(q.x >> 16);
     g.j[2] = (int)(q.y & 0xFFFFu);
     g.j[3] = (int)(q.y >> 16);
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        g.valid[k] = i + k < n;
-        if (!g.valid[k]) g.j[k] = 0;
-    }
     return g;
 }
 
@@ -796,7 +812,8 @@ hipError_t launch_selftest_reduce9(const float* in, float* out, hipStream_t s);
 int fail(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* where);
 // backward_power != 1 (the vendored renderCUDAFused semantics, backward.cu:850-1140)
-constexpr int JAC_FLOATS = 80;  // per-Gaussian linear chain pack, see gsr_backward_power.hip
+constexpr int JAC_FLOATS = 84;  // per-Gaussian linear chain pack, see gsr_backward_power.hip
+constexpr int JAC_CONIC = 80;   // conic (A, B, C) inside the pack
 int power_record_floats(int nsh);  // values stored per instance record
 hipError_t launch_gauss_jac(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, float* jac,
                             hipStream_t s);

@@ -45,7 +45,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
         if (!ok && cam.prefiltered) violation = true;
         float cov3[6];
         Proj pj;
-        float det = 0.f;
+        float det = 0.f, ca = 0.f, cb = 0.f, cc = 0.f;
         if (ok) {
             if (g.cov3D) {
 #pragma unroll
@@ -56,12 +56,10 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                 cov3d_fwd(s, cam.scale_modifier, q, cov3);
             }
             cov2d_fwd(p, cam.focal_x, cam.focal_y, cam.tan_fovx, cam.tan_fovy, cov3, cam.view, pj);
-            det = pj.a * pj.c - pj.b * pj.b;
+            det = conic_of(pj, ca, cb, cc);
             ok = det != 0.0f;
         }
         if (ok) {
-            float det_inv = 1.f / det;
-            float ca = pj.c * det_inv, cb = -pj.b * det_inv, cc = pj.a * det_inv;
             float mid = 0.5f * (pj.a + pj.c);
             float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
             float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
@@ -85,10 +83,10 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                 }
                 const uint32_t rlo = (uint32_t)x0 | ((uint32_t)y0 << 16), rhi = (uint32_t)x1 | ((uint32_t)y1 << 16);
                 float4* rr = geo.rr + (size_t)RR_F4 * i;
-                rr[0] = make_float4(px, py, ca, cb);
+                rr[0] = make_float4(px, py, K_AC * ca, K_AC * cc);  // render-record conic form
                 rr[2] = make_float4(rgb[0], rgb[1], rgb[2], __uint_as_float(rlo));
                 rr[3] = make_float4(c2[0], c2[1], c2[2], __uint_as_float(rhi));
-                q1 = make_float4(cc, g.opacities[i], pv.z, 0.f);  // .w: workgroup-local instance offset, below
+                q1 = make_float4(K_B * cb, g.opacities[i], pv.z, 0.f);  // .w: workgroup-local instance offset, below
                 geo.bin[i] = make_uint4(rlo, rhi, __float_as_uint(pv.z), tiles);
                 geo.clamp[i] = clamped;
                 for (int ty = y0; ty < y1; ty++)  // per-tile instance counts -> bucket ranges
@@ -706,10 +704,11 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         kclock_end(clk);
         return;
     }
-    __shared__ float4 s_a[RENDER_BATCH];
-    __shared__ float4 s_b[RENDER_BATCH];
-    __shared__ float4 s_c[RENDER_BATCH];
-    __shared__ float4 s_d[DUAL ? RENDER_BATCH : 1];
+    // entry RENDER_BATCH is a dummy (opacity 0, never blends) that pads the row lists
+    __shared__ float4 s_a[RENDER_BATCH + 1];
+    __shared__ float4 s_b[RENDER_BATCH + 1];
+    __shared__ float4 s_c[RENDER_BATCH + 1];
+    __shared__ float4 s_d[DUAL ? RENDER_BATCH + 1 : 1];
     __shared__ uint16_t s_mask[RENDER_BATCH];
     constexpr int LS = RENDER_BATCH + 4;  // row-list stride (u16)
     __shared__ __attribute__((aligned(16))) uint16_t s_list[16 * LS];
@@ -726,6 +725,12 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     float C3 = 0.f, C4 = 0.f, C5 = 0.f;
     uint32_t last = 0;
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
+    if (tid == 0) {
+        s_a[RENDER_BATCH] = pa;
+        s_b[RENDER_BATCH] = pa;
+        s_c[RENDER_BATCH] = pa;
+        if (DUAL) s_d[RENDER_BATCH] = pa;
+    }
     if (range.x + tid < range.y) {
         const RenderRec r = load_rr(rr, point_list[range.x + tid]);
         pa = r.q0; pb = r.q1; pc = r.q2;
@@ -735,8 +740,8 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
         const int cnt = (int)min((uint32_t)RENDER_BATCH, range.y - start);
         if (tid < cnt) {
-            s_a[tid] = stage_a(pa, pb);
-            s_b[tid] = stage_b(pa, pb);
+            s_a[tid] = pa;
+            s_b[tid] = pb;
             s_c[tid] = pc;
             if (DUAL) s_d[tid] = pd;
             s_mask[tid] = (uint16_t)block_mask(pa, pb, x0, y0);
@@ -750,16 +755,13 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 if (DUAL) pd = r.q3;
             }
         }
-        int nr[4];
         const int jmin0[4] = {0, 0, 0, 0};
-        build_row_lists(s_mask, cnt, w, jmin0, s_list + 4 * w * LS, LS, nr);
-        const int n = max(max(nr[0], nr[1]), max(nr[2], nr[3]));
-        const int nmine = row == 0 ? nr[0] : (row == 1 ? nr[1] : (row == 2 ? nr[2] : nr[3]));
+        const int n = build_row_lists(s_mask, cnt, w, jmin0, s_list + 4 * w * LS, LS, (uint16_t)RENDER_BATCH);
         const uint16_t* my_list = s_list + (4 * w + row) * LS;
         const uint32_t pos0 = start - range.x;
         for (int i = 0; i < n; i += 4) {
             if (__ballot(!done) == 0ull) break;
-            const RowGroup4 gq = load_row_group4(my_list, i, nmine);
+            const RowGroup4 gq = load_row_group4(my_list, i);
             float alpha[4], depth[4];
             bool ok[4];
 #pragma unroll
@@ -768,7 +770,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                 const float p2 = eval_p2(a, b, pix_delta(a, pix));           // log2(e) * power
                 alpha[k] = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(fminf(p2, 0.f)));
                 depth[k] = b.z;
-                ok[k] = gq.valid[k] && p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;
+                ok[k] = p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;  // the pad entry has alpha 0
             }
 #pragma unroll
             for (int k = 0; k < 4; k++) {

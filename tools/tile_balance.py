@@ -38,6 +38,7 @@ def instance_culling(geom, v, W, H, R, P):
     ty, tx = tile_of // gx, tile_of % gx
     ly, lx = torch.meshgrid(torch.arange(16, device=rng.device), torch.arange(16, device=rng.device), indexing="ij")
     any_tile = torch.zeros(R, dtype=torch.bool, device=rng.device)
+    blocks_exact, px_ok = [0.0], [0.0]
     strips = torch.zeros(R, 4, dtype=torch.bool, device=rng.device)
     for c0 in range(0, R, 65536):
         sl = slice(c0, min(R, c0 + 65536))
@@ -50,6 +51,9 @@ def instance_culling(geom, v, W, H, R, P):
         al = torch.clamp(o[g][:, None, None] * torch.exp(pw), max=0.99)
         ok = (pw <= 0) & (al >= 1.0 / 255.0) & (px < W) & (py < H)
         strips[sl] = ok.reshape(-1, 4, 64).any(2)
+        okb = ok.reshape(-1, 4, 4, 4, 4).permute(0, 1, 3, 2, 4).reshape(-1, 16, 16)  # [inst, block, px]
+        blocks_exact[0] += float(okb.any(2).sum())
+        px_ok[0] += float(ok.sum())
         any_tile[sl] = strips[sl].any(1)
     # strip_mask (gsr_common.h): the alpha ellipse's axis-aligned box against each strip
     det = A * C - B * B
@@ -85,6 +89,31 @@ def instance_culling(geom, v, W, H, R, P):
         hits = torch.stack(hits, 1).float()
         res[f"AABB pass, {sw}x{sh} sub-rects: px-evals/instance"] = float(hits.sum(1).mean() * sw * sh)
     res["bwd wave groups: sum max_w / sum mean_w"] = max_sum / max(mean_sum, 1)
+    # per-step cost models: lists per 4x4 block (one 16-lane row each), per 8x4 half-wave,
+    # per 8x8 wave; a wave steps max over its sub-lists, 4 entries per step, per 128-batch
+    def blocks(bw, bh):
+        out = []
+        for oy in range(0, 16, bh):
+            for ox in range(0, 16, bw):
+                out.append((x[g] + hx[g] >= x0 + ox) & (x[g] - hx[g] <= x0 + ox + bw - 1) &
+                           (y[g] + hy[g] >= y0 + oy) & (y[g] - hy[g] <= y0 + oy + bh - 1) & (255.0 * o[g] >= 0.999))
+        return torch.stack(out, 1).float()
+    def steps(bw, bh):
+        m = blocks(bw, bh)                                   # [R, nblocks] row-major over the tile
+        c = torch.zeros(T * nb, m.shape[1], device=rng.device)
+        c.index_add_(0, key, m)
+        nbx = 16 // bw
+        c = c.reshape(T * nb, 16 // bh, nbx)
+        # group sub-blocks into 8x8 waves
+        wy, wx = 8 // bh, 8 // bw
+        c = c.reshape(T * nb, 2, wy, 2, wx).permute(0, 1, 3, 2, 4).reshape(T * nb, 4, wy * wx)
+        return float(torch.ceil(c.max(2).values / 4).sum()), float(torch.ceil(c / 4).sum() / (wy * wx))
+    for bw, bh in ((8, 8), (8, 4), (4, 4)):
+        st, ideal = steps(bw, bh)
+        res[f"wave steps, lists per {bw}x{bh}: total (balanced)"] = st
+        res[f"wave steps, lists per {bw}x{bh}: balanced"] = ideal
+    res["4x4 blocks with a contributing pixel: px-evals/instance"] = 16 * blocks_exact[0] / R
+    res["contributing pixel-pairs/instance"] = px_ok[0] / R
     return {**res,
             "instances contributing (any pixel)": float(any_tile.float().mean()),
             "instances passing strip AABB": float(aabb.any(1).float().mean()),
