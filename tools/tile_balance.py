@@ -28,7 +28,9 @@ def instance_culling(geom, v, W, H, R, P):
     strip) reach alpha >= 1/255 inside power <= 0?  Same math as the render
     kernels (exp of the conic power, min(0.99, o * G))."""
     rr = geom[:16 * 4 * P].view(torch.float32).reshape(P, 16)
-    x, y, A, B, C, o = rr[:, 0], rr[:, 1], rr[:, 2], rr[:, 3], rr[:, 4], rr[:, 5]
+    # render-record form (gsr_common.h): q0 = (x, y, K_AC A, K_AC C), q1 = (K_B B, o, ...)
+    k_ac, k_b = -0.5 * 1.4426950408889634, -1.4426950408889634
+    x, y, A, C, B, o = rr[:, 0], rr[:, 1], rr[:, 2] / k_ac, rr[:, 3] / k_ac, rr[:, 4] / k_b, rr[:, 5]
     rng = v["ranges"].long()
     T = rng.shape[0]
     gx = (W + 15) // 16
