@@ -35,7 +35,11 @@
 extern "C" {
 #endif
 
-/* Scratch floats needed by gsr_track_transform_bwd / gsr_track_l1_fwd. */
+/* Scratch floats needed by gsr_track_transform_bwd(_adam) (n = P) and
+ * gsr_track_l1_fwd(_bwd) (n = H*W): per-workgroup partials followed by an
+ * arrival counter.  The scratch must be zero-filled before its first use; every
+ * call leaves it zero-filled, so one buffer serves any number of calls on one
+ * stream (not calls running concurrently). */
 int gsr_track_scratch_floats(int n);
 
 /* cam_q: the frame's unnormalised (w,x,y,z) quaternion, element k at cam_q[k * q_stride]
@@ -75,6 +79,13 @@ int gsr_track_transform_bwd_adam(int P, const float* means_world, const float* u
 int gsr_track_l1_fwd(int H, int W, const float* im, const float* depth_sil, const float* gt_im,
                      const float* gt_depth, float sil_thres, float w_im, float w_depth, float* loss, float* scratch,
                      void* stream);
+
+/* gsr_track_l1_fwd and gsr_track_l1_bwd in one pass (one launch): dL_dloss is
+ * read when the kernel runs, so the caller's loss seed must already hold its
+ * value (a static seed, e.g. the tracker's ones). */
+int gsr_track_l1_fwd_bwd(int H, int W, const float* im, const float* depth_sil, const float* gt_im,
+                         const float* gt_depth, float sil_thres, float w_im, float w_depth, const float* dL_dloss,
+                         float* loss, float* dL_dim, float* dL_ddepth_sil, float* scratch, void* stream);
 
 /* dL_dloss: 1 float (device).  Writes dL_dim [3,H,W] and dL_ddepth_sil [3,H,W]. */
 int gsr_track_l1_bwd(int H, int W, const float* im, const float* depth_sil, const float* gt_im,

@@ -73,6 +73,9 @@ SIGNATURES = {
                                  ctypes.c_float, ctypes.c_float, c_void_p, c_void_p, c_void_p]),
     "gsr_track_l1_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
                                  ctypes.c_float, ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gsr_track_l1_fwd_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
+                                     ctypes.c_float, ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_void_p]),
 }
 
 

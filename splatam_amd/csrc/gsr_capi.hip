@@ -303,11 +303,14 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
             if ((e = launch_preprocess(cam, g, geo, radii, lds_hist ? cmat : tile_count, lds_hist, ntiles, GL.nb,
                                        stream)) != hipSuccess)
                 return hip_fail(e, "preprocess");
-            if (lds_hist && (e = launch_tile_colscan(cmat, GL.nb, ntiles, tile_tot, stream)) != hipSuccess)
-                return hip_fail(e, "tile count scan");
-            if ((e = launch_scan_counts(geo, GL.nb, lds_hist ? tile_tot : tile_count, lds_hist ? 1 : TILE_CTR_STRIDE,
-                                        ntiles, ranges, capacity > 0 ? status : nullptr, stream)) != hipSuccess)
+            if (lds_hist) {  // column scan + instance / tile scans in one launch
+                if ((e = launch_tile_colscan(cmat, GL.nb, ntiles, tile_tot, geo, ranges,
+                                             capacity > 0 ? status : nullptr, stream)) != hipSuccess)
+                    return hip_fail(e, "tile count scan");
+            } else if ((e = launch_scan_counts(geo, GL.nb, tile_count, TILE_CTR_STRIDE, ntiles, ranges,
+                                               capacity > 0 ? status : nullptr, stream)) != hipSuccess) {
                 return hip_fail(e, "scan");
+            }
         }
         if (capacity <= 0) {
             if (!g_pinned.p) {

@@ -45,7 +45,8 @@ struct GeomLayout {       // per-Gaussian state ("geomBuffer")
     size_t tiles;         // u32    [P]  tiles touched
     size_t offsets;       // u32    [P]  exclusive instance offset (also in q1.w)
     size_t blocksums;     // u32    [nb] per-workgroup tile sums -> exclusive scan
-    size_t counters;      // u32    [4]  [0]=num_rendered [1]=prefiltered violation [2]=longest tile list
+    size_t counters;      // u32    [8]  [0]=num_rendered [1]=prefiltered violation [2]=longest tile list
+                          //             [3]=sort cap [4]=colscan arrival counter
     size_t total;
     int nb;
     static GeomLayout make(int P) {
@@ -58,7 +59,7 @@ struct GeomLayout {       // per-Gaussian state ("geomBuffer")
         L.tiles = o; o = align_up(o + 4 * p, 256);
         L.offsets = o; o = align_up(o + 4 * p, 256);
         L.blocksums = o; o = align_up(o + 4 * (size_t)(L.nb > 0 ? L.nb : 1), 256);
-        L.counters = o; o = align_up(o + 16, 256);
+        L.counters = o; o = align_up(o + 32, 256);
         L.total = o;
         return L;
     }
@@ -542,6 +543,69 @@ __device__ __forceinline__ void kclock_end(unsigned long long* clk) {  // every 
     }
 }
 
+// Cross-workgroup hand-off inside one launch without a release fence (an agent-
+// scope release is an L2 writeback per workgroup on this multi-XCD part): the
+// producers publish with agent-scope atomic stores (written through to the
+// coherence point), wait for them (vmcnt 0), and count themselves done with one
+// relaxed atomic; the last workgroup to arrive reads with agent-scope atomic
+// loads and resets the counter for the next launch.
+__device__ __forceinline__ void st_agent(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Same for large grids: 16 group counters (workgroup id mod 16, 64 B apart)
+// and a top counter, so no single address takes more than ~nb/16 atomics
+// (same-address atomics serialise: one counter for 1024 workgroups cost
+// ~15 us).  ctr: ARRIVE_GROUPED_WORDS words, zero before the first launch.
+constexpr int ARRIVE_STRIDE = 16;
+constexpr int ARRIVE_GROUPED_WORDS = 17 * ARRIVE_STRIDE;
+__device__ __forceinline__ bool last_block_arrive_grouped(uint32_t* ctr) {
+    __shared__ uint32_t s_last2;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t nb = gridDim.x * gridDim.y * gridDim.z;
+        const uint32_t b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, g = b & 15u;
+        const uint32_t ngroups = nb < 16u ? nb : 16u, gsize = nb / 16u + (g < nb % 16u ? 1u : 0u);
+        uint32_t* gc = ctr + ARRIVE_STRIDE * (1 + g);
+        uint32_t last = 0;
+        if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+            __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1) {
+                __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = 1;
+            }
+        }
+        s_last2 = last;
+    }
+    __syncthreads();
+    return s_last2 != 0u;
+}
+
+// Every thread of the workgroup calls this after its st_agent stores; true in
+// the last workgroup of the grid to arrive (then *counter is back to 0).
+__device__ __forceinline__ bool last_block_arrive(uint32_t* counter) {
+    __shared__ uint32_t s_last;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0): this thread's stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t nb = gridDim.x * gridDim.y * gridDim.z;
+        const uint32_t old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == nb - 1 ? 1u : 0u;
+        if (old == nb - 1) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return s_last != 0u;
+}
+
 // --------------------------------------------------------- wave64 helpers --
 template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float v) {
@@ -745,7 +809,8 @@ __device__ __forceinline__ uint32_t instance_slot(uint2 rect, uint32_t off, uint
 // ------------------------------------------------------- kernel launchers --
 hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* counts,
                              bool lds_hist, int ntiles, int nb, hipStream_t s);
-hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, hipStream_t s);
+hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, GeomPtrs geo, uint2* ranges,
+                               uint32_t* status, hipStream_t s);
 hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hipStream_t s);
 hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
                               uint2* ranges, uint32_t* status, hipStream_t s);

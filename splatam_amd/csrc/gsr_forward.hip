@@ -32,6 +32,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
         __syncthreads();
     }
     const int i = blockIdx.x * PRE_BLOCK + threadIdx.x;
+    if (i == 0) geo.counters[4] = 0u;  // tile_colscan_kernel's arrival counter (next launch)
     uint32_t tiles = 0;
     bool violation = false;  // prefiltered set but the point is culled (auxiliary.h:154-160)
     float4 q1;
@@ -138,8 +139,20 @@ hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, 
 // One workgroup per 64 tiles, 16 row segments each (coalesced across tiles).
 constexpr int CS_TILES = 64, CS_PARTS = 16;
 
+template <bool AGENT_TILES>
+__device__ void scan_counts_body(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t* __restrict__ tile_count,
+                                 uint32_t tile_stride, uint32_t ntiles, uint2* __restrict__ ranges,
+                                 uint32_t* __restrict__ counters, uint32_t sort_cap, uint32_t* __restrict__ status);
+constexpr int SCAN_THREADS = 1024;
+constexpr int SCAN_ITEMS = 4;
+
+// ... and, in the same launch, the scan of scan_counts_kernel: the workgroups
+// publish their tile totals (agent-scope stores), the last one to finish scans
+// the workgroup sums and the tile totals (one launch instead of two; the arrival
+// counter is GeomLayout counters[4], zeroed by preprocess).
 __global__ void __launch_bounds__(CS_TILES * CS_PARTS)
-tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t* __restrict__ tot) {
+tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t* __restrict__ tot, GeomPtrs geo,
+                    uint2* __restrict__ ranges, uint32_t sort_cap, uint32_t* __restrict__ status) {
     __shared__ uint32_t s_part[CS_PARTS][CS_TILES];
     const int tl = threadIdx.x % CS_TILES, q = threadIdx.x / CS_TILES;
     const int t = blockIdx.x * CS_TILES + tl;
@@ -160,23 +173,24 @@ tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t*
             counts[(size_t)b * ntiles + t] = run;
             run += v;
         }
-        if (q == CS_PARTS - 1) tot[t] = run;
+        if (q == CS_PARTS - 1) st_agent(&tot[t], run);
     }
+    if (!last_block_arrive(&geo.counters[4])) return;
+    scan_counts_body<true>(geo.blocksums, (uint32_t)nb, tot, 1u, (uint32_t)ntiles, ranges, geo.counters, sort_cap,
+                           status);
 }
 
-hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, hipStream_t s) {
+hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, GeomPtrs geo, uint2* ranges,
+                               uint32_t* status, hipStream_t s) {
+    static_assert(CS_TILES * CS_PARTS == SCAN_THREADS, "the last colscan workgroup runs the scan body");
     hipLaunchKernelGGL(tile_colscan_kernel, dim3((ntiles + CS_TILES - 1) / CS_TILES), dim3(CS_TILES * CS_PARTS), 0, s,
-                       counts, nb, ntiles, tot);
+                       counts, nb, ntiles, tot, geo, ranges, (uint32_t)TILE_SORT_CAP, status);
     return hipGetLastError();
 }
 
 // -------------------------------------------------------- exclusive scan --
 // One 1024-lane workgroup scans `n` u32 in place (exclusive) and writes the
 // grand total.  Used for the per-workgroup tile sums and radix histograms.
-constexpr int SCAN_THREADS = 1024;
-constexpr int SCAN_ITEMS = 4;
-
-
 __global__ void __launch_bounds__(SCAN_THREADS) exclusive_scan_kernel(uint32_t* data, uint32_t n, uint32_t* total) {
     __shared__ uint32_t wsums[SCAN_THREADS / 64];
     __shared__ uint32_t s_carry;
@@ -223,10 +237,12 @@ hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hi
 // offsets, total = num_rendered) and of the per-tile instance counts, which
 // directly gives every tile's [start, end) in the tile-major sorted list
 // (identifyTileRanges, rasterizer_impl.cu:116-138, without reading keys).
-__global__ void __launch_bounds__(SCAN_THREADS)
-scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t* __restrict__ tile_count,
-                   uint32_t tile_stride, uint32_t ntiles, uint2* __restrict__ ranges,
-                   uint32_t* __restrict__ counters, uint32_t sort_cap, uint32_t* __restrict__ status) {
+// AGENT_TILES: the tile counts were published by other workgroups of the same
+// launch (tile_colscan_kernel's last workgroup) and are read with agent-scope loads.
+template <bool AGENT_TILES>
+__device__ void scan_counts_body(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t* __restrict__ tile_count,
+                                 uint32_t tile_stride, uint32_t ntiles, uint2* __restrict__ ranges,
+                                 uint32_t* __restrict__ counters, uint32_t sort_cap, uint32_t* __restrict__ status) {
     // Writes all four counters (no reset needed): [0] num_rendered, [1] prefiltered violation
     // (top bits of the workgroup sums), [2] longest tile list, [3] sort_cap; and a copy to
     // `status` (static mode).
@@ -245,7 +261,8 @@ scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t
             const uint32_t i0 = base + (uint32_t)tid * SCAN_ITEMS;
 #pragma unroll
             for (int k = 0; k < SCAN_ITEMS; k++) {
-                x[k] = (i0 + k < n) ? src[(size_t)(i0 + k) * (pass == 0 ? 1u : tile_stride)] : 0u;
+                const uint32_t* ps = src + (size_t)(i0 + k) * (pass == 0 ? 1u : tile_stride);
+                x[k] = (i0 + k < n) ? ((AGENT_TILES && pass == 1) ? ld_agent(ps) : *ps) : 0u;
                 if (pass == 0) {  // workgroup sums carry the prefiltered-violation flag in bit 31
                     viol |= x[k] >> 31;
                     x[k] &= 0x7fffffffu;
@@ -291,6 +308,13 @@ scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t
         }
         __syncthreads();
     }
+}
+
+__global__ void __launch_bounds__(SCAN_THREADS)
+scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t* __restrict__ tile_count,
+                   uint32_t tile_stride, uint32_t ntiles, uint2* __restrict__ ranges,
+                   uint32_t* __restrict__ counters, uint32_t sort_cap, uint32_t* __restrict__ status) {
+    scan_counts_body<false>(blocksums, nb, tile_count, tile_stride, ntiles, ranges, counters, sort_cap, status);
 }
 
 hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
@@ -431,6 +455,8 @@ constexpr int TILE_SORT_THREADS = 256;
 // wave (j < 64 E): lane shuffle (lane ^ j/E, same slot); otherwise through LDS.
 // For n = 1024 only 3 of the 55 stages need barriers (the LDS version had 55).
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    // ds_bpermute: a DPP / permlane-swap version (VALU data movement, runtime switch
+    // on m) made the sort 2.5x slower
     const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
     return ((uint64_t)hi << 32) | lo;
@@ -489,8 +515,8 @@ __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, u
     }
     (void)lane;
 #pragma unroll
-    for (int e = 0; e < E; e++)
-        if (base + e < cnt) dst[base + e] = (uint32_t)v[e];
+    for (int e = 0; e < E; e++)  // (a padding key can only land here through a network bug: emit id 0, never
+        if (base + e < cnt) dst[base + e] = v[e] == ~0ull ? 0u : (uint32_t)v[e];  // an out-of-range id)
 }
 
 __global__ void __launch_bounds__(TILE_SORT_THREADS)

@@ -8,16 +8,17 @@
 //                         (slam_helpers.py:124-139) and the [z, 1, z^2] depth
 //                         colours (slam_helpers.py:196-213) in one pass: 44 B in,
 //                         64 B out per Gaussian (HBM-bound).
-//   track_transform_part  one lane per Gaussian, grid-stride: the 16 pose
+//   track_transform_bwd   one lane per Gaussian, grid-stride: the 16 pose
 //                         partial sums (sum g, sum g p^T, sum dquat_mult^T dr)
 //                         -> per-workgroup partials (transposed wave reduction +
-//                         LDS), fixed order;
-//   track_transform_fin   one workgroup: sums the partials in a fixed order and
-//                         applies the pose chain (R(n) -> n = c/|c| -> c =
-//                         q/max(|q|, 1e-12)).  Bitwise reproducible.
-//   track_l1_part / fin   masked L1 tracking loss (splatam.py:262-296),
-//                         two-level fixed-order sum;
-//   track_l1_bwd          its gradient w.r.t. both renders, one lane per pixel.
+//                         LDS); the last workgroup to finish sums them in a
+//                         fixed order and applies the pose chain (R(n) -> n =
+//                         c/|c| -> c = q/max(|q|, 1e-12)) and optionally Adam.
+//                         One launch, bitwise reproducible.
+//   track_l1              masked L1 tracking loss (splatam.py:262-296), same
+//                         one-launch fixed-order sum; optionally its gradient
+//                         w.r.t. both renders in the same pass;
+//   track_l1_bwd          the gradient alone (any dL/dloss), one lane per pixel.
 #include <math.h>
 
 #include <algorithm>
@@ -125,12 +126,68 @@ __device__ __forceinline__ void block_sum(const float (&v)[N], float* s_red /*4*
                                             (s_red[2 * N + threadIdx.x] + s_red[3 * N + threadIdx.x]);
 }
 
+struct PoseAdam {  // torch.optim.Adam (no weight decay, no amsgrad) on the frame's pose column
+    float lr_q, lr_t, beta1, beta2, eps;
+    float* state;     // device: m_q[4], v_q[4], m_t[3], v_t[3], step
+    float* q;         // the frame's quaternion column (stride qs), updated in place
+    float* t;         // the frame's translation column (stride qs)
+};
+
+// exp_avg = b1 m + (1-b1) g; exp_avg_sq = b2 v + (1-b2) g^2;
+// p -= lr / (1 - b1^s) * m / (sqrt(v) / sqrt(1 - b2^s) + eps)
+__device__ __forceinline__ void adam_update(float& p, float g, float& m, float& v, float lr, const PoseAdam& a,
+                                            float bc1, float bc2_sqrt) {
+    m = a.beta1 * m + (1.f - a.beta1) * g;
+    v = a.beta2 * v + (1.f - a.beta2) * g * g;
+    const float denom = sqrtf(v) / bc2_sqrt + a.eps;
+    p -= (lr / bc1) * (m / denom);
+}
+
+// The pose chain on the 16 summed terms S: dR -> dn (build_rotation) -> dc
+// (its own normalisation) -> dq (F.normalize), dt = S[0..2]; then either the
+// gradient is written (dq, dt) or the Adam step is applied in place.
+__device__ void pose_fin(const float* S, const float* cq, int qs, float* dq, float* dt, const PoseAdam& adam) {
+    const Pose ps = make_pose(cq, nullptr, qs);
+    // dR[j][k] = S[3 + 3j + k]; R = build_rotation(n), n = (r, x, y, z)
+    const float r = ps.n[0], x = ps.n[1], y = ps.n[2], z = ps.n[3];
+    const float d00 = S[3], d01 = S[4], d02 = S[5], d10 = S[6], d11 = S[7], d12 = S[8], d20 = S[9], d21 = S[10],
+                d22 = S[11];
+    const float4 dn = make_float4(
+        2.f * (-z * d01 + y * d02 + z * d10 - x * d12 - y * d20 + x * d21),
+        2.f * (y * d01 + z * d02 + y * d10 - 2.f * x * d11 - r * d12 + z * d20 + r * d21 - 2.f * x * d22),
+        2.f * (-2.f * y * d00 + x * d01 + r * d02 + x * d10 + z * d12 - r * d20 + z * d21 - 2.f * y * d22),
+        2.f * (-2.f * z * d00 - r * d01 + x * d02 + r * d10 - 2.f * z * d11 + y * d12 + x * d20 + y * d21));
+    // n = c / |c| (build_rotation, no eps), then c = q / max(|q|, eps) (F.normalize)
+    float4 dc = normalize4_bwd(make_float4(ps.n[0], ps.n[1], ps.n[2], ps.n[3]), ps.cn, dn);
+    dc.x += S[12]; dc.y += S[13]; dc.z += S[14]; dc.w += S[15];
+    const float4 g = normalize4_bwd(make_float4(ps.c[0], ps.c[1], ps.c[2], ps.c[3]), ps.qn, dc);
+    if (adam.state) {  // optimizer step fused here: the pose gradient never leaves the kernel
+        float* st = adam.state;
+        const float step = st[14] + 1.f;
+        st[14] = step;
+        const float bc1 = 1.f - powf(adam.beta1, step), bc2_sqrt = sqrtf(1.f - powf(adam.beta2, step));
+        const float gq[4] = {g.x, g.y, g.z, g.w};
+        for (int k = 0; k < 4; k++) adam_update(adam.q[k * qs], gq[k], st[k], st[4 + k], adam.lr_q, adam, bc1, bc2_sqrt);
+        for (int k = 0; k < 3; k++) adam_update(adam.t[k * qs], S[k], st[8 + k], st[11 + k], adam.lr_t, adam, bc1, bc2_sqrt);
+        return;
+    }
+    dq[0] = g.x; dq[qs] = g.y; dq[2 * qs] = g.z; dq[3 * qs] = g.w;
+    dt[0] = S[0]; dt[qs] = S[1]; dt[2 * qs] = S[2];
+}
+
+// Pose gradient in one launch: every workgroup publishes its partial of the 16
+// sums (sum g, sum g p^T, sum dquat_mult^T dr); the last one to arrive adds the
+// partials in a fixed order (bitwise reproducible) and runs pose_fin.
+// scratch: 16 * gridDim.x partials, then the arrival counters (zero before the
+// first launch; every launch leaves them zero).
 __global__ void __launch_bounds__(GLUE_BLOCK)
-track_transform_part_kernel(int P, const float* __restrict__ mw, const float* __restrict__ ur, int scols,
-                            const float* __restrict__ cq, int qs, const float* __restrict__ mc,
-                            const float* __restrict__ w2c, const float* __restrict__ gm,
-                            const float* __restrict__ gr, const float* __restrict__ gd, float* __restrict__ part) {
+track_transform_bwd_kernel(int P, const float* __restrict__ mw, const float* __restrict__ ur, int scols,
+                           const float* __restrict__ cq, int qs, const float* __restrict__ mc,
+                           const float* __restrict__ w2c, const float* __restrict__ gm,
+                           const float* __restrict__ gr, const float* __restrict__ gd, float* __restrict__ part,
+                           float* dq, float* dt, PoseAdam adam) {
     __shared__ float s_red[4 * POSE_PARTS];
+    __shared__ float s_tot[POSE_PARTS];
     float v[POSE_PARTS];
 #pragma unroll
     for (int k = 0; k < POSE_PARTS; k++) v[k] = 0.f;
@@ -165,67 +222,21 @@ track_transform_part_kernel(int P, const float* __restrict__ mw, const float* __
             v[15] += -d.x * u.w - d.y * u.z + d.z * u.y + d.w * u.x;
         }
     }
-    block_sum<POSE_PARTS>(v, s_red, part + POSE_PARTS * blockIdx.x);
-}
-
-struct PoseAdam {  // torch.optim.Adam (no weight decay, no amsgrad) on the frame's pose column
-    float lr_q, lr_t, beta1, beta2, eps;
-    float* state;     // device: m_q[4], v_q[4], m_t[3], v_t[3], step
-    float* q;         // the frame's quaternion column (stride qs), updated in place
-    float* t;         // the frame's translation column (stride qs)
-};
-
-// exp_avg = b1 m + (1-b1) g; exp_avg_sq = b2 v + (1-b2) g^2;
-// p -= lr / (1 - b1^s) * m / (sqrt(v) / sqrt(1 - b2^s) + eps)
-__device__ __forceinline__ void adam_update(float& p, float g, float& m, float& v, float lr, const PoseAdam& a,
-                                            float bc1, float bc2_sqrt) {
-    m = a.beta1 * m + (1.f - a.beta1) * g;
-    v = a.beta2 * v + (1.f - a.beta2) * g * g;
-    const float denom = sqrtf(v) / bc2_sqrt + a.eps;
-    p -= (lr / bc1) * (m / denom);
-}
-
-__global__ void __launch_bounds__(GLUE_BLOCK)
-track_transform_fin_kernel(int nblocks, const float* __restrict__ part, const float* __restrict__ cq, int qs,
-                           float* __restrict__ dq, float* __restrict__ dt, PoseAdam adam) {
-    __shared__ float s_red[4 * POSE_PARTS];
-    __shared__ float s_tot[POSE_PARTS];
-    float v[POSE_PARTS];
-#pragma unroll
-    for (int k = 0; k < POSE_PARTS; k++) v[k] = 0.f;
-    for (int b = threadIdx.x; b < nblocks; b += GLUE_BLOCK)
-#pragma unroll
-        for (int k = 0; k < POSE_PARTS; k++) v[k] += part[POSE_PARTS * b + k];
     block_sum<POSE_PARTS>(v, s_red, s_tot);
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    const Pose ps = make_pose(cq, nullptr, qs);
-    const float* S = s_tot;
-    // dR[j][k] = S[3 + 3j + k]; R = build_rotation(n), n = (r, x, y, z)
-    const float r = ps.n[0], x = ps.n[1], y = ps.n[2], z = ps.n[3];
-    const float d00 = S[3], d01 = S[4], d02 = S[5], d10 = S[6], d11 = S[7], d12 = S[8], d20 = S[9], d21 = S[10],
-                d22 = S[11];
-    const float4 dn = make_float4(
-        2.f * (-z * d01 + y * d02 + z * d10 - x * d12 - y * d20 + x * d21),
-        2.f * (y * d01 + z * d02 + y * d10 - 2.f * x * d11 - r * d12 + z * d20 + r * d21 - 2.f * x * d22),
-        2.f * (-2.f * y * d00 + x * d01 + r * d02 + x * d10 + z * d12 - r * d20 + z * d21 - 2.f * y * d22),
-        2.f * (-2.f * z * d00 - r * d01 + x * d02 + r * d10 - 2.f * z * d11 + y * d12 + x * d20 + y * d21));
-    // n = c / |c| (build_rotation, no eps), then c = q / max(|q|, eps) (F.normalize)
-    float4 dc = normalize4_bwd(make_float4(ps.n[0], ps.n[1], ps.n[2], ps.n[3]), ps.cn, dn);
-    dc.x += S[12]; dc.y += S[13]; dc.z += S[14]; dc.w += S[15];
-    const float4 g = normalize4_bwd(make_float4(ps.c[0], ps.c[1], ps.c[2], ps.c[3]), ps.qn, dc);
-    if (adam.state) {  // optimizer step fused here: the pose gradient never leaves the kernel
-        float* st = adam.state;
-        const float step = st[14] + 1.f;
-        st[14] = step;
-        const float bc1 = 1.f - powf(adam.beta1, step), bc2_sqrt = sqrtf(1.f - powf(adam.beta2, step));
-        const float gq[4] = {g.x, g.y, g.z, g.w};
-        for (int k = 0; k < 4; k++) adam_update(adam.q[k * qs], gq[k], st[k], st[4 + k], adam.lr_q, adam, bc1, bc2_sqrt);
-        for (int k = 0; k < 3; k++) adam_update(adam.t[k * qs], S[k], st[8 + k], st[11 + k], adam.lr_t, adam, bc1, bc2_sqrt);
-        return;
-    }
-    dq[0] = g.x; dq[qs] = g.y; dq[2 * qs] = g.z; dq[3 * qs] = g.w;
-    dt[0] = S[0]; dt[qs] = S[1]; dt[2 * qs] = S[2];
+    if (threadIdx.x < POSE_PARTS) st_agent(part + POSE_PARTS * blockIdx.x + threadIdx.x, s_tot[threadIdx.x]);
+    const int nb = gridDim.x;
+    if (!last_block_arrive_grouped(reinterpret_cast<uint32_t*>(part + POSE_PARTS * nb))) return;
+    // last workgroup: fixed-order sum of the partials
+#pragma unroll
+    for (int k = 0; k < POSE_PARTS; k++) v[k] = 0.f;
+    for (int b = threadIdx.x; b < nb; b += GLUE_BLOCK)
+#pragma unroll
+        for (int k = 0; k < POSE_PARTS; k++) v[k] += ld_agent(part + POSE_PARTS * b + k);
+    __syncthreads();
+    block_sum<POSE_PARTS>(v, s_red, s_tot);
+    __syncthreads();
+    if (threadIdx.x == 0) pose_fin(s_tot, cq, qs, dq, dt, adam);
 }
 
 // --------------------------------------------------------------- L1 loss --
@@ -235,35 +246,53 @@ __device__ __forceinline__ bool track_mask(int pid, int HW, const float* ds, con
     return gt_depth[pid] > 0.f && !isnan(d) && !isnan(unc) && sil > thres;
 }
 
-__global__ void __launch_bounds__(GLUE_BLOCK)
-track_l1_part_kernel(int HW, const float* __restrict__ im, const float* __restrict__ ds,
-                     const float* __restrict__ gt_im, const float* __restrict__ gt_d, float thres,
-                     float* __restrict__ part) {
-    __shared__ float s_red[4 * 4];
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int p = blockIdx.x * GLUE_BLOCK + threadIdx.x; p < HW; p += gridDim.x * GLUE_BLOCK) {
-        if (!track_mask(p, HW, ds, gt_d, thres)) continue;
-        v[0] += fabsf(gt_im[p] - im[p]) + fabsf(gt_im[HW + p] - im[HW + p]) + fabsf(gt_im[2 * HW + p] - im[2 * HW + p]);
-        v[1] += fabsf(gt_d[p] - ds[p]);
-    }
-    block_sum<4>(v, s_red, part + 4 * blockIdx.x);
-}
+__device__ __forceinline__ float neg_sgn(float x) { return x > 0.f ? -1.f : (x < 0.f ? 1.f : 0.f); }
 
+// Masked L1 loss in one launch: per-workgroup partial sums published, the last
+// workgroup adds them in a fixed order and writes the loss.  With dloss, the
+// gradient images are written in the same pass (g = *dloss, read now: the
+// caller's loss seed must already hold its value).  scratch: 4 * gridDim.x
+// partials, then the arrival counter (zero before the first launch; left zero).
 __global__ void __launch_bounds__(GLUE_BLOCK)
-track_l1_fin_kernel(int nblocks, const float* __restrict__ part, float w_im, float w_depth, float* __restrict__ loss) {
+track_l1_kernel(int HW, const float* __restrict__ im, const float* __restrict__ ds,
+                const float* __restrict__ gt_im, const float* __restrict__ gt_d, float thres, float w_im,
+                float w_depth, float* __restrict__ part, float* __restrict__ loss, const float* __restrict__ dloss,
+                float* __restrict__ dim, float* __restrict__ dds) {
     __shared__ float s_red[4 * 4];
     __shared__ float s_tot[4];
+    const float g = dloss ? dloss[0] : 0.f;
     float v[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int b = threadIdx.x; b < nblocks; b += GLUE_BLOCK) {
-        v[0] += part[4 * b];
-        v[1] += part[4 * b + 1];
+    for (int p = blockIdx.x * GLUE_BLOCK + threadIdx.x; p < HW; p += gridDim.x * GLUE_BLOCK) {
+        const bool m = track_mask(p, HW, ds, gt_d, thres);
+        if (m) {
+            v[0] += fabsf(gt_im[p] - im[p]) + fabsf(gt_im[HW + p] - im[HW + p]) +
+                    fabsf(gt_im[2 * HW + p] - im[2 * HW + p]);
+            v[1] += fabsf(gt_d[p] - ds[p]);
+        }
+        if (dloss) {  // d|gt - x|/dx = -sgn(gt - x) (torch.abs backward: sgn, 0 at 0)
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                dim[c * HW + p] = m ? (g * w_im) * neg_sgn(gt_im[c * HW + p] - im[c * HW + p]) : 0.f;
+            dds[p] = m ? (g * w_depth) * neg_sgn(gt_d[p] - ds[p]) : 0.f;
+            dds[HW + p] = 0.f;
+            dds[2 * HW + p] = 0.f;
+        }
     }
+    block_sum<4>(v, s_red, s_tot);
+    __syncthreads();
+    if (threadIdx.x < 2) st_agent(part + 4 * blockIdx.x + threadIdx.x, s_tot[threadIdx.x]);
+    const int nb = gridDim.x;
+    if (!last_block_arrive_grouped(reinterpret_cast<uint32_t*>(part + 4 * nb))) return;
+    v[0] = v[1] = v[2] = v[3] = 0.f;
+    for (int b = threadIdx.x; b < nb; b += GLUE_BLOCK) {
+        v[0] += ld_agent(part + 4 * b);
+        v[1] += ld_agent(part + 4 * b + 1);
+    }
+    __syncthreads();
     block_sum<4>(v, s_red, s_tot);
     __syncthreads();
     if (threadIdx.x == 0) loss[0] = w_im * s_tot[0] + w_depth * s_tot[1];
 }
-
-__device__ __forceinline__ float neg_sgn(float x) { return x > 0.f ? -1.f : (x < 0.f ? 1.f : 0.f); }
 
 __global__ void __launch_bounds__(GLUE_BLOCK)
 track_l1_bwd_kernel(int HW, const float* __restrict__ im, const float* __restrict__ ds,
@@ -282,6 +311,9 @@ track_l1_bwd_kernel(int HW, const float* __restrict__ im, const float* __restric
 }
 
 int blocks_for(int n) { return n <= 0 ? 1 : std::min(GLUE_MAX_BLOCKS, (n + GLUE_BLOCK - 1) / GLUE_BLOCK); }
+// the pose reduction's last workgroup reads 16 partials per workgroup: fewer, fuller workgroups
+constexpr int POSE_MAX_BLOCKS = 256;
+int pose_blocks(int n) { return n <= 0 ? 1 : std::min(POSE_MAX_BLOCKS, (n + GLUE_BLOCK - 1) / GLUE_BLOCK); }
 
 }  // namespace
 }  // namespace gsr
@@ -290,7 +322,8 @@ using namespace gsr;
 
 extern "C" {
 
-int gsr_track_scratch_floats(int n) { return POSE_PARTS * blocks_for(n); }
+// partials of the widest reduction + the arrival counters (the L1 needs 4 per workgroup)
+int gsr_track_scratch_floats(int n) { return POSE_PARTS * blocks_for(n) + ARRIVE_GROUPED_WORDS; }
 
 int gsr_track_transform_fwd(int P, const float* means_world, const float* unnorm_rot, const float* logit_opac,
                             const float* log_scales, int scale_cols, const float* cam_q, const float* cam_t,
@@ -318,12 +351,10 @@ int gsr_track_transform_bwd(int P, const float* means_world, const float* unnorm
     if (!cam_q || !dL_dcam_q || !dL_dcam_t || !scratch || !w2c || (P > 0 && (!means_world || !means_cam ||
                                                                         !dL_dmeans_cam || !unnorm_rot)))
         return fail(GSR_ERR_INVALID_ARG, "track_transform_bwd: null pointer");
-    hipStream_t s = (hipStream_t)stream;
-    const int nb = blocks_for(P);
-    hipLaunchKernelGGL(track_transform_part_kernel, dim3(nb), dim3(GLUE_BLOCK), 0, s, P, means_world, unnorm_rot,
-                       scale_cols, cam_q, q_stride, means_cam, w2c, dL_dmeans_cam, dL_drot, dL_ddepth_colors, scratch);
-    hipLaunchKernelGGL(track_transform_fin_kernel, dim3(1), dim3(GLUE_BLOCK), 0, s, nb, scratch, cam_q, q_stride,
-                       dL_dcam_q, dL_dcam_t, PoseAdam{0.f, 0.f, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr});
+    hipLaunchKernelGGL(track_transform_bwd_kernel, dim3(pose_blocks(P)), dim3(GLUE_BLOCK), 0, (hipStream_t)stream, P,
+                       means_world, unnorm_rot, scale_cols, cam_q, q_stride, means_cam, w2c, dL_dmeans_cam, dL_drot,
+                       dL_ddepth_colors, scratch, dL_dcam_q, dL_dcam_t,
+                       PoseAdam{0.f, 0.f, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr});
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GSR_OK : hip_fail(e, "track_transform_bwd");
 }
@@ -338,12 +369,10 @@ int gsr_track_transform_bwd_adam(int P, const float* means_world, const float* u
     if (!cam_q || !cam_t || !adam_state || !scratch || !w2c ||
         (P > 0 && (!means_world || !means_cam || !dL_dmeans_cam || !unnorm_rot)))
         return fail(GSR_ERR_INVALID_ARG, "track_transform_bwd_adam: null pointer");
-    hipStream_t s = (hipStream_t)stream;
-    const int nb = blocks_for(P);
-    hipLaunchKernelGGL(track_transform_part_kernel, dim3(nb), dim3(GLUE_BLOCK), 0, s, P, means_world, unnorm_rot,
-                       scale_cols, cam_q, q_stride, means_cam, w2c, dL_dmeans_cam, dL_drot, dL_ddepth_colors, scratch);
-    hipLaunchKernelGGL(track_transform_fin_kernel, dim3(1), dim3(GLUE_BLOCK), 0, s, nb, scratch, cam_q, q_stride,
-                       nullptr, nullptr, PoseAdam{lr_q, lr_t, beta1, beta2, eps, adam_state, cam_q, cam_t});
+    hipLaunchKernelGGL(track_transform_bwd_kernel, dim3(pose_blocks(P)), dim3(GLUE_BLOCK), 0, (hipStream_t)stream, P,
+                       means_world, unnorm_rot, scale_cols, cam_q, q_stride, means_cam, w2c, dL_dmeans_cam, dL_drot,
+                       dL_ddepth_colors, scratch, nullptr, nullptr,
+                       PoseAdam{lr_q, lr_t, beta1, beta2, eps, adam_state, cam_q, cam_t});
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GSR_OK : hip_fail(e, "track_transform_bwd_adam");
 }
@@ -354,13 +383,25 @@ int gsr_track_l1_fwd(int H, int W, const float* im, const float* depth_sil, cons
     if (H <= 0 || W <= 0) return fail(GSR_ERR_INVALID_ARG, "track_l1_fwd: bad image size");
     if (!im || !depth_sil || !gt_im || !gt_depth || !loss || !scratch)
         return fail(GSR_ERR_INVALID_ARG, "track_l1_fwd: null pointer");
-    hipStream_t s = (hipStream_t)stream;
-    const int HW = H * W, nb = blocks_for(HW);
-    hipLaunchKernelGGL(track_l1_part_kernel, dim3(nb), dim3(GLUE_BLOCK), 0, s, HW, im, depth_sil, gt_im, gt_depth,
-                       sil_thres, scratch);
-    hipLaunchKernelGGL(track_l1_fin_kernel, dim3(1), dim3(GLUE_BLOCK), 0, s, nb, scratch, w_im, w_depth, loss);
+    const int HW = H * W;
+    hipLaunchKernelGGL(track_l1_kernel, dim3(blocks_for(HW)), dim3(GLUE_BLOCK), 0, (hipStream_t)stream, HW, im,
+                       depth_sil, gt_im, gt_depth, sil_thres, w_im, w_depth, scratch, loss, nullptr, nullptr, nullptr);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GSR_OK : hip_fail(e, "track_l1_fwd");
+}
+
+int gsr_track_l1_fwd_bwd(int H, int W, const float* im, const float* depth_sil, const float* gt_im,
+                         const float* gt_depth, float sil_thres, float w_im, float w_depth, const float* dL_dloss,
+                         float* loss, float* dL_dim, float* dL_ddepth_sil, float* scratch, void* stream) {
+    if (H <= 0 || W <= 0) return fail(GSR_ERR_INVALID_ARG, "track_l1_fwd_bwd: bad image size");
+    if (!im || !depth_sil || !gt_im || !gt_depth || !loss || !scratch || !dL_dloss || !dL_dim || !dL_ddepth_sil)
+        return fail(GSR_ERR_INVALID_ARG, "track_l1_fwd_bwd: null pointer");
+    const int HW = H * W;
+    hipLaunchKernelGGL(track_l1_kernel, dim3(blocks_for(HW)), dim3(GLUE_BLOCK), 0, (hipStream_t)stream, HW, im,
+                       depth_sil, gt_im, gt_depth, sil_thres, w_im, w_depth, scratch, loss, dL_dloss, dL_dim,
+                       dL_ddepth_sil);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? GSR_OK : hip_fail(e, "track_l1_fwd_bwd");
 }
 
 int gsr_track_l1_bwd(int H, int W, const float* im, const float* depth_sil, const float* gt_im,

@@ -49,6 +49,22 @@ class PoseAdam:
         self.state.zero_()
 
 
+_SCRATCH: dict = {}
+
+
+def _scratch(t: torch.Tensor, n: int) -> torch.Tensor:
+    """Zero-filled scratch for the glue reductions (gsr_track_scratch_floats): the kernels
+    leave it zero-filled, so one persistent buffer per (device, stream, size) serves every
+    call issued on that stream (calls on one stream never overlap)."""
+    dev = t.device
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream, int(n))
+    buf = _SCRATCH.get(key)
+    if buf is None:
+        buf = torch.zeros(int(n), dtype=torch.float32, device=dev)
+        _SCRATCH[key] = buf
+    return buf
+
+
 class _TrackTransform(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cam_rots, cam_trans, means_world, unnorm_rot, logit_opac, log_scales, w2c, time_idx,
@@ -102,7 +118,7 @@ class _TrackTransform(torch.autograd.Function):
         g_dcol = g_dcol.contiguous() if g_dcol is not None else None
         opt = ctx.pose_adam
         if opt is not None:  # optimizer step fused into the backward: the pose is updated in place
-            scratch = torch.empty(lib.gsr_track_scratch_floats(P), dtype=torch.float32, device=means_world.device)
+            scratch = _scratch(means_world, lib.gsr_track_scratch_floats(P))
             rc = lib.gsr_track_transform_bwd_adam(
                 P, means_world.data_ptr(), unnorm_rot.data_ptr(), scols, cam_rots.data_ptr() + 4 * t,
                 cam_trans.data_ptr() + 4 * t, T, means_cam.data_ptr(), w2c.data_ptr(), g_means.data_ptr(),
@@ -113,7 +129,7 @@ class _TrackTransform(torch.autograd.Function):
             return none
         dq = torch.zeros_like(cam_rots)
         dt = torch.zeros_like(cam_trans)
-        scratch = torch.empty(lib.gsr_track_scratch_floats(P), dtype=torch.float32, device=means_world.device)
+        scratch = _scratch(means_world, lib.gsr_track_scratch_floats(P))
         rc = lib.gsr_track_transform_bwd(P, means_world.data_ptr(), unnorm_rot.data_ptr(), scols,
                                          cam_rots.data_ptr() + 4 * t, means_cam.data_ptr(), w2c.data_ptr(),
                                          g_means.data_ptr(), g_rot.data_ptr() if g_rot is not None else None,
@@ -136,24 +152,37 @@ def track_transform(params: dict, time_idx: int, w2c: torch.Tensor, pose_adam: P
 
 class _TrackingL1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, im, depth_sil, gt_im, gt_depth, sil_thres, w_im, w_depth):
+    def forward(ctx, im, depth_sil, gt_im, gt_depth, sil_thres, w_im, w_depth, seed=None):
         im, depth_sil = _f32c(im, "im"), _f32c(depth_sil, "depth_sil")
         gt_im, gt_depth = _f32c(gt_im, "gt_im"), _f32c(gt_depth, "gt_depth")
         _, H, W = im.shape
         if depth_sil.shape != (3, H, W) or gt_im.shape != (3, H, W) or gt_depth.shape != (1, H, W):
             raise RuntimeError("tracking_l1: expected im/depth_sil/gt_im [3,H,W] and gt_depth [1,H,W]")
         loss = torch.empty((), dtype=torch.float32, device=im.device)
-        scratch = torch.empty(lib.gsr_track_scratch_floats(H * W), dtype=torch.float32, device=im.device)
-        rc = lib.gsr_track_l1_fwd(H, W, im.data_ptr(), depth_sil.data_ptr(), gt_im.data_ptr(), gt_depth.data_ptr(),
-                                  float(sil_thres), float(w_im), float(w_depth), loss.data_ptr(), scratch.data_ptr(),
-                                  _stream(im))
-        _check(rc, "track_l1_fwd")
+        scratch = _scratch(im, lib.gsr_track_scratch_floats(H * W))
+        ctx.pre = None
+        if seed is not None:  # the caller's static loss seed: gradient images in the same pass
+            seed = _f32c(seed, "seed")
+            dim, dds = torch.empty_like(im), torch.empty_like(depth_sil)
+            rc = lib.gsr_track_l1_fwd_bwd(H, W, im.data_ptr(), depth_sil.data_ptr(), gt_im.data_ptr(),
+                                          gt_depth.data_ptr(), float(sil_thres), float(w_im), float(w_depth),
+                                          seed.data_ptr(), loss.data_ptr(), dim.data_ptr(), dds.data_ptr(),
+                                          scratch.data_ptr(), _stream(im))
+            _check(rc, "track_l1_fwd_bwd")
+            ctx.pre = (dim, dds, seed)  # the seed stays referenced: its address cannot be reused
+        else:
+            rc = lib.gsr_track_l1_fwd(H, W, im.data_ptr(), depth_sil.data_ptr(), gt_im.data_ptr(),
+                                      gt_depth.data_ptr(), float(sil_thres), float(w_im), float(w_depth),
+                                      loss.data_ptr(), scratch.data_ptr(), _stream(im))
+            _check(rc, "track_l1_fwd")
         ctx.save_for_backward(im, depth_sil, gt_im, gt_depth)
         ctx.meta = (float(sil_thres), float(w_im), float(w_depth))
         return loss
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.pre is not None and g.data_ptr() == ctx.pre[2].data_ptr():  # seeded with the forward's seed
+            return ctx.pre[0], ctx.pre[1], None, None, None, None, None, None
         im, depth_sil, gt_im, gt_depth = ctx.saved_tensors
         sil_thres, w_im, w_depth = ctx.meta
         _, H, W = im.shape
@@ -163,9 +192,14 @@ class _TrackingL1(torch.autograd.Function):
         rc = lib.gsr_track_l1_bwd(H, W, im.data_ptr(), depth_sil.data_ptr(), gt_im.data_ptr(), gt_depth.data_ptr(),
                                   sil_thres, w_im, w_depth, g.data_ptr(), dim.data_ptr(), dds.data_ptr(), _stream(im))
         _check(rc, "track_l1_bwd")
-        return dim, dds, None, None, None, None, None
+        return dim, dds, None, None, None, None, None, None
 
 
-def tracking_l1(im, depth_sil, gt_im, gt_depth, sil_thres=0.99, w_im=0.5, w_depth=1.0):
-    """w_im * sum(mask*|gt_im - im|) + w_depth * sum(mask*|gt_depth - depth|) with SplaTAM's tracking mask."""
-    return _TrackingL1.apply(im, depth_sil, gt_im, gt_depth, sil_thres, w_im, w_depth)
+def tracking_l1(im, depth_sil, gt_im, gt_depth, sil_thres=0.99, w_im=0.5, w_depth=1.0, seed=None):
+    """w_im * sum(mask*|gt_im - im|) + w_depth * sum(mask*|gt_depth - depth|) with SplaTAM's tracking mask.
+
+    seed: optional device scalar that the caller will pass to backward() (a static
+    seed, e.g. GraphTracker's ones): the gradient images are then computed in the
+    forward pass, from the seed's value at that time; a backward seeded with any
+    other tensor computes them itself."""
+    return _TrackingL1.apply(im, depth_sil, gt_im, gt_depth, sil_thres, w_im, w_depth, seed)

@@ -133,8 +133,9 @@ def fused_eligible(params, curr_data, cfg: TrackingConfig) -> bool:
 
 
 def _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg: TrackingConfig, dual=True, capacity=0,
-                             status=None, pose_adam=None, means2D=None):
-    """means2D: optional caller-owned [P,3] tensor (the tracker passes a static one without grad)."""
+                             status=None, pose_adam=None, means2D=None, seed=None):
+    """means2D: optional caller-owned [P,3] tensor (the tracker passes a static one without grad).
+    seed: the static loss seed the caller will backward with (loss gradient formed in the forward)."""
     from .glue import track_transform, tracking_l1
     means, rots, dcol, opac, scales = track_transform(params, iter_time_idx, curr_data["w2c"], pose_adam)
     P = means.shape[0]
@@ -151,7 +152,8 @@ def _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg: TrackingConf
                             scales=scales, rotations=rots)
         depth_sil, _, _ = ras(means3D=means, means2D=means2D_ds, colors_precomp=dcol, opacities=opac, scales=scales,
                               rotations=rots)
-    loss = tracking_l1(im, depth_sil, curr_data["im"], curr_data["depth"], cfg.sil_thres, cfg.w_im, cfg.w_depth)
+    loss = tracking_l1(im, depth_sil, curr_data["im"], curr_data["depth"], cfg.sil_thres, cfg.w_im, cfg.w_depth,
+                       seed=seed)
     return loss, radius, means2D
 
 

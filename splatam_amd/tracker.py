@@ -88,7 +88,7 @@ class GraphTracker:
     def _iteration(self, k: int):
         loss, _, _ = _get_loss_tracking_fused(self.params, self.curr, self.t, self.cfg, dual=True,
                                               capacity=self.capacity, status=self.status[k], pose_adam=self.adam,
-                                              means2D=self.means2D)
+                                              means2D=self.means2D, seed=self.seed)
         torch.autograd.backward(loss, self.seed)
         return loss.detach()
 

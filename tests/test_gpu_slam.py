@@ -144,3 +144,36 @@ def test_track_transform_marks_gaussian_outputs_non_differentiable(cuda, scale_c
     assert means.requires_grad and dcol.requires_grad
     assert not opac.requires_grad and not scales.requires_grad
     assert rots.requires_grad == (scale_cols == 3)
+
+
+def test_tracking_l1_seeded_forward_gradient(cuda):
+    """tracking_l1(seed=s) forms the loss gradient in the forward launch (one kernel);
+    backward(s) returns it, and equals the separate backward kernel bitwise; a backward
+    with another seed still computes its own gradient.  Repeated calls reuse the
+    self-resetting scratch."""
+    from splatam_amd.glue import tracking_l1
+    g = torch.Generator(device="cpu").manual_seed(5)
+    H, W = 48, 64
+    im = torch.rand(3, H, W, generator=g).to(cuda)
+    ds = torch.rand(3, H, W, generator=g).to(cuda)
+    ds[1] = 1.0
+    ds[2] = ds[0] ** 2
+    gt_im, gt_d = torch.rand(3, H, W, generator=g).to(cuda), torch.rand(1, H, W, generator=g).to(cuda)
+    ref = None
+    for _ in range(3):
+        a, b = im.clone().requires_grad_(True), ds.clone().requires_grad_(True)
+        loss = tracking_l1(a, b, gt_im, gt_d)
+        loss.backward(torch.full((), 2.0, device=cuda))
+        seed = torch.full((), 2.0, device=cuda)
+        a2, b2 = im.clone().requires_grad_(True), ds.clone().requires_grad_(True)
+        loss2 = tracking_l1(a2, b2, gt_im, gt_d, seed=seed)
+        loss2.backward(seed)
+        assert torch.equal(loss, loss2)
+        assert torch.equal(a.grad, a2.grad) and torch.equal(b.grad, b2.grad)
+        if ref is None:
+            ref = (loss.detach().clone(), a.grad.clone())
+        assert torch.equal(ref[0], loss2.detach()) and torch.equal(ref[1], a2.grad)
+    a3 = im.clone().requires_grad_(True)
+    loss3 = tracking_l1(a3, ds, gt_im, gt_d, seed=torch.ones((), device=cuda))
+    loss3.backward(torch.full((), 2.0, device=cuda))  # not the seed: computed in backward
+    assert torch.equal(a3.grad, ref[1])
