@@ -109,7 +109,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
                   const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
                   const float* __restrict__ final_T,
                   const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
-                  const float* __restrict__ dL_dpix2, float4* __restrict__ inst, BwdGuard guard,
+                  const float* __restrict__ dL_dpix2, float* __restrict__ inst, BwdGuard guard,
                   unsigned long long* clk) {
     static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
     kclock_begin(clk);
@@ -121,6 +121,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     constexpr int NV = bwd_nv<DUAL, OPAC, COL1, COL2, Q2>();
     constexpr int O_OP = 5, O_C1 = 5 + (OPAC ? 1 : 0), O_C2 = O_C1 + (COL1 ? 3 : 0);
     constexpr int BB = bwd_batch<NV>();
+    constexpr int RS = (NV + 1) & ~1;  // record stride (floats)
     constexpr int LS = BB + 4;  // row-list stride (u16)
     // entry BB is a dummy (opacity 0, never blends) that pads the row lists; its
     // per-block slots absorb the pad entries' (zero) sums
@@ -173,9 +174,9 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         const uint32_t gk = point_list[k];
         const RenderRec r = load_rr(rr, gk);
         const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), blockIdx.x, blockIdx.y);
-        inst[3 * u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        inst[3 * u + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
-        inst[3 * u + 2] = make_float4(0.f, 0.f, 0.f, 0.f);
+        float2* dst = reinterpret_cast<float2*>(inst + (size_t)RS * u);
+#pragma unroll
+        for (int m = 0; m < RS / 2; m++) dst[m] = make_float2(0.f, 0.f);
     }
     // background term of dL/dalpha, -T_final / (1 - alpha) * (bg . dL/dpix) (backward.cu:1014):
     // a per-pixel constant times 1 / (1 - alpha); exactly 0 when bg = 0
@@ -322,19 +323,11 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
 #pragma unroll
                 for (int m = 0; m < NV; m++) c[m] += src[m];
             }
-            float sum[12];
+            const uint32_t u = s_u[tid];  // packed record (RecLayout): the NV sums, zero pad
+            float2* dst = reinterpret_cast<float2*>(inst + (size_t)RS * u);
 #pragma unroll
-            for (int m = 0; m < 5; m++) sum[m] = c[m];
-            sum[5] = OPAC ? c[O_OP] : 0.f;
-#pragma unroll
-            for (int m = 0; m < 3; m++) {
-                sum[6 + m] = COL1 ? c[O_C1 + m] : 0.f;
-                sum[9 + m] = (COL2 && m < Q2) ? c[O_C2 + m] : 0.f;
-            }
-            const uint32_t u = s_u[tid];
-            inst[3 * u] = make_float4(sum[0], sum[1], sum[2], sum[3]);
-            inst[3 * u + 1] = make_float4(sum[4], sum[5], sum[6], sum[7]);
-            inst[3 * u + 2] = make_float4(sum[8], sum[9], sum[10], sum[11]);
+            for (int m = 0; m < RS / 2; m++)
+                dst[m] = make_float2(2 * m < NV ? c[2 * m] : 0.f, 2 * m + 1 < NV ? c[2 * m + 1] : 0.f);
         }
         __syncthreads();
     }
@@ -344,9 +337,26 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3>
 static auto bwd_variant() { return render_bwd_kernel<DUAL, OPAC, COL1, COL2, Q2>; }
 
+// The variant launch_render_bwd picks for (need, dual) and its record layout.
+RecLayout bwd_rec_layout(unsigned need, bool dual) {
+    const bool op = need & NEED_OPACITY, c1 = need & NEED_COLORS, c2 = dual && (need & NEED_COLORS2);
+    const int q2 = (dual && (need & NEED_DL2_CH0_ONLY) && !op && !c1) ? 1 : 3;
+    RecLayout L;
+    int nv = 5;
+    L.o_op = op ? nv : -1;
+    nv += op ? 1 : 0;
+    L.o_c1 = c1 ? nv : -1;
+    nv += c1 ? 3 : 0;
+    L.o_c2 = c2 ? nv : -1;
+    L.n_c2 = c2 ? q2 : 0;
+    nv += L.n_c2;
+    L.stride = (nv + 1) & ~1;
+    return L;
+}
+
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
-                             const float* colors2, const float* dL_dpix2, unsigned need, float4* inst,
+                             const float* colors2, const float* dL_dpix2, unsigned need, float* inst,
                              BwdGuard guard, hipStream_t s, unsigned long long* clk) {
     const bool op = need & NEED_OPACITY, c1 = need & NEED_COLORS, c2 = colors2 && (need & NEED_COLORS2);
     const bool q1 = need & NEED_DL2_CH0_ONLY;
@@ -368,8 +378,8 @@ hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint3
 }
 
 __global__ void __launch_bounds__(256)
-gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float4* __restrict__ inst,
-                 GradsOut out, BwdGuard guard) {
+gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float* __restrict__ inst,
+                 RecLayout rec, GradsOut out, BwdGuard guard) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= g.P) return;
     const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
@@ -382,14 +392,31 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     for (int k = 0; k < 48; k++) dsh[k] = 0.f;
     if (radii[i] > 0 && !guard.overflow()) {  // overflow: zero gradients, no record reads
         const uint32_t off = geo.offsets[i], cnt = geo.tiles[i];
+        // fixed-order sum of the Gaussian's instance records (deterministic)
+        float acc[INST_REC_MAX];
+#pragma unroll
+        for (int m = 0; m < INST_REC_MAX; m++) acc[m] = 0.f;
+        const int np = rec.stride / 2;
         for (uint32_t e = 0; e < cnt; e++) {
-            const float4 r0 = inst[3 * (off + e)];
-            const float4 r1 = inst[3 * (off + e) + 1];
-            const float4 r2 = inst[3 * (off + e) + 2];
-            g2[0] += r0.x; g2[1] += r0.y; g2[2] += r0.z; g2[3] += r0.w;
-            g2[4] += r1.x; g2[5] += r1.y; g2[6] += r1.z; g2[7] += r1.w;
-            g2[8] += r2.x;
-            dcol2[0] += r2.y; dcol2[1] += r2.z; dcol2[2] += r2.w;
+            const float2* r = reinterpret_cast<const float2*>(inst + (size_t)rec.stride * (off + e));
+#pragma unroll
+            for (int m = 0; m < INST_REC_MAX / 2; m++)
+                if (m < np) {
+                    const float2 v = r[m];
+                    acc[2 * m] += v.x;
+                    acc[2 * m + 1] += v.y;
+                }
+        }
+#pragma unroll
+        for (int m = 0; m < 5; m++) g2[m] = acc[m];
+#pragma unroll
+        for (int m = 0; m < INST_REC_MAX; m++) {  // constant-index selects (no dynamic register indexing)
+            if (m == rec.o_op) g2[5] = acc[m];
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                if (rec.o_c1 >= 0 && m == rec.o_c1 + k) g2[6 + k] = acc[m];
+                if (rec.o_c2 >= 0 && k < rec.n_c2 && m == rec.o_c2 + k) dcol2[k] = acc[m];
+            }
         }
         // instance records hold (hx, hy, hxx, hxy, hyy, dopacity, dcolor) sums (render_bwd_kernel);
         // the conic is recomputed exactly as preprocess computed it (the render record keeps
@@ -442,10 +469,10 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     }
 }
 
-hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float4* inst,
-                            const GradsOut& out, BwdGuard guard, hipStream_t s) {
+hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* inst,
+                            RecLayout rec, const GradsOut& out, BwdGuard guard, hipStream_t s) {
     if (g.P == 0) return hipSuccess;
-    hipLaunchKernelGGL(gauss_bwd_kernel, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii, inst, out,
+    hipLaunchKernelGGL(gauss_bwd_kernel, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii, inst, rec, out,
                        guard);
     return hipGetLastError();
 }

@@ -517,18 +517,19 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
             return hip_fail(e, "gaussian backward (power)");
         return GSR_OK;
     }
-    float4* inst = nullptr;
+    float* inst = nullptr;
+    // SH colours feed dL/dmeans3D through the view direction, so their sums are needed with SH
+    const unsigned need = (out.dopacity ? NEED_OPACITY : 0u) | ((out.dcolors || g.shs) ? NEED_COLORS : 0u) |
+                          (dcolors2 ? NEED_COLORS2 : 0u) | (dl2_channels == 1 ? NEED_DL2_CH0_ONLY : 0u);
+    const RecLayout rec = bwd_rec_layout(need, colors2 != nullptr);
     if (num_rendered > 0) {
         if (!binning_buffer) return fail(GSR_ERR_INVALID_ARG, "missing binning buffer");
         if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
-        inst = (float4*)obtain(alloc, alloc_ctx, GSR_BUF_SCRATCH, sizeof(float4) * INST_REC_F4 * (size_t)num_rendered);
+        inst = (float*)obtain(alloc, alloc_ctx, GSR_BUF_SCRATCH, sizeof(float) * rec.stride * (size_t)num_rendered);
         if (!inst) return fail(GSR_ERR_ALLOC, "allocator returned NULL (backward scratch)");
         const char* bb = (const char*)binning_buffer;
         const uint32_t* point_list = (const uint32_t*)(bb + BL.point_list);
         StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream, true);
-        // SH colours feed dL/dmeans3D through the view direction, so their sums are needed with SH
-        const unsigned need = (out.dopacity ? NEED_OPACITY : 0u) | ((out.dcolors || g.shs) ? NEED_COLORS : 0u) |
-                              (dcolors2 ? NEED_COLORS2 : 0u) | (dl2_channels == 1 ? NEED_DL2_CH0_ONLY : 0u);
         if ((e = launch_render_bwd(cam, ranges, point_list, geo, final_T, n_contrib, dL_dout_color, colors2,
                                    dL_dout_color2, need, inst, BwdGuard{geo.counters, (uint32_t)num_rendered},
                                    stream, t.kclock())) != hipSuccess)
@@ -537,7 +538,7 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     out.dcolors2 = dcolors2;
     {
         StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
-        if ((e = launch_gauss_bwd(cam, g, geo, radii, inst, out, BwdGuard{geo.counters, (uint32_t)num_rendered},
+        if ((e = launch_gauss_bwd(cam, g, geo, radii, inst, rec, out, BwdGuard{geo.counters, (uint32_t)num_rendered},
                                   stream)) != hipSuccess)
             return hip_fail(e, "gaussian backward");
     }

@@ -24,7 +24,7 @@ constexpr int SORT_ITEMS = 8;        // keys per thread per radix pass
 constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;
 constexpr int RADIX = 256;
 constexpr int RENDER_BATCH = 256;    // Gaussians staged in LDS per batch
-constexpr int INST_REC_F4 = 3;       // backward per-instance record: 3 x float4 (9 used floats)
+constexpr int INST_REC_MAX = 12;     // backward per-instance record: at most 12 floats (RecLayout)
 constexpr int TILE_CTR_STRIDE = 64;  // per-tile atomic counters one 256-B line apart (spread over L2 channels)
 
 // ---------------------------------------------------------------- layouts --
@@ -852,9 +852,18 @@ hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint3
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
                              unsigned long long* clk = nullptr);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* vis, hipStream_t s);
+// Per-(tile, Gaussian) instance record of the power-1 backward: the per-pair sums
+// the launched render_bwd variant forms, packed (no slots for absent terms):
+// [hx, hy, hxx, hxy, hyy | G dL/dalpha (o_op) | dch dp (o_c1, 3) | dch dq (o_c2, n_c2)]
+// padded to an even count (float2 stores); 6 floats (24 B) for SplaTAM tracking.
+struct RecLayout {
+    int stride;                 // floats per record (even)
+    int o_op, o_c1, o_c2, n_c2; // offsets, -1 when absent
+};
+RecLayout bwd_rec_layout(unsigned need, bool dual);
 hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
-                             const float* colors2, const float* dL_dpix2, unsigned need, float4* inst, BwdGuard guard,
+                             const float* colors2, const float* dL_dpix2, unsigned need, float* inst, BwdGuard guard,
                              hipStream_t s, unsigned long long* clk = nullptr);
 // which optional per-pair sums render_bwd forms (the geometric ones always)
 constexpr unsigned NEED_OPACITY = 1u, NEED_COLORS = 2u, NEED_COLORS2 = 4u;
@@ -870,8 +879,8 @@ struct GradsOut {
     float* drot;
     float* dcolors2;  // second colour set of a dual render (nullptr otherwise)
 };
-hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float4* inst,
-                            const GradsOut& out, BwdGuard guard, hipStream_t s);
+hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* inst,
+                            RecLayout rec, const GradsOut& out, BwdGuard guard, hipStream_t s);
 hipError_t launch_selftest_reduce9(const float* in, float* out, hipStream_t s);
 // error reporting shared by the C entry points (gsr_last_error)
 int fail(int code, const std::string& msg);
