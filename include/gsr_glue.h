@@ -92,6 +92,82 @@ int gsr_track_l1_bwd(int H, int W, const float* im, const float* depth_sil, cons
                      const float* gt_depth, float sil_thres, float w_im, float w_depth, const float* dL_dloss,
                      float* dL_dim, float* dL_ddepth_sil, void* stream);
 
+/* ------------------------------------------------------------------ mapping --
+ * get_loss(mapping=True, do_ba=False) (scripts/splatam.py:220-353) with the
+ * Replica mapping config (configs/replica/splatam.py:82-103: use_l1,
+ * use_sil_for_loss=False, ignore_outlier_depth_loss=False, weights im 0.5 /
+ * depth 1.0), and the mapping optimizer (splatam.py:166-172).  Forward of the
+ * transform is gsr_track_transform_fwd (identical outputs). */
+
+/* Persistent zero-filled scratch (same contract as gsr_track_scratch_floats)
+ * and the per-call state gsr_map_loss_fwd hands to gsr_map_loss_bwd. */
+int gsr_map_loss_scratch_floats(int H, int W);
+int gsr_map_loss_state_floats(int H, int W);
+
+/* loss = w_im * (0.8 * mean|im - gt_im| + 0.2 * (1 - calc_ssim(im, gt_im)))
+ *      + w_depth * mean over mask of |gt_depth - depth|,
+ * mask = (gt_depth > 0) & !isnan(depth) & !isnan(depth_sq - depth^2)
+ * (gs_helpers.py:18-19 l1_loss_v1, slam_external.py:66-97 calc_ssim with an
+ * 11x11 sigma-1.5 window and zero padding).  im/gt_im/depth_sil [3,H,W],
+ * gt_depth [1,H,W]; loss: 1 float (device); state: gsr_map_loss_state_floats. */
+int gsr_map_loss_fwd(int H, int W, const float* im, const float* depth_sil, const float* gt_im, const float* gt_depth,
+                     float w_im, float w_depth, float* loss, float* state, float* scratch, void* stream);
+
+/* Gradient of the loss above w.r.t. im [3,H,W] and depth_sil [3,H,W] (channels
+ * 1, 2 written as zero), given dL_dloss (1 float, device) and the forward's state. */
+int gsr_map_loss_bwd(int H, int W, const float* im, const float* depth_sil, const float* gt_im, const float* gt_depth,
+                     float w_im, float w_depth, const float* dL_dloss, const float* state, float* dL_dim,
+                     float* dL_ddepth_sil, void* stream);
+
+/* Backward of transform_to_frame(gaussians_grad=True, camera_grad=False) + the
+ * rendervar builders: from the gradients of (means_cam, rotations, depth
+ * colours, opacities, scales) [any but dL_dmeans_cam may be NULL] to the
+ * gradients of means3D [P,3], unnorm_rotations [P,4], logit_opacities [P,1] and
+ * log_scales [P,scale_cols] (outputs other than dL_dmeans may be NULL). */
+int gsr_map_transform_bwd(int P, const float* unnorm_rot, const float* logit_opac, const float* log_scales,
+                          int scale_cols, const float* cam_q, int q_stride, const float* means_cam, const float* w2c,
+                          const float* dL_dmeans_cam, const float* dL_drot, const float* dL_ddepth_colors,
+                          const float* dL_dopac, const float* dL_dscales, float* dL_dmeans, float* dL_dunnorm_rot,
+                          float* dL_dlogit_opac, float* dL_dlog_scales, void* stream);
+
+/* torch.optim.Adam state of the mapping optimizer for the five Gaussian
+ * parameter tensors [means3D, unnorm_rotations, logit_opacities, log_scales,
+ * colours (rgb_colors [P,3] or shs [P,M,3])]: exp_avg / exp_avg_sq of each
+ * tensor's shape, per-tensor lr, and the optimizer step (>= 1, i.e. already
+ * incremented) this update uses. */
+typedef struct gsr_map_adam {
+    float* exp_avg[5];
+    float* exp_avg_sq[5];
+    float lr[5];
+    int step;
+    float beta1, beta2, eps;
+} gsr_map_adam;
+
+/* gsr_map_transform_bwd with the optimizer step fused in: the parameters are
+ * updated in place, no gradient is written.  dL_dcolors (the rasterizer's
+ * gradient of the colour parameters, [P, color_cols]) steps `colors`; NULL
+ * leaves them (and their state) untouched. */
+int gsr_map_transform_bwd_adam(int P, float* means_world, float* unnorm_rot, float* logit_opac, float* log_scales,
+                               int scale_cols, float* colors, int color_cols, const float* cam_q, int q_stride,
+                               const float* means_cam, const float* w2c, const float* dL_dmeans_cam,
+                               const float* dL_drot, const float* dL_ddepth_colors, const float* dL_dopac,
+                               const float* dL_dscales, const float* dL_dcolors, const gsr_map_adam* adam,
+                               void* stream);
+
+/* torch.optim.Adam (foreach implementation, no weight decay / amsgrad /
+ * maximize) over up to 16 float32 tensors in one launch; every tensor shares
+ * `step` (>= 1, already incremented) and has its own lr. */
+typedef struct gsr_adam_tensor {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    long long n;
+    float lr;
+} gsr_adam_tensor;
+int gsr_adam_step(int n_tensors, const gsr_adam_tensor* tensors, int step, float beta1, float beta2, float eps,
+                  void* stream);
+
 #ifdef __cplusplus
 }
 #endif

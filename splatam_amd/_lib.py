@@ -33,6 +33,18 @@ class GsrGrads(ctypes.Structure):
                 ("dcov3D", c_void_p), ("dsh", c_void_p), ("dscales", c_void_p), ("drotations", c_void_p)]
 
 
+class GsrMapAdam(ctypes.Structure):
+    """gsr_map_adam (include/gsr_glue.h)."""
+    _fields_ = [("exp_avg", c_void_p * 5), ("exp_avg_sq", c_void_p * 5), ("lr", c_float * 5), ("step", c_int),
+                ("beta1", c_float), ("beta2", c_float), ("eps", c_float)]
+
+
+class GsrAdamTensor(ctypes.Structure):
+    """gsr_adam_tensor (include/gsr_glue.h)."""
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
+                ("n", ctypes.c_longlong), ("lr", c_float)]
+
+
 ALLOC_FN = ctypes.CFUNCTYPE(c_void_p, c_void_p, c_int, c_size_t)
 
 # every symbol declared in include/gsr.h: (name, restype, argtypes)
@@ -76,6 +88,20 @@ SIGNATURES = {
     "gsr_track_l1_fwd_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
                                      ctypes.c_float, ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p]),
+    # include/gsr_glue.h: fused SplaTAM mapping glue and optimizer
+    "gsr_map_loss_scratch_floats": (c_int, [c_int, c_int]),
+    "gsr_map_loss_state_floats": (c_int, [c_int, c_int]),
+    "gsr_map_loss_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_void_p,
+                                 c_void_p, c_void_p, c_void_p]),
+    "gsr_map_loss_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_void_p,
+                                 c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gsr_map_transform_bwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p]),
+    "gsr_map_transform_bwd_adam": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                                           c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, ctypes.POINTER(GsrMapAdam), c_void_p]),
+    "gsr_adam_step": (c_int, [c_int, ctypes.POINTER(GsrAdamTensor), c_int, c_float, c_float, c_float, c_void_p]),
 }
 
 

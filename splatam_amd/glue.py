@@ -15,6 +15,8 @@ path: these raise on non-ROCm tensors.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from ._lib import lib
@@ -203,3 +205,195 @@ def tracking_l1(im, depth_sil, gt_im, gt_depth, sil_thres=0.99, w_im=0.5, w_dept
     forward pass, from the seed's value at that time; a backward seeded with any
     other tensor computes them itself."""
     return _TrackingL1.apply(im, depth_sil, gt_im, gt_depth, sil_thres, w_im, w_depth, seed)
+
+
+# ------------------------------------------------------------------ mapping --
+class MapAdam:
+    """torch.optim.Adam state of SplaTAM's mapping optimizer (scripts/splatam.py:166-172:
+    one group per parameter, eps 1e-15) for the five Gaussian tensors, stepped inside the
+    mapping transform backward (gsr_map_transform_bwd_adam).  `step` counts like torch's
+    per-parameter state["step"]; SplaTAM re-creates the optimizer for every frame (reset())."""
+
+    def __init__(self, params: dict, lrs: dict, color_key: str = "rgb_colors", betas=(0.9, 0.999), eps=1e-15):
+        self.keys = ("means3D", "unnorm_rotations", "logit_opacities", "log_scales", color_key)
+        self.exp_avg = [torch.zeros_like(params[k]) for k in self.keys]
+        self.exp_avg_sq = [torch.zeros_like(params[k]) for k in self.keys]
+        self.lr = [float(lrs[k]) for k in self.keys]
+        self.betas, self.eps = (float(betas[0]), float(betas[1])), float(eps)
+        self.step = 0
+
+    def reset(self):
+        for t in self.exp_avg + self.exp_avg_sq:
+            t.zero_()
+        self.step = 0
+
+    def struct(self):
+        from ._lib import GsrMapAdam
+        s = GsrMapAdam()
+        for k in range(5):
+            s.exp_avg[k] = self.exp_avg[k].data_ptr()
+            s.exp_avg_sq[k] = self.exp_avg_sq[k].data_ptr()
+            s.lr[k] = self.lr[k]
+        s.step, s.beta1, s.beta2, s.eps = self.step, self.betas[0], self.betas[1], self.eps
+        return s
+
+
+class _MapTransform(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means_world, unnorm_rot, logit_opac, log_scales, colors, cam_rots, cam_trans, w2c, time_idx,
+                adam=None):
+        cam_rots, cam_trans = _f32c(cam_rots, "cam_unnorm_rots"), _f32c(cam_trans, "cam_trans")
+        means_world, unnorm_rot = _f32c(means_world, "means3D"), _f32c(unnorm_rot, "unnorm_rotations")
+        logit_opac, log_scales = _f32c(logit_opac, "logit_opacities"), _f32c(log_scales, "log_scales")
+        colors, w2c = _f32c(colors, "colors"), _f32c(w2c, "w2c")
+        T = cam_rots.shape[-1]
+        if cam_rots.shape != (1, 4, T) or cam_trans.shape != (1, 3, T):
+            raise RuntimeError("cam_unnorm_rots / cam_trans must be (1,4,T) / (1,3,T)")
+        t = int(time_idx)
+        P = means_world.shape[0]
+        scols = log_scales.shape[1]
+        if colors.shape[0] != P:
+            raise RuntimeError("colour parameters must have one row per Gaussian")
+        f32 = dict(dtype=torch.float32, device=means_world.device)
+        means_cam, rot, dcol = torch.empty(P, 3, **f32), torch.empty(P, 4, **f32), torch.empty(P, 3, **f32)
+        opac, scales = torch.empty(P, 1, **f32), torch.empty(P, 3, **f32)
+        rc = lib.gsr_track_transform_fwd(P, means_world.data_ptr(), unnorm_rot.data_ptr(), logit_opac.data_ptr(),
+                                         log_scales.data_ptr(), scols, cam_rots.data_ptr() + 4 * t,
+                                         cam_trans.data_ptr() + 4 * t, T, w2c.data_ptr(), means_cam.data_ptr(),
+                                         rot.data_ptr(), dcol.data_ptr(), opac.data_ptr(), scales.data_ptr(),
+                                         _stream(means_world))
+        _check(rc, "map_transform_fwd")
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(means_world, unnorm_rot, logit_opac, log_scales, colors, cam_rots, means_cam, w2c)
+        ctx.meta = (t, T, scols)
+        ctx.adam = adam
+        return means_cam, rot, dcol, opac, scales, colors.view_as(colors)
+
+    @staticmethod
+    def backward(ctx, g_means, g_rot, g_dcol, g_opac, g_scales, g_col):
+        means_world, unnorm_rot, logit_opac, log_scales, colors, cam_rots, means_cam, w2c = ctx.saved_tensors
+        t, T, scols = ctx.meta
+        P = means_world.shape[0]
+        c = lambda x: x.contiguous() if x is not None else None  # noqa: E731
+        p = lambda x: x.data_ptr() if x is not None else None  # noqa: E731
+        g_means, g_rot, g_dcol, g_opac, g_scales, g_col = map(c, (g_means, g_rot, g_dcol, g_opac, g_scales, g_col))
+        if g_means is None:
+            g_means = torch.zeros_like(means_cam)
+        adam = ctx.adam
+        if adam is not None:  # optimizer step fused into the backward: parameters updated in place
+            adam.step += 1
+            st = adam.struct()
+            ccols = colors.numel() // max(P, 1)
+            rc = lib.gsr_map_transform_bwd_adam(
+                P, means_world.data_ptr(), unnorm_rot.data_ptr(), logit_opac.data_ptr(), log_scales.data_ptr(), scols,
+                colors.data_ptr(), ccols, cam_rots.data_ptr() + 4 * t, T, means_cam.data_ptr(), w2c.data_ptr(),
+                g_means.data_ptr(), p(g_rot), p(g_dcol), p(g_opac), p(g_scales), p(g_col), ctypes.byref(st),
+                _stream(means_world))
+            _check(rc, "map_transform_bwd_adam")
+            return (None,) * 10
+        need = ctx.needs_input_grad
+        dm = torch.empty_like(means_world)
+        du = torch.empty_like(unnorm_rot) if need[1] else None
+        dl = torch.empty_like(logit_opac) if need[2] else None
+        ds = torch.empty_like(log_scales) if need[3] else None
+        rc = lib.gsr_map_transform_bwd(P, unnorm_rot.data_ptr(), logit_opac.data_ptr(), log_scales.data_ptr(), scols,
+                                       cam_rots.data_ptr() + 4 * t, T, means_cam.data_ptr(), w2c.data_ptr(),
+                                       g_means.data_ptr(), p(g_rot), p(g_dcol), p(g_opac), p(g_scales), dm.data_ptr(),
+                                       p(du), p(dl), p(ds), _stream(means_world))
+        _check(rc, "map_transform_bwd")
+        return (dm if need[0] else None), du, dl, ds, (g_col if need[4] else None), None, None, None, None, None
+
+
+def map_transform(params: dict, time_idx: int, w2c: torch.Tensor, color_key: str = "rgb_colors",
+                  adam: MapAdam | None = None):
+    """transform_to_frame(params, t, gaussians_grad=True, camera_grad=False) (slam_helpers.py:252-304)
+    + the rendervar builders (slam_helpers.py:124-139, 196-213, 234-249) for the mapping iteration.
+    Returns (means3D_cam, rotations, depth_colors [z,1,z^2], opacities, scales, colours); differentiable
+    w.r.t. the Gaussian parameters.  With `adam` the backward applies the mapping optimizer's step in
+    place (no .grad is produced)."""
+    return _MapTransform.apply(params["means3D"], params["unnorm_rotations"], params["logit_opacities"],
+                               params["log_scales"], params[color_key], params["cam_unnorm_rots"].detach(),
+                               params["cam_trans"].detach(), w2c, int(time_idx), adam)
+
+
+class _MappingLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, im, depth_sil, gt_im, gt_depth, w_im, w_depth):
+        im, depth_sil = _f32c(im, "im"), _f32c(depth_sil, "depth_sil")
+        gt_im, gt_depth = _f32c(gt_im, "gt_im"), _f32c(gt_depth, "gt_depth")
+        _, H, W = im.shape
+        if depth_sil.shape != (3, H, W) or gt_im.shape != (3, H, W) or gt_depth.shape != (1, H, W):
+            raise RuntimeError("mapping_loss: expected im/depth_sil/gt_im [3,H,W] and gt_depth [1,H,W]")
+        loss = torch.empty((), dtype=torch.float32, device=im.device)
+        state = torch.empty(lib.gsr_map_loss_state_floats(H, W), dtype=torch.float32, device=im.device)
+        scratch = _scratch(im, lib.gsr_map_loss_scratch_floats(H, W))
+        rc = lib.gsr_map_loss_fwd(H, W, im.data_ptr(), depth_sil.data_ptr(), gt_im.data_ptr(), gt_depth.data_ptr(),
+                                  float(w_im), float(w_depth), loss.data_ptr(), state.data_ptr(), scratch.data_ptr(),
+                                  _stream(im))
+        _check(rc, "map_loss_fwd")
+        ctx.save_for_backward(im, depth_sil, gt_im, gt_depth, state)
+        ctx.meta = (float(w_im), float(w_depth))
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        im, depth_sil, gt_im, gt_depth, state = ctx.saved_tensors
+        w_im, w_depth = ctx.meta
+        _, H, W = im.shape
+        g = g.contiguous()
+        dim, dds = torch.empty_like(im), torch.empty_like(depth_sil)
+        rc = lib.gsr_map_loss_bwd(H, W, im.data_ptr(), depth_sil.data_ptr(), gt_im.data_ptr(), gt_depth.data_ptr(),
+                                  w_im, w_depth, g.data_ptr(), state.data_ptr(), dim.data_ptr(), dds.data_ptr(),
+                                  _stream(im))
+        _check(rc, "map_loss_bwd")
+        return dim, dds, None, None, None, None
+
+
+def mapping_loss(im, depth_sil, gt_im, gt_depth, w_im=0.5, w_depth=1.0):
+    """w_im * (0.8 * l1_loss_v1(im, gt_im) + 0.2 * (1 - calc_ssim(im, gt_im))) + w_depth * masked mean depth L1
+    (get_loss with mapping=True, scripts/splatam.py:262-296), one fused SSIM/L1 launch each way."""
+    return _MappingLoss.apply(im, depth_sil, gt_im, gt_depth, w_im, w_depth)
+
+
+class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam (no weight decay / amsgrad / maximize) whose step is one HIP
+    launch per 16 tensors (gsr_adam_step).  State keys and shapes are torch's
+    ("step", "exp_avg", "exp_avg_sq"), so SplaTAM's optimizer surgery
+    (utils/slam_external.py update_params_and_optimizer / cat_params_to_optimizer /
+    remove_points) works on it unchanged."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        from ._lib import GsrAdamTensor
+        loss = closure() if closure is not None else None
+        batches = {}
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.device.type != "cuda" or p.dtype != torch.float32 or not p.is_contiguous():
+                    raise RuntimeError("FusedAdam: contiguous float32 ROCm tensors only (no CPU fallback)")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                key = (int(st["step"].item()), group["betas"], group["eps"], p.device)
+                batches.setdefault(key, []).append((p, p.grad.contiguous(), st, group["lr"]))
+        for (step, betas, eps, dev), items in batches.items():
+            for k in range(0, len(items), 16):
+                chunk = items[k:k + 16]
+                arr = (GsrAdamTensor * len(chunk))()
+                for j, (p, g, st, lr) in enumerate(chunk):
+                    arr[j].param, arr[j].grad = p.data_ptr(), g.data_ptr()
+                    arr[j].exp_avg, arr[j].exp_avg_sq = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
+                    arr[j].n, arr[j].lr = p.numel(), float(lr)
+                with torch.cuda.device(dev):
+                    rc = lib.gsr_adam_step(len(chunk), arr, step, float(betas[0]), float(betas[1]), float(eps),
+                                           torch.cuda.current_stream(dev).cuda_stream)
+                _check(rc, "adam_step")
+        return loss

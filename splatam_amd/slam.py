@@ -11,7 +11,8 @@ itself is splatam_amd.rasterizer (HIP).
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+import math
+from dataclasses import dataclass, field
 
 import torch
 import torch.nn.functional as F
@@ -103,13 +104,13 @@ def transformed_params2depthplussilhouette(params, w2c, tg, fast=True):
             "means2D": torch.zeros_like(params["means3D"], requires_grad=True) + 0}
 
 
-def camera_settings(cam, device) -> GaussianRasterizationSettings:
-    """setup_camera (recon_helpers.py:4-27) moved to `device`."""
+def camera_settings(cam, device, sh_degree: int = 0) -> GaussianRasterizationSettings:
+    """setup_camera (recon_helpers.py:4-27) moved to `device` (sh_degree > 0: SH colour renders)."""
     return GaussianRasterizationSettings(
         image_height=cam.H, image_width=cam.W, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
         bg=torch.zeros(3, dtype=torch.float32, device=device), scale_modifier=1.0,
         viewmatrix=cam.viewmatrix.to(device).contiguous(), projmatrix=cam.projmatrix.to(device).contiguous(),
-        sh_degree=0, campos=cam.campos.to(device).contiguous(), prefiltered=False)  # contiguous: no per-call copy
+        sh_degree=sh_degree, campos=cam.campos.to(device).contiguous(), prefiltered=False)  # contiguous: no per-call copy
 
 
 @dataclass
@@ -227,3 +228,133 @@ def init_tracking_params(scene: Scene, num_frames: int, device, pose_noise=(0.5,
     out = {k: v.to(device).float().contiguous() for k, v in params.items()}
     assert out["means3D"].shape[0] == P
     return out
+
+
+# ------------------------------------------------------------------ mapping --
+@dataclass
+class MappingConfig:
+    """configs/replica/splatam.py:82-103 (mapping block); `shs` is this build's lr for the
+    SH colour parameters of config 4 (SplaTAM itself renders precomputed rgb_colors)."""
+    use_sil_for_loss: bool = False
+    use_l1: bool = True
+    ignore_outlier_depth_loss: bool = False
+    w_im: float = 0.5
+    w_depth: float = 1.0
+    lrs: dict = field(default_factory=lambda: dict(means3D=0.0001, rgb_colors=0.0025, shs=0.0025,
+                                                   unnorm_rotations=0.001, logit_opacities=0.05, log_scales=0.001,
+                                                   cam_unnorm_rots=0.0, cam_trans=0.0))
+
+
+def _gaussian(window_size, sigma):
+    """slam_external.py:49-51."""
+    gauss = torch.Tensor([math.exp(-(x - window_size // 2) ** 2 / float(2 * sigma ** 2)) for x in range(window_size)])
+    return gauss / gauss.sum()
+
+
+def create_window(window_size, channel):
+    """slam_external.py:54-58."""
+    w1 = _gaussian(window_size, 1.5).unsqueeze(1)
+    w2 = w1.mm(w1.t()).float().unsqueeze(0).unsqueeze(0)
+    return w2.expand(channel, 1, window_size, window_size).contiguous()
+
+
+def calc_ssim(img1, img2, window_size=11, size_average=True):
+    """slam_external.py:61-97 (literal torch: five depthwise 11x11 convolutions)."""
+    channel = img1.size(-3)
+    window = create_window(window_size, channel).to(img1.device).type_as(img1)
+    pad = window_size // 2
+    mu1 = F.conv2d(img1, window, padding=pad, groups=channel)
+    mu2 = F.conv2d(img2, window, padding=pad, groups=channel)
+    mu1_sq, mu2_sq, mu1_mu2 = mu1.pow(2), mu2.pow(2), mu1 * mu2
+    sigma1_sq = F.conv2d(img1 * img1, window, padding=pad, groups=channel) - mu1_sq
+    sigma2_sq = F.conv2d(img2 * img2, window, padding=pad, groups=channel) - mu2_sq
+    sigma12 = F.conv2d(img1 * img2, window, padding=pad, groups=channel) - mu1_mu2
+    c1, c2 = 0.01 ** 2, 0.03 ** 2
+    ssim_map = ((2 * mu1_mu2 + c1) * (2 * sigma12 + c2)) / ((mu1_sq + mu2_sq + c1) * (sigma1_sq + sigma2_sq + c2))
+    return ssim_map.mean() if size_average else ssim_map.mean(1).mean(1).mean(1)
+
+
+def l1_loss_v1(x, y):
+    """utils/gs_helpers.py:18-19."""
+    return torch.abs(x - y).mean()
+
+
+def color_key(params) -> str:
+    return "shs" if "shs" in params else "rgb_colors"
+
+
+def _rendervar_colors(params, rv):
+    if "shs" in params:  # SH colours (config 4): the rasterizer evaluates them (forward.cu:20-73)
+        rv.pop("colors_precomp")
+        rv["shs"] = params["shs"]
+    return rv
+
+
+def fused_mapping_eligible(params, curr_data, cfg: MappingConfig) -> bool:
+    """The fused HIP glue covers SplaTAM's mapping configuration: Gaussians optimised, camera
+    fixed (do_ba=False), L1 + SSIM image loss, no silhouette mask, no outlier-depth rejection."""
+    return (cfg.use_l1 and not cfg.use_sil_for_loss and not cfg.ignore_outlier_depth_loss
+            and params["means3D"].is_cuda and not params["cam_unnorm_rots"].requires_grad
+            and not params["cam_trans"].requires_grad
+            and curr_data["im"].dim() == 3 and curr_data["depth"].dim() == 3)
+
+
+def get_loss_mapping(params, curr_data, iter_time_idx, cfg: MappingConfig = MappingConfig(), fused=True,
+                     adam=None):
+    """scripts/splatam.py:220-353 with mapping=True, do_ba=False: two renders (RGB or SH colours, and
+    [z,1,z^2]), masked mean depth L1 and 0.8 L1 + 0.2 (1 - SSIM) on the image.
+
+    fused=True (and fused_mapping_eligible): the transform / rendervar builders run as
+    gsr_track_transform_fwd + gsr_map_transform_bwd, both renders share one rasterization, and the
+    loss is the fused SSIM/L1 kernel pair; `adam` (glue.MapAdam) then applies the mapping optimizer's
+    step inside the transform backward.  fused=False is the literal statement of the reference."""
+    if fused and fused_mapping_eligible(params, curr_data, cfg):
+        from .glue import map_transform, mapping_loss
+        key = color_key(params)
+        means, rots, dcol, opac, scales, col = map_transform(params, iter_time_idx, curr_data["w2c"], key, adam)
+        P = means.shape[0]
+        means2D = torch.zeros(P, 3, device=means.device, requires_grad=True)
+        sh, colors = (col, None) if key == "shs" else (None, col)
+        im, depth_sil, radius, _ = rasterize_gaussians_dual(means, means2D, sh, colors, dcol, opac, scales, rots, None,
+                                                            curr_data["cam"], grad2_channels=1)
+        loss = mapping_loss(im, depth_sil, curr_data["im"], curr_data["depth"], cfg.w_im, cfg.w_depth)
+        return loss, radius, means2D
+    if adam is not None:
+        raise RuntimeError("get_loss_mapping: the fused optimizer step needs the fused glue")
+    tg = transform_to_frame(params, iter_time_idx, gaussians_grad=True, camera_grad=False, fast=False)
+    rendervar = _rendervar_colors(params, transformed_params2rendervar(params, tg))
+    depth_sil_rendervar = transformed_params2depthplussilhouette(params, curr_data["w2c"], tg, fast=False)
+    rendervar["means2D"].retain_grad()
+    im, radius, _ = GaussianRasterizer(raster_settings=curr_data["cam"])(**rendervar)
+    depth_sil, _, _ = GaussianRasterizer(raster_settings=curr_data["cam"])(**depth_sil_rendervar)
+    depth = depth_sil[0, :, :].unsqueeze(0)
+    depth_sq = depth_sil[2, :, :].unsqueeze(0)
+    uncertainty = (depth_sq - depth ** 2).detach()
+    nan_mask = (~torch.isnan(depth)) & (~torch.isnan(uncertainty))
+    mask = ((curr_data["depth"] > 0) & nan_mask).detach()
+    loss_depth = torch.abs(curr_data["depth"] - depth)[mask].mean()
+    loss_im = 0.8 * l1_loss_v1(im, curr_data["im"]) + 0.2 * (1.0 - calc_ssim(im, curr_data["im"]))
+    loss = cfg.w_im * loss_im + cfg.w_depth * loss_depth
+    return loss, radius, rendervar["means2D"]
+
+
+def init_mapping_params(scene: Scene, num_frames: int, device, pose_noise=(0.5, 0.01), seed=0):
+    """Mapping parameter dict: init_tracking_params plus anisotropic log_scales [P,3] when the scene
+    is anisotropic, and SH colours `shs` [P,M,3] when it carries them (config 4)."""
+    params = init_tracking_params(scene, num_frames, device, pose_noise, seed)
+    if not torch.allclose(scene.scales, scene.scales[:, :1].expand_as(scene.scales)):
+        params["log_scales"] = torch.log(scene.scales).to(device).float().contiguous()
+    if scene.shs is not None:
+        params["shs"] = scene.shs.to(device).float().contiguous()
+        del params["rgb_colors"]
+    return params
+
+
+def mapping_optimizer(params: dict, cfg: MappingConfig = MappingConfig(), fused=True):
+    """initialize_optimizer (scripts/splatam.py:166-172): one Adam group per parameter, eps 1e-15;
+    fused=True returns glue.FusedAdam (one HIP launch per step), else torch.optim.Adam."""
+    groups = [{"params": [v], "name": k, "lr": cfg.lrs[k]} for k, v in params.items()]
+    if fused:
+        from .glue import FusedAdam
+        return FusedAdam(groups, lr=0.0, eps=1e-15)
+    return torch.optim.Adam(groups, lr=0.0, eps=1e-15)

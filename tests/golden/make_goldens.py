@@ -150,6 +150,46 @@ def main():
     q = torch.randn(16, 4, generator=g)
     np.savez(os.path.join(OUT, "glue_build_rotation.npz"), q=q.numpy(), R=ext.build_rotation(q).numpy())
 
+    # ---- calc_ssim (slam_external.py:61-97): value and gradient w.r.t. the first image (mapping loss)
+    g2 = torch.Generator().manual_seed(2)
+    img1 = torch.rand(3, 37, 53, generator=g2, requires_grad=True)
+    img2 = (img1.detach() + 0.1 * torch.randn(3, 37, 53, generator=g2)).clamp(0.0, 1.0)
+    ssim = ext.calc_ssim(img1, img2)
+    ssim.backward()
+    np.savez(os.path.join(OUT, "glue_ssim.npz"), img1=img1.detach().numpy(), img2=img2.numpy(),
+             ssim=ssim.detach().numpy(), grad_img1=img1.grad.numpy())
+
+    # ---- mapping transform backward: transform_to_frame(gaussians_grad=True, camera_grad=False) +
+    # rendervar builders, seeded upstream gradients on every rendervar output
+    for iso in (True, False):
+        params = {
+            "means3D": torch.randn(P, 3, generator=g) + torch.tensor([0.0, 0.0, 3.0]),
+            "rgb_colors": torch.rand(P, 3, generator=g),
+            "unnorm_rotations": torch.randn(P, 4, generator=g),
+            "logit_opacities": torch.randn(P, 1, generator=g),
+            "log_scales": torch.randn(P, 1 if iso else 3, generator=g) - 3.0,
+            "cam_unnorm_rots": torch.randn(1, 4, T, generator=g),
+            "cam_trans": 0.1 * torch.randn(1, 3, T, generator=g),
+        }
+        for k in ("means3D", "rgb_colors", "unnorm_rotations", "logit_opacities", "log_scales"):
+            params[k].requires_grad_(True)
+        tg = slam.transform_to_frame(params, 2, gaussians_grad=True, camera_grad=False)
+        rv = slam.transformed_params2rendervar(params, tg)
+        dv = slam.transformed_params2depthplussilhouette(params, torch.tensor(w2c).float(), tg)
+        ups = {"g_means": torch.randn(P, 3, generator=g), "g_rot": torch.randn(P, 4, generator=g),
+               "g_opac": torch.randn(P, 1, generator=g), "g_scales": torch.randn(P, 3, generator=g),
+               "g_dcol": torch.randn(P, 3, generator=g)}
+        total = ((rv["means3D"] * ups["g_means"]).sum() + (rv["rotations"] * ups["g_rot"]).sum()
+                 + (rv["opacities"] * ups["g_opac"]).sum() + (rv["scales"] * ups["g_scales"]).sum()
+                 + (dv["colors_precomp"] * ups["g_dcol"]).sum())
+        total.backward()
+        name = "iso" if iso else "aniso"
+        np.savez(os.path.join(OUT, f"glue_map_transform_{name}.npz"),
+                 **{f"param_{k}": v.detach().numpy() for k, v in params.items()},
+                 **{k: v.numpy() for k, v in ups.items()}, time_idx=2, w2c=w2c.astype(np.float32),
+                 **{f"grad_{k}": params[k].grad.numpy()
+                    for k in ("means3D", "unnorm_rotations", "logit_opacities", "log_scales")})
+
     # ---- ABI capture: forward + backward through the reference autograd wrapper
     st = ref.GaussianRasterizationSettings(
         image_height=48, image_width=64, tanfovx=1.0, tanfovy=0.75, bg=torch.zeros(3), scale_modifier=1.0,

@@ -57,3 +57,61 @@ def test_synthetic_scene_is_seeded_and_in_frustum():
     z = a.means3D[:, 2]
     u = a.means3D[:, 0] / z * c.fx + c.cx
     assert float(z.min()) >= 0.5 and float(u.min()) > -1 and float(u.max()) < c.W + 1
+
+
+# ------------------------------------------------------------------ mapping --
+def test_calc_ssim_matches_reference():
+    g = np.load(os.path.join(GOLD, "glue_ssim.npz"))
+    img1 = torch.tensor(g["img1"], requires_grad=True)
+    s = slam.calc_ssim(img1, torch.tensor(g["img2"]))
+    s.backward()
+    np.testing.assert_allclose(float(s), float(g["ssim"]), rtol=1e-6)
+    np.testing.assert_allclose(img1.grad.numpy(), g["grad_img1"], rtol=1e-4, atol=1e-10)
+
+
+def _ssim_grad_by_partial_maps(x, y, win):
+    """The HIP map_loss kernels' factorisation (csrc/gsr_mapping.hip): per-pixel partials
+    dS/dmu1, dS/dE[x^2], dS/dE[xy], blurred back with the same zero-padded window."""
+    C = x.shape[0]
+    k2 = (win[:, None] * win[None, :]).to(x.dtype)  # float32 outer product, like create_window
+    w = k2.expand(C, 1, 11, 11)
+    conv = lambda t: torch.nn.functional.conv2d(t, w, padding=5, groups=C)  # noqa: E731
+    mu1, mu2, e11, e22, e12 = conv(x), conv(y), conv(x * x), conv(y * y), conv(x * y)
+    s11, s22, s12 = e11 - mu1 * mu1, e22 - mu2 * mu2, e12 - mu1 * mu2
+    A, B = 2 * mu1 * mu2 + 1e-4, 2 * s12 + 9e-4
+    Cc, D = mu1 * mu1 + mu2 * mu2 + 1e-4, s11 + s22 + 9e-4
+    s = A * B / (Cc * D)
+    g0 = 2 * mu2 * (B - A) / (Cc * D) - 2 * mu1 * s * (1 / Cc - 1 / D)
+    g1 = -s / D
+    g2 = 2 * A / (Cc * D)
+    n = s.numel()
+    return s.mean(), (conv(g0) + 2 * x * conv(g1) + y * conv(g2)) / n
+
+
+def test_ssim_partial_map_factorisation_equals_autograd():
+    gen = torch.Generator().manual_seed(5)
+    x = torch.rand(3, 29, 41, generator=gen, dtype=torch.float64, requires_grad=True)
+    y = torch.rand(3, 29, 41, generator=gen, dtype=torch.float64)
+    win = slam._gaussian(11, 1.5)
+    ref = slam.calc_ssim(x, y)
+    ref.backward()
+    s, grad = _ssim_grad_by_partial_maps(x.detach(), y, win)
+    assert abs(float(s) - float(ref)) < 1e-12
+    np.testing.assert_allclose(grad.numpy(), x.grad.numpy(), rtol=1e-9, atol=1e-13)
+
+
+def test_mapping_transform_gradients_match_reference():
+    for name in ("iso", "aniso"):
+        g = np.load(os.path.join(GOLD, f"glue_map_transform_{name}.npz"))
+        params = _params(g)
+        for k in ("means3D", "rgb_colors", "unnorm_rotations", "logit_opacities", "log_scales"):
+            params[k].requires_grad_(True)
+        tg = slam.transform_to_frame(params, int(g["time_idx"]), gaussians_grad=True, camera_grad=False, fast=False)
+        rv = slam.transformed_params2rendervar(params, tg)
+        dv = slam.transformed_params2depthplussilhouette(params, torch.tensor(g["w2c"]), tg, fast=False)
+        total = sum((rv[k] * torch.tensor(g[u])).sum() for k, u in (("means3D", "g_means"), ("rotations", "g_rot"),
+                                                                     ("opacities", "g_opac"), ("scales", "g_scales")))
+        total = total + (dv["colors_precomp"] * torch.tensor(g["g_dcol"])).sum()
+        total.backward()
+        for k in ("means3D", "unnorm_rotations", "logit_opacities", "log_scales"):
+            np.testing.assert_allclose(params[k].grad.numpy(), g[f"grad_{k}"], rtol=1e-4, atol=1e-6, err_msg=k)

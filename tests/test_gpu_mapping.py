@@ -1,0 +1,228 @@
+"""SplaTAM mapping iteration on the GPU (include/gsr_glue.h mapping entry points):
+the fused SSIM/L1 loss kernels, the mapping transform backward, the fused Adam
+step and the whole fused iteration against the literal restatement of
+scripts/splatam.py:220-353 (mapping=True) in splatam_amd.slam, whose torch glue
+is itself pinned to the reference's utils/*.py by tests/test_glue_cpu.py."""
+import pytest
+import torch
+
+from splatam_amd import slam
+from splatam_amd.glue import FusedAdam, MapAdam, map_transform, mapping_loss
+from splatam_amd.rasterizer import GaussianRasterizer
+from splatam_amd.scenes import make_scene
+
+pytestmark = pytest.mark.gpu
+
+GAUSS_KEYS = ("means3D", "unnorm_rotations", "logit_opacities", "log_scales")
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+
+
+def _images(cuda, H, W, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    im = torch.rand(3, H, W, generator=g)
+    gt = (im + 0.2 * torch.randn(3, H, W, generator=g)).clamp(0, 1)
+    ds = torch.stack([0.5 + 4 * torch.rand(H, W, generator=g), torch.rand(H, W, generator=g),
+                      torch.zeros(H, W)])
+    ds[2] = ds[0] * ds[0] + 0.01 * torch.rand(H, W, generator=g)
+    gd = (ds[0:1] + 0.3 * torch.randn(1, H, W, generator=g)).clamp_min(0)
+    gd[:, :, : W // 7] = 0.0                       # invalid depth stripe
+    ds[0, 3, 5] = float("nan")                     # a NaN depth pixel is masked out
+    return [t.to(cuda) for t in (im, ds, gt, gd)]
+
+
+def _literal_loss(im, ds, gt, gd, w_im=0.5, w_depth=1.0):
+    depth, dsq = ds[0:1], ds[2:3]
+    unc = (dsq - depth ** 2).detach()
+    mask = ((gd > 0) & ~torch.isnan(depth) & ~torch.isnan(unc)).detach()
+    l_d = torch.abs(gd - depth)[mask].mean()
+    l_im = 0.8 * slam.l1_loss_v1(im, gt) + 0.2 * (1.0 - slam.calc_ssim(im, gt))
+    return w_im * l_im + w_depth * l_d
+
+
+@pytest.mark.parametrize("hw", [(70, 150), (16, 64), (5, 7), (480, 640)])
+def test_mapping_loss_kernel_matches_literal(cuda, hw):
+    """Loss and both image gradients vs the literal torch expression in float64
+    (float32 kernel: loss within 1e-5 relative, gradients within 1e-5 relative L2)."""
+    H, W = hw
+    im, ds, gt, gd = _images(cuda, H, W)
+    a_im, a_ds = im.clone().requires_grad_(True), ds.clone().requires_grad_(True)
+    loss = mapping_loss(a_im, a_ds, gt, gd)
+    loss.backward()
+    r_im, r_ds = im.double().requires_grad_(True), ds.double().requires_grad_(True)
+    ref = _literal_loss(r_im, r_ds, gt.double(), gd.double())
+    ref.backward()
+    assert abs(float(loss) - float(ref)) <= 1e-5 * abs(float(ref)), (float(loss), float(ref))
+    assert _rel(a_im.grad, r_im.grad) <= 1e-5
+    g_ds = torch.nan_to_num(r_ds.grad, nan=0.0)
+    assert _rel(a_ds.grad, g_ds) <= 1e-6
+    assert float(a_ds.grad[1:].abs().sum()) == 0.0
+
+
+def test_mapping_loss_empty_depth_mask(cuda):
+    """No valid depth: the masked mean is NaN (torch's mean of an empty selection) and
+    the depth gradient is zero; the image gradient stays finite."""
+    im, ds, gt, gd = _images(cuda, 40, 70)
+    gd.zero_()
+    a_im, a_ds = im.clone().requires_grad_(True), ds.clone().requires_grad_(True)
+    loss = mapping_loss(a_im, a_ds, gt, gd)
+    loss.backward()
+    assert torch.isnan(loss)
+    assert float(a_ds.grad.abs().sum()) == 0.0 and bool(torch.isfinite(a_im.grad).all())
+
+
+def test_mapping_loss_deterministic(cuda):
+    im, ds, gt, gd = _images(cuda, 480, 640, seed=3)
+    outs = []
+    for _ in range(2):
+        a = im.clone().requires_grad_(True)
+        loss = mapping_loss(a, ds, gt, gd)
+        loss.backward()
+        outs.append((loss.item(), a.grad.clone()))
+    assert outs[0][0] == outs[1][0] and torch.equal(outs[0][1], outs[1][1])
+
+
+def _map_params(cuda, aniso, sh, P=3000, W=150, H=110, seed=3):
+    scene = make_scene(P, W, H, seed=seed, anisotropic=aniso, sh_degree=3 if sh else 0)
+    params = slam.init_mapping_params(scene, num_frames=3, device=cuda)
+    cam = slam.camera_settings(scene.cam, cuda, sh_degree=scene.sh_degree)
+    return scene, params, cam
+
+
+@pytest.mark.parametrize("aniso", [False, True])
+def test_map_transform_bwd_matches_autograd(cuda, aniso):
+    """gsr_map_transform_bwd vs autograd through the literal transform_to_frame + builders (float64)."""
+    _, params, _ = _map_params(cuda, aniso, False)
+    w2c = torch.eye(4, device=cuda)
+    w2c[:3, 3] = torch.tensor([0.05, -0.02, 0.1], device=cuda)
+    P = params["means3D"].shape[0]
+    g = torch.Generator().manual_seed(9)
+    ups = [torch.randn(P, n, generator=g).to(cuda) for n in (3, 4, 3, 1, 3)]
+    leaves = {k: params[k].clone().requires_grad_(True) for k in GAUSS_KEYS + ("rgb_colors",)}
+    p = dict(params, **leaves)
+    outs = map_transform(p, 2, w2c)
+    total = sum((o * u).sum() for o, u in zip(outs[:5], ups))
+    total.backward()
+    ref = {k: v.detach().double().requires_grad_(True) for k, v in params.items() if k in leaves}
+    pr = dict({k: v.double() for k, v in params.items()}, **ref)
+    tg = slam.transform_to_frame(pr, 2, gaussians_grad=True, camera_grad=False, fast=False)
+    rv = slam.transformed_params2rendervar(pr, tg)
+    dv = slam.transformed_params2depthplussilhouette(pr, w2c.double(), tg, fast=False)
+    outs_ref = (rv["means3D"], rv["rotations"], dv["colors_precomp"], rv["opacities"], rv["scales"])
+    for o, r in zip(outs, outs_ref):
+        assert _rel(o.detach(), r.detach()) <= 1e-6
+    sum((o * u.double()).sum() for o, u in zip(outs_ref, ups)).backward()
+    for k in GAUSS_KEYS:
+        assert _rel(leaves[k].grad, ref[k].grad) <= 1e-5, k
+
+
+def _scene_targets(params, cam, cuda):
+    """Targets rendered at the unperturbed pose with perturbed colours (so the loss is not ~0)."""
+    with torch.no_grad():
+        gt = dict(params)
+        gt["cam_unnorm_rots"] = torch.zeros_like(params["cam_unnorm_rots"])
+        gt["cam_unnorm_rots"][0, 0] = 1.0
+        gt["cam_trans"] = torch.zeros_like(params["cam_trans"])
+        key = slam.color_key(params)
+        gt[key] = params[key] * 0.8 + 0.05
+        tg = slam.transform_to_frame(gt, 1, False, False)
+        rv = slam._rendervar_colors(gt, slam.transformed_params2rendervar(gt, tg))
+        w2c = torch.eye(4, device=cuda)
+        im, _, _ = GaussianRasterizer(cam)(**rv)
+        ds, _, _ = GaussianRasterizer(cam)(**slam.transformed_params2depthplussilhouette(gt, w2c, tg))
+        gd = ds[0:1].clone()
+        gd[:, :, :7] = 0.0
+    return {"cam": cam, "w2c": w2c, "im": im.clamp(0, 1), "depth": gd}
+
+
+def _loss_and_grads(params, curr, fused):
+    p = dict(params)
+    key = slam.color_key(params)
+    for k in GAUSS_KEYS + (key,):
+        p[k] = params[k].detach().clone().requires_grad_(True)
+    loss, radius, _ = slam.get_loss_mapping(p, curr, 1, fused=fused)
+    loss.backward()
+    return loss.item(), {k: p[k].grad for k in GAUSS_KEYS + (key,)}, radius
+
+
+@pytest.mark.parametrize("aniso,sh", [(False, False), (True, False), (True, True)])
+def test_get_loss_mapping_fused_equals_literal(cuda, aniso, sh):
+    """Fused mapping iteration (HIP transform, dual render, fused SSIM/L1) vs the
+    literal one (torch glue, two GaussianRasterizer calls, conv2d SSIM): loss within
+    1e-5 relative, every Gaussian gradient within 1e-4 relative L2."""
+    _, params, cam = _map_params(cuda, aniso, sh)
+    curr = _scene_targets(params, cam, cuda)
+    assert slam.fused_mapping_eligible(params, curr, slam.MappingConfig())
+    l0, g0, r0 = _loss_and_grads(params, curr, fused=False)
+    l1, g1, r1 = _loss_and_grads(params, curr, fused=True)
+    assert abs(l0 - l1) <= 1e-5 * abs(l0), (l0, l1)
+    assert float((r0 == r1).float().mean()) >= 0.999
+    for k in g0:
+        assert float(g0[k].abs().sum()) > 0.0, k
+        assert _rel(g1[k], g0[k]) <= 1e-4, (k, _rel(g1[k], g0[k]))
+
+
+def test_fused_adam_matches_torch(cuda):
+    """FusedAdam (gsr_adam_step) vs torch.optim.Adam over 5 steps: several groups, sizes
+    that are not multiples of 4, a 16-byte-misaligned tensor (scalar path), eps 1e-15."""
+    g = torch.Generator().manual_seed(1)
+    base = torch.randn(10001, generator=g).to(cuda)
+    shapes = {"a": (1000, 3), "b": (777,), "c": (33, 16, 3), "d": None}
+    ps = {k: torch.randn(*s, generator=g).to(cuda) for k, s in shapes.items() if s}
+    ps["d"] = base[1:5001]  # misaligned view (contiguous)
+    lrs = {"a": 1e-4, "b": 0.05, "c": 0.0025, "d": 0.001}
+    mine = {k: v.clone() for k, v in ps.items()}
+    ref = {k: v.clone() for k, v in ps.items()}
+    opt_m = FusedAdam([{"params": [mine[k]], "lr": lrs[k]} for k in ps], lr=0.0, eps=1e-15)
+    opt_r = torch.optim.Adam([{"params": [ref[k]], "lr": lrs[k]} for k in ps], lr=0.0, eps=1e-15)
+    for s in range(5):
+        for k in ps:
+            gr = torch.randn(ps[k].shape, generator=g).to(cuda) * (10.0 ** (s - 2))
+            mine[k].grad, ref[k].grad = gr.clone(), gr.clone()
+        opt_m.step()
+        opt_r.step()
+    for k in ps:
+        torch.testing.assert_close(mine[k], ref[k], rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(opt_m.state[mine[k]]["exp_avg_sq"], opt_r.state[ref[k]]["exp_avg_sq"],
+                                   rtol=1e-6, atol=1e-12)
+        assert float(opt_m.state[mine[k]]["step"]) == 5.0
+
+
+@pytest.mark.parametrize("sh", [False, True])
+def test_fused_map_adam_follows_eager_optimizer(cuda, sh):
+    """Three fused mapping iterations with the Adam step inside the transform backward
+    (MapAdam) follow three fused iterations whose .grad is stepped by torch.optim.Adam
+    (mapping lrs, eps 1e-15).  The first step sees bitwise-equal gradients; later steps
+    start from parameters one rounding apart, and with eps = 1e-15 an element whose
+    gradient is pure rounding noise may step with the other sign (2 lr apart)."""
+    _, params, cam = _map_params(cuda, True, sh)
+    curr = _scene_targets(params, cam, cuda)
+    cfg = slam.MappingConfig()
+    key = slam.color_key(params)
+    keys = GAUSS_KEYS + (key,)
+    fused_p = {k: v.clone() for k, v in params.items()}
+    adam = MapAdam(fused_p, cfg.lrs, color_key=key)
+    eager_p = {k: v.clone() for k, v in params.items()}
+    for k in keys:
+        eager_p[k].requires_grad_(True)
+    opt = torch.optim.Adam([{"params": [eager_p[k]], "lr": cfg.lrs[k]} for k in keys], lr=0.0, eps=1e-15)
+    for it in range(3):
+        loss, _, _ = slam.get_loss_mapping(fused_p, curr, 1, cfg, fused=True, adam=adam)
+        loss.backward()
+        opt.zero_grad(set_to_none=True)
+        loss_e, _, _ = slam.get_loss_mapping(eager_p, curr, 1, cfg, fused=True)
+        loss_e.backward()
+        opt.step()
+        if it == 0:
+            for k in keys:
+                torch.testing.assert_close(fused_p[k], eager_p[k].detach(), rtol=1e-6, atol=1e-7)
+    assert adam.step == 3
+    for k in keys:
+        moved = (eager_p[k].detach() - params[k]).abs()
+        assert float(moved.max()) > 0.0, k
+        err = (fused_p[k] - eager_p[k].detach()).abs()
+        close = err <= 1e-6 * params[k].abs() + 1e-7
+        assert float(close.float().mean()) >= 0.999, (k, float(close.float().mean()))
+        assert float(err.max()) <= 6.0 * cfg.lrs[k] + 1e-6, k
