@@ -49,7 +49,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--config", type=int, default=None, help="BASELINE config (default: 3 tracking, 4 mapping)")
+    ap.add_argument("--workload", choices=("tracking", "mapping"), default="tracking",
+                    help="tracking: the headline metric (config 3); mapping: SplaTAM mapping iterations "
+                         "(config 4: 1M anisotropic Gaussians, SH degree 3, 1200x680)")
+    ap.add_argument("--keyframes", type=int, default=4, help="mapping: keyframes in the window")
     ap.add_argument("--bcast-every", type=int, default=40,
                     help="broadcast the Gaussian map every k steps (Replica: 40 tracking iters/frame)")
     ap.add_argument("--cpu-baseline", choices=("auto", "on", "off"), default="auto")
@@ -84,6 +88,10 @@ def main():
     world, rank, local = setup_dist(args)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.config is None:
+        args.config = 4 if args.workload == "mapping" else 3
+    if args.workload == "mapping":
+        return main_mapping(args, world, rank, dev)
 
     from splatam_amd import profiling
     from splatam_amd.scenes import config_scene
@@ -250,6 +258,108 @@ def main():
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items()},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def render_bwd_roofline(rb, I_avg, P, W, H, graph: bool):
+    """SURVEY.md 8(d) algorithmic bytes of one dual render-backward launch over its measured duration."""
+    Tt = ((W + 15) // 16) * ((H + 15) // 16)
+    N = W * H
+    # 8*Tt + 40*I + 20*N + 44*P per rasterization, for the dual launch (both colour sets):
+    # + colors2 gather 12*I, + dL_dpix2 12*N, + dcolors2 12*P
+    bytes_per_launch = 8 * Tt + 52 * I_avg + 32 * N + 56 * P
+    dur_s = rb["avg_us"] * 1e-6
+    achieved = bytes_per_launch / dur_s / 1e9 if dur_s > 0 else 0.0
+    return {"kernel": "render_bwd_kernel", "bound": "hbm", "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": None, "alg_bytes_per_launch": int(bytes_per_launch), "avg_us": round(rb["avg_us"], 2),
+            "num_rendered_avg": int(I_avg), "launches_timed": int(rb["launches"]),
+            "timing": "in-kernel wall_clock64 (first workgroup start to last workgroup end) of every launch in "
+                      "the timed HIP-graph replays" if graph else "hipEvents around each launch"}
+
+
+def main_mapping(args, world, rank, dev):
+    """SplaTAM mapping iterations (scripts/splatam.py:842-905, get_loss mapping=True): one step = one
+    iteration = transform + RGB(SH) and depth/silhouette render fwd+bwd (one dual rasterization) +
+    0.8 L1 + 0.2 (1 - SSIM) + masked depth L1 + Adam on every Gaussian parameter; replayed as a HIP
+    graph of --iters-per-graph iterations (one frame's mapping with a fresh optimizer), keyframes drawn
+    from a window of --keyframes synthetic frames.  Frame-sharded over ranks like tracking."""
+    from splatam_amd import dist as sd
+    from splatam_amd import profiling
+    from splatam_amd.mapper import GraphMapper
+    from splatam_amd.rasterizer import GaussianRasterizer
+    from splatam_amd.scenes import config_scene
+    from splatam_amd.slam import MappingConfig, _rendervar_colors, camera_settings, color_key, \
+        init_mapping_params, transform_to_frame, transformed_params2depthplussilhouette, \
+        transformed_params2rendervar
+
+    scene = config_scene(args.config)
+    P, W, H = scene.P, scene.cam.W, scene.cam.H
+    K = max(1, args.keyframes)
+    params = init_mapping_params(scene, num_frames=K * max(world, 1), device=dev)
+    sd.broadcast_map(params, keys=tuple(k for k in params))
+    cam = camera_settings(scene.cam, dev, sh_degree=scene.sh_degree)
+    w2c = torch.eye(4, device=dev)
+    key = color_key(params)
+    # keyframe targets: the map with perturbed colours rendered at each keyframe's pose
+    g = torch.Generator().manual_seed(1234)
+    kfs = []
+    with torch.no_grad():
+        truth = dict(params)
+        truth[key] = params[key] * 0.9 + 0.05 * torch.rand(params[key].shape, generator=g).to(dev)
+        for j in range(K):
+            t = rank * K + j
+            tg = transform_to_frame(truth, t, False, False)
+            im, _, _ = GaussianRasterizer(cam)(**_rendervar_colors(truth, transformed_params2rendervar(truth, tg)))
+            ds, _, _ = GaussianRasterizer(cam)(**transformed_params2depthplussilhouette(truth, w2c, tg))
+            kfs.append({"cam": cam, "w2c": w2c, "im": im.clamp(0, 1), "depth": ds[0:1].clone(), "id": t})
+        del truth
+    for k in ("means3D", "unnorm_rotations", "logit_opacities", "log_scales", key):
+        params[k].requires_grad_(True)
+    S = max(1, min(args.iters_per_graph, args.steps))
+    steps = -(-args.steps // S) * S
+    mapper = GraphMapper(params, kfs, iters_per_graph=S, cfg=MappingConfig(), timing=bool(args.timing))
+    for _ in range(max(1, args.warmup // S)):
+        mapper.run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    profiling.enable_timing(clock_stages=("render_bwd",))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps // S):
+        mapper.run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    stages = profiling.read_timing()
+    profiling.enable_timing(False)
+    if mapper.overflowed():
+        raise SystemExit(f"binning capacity overflow during the timed replays (capacity {mapper.capacity}): "
+                         "measurement invalid")
+    elapsed = sd.max_over_ranks(t1 - t0, device=dev)
+    value = steps * world / elapsed
+    nr = mapper.num_rendered()
+    roofline = render_bwd_roofline(stages["render_bwd"], sum(nr) / len(nr), P, W, H, graph=True)
+    if rank == 0:
+        line = {
+            "metric": f"mapping iterations/sec @{W}x{H}, {P // 1000}k anisotropic Gaussians, SH degree "
+                      f"{scene.sh_degree}", "value": round(value, 3), "unit": "iterations/s", "n_gpus": world,
+            "steps": steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "execution": f"HIP graph of {S} mapping iterations (one frame, fresh Adam), replayed; binning "
+                         f"capacity {mapper.capacity}, no overflow",
+            "data": f"synthetic (SURVEY.md 8(d) seeded scene; {K} keyframe targets rendered from a perturbed map)",
+            "config": {"workload": f"config {args.config}: {P} Gaussians, {W}x{H}, SplaTAM mapping iteration "
+                                   "(SH colour + depth/silhouette render fwd+bwd, L1 + SSIM + depth L1, Adam on "
+                                   "all Gaussian parameters)", "gaussians": P, "width": W, "height": H,
+                       "keyframes": K, "parallelism": f"frame-sharded x{world}"},
+            "roofline": roofline,
             "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items()},
         }
         print(json.dumps(line), flush=True)

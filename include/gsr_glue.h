@@ -65,14 +65,15 @@ int gsr_track_transform_bwd(int P, const float* means_world, const float* unnorm
  * instead of writing the pose gradient, applies torch.optim.Adam (no weight
  * decay, no amsgrad; the tracking optimizer of scripts/splatam.py) to the
  * frame's pose column in place: cam_q (4 values) / cam_t (3 values) at stride
- * q_stride.  adam_state: device, 15 floats [m_q 4, v_q 4, m_t 3, v_t 3, step],
+ * q_stride.  Hyperparameters are doubles (torch's are python floats: 1 - beta2
+ * rounded from a float beta2 would be 1.3e-5 off).  adam_state: device, 15 floats [m_q 4, v_q 4, m_t 3, v_t 3, step],
  * zero-initialised by the caller per frame (SplaTAM re-creates the optimizer per
  * frame). */
 int gsr_track_transform_bwd_adam(int P, const float* means_world, const float* unnorm_rot, int scale_cols,
                                  float* cam_q, float* cam_t, int q_stride, const float* means_cam,
                                  const float* w2c, const float* dL_dmeans_cam, const float* dL_drot,
-                                 const float* dL_ddepth_colors, float lr_q, float lr_t, float beta1,
-                                 float beta2, float eps, float* adam_state, float* scratch, void* stream);
+                                 const float* dL_ddepth_colors, double lr_q, double lr_t, double beta1,
+                                 double beta2, double eps, float* adam_state, float* scratch, void* stream);
 
 /* im [3,H,W], depth_sil [3,H,W] (depth, silhouette, depth^2), gt_im [3,H,W], gt_depth [1,H,W].
  * loss: 1 float (device).  scratch: gsr_track_scratch_floats(H*W) floats. */
@@ -138,9 +139,9 @@ int gsr_map_transform_bwd(int P, const float* unnorm_rot, const float* logit_opa
 typedef struct gsr_map_adam {
     float* exp_avg[5];
     float* exp_avg_sq[5];
-    float lr[5];
+    double lr[5];
     int step;
-    float beta1, beta2, eps;
+    double beta1, beta2, eps;
 } gsr_map_adam;
 
 /* gsr_map_transform_bwd with the optimizer step fused in: the parameters are
@@ -163,9 +164,9 @@ typedef struct gsr_adam_tensor {
     float* exp_avg;
     float* exp_avg_sq;
     long long n;
-    float lr;
+    double lr;
 } gsr_adam_tensor;
-int gsr_adam_step(int n_tensors, const gsr_adam_tensor* tensors, int step, float beta1, float beta2, float eps,
+int gsr_adam_step(int n_tensors, const gsr_adam_tensor* tensors, int step, double beta1, double beta2, double eps,
                   void* stream);
 
 #ifdef __cplusplus

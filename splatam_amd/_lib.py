@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSR_LIB", os.path.join(_HERE, "libgsr.so"))
 
 c_int, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+c_double = ctypes.c_double
 
 
 class GsrSettings(ctypes.Structure):
@@ -35,14 +36,14 @@ class GsrGrads(ctypes.Structure):
 
 class GsrMapAdam(ctypes.Structure):
     """gsr_map_adam (include/gsr_glue.h)."""
-    _fields_ = [("exp_avg", c_void_p * 5), ("exp_avg_sq", c_void_p * 5), ("lr", c_float * 5), ("step", c_int),
-                ("beta1", c_float), ("beta2", c_float), ("eps", c_float)]
+    _fields_ = [("exp_avg", c_void_p * 5), ("exp_avg_sq", c_void_p * 5), ("lr", c_double * 5), ("step", c_int),
+                ("beta1", c_double), ("beta2", c_double), ("eps", c_double)]
 
 
 class GsrAdamTensor(ctypes.Structure):
     """gsr_adam_tensor (include/gsr_glue.h)."""
     _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
-                ("n", ctypes.c_longlong), ("lr", c_float)]
+                ("n", ctypes.c_longlong), ("lr", c_double)]
 
 
 ALLOC_FN = ctypes.CFUNCTYPE(c_void_p, c_void_p, c_int, c_size_t)
@@ -78,9 +79,8 @@ SIGNATURES = {
     "gsr_track_transform_bwd": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "gsr_track_transform_bwd_adam": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                                             c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.c_float,
-                                             ctypes.c_float, ctypes.c_float, ctypes.c_float, c_void_p, c_void_p,
-                                             c_void_p]),
+                                             c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_double,
+                                             c_double, c_double, c_double, c_void_p, c_void_p, c_void_p]),
     "gsr_track_l1_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
                                  ctypes.c_float, ctypes.c_float, c_void_p, c_void_p, c_void_p]),
     "gsr_track_l1_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
@@ -101,7 +101,7 @@ SIGNATURES = {
     "gsr_map_transform_bwd_adam": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                                            c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                            c_void_p, c_void_p, c_void_p, ctypes.POINTER(GsrMapAdam), c_void_p]),
-    "gsr_adam_step": (c_int, [c_int, ctypes.POINTER(GsrAdamTensor), c_int, c_float, c_float, c_float, c_void_p]),
+    "gsr_adam_step": (c_int, [c_int, ctypes.POINTER(GsrAdamTensor), c_int, c_double, c_double, c_double, c_void_p]),
 }
 
 

@@ -59,20 +59,23 @@ track_transform_fwd_kernel(int P, const float* __restrict__ mw, const float* __r
 }
 
 struct PoseAdam {  // torch.optim.Adam (no weight decay, no amsgrad) on the frame's pose column
-    float lr_q, lr_t, beta1, beta2, eps;
+    double lr_q, lr_t, beta1, beta2;   // torch's hyperparameters are python floats (double)
+    float w1, omb2, eps;               // 1 - beta1, 1 - beta2 rounded from double, like torch's scalars
     float* state;     // device: m_q[4], v_q[4], m_t[3], v_t[3], step
     float* q;         // the frame's quaternion column (stride qs), updated in place
     float* t;         // the frame's translation column (stride qs)
 };
 
-// exp_avg = b1 m + (1-b1) g; exp_avg_sq = b2 v + (1-b2) g^2;
-// p -= lr / (1 - b1^s) * m / (sqrt(v) / sqrt(1 - b2^s) + eps)
-__device__ __forceinline__ void adam_update(float& p, float g, float& m, float& v, float lr, const PoseAdam& a,
-                                            float bc1, float bc2_sqrt) {
-    m = a.beta1 * m + (1.f - a.beta1) * g;
-    v = a.beta2 * v + (1.f - a.beta2) * g * g;
+// torch/optim/adam.py (foreach form): exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
+// p.addcdiv_(exp_avg, sqrt(exp_avg_sq) / sqrt(1 - b2^s) + eps, -lr / (1 - b1^s)), the scalars
+// formed in double like torch's python floats.
+__device__ __forceinline__ void adam_update(float& p, float g, float& m, float& v, float neg_step, const PoseAdam& a,
+                                            float bc2_sqrt) {
+    m = m + a.w1 * (g - m);                      // exp_avg.lerp_(g, 1 - beta1)
+    v = v * (float)a.beta2;                      // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+    v = v + a.omb2 * g * g;
     const float denom = sqrtf(v) / bc2_sqrt + a.eps;
-    p -= (lr / bc1) * (m / denom);
+    p = p + neg_step * (m / denom);
 }
 
 // The pose chain on the 16 summed terms S: dR -> dn (build_rotation) -> dc
@@ -97,10 +100,12 @@ __device__ void pose_fin(const float* S, const float* cq, int qs, float* dq, flo
         float* st = adam.state;
         const float step = st[14] + 1.f;
         st[14] = step;
-        const float bc1 = 1.f - powf(adam.beta1, step), bc2_sqrt = sqrtf(1.f - powf(adam.beta2, step));
+        const double bc1 = 1.0 - pow(adam.beta1, (double)step);
+        const float bc2_sqrt = (float)sqrt(1.0 - pow(adam.beta2, (double)step));
+        const float ss_q = (float)(-adam.lr_q / bc1), ss_t = (float)(-adam.lr_t / bc1);
         const float gq[4] = {g.x, g.y, g.z, g.w};
-        for (int k = 0; k < 4; k++) adam_update(adam.q[k * qs], gq[k], st[k], st[4 + k], adam.lr_q, adam, bc1, bc2_sqrt);
-        for (int k = 0; k < 3; k++) adam_update(adam.t[k * qs], S[k], st[8 + k], st[11 + k], adam.lr_t, adam, bc1, bc2_sqrt);
+        for (int k = 0; k < 4; k++) adam_update(adam.q[k * qs], gq[k], st[k], st[4 + k], ss_q, adam, bc2_sqrt);
+        for (int k = 0; k < 3; k++) adam_update(adam.t[k * qs], S[k], st[8 + k], st[11 + k], ss_t, adam, bc2_sqrt);
         return;
     }
     dq[0] = g.x; dq[qs] = g.y; dq[2 * qs] = g.z; dq[3 * qs] = g.w;
@@ -277,7 +282,7 @@ int gsr_track_transform_bwd(int P, const float* means_world, const float* unnorm
     hipLaunchKernelGGL(track_transform_bwd_kernel, dim3(pose_blocks(P)), dim3(GLUE_BLOCK), 0, (hipStream_t)stream, P,
                        means_world, unnorm_rot, scale_cols, cam_q, q_stride, means_cam, w2c, dL_dmeans_cam, dL_drot,
                        dL_ddepth_colors, scratch, dL_dcam_q, dL_dcam_t,
-                       PoseAdam{0.f, 0.f, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr});
+                       PoseAdam{0.0, 0.0, 0.0, 0.0, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr});
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GSR_OK : hip_fail(e, "track_transform_bwd");
 }
@@ -285,7 +290,7 @@ int gsr_track_transform_bwd(int P, const float* means_world, const float* unnorm
 int gsr_track_transform_bwd_adam(int P, const float* means_world, const float* unnorm_rot, int scale_cols,
                                  float* cam_q, float* cam_t, int q_stride, const float* means_cam, const float* w2c,
                                  const float* dL_dmeans_cam, const float* dL_drot, const float* dL_ddepth_colors,
-                                 float lr_q, float lr_t, float beta1, float beta2, float eps, float* adam_state,
+                                 double lr_q, double lr_t, double beta1, double beta2, double eps, float* adam_state,
                                  float* scratch, void* stream) {
     if (P < 0 || (scale_cols != 1 && scale_cols != 3) || q_stride < 1)
         return fail(GSR_ERR_INVALID_ARG, "track_transform_bwd_adam: bad sizes");
@@ -295,7 +300,8 @@ int gsr_track_transform_bwd_adam(int P, const float* means_world, const float* u
     hipLaunchKernelGGL(track_transform_bwd_kernel, dim3(pose_blocks(P)), dim3(GLUE_BLOCK), 0, (hipStream_t)stream, P,
                        means_world, unnorm_rot, scale_cols, cam_q, q_stride, means_cam, w2c, dL_dmeans_cam, dL_drot,
                        dL_ddepth_colors, scratch, nullptr, nullptr,
-                       PoseAdam{lr_q, lr_t, beta1, beta2, eps, adam_state, cam_q, cam_t});
+                       PoseAdam{lr_q, lr_t, beta1, beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
+                                adam_state, cam_q, cam_t});
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GSR_OK : hip_fail(e, "track_transform_bwd_adam");
 }

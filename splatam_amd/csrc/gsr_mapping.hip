@@ -436,13 +436,14 @@ int map_loss_blocks(int H, int W, dim3& grid) {
     return (int)(grid.x * grid.y * grid.z);
 }
 
-void fill_adam_common(float beta1, float beta2, float eps, int step, float& w1, float& b2, float& omb2,
+// torch forms these scalars from python floats (double) and rounds them to float in the kernels
+void fill_adam_common(double beta1, double beta2, double eps, int step, float& w1, float& b2, float& omb2,
                       float& bc2_sqrt, float& e) {
-    w1 = (float)(1.0 - (double)beta1);
-    b2 = beta2;
-    omb2 = (float)(1.0 - (double)beta2);
-    bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, (double)step));
-    e = eps;
+    w1 = (float)(1.0 - beta1);
+    b2 = (float)beta2;
+    omb2 = (float)(1.0 - beta2);
+    bc2_sqrt = (float)sqrt(1.0 - pow(beta2, (double)step));
+    e = (float)eps;
 }
 
 }  // namespace
@@ -524,12 +525,12 @@ int gsr_map_transform_bwd_adam(int P, float* means_world, float* unnorm_rot, flo
             if (k < 4 || dL_dcolors) return fail(GSR_ERR_INVALID_ARG, "map_transform_bwd_adam: null optimizer state");
     MapAdam a{};
     float* ps[5] = {means_world, unnorm_rot, logit_opac, log_scales, colors};
-    const double bc1 = 1.0 - pow((double)adam->beta1, (double)adam->step);
+    const double bc1 = 1.0 - pow(adam->beta1, (double)adam->step);
     for (int k = 0; k < 5; k++) {
         a.p[k] = ps[k];
         a.m[k] = adam->exp_avg[k];
         a.v[k] = adam->exp_avg_sq[k];
-        a.step_size[k] = (float)(-(double)adam->lr[k] / bc1);
+        a.step_size[k] = (float)(-adam->lr[k] / bc1);
     }
     fill_adam_common(adam->beta1, adam->beta2, adam->eps, adam->step, a.w1, a.beta2, a.omb2, a.bc2_sqrt, a.eps);
     hipLaunchKernelGGL(map_transform_bwd_kernel, dim3((P + GLUE_BLOCK - 1) / GLUE_BLOCK), dim3(GLUE_BLOCK), 0,
@@ -540,12 +541,12 @@ int gsr_map_transform_bwd_adam(int P, float* means_world, float* unnorm_rot, flo
     return e == hipSuccess ? GSR_OK : hip_fail(e, "map_transform_bwd_adam");
 }
 
-int gsr_adam_step(int n_tensors, const gsr_adam_tensor* tensors, int step, float beta1, float beta2, float eps,
+int gsr_adam_step(int n_tensors, const gsr_adam_tensor* tensors, int step, double beta1, double beta2, double eps,
                   void* stream) {
     if (n_tensors < 0 || n_tensors > ADAM_MAX || step < 1 || (n_tensors > 0 && !tensors))
         return fail(GSR_ERR_INVALID_ARG, "adam_step: bad arguments (at most 16 tensors, step >= 1)");
     AdamArgs a{};
-    const double bc1 = 1.0 - pow((double)beta1, (double)step);
+    const double bc1 = 1.0 - pow(beta1, (double)step);
     int blocks = 0, nt = 0;
     for (int t = 0; t < n_tensors; t++) {
         const gsr_adam_tensor& x = tensors[t];
@@ -553,7 +554,7 @@ int gsr_adam_step(int n_tensors, const gsr_adam_tensor* tensors, int step, float
         if (x.n == 0) continue;
         if (!x.param || !x.grad || !x.exp_avg || !x.exp_avg_sq) return fail(GSR_ERR_INVALID_ARG, "adam_step: null pointer");
         a.p[nt] = x.param; a.g[nt] = x.grad; a.m[nt] = x.exp_avg; a.v[nt] = x.exp_avg_sq; a.n[nt] = x.n;
-        a.step_size[nt] = (float)(-(double)x.lr / bc1);
+        a.step_size[nt] = (float)(-x.lr / bc1);
         const bool al = ((uintptr_t)x.param | (uintptr_t)x.grad | (uintptr_t)x.exp_avg | (uintptr_t)x.exp_avg_sq) % 16 == 0;
         if (al) a.vec |= 1 << nt;
         a.blk0[nt] = blocks;

@@ -310,7 +310,10 @@ def map_transform(params: dict, time_idx: int, w2c: torch.Tensor, color_key: str
     + the rendervar builders (slam_helpers.py:124-139, 196-213, 234-249) for the mapping iteration.
     Returns (means3D_cam, rotations, depth_colors [z,1,z^2], opacities, scales, colours); differentiable
     w.r.t. the Gaussian parameters.  With `adam` the backward applies the mapping optimizer's step in
-    place (no .grad is produced)."""
+    place (no .grad is produced); the parameters must then require grad, or autograd never calls it."""
+    if adam is not None and not params["means3D"].requires_grad:
+        raise RuntimeError("map_transform: the fused optimizer step runs in the backward; the Gaussian "
+                           "parameters must require grad")
     return _MapTransform.apply(params["means3D"], params["unnorm_rotations"], params["logit_opacities"],
                                params["log_scales"], params[color_key], params["cam_unnorm_rots"].detach(),
                                params["cam_trans"].detach(), w2c, int(time_idx), adam)

@@ -55,8 +55,8 @@ def transform_to_frame(params, time_idx, gaussians_grad, camera_grad, fast=True)
     if not camera_grad:
         rots, trans = rots.detach(), trans.detach()
     cam_rot = F.normalize(rots)
-    dev = params["means3D"].device
-    rel_w2c = torch.eye(4, device=dev, dtype=torch.float32)
+    dev, dt = params["means3D"].device, params["means3D"].dtype
+    rel_w2c = torch.eye(4, device=dev, dtype=dt)
     rel_w2c[:3, :3] = build_rotation(cam_rot)[0]
     rel_w2c[:3, 3] = trans[0]
     pts = params["means3D"] if gaussians_grad else params["means3D"].detach()
@@ -64,7 +64,7 @@ def transform_to_frame(params, time_idx, gaussians_grad, camera_grad, fast=True)
     if fast:
         out = {"means3D": _affine(pts, rel_w2c[:3, :3], rel_w2c[:3, 3])}
     else:
-        pts4 = torch.cat((pts, torch.ones(pts.shape[0], 1, device=dev)), dim=1)
+        pts4 = torch.cat((pts, torch.ones(pts.shape[0], 1, device=dev, dtype=dt)), dim=1)
         out = {"means3D": (rel_w2c @ pts4.T).T[:, :3]}
     if params["log_scales"].shape[1] == 1:
         out["unnorm_rotations"] = unnorm
@@ -90,7 +90,7 @@ def get_depth_and_silhouette(pts_3D, w2c, fast=True):
 
 def transformed_params2rendervar(params, tg):
     """slam_helpers.py:124-139."""
-    return {"means3D": tg["means3D"], "colors_precomp": params["rgb_colors"],
+    return {"means3D": tg["means3D"], "colors_precomp": params.get("rgb_colors"),
             "rotations": F.normalize(tg["unnorm_rotations"]), "opacities": torch.sigmoid(params["logit_opacities"]),
             "scales": _scales(params),
             "means2D": torch.zeros_like(params["means3D"], requires_grad=True) + 0}
@@ -299,26 +299,34 @@ def fused_mapping_eligible(params, curr_data, cfg: MappingConfig) -> bool:
             and curr_data["im"].dim() == 3 and curr_data["depth"].dim() == 3)
 
 
+def _get_loss_mapping_fused(params, curr_data, iter_time_idx, cfg: MappingConfig, adam=None, capacity=0, status=None,
+                            means2D=None):
+    """The fused mapping iteration; capacity > 0: static-capacity rasterization (HIP-graph capturable),
+    means2D: optional caller-owned [P,3] tensor (the mapper passes a static one without grad)."""
+    from .glue import map_transform, mapping_loss
+    key = color_key(params)
+    means, rots, dcol, opac, scales, col = map_transform(params, iter_time_idx, curr_data["w2c"], key, adam)
+    if means2D is None:
+        means2D = torch.zeros(means.shape[0], 3, device=means.device, requires_grad=True)
+    sh, colors = (col, None) if key == "shs" else (None, col)
+    im, depth_sil, radius, _ = rasterize_gaussians_dual(means, means2D, sh, colors, dcol, opac, scales, rots, None,
+                                                        curr_data["cam"], capacity, status, grad2_channels=1)
+    loss = mapping_loss(im, depth_sil, curr_data["im"], curr_data["depth"], cfg.w_im, cfg.w_depth)
+    return loss, radius, means2D
+
+
 def get_loss_mapping(params, curr_data, iter_time_idx, cfg: MappingConfig = MappingConfig(), fused=True,
-                     adam=None):
+                     adam=None, loss_dtype=None):
     """scripts/splatam.py:220-353 with mapping=True, do_ba=False: two renders (RGB or SH colours, and
     [z,1,z^2]), masked mean depth L1 and 0.8 L1 + 0.2 (1 - SSIM) on the image.
 
     fused=True (and fused_mapping_eligible): the transform / rendervar builders run as
     gsr_track_transform_fwd + gsr_map_transform_bwd, both renders share one rasterization, and the
     loss is the fused SSIM/L1 kernel pair; `adam` (glue.MapAdam) then applies the mapping optimizer's
-    step inside the transform backward.  fused=False is the literal statement of the reference."""
+    step inside the transform backward.  fused=False is the literal statement of the reference
+    (loss_dtype=torch.float64 evaluates its loss terms in double: a tighter test reference)."""
     if fused and fused_mapping_eligible(params, curr_data, cfg):
-        from .glue import map_transform, mapping_loss
-        key = color_key(params)
-        means, rots, dcol, opac, scales, col = map_transform(params, iter_time_idx, curr_data["w2c"], key, adam)
-        P = means.shape[0]
-        means2D = torch.zeros(P, 3, device=means.device, requires_grad=True)
-        sh, colors = (col, None) if key == "shs" else (None, col)
-        im, depth_sil, radius, _ = rasterize_gaussians_dual(means, means2D, sh, colors, dcol, opac, scales, rots, None,
-                                                            curr_data["cam"], grad2_channels=1)
-        loss = mapping_loss(im, depth_sil, curr_data["im"], curr_data["depth"], cfg.w_im, cfg.w_depth)
-        return loss, radius, means2D
+        return _get_loss_mapping_fused(params, curr_data, iter_time_idx, cfg, adam)
     if adam is not None:
         raise RuntimeError("get_loss_mapping: the fused optimizer step needs the fused glue")
     tg = transform_to_frame(params, iter_time_idx, gaussians_grad=True, camera_grad=False, fast=False)
@@ -327,13 +335,16 @@ def get_loss_mapping(params, curr_data, iter_time_idx, cfg: MappingConfig = Mapp
     rendervar["means2D"].retain_grad()
     im, radius, _ = GaussianRasterizer(raster_settings=curr_data["cam"])(**rendervar)
     depth_sil, _, _ = GaussianRasterizer(raster_settings=curr_data["cam"])(**depth_sil_rendervar)
+    gt_im, gt_depth = curr_data["im"], curr_data["depth"]
+    if loss_dtype is not None:
+        im, depth_sil, gt_im, gt_depth = (t.to(loss_dtype) for t in (im, depth_sil, gt_im, gt_depth))
     depth = depth_sil[0, :, :].unsqueeze(0)
     depth_sq = depth_sil[2, :, :].unsqueeze(0)
     uncertainty = (depth_sq - depth ** 2).detach()
     nan_mask = (~torch.isnan(depth)) & (~torch.isnan(uncertainty))
-    mask = ((curr_data["depth"] > 0) & nan_mask).detach()
-    loss_depth = torch.abs(curr_data["depth"] - depth)[mask].mean()
-    loss_im = 0.8 * l1_loss_v1(im, curr_data["im"]) + 0.2 * (1.0 - calc_ssim(im, curr_data["im"]))
+    mask = ((gt_depth > 0) & nan_mask).detach()
+    loss_depth = torch.abs(gt_depth - depth)[mask].mean()
+    loss_im = 0.8 * l1_loss_v1(im, gt_im) + 0.2 * (1.0 - calc_ssim(im, gt_im))
     loss = cfg.w_im * loss_im + cfg.w_depth * loss_depth
     return loss, radius, rendervar["means2D"]
 

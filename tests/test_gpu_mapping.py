@@ -137,31 +137,54 @@ def _scene_targets(params, cam, cuda):
     return {"cam": cam, "w2c": w2c, "im": im.clamp(0, 1), "depth": gd}
 
 
-def _loss_and_grads(params, curr, fused):
+def _loss_and_grads(params, curr, fused, loss_dtype=None):
     p = dict(params)
     key = slam.color_key(params)
     for k in GAUSS_KEYS + (key,):
         p[k] = params[k].detach().clone().requires_grad_(True)
-    loss, radius, _ = slam.get_loss_mapping(p, curr, 1, fused=fused)
+    loss, radius, _ = slam.get_loss_mapping(p, curr, 1, fused=fused, loss_dtype=loss_dtype)
     loss.backward()
     return loss.item(), {k: p[k].grad for k in GAUSS_KEYS + (key,)}, radius
+
+
+def _rows_close(a, r, tol=1e-4):
+    """Per-Gaussian relative error of the gradient rows (per-element checks on
+    Gaussians away from thresholds) -> (fraction of rows within tol, rel L2 over those rows)."""
+    a, r = a.double().reshape(a.shape[0], -1), r.double().reshape(r.shape[0], -1)
+    rn = r.norm(dim=1)
+    row = (a - r).norm(dim=1) / (rn + 1e-3 * rn.mean() + 1e-30)
+    ok = row <= tol
+    return float(ok.float().mean()), _rel(a[ok], r[ok])
 
 
 @pytest.mark.parametrize("aniso,sh", [(False, False), (True, False), (True, True)])
 def test_get_loss_mapping_fused_equals_literal(cuda, aniso, sh):
     """Fused mapping iteration (HIP transform, dual render, fused SSIM/L1) vs the
-    literal one (torch glue, two GaussianRasterizer calls, conv2d SSIM): loss within
-    1e-5 relative, every Gaussian gradient within 1e-4 relative L2."""
+    literal one (torch glue, two GaussianRasterizer calls, conv2d SSIM with its loss
+    terms in float64, so the reference carries no float32 convolution error).
+
+    Loss within 1e-5 relative.  Gradients: the HIP transform's camera-frame means
+    differ from the matmul formulation by an ulp, which flips alpha / transmittance
+    thresholds for a few (pixel, Gaussian) pairs, and the gradient of a Gaussian in
+    such a pair jumps; so >= 98 % of Gaussians must agree per row within 1e-4, and
+    those rows within 1e-5 relative L2.  Isotropic maps: the rotation gradient is
+    zero in exact arithmetic (both sides hold rounding noise), so only its size is
+    checked."""
     _, params, cam = _map_params(cuda, aniso, sh)
     curr = _scene_targets(params, cam, cuda)
     assert slam.fused_mapping_eligible(params, curr, slam.MappingConfig())
-    l0, g0, r0 = _loss_and_grads(params, curr, fused=False)
+    l0, g0, r0 = _loss_and_grads(params, curr, fused=False, loss_dtype=torch.float64)
     l1, g1, r1 = _loss_and_grads(params, curr, fused=True)
     assert abs(l0 - l1) <= 1e-5 * abs(l0), (l0, l1)
     assert float((r0 == r1).float().mean()) >= 0.999
     for k in g0:
+        if k == "unnorm_rotations" and not aniso:
+            scale = float(g0["means3D"].abs().max())
+            assert float(g1[k].abs().max()) <= 1e-4 * scale and float(g0[k].abs().max()) <= 1e-4 * scale
+            continue
         assert float(g0[k].abs().sum()) > 0.0, k
-        assert _rel(g1[k], g0[k]) <= 1e-4, (k, _rel(g1[k], g0[k]))
+        frac, rel = _rows_close(g1[k], g0[k])
+        assert frac >= 0.98 and rel <= 1e-5, (k, frac, rel)
 
 
 def test_fused_adam_matches_torch(cuda):
@@ -171,9 +194,11 @@ def test_fused_adam_matches_torch(cuda):
     base = torch.randn(10001, generator=g).to(cuda)
     shapes = {"a": (1000, 3), "b": (777,), "c": (33, 16, 3), "d": None}
     ps = {k: torch.randn(*s, generator=g).to(cuda) for k, s in shapes.items() if s}
-    ps["d"] = base[1:5001]  # misaligned view (contiguous)
+    ps["d"] = base[1:5001]
     lrs = {"a": 1e-4, "b": 0.05, "c": 0.0025, "d": 0.001}
     mine = {k: v.clone() for k, v in ps.items()}
+    mine["d"] = base.clone()[1:5001]  # 4-byte offset view: contiguous, not 16-byte aligned (scalar path)
+    assert mine["d"].data_ptr() % 16 != 0
     ref = {k: v.clone() for k, v in ps.items()}
     opt_m = FusedAdam([{"params": [mine[k]], "lr": lrs[k]} for k in ps], lr=0.0, eps=1e-15)
     opt_r = torch.optim.Adam([{"params": [ref[k]], "lr": lrs[k]} for k in ps], lr=0.0, eps=1e-15)
@@ -203,6 +228,8 @@ def test_fused_map_adam_follows_eager_optimizer(cuda, sh):
     key = slam.color_key(params)
     keys = GAUSS_KEYS + (key,)
     fused_p = {k: v.clone() for k, v in params.items()}
+    for k in keys:  # the fused step runs in the transform's backward: autograd must reach it
+        fused_p[k].requires_grad_(True)
     adam = MapAdam(fused_p, cfg.lrs, color_key=key)
     eager_p = {k: v.clone() for k, v in params.items()}
     for k in keys:
@@ -226,3 +253,55 @@ def test_fused_map_adam_follows_eager_optimizer(cuda, sh):
         close = err <= 1e-6 * params[k].abs() + 1e-7
         assert float(close.float().mean()) >= 0.999, (k, float(close.float().mean()))
         assert float(err.max()) <= 6.0 * cfg.lrs[k] + 1e-6, k
+
+
+def _keyframes(params, cam, cuda, K=3):
+    kfs = []
+    with torch.no_grad():
+        key = slam.color_key(params)
+        truth = dict(params)
+        truth[key] = params[key] * 0.8 + 0.05
+        w2c = torch.eye(4, device=cuda)
+        for t in range(K):
+            tg = slam.transform_to_frame(truth, t, False, False)
+            im, _, _ = GaussianRasterizer(cam)(**slam._rendervar_colors(truth, slam.transformed_params2rendervar(
+                truth, tg)))
+            ds, _, _ = GaussianRasterizer(cam)(**slam.transformed_params2depthplussilhouette(truth, w2c, tg))
+            kfs.append({"cam": cam, "w2c": w2c, "im": im.clamp(0, 1), "depth": ds[0:1].clone(), "id": t})
+    return kfs
+
+
+@pytest.mark.parametrize("sh", [False, True])
+def test_graph_mapper_matches_eager_iterations(cuda, sh):
+    """Two replays of a 6-iteration mapping graph (fresh optimizer per replay, keyframes
+    drawn at construction) follow the same 2 x 6 eager fused iterations with MapAdam."""
+    from splatam_amd.mapper import GraphMapper
+    _, params, cam = _map_params(cuda, True, sh)
+    kfs = _keyframes(params, cam, cuda)
+    key = slam.color_key(params)
+    keys = GAUSS_KEYS + (key,)
+    g_p = {k: v.clone() for k, v in params.items()}
+    e_p = {k: v.clone() for k, v in params.items()}
+    for k in keys:
+        g_p[k].requires_grad_(True)
+        e_p[k].requires_grad_(True)
+    mapper = GraphMapper(g_p, kfs, iters_per_graph=6)
+    for k in keys:  # construction (warm-up) leaves the parameters untouched
+        assert torch.equal(g_p[k].detach(), params[k]), k
+    mapper.run()
+    mapper.run()
+    torch.cuda.synchronize()
+    assert not mapper.overflowed()
+    adam = MapAdam(e_p, slam.MappingConfig().lrs, color_key=key)
+    for _ in range(2):
+        adam.reset()
+        for j in mapper.sequence:
+            kf = kfs[j]
+            loss, _, _ = slam.get_loss_mapping(e_p, kf, kf["id"], fused=True, adam=adam)
+            loss.backward()
+    for k in keys:
+        moved = (e_p[k].detach() - params[k]).abs()
+        assert float(moved.max()) > 0.0, k
+        err = (g_p[k].detach() - e_p[k].detach()).abs()
+        close = err <= 1e-6 * params[k].abs() + 1e-7
+        assert float(close.float().mean()) >= 0.995, (k, float(close.float().mean()))
