@@ -18,7 +18,7 @@ ROOT = os.path.dirname(HERE)
 OBJDIR = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libgsr.so")
 SOURCES = ["gsr_forward.hip", "gsr_backward.hip", "gsr_backward_power.hip", "gsr_capi.hip", "gsr_glue.hip",
-           "gsr_mapping.hip"]
+           "gsr_mapping.hip", "gsr_sh.hip"]
 ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
 
 

@@ -80,6 +80,7 @@ GaussIn make_gauss(const gsr_gaussians* g) {
     o.rotations = g->rotations;
     o.cov3D = g->cov3D_precomp;
     o.colors2 = nullptr;
+    o.sh_staged = 0;
     return o;
 }
 
@@ -300,6 +301,10 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         if (!radii) return fail(GSR_ERR_INVALID_ARG, "radii output required");
         {
             StageTimer t(GSR_STAGE_PREPROCESS, P, stream);
+            if (sh_staged(cam, g)) {  // SH colours with coalesced coefficient reads, ahead of preprocess
+                if ((e = launch_sh_eval(cam, g, geo, stream)) != hipSuccess) return hip_fail(e, "sh_eval");
+                g.sh_staged = 1;
+            }
             if ((e = launch_preprocess(cam, g, geo, radii, lds_hist ? cmat : tile_count, lds_hist, ntiles, GL.nb,
                                        stream)) != hipSuccess)
                 return hip_fail(e, "preprocess");
@@ -522,11 +527,21 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     const unsigned need = (out.dopacity ? NEED_OPACITY : 0u) | ((out.dcolors || g.shs) ? NEED_COLORS : 0u) |
                           (dcolors2 ? NEED_COLORS2 : 0u) | (dl2_channels == 1 ? NEED_DL2_CH0_ONLY : 0u);
     const RecLayout rec = bwd_rec_layout(need, colors2 != nullptr);
+    // staged SH backward: gauss_bwd leaves dL/dcolor in a scratch array, sh_bwd turns it into dsh and the
+    // view-direction term of dL/dmeans3D (gsr_sh.hip)
+    const bool shs_staged = sh_staged(cam, g);
+    const size_t rec_bytes = align_up(sizeof(float) * rec.stride * (size_t)num_rendered, 256);
+    const size_t scratch_bytes = (num_rendered > 0 ? rec_bytes : 0) + (shs_staged ? sizeof(float) * 3 * (size_t)P : 0);
+    char* scratch = nullptr;
+    if (scratch_bytes > 0) {
+        if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
+        scratch = (char*)obtain(alloc, alloc_ctx, GSR_BUF_SCRATCH, scratch_bytes);
+        if (!scratch) return fail(GSR_ERR_ALLOC, "allocator returned NULL (backward scratch)");
+    }
+    float* drgb = shs_staged ? (float*)(scratch + (num_rendered > 0 ? rec_bytes : 0)) : nullptr;
     if (num_rendered > 0) {
         if (!binning_buffer) return fail(GSR_ERR_INVALID_ARG, "missing binning buffer");
-        if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
-        inst = (float*)obtain(alloc, alloc_ctx, GSR_BUF_SCRATCH, sizeof(float) * rec.stride * (size_t)num_rendered);
-        if (!inst) return fail(GSR_ERR_ALLOC, "allocator returned NULL (backward scratch)");
+        inst = (float*)scratch;
         const char* bb = (const char*)binning_buffer;
         const uint32_t* point_list = (const uint32_t*)(bb + BL.point_list);
         StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream, true);
@@ -538,9 +553,20 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     out.dcolors2 = dcolors2;
     {
         StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
-        if ((e = launch_gauss_bwd(cam, g, geo, radii, inst, rec, out, BwdGuard{geo.counters, (uint32_t)num_rendered},
-                                  stream)) != hipSuccess)
+        const BwdGuard guard{geo.counters, (uint32_t)num_rendered};
+        GaussIn gc = g;
+        GradsOut oc = out;
+        if (shs_staged) {  // the chain without SH: dL/dcolor to scratch, dsh by sh_bwd below
+            gc.shs = nullptr;
+            gc.M = 0;
+            oc.dcolors = drgb;
+            oc.dsh = nullptr;
+        }
+        if ((e = launch_gauss_bwd(cam, gc, geo, radii, inst, rec, oc, guard, stream)) != hipSuccess)
             return hip_fail(e, "gaussian backward");
+        if (shs_staged && (e = launch_sh_bwd(cam, g, geo, radii, drgb, out.dmeans3D, out.dsh, guard, stream)) !=
+                              hipSuccess)
+            return hip_fail(e, "sh backward");
     }
     return GSR_OK;
 }

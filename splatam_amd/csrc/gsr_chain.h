@@ -22,6 +22,73 @@ __device__ inline void gaussian_conic(const Camera& cam, const GaussIn& g, int i
     (void)conic_of(pj, ca, cb, cc);
 }
 
+// SH backward (backward.cu:20-139) for one Gaussian: sh = its 3*M coefficients
+// (any address space), drgb = dL/dcolor before the clamp mask.  Writes dsh_out[3*nsh],
+// adds the view-direction term to dmean.
+__device__ __forceinline__ void sh_chain_bwd(const Camera& cam, float3 m, const float* sh, const float* drgb,
+                                             unsigned clamped, float* dsh_out, float dmean[3]) {
+    const float dox = m.x - cam.campos[0], doy = m.y - cam.campos[1], doz = m.z - cam.campos[2];
+    const float len = sqrtf(dox * dox + doy * doy + doz * doz);
+    const float x = dox / len, y = doy / len, z = doz / len;
+    const int D = cam.sh_degree;
+    float ddir0 = 0.f, ddir1 = 0.f, ddir2 = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        const float dRGB = ((clamped >> ch) & 1u) ? 0.f : drgb[ch];
+#define SH(k) sh[3 * (k) + ch]
+#define DSH(k) dsh_out[3 * (k) + ch]
+        float dx_ = 0.f, dy_ = 0.f, dz_ = 0.f;
+        DSH(0) = kSH_C0 * dRGB;
+        if (D > 0) {
+            DSH(1) = -kSH_C1 * y * dRGB;
+            DSH(2) = kSH_C1 * z * dRGB;
+            DSH(3) = -kSH_C1 * x * dRGB;
+            dx_ = -kSH_C1 * SH(3);
+            dy_ = -kSH_C1 * SH(1);
+            dz_ = kSH_C1 * SH(2);
+            if (D > 1) {
+                const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+                DSH(4) = kSH_C2[0] * xy * dRGB;
+                DSH(5) = kSH_C2[1] * yz * dRGB;
+                DSH(6) = kSH_C2[2] * (2.f * zz - xx - yy) * dRGB;
+                DSH(7) = kSH_C2[3] * xz * dRGB;
+                DSH(8) = kSH_C2[4] * (xx - yy) * dRGB;
+                dx_ += kSH_C2[0] * y * SH(4) + kSH_C2[2] * 2.f * -x * SH(6) + kSH_C2[3] * z * SH(7) + kSH_C2[4] * 2.f * x * SH(8);
+                dy_ += kSH_C2[0] * x * SH(4) + kSH_C2[1] * z * SH(5) + kSH_C2[2] * 2.f * -y * SH(6) + kSH_C2[4] * 2.f * -y * SH(8);
+                dz_ += kSH_C2[1] * y * SH(5) + kSH_C2[2] * 2.f * 2.f * z * SH(6) + kSH_C2[3] * x * SH(7);
+                if (D > 2) {
+                    DSH(9) = kSH_C3[0] * y * (3.f * xx - yy) * dRGB;
+                    DSH(10) = kSH_C3[1] * xy * z * dRGB;
+                    DSH(11) = kSH_C3[2] * y * (4.f * zz - xx - yy) * dRGB;
+                    DSH(12) = kSH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy) * dRGB;
+                    DSH(13) = kSH_C3[4] * x * (4.f * zz - xx - yy) * dRGB;
+                    DSH(14) = kSH_C3[5] * z * (xx - yy) * dRGB;
+                    DSH(15) = kSH_C3[6] * x * (xx - 3.f * yy) * dRGB;
+                    dx_ += kSH_C3[0] * SH(9) * 3.f * 2.f * xy + kSH_C3[1] * SH(10) * yz + kSH_C3[2] * SH(11) * -2.f * xy +
+                           kSH_C3[3] * SH(12) * -3.f * 2.f * xz + kSH_C3[4] * SH(13) * (-3.f * xx + 4.f * zz - yy) +
+                           kSH_C3[5] * SH(14) * 2.f * xz + kSH_C3[6] * SH(15) * 3.f * (xx - yy);
+                    dy_ += kSH_C3[0] * SH(9) * 3.f * (xx - yy) + kSH_C3[1] * SH(10) * xz +
+                           kSH_C3[2] * SH(11) * (-3.f * yy + 4.f * zz - xx) + kSH_C3[3] * SH(12) * -3.f * 2.f * yz +
+                           kSH_C3[4] * SH(13) * -2.f * xy + kSH_C3[5] * SH(14) * -2.f * yz + kSH_C3[6] * SH(15) * -3.f * 2.f * xy;
+                    dz_ += kSH_C3[1] * SH(10) * xy + kSH_C3[2] * SH(11) * 4.f * 2.f * yz +
+                           kSH_C3[3] * SH(12) * 3.f * (2.f * zz - xx - yy) + kSH_C3[4] * SH(13) * 4.f * 2.f * xz +
+                           kSH_C3[5] * SH(14) * (xx - yy);
+                }
+            }
+        }
+#undef SH
+#undef DSH
+        ddir0 += dx_ * dRGB;
+        ddir1 += dy_ * dRGB;
+        ddir2 += dz_ * dRGB;
+    }
+    const float sum2 = dox * dox + doy * doy + doz * doz;
+    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);  // dnormvdv, auxiliary.h:107-117
+    dmean[0] += ((sum2 - dox * dox) * ddir0 - doy * dox * ddir1 - doz * dox * ddir2) * invsum32;
+    dmean[1] += (-dox * doy * ddir0 + (sum2 - doy * doy) * ddir1 - doz * doy * ddir2) * invsum32;
+    dmean[2] += (-dox * doz * ddir0 - doy * doz * ddir1 + (sum2 - doz * doz) * ddir2) * invsum32;
+}
+
 // ------------------------------------------------------ per-Gaussian chain --
 // g2: [0..1] dL/dmean2D (NDC units), [2..4] dL/dconic (A, B/2, C), [5] dL/dopacity,
 // [6..8] dL/dcolor.  Outputs: dmean3D[3], dcov3D[6], dscale[3], drot[4], dsh[3*nsh].
@@ -94,69 +161,7 @@ __device__ inline void gauss_chain(const Camera& cam, const GaussIn& g, int i, c
     dmean[1] += (pr[4] * mw - pr[7] * mul1) * gx2 + (pr[5] * mw - pr[7] * mul2) * gy2;
     dmean[2] += (pr[8] * mw - pr[11] * mul1) * gx2 + (pr[9] * mw - pr[11] * mul2) * gy2;
     // SH bwd (backward.cu:20-139)
-    if (g.shs) {
-        const float* sh = g.shs + (size_t)3 * g.M * i;
-        const float dox = m.x - cam.campos[0], doy = m.y - cam.campos[1], doz = m.z - cam.campos[2];
-        const float len = sqrtf(dox * dox + doy * doy + doz * doz);
-        const float x = dox / len, y = doy / len, z = doz / len;
-        const int D = cam.sh_degree;
-        float ddir0 = 0.f, ddir1 = 0.f, ddir2 = 0.f;
-#pragma unroll
-        for (int ch = 0; ch < 3; ch++) {
-            const float dRGB = ((clamped >> ch) & 1u) ? 0.f : g2[6 + ch];
-#define SH(k) sh[3 * (k) + ch]
-#define DSH(k) dsh_out[3 * (k) + ch]
-            float dx_ = 0.f, dy_ = 0.f, dz_ = 0.f;
-            DSH(0) = kSH_C0 * dRGB;
-            if (D > 0) {
-                DSH(1) = -kSH_C1 * y * dRGB;
-                DSH(2) = kSH_C1 * z * dRGB;
-                DSH(3) = -kSH_C1 * x * dRGB;
-                dx_ = -kSH_C1 * SH(3);
-                dy_ = -kSH_C1 * SH(1);
-                dz_ = kSH_C1 * SH(2);
-                if (D > 1) {
-                    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-                    DSH(4) = kSH_C2[0] * xy * dRGB;
-                    DSH(5) = kSH_C2[1] * yz * dRGB;
-                    DSH(6) = kSH_C2[2] * (2.f * zz - xx - yy) * dRGB;
-                    DSH(7) = kSH_C2[3] * xz * dRGB;
-                    DSH(8) = kSH_C2[4] * (xx - yy) * dRGB;
-                    dx_ += kSH_C2[0] * y * SH(4) + kSH_C2[2] * 2.f * -x * SH(6) + kSH_C2[3] * z * SH(7) + kSH_C2[4] * 2.f * x * SH(8);
-                    dy_ += kSH_C2[0] * x * SH(4) + kSH_C2[1] * z * SH(5) + kSH_C2[2] * 2.f * -y * SH(6) + kSH_C2[4] * 2.f * -y * SH(8);
-                    dz_ += kSH_C2[1] * y * SH(5) + kSH_C2[2] * 2.f * 2.f * z * SH(6) + kSH_C2[3] * x * SH(7);
-                    if (D > 2) {
-                        DSH(9) = kSH_C3[0] * y * (3.f * xx - yy) * dRGB;
-                        DSH(10) = kSH_C3[1] * xy * z * dRGB;
-                        DSH(11) = kSH_C3[2] * y * (4.f * zz - xx - yy) * dRGB;
-                        DSH(12) = kSH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy) * dRGB;
-                        DSH(13) = kSH_C3[4] * x * (4.f * zz - xx - yy) * dRGB;
-                        DSH(14) = kSH_C3[5] * z * (xx - yy) * dRGB;
-                        DSH(15) = kSH_C3[6] * x * (xx - 3.f * yy) * dRGB;
-                        dx_ += kSH_C3[0] * SH(9) * 3.f * 2.f * xy + kSH_C3[1] * SH(10) * yz + kSH_C3[2] * SH(11) * -2.f * xy +
-                               kSH_C3[3] * SH(12) * -3.f * 2.f * xz + kSH_C3[4] * SH(13) * (-3.f * xx + 4.f * zz - yy) +
-                               kSH_C3[5] * SH(14) * 2.f * xz + kSH_C3[6] * SH(15) * 3.f * (xx - yy);
-                        dy_ += kSH_C3[0] * SH(9) * 3.f * (xx - yy) + kSH_C3[1] * SH(10) * xz +
-                               kSH_C3[2] * SH(11) * (-3.f * yy + 4.f * zz - xx) + kSH_C3[3] * SH(12) * -3.f * 2.f * yz +
-                               kSH_C3[4] * SH(13) * -2.f * xy + kSH_C3[5] * SH(14) * -2.f * yz + kSH_C3[6] * SH(15) * -3.f * 2.f * xy;
-                        dz_ += kSH_C3[1] * SH(10) * xy + kSH_C3[2] * SH(11) * 4.f * 2.f * yz +
-                               kSH_C3[3] * SH(12) * 3.f * (2.f * zz - xx - yy) + kSH_C3[4] * SH(13) * 4.f * 2.f * xz +
-                               kSH_C3[5] * SH(14) * (xx - yy);
-                    }
-                }
-            }
-#undef SH
-#undef DSH
-            ddir0 += dx_ * dRGB;
-            ddir1 += dy_ * dRGB;
-            ddir2 += dz_ * dRGB;
-        }
-        const float sum2 = dox * dox + doy * doy + doz * doz;
-        const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);  // dnormvdv, auxiliary.h:107-117
-        dmean[0] += ((sum2 - dox * dox) * ddir0 - doy * dox * ddir1 - doz * dox * ddir2) * invsum32;
-        dmean[1] += (-dox * doy * ddir0 + (sum2 - doy * doy) * ddir1 - doz * doy * ddir2) * invsum32;
-        dmean[2] += (-dox * doz * ddir0 - doy * doz * ddir1 + (sum2 - doz * doz) * ddir2) * invsum32;
-    }
+    if (g.shs) sh_chain_bwd(cam, m, g.shs + (size_t)3 * g.M * i, g2 + 6, clamped, dsh_out, dmean);
     (void)nsh;
     // computeCov3D bwd (backward.cu:412-475); dL/dscale w.r.t. (modifier * scale), as the reference
 #pragma unroll

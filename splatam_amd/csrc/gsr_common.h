@@ -148,6 +148,7 @@ struct GaussIn {
     const float* rotations;
     const float* cov3D;
     const float* colors2;  // second precomputed colour set of a dual render (else nullptr)
+    int sh_staged;         // SH colours already in rr[2].xyz / clamp (sh_eval_kernel, gsr_sh.hip)
 };
 
 struct GeomPtrs {
@@ -882,6 +883,11 @@ struct GradsOut {
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* inst,
                             RecLayout rec, const GradsOut& out, BwdGuard guard, hipStream_t s);
 hipError_t launch_selftest_reduce9(const float* in, float* out, hipStream_t s);
+// gsr_sh.hip: SH colour stages with LDS-staged, coalesced coefficient traffic
+bool sh_staged(const Camera& cam, const GaussIn& g);
+hipError_t launch_sh_eval(const Camera& cam, const GaussIn& g, GeomPtrs geo, hipStream_t s);
+hipError_t launch_sh_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* drgb,
+                         float* dmeans3D, float* dsh, BwdGuard guard, hipStream_t s);
 // error reporting shared by the C entry points (gsr_last_error)
 int fail(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* where);

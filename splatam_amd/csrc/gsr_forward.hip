@@ -74,6 +74,9 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                 unsigned clamped = 0;
                 if (g.colors) {
                     rgb[0] = g.colors[3 * i]; rgb[1] = g.colors[3 * i + 1]; rgb[2] = g.colors[3 * i + 2];
+                } else if (g.sh_staged) {  // sh_eval_kernel wrote rgb and the clamp bits
+                    const float4 c = geo.rr[(size_t)RR_F4 * i + 2];
+                    rgb[0] = c.x; rgb[1] = c.y; rgb[2] = c.z;
                 } else {
                     sh_fwd(cam.sh_degree, p, cam.campos, g.shs + (size_t)3 * g.M * i, rgb, clamped);
                 }
@@ -89,7 +92,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                 rr[3] = make_float4(c2[0], c2[1], c2[2], __uint_as_float(rhi));
                 q1 = make_float4(K_B * cb, g.opacities[i], pv.z, 0.f);  // .w: workgroup-local instance offset, below
                 geo.bin[i] = make_uint4(rlo, rhi, __float_as_uint(pv.z), tiles);
-                geo.clamp[i] = clamped;
+                if (!g.sh_staged) geo.clamp[i] = clamped;
                 for (int ty = y0; ty < y1; ty++)  // per-tile instance counts -> bucket ranges
                     for (int tx = x0; tx < x1; tx++) {
                         if (LDS_HIST) atomicAdd(&s_hist[ty * cam.gx + tx], 1u);

@@ -1,0 +1,163 @@
+// gsr_sh.hip -- spherical-harmonics colour stages with coalesced coefficient traffic.
+//
+// A Gaussian's 3 * (D+1)^2 SH coefficients are 192 contiguous bytes at D = 3, so
+// one lane per Gaussian reading or writing them directly touches 64 cache lines
+// per wave instruction, 48 times over.  Here a 256-Gaussian workgroup moves its
+// coefficient block between HBM and LDS as one contiguous float4 stream and each
+// lane works on its own LDS row (row stride 3*NSH + 1 floats: odd, so the 64
+// lanes of a wave hit 64 distinct banks).
+//
+//   sh_eval_kernel  computeColorFromSH (forward.cu:20-73) -> render-record rgb
+//                   (rr[2].xyz) and the clamp bits, before preprocess;
+//   sh_bwd_kernel   the SH part of preprocessCUDA's backward (backward.cu:20-139):
+//                   dsh (staged in LDS, written as one float4 stream) and the
+//                   view-direction term added to dL/dmeans3D, after gauss_bwd has
+//                   written dL/dcolor into a scratch array.
+#include "gsr_chain.h"
+
+namespace gsr {
+namespace {
+
+constexpr int SH_BLOCK = 256;
+
+template <int NSH>
+struct ShTile {
+    static constexpr int ROW = 3 * NSH;      // floats per Gaussian
+    static constexpr int PITCH = ROW + 1;    // LDS row pitch (odd: conflict-free per-lane rows)
+};
+
+// Global [n x ROW] block (contiguous: M == NSH) -> LDS rows.
+template <int NSH>
+__device__ __forceinline__ void stage_rows(float* s, const float* __restrict__ src, int n) {
+    using T = ShTile<NSH>;
+    const int total = n * T::ROW;
+    if (T::ROW % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        for (int e4 = threadIdx.x; 4 * e4 < total; e4 += SH_BLOCK) {
+            const float4 v = s4[e4];
+            const int e = 4 * e4, r = e / T::ROW, c = e - r * T::ROW;  // ROW % 4 == 0: no row straddle
+            float* d = s + r * T::PITCH + c;
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+    } else {
+        for (int e = threadIdx.x; e < total; e += SH_BLOCK) {
+            const int r = e / T::ROW, c = e - r * T::ROW;
+            s[r * T::PITCH + c] = src[e];
+        }
+    }
+}
+
+template <int NSH>
+__device__ __forceinline__ void unstage_rows(float* __restrict__ dst, const float* s, int n) {
+    using T = ShTile<NSH>;
+    const int total = n * T::ROW;
+    if (T::ROW % 4 == 0 && (reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        for (int e4 = threadIdx.x; 4 * e4 < total; e4 += SH_BLOCK) {
+            const int e = 4 * e4, r = e / T::ROW, c = e - r * T::ROW;
+            const float* q = s + r * T::PITCH + c;
+            d4[e4] = make_float4(q[0], q[1], q[2], q[3]);
+        }
+    } else {
+        for (int e = threadIdx.x; e < total; e += SH_BLOCK) {
+            const int r = e / T::ROW, c = e - r * T::ROW;
+            dst[e] = s[r * T::PITCH + c];
+        }
+    }
+}
+
+template <int NSH>
+__global__ void __launch_bounds__(SH_BLOCK) sh_eval_kernel(Camera cam, GaussIn g, GeomPtrs geo) {
+    using T = ShTile<NSH>;
+    __shared__ float s_sh[SH_BLOCK * T::PITCH];
+    const int base = blockIdx.x * SH_BLOCK;
+    const int n = min(SH_BLOCK, g.P - base);
+    stage_rows<NSH>(s_sh, g.shs + (size_t)T::ROW * base, n);
+    __syncthreads();
+    if ((int)threadIdx.x >= n) return;
+    const int i = base + threadIdx.x;
+    const float3 p = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
+    float rgb[3];
+    unsigned clamped = 0;
+    sh_fwd(cam.sh_degree, p, cam.campos, s_sh + threadIdx.x * T::PITCH, rgb, clamped);
+    geo.rr[(size_t)RR_F4 * i + 2] = make_float4(rgb[0], rgb[1], rgb[2], 0.f);  // .w: tile rect, by preprocess
+    geo.clamp[i] = clamped;
+}
+
+// drgb: [P,3] dL/dcolor (unmasked) from gauss_bwd; dmeans3D: += view-direction term.
+template <int NSH>
+__global__ void __launch_bounds__(SH_BLOCK)
+sh_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float* __restrict__ drgb,
+              float* __restrict__ dmeans3D, float* __restrict__ dsh, BwdGuard guard) {
+    using T = ShTile<NSH>;
+    __shared__ float s_sh[SH_BLOCK * T::PITCH];
+    const int base = blockIdx.x * SH_BLOCK;
+    const int n = min(SH_BLOCK, g.P - base);
+    stage_rows<NSH>(s_sh, g.shs + (size_t)T::ROW * base, n);
+    __syncthreads();
+    if ((int)threadIdx.x < n) {
+        const int i = base + threadIdx.x;
+        float* row = s_sh + threadIdx.x * T::PITCH;
+        if (radii[i] > 0 && !guard.overflow()) {
+            const float3 m = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
+            const float d[3] = {drgb[3 * i], drgb[3 * i + 1], drgb[3 * i + 2]};
+            float dmean[3] = {dmeans3D[3 * i], dmeans3D[3 * i + 1], dmeans3D[3 * i + 2]};
+            float dsh_r[T::ROW];
+            sh_chain_bwd(cam, m, row, d, geo.clamp[i], dsh_r, dmean);
+#pragma unroll
+            for (int k = 0; k < T::ROW; k++) row[k] = dsh_r[k];  // own row: no other lane reads it
+#pragma unroll
+            for (int k = 0; k < 3; k++) dmeans3D[3 * i + k] = dmean[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < T::ROW; k++) row[k] = 0.f;
+        }
+    }
+    __syncthreads();
+    if (dsh) unstage_rows<NSH>(dsh + (size_t)T::ROW * base, s_sh, n);
+}
+
+template <int NSH>
+hipError_t launch_sh_eval_t(const Camera& cam, const GaussIn& g, GeomPtrs geo, hipStream_t s) {
+    hipLaunchKernelGGL(sh_eval_kernel<NSH>, dim3((g.P + SH_BLOCK - 1) / SH_BLOCK), dim3(SH_BLOCK), 0, s, cam, g, geo);
+    return hipGetLastError();
+}
+
+template <int NSH>
+hipError_t launch_sh_bwd_t(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* drgb,
+                           float* dmeans3D, float* dsh, BwdGuard guard, hipStream_t s) {
+    hipLaunchKernelGGL(sh_bwd_kernel<NSH>, dim3((g.P + SH_BLOCK - 1) / SH_BLOCK), dim3(SH_BLOCK), 0, s, cam, g, geo,
+                       radii, drgb, dmeans3D, dsh, guard);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// The staged kernels need M == (D+1)^2 (coefficient rows contiguous); otherwise the
+// per-lane paths (preprocess / gauss_chain) keep handling SH.
+bool sh_staged(const Camera& cam, const GaussIn& g) {
+    return g.shs && cam.sh_degree >= 0 && cam.sh_degree <= 3 && g.M == (cam.sh_degree + 1) * (cam.sh_degree + 1);
+}
+
+hipError_t launch_sh_eval(const Camera& cam, const GaussIn& g, GeomPtrs geo, hipStream_t s) {
+    if (g.P == 0) return hipSuccess;
+    switch (cam.sh_degree) {
+        case 0: return launch_sh_eval_t<1>(cam, g, geo, s);
+        case 1: return launch_sh_eval_t<4>(cam, g, geo, s);
+        case 2: return launch_sh_eval_t<9>(cam, g, geo, s);
+        default: return launch_sh_eval_t<16>(cam, g, geo, s);
+    }
+}
+
+hipError_t launch_sh_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* drgb,
+                         float* dmeans3D, float* dsh, BwdGuard guard, hipStream_t s) {
+    if (g.P == 0) return hipSuccess;
+    switch (cam.sh_degree) {
+        case 0: return launch_sh_bwd_t<1>(cam, g, geo, radii, drgb, dmeans3D, dsh, guard, s);
+        case 1: return launch_sh_bwd_t<4>(cam, g, geo, radii, drgb, dmeans3D, dsh, guard, s);
+        case 2: return launch_sh_bwd_t<9>(cam, g, geo, radii, drgb, dmeans3D, dsh, guard, s);
+        default: return launch_sh_bwd_t<16>(cam, g, geo, radii, drgb, dmeans3D, dsh, guard, s);
+    }
+}
+
+}  // namespace gsr
