@@ -51,3 +51,59 @@ def test_frame_sharding_world2():
     assert h0 == h1 == 3.0                       # Fisher / Hessian merge
     assert t0 == t1 == 1.5                       # max-over-ranks timing
     assert sent0 == 100 * (3 + 3 + 4 + 1 + 1) * 4
+
+
+def _fisher_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from splatam_amd.fisher import FisherScorer
+
+    def fake_hessian(w2c):  # deterministic per pose, positive like a Fisher diagonal
+        s = float(w2c[0, 3]) + 1.0
+        return torch.arange(40, dtype=torch.float32).reshape(10, 4) * s + s
+
+    params = {"means3D": torch.zeros(10, 3)}
+    sc = FisherScorer(params, None, hessian_fn=fake_hessian)
+    visited = [torch.eye(4) for _ in range(3)]
+    for j, v in enumerate(visited):
+        v[0, 3] = float(j)
+    cands = [torch.eye(4) for _ in range(5)]
+    for j, c in enumerate(cands):
+        c[0, 3] = 0.5 * j
+    hinv = sc.fit_visited(visited)
+    scores = sc.eig_scores(cands)
+    q.put((rank, hinv.clone(), scores.clone()))
+    dist.destroy_process_group()
+
+
+def test_fisher_scoring_sharded_world2():
+    """Visited-pose Hessians summed across ranks (all-reduce) and candidate EIG scores
+    gathered in pose order equal the single-process result (ros_handler.py:807-836)."""
+    from splatam_amd.fisher import FisherScorer
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fisher_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in procs), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+    def fake_hessian(w2c):
+        s = float(w2c[0, 3]) + 1.0
+        return torch.arange(40, dtype=torch.float32).reshape(10, 4) * s + s
+
+    ref = FisherScorer({"means3D": torch.zeros(10, 3)}, None, hessian_fn=fake_hessian)
+    visited = [torch.eye(4) for _ in range(3)]
+    for j, v in enumerate(visited):
+        v[0, 3] = float(j)
+    cands = [torch.eye(4) for _ in range(5)]
+    for j, c in enumerate(cands):
+        c[0, 3] = 0.5 * j
+    hinv = ref.fit_visited(visited)
+    scores = ref.eig_scores(cands)
+    for _, h, s in res:
+        assert torch.allclose(h, hinv) and torch.allclose(s, scores)
+    assert bool((scores[1:] > scores[:-1]).all())
