@@ -10,8 +10,11 @@ What is captured (all small):
     setup_camera (utils/recon_helpers.py:4-27), transform_to_frame,
     transformed_params2rendervar, transformed_params2depthplussilhouette,
     get_depth_and_silhouette (utils/slam_helpers.py), build_rotation
-    (utils/slam_external.py:25-42), with `.cuda()` / device="cuda" redirected to
-    the CPU.
+    (utils/slam_external.py:25-42), calc_ssim (slam_external.py:61-97, value and
+    gradient) and the mapping transform's parameter gradients, with `.cuda()` /
+    device="cuda" redirected to the CPU;
+  * ref_params.npz -- a small parameter checkpoint written by the reference's own
+    save_params (utils/common_utils.py:35-42), for checkpoint interop.
 
 The reference's CUDA kernels cannot run here (no nvcc / NVIDIA GPU), so no
 kernel-level golden exists; see DESIGN.md "Parity".  Run:
@@ -189,6 +192,24 @@ def main():
                  **{k: v.numpy() for k, v in ups.items()}, time_idx=2, w2c=w2c.astype(np.float32),
                  **{f"grad_{k}": params[k].grad.numpy()
                     for k in ("means3D", "unnorm_rotations", "logit_opacities", "log_scales")})
+
+    # ---- params*.npz written by the reference's own save_params (utils/common_utils.py:35-42)
+    cu = importlib.import_module("utils.common_utils")
+    import tempfile
+    g3 = torch.Generator().manual_seed(3)
+    ck = {"means3D": torch.randn(16, 3, generator=g3), "rgb_colors": torch.rand(16, 3, generator=g3),
+          "unnorm_rotations": torch.randn(16, 4, generator=g3), "logit_opacities": torch.randn(16, 1, generator=g3),
+          "log_scales": torch.randn(16, 1, generator=g3), "cam_unnorm_rots": torch.randn(1, 4, 5, generator=g3),
+          "cam_trans": torch.randn(1, 3, 5, generator=g3), "timestep": torch.zeros(16),
+          "intrinsics": np.eye(3, dtype=np.float32), "w2c": np.eye(4, dtype=np.float32), "org_width": 640,
+          "org_height": 480, "gt_w2c_all_frames": np.stack([np.eye(4, dtype=np.float32)] * 5),
+          "keyframe_time_indices": np.array([0, 5])}
+    with tempfile.TemporaryDirectory() as td:
+        cu.save_params(ck, td)
+        with open(os.path.join(td, "params.npz"), "rb") as f:
+            blob = f.read()
+    with open(os.path.join(OUT, "ref_params.npz"), "wb") as f:
+        f.write(blob)
 
     # ---- ABI capture: forward + backward through the reference autograd wrapper
     st = ref.GaussianRasterizationSettings(

@@ -115,3 +115,53 @@ def test_mapping_transform_gradients_match_reference():
         total.backward()
         for k in ("means3D", "unnorm_rotations", "logit_opacities", "log_scales"):
             np.testing.assert_allclose(params[k].grad.numpy(), g[f"grad_{k}"], rtol=1e-4, atol=1e-6, err_msg=k)
+
+
+def test_checkpoint_roundtrip_matches_reference_writer(tmp_path):
+    """A params.npz written by the reference's save_params loads without unpickling, and
+    ours writes the same keys and arrays back (utils/common_utils.py:35-52)."""
+    from splatam_amd import checkpoint
+    ref = os.path.join(GOLD, "ref_params.npz")
+    p = checkpoint.load_params(ref, device="cpu")
+    with np.load(ref, allow_pickle=False) as z:
+        keys = sorted(z.files)
+        for k in keys:
+            np.testing.assert_array_equal(p[k].detach().numpy(), z[k].astype(np.float32))
+    assert p["means3D"].requires_grad and p["means3D"].dtype == torch.float32
+    out = checkpoint.save_params_ckpt({k: v for k, v in p.items()}, str(tmp_path), 7)
+    assert out.endswith("params7.npz")
+    with np.load(out, allow_pickle=False) as z2, np.load(ref, allow_pickle=False) as z:
+        assert sorted(z2.files) == keys
+        for k in keys:
+            np.testing.assert_array_equal(z2[k], z[k].astype(np.float32))
+
+
+def test_prune_and_surgery_keep_optimizer_state_aligned():
+    """remove_points / cat_params_to_optimizer / prune_gaussians (slam_external.py:107-192)
+    on torch.optim.Adam: moments follow their Gaussians."""
+    from splatam_amd import surgery
+    g = torch.Generator().manual_seed(0)
+    P = 50
+    params = {"means3D": torch.randn(P, 3, generator=g), "logit_opacities": torch.randn(P, 1, generator=g) * 3,
+              "log_scales": torch.randn(P, 1, generator=g) - 3, "cam_unnorm_rots": torch.randn(1, 4, 2),
+              "cam_trans": torch.randn(1, 3, 2)}
+    params = {k: torch.nn.Parameter(v) for k, v in params.items()}
+    opt = torch.optim.Adam([{"params": [v], "name": k, "lr": 0.01} for k, v in params.items()], lr=0.0, eps=1e-15)
+    loss = sum((v ** 2).sum() for v in params.values())
+    loss.backward()
+    opt.step()
+    m_before = opt.state[params["means3D"]]["exp_avg"].clone()
+    keep_ref = torch.sigmoid(params["logit_opacities"].detach()).squeeze() >= 0.1
+    variables = {"scene_radius": 100.0, "means2D_gradient_accum": torch.arange(P).float(), "denom": torch.ones(P),
+                 "max_2D_radius": torch.zeros(P), "timestep": torch.zeros(P)}
+    pd = dict(start_after=0, remove_big_after=0, stop_after=20, prune_every=20, removal_opacity_threshold=0.1,
+              final_removal_opacity_threshold=0.1, reset_opacities=False, reset_opacities_every=500)
+    params, variables = surgery.prune_gaussians(params, variables, opt, 0, pd)
+    n = int(keep_ref.sum())
+    assert 0 < n < P and params["means3D"].shape[0] == n and params["cam_trans"].shape == (1, 3, 2)
+    torch.testing.assert_close(opt.state[params["means3D"]]["exp_avg"], m_before[keep_ref])
+    assert torch.equal(variables["means2D_gradient_accum"], torch.arange(P).float()[keep_ref])
+    new = {k: params[k].detach()[:3].clone() for k in ("means3D", "logit_opacities", "log_scales")}
+    params = surgery.cat_params_to_optimizer(new, params, opt)
+    assert params["means3D"].shape[0] == n + 3
+    assert float(opt.state[params["means3D"]]["exp_avg"][n:].abs().sum()) == 0.0

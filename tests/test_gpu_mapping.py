@@ -305,3 +305,32 @@ def test_graph_mapper_matches_eager_iterations(cuda, sh):
         err = (g_p[k].detach() - e_p[k].detach()).abs()
         close = err <= 1e-6 * params[k].abs() + 1e-7
         assert float(close.float().mean()) >= 0.995, (k, float(close.float().mean()))
+
+
+def test_fused_adam_through_gaussian_surgery(cuda):
+    """FusedAdam keeps torch's state layout, so SplaTAM's optimizer surgery (remove_points /
+    cat_params_to_optimizer, slam_external.py:122-163) works on it: after pruning and
+    appending Gaussians, further steps match torch.optim.Adam put through the same surgery."""
+    from splatam_amd import surgery
+    g = torch.Generator().manual_seed(4)
+    base = {"means3D": torch.randn(300, 3, generator=g), "logit_opacities": torch.randn(300, 1, generator=g),
+            "log_scales": torch.randn(300, 3, generator=g) - 3}
+    lrs = {"means3D": 1e-4, "logit_opacities": 0.05, "log_scales": 1e-3}
+    runs = []
+    for cls in (FusedAdam, torch.optim.Adam):
+        params = {k: torch.nn.Parameter(v.clone().to(cuda)) for k, v in base.items()}
+        opt = cls([{"params": [v], "name": k, "lr": lrs[k]} for k, v in params.items()], lr=0.0, eps=1e-15)
+        gg = torch.Generator().manual_seed(5)
+        for s in range(4):
+            for k, v in params.items():
+                v.grad = torch.randn(v.shape, generator=gg).to(cuda)
+            opt.step()
+            if s == 1:
+                keep = torch.arange(params["means3D"].shape[0], device=cuda) % 3 != 0
+                params, _ = surgery.remove_points(~keep, params, {}, opt)
+                new = {k: v.detach()[:10] * 1.5 for k, v in params.items()}
+                params = surgery.cat_params_to_optimizer(new, params, opt)
+        runs.append(params)
+    for k in base:
+        assert runs[0][k].shape == runs[1][k].shape
+        torch.testing.assert_close(runs[0][k].detach(), runs[1][k].detach(), rtol=1e-6, atol=1e-7)
