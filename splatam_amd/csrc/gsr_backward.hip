@@ -340,7 +340,7 @@ static auto bwd_variant() { return render_bwd_kernel<DUAL, OPAC, COL1, COL2, Q2>
 // The variant launch_render_bwd picks for (need, dual) and its record layout.
 RecLayout bwd_rec_layout(unsigned need, bool dual) {
     const bool op = need & NEED_OPACITY, c1 = need & NEED_COLORS, c2 = dual && (need & NEED_COLORS2);
-    const int q2 = (dual && (need & NEED_DL2_CH0_ONLY) && !op && !c1) ? 1 : 3;
+    const int q2 = (dual && (need & NEED_DL2_CH0_ONLY)) ? 1 : 3;
     RecLayout L;
     int nv = 5;
     L.o_op = op ? nv : -1;
@@ -366,6 +366,10 @@ hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint3
                : (c1 ? bwd_variant<false, 0, 1, 0>() : bwd_variant<false, 0, 0, 0>());
     } else if (q1 && !op && !c1) {  // SplaTAM tracking: depth-channel gradient only
         k = c2 ? bwd_variant<true, 0, 0, 1, 1>() : bwd_variant<true, 0, 0, 0, 1>();
+    } else if (q1) {  // SplaTAM mapping: every Gaussian gradient, depth channel of the second image
+        k = op ? (c1 ? (c2 ? bwd_variant<true, 1, 1, 1, 1>() : bwd_variant<true, 1, 1, 0, 1>())
+                     : (c2 ? bwd_variant<true, 1, 0, 1, 1>() : bwd_variant<true, 1, 0, 0, 1>()))
+               : (c2 ? bwd_variant<true, 0, 1, 1, 1>() : bwd_variant<true, 0, 1, 0, 1>());
     } else {
         k = op ? (c1 ? (c2 ? bwd_variant<true, 1, 1, 1>() : bwd_variant<true, 1, 1, 0>())
                      : (c2 ? bwd_variant<true, 1, 0, 1>() : bwd_variant<true, 1, 0, 0>()))
