@@ -39,7 +39,8 @@ def main(src, tag):
                    "correction of MI355X_MICROARCH.md HBM; gather widths are uncalibrated there)."}
     json.dump(out, open(f"{dst}/{tag}_summary.json", "w"), indent=1)
     rb = summary.get("render_bwd_kernel")
-    if rb:
+    headline = bench is not None and str(bench.get("metric", "")).startswith("rasterize fwd+bwd")
+    if rb and headline:  # bench.py's roofline.traffic of the headline (tracking) workload
         json.dump({"kernel": "render_bwd_kernel", "hbm_bytes_per_launch": rb["hbm_bytes_per_launch"],
                    "source": f"profiles/{tag}_summary.json"}, open(f"{dst}/render_bwd_pmc.json", "w"), indent=1)
     shutil.copy(f"{src}/bench.log", f"{dst}/{tag}_bench.log")
