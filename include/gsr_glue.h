@@ -31,6 +31,8 @@
 #ifndef GSR_GLUE_H
 #define GSR_GLUE_H
 
+#include "gsr.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -92,6 +94,29 @@ int gsr_track_l1_fwd_bwd(int H, int W, const float* im, const float* depth_sil, 
 int gsr_track_l1_bwd(int H, int W, const float* im, const float* depth_sil, const float* gt_im,
                      const float* gt_depth, float sil_thres, float w_im, float w_depth, const float* dL_dloss,
                      float* dL_dim, float* dL_ddepth_sil, void* stream);
+
+/* Tracking backward with the pose chain fused into the rasterizer's per-Gaussian
+ * backward: gsr_backward_dual's render backward (depth channel of the second
+ * image, no opacity / colour sums), then one per-Gaussian kernel whose
+ * dL/dmeans_cam, dL/d[z,1,z^2] and (anisotropic) dL/drotation feed the 16 pose
+ * sums of gsr_track_transform_bwd directly -- no per-Gaussian gradient reaches
+ * memory.  The last workgroup applies the pose chain and, with adam_state, the
+ * Adam step in place (gsr_track_transform_bwd_adam semantics); without it the
+ * pose gradient goes to dL_dcam_q / dL_dcam_t (stride q_stride).  settings,
+ * gaussians (camera-frame rendervars), radii, colors2 ([z,1,z^2]) and the buffers
+ * are those of the gsr_forward_dual(_static) call; means_world / unnorm_rot /
+ * scale_cols / cam_q / cam_t / w2c those of gsr_track_transform_fwd.  scratch:
+ * gsr_track_backward_scratch_floats(P) floats, zero-filled before first use,
+ * left zero-filled. */
+int gsr_track_backward_scratch_floats(int P);
+int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
+                            const float* colors2, const float* dL_dout_color, const float* dL_dout_color2,
+                            int num_rendered, const void* geom_buffer, const void* binning_buffer,
+                            const void* image_buffer, const float* means_world, const float* unnorm_rot,
+                            int scale_cols, float* cam_q, float* cam_t, int q_stride, const float* w2c, double lr_q,
+                            double lr_t, double beta1, double beta2, double eps, float* adam_state,
+                            float* dL_dcam_q, float* dL_dcam_t, float* scratch, gsr_alloc_fn alloc, void* alloc_ctx,
+                            void* stream);
 
 /* ------------------------------------------------------------------ mapping --
  * get_loss(mapping=True, do_ba=False) (scripts/splatam.py:220-353) with the

@@ -264,3 +264,35 @@ def mark_visible(means3D, viewmatrix, projmatrix):
         rc = lib.gsr_mark_visible(P, m.data_ptr(), v.data_ptr(), p.data_ptr(), present.data_ptr(), _stream(device))
         _check(rc, "mark_visible")
     return present
+
+
+def track_backward_dual(settings, means3D, radii, colors, colors2, scales, rotations, dL_dout_color, dL_dout_color2,
+                        geomBuffer, R, binningBuffer, imageBuffer, means_world, unnorm_rot, scale_cols, cam_q_ptr,
+                        cam_t_ptr, q_stride, w2c, scratch, adam=None, dq_ptr=None, dt_ptr=None):
+    """gsr_track_backward_dual (include/gsr_glue.h): the tracking backward with the pose chain fused into
+    the per-Gaussian backward.  adam = (lr_q, lr_t, beta1, beta2, eps, state tensor) applies the Adam step
+    to the pose in place; otherwise the pose gradient is written at dq_ptr / dt_ptr."""
+    device = means3D.device
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    with torch.cuda.device(device):
+        st = settings
+        s, keep_s = _settings(st.bg, st.viewmatrix, st.projmatrix, st.campos, st.tanfovx, st.tanfovy, H, W,
+                              st.scale_modifier, st.sh_degree, False, device)
+        g, keep_g, _ = _gaussians(means3D, None, colors, None, scales, rotations, None, device)
+        c2 = _dev_f32(colors2, device, "colors2")
+        dpix = _dev_f32(dL_dout_color, device, "dL_dout_color")
+        dpix2 = _dev_f32(dL_dout_color2, device, "dL_dout_color2")
+        lr_q = lr_t = b1 = b2 = eps = 0.0
+        state = None
+        if adam is not None:
+            lr_q, lr_t, b1, b2, eps, state = adam
+        _begin(device)
+        rc = lib.gsr_track_backward_dual(
+            ctypes.byref(s), ctypes.byref(g), radii.data_ptr(), _ptr(c2), dpix.data_ptr(), dpix2.data_ptr(), int(R),
+            geomBuffer.data_ptr(), binningBuffer.data_ptr() if binningBuffer.numel() else None,
+            imageBuffer.data_ptr(), means_world.data_ptr(), unnorm_rot.data_ptr(), int(scale_cols),
+            cam_q_ptr, cam_t_ptr, int(q_stride), w2c.data_ptr(), float(lr_q), float(lr_t), float(b1), float(b2),
+            float(eps), state.data_ptr() if state is not None else None, dq_ptr, dt_ptr, scratch.data_ptr(),
+            _ALLOC_CB, None, _stream(device))
+        _check(rc, "track_backward_dual")
+        _tls.buffers = {}

@@ -88,6 +88,12 @@ SIGNATURES = {
     "gsr_track_l1_fwd_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
                                      ctypes.c_float, ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p]),
+    "gsr_track_backward_scratch_floats": (c_int, [c_int]),
+    "gsr_track_backward_dual": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_int, c_void_p, c_void_p, c_int, c_void_p, c_double, c_double, c_double,
+                                        c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p, ALLOC_FN,
+                                        c_void_p, c_void_p]),
     # include/gsr_glue.h: fused SplaTAM mapping glue and optimizer
     "gsr_map_loss_scratch_floats": (c_int, [c_int, c_int]),
     "gsr_map_loss_state_floats": (c_int, [c_int, c_int]),

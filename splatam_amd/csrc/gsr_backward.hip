@@ -17,6 +17,7 @@
 #include <cstdlib>
 
 #include "gsr_chain.h"
+#include "gsr_glue_common.h"
 
 namespace gsr {
 
@@ -381,11 +382,13 @@ hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint3
     return hipGetLastError();
 }
 
+template <bool POSE>
 __global__ void __launch_bounds__(256)
 gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float* __restrict__ inst,
-                 RecLayout rec, GradsOut out, BwdGuard guard) {
+                 RecLayout rec, GradsOut out, BwdGuard guard, PoseFuse pf) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= g.P) return;
+    if (!POSE && i >= g.P) return;  // (POSE: every lane takes part in the workgroup sum)
+    const bool live = i < g.P;
     const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
     float g2[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float dcol2[3] = {0.f, 0.f, 0.f};
@@ -394,7 +397,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     float dsh[48];
 #pragma unroll
     for (int k = 0; k < 48; k++) dsh[k] = 0.f;
-    if (radii[i] > 0 && !guard.overflow()) {  // overflow: zero gradients, no record reads
+    if (live && radii[i] > 0 && !guard.overflow()) {  // overflow: zero gradients, no record reads
         const uint32_t off = geo.offsets[i], cnt = geo.tiles[i];
         // fixed-order sum of the Gaussian's instance records (deterministic)
         float acc[INST_REC_MAX];
@@ -437,6 +440,43 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         const unsigned clamped = geo.clamp[i];
         gauss_chain(cam, g, i, g2, clamped, dmean, dcov, dscale, drot, dsh, nsh);
     }
+    if constexpr (POSE) {
+        // tracking: the pose sums of this Gaussian (track_transform_bwd_kernel's, gsr_glue.hip), then
+        // one fixed-order workgroup sum, published; the last workgroup finishes the pose chain / Adam
+        __shared__ float s_red[4 * POSE_PARTS];
+        __shared__ float s_tot[POSE_PARTS];
+        float v[POSE_PARTS];
+#pragma unroll
+        for (int k = 0; k < POSE_PARTS; k++) v[k] = 0.f;
+        float c[4] = {0.f, 0.f, 0.f, 0.f};
+        if (pf.scols != 1) {
+            const Pose ps = make_pose(pf.cam_q, nullptr, pf.qs);
+#pragma unroll
+            for (int k = 0; k < 4; k++) c[k] = ps.c[k];
+        }
+        if (live)
+            pose_partials(v, i, dmean, dcol2, pf.scols != 1 ? drot : nullptr, pf.means_world, pf.unnorm_rot,
+                          g.means3D, pf.w2c, c);
+        block_sum<POSE_PARTS>(v, s_red, s_tot);
+        __syncthreads();
+        if (threadIdx.x < POSE_PARTS) st_agent(pf.part + POSE_PARTS * blockIdx.x + threadIdx.x, s_tot[threadIdx.x]);
+        const int nb = gridDim.x;
+        if (!last_block_arrive_grouped(reinterpret_cast<uint32_t*>(pf.part + POSE_PARTS * nb))) return;
+#pragma unroll
+        for (int k = 0; k < POSE_PARTS; k++) v[k] = 0.f;
+        for (int b = threadIdx.x; b < nb; b += 256)
+#pragma unroll
+            for (int k = 0; k < POSE_PARTS; k++) v[k] += ld_agent(pf.part + POSE_PARTS * b + k);
+        __syncthreads();
+        block_sum<POSE_PARTS>(v, s_red, s_tot);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const PoseAdam adam{pf.lr_q, pf.lr_t, pf.beta1, pf.beta2, (float)(1.0 - pf.beta1),
+                                (float)(1.0 - pf.beta2), (float)pf.eps, pf.adam_state, pf.cam_q, pf.cam_t};
+            pose_fin(s_tot, pf.cam_q, pf.qs, pf.dq, pf.dt, adam);
+        }
+        return;
+    }
     if (out.dmeans2D) {
         out.dmeans2D[3 * i] = g2[0];
         out.dmeans2D[3 * i + 1] = g2[1];
@@ -473,11 +513,17 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     }
 }
 
+int pose_fuse_scratch_floats(int P) { return POSE_PARTS * ((P + 255) / 256) + ARRIVE_GROUPED_WORDS; }
+
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* inst,
-                            RecLayout rec, const GradsOut& out, BwdGuard guard, hipStream_t s) {
+                            RecLayout rec, const GradsOut& out, BwdGuard guard, hipStream_t s, const PoseFuse* pose) {
     if (g.P == 0) return hipSuccess;
-    hipLaunchKernelGGL(gauss_bwd_kernel, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii, inst, rec, out,
-                       guard);
+    if (pose)
+        hipLaunchKernelGGL(gauss_bwd_kernel<true>, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii, inst,
+                           rec, out, guard, *pose);
+    else
+        hipLaunchKernelGGL(gauss_bwd_kernel<false>, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii,
+                           inst, rec, out, guard, PoseFuse{});
     return hipGetLastError();
 }
 

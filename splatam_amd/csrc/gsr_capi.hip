@@ -461,7 +461,8 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
                          const float* dL_dout_color, const float* colors2, const float* dL_dout_color2,
                          int num_rendered, const void* geom_buffer, const void* binning_buffer,
                          const void* image_buffer, int power, const gsr_grads* grads, float* dcolors2,
-                         int dl2_channels, gsr_alloc_fn alloc, void* alloc_ctx, void* stream_) {
+                         int dl2_channels, gsr_alloc_fn alloc, void* alloc_ctx, void* stream_,
+                         const PoseFuse* pose = nullptr) {
     int rc = validate(settings, gaussians, false);
     if (dl2_channels != 1 && dl2_channels != 3) return fail(GSR_ERR_INVALID_ARG, "dl2_channels must be 1 or 3");
     if (rc != GSR_OK) return rc;
@@ -487,7 +488,7 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     hipError_t e;
     GradsOut out{grads->dmeans2D, grads->dcolors, grads->dopacity, grads->dmeans3D,
                  grads->dcov3D,   grads->dsh,     grads->dscales,  grads->drotations};
-    if (!out.dmeans3D) return fail(GSR_ERR_INVALID_ARG, "dmeans3D output pointer required");
+    if (!out.dmeans3D && !pose) return fail(GSR_ERR_INVALID_ARG, "dmeans3D output pointer required");
     if (power != 1) {
         if (!out.dmeans2D || !out.dcolors || !out.dopacity || !out.dcov3D || !out.dscales || !out.drot)
             return fail(GSR_ERR_INVALID_ARG, "backward_power != 1 needs every gradient output pointer");
@@ -524,8 +525,10 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     }
     float* inst = nullptr;
     // SH colours feed dL/dmeans3D through the view direction, so their sums are needed with SH
-    const unsigned need = (out.dopacity ? NEED_OPACITY : 0u) | ((out.dcolors || g.shs) ? NEED_COLORS : 0u) |
-                          (dcolors2 ? NEED_COLORS2 : 0u) | (dl2_channels == 1 ? NEED_DL2_CH0_ONLY : 0u);
+    // pose-fused tracking backward: the pose needs the geometric sums and the depth colours only
+    const unsigned need = pose ? (NEED_COLORS2 | NEED_DL2_CH0_ONLY)
+                               : (out.dopacity ? NEED_OPACITY : 0u) | ((out.dcolors || g.shs) ? NEED_COLORS : 0u) |
+                                     (dcolors2 ? NEED_COLORS2 : 0u) | (dl2_channels == 1 ? NEED_DL2_CH0_ONLY : 0u);
     const RecLayout rec = bwd_rec_layout(need, colors2 != nullptr);
     // staged SH backward: gauss_bwd leaves dL/dcolor in a scratch array, sh_bwd turns it into dsh and the
     // view-direction term of dL/dmeans3D (gsr_sh.hip)
@@ -562,13 +565,38 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
             oc.dcolors = drgb;
             oc.dsh = nullptr;
         }
-        if ((e = launch_gauss_bwd(cam, gc, geo, radii, inst, rec, oc, guard, stream)) != hipSuccess)
+        if ((e = launch_gauss_bwd(cam, gc, geo, radii, inst, rec, oc, guard, stream, pose)) != hipSuccess)
             return hip_fail(e, "gaussian backward");
         if (shs_staged && (e = launch_sh_bwd(cam, g, geo, radii, drgb, out.dmeans3D, out.dsh, guard, stream)) !=
                               hipSuccess)
             return hip_fail(e, "sh backward");
     }
     return GSR_OK;
+}
+
+int gsr_track_backward_scratch_floats(int P) { return pose_fuse_scratch_floats(P < 1 ? 1 : P); }
+
+int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
+                            const float* colors2, const float* dL_dout_color, const float* dL_dout_color2,
+                            int num_rendered, const void* geom_buffer, const void* binning_buffer,
+                            const void* image_buffer, const float* means_world, const float* unnorm_rot,
+                            int scale_cols, float* cam_q, float* cam_t, int q_stride, const float* w2c, double lr_q,
+                            double lr_t, double beta1, double beta2, double eps, float* adam_state,
+                            float* dL_dcam_q, float* dL_dcam_t, float* scratch, gsr_alloc_fn alloc, void* alloc_ctx,
+                            void* stream) {
+    if (!gaussians || (scale_cols != 1 && scale_cols != 3) || q_stride < 1)
+        return fail(GSR_ERR_INVALID_ARG, "track_backward_dual: bad sizes");
+    if (!colors2 || !means_world || !unnorm_rot || !cam_q || !cam_t || !w2c || !scratch ||
+        (!adam_state && (!dL_dcam_q || !dL_dcam_t)))
+        return fail(GSR_ERR_INVALID_ARG, "track_backward_dual: null pointer");
+    if (scale_cols != 1 && !gaussians->rotations)
+        return fail(GSR_ERR_INVALID_ARG, "track_backward_dual: anisotropic maps need the rendered rotations");
+    PoseFuse pf{means_world, unnorm_rot, scale_cols, cam_q, cam_t, q_stride, w2c, scratch, adam_state,
+                lr_q, lr_t, beta1, beta2, eps, dL_dcam_q, dL_dcam_t};
+    gsr_grads none{};
+    return backward_impl(settings, gaussians, radii, dL_dout_color, colors2, dL_dout_color2, num_rendered,
+                         geom_buffer, binning_buffer, image_buffer, 1, &none, nullptr, 1, alloc, alloc_ctx, stream,
+                         &pf);
 }
 
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -880,8 +880,27 @@ struct GradsOut {
     float* drot;
     float* dcolors2;  // second colour set of a dual render (nullptr otherwise)
 };
+// Tracking (gsr_track_backward_dual): the pose gradient -- and the pose Adam step -- fused into
+// gauss_bwd, whose per-Gaussian dL/dmeans_cam, dL/d[z,1,z^2] and (anisotropic) dL/drotation
+// never leave registers.  Same maths as track_transform_bwd_kernel (gsr_glue.hip).
+struct PoseFuse {
+    const float* means_world;  // [P,3]
+    const float* unnorm_rot;   // [P,4]
+    int scols;                 // 1: isotropic map (rotation does not depend on the pose)
+    float* cam_q;              // frame's quaternion column (stride qs)
+    float* cam_t;              // frame's translation column (stride qs)
+    int qs;
+    const float* w2c;          // [16] row-major, depth colours
+    float* part;               // zero-filled scratch: 16 * nblocks partials + arrival counters
+    float* adam_state;         // 15 floats (nullptr: write dq / dt instead)
+    double lr_q, lr_t, beta1, beta2, eps;
+    float* dq;                 // gradient outputs when adam_state == nullptr
+    float* dt;
+};
+int pose_fuse_scratch_floats(int P);
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* inst,
-                            RecLayout rec, const GradsOut& out, BwdGuard guard, hipStream_t s);
+                            RecLayout rec, const GradsOut& out, BwdGuard guard, hipStream_t s,
+                            const PoseFuse* pose = nullptr);
 hipError_t launch_selftest_reduce9(const float* in, float* out, hipStream_t s);
 // gsr_sh.hip: SH colour stages with LDS-staged, coalesced coefficient traffic
 bool sh_staged(const Camera& cam, const GaussIn& g);

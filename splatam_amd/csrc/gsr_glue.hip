@@ -58,60 +58,6 @@ track_transform_fwd_kernel(int P, const float* __restrict__ mw, const float* __r
     for (int k = 0; k < 3; k++) scl[3 * i + k] = expf(ls[scols == 1 ? i : 3 * i + k]);
 }
 
-struct PoseAdam {  // torch.optim.Adam (no weight decay, no amsgrad) on the frame's pose column
-    double lr_q, lr_t, beta1, beta2;   // torch's hyperparameters are python floats (double)
-    float w1, omb2, eps;               // 1 - beta1, 1 - beta2 rounded from double, like torch's scalars
-    float* state;     // device: m_q[4], v_q[4], m_t[3], v_t[3], step
-    float* q;         // the frame's quaternion column (stride qs), updated in place
-    float* t;         // the frame's translation column (stride qs)
-};
-
-// torch/optim/adam.py (foreach form): exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
-// p.addcdiv_(exp_avg, sqrt(exp_avg_sq) / sqrt(1 - b2^s) + eps, -lr / (1 - b1^s)), the scalars
-// formed in double like torch's python floats.
-__device__ __forceinline__ void adam_update(float& p, float g, float& m, float& v, float neg_step, const PoseAdam& a,
-                                            float bc2_sqrt) {
-    m = m + a.w1 * (g - m);                      // exp_avg.lerp_(g, 1 - beta1)
-    v = v * (float)a.beta2;                      // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
-    v = v + a.omb2 * g * g;
-    const float denom = sqrtf(v) / bc2_sqrt + a.eps;
-    p = p + neg_step * (m / denom);
-}
-
-// The pose chain on the 16 summed terms S: dR -> dn (build_rotation) -> dc
-// (its own normalisation) -> dq (F.normalize), dt = S[0..2]; then either the
-// gradient is written (dq, dt) or the Adam step is applied in place.
-__device__ void pose_fin(const float* S, const float* cq, int qs, float* dq, float* dt, const PoseAdam& adam) {
-    const Pose ps = make_pose(cq, nullptr, qs);
-    // dR[j][k] = S[3 + 3j + k]; R = build_rotation(n), n = (r, x, y, z)
-    const float r = ps.n[0], x = ps.n[1], y = ps.n[2], z = ps.n[3];
-    const float d00 = S[3], d01 = S[4], d02 = S[5], d10 = S[6], d11 = S[7], d12 = S[8], d20 = S[9], d21 = S[10],
-                d22 = S[11];
-    const float4 dn = make_float4(
-        2.f * (-z * d01 + y * d02 + z * d10 - x * d12 - y * d20 + x * d21),
-        2.f * (y * d01 + z * d02 + y * d10 - 2.f * x * d11 - r * d12 + z * d20 + r * d21 - 2.f * x * d22),
-        2.f * (-2.f * y * d00 + x * d01 + r * d02 + x * d10 + z * d12 - r * d20 + z * d21 - 2.f * y * d22),
-        2.f * (-2.f * z * d00 - r * d01 + x * d02 + r * d10 - 2.f * z * d11 + y * d12 + x * d20 + y * d21));
-    // n = c / |c| (build_rotation, no eps), then c = q / max(|q|, eps) (F.normalize)
-    float4 dc = normalize4_bwd(make_float4(ps.n[0], ps.n[1], ps.n[2], ps.n[3]), ps.cn, dn);
-    dc.x += S[12]; dc.y += S[13]; dc.z += S[14]; dc.w += S[15];
-    const float4 g = normalize4_bwd(make_float4(ps.c[0], ps.c[1], ps.c[2], ps.c[3]), ps.qn, dc);
-    if (adam.state) {  // optimizer step fused here: the pose gradient never leaves the kernel
-        float* st = adam.state;
-        const float step = st[14] + 1.f;
-        st[14] = step;
-        const double bc1 = 1.0 - pow(adam.beta1, (double)step);
-        const float bc2_sqrt = (float)sqrt(1.0 - pow(adam.beta2, (double)step));
-        const float ss_q = (float)(-adam.lr_q / bc1), ss_t = (float)(-adam.lr_t / bc1);
-        const float gq[4] = {g.x, g.y, g.z, g.w};
-        for (int k = 0; k < 4; k++) adam_update(adam.q[k * qs], gq[k], st[k], st[4 + k], ss_q, adam, bc2_sqrt);
-        for (int k = 0; k < 3; k++) adam_update(adam.t[k * qs], S[k], st[8 + k], st[11 + k], ss_t, adam, bc2_sqrt);
-        return;
-    }
-    dq[0] = g.x; dq[qs] = g.y; dq[2 * qs] = g.z; dq[3 * qs] = g.w;
-    dt[0] = S[0]; dt[qs] = S[1]; dt[2 * qs] = S[2];
-}
-
 // Pose gradient in one launch: every workgroup publishes its partial of the 16
 // sums (sum g, sum g p^T, sum dquat_mult^T dr); the last one to arrive adds the
 // partials in a fixed order (bitwise reproducible) and runs pose_fin.
@@ -133,31 +79,10 @@ track_transform_bwd_kernel(int P, const float* __restrict__ mw, const float* __r
         const Pose ps = make_pose(cq, nullptr, qs);  // only c is used
         for (int k = 0; k < 4; k++) c[k] = ps.c[k];
     }
-    const float wz0 = w2c[8], wz1 = w2c[9], wz2 = w2c[10];
     for (int i = blockIdx.x * GLUE_BLOCK + threadIdx.x; i < P; i += gridDim.x * GLUE_BLOCK) {
-        float g0 = gm[3 * i], g1 = gm[3 * i + 1], g2 = gm[3 * i + 2];
-        if (gd) {  // colours [z, 1, z^2]: dz = dc0 + 2 z dc2, z = w2c[2,:3] . m + w2c[2,3]
-            const float z = wz0 * mc[3 * i] + wz1 * mc[3 * i + 1] + wz2 * mc[3 * i + 2] + w2c[11];
-            const float dz = gd[3 * i] + 2.f * z * gd[3 * i + 2];
-            g0 += dz * wz0; g1 += dz * wz1; g2 += dz * wz2;
-        }
-        const float p0 = mw[3 * i], p1 = mw[3 * i + 1], p2 = mw[3 * i + 2];
-        v[0] += g0; v[1] += g1; v[2] += g2;
-        v[3] += g0 * p0; v[4] += g0 * p1; v[5] += g0 * p2;
-        v[6] += g1 * p0; v[7] += g1 * p1; v[8] += g1 * p2;
-        v[9] += g2 * p0; v[10] += g2 * p1; v[11] += g2 * p2;
-        if (scols != 1 && gr) {
-            // rot = normalize(o), o = quat_mult(c, u), u = normalize(unnorm)
-            float un_norm, o_norm;
-            const float4 u = normalize4(load4(ur + 4 * i), un_norm);
-            const float4 o = quat_mult(c, u);
-            const float4 r = normalize4(o, o_norm);
-            const float4 d = normalize4_bwd(r, o_norm, load4(gr + 4 * i));
-            v[12] += d.x * u.x + d.y * u.y + d.z * u.z + d.w * u.w;
-            v[13] += -d.x * u.y + d.y * u.x - d.z * u.w + d.w * u.z;
-            v[14] += -d.x * u.z + d.y * u.w + d.z * u.x - d.w * u.y;
-            v[15] += -d.x * u.w - d.y * u.z + d.z * u.y + d.w * u.x;
-        }
+        const float g[3] = {gm[3 * i], gm[3 * i + 1], gm[3 * i + 2]};
+        pose_partials(v, i, g, gd ? gd + 3 * i : nullptr, (scols != 1 && gr) ? gr + 4 * i : nullptr, mw, ur, mc, w2c,
+                      c);
     }
     block_sum<POSE_PARTS>(v, s_red, s_tot);
     __syncthreads();

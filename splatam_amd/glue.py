@@ -400,3 +400,107 @@ class FusedAdam(torch.optim.Optimizer):
                                            torch.cuda.current_stream(dev).cuda_stream)
                 _check(rc, "adam_step")
         return loss
+
+
+# ------------------------------------------------- fused tracking iteration --
+class _TrackIteration(torch.autograd.Function):
+    """One SplaTAM tracking iteration (get_loss(tracking=True), scripts/splatam.py:220-353) whose backward
+    is gsr_track_backward_dual: render backward, then the per-Gaussian backward with the pose chain (and
+    the pose Adam step) fused in.  Differentiable w.r.t. the pose only, like track_transform."""
+
+    @staticmethod
+    def forward(ctx, cam_rots, cam_trans, params, curr, t, cfg, pose_adam, capacity, status, means2D, seed):
+        from . import _C
+        cam = curr["cam"]
+        cam_rots, cam_trans = _f32c(cam_rots, "cam_unnorm_rots"), _f32c(cam_trans, "cam_trans")
+        mw = _f32c(params["means3D"].detach(), "means3D")
+        ur = _f32c(params["unnorm_rotations"].detach(), "unnorm_rotations")
+        lo = _f32c(params["logit_opacities"].detach(), "logit_opacities")
+        ls = _f32c(params["log_scales"].detach(), "log_scales")
+        w2c = _f32c(curr["w2c"], "w2c")
+        T = cam_rots.shape[-1]
+        P, scols = mw.shape[0], ls.shape[1]
+        dev = mw.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        means, rot, dcol = torch.empty(P, 3, **f32), torch.empty(P, 4, **f32), torch.empty(P, 3, **f32)
+        opac, scales = torch.empty(P, 1, **f32), torch.empty(P, 3, **f32)
+        rc = lib.gsr_track_transform_fwd(P, mw.data_ptr(), ur.data_ptr(), lo.data_ptr(), ls.data_ptr(), scols,
+                                         cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c.data_ptr(),
+                                         means.data_ptr(), rot.data_ptr(), dcol.data_ptr(), opac.data_ptr(),
+                                         scales.data_ptr(), _stream(mw))
+        _check(rc, "track_transform_fwd")
+        rgb = _f32c(params["rgb_colors"].detach(), "rgb_colors")
+        empty = torch.Tensor([])
+        n, im, ds, radii, geom, binning, img, _ = _C.rasterize_gaussians_dual(
+            cam.bg, means, rgb, dcol, opac, scales, rot, cam.scale_modifier, empty, cam.viewmatrix, cam.projmatrix,
+            cam.tanfovx, cam.tanfovy, cam.image_height, cam.image_width, empty, cam.sh_degree, cam.campos,
+            cam.prefiltered, capacity=capacity, status=status)
+        gt_im, gt_d = _f32c(curr["im"], "gt_im"), _f32c(curr["depth"], "gt_depth")
+        H, W = cam.image_height, cam.image_width
+        loss = torch.empty((), **f32)
+        scratch = _scratch(mw, lib.gsr_track_scratch_floats(H * W))
+        ctx.pre = None
+        if seed is not None:  # static loss seed: the loss gradient images in the same pass
+            seed = _f32c(seed, "seed")
+            dim, dds = torch.empty_like(im), torch.empty_like(ds)
+            rc = lib.gsr_track_l1_fwd_bwd(H, W, im.data_ptr(), ds.data_ptr(), gt_im.data_ptr(), gt_d.data_ptr(),
+                                          float(cfg.sil_thres), float(cfg.w_im), float(cfg.w_depth), seed.data_ptr(),
+                                          loss.data_ptr(), dim.data_ptr(), dds.data_ptr(), scratch.data_ptr(),
+                                          _stream(mw))
+            ctx.pre = (dim, dds, seed)
+        else:
+            rc = lib.gsr_track_l1_fwd(H, W, im.data_ptr(), ds.data_ptr(), gt_im.data_ptr(), gt_d.data_ptr(),
+                                      float(cfg.sil_thres), float(cfg.w_im), float(cfg.w_depth), loss.data_ptr(),
+                                      scratch.data_ptr(), _stream(mw))
+        _check(rc, "track_l1")
+        ctx.save_for_backward(cam_rots, cam_trans, mw, ur, means, rot, dcol, scales, rgb, radii, geom, binning, img,
+                              im, ds, gt_im, gt_d, w2c)
+        ctx.meta = (t, T, scols, int(n), cam, cfg)
+        ctx.pose_adam = pose_adam
+        ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)
+        return loss, radii
+
+    @staticmethod
+    def backward(ctx, g, _g_radii):
+        from . import _C
+        (cam_rots, cam_trans, mw, ur, means, rot, dcol, scales, rgb, radii, geom, binning, img, im, ds, gt_im, gt_d,
+         w2c) = ctx.saved_tensors
+        t, T, scols, n, cam, cfg = ctx.meta
+        nones = (None,) * 11
+        if ctx.pre is not None and g is not None and g.data_ptr() == ctx.pre[2].data_ptr():
+            dim, dds = ctx.pre[0], ctx.pre[1]
+        else:
+            if g is None:
+                return nones
+            H, W = cam.image_height, cam.image_width
+            g = g.contiguous()
+            dim, dds = torch.empty_like(im), torch.empty_like(ds)
+            rc = lib.gsr_track_l1_bwd(H, W, im.data_ptr(), ds.data_ptr(), gt_im.data_ptr(), gt_d.data_ptr(),
+                                      float(cfg.sil_thres), float(cfg.w_im), float(cfg.w_depth), g.data_ptr(),
+                                      dim.data_ptr(), dds.data_ptr(), _stream(im))
+            _check(rc, "track_l1_bwd")
+        P = mw.shape[0]
+        scratch = _scratch(mw, lib.gsr_track_backward_scratch_floats(P))
+        opt = ctx.pose_adam
+        rot_in = rot  # the rendered (camera-frame) rotations: their gradient feeds the pose (anisotropic maps)
+        if opt is not None:
+            _C.track_backward_dual(cam, means, radii, rgb, dcol, scales, rot_in, dim, dds, geom, n, binning, img, mw,
+                                   ur, scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c,
+                                   scratch, adam=(opt.lr_q, opt.lr_t, float(opt.betas[0]), float(opt.betas[1]),
+                                                  opt.eps, opt.state))
+            return nones
+        dq, dt = torch.zeros_like(cam_rots), torch.zeros_like(cam_trans)
+        _C.track_backward_dual(cam, means, radii, rgb, dcol, scales, rot_in, dim, dds, geom, n, binning, img, mw, ur,
+                               scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c, scratch,
+                               dq_ptr=dq.data_ptr() + 4 * t, dt_ptr=dt.data_ptr() + 4 * t)
+        return (dq, dt) + (None,) * 9
+
+
+def tracking_iteration(params: dict, curr: dict, time_idx: int, cfg, pose_adam: PoseAdam | None = None,
+                       capacity: int = 0, status=None, seed=None):
+    """get_loss(tracking=True) as one fused forward (transform, dual rasterization, masked L1) whose backward
+    runs the render backward and the per-Gaussian backward with the pose chain (+ pose Adam) fused in:
+    no per-Gaussian gradient array, no separate pose-reduction launch.  Returns (loss, radii)."""
+    return _TrackIteration.apply(params["cam_unnorm_rots"], params["cam_trans"], params, curr, int(time_idx), cfg,
+                                 pose_adam, int(capacity), status, None, seed)

@@ -159,7 +159,7 @@ def _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg: TrackingConf
 
 
 def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = TrackingConfig(), fast=True,
-                      fused=True, dual=True):
+                      fused=True, dual=True, fuse_pose=False):
     """scripts/splatam.py:220-353 with tracking=True: two renders (RGB, [z,1,z^2]), masked L1 sums.
 
     fused=True (and fused_eligible): the pose transform / rendervar builders and
@@ -169,8 +169,14 @@ def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = Tr
     indexing `x[mask].sum()` becomes `where(mask, x, 0).sum()` (same value and
     gradient, NaNs outside the mask excluded exactly as indexing excludes them),
     and the pose transform avoids the K=P GEMM (see _affine).  fast=False is the
-    literal statement of the reference code."""
+    literal statement of the reference code.  fuse_pose=True (with fused, dual): one autograd node for the
+    whole iteration whose backward fuses the pose chain into the rasterizer's per-Gaussian backward
+    (glue.tracking_iteration, gsr_track_backward_dual)."""
     if fused and fast and fused_eligible(params, curr_data, cfg):
+        if fuse_pose and dual:
+            from .glue import tracking_iteration
+            loss, radius = tracking_iteration(params, curr_data, iter_time_idx, cfg)
+            return loss, radius, None
         return _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg, dual=dual)
     tg = transform_to_frame(params, iter_time_idx, gaussians_grad=False, camera_grad=True, fast=fast)
     rendervar = transformed_params2rendervar(params, tg)

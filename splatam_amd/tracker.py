@@ -49,10 +49,11 @@ def probe_num_rendered(params, curr_data, time_idx) -> tuple[int, int]:
 class GraphTracker:
     def __init__(self, params: dict, curr_data: dict, time_idx: int, iters_per_graph: int = 20,
                  cfg: TrackingConfig = TrackingConfig(), lrs=(0.0004, 0.002), headroom: float = 1.5,
-                 warmup_iters: int = 3, min_extra: int = 65536, timing: bool = False):
+                 warmup_iters: int = 3, min_extra: int = 65536, timing: bool = False, fuse_pose: bool = False):
         if not fused_eligible(params, curr_data, cfg):
             raise RuntimeError("GraphTracker needs the fused tracking configuration (only the pose requires grad)")
         self.params, self.curr, self.t, self.cfg = params, curr_data, time_idx, cfg
+        self.fuse_pose = fuse_pose  # pose chain + Adam inside the rasterizer's per-Gaussian backward
         dev = params["means3D"].device
         n, longest = probe_num_rendered(params, curr_data, time_idx)
         if longest > TILE_SORT_CAP:
@@ -86,6 +87,12 @@ class GraphTracker:
                 self.loss = self._iteration(k)
 
     def _iteration(self, k: int):
+        if self.fuse_pose:
+            from .glue import tracking_iteration
+            loss, _ = tracking_iteration(self.params, self.curr, self.t, self.cfg, pose_adam=self.adam,
+                                         capacity=self.capacity, status=self.status[k], seed=self.seed)
+            torch.autograd.backward(loss, self.seed)
+            return loss.detach()
         loss, _, _ = _get_loss_tracking_fused(self.params, self.curr, self.t, self.cfg, dual=True,
                                               capacity=self.capacity, status=self.status[k], pose_adam=self.adam,
                                               means2D=self.means2D, seed=self.seed)

@@ -30,7 +30,8 @@ def _setup(cuda, aniso):
 
 
 MODES = {"literal": dict(fast=False), "torch_fast": dict(fast=True, fused=False),
-         "fused": dict(fast=True, fused=True, dual=False), "fused_dual": dict(fast=True, fused=True, dual=True)}
+         "fused": dict(fast=True, fused=True, dual=False), "fused_dual": dict(fast=True, fused=True, dual=True),
+         "fused_pose": dict(fast=True, fused=True, dual=True, fuse_pose=True)}
 
 
 def _run(params, curr, mode):
@@ -39,11 +40,11 @@ def _run(params, curr, mode):
     p = dict(params, cam_unnorm_rots=rots, cam_trans=trans)
     loss, radius, means2D = get_loss_tracking(p, curr, 1, **MODES[mode])
     loss.backward()
-    return loss.item(), rots.grad.clone(), trans.grad.clone(), radius, means2D.grad
+    return loss.item(), rots.grad.clone(), trans.grad.clone(), radius, (means2D.grad if means2D is not None else None)
 
 
 @pytest.mark.parametrize("aniso", [False, True])
-@pytest.mark.parametrize("mode", ["torch_fast", "fused", "fused_dual"])
+@pytest.mark.parametrize("mode", ["torch_fast", "fused", "fused_dual", "fused_pose"])
 def test_glue_equals_literal(cuda, aniso, mode):
     """Loss within 1e-5 relative; pose gradients within 1e-4 (float32 reduction
     order differs; the L1 gradient is sign-based, so a pixel whose residual or
@@ -61,25 +62,28 @@ def test_glue_equals_literal(cuda, aniso, mode):
     assert float(l0) > 0.0 and float(r0.abs().sum()) > 0.0
     # means2D gradient of the RGB render (retained by the reference for densification stats);
     # the dual rasterization returns the sum over both images instead (documented)
-    if mode != "fused_dual":
+    if mode not in ("fused_dual", "fused_pose"):
         assert m1 is not None and float((m1 - m0).norm() / m0.norm()) <= 1e-3
 
 
-def test_fused_glue_deterministic(cuda):
+@pytest.mark.parametrize("mode", ["fused_dual", "fused_pose"])
+def test_fused_glue_deterministic(cuda, mode):
     params, curr = _setup(cuda, True)
-    a = _run(params, curr, "fused_dual")
-    b = _run(params, curr, "fused_dual")
+    a = _run(params, curr, mode)
+    b = _run(params, curr, mode)
     assert a[0] == b[0] and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
 
 
-def test_fused_glue_time_index_and_w2c(cuda):
+@pytest.mark.parametrize("mode", ["fused_dual", "fused_pose"])
+@pytest.mark.parametrize("aniso", [False, True])
+def test_fused_glue_time_index_and_w2c(cuda, mode, aniso):
     """Strided pose column (t = 1 of T = 2) and a non-identity w2c for the depth colours."""
-    params, curr = _setup(cuda, False)
+    params, curr = _setup(cuda, aniso)
     w2c = torch.eye(4, device=cuda)
     w2c[:3, 3] = torch.tensor([0.05, -0.02, 0.1], device=cuda)
     curr = dict(curr, w2c=w2c)
     l0, r0, t0, _, _ = _run(params, curr, "literal")
-    l1, r1, t1, _, _ = _run(params, curr, "fused_dual")
+    l1, r1, t1, _, _ = _run(params, curr, mode)
     assert abs(l0 - l1) <= 1e-5 * abs(l0)
     torch.testing.assert_close(r1, r0, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(t1, t0, rtol=1e-4, atol=1e-6)
@@ -93,7 +97,8 @@ def _pose_leaves(params):
     return p
 
 
-def test_graph_tracker_matches_eager_iterations(cuda):
+@pytest.mark.parametrize("fuse_pose", [False, True])
+def test_graph_tracker_matches_eager_iterations(cuda, fuse_pose):
     """HIP-graph replay (static-capacity forward, pose Adam fused into the transform
     backward) follows the pose trajectory of the same number of eager iterations
     with torch.optim.Adam (float rounding of the Adam update differs: 1e-6 abs)."""
@@ -109,7 +114,7 @@ def test_graph_tracker_matches_eager_iterations(cuda):
         loss.backward()
         opt.step()
     pg = _pose_leaves(params)
-    tr = GraphTracker(pg, curr, 1, iters_per_graph=S, warmup_iters=W)
+    tr = GraphTracker(pg, curr, 1, iters_per_graph=S, warmup_iters=W, fuse_pose=fuse_pose)
     tr.run()
     torch.cuda.synchronize()
     assert not tr.overflowed()
