@@ -95,6 +95,21 @@ int gsr_track_l1_bwd(int H, int W, const float* im, const float* depth_sil, cons
                      const float* gt_depth, float sil_thres, float w_im, float w_depth, const float* dL_dloss,
                      float* dL_dim, float* dL_ddepth_sil, void* stream);
 
+/* gsr_forward_dual_static with the tracking L1 loss (gsr_track_l1_fwd_bwd
+ * semantics) formed in the render's per-pixel epilogue: the loss (1 float) and
+ * its gradient images dL_dim [3,H,W] / dL_ddepth_sil [3,H,W] are written without
+ * reading the rendered images back; dL_dloss (device scalar, the caller's static
+ * loss seed) is read when the kernel runs.  scratch:
+ * gsr_track_forward_scratch_floats(W, H) floats, zero-filled before first use, left
+ * zero-filled.  The loss is valid iff the status reports no overflow. */
+int gsr_track_forward_scratch_floats(int image_width, int image_height);
+int gsr_track_forward_dual_static(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
+                                  int capacity, unsigned* status, float* out_color, float* out_color2,
+                                  float* out_depth, int* radii, const float* gt_im, const float* gt_depth,
+                                  float sil_thres, float w_im, float w_depth, const float* dL_dloss, float* loss,
+                                  float* dL_dim, float* dL_ddepth_sil, float* scratch, gsr_alloc_fn alloc,
+                                  void* alloc_ctx, void* stream);
+
 /* Tracking backward with the pose chain fused into the rasterizer's per-Gaussian
  * backward: gsr_backward_dual's render backward (depth channel of the second
  * image, no opacity / colour sums), then one per-Gaussian kernel whose

@@ -296,3 +296,38 @@ def track_backward_dual(settings, means3D, radii, colors, colors2, scales, rotat
             _ALLOC_CB, None, _stream(device))
         _check(rc, "track_backward_dual")
         _tls.buffers = {}
+
+
+def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scales, rotations, capacity, status, gt_im,
+                              gt_depth, sil_thres, w_im, w_depth, seed, scratch):
+    """gsr_track_forward_dual_static (include/gsr_glue.h): the static dual forward with SplaTAM's
+    tracking L1 loss and its gradient images formed in the render epilogue.  Returns (num_rendered=capacity,
+    color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth, loss, dL_dim, dL_ddepth_sil)."""
+    st = settings
+    device = means3D.device
+    P = means3D.size(0)
+    H, W = int(st.image_height), int(st.image_width)
+    f32 = dict(dtype=torch.float32, device=device)
+    with torch.cuda.device(device):
+        s, keep_s = _settings(st.bg, st.viewmatrix, st.projmatrix, st.campos, st.tanfovx, st.tanfovy, H, W,
+                              st.scale_modifier, st.sh_degree, st.prefiltered, device)
+        g, keep_g, _ = _gaussians(means3D, None, colors, opacity, scales, rotations, None, device)
+        c2 = _dev_f32(colors2, device, "colors2")
+        gi, gd, sd = (_dev_f32(gt_im, device, "gt_im"), _dev_f32(gt_depth, device, "gt_depth"),
+                      _dev_f32(seed, device, "seed"))
+        out_color, out_color2 = torch.empty(3, H, W, **f32), torch.empty(3, H, W, **f32)
+        out_depth = torch.empty(1, H, W, **f32)
+        radii = torch.empty(P, dtype=torch.int32, device=device)
+        loss = torch.empty((), **f32)
+        dim, dds = torch.empty(3, H, W, **f32), torch.empty(3, H, W, **f32)
+        if status is None or status.device != device or status.numel() < 4:
+            raise RuntimeError("static dual forward needs a device status tensor of 4 int32")
+        _begin(device)
+        n = lib.gsr_track_forward_dual_static(
+            ctypes.byref(s), ctypes.byref(g), _ptr(c2), int(capacity), status.data_ptr(), out_color.data_ptr(),
+            out_color2.data_ptr(), out_depth.data_ptr(), radii.data_ptr() if P else None, gi.data_ptr(),
+            gd.data_ptr(), float(sil_thres), float(w_im), float(w_depth), sd.data_ptr(), loss.data_ptr(),
+            dim.data_ptr(), dds.data_ptr(), scratch.data_ptr(), _ALLOC_CB, None, _stream(device))
+        _check(n, "track_forward_dual_static")
+        bufs = _tls.buffers
+        return (int(n), out_color, out_color2, radii, bufs[0], bufs[1], bufs[2], out_depth, loss, dim, dds)

@@ -88,6 +88,11 @@ SIGNATURES = {
     "gsr_track_l1_fwd_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
                                      ctypes.c_float, ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p]),
+    "gsr_track_forward_scratch_floats": (c_int, [c_int, c_int]),
+    "gsr_track_forward_dual_static": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p,
+                                              c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_void_p, ALLOC_FN, c_void_p, c_void_p]),
     "gsr_track_backward_scratch_floats": (c_int, [c_int]),
     "gsr_track_backward_dual": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

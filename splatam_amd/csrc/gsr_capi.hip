@@ -259,7 +259,8 @@ size_t gsr_image_buffer_bytes(int W, int H) { return ImgLayout::make(W, H).total
 // `status` and the call returns `capacity` (the layout size for the backward).
 static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
                         float* out_color, float* out_color2, float* out_depth, int* radii, gsr_alloc_fn alloc,
-                        void* alloc_ctx, void* stream_, int capacity = 0, uint32_t* status = nullptr) {
+                        void* alloc_ctx, void* stream_, int capacity = 0, uint32_t* status = nullptr,
+                        const TrackL1* l1 = nullptr) {
     int rc = validate(settings, gaussians, true);
     if (rc != GSR_OK) return rc;
     if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
@@ -389,7 +390,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         {
             StageTimer t(GSR_STAGE_RENDER_FWD, 0, stream, true);
             if ((e = launch_render_fwd(cam, ranges, point_list, geo, colors2, final_T, n_contrib, out_color,
-                                       out_color2, out_depth, guard, stream, t.kclock())) != hipSuccess)
+                                       out_color2, out_depth, guard, stream, t.kclock(), l1)) != hipSuccess)
                 return hip_fail(e, "render");
         }
         speculated = true;
@@ -451,7 +452,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     {
         StageTimer t(GSR_STAGE_RENDER_FWD, I, stream, true);
         if ((e = launch_render_fwd(cam, ranges, point_list, geo, colors2, final_T, n_contrib, out_color, out_color2,
-                                   out_depth, none, stream, t.kclock())) != hipSuccess)
+                                   out_depth, none, stream, t.kclock(), l1)) != hipSuccess)
             return hip_fail(e, "render");
     }
     return (int)I;
@@ -572,6 +573,26 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
             return hip_fail(e, "sh backward");
     }
     return GSR_OK;
+}
+
+int gsr_track_forward_scratch_floats(int image_width, int image_height) {
+    const int gx = (image_width + TILE_X - 1) / TILE_X, gy = (image_height + TILE_Y - 1) / TILE_Y;
+    return track_l1_fused_scratch_floats(gx * gy > 0 ? gx * gy : 1);
+}
+
+int gsr_track_forward_dual_static(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
+                                  int capacity, unsigned* status, float* out_color, float* out_color2,
+                                  float* out_depth, int* radii, const float* gt_im, const float* gt_depth,
+                                  float sil_thres, float w_im, float w_depth, const float* dL_dloss, float* loss,
+                                  float* dL_dim, float* dL_ddepth_sil, float* scratch, gsr_alloc_fn alloc,
+                                  void* alloc_ctx, void* stream) {
+    if (!colors2) return fail(GSR_ERR_INVALID_ARG, "colors2 required");
+    if (capacity <= 0 || !status) return fail(GSR_ERR_INVALID_ARG, "static mode needs capacity > 0 and status");
+    if (!gt_im || !gt_depth || !dL_dloss || !loss || !dL_dim || !dL_ddepth_sil || !scratch)
+        return fail(GSR_ERR_INVALID_ARG, "track_forward_dual_static: null pointer");
+    const TrackL1 l1{gt_im, gt_depth, sil_thres, w_im, w_depth, dL_dloss, dL_dim, dL_ddepth_sil, scratch, loss};
+    return forward_impl(settings, gaussians, colors2, out_color, out_color2, out_depth, radii, alloc, alloc_ctx,
+                        stream, capacity, status, &l1);
 }
 
 int gsr_track_backward_scratch_floats(int P) { return pose_fuse_scratch_floats(P < 1 ? 1 : P); }

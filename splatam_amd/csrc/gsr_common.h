@@ -848,10 +848,24 @@ hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* his
                              hipStream_t s);
 hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t* point_list, uint32_t n,
                              hipStream_t s);
+// SplaTAM's tracking L1 loss (get_loss tracking=True, scripts/splatam.py:262-296) and its
+// gradient images formed in the dual forward's per-pixel epilogue (gsr_track_forward_dual_static):
+// the same mask / sums / sign gradient as gsr_track_l1_fwd_bwd, without reading the images back.
+struct TrackL1 {
+    const float* gt_im;     // [3,H,W]
+    const float* gt_depth;  // [1,H,W]
+    float sil_thres, w_im, w_depth;
+    const float* seed;      // dL/dloss (device scalar, read when the kernel runs)
+    float* dL_dim;          // [3,H,W]
+    float* dL_dds;          // [3,H,W] (channels 1, 2 written as zero)
+    float* part;            // zero-filled scratch: 2 partials per tile + arrival counters
+    float* loss;            // device scalar
+};
+int track_l1_fused_scratch_floats(int ntiles);
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
-                             unsigned long long* clk = nullptr);
+                             unsigned long long* clk = nullptr, const TrackL1* l1 = nullptr);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* vis, hipStream_t s);
 // Per-(tile, Gaussian) instance record of the power-1 backward: the per-pair sums
 // the launched render_bwd variant forms, packed (no slots for absent terms):

@@ -722,12 +722,14 @@ hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t
 // DUAL: a second colour set (colors2, e.g. SplaTAM's [z, 1, z^2]) is composited
 // in the same pass -- same alpha / T / termination, so each output is bitwise
 // the image a separate call would produce.
-template <bool DUAL>
+// L1 (with DUAL): the tracking loss epilogue of TrackL1 (gsr_common.h).
+template <bool DUAL, bool L1 = false>
 __global__ void __launch_bounds__(TILE_PIX, 5)
 render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                   const float4* __restrict__ rr, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                   float* __restrict__ out_color, float* __restrict__ out_color2, float* __restrict__ out_depth,
-                  SpecGuard guard, unsigned long long* clk) {
+                  SpecGuard guard, unsigned long long* clk, TrackL1 l1) {
+    static_assert(DUAL || !L1, "the tracking loss needs the depth / silhouette colour set");
     kclock_begin(clk);
     if (guard.overflow()) {
         kclock_end(clk);
@@ -845,16 +847,78 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             out_color2[2 * HW + pid] = C5 + T * cam.bg[2];
         }
     }
+    if constexpr (L1) {
+        // get_loss(tracking=True) on this pixel (gsr_glue.hip track_l1_kernel, same expressions on the
+        // values just written): mask = gt_depth > 0 & !isnan(depth) & !isnan(depth_sq - depth^2) &
+        // silhouette > thres; sums of |gt - x| over the mask; dL/dx = -sgn(gt - x) * w * dL/dloss
+        __shared__ float s_red[4 * 4];
+        __shared__ float s_tot[4];
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (inside) {
+            const int pid = py * cam.W + px;
+            const int HW = cam.W * cam.H;
+            const float g = l1.seed[0];
+            const float im[3] = {C0 + T * cam.bg[0], C1 + T * cam.bg[1], C2 + T * cam.bg[2]};
+            const float d = C3 + T * cam.bg[0], sil = C4 + T * cam.bg[1], dsq = C5 + T * cam.bg[2];
+            const float gd = l1.gt_depth[pid];
+            const float unc = dsq - d * d;
+            const bool m = gd > 0.f && !isnan(d) && !isnan(unc) && sil > l1.sil_thres;
+            float gi[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) gi[c] = l1.gt_im[c * HW + pid];
+            if (m) {
+                v[0] = fabsf(gi[0] - im[0]) + fabsf(gi[1] - im[1]) + fabsf(gi[2] - im[2]);
+                v[1] = fabsf(gd - d);
+            }
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const float x = gi[c] - im[c];
+                l1.dL_dim[c * HW + pid] = m ? (g * l1.w_im) * (x > 0.f ? -1.f : (x < 0.f ? 1.f : 0.f)) : 0.f;
+            }
+            const float xd = gd - d;
+            l1.dL_dds[pid] = m ? (g * l1.w_depth) * (xd > 0.f ? -1.f : (xd < 0.f ? 1.f : 0.f)) : 0.f;
+            l1.dL_dds[HW + pid] = 0.f;
+            l1.dL_dds[2 * HW + pid] = 0.f;
+        }
+        // fixed-order workgroup sums, published; the last workgroup adds them in tile order
+        float r[1];
+        wave_reduce_n<4>(v, r);
+        const int lane = tid & 63, row4 = lane >> 4;
+        if ((lane & 15) == 0) s_red[w * 4 + row4] = r[0];
+        __syncthreads();
+        if (tid < 4) s_tot[tid] = (s_red[tid] + s_red[4 + tid]) + (s_red[8 + tid] + s_red[12 + tid]);
+        __syncthreads();
+        const int nb = gridDim.x * gridDim.y;
+        if (tid < 2) st_agent(l1.part + 2 * tile + tid, s_tot[tid]);
+        if (last_block_arrive_grouped(reinterpret_cast<uint32_t*>(l1.part + 2 * nb))) {
+            v[0] = v[1] = v[2] = v[3] = 0.f;
+            for (int b = tid; b < nb; b += TILE_PIX) {
+                v[0] += ld_agent(l1.part + 2 * b);
+                v[1] += ld_agent(l1.part + 2 * b + 1);
+            }
+            wave_reduce_n<4>(v, r);
+            if ((lane & 15) == 0) s_red[w * 4 + row4] = r[0];
+            __syncthreads();
+            if (tid == 0) {
+                const float s0 = (s_red[0] + s_red[4]) + (s_red[8] + s_red[12]);
+                const float s1 = (s_red[1] + s_red[5]) + (s_red[9] + s_red[13]);
+                l1.loss[0] = l1.w_im * s0 + l1.w_depth * s1;
+            }
+        }
+    }
     kclock_end(clk);
 }
+
+int track_l1_fused_scratch_floats(int ntiles) { return 2 * ntiles + ARRIVE_GROUPED_WORDS; }
 
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
-                             unsigned long long* clk) {
-    auto k = colors2 ? render_fwd_kernel<true> : render_fwd_kernel<false>;
+                             unsigned long long* clk, const TrackL1* l1) {
+    auto k = colors2 ? (l1 ? render_fwd_kernel<true, true> : render_fwd_kernel<true, false>)
+                     : render_fwd_kernel<false, false>;
     hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rr, final_T,
-                       n_contrib, out_color, out_color2, out_depth, guard, clk);
+                       n_contrib, out_color, out_color2, out_depth, guard, clk, l1 ? *l1 : TrackL1{});
     return hipGetLastError();
 }
 

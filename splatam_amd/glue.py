@@ -504,3 +504,59 @@ def tracking_iteration(params: dict, curr: dict, time_idx: int, cfg, pose_adam: 
     no per-Gaussian gradient array, no separate pose-reduction launch.  Returns (loss, radii)."""
     return _TrackIteration.apply(params["cam_unnorm_rots"], params["cam_trans"], params, curr, int(time_idx), cfg,
                                  pose_adam, int(capacity), status, None, seed)
+
+
+class _DualRenderL1(torch.autograd.Function):
+    """Static dual rasterization + SplaTAM's tracking L1 loss in one forward
+    (gsr_track_forward_dual_static: loss and gradient images from the render epilogue), backward
+    through gsr_backward_dual with the precomputed gradient images when seeded with the static seed."""
+
+    @staticmethod
+    def forward(ctx, means3D, colors, colors2, opacities, scales, rotations, st, capacity, status, gt_im, gt_depth,
+                cfg, seed):
+        from . import _C
+        H, W = st.image_height, st.image_width
+        scratch = _scratch(means3D, lib.gsr_track_forward_scratch_floats(W, H))
+        (n, im, ds, radii, geom, binning, img, _, loss, dim, dds) = _C.track_forward_dual_static(
+            st, means3D, colors, colors2, opacities, scales, rotations, capacity, status, gt_im, gt_depth,
+            cfg.sil_thres, cfg.w_im, cfg.w_depth, seed, scratch)
+        ctx.save_for_backward(colors, colors2, means3D, scales, rotations, radii, geom, binning, img, im, ds, gt_im,
+                              gt_depth)
+        ctx.meta = (st, int(n), cfg)
+        ctx.pre = (dim, dds, seed)
+        ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)
+        return loss, radii
+
+    @staticmethod
+    def backward(ctx, g, _g_radii):
+        from . import _C
+        colors, colors2, means3D, scales, rotations, radii, geom, binning, img, im, ds, gt_im, gt_d = ctx.saved_tensors
+        st, n, cfg = ctx.meta
+        if g is None:
+            return (None,) * 13
+        if g.data_ptr() == ctx.pre[2].data_ptr():
+            dim, dds = ctx.pre[0], ctx.pre[1]
+        else:
+            g = g.contiguous()
+            dim, dds = torch.empty_like(im), torch.empty_like(ds)
+            rc = lib.gsr_track_l1_bwd(st.image_height, st.image_width, im.data_ptr(), ds.data_ptr(), gt_im.data_ptr(),
+                                      gt_d.data_ptr(), float(cfg.sil_thres), float(cfg.w_im), float(cfg.w_depth),
+                                      g.data_ptr(), dim.data_ptr(), dds.data_ptr(), _stream(im))
+            _check(rc, "track_l1_bwd")
+        nd = ctx.needs_input_grad  # (means3D, colors, colors2, opacities, scales, rotations, ...)
+        needs = (False, nd[1], nd[2], nd[3], nd[0], False, False, nd[4], nd[5])
+        empty = torch.Tensor([])
+        (_, g_col, g_col2, g_op, g_m3, _, _, g_sc, g_rot) = _C.rasterize_gaussians_dual_backward(
+            st.bg, means3D, radii, colors, colors2, scales, rotations, st.scale_modifier, empty, st.viewmatrix,
+            st.projmatrix, st.tanfovx, st.tanfovy, dim, dds, empty, st.sh_degree, st.campos, geom, n, binning, img,
+            needs=needs, dl2_channels=1)
+        return (g_m3 if nd[0] else None, g_col, g_col2, g_op, g_sc, g_rot) + (None,) * 7
+
+
+def dual_render_tracking_l1(means3D, colors, colors2, opacities, scales, rotations, raster_settings, capacity, status,
+                            gt_im, gt_depth, cfg, seed):
+    """(loss, radii) of the tracking iteration's two renders + L1 loss, one static dual rasterization with
+    the loss formed in the render epilogue (HIP-graph capturable; check `status` for overflow)."""
+    return _DualRenderL1.apply(means3D, colors, colors2, opacities, scales, rotations, raster_settings, int(capacity),
+                               status, gt_im, gt_depth, cfg, seed)

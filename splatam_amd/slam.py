@@ -137,11 +137,15 @@ def _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg: TrackingConf
                              status=None, pose_adam=None, means2D=None, seed=None):
     """means2D: optional caller-owned [P,3] tensor (the tracker passes a static one without grad).
     seed: the static loss seed the caller will backward with (loss gradient formed in the forward)."""
-    from .glue import track_transform, tracking_l1
+    from .glue import dual_render_tracking_l1, track_transform, tracking_l1
     means, rots, dcol, opac, scales = track_transform(params, iter_time_idx, curr_data["w2c"], pose_adam)
     P = means.shape[0]
     if means2D is None:
         means2D = torch.zeros(P, 3, device=means.device, requires_grad=True)
+    if dual and capacity > 0 and seed is not None:  # static mode with a static seed: loss in the render epilogue
+        loss, radius = dual_render_tracking_l1(means, params["rgb_colors"], dcol, opac, scales, rots, curr_data["cam"],
+                                               capacity, status, curr_data["im"], curr_data["depth"], cfg, seed)
+        return loss, radius, means2D
     if dual:  # both renders in one rasterization (means2D.grad then holds the sum over both images)
         im, depth_sil, radius, _ = rasterize_gaussians_dual(means, means2D, None, params["rgb_colors"], dcol, opac,
                                                             scales, rots, None, curr_data["cam"], capacity, status,

@@ -182,3 +182,37 @@ def test_tracking_l1_seeded_forward_gradient(cuda):
     loss3 = tracking_l1(a3, ds, gt_im, gt_d, seed=torch.ones((), device=cuda))
     loss3.backward(torch.full((), 2.0, device=cuda))  # not the seed: computed in backward
     assert torch.equal(a3.grad, ref[1])
+
+
+@pytest.mark.parametrize("aniso", [False, True])
+def test_render_epilogue_l1_matches_separate_kernel(cuda, aniso):
+    """gsr_track_forward_dual_static (loss + gradient images in the render epilogue) against the static
+    dual forward followed by gsr_track_l1_fwd_bwd: images and gradient images bitwise equal, loss equal
+    up to the summation order, and the same backward gradients."""
+    from splatam_amd.glue import dual_render_tracking_l1, track_transform, tracking_l1
+    from splatam_amd.rasterizer import rasterize_gaussians_dual
+    from splatam_amd.slam import TrackingConfig
+    params, curr = _setup(cuda, aniso)
+    cfg = TrackingConfig()
+    seed = torch.ones((), device=cuda)
+    outs = []
+    for fused in (False, True):
+        p = _pose_leaves(params)
+        means, rots, dcol, opac, scales = track_transform(p, 1, curr["w2c"])
+        status = torch.zeros(4, dtype=torch.int32, device=cuda)
+        if fused:
+            loss, radii = dual_render_tracking_l1(means, p["rgb_colors"], dcol, opac, scales, rots, curr["cam"],
+                                                  400000, status, curr["im"], curr["depth"], cfg, seed)
+        else:
+            m2 = torch.zeros(means.shape[0], 3, device=cuda)
+            im, ds, radii, _ = rasterize_gaussians_dual(means, m2, None, p["rgb_colors"], dcol, opac, scales, rots,
+                                                        None, curr["cam"], 400000, status, grad2_channels=1)
+            loss = tracking_l1(im, ds, curr["im"], curr["depth"], cfg.sil_thres, cfg.w_im, cfg.w_depth, seed=seed)
+        torch.autograd.backward(loss, seed)
+        outs.append((float(loss), p["cam_unnorm_rots"].grad.clone(), p["cam_trans"].grad.clone(), radii.clone()))
+        assert int(status[0]) <= 400000 and int(status[1]) == 0
+    (l0, q0, t0, r0), (l1, q1, t1, r1) = outs
+    assert abs(l0 - l1) <= 1e-6 * abs(l0)
+    assert torch.equal(r0, r1)
+    torch.testing.assert_close(q1, q0, rtol=1e-6, atol=1e-9)
+    torch.testing.assert_close(t1, t0, rtol=1e-6, atol=1e-9)
