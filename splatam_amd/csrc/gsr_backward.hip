@@ -110,7 +110,7 @@ constexpr int bwd_waves() { return (DUAL && Q2 == 3) ? 4 : 5; }
 
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3>
 __global__ void __launch_bounds__(TILE_PIX, (bwd_waves<DUAL, OPAC, COL1, COL2, Q2>()))
-render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
+render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry* __restrict__ point_list,
                   const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
                   const float* __restrict__ final_T,
                   const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
@@ -176,7 +176,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     const int rm[4] = {(int)s_rmax[4 * w], (int)s_rmax[4 * w + 1], (int)s_rmax[4 * w + 2], (int)s_rmax[4 * w + 3]};
     // Instances behind every pixel's last contributor receive zero gradient.
     for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {
-        const uint32_t gk = point_list[k];
+        const uint32_t gk = pe_id(point_list[k]);
         const RenderRec r = load_rr(rr, gk);
         const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), blockIdx.x, blockIdx.y);
         float2* dst = reinterpret_cast<float2*>(inst + (size_t)RS * u);
@@ -207,10 +207,12 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     // Batch staging: thread t < batch holds entry t's render record (already in its
     // LDS form) for the next batch while the current one is rasterised.
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
-    uint32_t pu = 0;
+    uint32_t pu = 0, pm = 0;
     auto fetch = [&](int hi_) {
         if (tid < min(BB, hi_)) {
-            const uint32_t gi = point_list[range.x + (uint32_t)(hi_ - 1 - tid)];
+            const PointEntry pe = point_list[range.x + (uint32_t)(hi_ - 1 - tid)];
+            const uint32_t gi = pe_id(pe);
+            pm = pe_mask(pe);
             const RenderRec r = load_rr(rr, gi);
             pu = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), blockIdx.x, blockIdx.y);
             pa = r.q0; pb = r.q1; pc = r.q2;
@@ -226,7 +228,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             s_b[tid] = pb;
             s_c[tid] = pc;
             if (DUAL) s_d[tid] = pd;
-            s_mask[tid] = (uint16_t)block_mask(pa, pb, x0, y0);
+            s_mask[tid] = (uint16_t)pm;  // the instance's exact 4x4-block mask (sorted list entry)
         }
         for (int q = tid; q < 16 * SL * NV / 4; q += TILE_PIX)
             reinterpret_cast<float4*>(s_acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -370,7 +372,7 @@ RecLayout bwd_rec_layout(unsigned need, bool dual) {
     return L;
 }
 
-hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
+hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint64_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
                              const float* colors2, const float* dL_dpix2, unsigned need, float* inst,
                              BwdGuard guard, hipStream_t s, unsigned long long* clk) {

@@ -95,7 +95,7 @@ __device__ __forceinline__ float pow_pair(float x, int p) { return p == 2 ? x * 
 template <int NSH>
 __global__ void __launch_bounds__(TILE_PIX)
 render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __restrict__ ranges,
-                        const uint32_t* __restrict__ point_list, const float4* __restrict__ rr,
+                        const PointEntry* __restrict__ point_list, const float4* __restrict__ rr,
                         const uint32_t* __restrict__ blocksums,
                         const uint32_t* __restrict__ clamp_bits,
                         const float4* __restrict__ jac, const float* __restrict__ final_T,
@@ -138,7 +138,7 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
     __syncthreads();
     const uint32_t bmax = max(max(s_wmax[0], s_wmax[1]), max(s_wmax[2], s_wmax[3]));
     for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {
-        const uint32_t gk = point_list[k];
+        const uint32_t gk = pe_id(point_list[k]);
         const RenderRec r = load_rr(rr, gk);
         const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), blockIdx.x, blockIdx.y);
 #pragma unroll
@@ -154,7 +154,7 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
     for (int hi = (int)bmax; hi > 0; hi -= B) {
         const int cnt = min(B, hi);
         if (tid < cnt) {
-            const uint32_t gi = point_list[range.x + (uint32_t)(hi - 1 - tid)];
+            const uint32_t gi = pe_id(point_list[range.x + (uint32_t)(hi - 1 - tid)]);
             const RenderRec r = load_rr(rr, gi);
             const float4 pa = r.q0, pb = r.q1;
             s_g[tid] = gi;
@@ -273,7 +273,7 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
 }
 
 hipError_t launch_render_bwd_power(const Camera& cam, const GaussIn& g, const uint2* ranges,
-                                   const uint32_t* point_list, GeomPtrs geo, const float* jac, const float* final_T,
+                                   const uint64_t* point_list, GeomPtrs geo, const float* jac, const float* final_T,
                                    const uint32_t* n_contrib, const float* dL_dpix, int power, float* rec,
                                    BwdGuard guard, hipStream_t s) {
     const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;

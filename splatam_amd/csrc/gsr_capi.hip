@@ -356,19 +356,20 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     const uint32_t cap = capacity > 0 ? (uint32_t)capacity
                                       : (uint32_t)std::min(2.0e9, std::max(1024.0, 1.5 * ratio * P));
     auto bin_ptrs = [&](void* bin, const BinLayout& BL, uint64_t** keys, uint32_t** vals, uint32_t*& gid,
-                        uint32_t*& point_list, uint32_t*& hist) {
+                        uint64_t*& point_list, uint32_t*& hist) {
         char* bb = (char*)bin;
         keys[0] = (uint64_t*)(bb + BL.keys[0]);
         keys[1] = (uint64_t*)(bb + BL.keys[1]);
         vals[0] = (uint32_t*)(bb + BL.vals[0]);
         vals[1] = (uint32_t*)(bb + BL.vals[1]);
         gid = (uint32_t*)(bb + BL.gid);
-        point_list = (uint32_t*)(bb + BL.point_list);
+        point_list = (uint64_t*)(bb + BL.point_list);
         hist = (uint32_t*)(bb + BL.hist);
     };
     uint64_t* keys[2];
     uint32_t* vals[2];
-    uint32_t *gid, *point_list, *hist;
+    uint32_t *gid, *hist;
+    uint64_t* point_list;
     bool speculated = false;
     if (!force_radix) {
         const BinLayout SL = BinLayout::make((int)cap, W, H);
@@ -384,7 +385,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         }
         {
             StageTimer t(GSR_STAGE_SORT, 0, stream);
-            if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, guard, stream)) != hipSuccess)
+            if ((e = launch_tile_sort(ntiles, cam.gx, geo.rr, ranges, keys[0], point_list, guard, stream)) !=
+                hipSuccess)
                 return hip_fail(e, "tile sort");
         }
         {
@@ -426,7 +428,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         }
         {
             StageTimer t(GSR_STAGE_SORT, I, stream);
-            if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, none, stream)) != hipSuccess)
+            if ((e = launch_tile_sort(ntiles, cam.gx, geo.rr, ranges, keys[0], point_list, none, stream)) !=
+                hipSuccess)
                 return hip_fail(e, "tile sort");
         }
     } else if (I > 0) {
@@ -445,7 +448,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         }
         {
             StageTimer t(GSR_STAGE_RANGES, I, stream);
-            if ((e = launch_gather_ids(vals[BL.final_buf], gid, point_list, I, stream)) != hipSuccess)
+            if ((e = launch_gather_ids(vals[BL.final_buf], gid, keys[BL.final_buf], cam.gx, geo.rr, point_list, I,
+                                       stream)) != hipSuccess)
                 return hip_fail(e, "gather ids");
         }
     }
@@ -511,7 +515,7 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
                 return hip_fail(e, "gaussian jacobian");
         }
         if (num_rendered > 0) {
-            const uint32_t* point_list = (const uint32_t*)((const char*)binning_buffer + BL.point_list);
+            const uint64_t* point_list = (const uint64_t*)((const char*)binning_buffer + BL.point_list);
             StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream);
             if ((e = launch_render_bwd_power(cam, g, ranges, point_list, geo, jac, final_T, n_contrib, dL_dout_color,
                                              power, rec, BwdGuard{geo.counters, (uint32_t)num_rendered}, stream)) !=
@@ -547,7 +551,7 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
         if (!binning_buffer) return fail(GSR_ERR_INVALID_ARG, "missing binning buffer");
         inst = (float*)scratch;
         const char* bb = (const char*)binning_buffer;
-        const uint32_t* point_list = (const uint32_t*)(bb + BL.point_list);
+        const uint64_t* point_list = (const uint64_t*)(bb + BL.point_list);
         StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream, true);
         if ((e = launch_render_bwd(cam, ranges, point_list, geo, final_T, n_contrib, dL_dout_color, colors2,
                                    dL_dout_color2, need, inst, BwdGuard{geo.counters, (uint32_t)num_rendered},

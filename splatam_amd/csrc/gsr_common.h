@@ -94,7 +94,7 @@ inline int higher_msb(uint32_t n) {  // rasterizer_impl.cu:35-50 (bits needed fo
 constexpr int TILE_SORT_CAP = 4096;  // longest tile list sorted in LDS (32 KiB of u64 keys)
 
 struct BinLayout {        // per-instance state ("binningBuffer")
-    size_t point_list;    // u32 [I] Gaussian ids in (tile, depth, id) order -- always at offset 0
+    size_t point_list;    // u64 [I] PointEntry (mask << 32 | Gaussian id) in (tile, depth, id) order -- offset 0
     size_t keys[2];       // u64 [I] bucketed (depth<<32 | id) keys / radix ping-pong (tile<<32 | depth)
     size_t vals[2];       // u32 [I] radix ping-pong values (fallback path only)
     size_t gid;           // u32 [I] Gaussian id of each unsorted instance (fallback path only)
@@ -112,7 +112,7 @@ struct BinLayout {        // per-instance state ("binningBuffer")
         L.final_buf = L.npass & 1;
         L.nsb = (int)((n + SORT_TILE - 1) / SORT_TILE);
         size_t o = 0;
-        L.point_list = o; o = align_up(o + 4 * n, 256);
+        L.point_list = o; o = align_up(o + 8 * n, 256);
         L.keys[0] = o; o = align_up(o + 8 * n, 256);
         L.keys[1] = o; o = align_up(o + 8 * n, 256);
         L.vals[0] = o; o = align_up(o + 4 * n, 256);
@@ -424,6 +424,67 @@ __device__ __forceinline__ uint32_t block_mask(float4 a, float4 b, float x0, flo
         m |= ((mx >> cx) & (my >> cy) & 1u) << bi;
     }
     return m;
+}
+
+// Sorted tile list entries: (4x4-block mask << 32) | Gaussian id.  The mask is the
+// ellipse-exact block_mask_exact of the (tile, Gaussian) instance, computed once by
+// the pass that writes the sorted list (tile sort / gather), so the render kernels'
+// batch staging reads it instead of evaluating a mask per staged entry.
+typedef uint64_t PointEntry;
+__device__ __forceinline__ uint32_t pe_id(PointEntry p) { return (uint32_t)p; }
+__device__ __forceinline__ uint32_t pe_mask(PointEntry p) { return (uint32_t)(p >> 32); }
+
+// block_mask with the ellipse instead of its bounding box: per block row the
+// x-extent of the alpha >= 1/255 ellipse q(u) = A ux^2 + 2B ux uy + C uy^2 <= 2 tau
+// over the row's y-span is exact (the left boundary (-B uy - sqrt(2 tau A - det
+// uy^2)) / A is convex in uy, so its minimum over an interval is the leftmost
+// point uy = B sqrt(2 tau / (det C)) clamped to the interval; symmetrically on
+// the right); margins cover the float32 error.  ~10 % fewer pixel-pair
+// evaluations than the box on a frame (tools/tile_balance.py).
+__device__ __forceinline__ uint32_t block_mask_exact(float4 a, float4 b, float x0, float y0) {
+    float hx = 0.f, hy = 0.f;
+    bool never;
+    if (!alpha_extent(a, b, hx, hy, never)) return 0xFFFFu;
+    if (never) return 0u;
+    const float xl = a.x - hx, xh = a.x + hx, yl = a.y - hy, yh = a.y + hy;
+    uint32_t mx = 0, my = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        mx |= (xh >= x0 + 4.f * c && xl <= x0 + 4.f * c + 3.f) ? 1u << c : 0u;
+        my |= (yh >= y0 + 4.f * c && yl <= y0 + 4.f * c + 3.f) ? 1u << c : 0u;
+    }
+    if (!mx || !my) return 0u;
+    const float A = a.z * (1.f / K_AC), B = b.x * (1.f / K_B), C = a.w * (1.f / K_AC);
+    const float det = A * C - B * B;
+    const float kappa = A * C / det;
+    const float tau = fmaxf(__logf(255.f * b.y), 0.f) * (1.001f + 4e-6f * kappa) + 1e-3f;  // as alpha_extent
+    const float twoA_tau = 2.f * tau * A, inv_A = 1.f / A;
+    const float us = B * sqrtf(2.f * tau / (det * C));  // uy of the leftmost point (rightmost: -us)
+    const float eps = 0.02f + 0.002f * hx;
+    uint32_t m = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const float lo = fmaxf(y0 + 4.f * r - a.y, -hy), hi = fminf(y0 + 4.f * r + 3.f - a.y, hy);
+        const float ul = fminf(fmaxf(us, lo), hi), ur = fminf(fmaxf(-us, lo), hi);
+        const float wl = sqrtf(fmaxf(twoA_tau - det * ul * ul, 0.f)), wr = sqrtf(fmaxf(twoA_tau - det * ur * ur, 0.f));
+        const float xmin = a.x + (-B * ul - wl) * inv_A - eps, xmax = a.x + (-B * ur + wr) * inv_A + eps;
+        uint32_t cm = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) cm |= (xmax >= x0 + 4.f * c && xmin <= x0 + 4.f * c + 3.f) ? 1u << c : 0u;
+        cm &= ((my >> r) & 1u) ? mx : 0u;
+        // block (column c, row r) -> bit 4w + rr, w = 2 (r >> 1) + (c >> 1), rr = 2 (r & 1) + (c & 1)
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            m |= ((cm >> c) & 1u) << (4 * (2 * (r >> 1) + (c >> 1)) + 2 * (r & 1) + (c & 1));
+    }
+    return m;
+}
+// The sorted-list entry of Gaussian gi in tile (tx, ty).
+__device__ __forceinline__ PointEntry make_point_entry(const float4* __restrict__ rr, uint32_t gi, uint32_t tx,
+                                                       uint32_t ty) {
+    const uint32_t m = block_mask_exact(rr[(size_t)RR_F4 * gi], rr[(size_t)RR_F4 * gi + 1], (float)(tx * TILE_X),
+                                        (float)(ty * TILE_Y));
+    return ((PointEntry)m << 32) | gi;
 }
 
 // 4-bit mask of the 8x8-pixel wave quadrants of a tile (bit w: pixel centres
@@ -842,11 +903,13 @@ struct BwdGuard {
 };
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
                                    bool lds_hist, int ntiles, uint64_t* keys, int nb, SpecGuard guard, hipStream_t s);
-hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint32_t* point_list,
+hipError_t launch_tile_sort(int ntiles, int gx, const float4* rr, const uint2* ranges, const uint64_t* keys,
+                            uint64_t* point_list,
                             SpecGuard guard, hipStream_t s);
 hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t n, int nsb, int npass,
                              hipStream_t s);
-hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t* point_list, uint32_t n,
+hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, const uint64_t* keys, int gx, const float4* rr,
+                            uint64_t* point_list, uint32_t n,
                              hipStream_t s);
 // SplaTAM's tracking L1 loss (get_loss tracking=True, scripts/splatam.py:262-296) and its
 // gradient images formed in the dual forward's per-pixel epilogue (gsr_track_forward_dual_static):
@@ -862,7 +925,7 @@ struct TrackL1 {
     float* loss;            // device scalar
 };
 int track_l1_fused_scratch_floats(int ntiles);
-hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
+hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint64_t* point_list, GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
                              unsigned long long* clk = nullptr, const TrackL1* l1 = nullptr);
@@ -876,7 +939,7 @@ struct RecLayout {
     int o_op, o_c1, o_c2, n_c2; // offsets, -1 when absent
 };
 RecLayout bwd_rec_layout(unsigned need, bool dual);
-hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
+hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint64_t* point_list, GeomPtrs geo,
                              const float* final_T, const uint32_t* n_contrib, const float* dL_dpix,
                              const float* colors2, const float* dL_dpix2, unsigned need, float* inst, BwdGuard guard,
                              hipStream_t s, unsigned long long* clk = nullptr);
@@ -931,7 +994,7 @@ int power_record_floats(int nsh);  // values stored per instance record
 hipError_t launch_gauss_jac(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, float* jac,
                             hipStream_t s);
 hipError_t launch_render_bwd_power(const Camera& cam, const GaussIn& g, const uint2* ranges,
-                                   const uint32_t* point_list, GeomPtrs geo, const float* jac, const float* final_T,
+                                   const uint64_t* point_list, GeomPtrs geo, const float* jac, const float* final_T,
                                    const uint32_t* n_contrib, const float* dL_dpix, int power, float* rec,
                                    BwdGuard guard, hipStream_t s);
 hipError_t launch_gauss_bwd_power(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii,

@@ -506,9 +506,8 @@ __device__ __forceinline__ uint64_t bitonic_pick(uint64_t v, uint64_t o, bool ke
     return ((o < v) == keep_min) ? o : v;
 }
 
-template <int E>
-__device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, uint32_t* __restrict__ dst,
-                               uint64_t* sk) {
+template <int E, typename Emit>
+__device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, Emit emit, uint64_t* sk) {
     constexpr uint32_t n = 256u * E;
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t base = tid * E;
@@ -542,28 +541,31 @@ __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, u
     (void)lane;
 #pragma unroll
     for (int e = 0; e < E; e++)  // (a padding key can only land here through a network bug: emit id 0, never
-        if (base + e < cnt) dst[base + e] = v[e] == ~0ull ? 0u : (uint32_t)v[e];  // an out-of-range id)
+        if (base + e < cnt) emit(base + e, v[e] == ~0ull ? 0u : (uint32_t)v[e]);  // an out-of-range id)
 }
 
 __global__ void __launch_bounds__(TILE_SORT_THREADS)
-tile_sort_kernel(const uint2* __restrict__ ranges, const uint64_t* __restrict__ keys,
-                 uint32_t* __restrict__ point_list, SpecGuard guard) {
+tile_sort_kernel(int gx, const float4* __restrict__ rr, const uint2* __restrict__ ranges,
+                 const uint64_t* __restrict__ keys, uint64_t* __restrict__ point_list, SpecGuard guard) {
     __shared__ uint64_t sk[TILE_SORT_CAP];
     if (guard.overflow()) return;
     const uint2 range = ranges[blockIdx.x];
     const uint32_t cnt = range.y - range.x;
+    const uint32_t tx = blockIdx.x % (uint32_t)gx, ty = blockIdx.x / (uint32_t)gx;
+    PointEntry* dst = point_list + range.x;
+    // sorted entry i: Gaussian id plus the instance's exact 4x4-block mask
+    auto emit = [&](uint32_t i, uint32_t gi) { dst[i] = make_point_entry(rr, gi, tx, ty); };
     if (cnt <= 1) {
-        if (cnt == 1 && threadIdx.x == 0) point_list[range.x] = (uint32_t)keys[range.x];
+        if (cnt == 1 && threadIdx.x == 0) emit(0, (uint32_t)keys[range.x]);
         return;
     }
     const uint64_t* src = keys + range.x;
-    uint32_t* dst = point_list + range.x;
     if (cnt <= 256) {
-        tile_sort_regs<1>(src, cnt, dst, sk);
+        tile_sort_regs<1>(src, cnt, emit, sk);
     } else if (cnt <= 512) {
-        tile_sort_regs<2>(src, cnt, dst, sk);
+        tile_sort_regs<2>(src, cnt, emit, sk);
     } else if (cnt <= 1024) {
-        tile_sort_regs<4>(src, cnt, dst, sk);
+        tile_sort_regs<4>(src, cnt, emit, sk);
     } else {
         // long lists (<= TILE_SORT_CAP): the same network entirely through LDS -- more keys
         // per thread in registers would raise the whole kernel's VGPR count (occupancy 5 -> 3)
@@ -584,14 +586,14 @@ tile_sort_kernel(const uint2* __restrict__ ranges, const uint64_t* __restrict__ 
                 __syncthreads();
             }
         }
-        for (uint32_t i = threadIdx.x; i < cnt; i += TILE_SORT_THREADS) dst[i] = (uint32_t)sk[i];
+        for (uint32_t i = threadIdx.x; i < cnt; i += TILE_SORT_THREADS) emit(i, (uint32_t)sk[i]);
     }
 }
 
-hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint32_t* point_list,
-                            SpecGuard guard, hipStream_t s) {
+hipError_t launch_tile_sort(int ntiles, int gx, const float4* rr, const uint2* ranges, const uint64_t* keys,
+                            uint64_t* point_list, SpecGuard guard, hipStream_t s) {
     static_assert(TILE_SORT_THREADS == 256 && TILE_SORT_CAP <= 4096, "tile_sort_regs assumes 256 x E; sk holds the cap");
-    hipLaunchKernelGGL(tile_sort_kernel, dim3(ntiles), dim3(TILE_SORT_THREADS), 0, s, ranges, keys, point_list,
+    hipLaunchKernelGGL(tile_sort_kernel, dim3(ntiles), dim3(TILE_SORT_THREADS), 0, s, gx, rr, ranges, keys, point_list,
                        guard);
     return hipGetLastError();
 }
@@ -722,15 +724,21 @@ hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* his
 // Fallback path only: Gaussian ids of the radix-sorted instances (values are
 // unsorted instance indices).  Tile ranges already come from scan_counts_kernel.
 __global__ void gather_ids_kernel(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ gid,
-                                  uint32_t* __restrict__ point_list, uint32_t n) {
+                                  const uint64_t* __restrict__ keys, int gx, const float4* __restrict__ rr,
+                                  uint64_t* __restrict__ point_list, uint32_t n) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) point_list[k] = gid[vals[k]];
+    if (k < n) {  // sorted keys are (tile << 32 | depth)
+        const uint32_t tile = (uint32_t)(keys[k] >> 32);
+        point_list[k] = make_point_entry(rr, gid[vals[k]], tile % (uint32_t)gx, tile / (uint32_t)gx);
+    }
 }
 
-hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t* point_list, uint32_t n,
+hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, const uint64_t* keys, int gx, const float4* rr,
+                            uint64_t* point_list, uint32_t n,
                              hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(gather_ids_kernel, dim3((n + 255) / 256), dim3(256), 0, s, vals, gid, point_list, n);
+    hipLaunchKernelGGL(gather_ids_kernel, dim3((n + 255) / 256), dim3(256), 0, s, vals, gid, keys, gx, rr,
+                       point_list, n);
     return hipGetLastError();
 }
 
@@ -748,7 +756,7 @@ hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint32_t
 // L1 (with DUAL): the tracking loss epilogue of TrackL1 (gsr_common.h).
 template <bool DUAL, bool L1 = false>
 __global__ void __launch_bounds__(TILE_PIX, 5)
-render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
+render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry* __restrict__ point_list,
                   const float4* __restrict__ rr, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                   float* __restrict__ out_color, float* __restrict__ out_color2, float* __restrict__ out_depth,
                   SpecGuard guard, unsigned long long* clk, TrackL1 l1) {
@@ -779,6 +787,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
     float C3 = 0.f, C4 = 0.f, C5 = 0.f;
     uint32_t last = 0;
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
+    uint32_t pm = 0;  // the staged entry's 4x4-block mask (from the sorted list)
     if (tid == 0) {
         s_a[RENDER_BATCH] = pa;
         s_b[RENDER_BATCH] = pa;
@@ -786,9 +795,11 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
         if (DUAL) s_d[RENDER_BATCH] = pa;
     }
     if (range.x + tid < range.y) {
-        const RenderRec r = load_rr(rr, point_list[range.x + tid]);
+        const PointEntry pe = point_list[range.x + tid];
+        const RenderRec r = load_rr(rr, pe_id(pe));
         pa = r.q0; pb = r.q1; pc = r.q2;
         if (DUAL) pd = r.q3;
+        pm = pe_mask(pe);
     }
     for (uint32_t start = range.x; start < range.y; start += RENDER_BATCH) {
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
@@ -798,15 +809,17 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
             s_b[tid] = pb;
             s_c[tid] = pc;
             if (DUAL) s_d[tid] = pd;
-            s_mask[tid] = (uint16_t)block_mask(pa, pb, x0, y0);
+            s_mask[tid] = (uint16_t)pm;
         }
         __syncthreads();
         {   // prefetch the next batch while this one is rasterised
             const uint32_t k = start + RENDER_BATCH + tid;
             if (k < range.y) {
-                const RenderRec r = load_rr(rr, point_list[k]);
+                const PointEntry pe = point_list[k];
+                const RenderRec r = load_rr(rr, pe_id(pe));
                 pa = r.q0; pb = r.q1; pc = r.q2;
                 if (DUAL) pd = r.q3;
+                pm = pe_mask(pe);
             }
         }
         const int jmin0[4] = {0, 0, 0, 0};
@@ -934,7 +947,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const uint32_t* 
 
 int track_l1_fused_scratch_floats(int ntiles) { return 2 * ntiles + ARRIVE_GROUPED_WORDS; }
 
-hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint32_t* point_list, GeomPtrs geo,
+hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint64_t* point_list, GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
                              unsigned long long* clk, const TrackL1* l1) {

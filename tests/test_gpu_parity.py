@@ -282,3 +282,51 @@ def test_dual_render_depth_channel_only_gradient(cuda):
     assert harness.rel_l2(c2_lean[:, 0], c2_full[:, 0]) <= 1e-5
     assert np.all(c2_lean[:, 1:] == 0)
     assert np.abs(c2_full[:, 0]).sum() > 0
+
+
+@pytest.mark.parametrize("aniso", [False, True])
+def test_block_masks_are_conservative(cuda, aniso):
+    """The exact ellipse-vs-block masks carried by the sorted tile lists (block_mask_exact)
+    never drop a 4x4 block in which the Gaussian reaches alpha >= 1/255 at some pixel
+    (evaluated per pixel in float32 with the render kernels' formula), and cull blocks the
+    bounding box keeps."""
+    from splatam_amd import _C
+    from splatam_amd.layout import views
+    scene = make_scene(4000, 160, 112, seed=41, anisotropic=aniso)
+    c = scene.cam
+    dev = torch.device(cuda)
+    e = torch.Tensor([])
+    out = _C.rasterize_gaussians(torch.zeros(3, device=dev), scene.means3D.to(dev), scene.colors.to(dev),
+                                 scene.opacities.to(dev), scene.scales.to(dev), scene.rotations.to(dev), 1.0, e,
+                                 c.viewmatrix.to(dev), c.projmatrix.to(dev), c.tanfovx, c.tanfovy, c.H, c.W, e, 0,
+                                 c.campos.to(dev), False)
+    n, geom, binning, img = out[0], out[3], out[4], out[5]
+    v = views(img, binning, c.W, c.H, n)
+    P = scene.P
+    rr = geom[:64 * P].view(torch.float32).reshape(P, 16)
+    k_ac, k_b = -0.5 * 1.4426950408889634, -1.4426950408889634
+    x, y, A, C, B, o = rr[:, 0], rr[:, 1], rr[:, 2] / k_ac, rr[:, 3] / k_ac, rr[:, 4] / k_b, rr[:, 5]
+    rng = v["ranges"].long()
+    gx = (c.W + 15) // 16
+    tile_of = torch.repeat_interleave(torch.arange(rng.shape[0], device=dev), (rng[:, 1] - rng[:, 0]).clamp(min=0))
+    gid = v["point_list"].long()[:n]
+    mask = v["block_masks"].long()[:n] & 0xFFFF
+    ty, tx = tile_of // gx, tile_of % gx
+    ly, lx = torch.meshgrid(torch.arange(16, device=dev), torch.arange(16, device=dev), indexing="ij")
+    px = (tx * 16)[:, None, None] + lx[None]
+    py = (ty * 16)[:, None, None] + ly[None]
+    dx, dy = x[gid][:, None, None] - px, y[gid][:, None, None] - py
+    pw = -0.5 * (A[gid][:, None, None] * dx * dx + C[gid][:, None, None] * dy * dy) - B[gid][:, None, None] * dx * dy
+    al = torch.clamp(o[gid][:, None, None] * torch.exp(pw), max=0.99)
+    ok = (pw <= 0) & (al >= 1.0 / 255.0 * 0.999) & (px < c.W) & (py < c.H)
+    # block (cx, cy) of the tile -> mask bit 4 (2 (cy >> 1) + (cx >> 1)) + 2 (cy & 1) + (cx & 1)
+    blk = ok.reshape(-1, 4, 4, 4, 4).any(4).any(2)  # [inst, cy, cx]
+    bits = torch.zeros(n, dtype=torch.long, device=dev)
+    for cy in range(4):
+        for cx in range(4):
+            bit = 4 * (2 * (cy >> 1) + (cx >> 1)) + 2 * (cy & 1) + (cx & 1)
+            bits |= blk[:, cy, cx].long() << bit
+    missed = (bits & ~mask) != 0
+    assert int(missed.sum()) == 0, int(missed.sum())
+    kept = torch.stack([(mask >> b) & 1 for b in range(16)], 1).sum()
+    assert int(kept) < 16 * n  # it does cull
