@@ -99,6 +99,8 @@ struct BinLayout {        // per-instance state ("binningBuffer")
     size_t vals[2];       // u32 [I] radix ping-pong values (fallback path only)
     size_t gid;           // u32 [I] Gaussian id of each unsorted instance (fallback path only)
     size_t hist;          // u32 [RADIX * nsb] + [RADIX] digit totals (fallback path only)
+    size_t mask;          // u16 [I] block mask of each instance at its unsorted slot (duplicate -> render_fwd;
+                          //     the forward then stores it in the sorted entry for the backward)
     size_t total;
     int nsb;              // radix-sort workgroups
     int npass;            // 8-bit LSD passes over bits [0, 32 + msb(tiles))
@@ -119,6 +121,7 @@ struct BinLayout {        // per-instance state ("binningBuffer")
         L.vals[1] = o; o = align_up(o + 4 * n, 256);
         L.gid = o; o = align_up(o + 4 * n, 256);
         L.hist = o; o = align_up(o + 4 * ((size_t)RADIX * L.nsb + RADIX), 256);  // + digit totals
+        L.mask = o; o = align_up(o + 2 * n, 256);
         L.total = o;
         return L;
     }
@@ -427,9 +430,11 @@ __device__ __forceinline__ uint32_t block_mask(float4 a, float4 b, float x0, flo
 }
 
 // Sorted tile list entries: (4x4-block mask << 32) | Gaussian id.  The mask is the
-// ellipse-exact block_mask_exact of the (tile, Gaussian) instance, computed once by
-// the pass that writes the sorted list (tile sort / gather), so the render kernels'
-// batch staging reads it instead of evaluating a mask per staged entry.
+// ellipse-exact block_mask_exact of the (tile, Gaussian) instance, computed once per
+// instance by the duplicate pass (consecutive instances share their Gaussian's
+// record: cache-friendly) at the instance's unsorted slot; render_fwd looks it up
+// when it stages the entry and writes it into the entry's high half, where
+// render_bwd (which only stages entries render_fwd staged) reads it.
 typedef uint64_t PointEntry;
 __device__ __forceinline__ uint32_t pe_id(PointEntry p) { return (uint32_t)p; }
 __device__ __forceinline__ uint32_t pe_mask(PointEntry p) { return (uint32_t)(p >> 32); }
@@ -479,12 +484,11 @@ __device__ __forceinline__ uint32_t block_mask_exact(float4 a, float4 b, float x
     }
     return m;
 }
-// The sorted-list entry of Gaussian gi in tile (tx, ty).
-__device__ __forceinline__ PointEntry make_point_entry(const float4* __restrict__ rr, uint32_t gi, uint32_t tx,
-                                                       uint32_t ty) {
-    const uint32_t m = block_mask_exact(rr[(size_t)RR_F4 * gi], rr[(size_t)RR_F4 * gi + 1], (float)(tx * TILE_X),
-                                        (float)(ty * TILE_Y));
-    return ((PointEntry)m << 32) | gi;
+// The exact block mask of Gaussian gi's instance in tile (tx, ty).
+__device__ __forceinline__ uint16_t instance_mask(const float4* __restrict__ rr, uint32_t gi, uint32_t tx,
+                                                  uint32_t ty) {
+    return (uint16_t)block_mask_exact(rr[(size_t)RR_F4 * gi], rr[(size_t)RR_F4 * gi + 1], (float)(tx * TILE_X),
+                                      (float)(ty * TILE_Y));
 }
 
 // 4-bit mask of the 8x8-pixel wave quadrants of a tile (bit w: pixel centres
@@ -876,8 +880,8 @@ hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* t
 hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hipStream_t s);
 hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
                               uint2* ranges, uint32_t* status, hipStream_t s);
-hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid, int nb,
-                            hipStream_t s);
+hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid, uint16_t* masks,
+                            int nb, hipStream_t s);
 // Speculative launches: kernels exit early when the device-side counters show
 // num_rendered > cap_inst or a tile list longer than cap_tile (the host then
 // re-launches with an exact buffer).  Pass UINT32_MAX to disable the guard.
@@ -902,14 +906,13 @@ struct BwdGuard {
     }
 };
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
-                                   bool lds_hist, int ntiles, uint64_t* keys, int nb, SpecGuard guard, hipStream_t s);
-hipError_t launch_tile_sort(int ntiles, int gx, const float4* rr, const uint2* ranges, const uint64_t* keys,
-                            uint64_t* point_list,
+                                   bool lds_hist, int ntiles, uint64_t* keys, uint16_t* masks, int nb, SpecGuard guard,
+                                   hipStream_t s);
+hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint64_t* point_list,
                             SpecGuard guard, hipStream_t s);
 hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t n, int nsb, int npass,
                              hipStream_t s);
-hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, const uint64_t* keys, int gx, const float4* rr,
-                            uint64_t* point_list, uint32_t n,
+hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint64_t* point_list, uint32_t n,
                              hipStream_t s);
 // SplaTAM's tracking L1 loss (get_loss tracking=True, scripts/splatam.py:262-296) and its
 // gradient images formed in the dual forward's per-pixel epilogue (gsr_track_forward_dual_static):
@@ -925,7 +928,8 @@ struct TrackL1 {
     float* loss;            // device scalar
 };
 int track_l1_fused_scratch_floats(int ntiles);
-hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint64_t* point_list, GeomPtrs geo,
+hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* point_list, const uint16_t* masks,
+                             GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
                              unsigned long long* clk = nullptr, const TrackL1* l1 = nullptr);

@@ -353,7 +353,8 @@ hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, 
 
 // -------------------------------------------------------------- duplicate --
 __global__ void __launch_bounds__(PRE_BLOCK)
-duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, uint32_t* __restrict__ gid) {
+duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, uint32_t* __restrict__ gid,
+                 uint16_t* __restrict__ masks) {
     __shared__ uint32_t s_incl[PRE_BLOCK];   // inclusive scan of tiles touched
     __shared__ uint32_t s_x0[PRE_BLOCK], s_y0[PRE_BLOCK], s_w[PRE_BLOCK], s_depth[PRE_BLOCK];
     __shared__ uint32_t wsum[PRE_BLOCK / 64];
@@ -391,15 +392,17 @@ duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, u
         const uint32_t ty = s_y0[lo] + local / wdt;
         const uint32_t tx = s_x0[lo] + local % wdt;
         const uint32_t u = base + e;
+        const uint32_t gi = blockIdx.x * PRE_BLOCK + lo;
         keys[u] = ((uint64_t)(ty * (uint32_t)cam.gx + tx) << 32) | (uint64_t)s_depth[lo];
-        gid[u] = (uint32_t)(blockIdx.x * PRE_BLOCK + lo);
+        gid[u] = gi;
+        masks[u] = instance_mask(geo.rr, gi, tx, ty);
     }
 }
 
-hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid, int nb,
-                            hipStream_t s) {
+hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid, uint16_t* masks,
+                            int nb, hipStream_t s) {
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(duplicate_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, keys, gid);
+    hipLaunchKernelGGL(duplicate_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, keys, gid, masks);
     return hipGetLastError();
 }
 
@@ -410,7 +413,8 @@ hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* ke
 template <bool LDS_HIST>
 __global__ void __launch_bounds__(PRE_BLOCK)
 duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict__ ranges,
-                        uint32_t* __restrict__ cursor, int ntiles, uint64_t* __restrict__ keys, SpecGuard guard) {
+                        uint32_t* __restrict__ cursor, int ntiles, uint64_t* __restrict__ keys,
+                        uint16_t* __restrict__ masks, SpecGuard guard) {
     if (guard.overflow()) return;
     // LDS_HIST: cursor = the column-scanned count matrix; this workgroup's
     // instances of tile t go to ranges[t].x + cursor[block][t] + (LDS rank)
@@ -453,19 +457,23 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict
         const uint32_t tile = (s_y0[lo] + local / wdt) * (uint32_t)cam.gx + s_x0[lo] + local % wdt;
         const uint32_t pos = LDS_HIST ? atomicAdd(&s_cur[tile], 1u)
                                       : ranges[tile].x + atomicAdd(&cursor[tile * TILE_CTR_STRIDE], 1u);
-        keys[pos] = ((uint64_t)s_depth[lo] << 32) | (uint64_t)(blockIdx.x * PRE_BLOCK + lo);
+        const uint32_t gi = blockIdx.x * PRE_BLOCK + lo;
+        keys[pos] = ((uint64_t)s_depth[lo] << 32) | (uint64_t)gi;
+        // exact block mask at the unsorted slot (offsets[gi] + local = base + e)
+        masks[base + e] = instance_mask(geo.rr, gi, tile % (uint32_t)cam.gx, tile / (uint32_t)cam.gx);
     }
 }
 
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
-                                   bool lds_hist, int ntiles, uint64_t* keys, int nb, SpecGuard guard, hipStream_t s) {
+                                   bool lds_hist, int ntiles, uint64_t* keys, uint16_t* masks, int nb, SpecGuard guard,
+                                   hipStream_t s) {
     if (nb == 0) return hipSuccess;
     if (lds_hist)
         hipLaunchKernelGGL(duplicate_bucket_kernel<true>, dim3(nb), dim3(PRE_BLOCK), sizeof(uint32_t) * ntiles, s, cam,
-                           P, geo, ranges, cursor, ntiles, keys, guard);
+                           P, geo, ranges, cursor, ntiles, keys, masks, guard);
     else
         hipLaunchKernelGGL(duplicate_bucket_kernel<false>, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, ranges,
-                           cursor, ntiles, keys, guard);
+                           cursor, ntiles, keys, masks, guard);
     return hipGetLastError();
 }
 
@@ -545,16 +553,15 @@ __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, E
 }
 
 __global__ void __launch_bounds__(TILE_SORT_THREADS)
-tile_sort_kernel(int gx, const float4* __restrict__ rr, const uint2* __restrict__ ranges,
-                 const uint64_t* __restrict__ keys, uint64_t* __restrict__ point_list, SpecGuard guard) {
+tile_sort_kernel(const uint2* __restrict__ ranges, const uint64_t* __restrict__ keys,
+                 uint64_t* __restrict__ point_list, SpecGuard guard) {
     __shared__ uint64_t sk[TILE_SORT_CAP];
     if (guard.overflow()) return;
     const uint2 range = ranges[blockIdx.x];
     const uint32_t cnt = range.y - range.x;
-    const uint32_t tx = blockIdx.x % (uint32_t)gx, ty = blockIdx.x / (uint32_t)gx;
     PointEntry* dst = point_list + range.x;
-    // sorted entry i: Gaussian id plus the instance's exact 4x4-block mask
-    auto emit = [&](uint32_t i, uint32_t gi) { dst[i] = make_point_entry(rr, gi, tx, ty); };
+    // sorted entry i: the Gaussian id (render_fwd adds the block mask in the high half)
+    auto emit = [&](uint32_t i, uint32_t gi) { dst[i] = (PointEntry)gi; };
     if (cnt <= 1) {
         if (cnt == 1 && threadIdx.x == 0) emit(0, (uint32_t)keys[range.x]);
         return;
@@ -590,10 +597,10 @@ tile_sort_kernel(int gx, const float4* __restrict__ rr, const uint2* __restrict_
     }
 }
 
-hipError_t launch_tile_sort(int ntiles, int gx, const float4* rr, const uint2* ranges, const uint64_t* keys,
-                            uint64_t* point_list, SpecGuard guard, hipStream_t s) {
+hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint64_t* point_list,
+                            SpecGuard guard, hipStream_t s) {
     static_assert(TILE_SORT_THREADS == 256 && TILE_SORT_CAP <= 4096, "tile_sort_regs assumes 256 x E; sk holds the cap");
-    hipLaunchKernelGGL(tile_sort_kernel, dim3(ntiles), dim3(TILE_SORT_THREADS), 0, s, gx, rr, ranges, keys, point_list,
+    hipLaunchKernelGGL(tile_sort_kernel, dim3(ntiles), dim3(TILE_SORT_THREADS), 0, s, ranges, keys, point_list,
                        guard);
     return hipGetLastError();
 }
@@ -724,21 +731,15 @@ hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* his
 // Fallback path only: Gaussian ids of the radix-sorted instances (values are
 // unsorted instance indices).  Tile ranges already come from scan_counts_kernel.
 __global__ void gather_ids_kernel(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ gid,
-                                  const uint64_t* __restrict__ keys, int gx, const float4* __restrict__ rr,
                                   uint64_t* __restrict__ point_list, uint32_t n) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) {  // sorted keys are (tile << 32 | depth)
-        const uint32_t tile = (uint32_t)(keys[k] >> 32);
-        point_list[k] = make_point_entry(rr, gid[vals[k]], tile % (uint32_t)gx, tile / (uint32_t)gx);
-    }
+    if (k < n) point_list[k] = (PointEntry)gid[vals[k]];
 }
 
-hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, const uint64_t* keys, int gx, const float4* rr,
-                            uint64_t* point_list, uint32_t n,
+hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint64_t* point_list, uint32_t n,
                              hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(gather_ids_kernel, dim3((n + 255) / 256), dim3(256), 0, s, vals, gid, keys, gx, rr,
-                       point_list, n);
+    hipLaunchKernelGGL(gather_ids_kernel, dim3((n + 255) / 256), dim3(256), 0, s, vals, gid, point_list, n);
     return hipGetLastError();
 }
 
@@ -756,7 +757,8 @@ hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, const ui
 // L1 (with DUAL): the tracking loss epilogue of TrackL1 (gsr_common.h).
 template <bool DUAL, bool L1 = false>
 __global__ void __launch_bounds__(TILE_PIX, 5)
-render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry* __restrict__ point_list,
+render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __restrict__ point_list,
+                  const uint16_t* __restrict__ masks, const uint32_t* __restrict__ blocksums,
                   const float4* __restrict__ rr, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                   float* __restrict__ out_color, float* __restrict__ out_color2, float* __restrict__ out_depth,
                   SpecGuard guard, unsigned long long* clk, TrackL1 l1) {
@@ -787,7 +789,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     float C3 = 0.f, C4 = 0.f, C5 = 0.f;
     uint32_t last = 0;
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
-    uint32_t pm = 0;  // the staged entry's 4x4-block mask (from the sorted list)
+    uint32_t pm = 0, pg = 0;  // the staged entry's 4x4-block mask and Gaussian id
     if (tid == 0) {
         s_a[RENDER_BATCH] = pa;
         s_b[RENDER_BATCH] = pa;
@@ -795,11 +797,11 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         if (DUAL) s_d[RENDER_BATCH] = pa;
     }
     if (range.x + tid < range.y) {
-        const PointEntry pe = point_list[range.x + tid];
-        const RenderRec r = load_rr(rr, pe_id(pe));
+        pg = pe_id(point_list[range.x + tid]);
+        const RenderRec r = load_rr(rr, pg);
         pa = r.q0; pb = r.q1; pc = r.q2;
         if (DUAL) pd = r.q3;
-        pm = pe_mask(pe);
+        pm = masks[instance_slot(rr_rect(r), rr_offset(r, blocksums, pg), blockIdx.x, blockIdx.y)];
     }
     for (uint32_t start = range.x; start < range.y; start += RENDER_BATCH) {
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
@@ -810,16 +812,17 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             s_c[tid] = pc;
             if (DUAL) s_d[tid] = pd;
             s_mask[tid] = (uint16_t)pm;
+            point_list[start + tid] = ((PointEntry)pm << 32) | pg;  // the mask, for render_bwd
         }
         __syncthreads();
         {   // prefetch the next batch while this one is rasterised
             const uint32_t k = start + RENDER_BATCH + tid;
             if (k < range.y) {
-                const PointEntry pe = point_list[k];
-                const RenderRec r = load_rr(rr, pe_id(pe));
+                pg = pe_id(point_list[k]);
+                const RenderRec r = load_rr(rr, pg);
                 pa = r.q0; pb = r.q1; pc = r.q2;
                 if (DUAL) pd = r.q3;
-                pm = pe_mask(pe);
+                pm = masks[instance_slot(rr_rect(r), rr_offset(r, blocksums, pg), blockIdx.x, blockIdx.y)];
             }
         }
         const int jmin0[4] = {0, 0, 0, 0};
@@ -947,13 +950,15 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
 
 int track_l1_fused_scratch_floats(int ntiles) { return 2 * ntiles + ARRIVE_GROUPED_WORDS; }
 
-hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, const uint64_t* point_list, GeomPtrs geo,
+hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* point_list, const uint16_t* masks,
+                             GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
                              unsigned long long* clk, const TrackL1* l1) {
     auto k = colors2 ? (l1 ? render_fwd_kernel<true, true> : render_fwd_kernel<true, false>)
                      : render_fwd_kernel<false, false>;
-    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rr, final_T,
+    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, masks, geo.blocksums,
+                       geo.rr, final_T,
                        n_contrib, out_color, out_color2, out_depth, guard, clk, l1 ? *l1 : TrackL1{});
     return hipGetLastError();
 }

@@ -326,7 +326,15 @@ def test_block_masks_are_conservative(cuda, aniso):
         for cx in range(4):
             bit = 4 * (2 * (cy >> 1) + (cx >> 1)) + 2 * (cy & 1) + (cx & 1)
             bits |= blk[:, cy, cx].long() << bit
-    missed = (bits & ~mask) != 0
+    # the mask reaches the sorted entry when render_fwd stages it: every entry up to the tile's last
+    # contributor (the entries render_bwd stages)
+    nc = v["n_contrib"].reshape(c.H, c.W).long()
+    nc = torch.nn.functional.pad(nc, (0, gx * 16 - c.W, 0, ((c.H + 15) // 16) * 16 - c.H))
+    tile_last = nc.reshape((c.H + 15) // 16, 16, gx, 16).amax(dim=(1, 3)).reshape(-1)
+    pos = torch.arange(n, device=dev) - rng[tile_of, 0]
+    staged = pos < tile_last[tile_of]
+    missed = ((bits & ~mask) != 0) & staged
+    assert int(staged.sum()) > 0
     assert int(missed.sum()) == 0, int(missed.sum())
-    kept = torch.stack([(mask >> b) & 1 for b in range(16)], 1).sum()
-    assert int(kept) < 16 * n  # it does cull
+    kept = torch.stack([(mask[staged] >> b) & 1 for b in range(16)], 1).sum()
+    assert int(kept) < 16 * int(staged.sum())  # it does cull
