@@ -356,9 +356,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     const uint32_t cap = capacity > 0 ? (uint32_t)capacity
                                       : (uint32_t)std::min(2.0e9, std::max(1024.0, 1.5 * ratio * P));
     auto bin_ptrs = [&](void* bin, const BinLayout& BL, uint64_t** keys, uint32_t** vals, uint32_t*& gid,
-                        uint64_t*& point_list, uint32_t*& hist, uint16_t*& masks) {
+                        uint64_t*& point_list, uint32_t*& hist) {
         char* bb = (char*)bin;
-        masks = (uint16_t*)(bb + BL.mask);
         keys[0] = (uint64_t*)(bb + BL.keys[0]);
         keys[1] = (uint64_t*)(bb + BL.keys[1]);
         vals[0] = (uint32_t*)(bb + BL.vals[0]);
@@ -371,18 +370,17 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     uint32_t* vals[2];
     uint32_t *gid, *hist;
     uint64_t* point_list;
-    uint16_t* masks;
     bool speculated = false;
     if (!force_radix) {
         const BinLayout SL = BinLayout::make((int)cap, W, H);
         void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, SL.total);
         if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
-        bin_ptrs(bin, SL, keys, vals, gid, point_list, hist, masks);
+        bin_ptrs(bin, SL, keys, vals, gid, point_list, hist);
         const SpecGuard guard{geo.counters, cap, (uint32_t)TILE_SORT_CAP};
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
             if ((e = launch_duplicate_bucket(cam, P, geo, ranges, lds_hist ? cmat : cursor, lds_hist, ntiles, keys[0],
-                                             masks, GL.nb, guard, stream)) != hipSuccess)
+                                             GL.nb, guard, stream)) != hipSuccess)
                 return hip_fail(e, "duplicate");
         }
         {
@@ -392,7 +390,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         }
         {
             StageTimer t(GSR_STAGE_RENDER_FWD, 0, stream, true);
-            if ((e = launch_render_fwd(cam, ranges, point_list, masks, geo, colors2, final_T, n_contrib, out_color,
+            if ((e = launch_render_fwd(cam, ranges, point_list, geo, colors2, final_T, n_contrib, out_color,
                                        out_color2, out_depth, guard, stream, t.kclock(), l1)) != hipSuccess)
                 return hip_fail(e, "render");
         }
@@ -418,13 +416,13 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     const BinLayout BL = BinLayout::make((int)I, W, H);
     void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, BL.total);
     if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
-    bin_ptrs(bin, BL, keys, vals, gid, point_list, hist, masks);
+    bin_ptrs(bin, BL, keys, vals, gid, point_list, hist);
     const SpecGuard none{geo.counters, 0xffffffffu, 0xffffffffu};
     if (I > 0 && longest <= (uint32_t)TILE_SORT_CAP && !force_radix) {
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
             if ((e = launch_duplicate_bucket(cam, P, geo, ranges, lds_hist ? cmat : cursor, lds_hist, ntiles, keys[0],
-                                             masks, GL.nb, none, stream)) != hipSuccess)
+                                             GL.nb, none, stream)) != hipSuccess)
                 return hip_fail(e, "duplicate");
         }
         {
@@ -438,7 +436,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
             return hip_fail(e, "sort path flag");
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
-            if ((e = launch_duplicate(cam, P, geo, keys[0], gid, masks, GL.nb, stream)) != hipSuccess)
+            if ((e = launch_duplicate(cam, P, geo, keys[0], gid, GL.nb, stream)) != hipSuccess)
                 return hip_fail(e, "duplicate");
         }
         {
@@ -454,7 +452,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     }
     {
         StageTimer t(GSR_STAGE_RENDER_FWD, I, stream, true);
-        if ((e = launch_render_fwd(cam, ranges, point_list, masks, geo, colors2, final_T, n_contrib, out_color, out_color2,
+        if ((e = launch_render_fwd(cam, ranges, point_list, geo, colors2, final_T, n_contrib, out_color, out_color2,
                                    out_depth, none, stream, t.kclock(), l1)) != hipSuccess)
             return hip_fail(e, "render");
     }

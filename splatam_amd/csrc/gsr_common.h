@@ -99,8 +99,6 @@ struct BinLayout {        // per-instance state ("binningBuffer")
     size_t vals[2];       // u32 [I] radix ping-pong values (fallback path only)
     size_t gid;           // u32 [I] Gaussian id of each unsorted instance (fallback path only)
     size_t hist;          // u32 [RADIX * nsb] + [RADIX] digit totals (fallback path only)
-    size_t mask;          // u16 [I] block mask of each instance at its unsorted slot (duplicate -> render_fwd;
-                          //     the forward then stores it in the sorted entry for the backward)
     size_t total;
     int nsb;              // radix-sort workgroups
     int npass;            // 8-bit LSD passes over bits [0, 32 + msb(tiles))
@@ -121,7 +119,6 @@ struct BinLayout {        // per-instance state ("binningBuffer")
         L.vals[1] = o; o = align_up(o + 4 * n, 256);
         L.gid = o; o = align_up(o + 4 * n, 256);
         L.hist = o; o = align_up(o + 4 * ((size_t)RADIX * L.nsb + RADIX), 256);  // + digit totals
-        L.mask = o; o = align_up(o + 2 * n, 256);
         L.total = o;
         return L;
     }
@@ -429,12 +426,11 @@ __device__ __forceinline__ uint32_t block_mask(float4 a, float4 b, float x0, flo
     return m;
 }
 
-// Sorted tile list entries: (4x4-block mask << 32) | Gaussian id.  The mask is the
-// ellipse-exact block_mask_exact of the (tile, Gaussian) instance, computed once per
-// instance by the duplicate pass (consecutive instances share their Gaussian's
-// record: cache-friendly) at the instance's unsorted slot; render_fwd looks it up
-// when it stages the entry and writes it into the entry's high half, where
-// render_bwd (which only stages entries render_fwd staged) reads it.
+// Sorted tile list entries: (4x4-block mask << 32) | Gaussian id.  The sort writes
+// plain ids; render_fwd computes the ellipse-exact block_mask_exact of every entry
+// it stages (one per thread, from the render record it loads anyway) and writes
+// it into the entry's high half, where render_bwd (which only stages entries
+// render_fwd staged) reads it.
 typedef uint64_t PointEntry;
 __device__ __forceinline__ uint32_t pe_id(PointEntry p) { return (uint32_t)p; }
 __device__ __forceinline__ uint32_t pe_mask(PointEntry p) { return (uint32_t)(p >> 32); }
@@ -446,12 +442,44 @@ __device__ __forceinline__ uint32_t pe_mask(PointEntry p) { return (uint32_t)(p 
 // point uy = B sqrt(2 tau / (det C)) clamped to the interval; symmetrically on
 // the right); margins cover the float32 error.  ~10 % fewer pixel-pair
 // evaluations than the box on a frame (tools/tile_balance.py).
-__device__ __forceinline__ uint32_t block_mask_exact(float4 a, float4 b, float x0, float y0) {
+// The per-Gaussian half of block_mask_exact.  hx < 0: no culling (full mask);
+// hy < 0: never blended (empty mask).
+struct MaskGeom {
+    float ax, ay, hx, hy, B, inv_A, twoA_tau, det, us, eps;
+};
+constexpr int MASK_GEOM_F = 10;
+__device__ __forceinline__ MaskGeom mask_geom(float4 a, float4 b) {
+    MaskGeom g;
+    g.ax = a.x;
+    g.ay = a.y;
     float hx = 0.f, hy = 0.f;
     bool never;
-    if (!alpha_extent(a, b, hx, hy, never)) return 0xFFFFu;
-    if (never) return 0u;
-    const float xl = a.x - hx, xh = a.x + hx, yl = a.y - hy, yh = a.y + hy;
+    if (!alpha_extent(a, b, hx, hy, never)) {
+        g.hx = -1.f;
+        g.hy = 0.f;
+    } else if (never) {
+        g.hx = 0.f;
+        g.hy = -1.f;
+    } else {
+        g.hx = hx;
+        g.hy = hy;
+    }
+    const float A = a.z * (1.f / K_AC), B = b.x * (1.f / K_B), C = a.w * (1.f / K_AC);
+    const float det = A * C - B * B;
+    const float kappa = A * C / det;
+    const float tau = fmaxf(__logf(255.f * b.y), 0.f) * (1.001f + 4e-6f * kappa) + 1e-3f;  // as alpha_extent
+    g.B = B;
+    g.det = det;
+    g.twoA_tau = 2.f * tau * A;
+    g.inv_A = 1.f / A;
+    g.us = B * sqrtf(2.f * tau / (det * C));  // uy of the leftmost point (rightmost: -us)
+    g.eps = 0.02f + 0.002f * hx;
+    return g;
+}
+__device__ __forceinline__ uint32_t mask_of_geom(const MaskGeom& g, float x0, float y0) {
+    if (g.hx < 0.f) return 0xFFFFu;
+    if (g.hy < 0.f) return 0u;
+    const float xl = g.ax - g.hx, xh = g.ax + g.hx, yl = g.ay - g.hy, yh = g.ay + g.hy;
     uint32_t mx = 0, my = 0;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
@@ -459,20 +487,14 @@ __device__ __forceinline__ uint32_t block_mask_exact(float4 a, float4 b, float x
         my |= (yh >= y0 + 4.f * c && yl <= y0 + 4.f * c + 3.f) ? 1u << c : 0u;
     }
     if (!mx || !my) return 0u;
-    const float A = a.z * (1.f / K_AC), B = b.x * (1.f / K_B), C = a.w * (1.f / K_AC);
-    const float det = A * C - B * B;
-    const float kappa = A * C / det;
-    const float tau = fmaxf(__logf(255.f * b.y), 0.f) * (1.001f + 4e-6f * kappa) + 1e-3f;  // as alpha_extent
-    const float twoA_tau = 2.f * tau * A, inv_A = 1.f / A;
-    const float us = B * sqrtf(2.f * tau / (det * C));  // uy of the leftmost point (rightmost: -us)
-    const float eps = 0.02f + 0.002f * hx;
     uint32_t m = 0;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const float lo = fmaxf(y0 + 4.f * r - a.y, -hy), hi = fminf(y0 + 4.f * r + 3.f - a.y, hy);
-        const float ul = fminf(fmaxf(us, lo), hi), ur = fminf(fmaxf(-us, lo), hi);
-        const float wl = sqrtf(fmaxf(twoA_tau - det * ul * ul, 0.f)), wr = sqrtf(fmaxf(twoA_tau - det * ur * ur, 0.f));
-        const float xmin = a.x + (-B * ul - wl) * inv_A - eps, xmax = a.x + (-B * ur + wr) * inv_A + eps;
+        const float lo = fmaxf(y0 + 4.f * r - g.ay, -g.hy), hi = fminf(y0 + 4.f * r + 3.f - g.ay, g.hy);
+        const float ul = fminf(fmaxf(g.us, lo), hi), ur = fminf(fmaxf(-g.us, lo), hi);
+        const float wl = sqrtf(fmaxf(g.twoA_tau - g.det * ul * ul, 0.f));
+        const float wr = sqrtf(fmaxf(g.twoA_tau - g.det * ur * ur, 0.f));
+        const float xmin = g.ax + (-g.B * ul - wl) * g.inv_A - g.eps, xmax = g.ax + (-g.B * ur + wr) * g.inv_A + g.eps;
         uint32_t cm = 0;
 #pragma unroll
         for (int c = 0; c < 4; c++) cm |= (xmax >= x0 + 4.f * c && xmin <= x0 + 4.f * c + 3.f) ? 1u << c : 0u;
@@ -484,13 +506,9 @@ __device__ __forceinline__ uint32_t block_mask_exact(float4 a, float4 b, float x
     }
     return m;
 }
-// The exact block mask of Gaussian gi's instance in tile (tx, ty).
-__device__ __forceinline__ uint16_t instance_mask(const float4* __restrict__ rr, uint32_t gi, uint32_t tx,
-                                                  uint32_t ty) {
-    return (uint16_t)block_mask_exact(rr[(size_t)RR_F4 * gi], rr[(size_t)RR_F4 * gi + 1], (float)(tx * TILE_X),
-                                      (float)(ty * TILE_Y));
+__device__ __forceinline__ uint32_t block_mask_exact(float4 a, float4 b, float x0, float y0) {
+    return mask_of_geom(mask_geom(a, b), x0, y0);
 }
-
 // 4-bit mask of the 8x8-pixel wave quadrants of a tile (bit w: pixel centres
 // x0+8(w&1) .. +7, y0+8(w>>1) .. +7) that a Gaussian can contribute to.
 __device__ __forceinline__ uint32_t quad_mask(float4 a, float4 b, float x0, float y0) {
@@ -880,7 +898,7 @@ hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* t
 hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hipStream_t s);
 hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
                               uint2* ranges, uint32_t* status, hipStream_t s);
-hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid, uint16_t* masks,
+hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid,
                             int nb, hipStream_t s);
 // Speculative launches: kernels exit early when the device-side counters show
 // num_rendered > cap_inst or a tile list longer than cap_tile (the host then
@@ -906,7 +924,7 @@ struct BwdGuard {
     }
 };
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
-                                   bool lds_hist, int ntiles, uint64_t* keys, uint16_t* masks, int nb, SpecGuard guard,
+                                   bool lds_hist, int ntiles, uint64_t* keys, int nb, SpecGuard guard,
                                    hipStream_t s);
 hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint64_t* point_list,
                             SpecGuard guard, hipStream_t s);
@@ -928,7 +946,7 @@ struct TrackL1 {
     float* loss;            // device scalar
 };
 int track_l1_fused_scratch_floats(int ntiles);
-hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* point_list, const uint16_t* masks,
+hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* point_list,
                              GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,

@@ -353,8 +353,7 @@ hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, 
 
 // -------------------------------------------------------------- duplicate --
 __global__ void __launch_bounds__(PRE_BLOCK)
-duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, uint32_t* __restrict__ gid,
-                 uint16_t* __restrict__ masks) {
+duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, uint32_t* __restrict__ gid) {
     __shared__ uint32_t s_incl[PRE_BLOCK];   // inclusive scan of tiles touched
     __shared__ uint32_t s_x0[PRE_BLOCK], s_y0[PRE_BLOCK], s_w[PRE_BLOCK], s_depth[PRE_BLOCK];
     __shared__ uint32_t wsum[PRE_BLOCK / 64];
@@ -395,14 +394,13 @@ duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, u
         const uint32_t gi = blockIdx.x * PRE_BLOCK + lo;
         keys[u] = ((uint64_t)(ty * (uint32_t)cam.gx + tx) << 32) | (uint64_t)s_depth[lo];
         gid[u] = gi;
-        masks[u] = instance_mask(geo.rr, gi, tx, ty);
     }
 }
 
-hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid, uint16_t* masks,
+hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid,
                             int nb, hipStream_t s) {
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(duplicate_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, keys, gid, masks);
+    hipLaunchKernelGGL(duplicate_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, keys, gid);
     return hipGetLastError();
 }
 
@@ -414,7 +412,7 @@ template <bool LDS_HIST>
 __global__ void __launch_bounds__(PRE_BLOCK)
 duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict__ ranges,
                         uint32_t* __restrict__ cursor, int ntiles, uint64_t* __restrict__ keys,
-                        uint16_t* __restrict__ masks, SpecGuard guard) {
+                        SpecGuard guard) {
     if (guard.overflow()) return;
     // LDS_HIST: cursor = the column-scanned count matrix; this workgroup's
     // instances of tile t go to ranges[t].x + cursor[block][t] + (LDS rank)
@@ -459,21 +457,19 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict
                                       : ranges[tile].x + atomicAdd(&cursor[tile * TILE_CTR_STRIDE], 1u);
         const uint32_t gi = blockIdx.x * PRE_BLOCK + lo;
         keys[pos] = ((uint64_t)s_depth[lo] << 32) | (uint64_t)gi;
-        // exact block mask at the unsorted slot (offsets[gi] + local = base + e)
-        masks[base + e] = instance_mask(geo.rr, gi, tile % (uint32_t)cam.gx, tile / (uint32_t)cam.gx);
     }
 }
 
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
-                                   bool lds_hist, int ntiles, uint64_t* keys, uint16_t* masks, int nb, SpecGuard guard,
+                                   bool lds_hist, int ntiles, uint64_t* keys, int nb, SpecGuard guard,
                                    hipStream_t s) {
     if (nb == 0) return hipSuccess;
     if (lds_hist)
         hipLaunchKernelGGL(duplicate_bucket_kernel<true>, dim3(nb), dim3(PRE_BLOCK), sizeof(uint32_t) * ntiles, s, cam,
-                           P, geo, ranges, cursor, ntiles, keys, masks, guard);
+                           P, geo, ranges, cursor, ntiles, keys, guard);
     else
         hipLaunchKernelGGL(duplicate_bucket_kernel<false>, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, ranges,
-                           cursor, ntiles, keys, masks, guard);
+                           cursor, ntiles, keys, guard);
     return hipGetLastError();
 }
 
@@ -758,7 +754,6 @@ hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint64_t
 template <bool DUAL, bool L1 = false>
 __global__ void __launch_bounds__(TILE_PIX, 5)
 render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __restrict__ point_list,
-                  const uint16_t* __restrict__ masks, const uint32_t* __restrict__ blocksums,
                   const float4* __restrict__ rr, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                   float* __restrict__ out_color, float* __restrict__ out_color2, float* __restrict__ out_depth,
                   SpecGuard guard, unsigned long long* clk, TrackL1 l1) {
@@ -801,7 +796,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         const RenderRec r = load_rr(rr, pg);
         pa = r.q0; pb = r.q1; pc = r.q2;
         if (DUAL) pd = r.q3;
-        pm = masks[instance_slot(rr_rect(r), rr_offset(r, blocksums, pg), blockIdx.x, blockIdx.y)];
+        pm = block_mask_exact(pa, pb, x0, y0);
     }
     for (uint32_t start = range.x; start < range.y; start += RENDER_BATCH) {
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
@@ -822,7 +817,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
                 const RenderRec r = load_rr(rr, pg);
                 pa = r.q0; pb = r.q1; pc = r.q2;
                 if (DUAL) pd = r.q3;
-                pm = masks[instance_slot(rr_rect(r), rr_offset(r, blocksums, pg), blockIdx.x, blockIdx.y)];
+                pm = block_mask_exact(pa, pb, x0, y0);
             }
         }
         const int jmin0[4] = {0, 0, 0, 0};
@@ -950,14 +945,14 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
 
 int track_l1_fused_scratch_floats(int ntiles) { return 2 * ntiles + ARRIVE_GROUPED_WORDS; }
 
-hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* point_list, const uint16_t* masks,
+hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* point_list,
                              GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
                              unsigned long long* clk, const TrackL1* l1) {
     auto k = colors2 ? (l1 ? render_fwd_kernel<true, true> : render_fwd_kernel<true, false>)
                      : render_fwd_kernel<false, false>;
-    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, masks, geo.blocksums,
+    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list,
                        geo.rr, final_T,
                        n_contrib, out_color, out_color2, out_depth, guard, clk, l1 ? *l1 : TrackL1{});
     return hipGetLastError();
