@@ -298,6 +298,23 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     } else if ((e = zero_async(tile_count, 8 * (size_t)ntiles * TILE_CTR_STRIDE, stream)) != hipSuccess) {
         return hip_fail(e, "memset tile counts");
     }
+    static const bool force_radix_env = getenv("GSR_FORCE_RADIX") && atoi(getenv("GSR_FORCE_RADIX")) != 0;
+    const bool force_radix = force_radix_env && capacity <= 0;
+    // the bucketed duplicate does the instance / tile scans itself (lds_hist); otherwise a
+    // scan launch does them, and the counters are final right after it
+    const bool scan_in_duplicate = lds_hist && !force_radix;
+    auto snapshot_counters = [&]() -> int {  // num_rendered & co. to pinned host memory (eager mode)
+        if (!g_pinned.p) {
+            if ((e = hipHostMalloc((void**)&g_pinned.p, 16, hipHostMallocDefault)) != hipSuccess)
+                return hip_fail(e, "hipHostMalloc");
+        }
+        if (!g_pinned.ev && (e = hipEventCreateWithFlags(&g_pinned.ev, hipEventDisableTiming)) != hipSuccess)
+            return hip_fail(e, "hipEventCreate");
+        if ((e = hipMemcpyAsync(g_pinned.p, geo.counters, 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+            return hip_fail(e, "copy num_rendered");
+        if ((e = hipEventRecord(g_pinned.ev, stream)) != hipSuccess) return hip_fail(e, "record num_rendered");
+        return GSR_OK;
+    };
     if (P > 0) {
         if (!radii) return fail(GSR_ERR_INVALID_ARG, "radii output required");
         {
@@ -309,26 +326,17 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
             if ((e = launch_preprocess(cam, g, geo, radii, lds_hist ? cmat : tile_count, lds_hist, ntiles, GL.nb,
                                        stream)) != hipSuccess)
                 return hip_fail(e, "preprocess");
-            if (lds_hist) {  // column scan + instance / tile scans in one launch
+            if (lds_hist) {  // column scan (+ instance / tile scans in the same launch unless scan_in_duplicate)
                 if ((e = launch_tile_colscan(cmat, GL.nb, ntiles, tile_tot, geo, ranges,
-                                             capacity > 0 ? status : nullptr, stream)) != hipSuccess)
+                                             capacity > 0 ? status : nullptr, !scan_in_duplicate, stream)) !=
+                    hipSuccess)
                     return hip_fail(e, "tile count scan");
             } else if ((e = launch_scan_counts(geo, GL.nb, tile_count, TILE_CTR_STRIDE, ntiles, ranges,
                                                capacity > 0 ? status : nullptr, stream)) != hipSuccess) {
                 return hip_fail(e, "scan");
             }
         }
-        if (capacity <= 0) {
-            if (!g_pinned.p) {
-                if ((e = hipHostMalloc((void**)&g_pinned.p, 16, hipHostMallocDefault)) != hipSuccess)
-                    return hip_fail(e, "hipHostMalloc");
-            }
-            if (!g_pinned.ev && (e = hipEventCreateWithFlags(&g_pinned.ev, hipEventDisableTiming)) != hipSuccess)
-                return hip_fail(e, "hipEventCreate");
-            if ((e = hipMemcpyAsync(g_pinned.p, geo.counters, 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-                return hip_fail(e, "copy num_rendered");
-            if ((e = hipEventRecord(g_pinned.ev, stream)) != hipSuccess) return hip_fail(e, "record num_rendered");
-        }
+        if (capacity <= 0 && !scan_in_duplicate && (rc = snapshot_counters()) != GSR_OK) return rc;
     } else {
         if ((e = zero_async(ranges, sizeof(uint2) * (size_t)ntiles, stream)) != hipSuccess)
             return hip_fail(e, "memset ranges");
@@ -350,8 +358,6 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     // calls' instances-per-Gaussian ratio, so everything is enqueued before the
     // host waits on num_rendered (the reference blocks right after the scan,
     // rasterizer_impl.cu:282, leaving the GPU idle while it launches the rest).
-    static const bool force_radix_env = getenv("GSR_FORCE_RADIX") && atoi(getenv("GSR_FORCE_RADIX")) != 0;
-    const bool force_radix = force_radix_env && capacity <= 0;
     const double ratio = g_inst_ratio.load(std::memory_order_relaxed);
     const uint32_t cap = capacity > 0 ? (uint32_t)capacity
                                       : (uint32_t)std::min(2.0e9, std::max(1024.0, 1.5 * ratio * P));
@@ -379,10 +385,12 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         const SpecGuard guard{geo.counters, cap, (uint32_t)TILE_SORT_CAP};
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
-            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, lds_hist ? cmat : cursor, lds_hist, ntiles, keys[0],
-                                             GL.nb, guard, stream)) != hipSuccess)
+            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
+                                             ntiles, keys[0], GL.nb, guard, capacity > 0 ? status : nullptr,
+                                             stream)) != hipSuccess)
                 return hip_fail(e, "duplicate");
         }
+        if (capacity <= 0 && scan_in_duplicate && (rc = snapshot_counters()) != GSR_OK) return rc;
         {
             StageTimer t(GSR_STAGE_SORT, 0, stream);
             if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, guard, stream)) != hipSuccess)
@@ -421,8 +429,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     if (I > 0 && longest <= (uint32_t)TILE_SORT_CAP && !force_radix) {
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
-            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, lds_hist ? cmat : cursor, lds_hist, ntiles, keys[0],
-                                             GL.nb, none, stream)) != hipSuccess)
+            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
+                                             ntiles, keys[0], GL.nb, none, nullptr, stream)) != hipSuccess)
                 return hip_fail(e, "duplicate");
         }
         {

@@ -44,7 +44,8 @@ struct GeomLayout {       // per-Gaussian state ("geomBuffer")
     size_t bin;           // uint4  [P]  (rect lo, rect hi, depth bits, tiles) for duplicate
     size_t tiles;         // u32    [P]  tiles touched
     size_t offsets;       // u32    [P]  exclusive instance offset (also in q1.w)
-    size_t blocksums;     // u32    [nb] per-workgroup tile sums -> exclusive scan
+    size_t blocksums;     // u32    [nb] exclusive scan of the per-workgroup instance totals
+    size_t wgsum;         // u32    [nb] per-workgroup instance totals (bit 31: prefiltered violation)
     size_t counters;      // u32    [8]  [0]=num_rendered [1]=prefiltered violation [2]=longest tile list
                           //             [3]=sort cap [4]=colscan arrival counter
     size_t total;
@@ -59,6 +60,7 @@ struct GeomLayout {       // per-Gaussian state ("geomBuffer")
         L.tiles = o; o = align_up(o + 4 * p, 256);
         L.offsets = o; o = align_up(o + 4 * p, 256);
         L.blocksums = o; o = align_up(o + 4 * (size_t)(L.nb > 0 ? L.nb : 1), 256);
+        L.wgsum = o; o = align_up(o + 4 * (size_t)(L.nb > 0 ? L.nb : 1), 256);
         L.counters = o; o = align_up(o + 32, 256);
         L.total = o;
         return L;
@@ -159,11 +161,12 @@ struct GeomPtrs {
     uint32_t* offsets;
     uint32_t* blocksums;
     uint32_t* counters;
+    uint32_t* wgsum;
     static GeomPtrs at(void* base, const GeomLayout& L) {
         char* b = (char*)base;
         return {(float4*)(b + L.rr), (uint32_t*)(b + L.clamp), (uint4*)(b + L.bin), (uint32_t*)(b + L.tiles),
-                (uint32_t*)(b + L.offsets),
-                (uint32_t*)(b + L.blocksums), (uint32_t*)(b + L.counters)};
+                (uint32_t*)(b + L.offsets), (uint32_t*)(b + L.blocksums), (uint32_t*)(b + L.counters),
+                (uint32_t*)(b + L.wgsum)};
     }
 };
 
@@ -894,7 +897,7 @@ __device__ __forceinline__ uint32_t instance_slot(uint2 rect, uint32_t off, uint
 hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* counts,
                              bool lds_hist, int ntiles, int nb, hipStream_t s);
 hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, GeomPtrs geo, uint2* ranges,
-                               uint32_t* status, hipStream_t s);
+                               uint32_t* status, bool tail, hipStream_t s);
 hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hipStream_t s);
 hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
                               uint2* ranges, uint32_t* status, hipStream_t s);
@@ -923,9 +926,12 @@ struct BwdGuard {
         return counters[0] > cap_inst || counters[2] > counters[3];
     }
 };
-hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
-                                   bool lds_hist, int ntiles, uint64_t* keys, int nb, SpecGuard guard,
-                                   hipStream_t s);
+// lds_hist: the colscan ran without its scan tail; every workgroup scans the
+// workgroup and tile totals (`tot`) itself, workgroup 0 writes ranges,
+// counters and `status` (static mode; may be null).
+hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2* ranges, const uint32_t* tot,
+                                   uint32_t* cursor, bool lds_hist, int ntiles, uint64_t* keys, int nb,
+                                   SpecGuard guard, uint32_t* status, hipStream_t s);
 hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint64_t* point_list,
                             SpecGuard guard, hipStream_t s);
 hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t n, int nsb, int npass,

@@ -106,7 +106,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     }
     // workgroup scan of tiles touched: the local instance offset goes into the render
     // record (q1.w; the render kernels add the scanned workgroup base, blocksums[i >> 10]),
-    // the workgroup total into blocksums (input of the two-level scan)
+    // the workgroup total into wgsum (input of the two-level scan)
     __shared__ uint32_t wsum[PRE_BLOCK / 64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t incl = wave_incl_scan(tiles);
@@ -120,7 +120,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     }
     // top bit: prefiltered violation anywhere in the workgroup (folded into counters[1] by the scan)
     const bool viol = __syncthreads_or(violation);
-    if (threadIdx.x == PRE_BLOCK - 1) geo.blocksums[blockIdx.x] = (woff + incl) | (viol ? 0x80000000u : 0u);
+    if (threadIdx.x == PRE_BLOCK - 1) geo.wgsum[blockIdx.x] = (woff + incl) | (viol ? 0x80000000u : 0u);
     if (LDS_HIST)
         for (int t = threadIdx.x; t < ntiles; t += PRE_BLOCK) counts[(size_t)blockIdx.x * ntiles + t] = s_hist[t];
 }
@@ -146,16 +146,21 @@ hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, 
 // load passes: 16.5 us at config 3).
 constexpr int CS_TILES = 16, CS_PARTS = 64, CS_RQ = 16;
 template <bool AGENT_TILES>
-__device__ void scan_counts_body(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t* __restrict__ tile_count,
-                                 uint32_t tile_stride, uint32_t ntiles, uint2* __restrict__ ranges,
-                                 uint32_t* __restrict__ counters, uint32_t sort_cap, uint32_t* __restrict__ status);
+__device__ void scan_counts_body(const uint32_t* __restrict__ wgsum, uint32_t* __restrict__ blocksums, uint32_t nb,
+                                 const uint32_t* __restrict__ tile_count, uint32_t tile_stride, uint32_t ntiles,
+                                 uint2* __restrict__ ranges, uint32_t* __restrict__ counters, uint32_t sort_cap,
+                                 uint32_t* __restrict__ status);
 constexpr int SCAN_THREADS = 1024;
 constexpr int SCAN_ITEMS = 4;
 
-// ... and, in the same launch, the scan of scan_counts_kernel: the workgroups
-// publish their tile totals (agent-scope stores), the last one to finish scans
-// the workgroup sums and the tile totals (one launch instead of two; the arrival
-// counter is GeomLayout counters[4], zeroed by preprocess).
+// TAIL: ... and, in the same launch, the scan of scan_counts_kernel: the
+// workgroups publish their tile totals (agent-scope stores), the last one to
+// finish scans the workgroup sums and the tile totals (the arrival counter is
+// GeomLayout counters[4], zeroed by preprocess).  Without TAIL (the bucketed
+// path) every duplicate_bucket workgroup does those scans itself in its
+// prologue, which removes this launch's serial tail (arrival + one-workgroup
+// scan: ~10 us of latency at config 3).
+template <bool TAIL>
 __global__ void __launch_bounds__(CS_TILES * CS_PARTS)
 tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t* __restrict__ tot, GeomPtrs geo,
                     uint2* __restrict__ ranges, uint32_t sort_cap, uint32_t* __restrict__ status) {
@@ -199,17 +204,22 @@ tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t*
                 run += v;
             }
         }
-        if (q == CS_PARTS - 1) st_agent(&tot[t], run);
+        if (q == CS_PARTS - 1) {
+            if (TAIL) st_agent(&tot[t], run);
+            else tot[t] = run;
+        }
     }
+    if (!TAIL) return;
     if (!last_block_arrive(&geo.counters[4])) return;
-    scan_counts_body<true>(geo.blocksums, (uint32_t)nb, tot, 1u, (uint32_t)ntiles, ranges, geo.counters, sort_cap,
-                           status);
+    scan_counts_body<true>(geo.wgsum, geo.blocksums, (uint32_t)nb, tot, 1u, (uint32_t)ntiles, ranges, geo.counters,
+                           sort_cap, status);
 }
 
 hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, GeomPtrs geo, uint2* ranges,
-                               uint32_t* status, hipStream_t s) {
+                               uint32_t* status, bool tail, hipStream_t s) {
     static_assert(CS_TILES * CS_PARTS == SCAN_THREADS, "the last colscan workgroup runs the scan body");
-    hipLaunchKernelGGL(tile_colscan_kernel, dim3((ntiles + CS_TILES - 1) / CS_TILES), dim3(CS_TILES * CS_PARTS), 0, s,
+    hipLaunchKernelGGL(tail ? tile_colscan_kernel<true> : tile_colscan_kernel<false>,
+                       dim3((ntiles + CS_TILES - 1) / CS_TILES), dim3(CS_TILES * CS_PARTS), 0, s,
                        counts, nb, ntiles, tot, geo, ranges, (uint32_t)TILE_SORT_CAP, status);
     return hipGetLastError();
 }
@@ -266,9 +276,10 @@ hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hi
 // AGENT_TILES: the tile counts were published by other workgroups of the same
 // launch (tile_colscan_kernel's last workgroup) and are read with agent-scope loads.
 template <bool AGENT_TILES>
-__device__ void scan_counts_body(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t* __restrict__ tile_count,
-                                 uint32_t tile_stride, uint32_t ntiles, uint2* __restrict__ ranges,
-                                 uint32_t* __restrict__ counters, uint32_t sort_cap, uint32_t* __restrict__ status) {
+__device__ void scan_counts_body(const uint32_t* __restrict__ wgsum, uint32_t* __restrict__ blocksums, uint32_t nb,
+                                 const uint32_t* __restrict__ tile_count, uint32_t tile_stride, uint32_t ntiles,
+                                 uint2* __restrict__ ranges, uint32_t* __restrict__ counters, uint32_t sort_cap,
+                                 uint32_t* __restrict__ status) {
     // Writes all four counters (no reset needed): [0] num_rendered, [1] prefiltered violation
     // (top bits of the workgroup sums), [2] longest tile list, [3] sort_cap; and a copy to
     // `status` (static mode).
@@ -278,7 +289,7 @@ __device__ void scan_counts_body(uint32_t* __restrict__ blocksums, uint32_t nb, 
     if (tid == 0) s_viol = 0;
     for (int pass = 0; pass < 2; pass++) {
         const uint32_t n = pass == 0 ? nb : ntiles;
-        const uint32_t* src = pass == 0 ? blocksums : tile_count;
+        const uint32_t* src = pass == 0 ? wgsum : tile_count;
         if (tid == 0) { s_carry = 0; s_max = 0; }
         __syncthreads();
         uint32_t vmax = 0, viol = 0;
@@ -337,15 +348,17 @@ __device__ void scan_counts_body(uint32_t* __restrict__ blocksums, uint32_t nb, 
 }
 
 __global__ void __launch_bounds__(SCAN_THREADS)
-scan_counts_kernel(uint32_t* __restrict__ blocksums, uint32_t nb, const uint32_t* __restrict__ tile_count,
+scan_counts_kernel(const uint32_t* __restrict__ wgsum, uint32_t* __restrict__ blocksums, uint32_t nb,
+                   const uint32_t* __restrict__ tile_count,
                    uint32_t tile_stride, uint32_t ntiles, uint2* __restrict__ ranges,
                    uint32_t* __restrict__ counters, uint32_t sort_cap, uint32_t* __restrict__ status) {
-    scan_counts_body<false>(blocksums, nb, tile_count, tile_stride, ntiles, ranges, counters, sort_cap, status);
+    scan_counts_body<false>(wgsum, blocksums, nb, tile_count, tile_stride, ntiles, ranges, counters, sort_cap, status);
 }
 
 hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
                               uint2* ranges, uint32_t* status, hipStream_t s) {
-    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, geo.blocksums, (uint32_t)nb, tile_count,
+    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, geo.wgsum, geo.blocksums, (uint32_t)nb,
+                       tile_count,
                        (uint32_t)tile_stride, (uint32_t)ntiles, ranges, geo.counters, (uint32_t)TILE_SORT_CAP,
                        status);
     return hipGetLastError();
@@ -408,28 +421,140 @@ hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* ke
 // (slot from a per-tile cursor), keyed (depth bits << 32 | Gaussian id).  The
 // order inside a bucket is arbitrary; tile_sort_kernel restores the reference
 // order (depth, then id: cub's stable LSD sort, rasterizer_impl.cu:304-309).
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v += (uint32_t)__shfl_xor((int)v, m);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m));
+    return v;
+}
+
 template <bool LDS_HIST>
 __global__ void __launch_bounds__(PRE_BLOCK)
-duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict__ ranges,
+duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges, const uint32_t* __restrict__ tot,
                         uint32_t* __restrict__ cursor, int ntiles, uint64_t* __restrict__ keys,
-                        SpecGuard guard) {
-    if (guard.overflow()) return;
+                        SpecGuard guard, uint32_t sort_cap, uint32_t* __restrict__ status) {
     // LDS_HIST: cursor = the column-scanned count matrix; this workgroup's
-    // instances of tile t go to ranges[t].x + cursor[block][t] + (LDS rank)
+    // instances of tile t go to start[t] + cursor[block][t] + (LDS rank)
     extern __shared__ uint32_t s_cur[];
-    if (LDS_HIST)
-        for (int t = threadIdx.x; t < ntiles; t += PRE_BLOCK)
-            s_cur[t] = ranges[t].x + cursor[(size_t)blockIdx.x * ntiles + t];
     __shared__ uint32_t s_incl[PRE_BLOCK];
     __shared__ uint32_t s_x0[PRE_BLOCK], s_y0[PRE_BLOCK], s_w[PRE_BLOCK], s_depth[PRE_BLOCK];
     __shared__ uint32_t wsum[PRE_BLOCK / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int i = blockIdx.x * PRE_BLOCK + tid;
-    uint32_t t = (i < P) ? geo.tiles[i] : 0u;
+    // the Gaussian's tile count and rect, loaded ahead of the prologue's loads (one round trip)
+    const uint32_t t = (i < P) ? geo.tiles[i] : 0u;
+    const uint4 r = (i < P) ? geo.bin[i] : make_uint4(0u, 0u, 0u, 0u);  // (rect lo, rect hi, depth bits, tiles)
+    uint32_t base;
+    if (LDS_HIST) {
+        // The scans of scan_counts_body, redone by every workgroup (the inputs are
+        // a few KB, L2-resident): this workgroup's instance base from the raw
+        // workgroup totals, num_rendered, the prefiltered flag, and the exclusive
+        // scan of the tile totals (bucket starts).  Workgroup 0 publishes them
+        // (ranges, counters, status) for the later launches and the host.
+        constexpr int TPT = 4;  // tiles per thread kept in registers (<= 4096 tiles), else staged in LDS
+        __shared__ uint32_t s_red[5][PRE_BLOCK / 64];
+        const uint32_t b = blockIdx.x, nb = gridDim.x;
+        const int per = (ntiles + PRE_BLOCK - 1) / PRE_BLOCK;  // contiguous tiles per thread
+        const int t0 = min(ntiles, tid * per), t1 = min(ntiles, t0 + per);
+        const bool in_regs = per <= TPT;
+        uint32_t tv[TPT], cv[TPT];
+#pragma unroll
+        for (int k = 0; k < TPT; k++) {
+            const bool ok = in_regs && t0 + k < t1;
+            tv[k] = ok ? tot[t0 + k] : 0u;
+            cv[k] = ok ? cursor[(size_t)b * ntiles + t0 + k] : 0u;
+        }
+        uint32_t pre = 0, all = 0, viol = 0, vmax = 0;
+        for (uint32_t k = tid; k < nb; k += PRE_BLOCK) {
+            const uint32_t v = geo.wgsum[k];
+            viol |= v >> 31;
+            all += v & 0x7fffffffu;
+            pre += k < b ? (v & 0x7fffffffu) : 0u;
+        }
+        uint32_t csum = 0;
+        if (in_regs) {
+#pragma unroll
+            for (int k = 0; k < TPT; k++) {
+                csum += tv[k];
+                vmax = max(vmax, tv[k]);
+            }
+        } else {
+            for (int u = t0; u < t1; u++) {
+                const uint32_t v = tot[u];
+                s_cur[u] = v;
+                csum += v;
+                vmax = max(vmax, v);
+            }
+        }
+        const uint32_t cincl = wave_incl_scan(csum);
+        pre = wave_sum_u32(pre);
+        all = wave_sum_u32(all);
+        viol = wave_max_u32(viol);
+        vmax = wave_max_u32(vmax);
+        if (lane == 0) {
+            s_red[0][w] = pre;
+            s_red[1][w] = all;
+            s_red[2][w] = viol;
+            s_red[3][w] = vmax;
+        }
+        if (lane == 63) s_red[4][w] = cincl;
+        __syncthreads();
+        uint32_t woff = 0;
+        pre = all = viol = vmax = 0;
+#pragma unroll
+        for (int k = 0; k < PRE_BLOCK / 64; k++) {
+            pre += s_red[0][k];
+            all += s_red[1][k];
+            viol |= s_red[2][k];
+            vmax = max(vmax, s_red[3][k]);
+            woff += k < w ? s_red[4][k] : 0u;
+        }
+        uint32_t run = woff + cincl - csum;  // bucket start of this thread's first tile
+        if (in_regs) {
+#pragma unroll
+            for (int k = 0; k < TPT; k++)
+                if (t0 + k < t1) {
+                    if (b == 0) ranges[t0 + k] = make_uint2(run, run + tv[k]);
+                    s_cur[t0 + k] = run + cv[k];
+                    run += tv[k];
+                }
+        } else {
+            for (int u = t0; u < t1; u++) {
+                const uint32_t v = s_cur[u];
+                if (b == 0) ranges[u] = make_uint2(run, run + v);
+                s_cur[u] = run + cursor[(size_t)b * ntiles + u];
+                run += v;
+            }
+        }
+        if (tid == 0) {
+            geo.blocksums[b] = pre;
+            if (b == 0) {
+                // [0] num_rendered [1] prefiltered violation [2] longest tile list [3] sort cap
+                geo.counters[0] = all;
+                geo.counters[1] = viol;
+                geo.counters[2] = vmax;
+                geo.counters[3] = sort_cap;
+                if (status) {
+                    status[0] = all;
+                    status[1] = viol;
+                    status[2] = vmax;
+                    status[3] = sort_cap;
+                }
+            }
+        }
+        base = pre;
+        if (all > guard.cap_inst || vmax > guard.cap_tile) return;  // workgroup-uniform
+    } else {
+        if (guard.overflow()) return;
+        base = geo.blocksums[blockIdx.x];
+    }
     uint32_t incl = wave_incl_scan(t);
     if (lane == 63) wsum[w] = incl;
     if (t) {
-        const uint4 r = geo.bin[i];  // (rect lo, rect hi, depth bits, tiles)
         s_x0[tid] = r.x & 0xFFFFu;
         s_y0[tid] = r.x >> 16;
         s_w[tid] = (r.y & 0xFFFFu) - (r.x & 0xFFFFu);
@@ -440,7 +565,6 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict
     for (int k = 0; k < w; k++) woff += wsum[k];
     incl += woff;
     s_incl[tid] = incl;
-    const uint32_t base = geo.blocksums[blockIdx.x];
     if (i < P) geo.offsets[i] = base + incl - t;
     __syncthreads();
     const uint32_t total = s_incl[PRE_BLOCK - 1];
@@ -460,16 +584,16 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, const uint2* __restrict
     }
 }
 
-hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, const uint2* ranges, uint32_t* cursor,
-                                   bool lds_hist, int ntiles, uint64_t* keys, int nb, SpecGuard guard,
-                                   hipStream_t s) {
+hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2* ranges, const uint32_t* tot,
+                                   uint32_t* cursor, bool lds_hist, int ntiles, uint64_t* keys, int nb,
+                                   SpecGuard guard, uint32_t* status, hipStream_t s) {
     if (nb == 0) return hipSuccess;
     if (lds_hist)
         hipLaunchKernelGGL(duplicate_bucket_kernel<true>, dim3(nb), dim3(PRE_BLOCK), sizeof(uint32_t) * ntiles, s, cam,
-                           P, geo, ranges, cursor, ntiles, keys, guard);
+                           P, geo, ranges, tot, cursor, ntiles, keys, guard, (uint32_t)TILE_SORT_CAP, status);
     else
-        hipLaunchKernelGGL(duplicate_bucket_kernel<false>, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, ranges,
-                           cursor, ntiles, keys, guard);
+        hipLaunchKernelGGL(duplicate_bucket_kernel<false>, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, ranges, tot,
+                           cursor, ntiles, keys, guard, (uint32_t)TILE_SORT_CAP, status);
     return hipGetLastError();
 }
 
