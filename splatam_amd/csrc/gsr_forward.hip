@@ -606,14 +606,38 @@ constexpr int TILE_SORT_THREADS = 256;
 // Bitonic network over n = 256 * E keys (E per thread, blocked: thread t holds
 // indices [t*E, t*E+E)).  Element i pairs with i ^ j, ascending iff (i & k) == 0.
 // Partner in the same thread (j < E): register compare-exchange; in the same
-// wave (j < 64 E): lane shuffle (lane ^ j/E, same slot); otherwise through LDS.
-// For n = 1024 only 3 of the 55 stages need barriers (the LDS version had 55).
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-    // ds_bpermute: a DPP / permlane-swap version (VALU data movement, runtime switch
-    // on m) made the sort 2.5x slower
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
-    return ((uint64_t)hi << 32) | lo;
+// wave (j < 64 E): lane xor j/E, same slot; otherwise through LDS (3 of the 55
+// stages for n = 1024).  The network is unrolled at compile time (template
+// recursion over the stages), so every lane exchange is a fixed VALU permute:
+// DPP quad_perm (xor 1, 2), DPP row shifts (xor 4), DPP row_ror (xor 8) and the
+// gfx950 permlane16/32 swaps (xor 16, 32) -- no ds_bpermute, no loop control
+// (the runtime-loop ds_bpermute version spent most of its time in SALU/branch
+// overhead and LDS-permute latency: 32 us on the config-3 buckets,
+// tools/micro/sort_bench.hip).  Lane mappings checked by tools/micro/lane_xor.hip.
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t x) {
+    static_assert(M == 1 || M == 2 || M == 4 || M == 8 || M == 16 || M == 32, "lane xor distance");
+    if constexpr (M == 1) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    } else if constexpr (M == 2) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    } else if constexpr (M == 4) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x104, 0xF, 0xF, false);  // row_shl:4 (l+4)
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xF, 0xF, false);  // row_shr:4 (l-4)
+        return (__lane_id() & 4) ? dn : up;
+    } else if constexpr (M == 8) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
+    } else if constexpr (M == 16) {
+        const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (__lane_id() & 16) ? p[0] : p[1];
+    } else {
+        const auto p = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (__lane_id() & 32) ? p[0] : p[1];
+    }
+}
+template <int M>
+__device__ __forceinline__ uint64_t lane_xor64(uint64_t v) {
+    return ((uint64_t)lane_xor<M>((uint32_t)(v >> 32)) << 32) | lane_xor<M>((uint32_t)v);
 }
 
 template <int E, int J>
@@ -634,39 +658,41 @@ __device__ __forceinline__ uint64_t bitonic_pick(uint64_t v, uint64_t o, bool ke
     return ((o < v) == keep_min) ? o : v;
 }
 
+// stage (k = 2^LK, j = 2^LJ) of the network, then the rest of the network
+template <int E, int LK, int LJ>
+__device__ __forceinline__ void bitonic_net(uint64_t (&v)[E], uint32_t base, uint64_t* sk) {
+    constexpr uint32_t k = 1u << LK, j = 1u << LJ;
+    if constexpr (j >= (uint32_t)E) {
+        // j >= E, so k > j covers only thread-index bits: direction and side are the
+        // same for all E slots of a thread
+        const bool up = (base & k) == 0, keep_min = ((base & j) == 0) == up;
+        if constexpr (j >= 64u * E) {  // partner in another wave
+#pragma unroll
+            for (int e = 0; e < E; e++) sk[base + e] = v[e];
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < E; e++) v[e] = bitonic_pick(v[e], sk[(base + e) ^ j], keep_min);
+            __syncthreads();
+        } else {  // partner lane ^ j/E, same slot
+#pragma unroll
+            for (int e = 0; e < E; e++) v[e] = bitonic_pick(v[e], lane_xor64<(int)(j / E)>(v[e]), keep_min);
+        }
+    } else {  // partner in this thread
+        bitonic_reg_stage<E, (int)j>(v, base, k);
+    }
+    constexpr int LOGN = E == 1 ? 8 : E == 2 ? 9 : 10;
+    if constexpr (LJ > 0) bitonic_net<E, LK, LJ - 1>(v, base, sk);
+    else if constexpr (LK < LOGN) bitonic_net<E, LK + 1, LK>(v, base, sk);
+}
+
 template <int E, typename Emit>
 __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, Emit emit, uint64_t* sk) {
-    constexpr uint32_t n = 256u * E;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t base = tid * E;
+    static_assert(E == 1 || E == 2 || E == 4, "256 x E keys");
+    const uint32_t base = threadIdx.x * E;
     uint64_t v[E];
 #pragma unroll
     for (int e = 0; e < E; e++) v[e] = base + e < cnt ? src[base + e] : ~0ull;
-    for (uint32_t k = 2; k <= n; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            if (j >= (uint32_t)E) {
-                // j >= E, so k > j covers only thread-index bits: direction and side are the
-                // same for all E slots of a thread
-                const bool up = (base & k) == 0, keep_min = ((base & j) == 0) == up;
-                if (j >= 64u * E) {  // partner in another wave
-#pragma unroll
-                    for (int e = 0; e < E; e++) sk[base + e] = v[e];
-                    __syncthreads();
-#pragma unroll
-                    for (int e = 0; e < E; e++) v[e] = bitonic_pick(v[e], sk[(base + e) ^ j], keep_min);
-                    __syncthreads();
-                } else {  // partner lane ^ j/E, same slot
-                    const int m = (int)(j / E);
-#pragma unroll
-                    for (int e = 0; e < E; e++) v[e] = bitonic_pick(v[e], shfl_xor_u64(v[e], m), keep_min);
-                }
-            } else {  // partner in this thread
-                if (E > 2 && j == 2) bitonic_reg_stage<E, (E > 2 ? 2 : 1)>(v, base, k);
-                else if (E > 1 && j == 1) bitonic_reg_stage<E, 1>(v, base, k);
-            }
-        }
-    }
-    (void)lane;
+    bitonic_net<E, 1, 0>(v, base, sk);
 #pragma unroll
     for (int e = 0; e < E; e++)  // (a padding key can only land here through a network bug: emit id 0, never
         if (base + e < cnt) emit(base + e, v[e] == ~0ull ? 0u : (uint32_t)v[e]);  // an out-of-range id)

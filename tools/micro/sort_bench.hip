@@ -4,15 +4,16 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <algorithm>
 
 #include "gsr_common.h"
 
 namespace gsr {
-hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint32_t* point_list,
+hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint64_t* point_list,
                             SpecGuard guard, hipStream_t s);
 }
 
-__global__ void __launch_bounds__(256) empty_kernel(const uint2* r, uint32_t* out) {
+__global__ void __launch_bounds__(256) empty_kernel(const uint2* r, uint64_t* out) {
     __shared__ uint64_t sk[4096];
     sk[threadIdx.x] = r[blockIdx.x].x;
     __syncthreads();
@@ -29,10 +30,10 @@ int main() {
         ranges[t] = make_uint2((uint32_t)keys.size(), (uint32_t)(keys.size() + c));
         for (int i = 0; i < c; i++) keys.push_back(((uint64_t)(0x3f000000u + rand() % 0x800000) << 32) | (uint64_t)(rand() % 300000));
     }
-    uint2* dr; uint64_t* dk; uint32_t *dp, *dc;
+    uint2* dr; uint64_t *dk, *dp; uint32_t* dc;
     (void)hipMalloc(&dr, sizeof(uint2) * T);
     (void)hipMalloc(&dk, 8 * keys.size());
-    (void)hipMalloc(&dp, 4 * keys.size());
+    (void)hipMalloc(&dp, 8 * keys.size());
     (void)hipMalloc(&dc, 16);
     (void)hipMemcpy(dr, ranges.data(), sizeof(uint2) * T, hipMemcpyHostToDevice);
     (void)hipMemcpy(dk, keys.data(), 8 * keys.size(), hipMemcpyHostToDevice);
@@ -53,9 +54,15 @@ int main() {
         }
         printf("%s: %.2f us\n", variant == 0 ? "tile_sort" : "empty (same grid, 32KB LDS)", best * 1000);
     }
-    // check sortedness
-    std::vector<uint32_t> pl(keys.size());
-    (void)hipMemcpy(pl.data(), dp, 4 * keys.size(), hipMemcpyDeviceToHost);
-    printf("done %zu keys\n", keys.size());
-    return 0;
+    // check: every tile's ids in (depth, id) order of its keys
+    std::vector<uint64_t> pl(keys.size());
+    (void)hipMemcpy(pl.data(), dp, 8 * keys.size(), hipMemcpyDeviceToHost);
+    size_t bad = 0;
+    for (int t = 0; t < T; t++) {
+        std::vector<uint64_t> k(keys.begin() + ranges[t].x, keys.begin() + ranges[t].y);
+        std::sort(k.begin(), k.end());
+        for (size_t i = 0; i < k.size(); i++) bad += (uint32_t)pl[ranges[t].x + i] != (uint32_t)k[i];
+    }
+    printf("done %zu keys, %zu misplaced\n", keys.size(), bad);
+    return bad != 0;
 }
