@@ -393,13 +393,14 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         if (capacity <= 0 && scan_in_duplicate && (rc = snapshot_counters()) != GSR_OK) return rc;
         {
             StageTimer t(GSR_STAGE_SORT, 0, stream);
-            if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, guard, stream)) != hipSuccess)
+            if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, guard, true, stream)) != hipSuccess)
                 return hip_fail(e, "tile sort");
         }
         {
             StageTimer t(GSR_STAGE_RENDER_FWD, 0, stream, true);
-            if ((e = launch_render_fwd(cam, ranges, point_list, geo, colors2, final_T, n_contrib, out_color,
-                                       out_color2, out_depth, guard, stream, t.kclock(), l1)) != hipSuccess)
+            if ((e = launch_render_fwd(cam, ranges, point_list, keys[0], geo, colors2, final_T, n_contrib,
+                                       out_color, out_color2, out_depth, guard, stream, t.kclock(), l1)) !=
+                hipSuccess)
                 return hip_fail(e, "render");
         }
         speculated = true;
@@ -426,7 +427,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
     bin_ptrs(bin, BL, keys, vals, gid, point_list, hist);
     const SpecGuard none{geo.counters, 0xffffffffu, 0xffffffffu};
-    if (I > 0 && longest <= (uint32_t)TILE_SORT_CAP && !force_radix) {
+    const bool tile_sorted = I > 0 && longest <= (uint32_t)TILE_SORT_CAP && !force_radix;
+    if (tile_sorted) {
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
             if ((e = launch_duplicate_bucket(cam, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
@@ -435,7 +437,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         }
         {
             StageTimer t(GSR_STAGE_SORT, I, stream);
-            if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, none, stream)) != hipSuccess)
+            if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, none, true, stream)) != hipSuccess)
                 return hip_fail(e, "tile sort");
         }
     } else if (I > 0) {
@@ -460,8 +462,9 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     }
     {
         StageTimer t(GSR_STAGE_RENDER_FWD, I, stream, true);
-        if ((e = launch_render_fwd(cam, ranges, point_list, geo, colors2, final_T, n_contrib, out_color, out_color2,
-                                   out_depth, none, stream, t.kclock(), l1)) != hipSuccess)
+        if ((e = launch_render_fwd(cam, ranges, point_list, tile_sorted ? keys[0] : nullptr, geo, colors2,
+                                   final_T, n_contrib, out_color, out_color2, out_depth, none, stream, t.kclock(),
+                                   l1)) != hipSuccess)
             return hip_fail(e, "render");
     }
     return (int)I;

@@ -602,6 +602,8 @@ hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2
 // (depth bits, id) are unique inside a tile, so the order is a total order and
 // equals the reference's stable (tile, depth) radix order.
 constexpr int TILE_SORT_THREADS = 256;
+constexpr uint32_t TILE_SORT_REGS = 1024;  // longest list sorted in registers (256 threads x 4)
+constexpr int TILE_SORT_TILES = 4;         // tiles per workgroup of the long-list sort launch
 
 // Bitonic network over n = 256 * E keys (E per thread, blocked: thread t holds
 // indices [t*E, t*E+E)).  Element i pairs with i ^ j, ascending iff (i & k) == 0.
@@ -698,32 +700,49 @@ __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, E
         if (base + e < cnt) emit(base + e, v[e] == ~0ull ? 0u : (uint32_t)v[e]);  // an out-of-range id)
 }
 
-__global__ void __launch_bounds__(TILE_SORT_THREADS)
-tile_sort_kernel(const uint2* __restrict__ ranges, const uint64_t* __restrict__ keys,
-                 uint64_t* __restrict__ point_list, SpecGuard guard) {
-    __shared__ uint64_t sk[TILE_SORT_CAP];
-    if (guard.overflow()) return;
-    const uint2 range = ranges[blockIdx.x];
-    const uint32_t cnt = range.y - range.x;
-    PointEntry* dst = point_list + range.x;
-    // sorted entry i: the Gaussian id (render_fwd adds the block mask in the high half)
+// Sorts one tile's bucket of cnt <= TILE_SORT_REGS keys into dst (Gaussian ids;
+// render_fwd adds the block mask in the high half when it stages an entry).
+// Every thread of the workgroup calls it (cnt is workgroup-uniform); sk: LDS for
+// 256 * 4 keys (the cross-wave stages).
+__device__ __forceinline__ void tile_sort_short(const uint64_t* __restrict__ src, uint32_t cnt,
+                                                PointEntry* __restrict__ dst, uint64_t* sk) {
     auto emit = [&](uint32_t i, uint32_t gi) { dst[i] = (PointEntry)gi; };
     if (cnt <= 1) {
-        if (cnt == 1 && threadIdx.x == 0) emit(0, (uint32_t)keys[range.x]);
-        return;
-    }
-    const uint64_t* src = keys + range.x;
-    if (cnt <= 256) {
+        if (cnt == 1 && threadIdx.x == 0) emit(0, (uint32_t)src[0]);
+    } else if (cnt <= 256) {
         tile_sort_regs<1>(src, cnt, emit, sk);
     } else if (cnt <= 512) {
         tile_sort_regs<2>(src, cnt, emit, sk);
-    } else if (cnt <= 1024) {
-        tile_sort_regs<4>(src, cnt, emit, sk);
     } else {
+        tile_sort_regs<4>(src, cnt, emit, sk);
+    }
+}
+
+// LONG_ONLY: lists of <= TILE_SORT_REGS keys are left to render_fwd, which sorts
+// them in its prologue (no separate launch, no key round trip); this launch then
+// only sorts the long lists, TILE_SORT_TILES tiles per workgroup.
+template <bool LONG_ONLY>
+__global__ void __launch_bounds__(TILE_SORT_THREADS)
+tile_sort_kernel(const uint2* __restrict__ ranges, const uint64_t* __restrict__ keys,
+                 uint64_t* __restrict__ point_list, SpecGuard guard, int ntiles) {
+    __shared__ uint64_t sk[TILE_SORT_CAP];
+    if (guard.overflow()) return;
+    const int t0 = blockIdx.x * (LONG_ONLY ? TILE_SORT_TILES : 1);
+    const int t1 = min(ntiles, t0 + (LONG_ONLY ? TILE_SORT_TILES : 1));
+    for (int tile = t0; tile < t1; tile++) {
+        const uint2 range = ranges[tile];
+        const uint32_t cnt = range.y - range.x;
+        const uint64_t* src = keys + range.x;
+        PointEntry* dst = point_list + range.x;
+        if (cnt <= TILE_SORT_REGS) {
+            if (!LONG_ONLY) tile_sort_short(src, cnt, dst, sk);
+            continue;
+        }
         // long lists (<= TILE_SORT_CAP): the same network entirely through LDS -- more keys
-        // per thread in registers would raise the whole kernel's VGPR count (occupancy 5 -> 3)
+        // per thread in registers would raise the whole kernel's VGPR count
         uint32_t n = 2048;
         while (n < cnt) n <<= 1;
+        __syncthreads();  // sk reuse across tiles
         for (uint32_t i = threadIdx.x; i < n; i += TILE_SORT_THREADS) sk[i] = i < cnt ? src[i] : ~0ull;
         __syncthreads();
         for (uint32_t k = 2; k <= n; k <<= 1) {
@@ -739,15 +758,19 @@ tile_sort_kernel(const uint2* __restrict__ ranges, const uint64_t* __restrict__ 
                 __syncthreads();
             }
         }
-        for (uint32_t i = threadIdx.x; i < cnt; i += TILE_SORT_THREADS) emit(i, (uint32_t)sk[i]);
+        for (uint32_t i = threadIdx.x; i < cnt; i += TILE_SORT_THREADS) dst[i] = (PointEntry)(uint32_t)sk[i];
     }
 }
 
 hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint64_t* point_list,
-                            SpecGuard guard, hipStream_t s) {
+                            SpecGuard guard, bool long_only, hipStream_t s) {
     static_assert(TILE_SORT_THREADS == 256 && TILE_SORT_CAP <= 4096, "tile_sort_regs assumes 256 x E; sk holds the cap");
-    hipLaunchKernelGGL(tile_sort_kernel, dim3(ntiles), dim3(TILE_SORT_THREADS), 0, s, ranges, keys, point_list,
-                       guard);
+    if (long_only)
+        hipLaunchKernelGGL(tile_sort_kernel<true>, dim3((ntiles + TILE_SORT_TILES - 1) / TILE_SORT_TILES),
+                           dim3(TILE_SORT_THREADS), 0, s, ranges, keys, point_list, guard, ntiles);
+    else
+        hipLaunchKernelGGL(tile_sort_kernel<false>, dim3(ntiles), dim3(TILE_SORT_THREADS), 0, s, ranges, keys,
+                           point_list, guard, ntiles);
     return hipGetLastError();
 }
 
@@ -904,7 +927,7 @@ hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint64_t
 template <bool DUAL, bool L1 = false>
 __global__ void __launch_bounds__(TILE_PIX, 5)
 render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __restrict__ point_list,
-                  const float4* __restrict__ rr, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
+                  const uint64_t* __restrict__ keys, const float4* __restrict__ rr, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                   float* __restrict__ out_color, float* __restrict__ out_color2, float* __restrict__ out_depth,
                   SpecGuard guard, unsigned long long* clk, TrackL1 l1) {
     static_assert(DUAL || !L1, "the tracking loss needs the depth / silhouette colour set");
@@ -914,8 +937,11 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         return;
     }
     // entry RENDER_BATCH is a dummy (opacity 0, never blends) that pads the row lists
-    __shared__ float4 s_a[RENDER_BATCH + 1];
-    __shared__ float4 s_b[RENDER_BATCH + 1];
+    // s_a and s_b share one array: before the first batch it is the tile sort's LDS
+    __shared__ float4 s_ab[2 * (RENDER_BATCH + 1)];
+    static_assert(sizeof(s_ab) >= TILE_SORT_REGS * sizeof(uint64_t), "tile sort LDS aliases s_a / s_b");
+    float4* const s_a = s_ab;
+    float4* const s_b = s_ab + RENDER_BATCH + 1;
     __shared__ float4 s_c[RENDER_BATCH + 1];
     __shared__ float4 s_d[DUAL ? RENDER_BATCH + 1 : 1];
     __shared__ uint16_t s_mask[RENDER_BATCH];
@@ -935,6 +961,13 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
     uint32_t last = 0;
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
     uint32_t pm = 0, pg = 0;  // the staged entry's 4x4-block mask and Gaussian id
+    if (keys != nullptr && range.y - range.x <= TILE_SORT_REGS) {
+        // this tile's bucket is short: sort it here (tile_sort_kernel<true> only took the long ones);
+        // the sorted ids land in point_list, read back below by the same workgroup
+        tile_sort_short(keys + range.x, range.y - range.x, point_list + range.x,
+                        reinterpret_cast<uint64_t*>(s_ab));
+        __syncthreads();
+    }
     if (tid == 0) {
         s_a[RENDER_BATCH] = pa;
         s_b[RENDER_BATCH] = pa;
@@ -1096,13 +1129,13 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
 int track_l1_fused_scratch_floats(int ntiles) { return 2 * ntiles + ARRIVE_GROUPED_WORDS; }
 
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* point_list,
-                             GeomPtrs geo,
+                             const uint64_t* keys, GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
                              unsigned long long* clk, const TrackL1* l1) {
     auto k = colors2 ? (l1 ? render_fwd_kernel<true, true> : render_fwd_kernel<true, false>)
                      : render_fwd_kernel<false, false>;
-    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list,
+    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, keys,
                        geo.rr, final_T,
                        n_contrib, out_color, out_color2, out_depth, guard, clk, l1 ? *l1 : TrackL1{});
     return hipGetLastError();
