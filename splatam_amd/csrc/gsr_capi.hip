@@ -392,11 +392,6 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         }
         if (capacity <= 0 && scan_in_duplicate && (rc = snapshot_counters()) != GSR_OK) return rc;
         {
-            StageTimer t(GSR_STAGE_SORT, 0, stream);
-            if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, guard, true, stream)) != hipSuccess)
-                return hip_fail(e, "tile sort");
-        }
-        {
             StageTimer t(GSR_STAGE_RENDER_FWD, 0, stream, true);
             if ((e = launch_render_fwd(cam, ranges, point_list, keys[0], geo, colors2, final_T, n_contrib,
                                        out_color, out_color2, out_depth, guard, stream, t.kclock(), l1)) !=
@@ -434,11 +429,6 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
             if ((e = launch_duplicate_bucket(cam, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
                                              ntiles, keys[0], GL.nb, none, nullptr, stream)) != hipSuccess)
                 return hip_fail(e, "duplicate");
-        }
-        {
-            StageTimer t(GSR_STAGE_SORT, I, stream);
-            if ((e = launch_tile_sort(ntiles, ranges, keys[0], point_list, none, true, stream)) != hipSuccess)
-                return hip_fail(e, "tile sort");
         }
     } else if (I > 0) {
         // fallback for tiles longer than the LDS sort: global stable LSD radix sort of (tile, depth)

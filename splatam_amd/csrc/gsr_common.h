@@ -93,7 +93,7 @@ inline int higher_msb(uint32_t n) {  // rasterizer_impl.cu:35-50 (bits needed fo
     return b;
 }
 
-constexpr int TILE_SORT_CAP = 4096;  // longest tile list sorted in LDS (32 KiB of u64 keys)
+constexpr int TILE_SORT_CAP = 4096;  // longest tile list render_fwd sorts (4 chunks of 1024 keys)
 
 struct BinLayout {        // per-instance state ("binningBuffer")
     size_t point_list;    // u64 [I] PointEntry (mask << 32 | Gaussian id) in (tile, depth, id) order -- offset 0
@@ -932,9 +932,6 @@ struct BwdGuard {
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2* ranges, const uint32_t* tot,
                                    uint32_t* cursor, bool lds_hist, int ntiles, uint64_t* keys, int nb,
                                    SpecGuard guard, uint32_t* status, hipStream_t s);
-// long_only: sort only the buckets longer than TILE_SORT_REGS (render_fwd, given the keys, sorts the rest)
-hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint64_t* point_list,
-                            SpecGuard guard, bool long_only, hipStream_t s);
 hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t n, int nsb, int npass,
                              hipStream_t s);
 hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint64_t* point_list, uint32_t n,
@@ -953,10 +950,11 @@ struct TrackL1 {
     float* loss;            // device scalar
 };
 int track_l1_fused_scratch_floats(int ntiles);
-// keys: the bucketed tile keys while short buckets are still unsorted (render_fwd sorts them
-// in its prologue); nullptr when point_list is already fully sorted (radix fallback)
+// keys: the unsorted tile buckets (render_fwd sorts each tile's bucket into point_list in
+// its prologue; the keys are scratch afterwards); nullptr when point_list is already
+// sorted (radix fallback)
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* point_list,
-                             const uint64_t* keys, GeomPtrs geo,
+                             uint64_t* keys, GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
                              unsigned long long* clk = nullptr, const TrackL1* l1 = nullptr);

@@ -419,7 +419,7 @@ hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* ke
 
 // Bucketed duplicate: every instance goes straight into its tile's bucket
 // (slot from a per-tile cursor), keyed (depth bits << 32 | Gaussian id).  The
-// order inside a bucket is arbitrary; tile_sort_kernel restores the reference
+// order inside a bucket is arbitrary; render_fwd (tile_sort_bucket) restores the reference
 // order (depth, then id: cub's stable LSD sort, rasterizer_impl.cu:304-309).
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
@@ -597,13 +597,12 @@ hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2
     return hipGetLastError();
 }
 
-// One workgroup per tile: bitonic sort of the tile's bucket (<= TILE_SORT_CAP
-// u64 keys) in LDS, then the Gaussian ids are written in sorted order.  Keys
-// (depth bits, id) are unique inside a tile, so the order is a total order and
+// Per-tile sort of the bucketed (depth bits << 32 | id) keys, done by render_fwd
+// in its prologue (one workgroup per tile; no separate launch, no key round
+// trip).  Keys are unique inside a tile, so the order is a total order and
 // equals the reference's stable (tile, depth) radix order.
 constexpr int TILE_SORT_THREADS = 256;
 constexpr uint32_t TILE_SORT_REGS = 1024;  // longest list sorted in registers (256 threads x 4)
-constexpr int TILE_SORT_TILES = 4;         // tiles per workgroup of the long-list sort launch
 
 // Bitonic network over n = 256 * E keys (E per thread, blocked: thread t holds
 // indices [t*E, t*E+E)).  Element i pairs with i ^ j, ascending iff (i & k) == 0.
@@ -700,78 +699,79 @@ __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, E
         if (base + e < cnt) emit(base + e, v[e] == ~0ull ? 0u : (uint32_t)v[e]);  // an out-of-range id)
 }
 
-// Sorts one tile's bucket of cnt <= TILE_SORT_REGS keys into dst (Gaussian ids;
-// render_fwd adds the block mask in the high half when it stages an entry).
+// Sorts one tile's bucket src[0, cnt) (cnt <= TILE_SORT_CAP) into dst as Gaussian
+// ids (render_fwd adds the block mask in the high half when it stages an entry).
 // Every thread of the workgroup calls it (cnt is workgroup-uniform); sk: LDS for
-// 256 * 4 keys (the cross-wave stages).
-__device__ __forceinline__ void tile_sort_short(const uint64_t* __restrict__ src, uint32_t cnt,
-                                                PointEntry* __restrict__ dst, uint64_t* sk) {
+// TILE_SORT_REGS keys (the network's cross-wave stages, the rank searches).
+//   cnt <= 512:  one register network of 256 or 512 keys, ids emitted directly.
+//   otherwise:   the bucket is cut into chunks of TILE_SORT_REGS keys, each sorted by
+//                the 256 x 4 register network; a single chunk is emitted directly,
+//                several are written back in place (the keys are scratch once sorted)
+//                and every key's final position is its index in its own chunk plus,
+//                for every other chunk (staged in LDS), the number of that chunk's
+//                keys below it -- exact, as the keys are unique in a tile.
+// The result equals a stable (tile, depth) radix order (ids break depth ties).
+__device__ __forceinline__ void tile_sort_bucket(uint64_t* __restrict__ src, uint32_t cnt,
+                                                 PointEntry* __restrict__ dst, uint64_t* sk) {
     auto emit = [&](uint32_t i, uint32_t gi) { dst[i] = (PointEntry)gi; };
     if (cnt <= 1) {
         if (cnt == 1 && threadIdx.x == 0) emit(0, (uint32_t)src[0]);
-    } else if (cnt <= 256) {
-        tile_sort_regs<1>(src, cnt, emit, sk);
-    } else if (cnt <= 512) {
-        tile_sort_regs<2>(src, cnt, emit, sk);
-    } else {
-        tile_sort_regs<4>(src, cnt, emit, sk);
+        return;
     }
-}
-
-// LONG_ONLY: lists of <= TILE_SORT_REGS keys are left to render_fwd, which sorts
-// them in its prologue (no separate launch, no key round trip); this launch then
-// only sorts the long lists, TILE_SORT_TILES tiles per workgroup.
-template <bool LONG_ONLY>
-__global__ void __launch_bounds__(TILE_SORT_THREADS)
-tile_sort_kernel(const uint2* __restrict__ ranges, const uint64_t* __restrict__ keys,
-                 uint64_t* __restrict__ point_list, SpecGuard guard, int ntiles) {
-    __shared__ uint64_t sk[TILE_SORT_CAP];
-    if (guard.overflow()) return;
-    const int t0 = blockIdx.x * (LONG_ONLY ? TILE_SORT_TILES : 1);
-    const int t1 = min(ntiles, t0 + (LONG_ONLY ? TILE_SORT_TILES : 1));
-    for (int tile = t0; tile < t1; tile++) {
-        const uint2 range = ranges[tile];
-        const uint32_t cnt = range.y - range.x;
-        const uint64_t* src = keys + range.x;
-        PointEntry* dst = point_list + range.x;
-        if (cnt <= TILE_SORT_REGS) {
-            if (!LONG_ONLY) tile_sort_short(src, cnt, dst, sk);
-            continue;
+    if (cnt <= 256) {
+        tile_sort_regs<1>(src, cnt, emit, sk);
+        return;
+    }
+    if (cnt <= 512) {
+        tile_sort_regs<2>(src, cnt, emit, sk);
+        return;
+    }
+    const uint32_t nch = (cnt + TILE_SORT_REGS - 1) / TILE_SORT_REGS;
+    const uint32_t base = threadIdx.x * 4;
+    for (uint32_t c = 0; c < nch; c++) {  // one network instance for every chunk
+        const uint32_t c0 = c * TILE_SORT_REGS, len = min(TILE_SORT_REGS, cnt - c0);
+        uint64_t v[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) v[e] = base + e < len ? src[c0 + base + e] : ~0ull;
+        bitonic_net<4, 1, 0>(v, base, sk);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            if (base + e >= len) continue;
+            if (nch == 1) emit(base + e, v[e] == ~0ull ? 0u : (uint32_t)v[e]);  // (never an out-of-range id)
+            else src[c0 + base + e] = v[e];
         }
-        // long lists (<= TILE_SORT_CAP): the same network entirely through LDS -- more keys
-        // per thread in registers would raise the whole kernel's VGPR count
-        uint32_t n = 2048;
-        while (n < cnt) n <<= 1;
-        __syncthreads();  // sk reuse across tiles
-        for (uint32_t i = threadIdx.x; i < n; i += TILE_SORT_THREADS) sk[i] = i < cnt ? src[i] : ~0ull;
-        __syncthreads();
-        for (uint32_t k = 2; k <= n; k <<= 1) {
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = threadIdx.x; i < n / 2; i += TILE_SORT_THREADS) {
-                    const uint32_t lo = 2 * i - (i & (j - 1)), hi = lo + j;
-                    const uint64_t a = sk[lo], b = sk[hi];
-                    if ((a > b) == ((lo & k) == 0)) {
-                        sk[lo] = b;
-                        sk[hi] = a;
-                    }
-                }
-                __syncthreads();
+    }
+    if (nch == 1) return;
+    __syncthreads();  // the sorted chunks (global) are visible to the workgroup
+    for (uint32_t c = 0; c < nch; c++) {
+        const uint32_t c0 = c * TILE_SORT_REGS, len = min(TILE_SORT_REGS, cnt - c0);
+        uint64_t v[4];
+        uint32_t pos[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            v[e] = base + e < len ? src[c0 + base + e] : ~0ull;
+            pos[e] = base + e;
+        }
+        for (uint32_t c2 = 0; c2 < nch; c2++) {
+            if (c2 == c) continue;
+            const uint32_t d0 = c2 * TILE_SORT_REGS, dlen = min(TILE_SORT_REGS, cnt - d0);
+            __syncthreads();  // sk is free
+            for (uint32_t i = threadIdx.x; i < dlen; i += TILE_SORT_THREADS) sk[i] = src[d0 + i];
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < 4; e++) {  // keys of chunk c2 below v[e]: branch-free lower bound
+                uint32_t lo = 0;
+#pragma unroll
+                for (uint32_t st = TILE_SORT_REGS; st > 0; st >>= 1)
+                    if (lo + st <= dlen && sk[lo + st - 1] < v[e]) lo += st;
+                pos[e] += lo;
             }
         }
-        for (uint32_t i = threadIdx.x; i < cnt; i += TILE_SORT_THREADS) dst[i] = (PointEntry)(uint32_t)sk[i];
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+            if (base + e < len) emit(pos[e], (uint32_t)v[e]);
     }
-}
-
-hipError_t launch_tile_sort(int ntiles, const uint2* ranges, const uint64_t* keys, uint64_t* point_list,
-                            SpecGuard guard, bool long_only, hipStream_t s) {
-    static_assert(TILE_SORT_THREADS == 256 && TILE_SORT_CAP <= 4096, "tile_sort_regs assumes 256 x E; sk holds the cap");
-    if (long_only)
-        hipLaunchKernelGGL(tile_sort_kernel<true>, dim3((ntiles + TILE_SORT_TILES - 1) / TILE_SORT_TILES),
-                           dim3(TILE_SORT_THREADS), 0, s, ranges, keys, point_list, guard, ntiles);
-    else
-        hipLaunchKernelGGL(tile_sort_kernel<false>, dim3(ntiles), dim3(TILE_SORT_THREADS), 0, s, ranges, keys,
-                           point_list, guard, ntiles);
-    return hipGetLastError();
+    __syncthreads();  // sk (aliased by the caller) is free again
 }
 
 // ------------------------------------------------------------- radix sort --
@@ -927,7 +927,7 @@ hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint64_t
 template <bool DUAL, bool L1 = false>
 __global__ void __launch_bounds__(TILE_PIX, 5)
 render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __restrict__ point_list,
-                  const uint64_t* __restrict__ keys, const float4* __restrict__ rr, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
+                  uint64_t* __restrict__ keys, const float4* __restrict__ rr, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                   float* __restrict__ out_color, float* __restrict__ out_color2, float* __restrict__ out_depth,
                   SpecGuard guard, unsigned long long* clk, TrackL1 l1) {
     static_assert(DUAL || !L1, "the tracking loss needs the depth / silhouette colour set");
@@ -939,7 +939,8 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
     // entry RENDER_BATCH is a dummy (opacity 0, never blends) that pads the row lists
     // s_a and s_b share one array: before the first batch it is the tile sort's LDS
     __shared__ float4 s_ab[2 * (RENDER_BATCH + 1)];
-    static_assert(sizeof(s_ab) >= TILE_SORT_REGS * sizeof(uint64_t), "tile sort LDS aliases s_a / s_b");
+    static_assert(sizeof(s_ab) >= TILE_SORT_REGS * sizeof(uint64_t) && TILE_SORT_THREADS == TILE_PIX,
+                  "tile sort (256 x 4 keys) LDS aliases s_a / s_b");
     float4* const s_a = s_ab;
     float4* const s_b = s_ab + RENDER_BATCH + 1;
     __shared__ float4 s_c[RENDER_BATCH + 1];
@@ -961,11 +962,11 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
     uint32_t last = 0;
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
     uint32_t pm = 0, pg = 0;  // the staged entry's 4x4-block mask and Gaussian id
-    if (keys != nullptr && range.y - range.x <= TILE_SORT_REGS) {
-        // this tile's bucket is short: sort it here (tile_sort_kernel<true> only took the long ones);
-        // the sorted ids land in point_list, read back below by the same workgroup
-        tile_sort_short(keys + range.x, range.y - range.x, point_list + range.x,
-                        reinterpret_cast<uint64_t*>(s_ab));
+    if (keys != nullptr) {
+        // the tile's bucket is sorted here; the sorted ids land in point_list and are read
+        // back below by this same workgroup (guard: every list is <= TILE_SORT_CAP)
+        tile_sort_bucket(keys + range.x, range.y - range.x, point_list + range.x,
+                         reinterpret_cast<uint64_t*>(s_ab));
         __syncthreads();
     }
     if (tid == 0) {
@@ -1129,7 +1130,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
 int track_l1_fused_scratch_floats(int ntiles) { return 2 * ntiles + ARRIVE_GROUPED_WORDS; }
 
 hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* point_list,
-                             const uint64_t* keys, GeomPtrs geo,
+                             uint64_t* keys, GeomPtrs geo,
                              const float* colors2, float* final_T, uint32_t* n_contrib, float* out_color,
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
                              unsigned long long* clk, const TrackL1* l1) {

@@ -123,7 +123,9 @@ def _binning_gpu(scene, cuda):
 BIN_CASES = [
     dict(name="cfg1_like", P=4000, W=160, H=120, aniso=False),
     dict(name="aniso", P=3000, W=128, H=96, aniso=True),
-    dict(name="long_lists", P=12000, W=48, H=32, aniso=False),   # > TILE_SORT_CAP -> radix fallback
+    dict(name="long_lists", P=12000, W=48, H=32, aniso=False, near=True, scale=12.0),  # > TILE_SORT_CAP -> radix
+    # lists of 1025-2048 / 2049-3072 / 3073-4096 keys: 2, 3 and 4 sorted chunks merged by rank in render_fwd
+    dict(name="chunked_lists", P=6000, W=96, H=64, aniso=False, near=True, scale=7.0),
     dict(name="many_tiles", P=6000, W=2080, H=2080, aniso=True),  # > MAX_LDS_TILES -> global-atomic counts
 ]
 
@@ -133,9 +135,8 @@ def test_binning_bit_exact(cuda, case):
     """Integer work is bit-exact: num_rendered, per-tile ranges and the sorted
     Gaussian-id list equal the oracle's (tile, depth, id) order."""
     scene = make_scene(case["P"], case["W"], case["H"], seed=13, anisotropic=case["aniso"],
-                       z_range=(0.5, 1.0) if case["name"] == "long_lists" else (0.5, 5.0))
-    if case["name"] == "long_lists":
-        scene.scales *= 12.0
+                       z_range=(0.5, 1.0) if case.get("near") else (0.5, 5.0))
+    scene.scales *= case.get("scale", 1.0)
     fr, _ = harness.run_oracle(scene, backward=False)
     n, v = _binning_gpu(scene, cuda)
     assert n == fr.num_rendered
@@ -147,6 +148,10 @@ def test_binning_bit_exact(cuda, case):
     np.testing.assert_array_equal(v["point_list"], fr.point_list)
     if case["name"] == "long_lists":
         assert cnt_ref.max() > 4096
+    if case["name"] == "chunked_lists":
+        assert cnt_ref.max() <= 4096
+        for lo, hi in ((1024, 2048), (2048, 3072), (3072, 4096)):
+            assert ((cnt_ref > lo) & (cnt_ref <= hi)).any(), (lo, hi)
 
 
 POWER_CASES = [
