@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=("auto", "on", "off"), default="auto")
     ap.add_argument("--graph", type=int, default=1, help="1: replay the tracking iterations as a HIP graph")
     ap.add_argument("--iters-per-graph", type=int, default=20)
+    ap.add_argument("--fuse-pose", type=int, default=0,
+                    help="tracking: 1 = pose chain + Adam inside the per-Gaussian backward (one launch fewer)")
     ap.add_argument("--timing", type=int, default=1,
                     help="0: no device-clock timing of render_bwd in the graph (A/B check; no roofline)")
     return ap.parse_args()
@@ -139,6 +141,7 @@ def main():
         S = max(1, min(args.iters_per_graph, args.steps))
         steps = -(-args.steps // S) * S
         tracker = GraphTracker(params, curr, frame, iters_per_graph=S, timing=bool(args.timing),
+                               fuse_pose=bool(args.fuse_pose),
                                warmup_iters=min(3, max(1, args.warmup)))
         for _ in range(max(1, args.warmup // S)):
             tracker.run()

@@ -133,7 +133,7 @@ int gsr_forward_dual(const gsr_settings* settings, const gsr_gaussians* gaussian
  * host.  The device counters are copied to `status` (device, 4 x u32:
  * [0] num_rendered, [1] prefiltered violation, [2] longest tile list) when the
  * stream reaches that point.  Outputs are valid iff status[0] <= capacity and
- * status[2] <= 4096 (the LDS tile sort; longer lists need gsr_forward_dual);
+ * status[2] <= 4096 (the per-tile sort; longer lists need gsr_forward_dual);
  * otherwise every kernel after the scan skipped its work (no out-of-bounds
  * writes) and the call must be repeated with a larger capacity or in the
  * synchronous mode.  Returns `capacity`: pass it as num_rendered to

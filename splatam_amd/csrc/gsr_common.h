@@ -915,7 +915,7 @@ struct SpecGuard {
 };
 // Backward-side check that the forward state is valid for a binning layout of
 // `cap_inst` instances: counters[3] holds the longest tile list the sort path
-// that produced point_list handles (TILE_SORT_CAP for the LDS tile sort,
+// that produced point_list handles (TILE_SORT_CAP for render_fwd's tile sort,
 // 0xffffffff for the radix fallback), set by the forward.  Only a static-mode
 // forward can leave it failing; the backward kernels then do no work (no
 // out-of-bounds access) and the gradients are zero.

@@ -25,7 +25,7 @@ from .glue import MapAdam, map_transform
 from .layout import views
 from .slam import MappingConfig, _get_loss_mapping_fused, color_key, fused_mapping_eligible
 
-TILE_SORT_CAP = 4096  # longest tile list the static mode handles (LDS tile sort)
+TILE_SORT_CAP = 4096  # longest tile list the static mode handles (render_fwd's per-tile sort)
 GAUSS_KEYS = ("means3D", "unnorm_rotations", "logit_opacities", "log_scales")
 
 

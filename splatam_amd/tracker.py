@@ -27,7 +27,7 @@ from .layout import views
 from .rasterizer import GaussianRasterizationSettings
 from .slam import TrackingConfig, _get_loss_tracking_fused, fused_eligible
 
-TILE_SORT_CAP = 4096  # longest tile list the static mode handles (LDS tile sort)
+TILE_SORT_CAP = 4096  # longest tile list the static mode handles (render_fwd's per-tile sort)
 
 
 def probe_num_rendered(params, curr_data, time_idx) -> tuple[int, int]:
