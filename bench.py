@@ -59,8 +59,9 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=("auto", "on", "off"), default="auto")
     ap.add_argument("--graph", type=int, default=1, help="1: replay the tracking iterations as a HIP graph")
     ap.add_argument("--iters-per-graph", type=int, default=20)
-    ap.add_argument("--fuse-pose", type=int, default=0,
-                    help="tracking: 1 = pose chain + Adam inside the per-Gaussian backward (one launch fewer)")
+    ap.add_argument("--fuse-pose", type=int, default=1,
+                    help="tracking: 1 = pose chain + Adam inside the per-Gaussian backward (one launch fewer), "
+                         "0 = separate pose kernel")
     ap.add_argument("--timing", type=int, default=1,
                     help="0: no device-clock timing of render_bwd in the graph (A/B check; no roofline)")
     return ap.parse_args()

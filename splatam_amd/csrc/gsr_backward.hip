@@ -477,13 +477,47 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         block_sum<POSE_PARTS>(v, s_red, s_tot);
         __syncthreads();
         if (threadIdx.x < POSE_PARTS) st_agent(pf.part + POSE_PARTS * blockIdx.x + threadIdx.x, s_tot[threadIdx.x]);
+        // Two-level fixed-order sum of the ~1200 workgroup partials: the last workgroup of each
+        // of the 16 arrival groups (b = g mod 16) adds its group's partials (one per thread)
+        // and publishes the group sum; the last group then adds the 16 group sums.  (One
+        // workgroup reading all partials serially cost ~18 us more than the separate pose kernel.)
         const int nb = gridDim.x;
-        if (!last_block_arrive_grouped(reinterpret_cast<uint32_t*>(pf.part + POSE_PARTS * nb))) return;
+        uint32_t* ctr = reinterpret_cast<uint32_t*>(pf.part + POSE_PARTS * nb);
+        float* gsum = pf.part + POSE_PARTS * nb + ARRIVE_GROUPED_WORDS;
+        __shared__ uint32_t s_flag;
+        const uint32_t g = (uint32_t)blockIdx.x & 15u;
+        const uint32_t ngroups = nb < 16 ? (uint32_t)nb : 16u;
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // s_waitcnt vmcnt(0): the partial stores have landed
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t gsize = (uint32_t)nb / 16u + (g < (uint32_t)nb % 16u ? 1u : 0u);
+            uint32_t* gc = ctr + ARRIVE_STRIDE * (1 + g);
+            const bool last = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1;
+            if (last) __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_flag = last;
+        }
+        __syncthreads();
+        if (!s_flag) return;
 #pragma unroll
         for (int k = 0; k < POSE_PARTS; k++) v[k] = 0.f;
-        for (int b = threadIdx.x; b < nb; b += 256)
+        for (int b = (int)g + 16 * threadIdx.x; b < nb; b += 16 * 256)
 #pragma unroll
             for (int k = 0; k < POSE_PARTS; k++) v[k] += ld_agent(pf.part + POSE_PARTS * b + k);
+        __syncthreads();
+        block_sum<POSE_PARTS>(v, s_red, s_tot);
+        __syncthreads();
+        if (threadIdx.x < POSE_PARTS) st_agent(gsum + POSE_PARTS * g + threadIdx.x, s_tot[threadIdx.x]);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const bool last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1;
+            if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_flag = last;
+        }
+        __syncthreads();
+        if (!s_flag) return;
+#pragma unroll
+        for (int k = 0; k < POSE_PARTS; k++) v[k] = threadIdx.x < ngroups ? ld_agent(gsum + POSE_PARTS * threadIdx.x + k) : 0.f;
         __syncthreads();
         block_sum<POSE_PARTS>(v, s_red, s_tot);
         __syncthreads();
@@ -530,7 +564,8 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     }
 }
 
-int pose_fuse_scratch_floats(int P) { return POSE_PARTS * ((P + 255) / 256) + ARRIVE_GROUPED_WORDS; }
+// workgroup partials, arrival counters, the 16 group sums
+int pose_fuse_scratch_floats(int P) { return POSE_PARTS * ((P + 255) / 256) + ARRIVE_GROUPED_WORDS + 16 * POSE_PARTS; }
 
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* inst,
                             RecLayout rec, const GradsOut& out, BwdGuard guard, hipStream_t s, const PoseFuse* pose) {
