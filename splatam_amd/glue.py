@@ -431,15 +431,29 @@ class _TrackIteration(torch.autograd.Function):
         _check(rc, "track_transform_fwd")
         rgb = _f32c(params["rgb_colors"].detach(), "rgb_colors")
         empty = torch.Tensor([])
+        gt_im, gt_d = _f32c(curr["im"], "gt_im"), _f32c(curr["depth"], "gt_depth")
+        H, W = cam.image_height, cam.image_width
+        ctx.pre = None
+        if seed is not None and capacity > 0:  # static mode, static seed: loss + gradient images in the render epilogue
+            seed = _f32c(seed, "seed")
+            scratch = _scratch(mw, lib.gsr_track_forward_scratch_floats(W, H))
+            (n, im, ds, radii, geom, binning, img, _, loss, dim, dds) = _C.track_forward_dual_static(
+                cam, means, rgb, dcol, opac, scales, rot, capacity, status, gt_im, gt_d, cfg.sil_thres, cfg.w_im,
+                cfg.w_depth, seed, scratch)
+            ctx.pre = (dim, dds, seed)
+            ctx.save_for_backward(cam_rots, cam_trans, mw, ur, means, rot, dcol, scales, rgb, radii, geom, binning,
+                                  img, im, ds, gt_im, gt_d, w2c)
+            ctx.meta = (t, T, scols, int(n), cam, cfg)
+            ctx.pose_adam = pose_adam
+            ctx.mark_non_differentiable(radii)
+            ctx.set_materialize_grads(False)
+            return loss, radii
         n, im, ds, radii, geom, binning, img, _ = _C.rasterize_gaussians_dual(
             cam.bg, means, rgb, dcol, opac, scales, rot, cam.scale_modifier, empty, cam.viewmatrix, cam.projmatrix,
             cam.tanfovx, cam.tanfovy, cam.image_height, cam.image_width, empty, cam.sh_degree, cam.campos,
             cam.prefiltered, capacity=capacity, status=status)
-        gt_im, gt_d = _f32c(curr["im"], "gt_im"), _f32c(curr["depth"], "gt_depth")
-        H, W = cam.image_height, cam.image_width
         loss = torch.empty((), **f32)
         scratch = _scratch(mw, lib.gsr_track_scratch_floats(H * W))
-        ctx.pre = None
         if seed is not None:  # static loss seed: the loss gradient images in the same pass
             seed = _f32c(seed, "seed")
             dim, dds = torch.empty_like(im), torch.empty_like(ds)

@@ -124,10 +124,12 @@ def test_graph_tracker_matches_eager_iterations(cuda, fuse_pose):
     assert float(tr.loss) > 0.0
 
 
-def test_graph_tracker_reports_overflow(cuda):
+@pytest.mark.parametrize("fuse_pose", [False, True])
+def test_graph_tracker_reports_overflow(cuda, fuse_pose):
     from splatam_amd.tracker import GraphTracker
     params, curr = _setup(cuda, False)
-    tr = GraphTracker(_pose_leaves(params), curr, 1, iters_per_graph=2, warmup_iters=1, headroom=0.5, min_extra=0)
+    tr = GraphTracker(_pose_leaves(params), curr, 1, iters_per_graph=2, warmup_iters=1, headroom=0.5, min_extra=0,
+                      fuse_pose=fuse_pose)
     tr.run()
     torch.cuda.synchronize()
     assert tr.overflowed()
