@@ -421,14 +421,27 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
 #pragma unroll
         for (int m = 0; m < INST_REC_MAX; m++) acc[m] = 0.f;
         const int np = rec.stride / 2;
-        for (uint32_t e = 0; e < cnt; e++) {
-            const float2* r = reinterpret_cast<const float2*>(inst + (size_t)rec.stride * (off + e));
+        // RU records' loads issued together (one memory round trip per RU instances instead of
+        // per instance), then added in instance order: the same sums, bit for bit
+        constexpr int RU = 4;
+        for (uint32_t e0 = 0; e0 < cnt; e0 += RU) {
+            float2 v[RU][INST_REC_MAX / 2];
 #pragma unroll
-            for (int m = 0; m < INST_REC_MAX / 2; m++)
-                if (m < np) {
-                    const float2 v = r[m];
-                    acc[2 * m] += v.x;
-                    acc[2 * m + 1] += v.y;
+            for (int k = 0; k < RU; k++) {
+                const float2* r = reinterpret_cast<const float2*>(inst + (size_t)rec.stride * (off + e0 + k));
+#pragma unroll
+                for (int m = 0; m < INST_REC_MAX / 2; m++)
+                    v[k][m] = (m < np && e0 + k < cnt) ? r[m] : make_float2(0.f, 0.f);
+            }
+#pragma unroll
+            for (int k = 0; k < RU; k++)
+                if (e0 + k < cnt) {
+#pragma unroll
+                    for (int m = 0; m < INST_REC_MAX / 2; m++)
+                        if (m < np) {
+                            acc[2 * m] += v[k][m].x;
+                            acc[2 * m + 1] += v[k][m].y;
+                        }
                 }
         }
 #pragma unroll
