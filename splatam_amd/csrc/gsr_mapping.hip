@@ -345,6 +345,32 @@ __device__ __forceinline__ float adam_apply(float* p, float g, float* m, float* 
     return np;
 }
 
+// adam_apply on N elements p[k * stride] (k < N): every load is issued before the first
+// store (the pointers may alias as far as the compiler knows, so element-wise calls would
+// serialise one memory round trip per element); same arithmetic, same results
+template <int N>
+__device__ __forceinline__ void adam_apply_n(float* p, const float* g, float* m, float* v, size_t stride, float ss,
+                                             const MapAdam& a) {
+    float pv[N], mv[N], vv[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        pv[k] = p[k * stride];
+        mv[k] = m[k * stride];
+        vv[k] = v[k * stride];
+    }
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        float mm = mv[k], v2 = vv[k];
+        mm = mm + a.w1 * (g[k] - mm);
+        v2 = v2 * a.beta2;
+        v2 = v2 + a.omb2 * g[k] * g[k];
+        const float denom = sqrtf(v2) / a.bc2_sqrt + a.eps;
+        m[k * stride] = mm;
+        v[k * stride] = v2;
+        p[k * stride] = pv[k] + ss * (mm / denom);
+    }
+}
+
 // One lane per Gaussian.  Forward (gsr_track_transform_fwd): m = R p + t,
 // rot = normalize(u) (isotropic) or normalize(quat_mult(c, normalize(u))),
 // opac = sigmoid(lo), scales = exp(ls) (tiled when S = 1), depth colours
@@ -360,10 +386,19 @@ map_transform_bwd_kernel(int P, const float* __restrict__ ur, const float* __res
                          MapAdam adam) {
     const int i = blockIdx.x * GLUE_BLOCK + threadIdx.x;
     const bool step = adam.p[0] != nullptr;
-    if (step && gcol) {  // colour parameters: element k * P + i (coalesced across the wave)
-        for (int k = 0; k < ccols; k++) {
+    if (step && gcol && i < P) {  // colour parameters: element k * P + i (coalesced across the wave)
+        constexpr int CU = 4;  // colour columns per round trip
+        int k = 0;
+        for (; k + CU <= ccols; k += CU) {
             const size_t e = (size_t)k * P + i;
-            if (i < P) adam_apply(adam.p[4] + e, gcol[e], adam.m[4] + e, adam.v[4] + e, adam.step_size[4], adam);
+            float g[CU];
+#pragma unroll
+            for (int j = 0; j < CU; j++) g[j] = gcol[e + (size_t)j * P];
+            adam_apply_n<CU>(adam.p[4] + e, g, adam.m[4] + e, adam.v[4] + e, (size_t)P, adam.step_size[4], adam);
+        }
+        for (; k < ccols; k++) {
+            const size_t e = (size_t)k * P + i;
+            adam_apply(adam.p[4] + e, gcol[e], adam.m[4] + e, adam.v[4] + e, adam.step_size[4], adam);
         }
     }
     if (i >= P) return;
@@ -418,17 +453,16 @@ map_transform_bwd_kernel(int P, const float* __restrict__ ur, const float* __res
         if (dls) for (int k = 0; k < scols; k++) dls[scols * i + k] = dsc[k];
         return;
     }
-#pragma unroll
-    for (int k = 0; k < 3; k++)
-        adam_apply(adam.p[0] + 3 * i + k, dp[k], adam.m[0] + 3 * i + k, adam.v[0] + 3 * i + k, adam.step_size[0], adam);
+    adam_apply_n<3>(adam.p[0] + 3 * i, dp, adam.m[0] + 3 * i, adam.v[0] + 3 * i, 1, adam.step_size[0], adam);
     const float duv[4] = {du.x, du.y, du.z, du.w};
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        adam_apply(adam.p[1] + 4 * i + k, duv[k], adam.m[1] + 4 * i + k, adam.v[1] + 4 * i + k, adam.step_size[1], adam);
+    adam_apply_n<4>(adam.p[1] + 4 * i, duv, adam.m[1] + 4 * i, adam.v[1] + 4 * i, 1, adam.step_size[1], adam);
     adam_apply(adam.p[2] + i, dl, adam.m[2] + i, adam.v[2] + i, adam.step_size[2], adam);
-    for (int k = 0; k < scols; k++)
-        adam_apply(adam.p[3] + scols * i + k, dsc[k], adam.m[3] + scols * i + k, adam.v[3] + scols * i + k,
-                   adam.step_size[3], adam);
+    if (scols == 3)
+        adam_apply_n<3>(adam.p[3] + 3 * i, dsc, adam.m[3] + 3 * i, adam.v[3] + 3 * i, 1, adam.step_size[3], adam);
+    else
+        for (int k = 0; k < scols; k++)
+            adam_apply(adam.p[3] + scols * i + k, dsc[k], adam.m[3] + scols * i + k, adam.v[3] + scols * i + k,
+                       adam.step_size[3], adam);
 }
 
 int map_loss_blocks(int H, int W, dim3& grid) {
