@@ -62,6 +62,10 @@ def parse():
     ap.add_argument("--fuse-pose", type=int, default=1,
                     help="tracking: 1 = pose chain + Adam inside the per-Gaussian backward (one launch fewer), "
                          "0 = separate pose kernel")
+    ap.add_argument("--dropin", choices=("on", "off"), default="on",
+                    help="also time the unchanged-caller path: SURVEY 8(d)'s unit through "
+                         "diff_gaussian_rasterization.GaussianRasterizer, eager (the 'dropin' object)")
+    ap.add_argument("--dropin-frames", type=int, default=3, help="dropin: timed frames of 40 iterations")
     ap.add_argument("--timing", type=int, default=1,
                     help="0: no device-clock timing of render_bwd in the graph (A/B check; no roofline)")
     return ap.parse_args()
@@ -210,6 +214,8 @@ def main():
                 "timing": "in-kernel wall_clock64 (first workgroup start to last workgroup end) of every launch in the timed HIP-graph replays" if tracker is not None
                 else "hipEvents around each launch"}
 
+    dropin = dropin_leg(args, scene, dev) if args.dropin == "on" else None
+
     # ---- CPU baseline: the float32 C oracle on one frame (rank 0, N=1) ------
     cpu = None
     want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
@@ -263,10 +269,67 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items()},
+            "dropin": dropin,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dropin_leg(args, scene, dev, iters_per_frame: int = 40):
+    """SURVEY.md 8(d)'s unit of work as an unchanged scripts/splatam.py runs it: every parameter an
+    nn.Parameter requiring grad (splatam.py:150-155), the literal get_loss(tracking=True) with two
+    diff_gaussian_rasterization.GaussianRasterizer calls (:255,259), loss.backward() (:722), torch Adam over
+    every group (:166-172,723-724), the best-candidate pose (:726-731,760-763) -- eager, one Python
+    iteration at a time.  Returns frames(=iterations)/s and the render-backward kernel's average."""
+    import diff_gaussian_rasterization as dgr
+    from splatam_amd import profiling
+    from splatam_amd.rasterizer import GaussianRasterizer
+    from splatam_amd.slam import as_parameters, camera_settings, init_tracking_params, track_frame_literal, \
+        tracking_variables, transform_to_frame, transformed_params2depthplussilhouette, transformed_params2rendervar
+    P, W, H = scene.P, scene.cam.W, scene.cam.H
+    nf = max(1, args.dropin_frames) + 1
+    base = init_tracking_params(scene, num_frames=nf, device=dev)
+    cam = camera_settings(scene.cam, dev)
+    w2c = torch.eye(4, device=dev)
+    with torch.no_grad():
+        gt = dict(base)
+        gt["cam_unnorm_rots"] = torch.zeros_like(base["cam_unnorm_rots"])
+        gt["cam_unnorm_rots"][0, 0] = 1.0
+        gt["cam_trans"] = torch.zeros_like(base["cam_trans"])
+        tg = transform_to_frame(gt, 0, False, False)
+        im, _, _ = GaussianRasterizer(cam)(**transformed_params2rendervar(gt, tg))
+        ds, _, _ = GaussianRasterizer(cam)(**transformed_params2depthplussilhouette(gt, w2c, tg))
+    curr = {"cam": cam, "w2c": w2c, "im": im.clone(), "depth": ds[0:1].clone()}
+    params = as_parameters(base)
+    variables = tracking_variables(P, dev)
+    R = dgr.GaussianRasterizer
+    track_frame_literal(params, variables, curr, 0, 10, renderer=R)  # warm-up (allocator, kernels)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for f in range(1, nf):
+        track_frame_literal(params, variables, curr, f, iters_per_frame, renderer=R)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    iters = (nf - 1) * iters_per_frame
+    profiling.enable_timing(True)  # separate pass: hipEvents around every stage
+    track_frame_literal(params, variables, curr, 0, 10, renderer=R)
+    torch.cuda.synchronize()
+    st = profiling.read_timing()
+    profiling.enable_timing(False)
+    rb = st["render_bwd"]
+    I_avg = st["render_fwd"]["units"] / max(st["render_fwd"]["launches"], 1)
+    Tt = ((W + 15) // 16) * ((H + 15) // 16)
+    alg = 8 * Tt + 40 * I_avg + 20 * W * H + 44 * P  # SURVEY 8(d): one single-image render backward
+    return {"value": round(iters / dt, 3), "unit": "frames/s", "ms_per_step": round(1000 * dt / iters, 4),
+            "iterations": iters,
+            "path": "unchanged scripts/splatam.py tracking loop body: literal get_loss(tracking=True), "
+                    "2x diff_gaussian_rasterization.GaussianRasterizer + loss.backward() + torch.optim.Adam "
+                    "(all 7 groups) + best-candidate pose, eager",
+            "render_bwd": {"avg_us": round(rb["avg_us"], 2), "launches_per_step": 2,
+                           "alg_bytes_per_launch": int(alg),
+                           "frac": round(alg / (rb["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 5) if rb["avg_us"] else None},
+            "stages_us": {k: round(v["avg_us"], 2) for k, v in st.items()}}
 
 
 def render_bwd_roofline(rb, I_avg, P, W, H, graph: bool):

@@ -29,11 +29,28 @@
  *     powf(value, power) applied per pair before summation.  The two vendored
  *     SH bugs (backward.cu:1067 offset M*gid instead of 3*M*gid, and
  *     backward.cu:1117 dropping SH grads when D==0) are NOT replicated.
+ *
+ * Threads (OpenMP): preprocess over Gaussians, render / backward over tiles.
+ * Results do not depend on the thread count: the backward sums each pair's
+ * terms into the record of its (tile, Gaussian) instance (pixels of a tile in
+ * order), then each Gaussian's records in instance order.  oracle_set_threads
+ * (0 = OpenMP default) sets the count.
+ *
+ * Threshold proximity (test support): the forward flags every pixel with an
+ * evaluated pair whose alpha lies within a relative ALPHA_BAND of 1/255 or
+ * whose test_T lies within a relative T_BAND of 1e-4 (a float32 implementation
+ * may decide such a pair the other way) with bit 0, a T = 0.5 crossing within
+ * T_BAND (the median depth's decision) with bit 1, and `unstable` marks every Gaussian
+ * evaluated at a flagged pixel (its gradient depends on that decision through
+ * T and the accumulated colour).  Per-element gradient checks skip them.
  */
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #ifndef REAL
 #define REAL float
@@ -45,6 +62,19 @@ typedef REAL real;
 
 #define GSR_ORACLE_UPSTREAM 0
 #define GSR_ORACLE_FUSED 1
+#define ALPHA_BAND 2e-5
+#define T_BAND 1e-4
+
+static int g_threads = 0; /* 0: OpenMP default (OMP_NUM_THREADS / all cores) */
+void oracle_set_threads(int n) { g_threads = n < 0 ? 0 : n; }
+static int nthreads(void)
+{
+#ifdef _OPENMP
+    return g_threads > 0 ? g_threads : omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
 
 /* auxiliary.h:22-39 */
 static const real SH_C0 = (real)0.28209479177387814;
@@ -136,6 +166,7 @@ typedef struct {
     real xmul, ymul;          /* backward.cu:175-176: 0 where the clamp is active   */
     real Mx[2][3];            /* M = J V3 (2x3) */
     real a, b, c;             /* cov2D entries after the +0.3 low-pass */
+    int near;                 /* tx/tz or ty/tz within a relative 1e-5 of the clamp limit */
 } proj_t;
 
 static void cov2d_fwd(v3 mean, real fx, real fy, real tanx, real tany, const real* cov3, const real* view, proj_t* o)
@@ -145,6 +176,7 @@ static void cov2d_fwd(v3 mean, real fx, real fy, real tanx, real tany, const rea
     real txtz = t.x / t.z, tytz = t.y / t.z;
     o->xmul = (txtz < -limx || txtz > limx) ? (real)0 : (real)1;
     o->ymul = (tytz < -limy || tytz > limy) ? (real)0 : (real)1;
+    o->near = fabs(fabs((double)txtz) / limx - 1.0) <= 1e-5 || fabs(fabs((double)tytz) / limy - 1.0) <= 1e-5;
     t.x = rmin(limx, rmax(-limx, txtz)) * t.z;
     t.y = rmin(limy, rmax(-limy, tytz)) * t.z;
     o->tx = t.x; o->ty = t.y; o->tz = t.z;
@@ -170,7 +202,8 @@ static void cov2d_fwd(v3 mean, real fx, real fy, real tanx, real tany, const rea
 }
 
 /* forward.cu:20-71: SH -> RGB (+0.5, clamp >= 0, per-channel clamped flags) */
-static void sh_fwd(int deg, int M, v3 pos, const real* campos, const real* sh, real* rgb, unsigned char* clamped)
+static void sh_fwd(int deg, int M, v3 pos, const real* campos, const real* sh, real* rgb, unsigned char* clamped,
+                   unsigned char* near)
 {
     real dx = pos.x - campos[0], dy = pos.y - campos[1], dz = pos.z - campos[2];
     real len = RSQRT(dx * dx + dy * dy + dz * dz);
@@ -198,6 +231,7 @@ static void sh_fwd(int deg, int M, v3 pos, const real* campos, const real* sh, r
 #undef S
         res = res + (real)0.5;
         clamped[ch] = res < (real)0;
+        if (near && fabs((double)res) <= 1e-5) *near = 1; /* the clamp decision sits on its threshold */
         rgb[ch] = rmax(res, (real)0);
     }
 }
@@ -239,6 +273,9 @@ typedef struct {
     int* ranges;      /* [tiles,2] */
     /* allocated here, freed by oracle_free_list */
     int* point_list;  /* [num_rendered] gaussian ids in (tile, depth, id) order */
+    /* optional (NULL: not computed): threshold proximity, see the header */
+    unsigned char* unstable_pix; /* [H*W] */
+    unsigned char* unstable;     /* [P]   */
 } oracle_fwd_out;
 
 typedef struct { uint32_t tile; real depth; int id; } inst_t;
@@ -256,6 +293,7 @@ static int inst_cmp(const void* pa, const void* pb)
 /* forward.cu:155-256 (preprocessCUDA); auxiliary.h:139-164 (in_frustum) */
 static void preprocess(const oracle_in* in, oracle_fwd_out* o, int gx, int gy, real fx, real fy)
 {
+#pragma omp parallel for schedule(static) num_threads(nthreads())
     for (int i = 0; i < in->P; i++) {
         o->radii[i] = 0;
         o->tiles_touched[i] = 0;
@@ -284,8 +322,10 @@ static void preprocess(const oracle_in* in, oracle_fwd_out* o, int gx, int gy, r
         int x0, y0, x1, y1;
         get_rect(px, py, (int)rad, gx, gy, &x0, &y0, &x1, &y1);
         if ((x1 - x0) * (y1 - y0) == 0) continue;
-        if (!in->colors) sh_fwd(in->D, in->M, p, in->campos, in->shs + (size_t)3 * in->M * i, o->rgb + 3 * i, o->clamped + 3 * i);
+        unsigned char nr = (unsigned char)pj.near;
+        if (!in->colors) sh_fwd(in->D, in->M, p, in->campos, in->shs + (size_t)3 * in->M * i, o->rgb + 3 * i, o->clamped + 3 * i, &nr);
         else { for (int c = 0; c < 3; c++) { o->rgb[3 * i + c] = in->colors[3 * i + c]; o->clamped[3 * i + c] = 0; } }
+        if (o->unstable) o->unstable[i] = nr;
         o->depths[i] = pv.z;
         o->radii[i] = (int)rad;
         o->means2D[2 * i] = px; o->means2D[2 * i + 1] = py;
@@ -296,27 +336,32 @@ static void preprocess(const oracle_in* in, oracle_fwd_out* o, int gx, int gy, r
 }
 
 /* forward.cu:261-393 (renderCUDA), one tile at a time, pixels sequential */
-static void render_tile(const oracle_in* in, oracle_fwd_out* o, int tx, int ty, int start, int end, long long* evals)
+static long long render_tile(const oracle_in* in, oracle_fwd_out* o, int tx, int ty, int start, int end)
 {
+    long long evals = 0;
     for (int ly = 0; ly < BLOCK_Y; ly++)
         for (int lx = 0; lx < BLOCK_X; lx++) {
             int px = tx * BLOCK_X + lx, py = ty * BLOCK_Y + ly;
             if (px >= in->W || py >= in->H) continue;
             real T = 1, C[3] = {0, 0, 0}, D = (real)15;
             int contributor = 0, last = 0;
+            unsigned char near = 0;
             for (int k = start; k < end; k++) {
                 contributor++;
-                if (evals) (*evals)++;
+                evals++;
                 int g = o->point_list[k];
                 real dx = o->means2D[2 * g] - (real)px, dy = o->means2D[2 * g + 1] - (real)py;
                 const real* co = o->conic_opacity + 4 * g;
                 real power = (real)-0.5 * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                 if (power > (real)0) continue;
                 real alpha = rmin((real)0.99, co[3] * REXP(power));
+                if (fabs((double)alpha * 255.0 - 1.0) <= ALPHA_BAND) near = 1;
                 if (alpha < (real)1 / (real)255) continue;
                 real test_T = T * ((real)1 - alpha);
+                if (fabs((double)test_T * 1e4 - 1.0) <= T_BAND) near = 1;
                 if (test_T < (real)0.0001) break; /* done = true: no further entries are visited */
                 for (int c = 0; c < 3; c++) C[c] += o->rgb[3 * g + c] * alpha * T;
+                if (fabs((double)test_T * 2.0 - 1.0) <= T_BAND || fabs((double)T * 2.0 - 1.0) <= T_BAND) near |= 2;
                 if (T > (real)0.5 && test_T < (real)0.5) D = o->depths[g];
                 T = test_T;
                 last = contributor;
@@ -326,7 +371,9 @@ static void render_tile(const oracle_in* in, oracle_fwd_out* o, int tx, int ty, 
             o->n_contrib[pid] = last;
             for (int c = 0; c < 3; c++) o->out_color[c * in->H * in->W + pid] = C[c] + T * in->bg[c];
             o->out_depth[pid] = D;
+            if (o->unstable_pix) o->unstable_pix[pid] = near;
         }
+    return evals;
 }
 
 /* rasterizer_impl.cu:198-339 (Rasterizer::forward). Returns num_rendered. */
@@ -336,6 +383,7 @@ int oracle_forward(const oracle_in* in, oracle_fwd_out* o, long long* pair_evals
     real fy = (real)H / ((real)2 * in->tan_fovy);
     real fx = (real)W / ((real)2 * in->tan_fovx);
     int gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
+    if (o->unstable) memset(o->unstable, 0, (size_t)in->P);
     preprocess(in, o, gx, gy, fx, fy);
     /* rasterizer_impl.cu:277-309: scan, duplicateWithKeys, stable sort by (tile, depth) */
     long long I = 0;
@@ -365,12 +413,35 @@ int oracle_forward(const oracle_in* in, oracle_fwd_out* o, long long* pair_evals
         if (k == I - 1 || inst[k + 1].tile != t) o->ranges[2 * t + 1] = (int)(k + 1);
     }
     free(inst);
-    if (pair_evals) *pair_evals = 0;
-    for (int ty = 0; ty < gy; ty++)
-        for (int tx = 0; tx < gx; tx++) {
-            int t = ty * gx + tx;
-            render_tile(in, o, tx, ty, o->ranges[2 * t], o->ranges[2 * t + 1], pair_evals);
+    long long ev = 0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : ev) num_threads(nthreads())
+    for (int t = 0; t < gx * gy; t++)
+        ev += render_tile(in, o, t % gx, t / gx, o->ranges[2 * t], o->ranges[2 * t + 1]);
+    if (pair_evals) *pair_evals = ev;
+    if (o->unstable_pix && o->unstable) {
+        /* every Gaussian with a (near-)contributing pair at a flagged pixel, up to the (near-)terminating
+         * pair: its per-pair terms there depend on the flagged decision through T and the accumulated colour */
+        for (int pid = 0; pid < W * H; pid++) {
+            if (!(o->unstable_pix[pid] & 1)) continue;
+            int px = pid % W, py = pid / W, t = (py / BLOCK_Y) * gx + px / BLOCK_X;
+            int start = o->ranges[2 * t], end = o->ranges[2 * t + 1];
+            double T = 1.0;
+            for (int k = start; k < end; k++) {
+                int g = o->point_list[k];
+                double dx = (double)o->means2D[2 * g] - px, dy = (double)o->means2D[2 * g + 1] - py;
+                const real* co = o->conic_opacity + 4 * g;
+                double pw = -0.5 * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                if (pw > 0) continue;
+                double a = co[3] * exp(pw);
+                if (a > 0.99) a = 0.99;
+                if (a * 255.0 < 1.0 - 2 * ALPHA_BAND) continue;
+                o->unstable[g] = 1;
+                if (a * 255.0 < 1.0) continue;
+                T *= 1.0 - a;
+                if (T * 1e4 < 1.0 - 2 * T_BAND) break;
+            }
         }
+    }
     return (int)I;
 }
 
@@ -569,11 +640,20 @@ static void chain(const oracle_in* in, const oracle_fwd_out* fo, int g, const re
 
 static inline real apply_power(real v, int p) { return p == 1 ? v : RPOW(v, (real)p); }
 
-/* Per-pixel back-to-front pass (backward.cu:586-748 / 850-1040). For every
- * contributing pair calls sink(g, g2) with the 9 per-pair 2D quantities. */
+/* Per-pixel back-to-front pass (backward.cu:586-748 / 850-1040).  Every
+ * contributing pair's terms go to the record of its (tile, Gaussian) instance
+ * (its index k in point_list): upstream mode the 9 per-pair 2D quantities,
+ * fused mode the per-pair chain outputs after powf.  Tiles run in parallel,
+ * the pixels of a tile in order; the records are then added per Gaussian in
+ * instance order, so the sums do not depend on the thread count. */
+#define NV_FUSED_FIXED 22 /* dcolors 3, dmeans2D 2, dmeans3D 3, dcov3D 6, dscales 3, drot 4, dopacity 1 */
 int oracle_backward(const oracle_in* in, const oracle_fwd_out* fo, const real* dL_dpix, int mode, int power,
-                    oracle_grads* go, long long* pair_evals, long long* pair_contrib)
+                    oracle_grads* go, long long* pair_evals, long long* pair_contrib, oracle_grads* gs)
 {
+    /* gs (upstream mode, optional): per-element error scale of every gradient -- the
+     * chain's Jacobian in absolute value applied to the per-Gaussian sums of |per-pair
+     * term| (a float32 sum of those terms is accurate to a small multiple of
+     * eps * scale whatever the cancellation); NULL skips it. */
     int P = in->P, W = in->W, H = in->H;
     real fy = (real)H / ((real)2 * in->tan_fovy);
     real fx = (real)W / ((real)2 * in->tan_fovx);
@@ -589,15 +669,33 @@ int oracle_backward(const oracle_in* in, const oracle_fwd_out* fo, const real* d
     if (go->dsh) memset(go->dsh, 0, sizeof(real) * 3 * (size_t)in->M * P);
     memset(go->dscales, 0, sizeof(real) * 3 * (size_t)P);
     memset(go->drot, 0, sizeof(real) * 4 * (size_t)P);
-    real* acc2 = NULL; /* per-Gaussian 2D sums (upstream mode) */
-    if (mode == GSR_ORACLE_UPSTREAM) acc2 = (real*)calloc((size_t)P * 9, sizeof(real));
-    real* outbuf = (real*)malloc(sizeof(real) * (NOUT_FIXED + 48));
+    if (gs) {
+        if (mode != GSR_ORACLE_UPSTREAM) return -1;
+        memset(gs->dmeans2D, 0, sizeof(real) * 3 * (size_t)P);
+        memset(gs->dcolors, 0, sizeof(real) * 3 * (size_t)P);
+        memset(gs->dopacity, 0, sizeof(real) * (size_t)P);
+        memset(gs->dmeans3D, 0, sizeof(real) * 3 * (size_t)P);
+        memset(gs->dcov3D, 0, sizeof(real) * 6 * (size_t)P);
+        if (gs->dsh) memset(gs->dsh, 0, sizeof(real) * 3 * (size_t)in->M * P);
+        memset(gs->dscales, 0, sizeof(real) * 3 * (size_t)P);
+        memset(gs->drot, 0, sizeof(real) * 4 * (size_t)P);
+    }
+    long long I = 0;
+    for (int t = 0; t < gx * gy; t++)
+        if (fo->ranges[2 * t + 1] > I) I = fo->ranges[2 * t + 1];
+    const int NVS = mode == GSR_ORACLE_UPSTREAM ? 9 : NV_FUSED_FIXED + 3 * nsh;
+    const int NV = (mode == GSR_ORACLE_UPSTREAM && gs) ? 18 : NVS; /* + the |term| sums */
+    real* rec = (real*)calloc((size_t)(I > 0 ? I : 1) * NV, sizeof(real));
+    if (!rec) return -2;
     real ddelx = (real)(0.5 * W), ddely = (real)(0.5 * H);
     real bgdot_w[3] = {in->bg[0], in->bg[1], in->bg[2]};
     long long ev = 0, ct = 0;
-    for (int ty = 0; ty < gy; ty++)
-        for (int tx = 0; tx < gx; tx++) {
-            int t = ty * gx + tx;
+#pragma omp parallel num_threads(nthreads()) reduction(+ : ev, ct)
+    {
+        real* outbuf = (real*)malloc(sizeof(real) * (NOUT_FIXED + 48));
+#pragma omp for schedule(dynamic, 4)
+        for (int t = 0; t < gx * gy; t++) {
+            int tx = t % gx, ty = t / gx;
             int start = fo->ranges[2 * t], end = fo->ranges[2 * t + 1];
             for (int ly = 0; ly < BLOCK_Y; ly++)
                 for (int lx = 0; lx < BLOCK_X; lx++) {
@@ -649,48 +747,104 @@ int oracle_backward(const oracle_in* in, const oracle_fwd_out* fo, const real* d
                         g2[3] = (real)-0.5 * gdx * dy * dL_dG;
                         g2[4] = (real)-0.5 * gdy * dy * dL_dG;
                         g2[5] = G * dL_dalpha;
+                        real* r = rec + (size_t)k * NV;
                         if (mode == GSR_ORACLE_UPSTREAM) {
-                            for (int q = 0; q < 9; q++) acc2[9 * g + q] += g2[q];
+                            for (int q = 0; q < 9; q++) r[q] += g2[q];
+                            if (NV == 18)
+                                for (int q = 0; q < 9; q++) r[9 + q] += g2[q] < 0 ? -g2[q] : g2[q];
                         } else {
                             /* backward.cu:1040-1137: chain per pair, powf per pair, then sum */
                             chain(in, fo, g, g2, fx, fy, outbuf);
-                            for (int c = 0; c < 3; c++) go->dcolors[3 * g + c] += apply_power(g2[6 + c], power);
-                            go->dmeans2D[3 * g] += apply_power(g2[0], power);
-                            go->dmeans2D[3 * g + 1] += apply_power(g2[1], power);
-                            for (int c = 0; c < 3; c++) go->dmeans3D[3 * g + c] += apply_power(outbuf[c], power);
-                            for (int c = 0; c < 6; c++) go->dcov3D[6 * g + c] += apply_power(outbuf[3 + c], power);
-                            if (go->dsh && nsh > 0)
-                                for (int c = 0; c < 3 * nsh; c++) go->dsh[(size_t)3 * in->M * g + c] += apply_power(outbuf[NOUT_FIXED + c], power);
+                            for (int c = 0; c < 3; c++) r[c] += apply_power(g2[6 + c], power);
+                            r[3] += apply_power(g2[0], power);
+                            r[4] += apply_power(g2[1], power);
+                            for (int c = 0; c < 3; c++) r[5 + c] += apply_power(outbuf[c], power);
+                            for (int c = 0; c < 6; c++) r[8 + c] += apply_power(outbuf[3 + c], power);
                             if (in->scales) {
-                                for (int c = 0; c < 3; c++) go->dscales[3 * g + c] += apply_power(outbuf[9 + c], power);
-                                for (int c = 0; c < 4; c++) go->drot[4 * g + c] += apply_power(outbuf[12 + c], power);
+                                for (int c = 0; c < 3; c++) r[14 + c] += apply_power(outbuf[9 + c], power);
+                                for (int c = 0; c < 4; c++) r[17 + c] += apply_power(outbuf[12 + c], power);
                             }
-                            go->dopacity[g] += apply_power(g2[5], power);
+                            r[21] += apply_power(g2[5], power);
+                            for (int c = 0; c < 3 * nsh; c++) r[22 + c] += apply_power(outbuf[NOUT_FIXED + c], power);
                         }
                     }
                 }
         }
+        free(outbuf);
+    }
+    /* per-Gaussian sums of the instance records, in instance order */
+    real* acc = (real*)calloc((size_t)(P > 0 ? P : 1) * NV, sizeof(real));
+    for (long long k = 0; k < I; k++) {
+        int g = fo->point_list[k];
+        real* a = acc + (size_t)g * NV;
+        const real* r = rec + (size_t)k * NV;
+        for (int q = 0; q < NV; q++) a[q] += r[q];
+    }
+    free(rec);
     if (mode == GSR_ORACLE_UPSTREAM) {
-        for (int g = 0; g < P; g++) {
-            if (fo->radii[g] <= 0) continue;
-            const real* a2 = acc2 + 9 * g;
-            go->dmeans2D[3 * g] = a2[0];
-            go->dmeans2D[3 * g + 1] = a2[1];
-            go->dopacity[g] = a2[5];
-            for (int c = 0; c < 3; c++) go->dcolors[3 * g + c] = a2[6 + c];
-            chain(in, fo, g, a2, fx, fy, outbuf);
-            for (int c = 0; c < 3; c++) go->dmeans3D[3 * g + c] = outbuf[c];
-            for (int c = 0; c < 6; c++) go->dcov3D[6 * g + c] = outbuf[3 + c];
-            if (go->dsh && nsh > 0)
-                for (int c = 0; c < 3 * nsh; c++) go->dsh[(size_t)3 * in->M * g + c] = outbuf[NOUT_FIXED + c];
-            if (in->scales) {
-                for (int c = 0; c < 3; c++) go->dscales[3 * g + c] = outbuf[9 + c];
-                for (int c = 0; c < 4; c++) go->drot[4 * g + c] = outbuf[12 + c];
+#pragma omp parallel num_threads(nthreads())
+        {
+            real* outbuf = (real*)malloc(sizeof(real) * (NOUT_FIXED + 48));
+#pragma omp for schedule(static)
+            for (int g = 0; g < P; g++) {
+                if (fo->radii[g] <= 0) continue;
+                const real* a2 = acc + (size_t)NV * g;
+                go->dmeans2D[3 * g] = a2[0];
+                go->dmeans2D[3 * g + 1] = a2[1];
+                go->dopacity[g] = a2[5];
+                for (int c = 0; c < 3; c++) go->dcolors[3 * g + c] = a2[6 + c];
+                chain(in, fo, g, a2, fx, fy, outbuf);
+                for (int c = 0; c < 3; c++) go->dmeans3D[3 * g + c] = outbuf[c];
+                for (int c = 0; c < 6; c++) go->dcov3D[6 * g + c] = outbuf[3 + c];
+                if (go->dsh && nsh > 0)
+                    for (int c = 0; c < 3 * nsh; c++) go->dsh[(size_t)3 * in->M * g + c] = outbuf[NOUT_FIXED + c];
+                if (in->scales) {
+                    for (int c = 0; c < 3; c++) go->dscales[3 * g + c] = outbuf[9 + c];
+                    for (int c = 0; c < 4; c++) go->drot[4 * g + c] = outbuf[12 + c];
+                }
+                if (NV == 18) { /* error scale: |J| applied to the |term| sums (chain is linear in g2) */
+                    const real* s2 = acc + (size_t)18 * g + 9;
+                    real sc[NOUT_FIXED + 48], e[9], col[NOUT_FIXED + 48];
+                    const int no = NOUT_FIXED + 3 * nsh;
+                    for (int q = 0; q < no; q++) sc[q] = 0;
+                    for (int q = 0; q < 9; q++) {
+                        if (s2[q] == 0) continue;
+                        for (int u = 0; u < 9; u++) e[u] = u == q ? 1 : 0;
+                        chain(in, fo, g, e, fx, fy, col);
+                        for (int o2 = 0; o2 < no; o2++) sc[o2] += (col[o2] < 0 ? -col[o2] : col[o2]) * s2[q];
+                    }
+                    gs->dmeans2D[3 * g] = s2[0];
+                    gs->dmeans2D[3 * g + 1] = s2[1];
+                    gs->dopacity[g] = s2[5];
+                    for (int c = 0; c < 3; c++) gs->dcolors[3 * g + c] = s2[6 + c];
+                    for (int c = 0; c < 3; c++) gs->dmeans3D[3 * g + c] = sc[c];
+                    for (int c = 0; c < 6; c++) gs->dcov3D[6 * g + c] = sc[3 + c];
+                    if (gs->dsh && nsh > 0)
+                        for (int c = 0; c < 3 * nsh; c++) gs->dsh[(size_t)3 * in->M * g + c] = sc[NOUT_FIXED + c];
+                    if (in->scales) {
+                        for (int c = 0; c < 3; c++) gs->dscales[3 * g + c] = sc[9 + c];
+                        for (int c = 0; c < 4; c++) gs->drot[4 * g + c] = sc[12 + c];
+                    }
+                }
             }
+            free(outbuf);
+        }
+    } else {
+        for (int g = 0; g < P; g++) {
+            const real* a = acc + (size_t)NV * g;
+            for (int c = 0; c < 3; c++) go->dcolors[3 * g + c] = a[c];
+            go->dmeans2D[3 * g] = a[3];
+            go->dmeans2D[3 * g + 1] = a[4];
+            for (int c = 0; c < 3; c++) go->dmeans3D[3 * g + c] = a[5 + c];
+            for (int c = 0; c < 6; c++) go->dcov3D[6 * g + c] = a[8 + c];
+            for (int c = 0; c < 3; c++) go->dscales[3 * g + c] = a[14 + c];
+            for (int c = 0; c < 4; c++) go->drot[4 * g + c] = a[17 + c];
+            go->dopacity[g] = a[21];
+            if (go->dsh && nsh > 0)
+                for (int c = 0; c < 3 * nsh; c++) go->dsh[(size_t)3 * in->M * g + c] = a[22 + c];
         }
     }
-    free(acc2);
-    free(outbuf);
+    free(acc);
     if (pair_evals) *pair_evals = ev;
     if (pair_contrib) *pair_contrib = ct;
     return 0;

@@ -30,6 +30,16 @@ def build() -> None:
 
 
 _libs: dict = {}
+_threads = 0  # 0: OpenMP default (OMP_NUM_THREADS or every core); results do not depend on it
+
+
+def set_threads(n: int) -> None:
+    """Threads of the oracle's parallel loops (0 = OpenMP default).  The results are
+    identical for any count (fixed-order per-instance sums, see gsr_oracle.c)."""
+    global _threads
+    _threads = int(n)
+    for lib, *_ in _libs.values():
+        lib.oracle_set_threads(_threads)
 
 
 def _lib(dtype):
@@ -58,7 +68,8 @@ def _lib(dtype):
                         ("rgb", P(real)), ("clamped", P(ctypes.c_ubyte)),
                         ("tiles_touched", P(ctypes.c_int)), ("final_T", P(real)),
                         ("n_contrib", P(ctypes.c_int)), ("ranges", P(ctypes.c_int)),
-                        ("point_list", P(ctypes.c_int))]
+                        ("point_list", P(ctypes.c_int)), ("unstable_pix", P(ctypes.c_ubyte)),
+                        ("unstable", P(ctypes.c_ubyte))]
 
         class Grads(ctypes.Structure):
             _fields_ = [("dmeans2D", P(real)), ("dcolors", P(real)), ("dopacity", P(real)),
@@ -68,10 +79,12 @@ def _lib(dtype):
         lib.oracle_forward.argtypes = [P(In), P(FwdOut), P(ctypes.c_longlong)]
         lib.oracle_forward.restype = ctypes.c_int
         lib.oracle_backward.argtypes = [P(In), P(FwdOut), P(real), ctypes.c_int, ctypes.c_int, P(Grads),
-                                        P(ctypes.c_longlong), P(ctypes.c_longlong)]
+                                        P(ctypes.c_longlong), P(ctypes.c_longlong), P(Grads)]
         lib.oracle_backward.restype = ctypes.c_int
         lib.oracle_free_list.argtypes = [P(FwdOut)]
         lib.oracle_mark_visible.argtypes = [ctypes.c_int, P(real), P(real), P(ctypes.c_ubyte)]
+        lib.oracle_set_threads.argtypes = [ctypes.c_int]
+        lib.oracle_set_threads(_threads)
         _libs[key] = (lib, real, In, FwdOut, Grads)
     return _libs[key]
 
@@ -107,6 +120,9 @@ class ForwardResult:
     ranges: np.ndarray         # [tiles,2] int32
     point_list: np.ndarray     # [num_rendered] int32
     pair_evals: int
+    unstable: np.ndarray       # [P] bool: evaluated at a pixel with an alpha / T decision near its threshold
+    unstable_pix: np.ndarray   # [H,W] bool: an alpha / T(1e-4) decision near its threshold
+    unstable_depth_pix: np.ndarray  # [H,W] bool: a T = 0.5 crossing (median depth) near its threshold
     _keep: dict = field(default_factory=dict, repr=False)
 
 
@@ -137,7 +153,10 @@ def forward(means3D, opacities, *, view, proj, campos, tanfovx, tanfovy, H, W, b
              clamped=np.zeros((P, 3), np.uint8), tiles_touched=np.zeros(P, np.int32),
              final_T=np.zeros((H, W), dtype), n_contrib=np.zeros((H, W), np.int32),
              ranges=np.zeros((gx * gy, 2), np.int32))
-    fo = FwdOut(out_color=_ptr(o["color"], real), out_depth=_ptr(o["depth"], real),
+    unstable_pix = np.zeros((H, W), np.uint8)
+    unstable = np.zeros(P, np.uint8)
+    fo = FwdOut(unstable_pix=_ptr(unstable_pix, ctypes.c_ubyte), unstable=_ptr(unstable, ctypes.c_ubyte),
+                out_color=_ptr(o["color"], real), out_depth=_ptr(o["depth"], real),
                 radii=_ptr(o["radii"], ctypes.c_int), means2D=_ptr(o["means2D"], real),
                 depths=_ptr(o["depths"], real), conic_opacity=_ptr(o["conic_opacity"], real),
                 rgb=_ptr(o["rgb"], real), clamped=_ptr(o["clamped"], ctypes.c_ubyte),
@@ -150,12 +169,17 @@ def forward(means3D, opacities, *, view, proj, campos, tanfovx, tanfovy, H, W, b
     keep["inp"] = inp
     keep["dtype"] = np.dtype(dtype)
     keep["M"] = M
-    return ForwardResult(num_rendered=n, point_list=pl, pair_evals=evals.value, _keep=keep, **o)
+    return ForwardResult(num_rendered=n, point_list=pl, pair_evals=evals.value, _keep=keep,
+                         unstable=unstable.astype(bool), unstable_pix=(unstable_pix & 1).astype(bool),
+                         unstable_depth_pix=(unstable_pix & 2).astype(bool), **o)
 
 
-def backward(fr: ForwardResult, dL_dcolor, *, power=1, mode=UPSTREAM) -> dict:
+def backward(fr: ForwardResult, dL_dcolor, *, power=1, mode=UPSTREAM, error_scale=False) -> dict:
     """Reference backward; returns a dict with the 8 gradient arrays of
-    rasterize_points.cu:195 plus pair counters."""
+    rasterize_points.cu:195 plus pair counters.  error_scale=True (upstream mode): also
+    g["scale"], the per-element error scale of each gradient (|Jacobian of the chain| applied
+    to each Gaussian's sums of |per-pair term|): a float32 implementation's error on an
+    element is a small multiple of eps * scale, whatever cancellation the sum has."""
     dtype = fr._keep["dtype"]
     lib, real, In, FwdOut, Grads = _lib(dtype)
     P = fr.radii.shape[0]
@@ -178,10 +202,20 @@ def backward(fr: ForwardResult, dL_dcolor, *, power=1, mode=UPSTREAM) -> dict:
                dscales=_ptr(g["dscales"], real), drot=_ptr(g["drot"], real))
     dpix = np.ascontiguousarray(np.asarray(dL_dcolor, dtype).reshape(3, H, W))
     ev, ct = ctypes.c_longlong(0), ctypes.c_longlong(0)
+    gsp = None
+    if error_scale:
+        sc = {k: np.zeros_like(v) for k, v in g.items()}
+        gsp = Grads(dmeans2D=_ptr(sc["dmeans2D"], real), dcolors=_ptr(sc["dcolors"], real),
+                    dopacity=_ptr(sc["dopacity"], real), dmeans3D=_ptr(sc["dmeans3D"], real),
+                    dcov3D=_ptr(sc["dcov3D"], real), dsh=_ptr(sc["dsh"] if M else None, real),
+                    dscales=_ptr(sc["dscales"], real), drot=_ptr(sc["drot"], real))
     rc = lib.oracle_backward(ctypes.byref(fr._keep["inp"]), ctypes.byref(fo), _ptr(dpix, real), int(mode),
-                             int(power), ctypes.byref(go), ctypes.byref(ev), ctypes.byref(ct))
+                             int(power), ctypes.byref(go), ctypes.byref(ev), ctypes.byref(ct),
+                             ctypes.byref(gsp) if gsp is not None else None)
     if rc != 0:
-        raise ValueError("oracle_backward: upstream mode supports power == 1 only")
+        raise ValueError("oracle_backward: upstream mode (and error_scale) support power == 1 only")
+    if error_scale:
+        g["scale"] = sc
     g["pair_evals"] = ev.value
     g["pair_contrib"] = ct.value
     return g

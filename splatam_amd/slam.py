@@ -163,7 +163,7 @@ def _get_loss_tracking_fused(params, curr_data, iter_time_idx, cfg: TrackingConf
 
 
 def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = TrackingConfig(), fast=True,
-                      fused=True, dual=True, fuse_pose=False):
+                      fused=True, dual=True, fuse_pose=False, variables=None, renderer=None):
     """scripts/splatam.py:220-353 with tracking=True: two renders (RGB, [z,1,z^2]), masked L1 sums.
 
     fused=True (and fused_eligible): the pose transform / rendervar builders and
@@ -175,7 +175,8 @@ def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = Tr
     and the pose transform avoids the K=P GEMM (see _affine).  fast=False is the
     literal statement of the reference code.  fuse_pose=True (with fused, dual): one autograd node for the
     whole iteration whose backward fuses the pose chain into the rasterizer's per-Gaussian backward
-    (glue.tracking_iteration, gsr_track_backward_dual)."""
+    (glue.tracking_iteration, gsr_track_backward_dual).  variables: SplaTAM's densification statistics,
+    updated like splatam.py:257,349-351 (literal path only)."""
     if fused and fast and fused_eligible(params, curr_data, cfg):
         if fuse_pose and dual:
             from .glue import tracking_iteration
@@ -185,9 +186,10 @@ def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = Tr
     tg = transform_to_frame(params, iter_time_idx, gaussians_grad=False, camera_grad=True, fast=fast)
     rendervar = transformed_params2rendervar(params, tg)
     depth_sil_rendervar = transformed_params2depthplussilhouette(params, curr_data["w2c"], tg, fast=fast)
+    Renderer = GaussianRasterizer if renderer is None else renderer
     rendervar["means2D"].retain_grad()
-    im, radius, _ = GaussianRasterizer(raster_settings=curr_data["cam"])(**rendervar)
-    depth_sil, _, _ = GaussianRasterizer(raster_settings=curr_data["cam"])(**depth_sil_rendervar)
+    im, radius, _ = Renderer(raster_settings=curr_data["cam"])(**rendervar)
+    depth_sil, _, _ = Renderer(raster_settings=curr_data["cam"])(**depth_sil_rendervar)
     depth = depth_sil[0, :, :].unsqueeze(0)
     silhouette = depth_sil[1, :, :]
     presence_sil_mask = silhouette > cfg.sil_thres
@@ -207,6 +209,11 @@ def get_loss_tracking(params, curr_data, iter_time_idx, cfg: TrackingConfig = Tr
         loss_depth = torch.abs(curr_data["depth"] - depth)[mask].sum()
         loss_im = torch.abs(curr_data["im"] - im)[color_mask].sum()
     loss = cfg.w_im * loss_im + cfg.w_depth * loss_depth
+    if variables is not None:  # splatam.py:257,349-351
+        variables["means2D"] = rendervar["means2D"]
+        seen = radius > 0
+        variables["max_2D_radius"][seen] = torch.max(radius[seen], variables["max_2D_radius"][seen])
+        variables["seen"] = seen
     return loss, radius, rendervar["means2D"]
 
 
@@ -379,3 +386,58 @@ def mapping_optimizer(params: dict, cfg: MappingConfig = MappingConfig(), fused=
         from .glue import FusedAdam
         return FusedAdam(groups, lr=0.0, eps=1e-15)
     return torch.optim.Adam(groups, lr=0.0, eps=1e-15)
+
+
+# ------------------------------------------------ literal per-frame tracking --
+TRACKING_LRS = dict(means3D=0.0, rgb_colors=0.0, unnorm_rotations=0.0, logit_opacities=0.0, log_scales=0.0,
+                    cam_unnorm_rots=0.0004, cam_trans=0.002)  # configs/replica/splatam.py:71-79
+
+
+def as_parameters(params: dict) -> dict:
+    """initialize_params (scripts/splatam.py:150-155): every entry an nn.Parameter requiring grad."""
+    return {k: torch.nn.Parameter(v.detach().clone().float().contiguous().requires_grad_(True))
+            for k, v in params.items()}
+
+
+def tracking_variables(P: int, device) -> dict:
+    """scripts/splatam.py:157-160."""
+    z = lambda: torch.zeros(P, device=device, dtype=torch.float32)  # noqa: E731
+    return {"max_2D_radius": z(), "means2D_gradient_accum": z(), "denom": z(), "timestep": z()}
+
+
+def tracking_optimizer(params: dict, lrs: dict = TRACKING_LRS):
+    """initialize_optimizer(params, lrs, tracking=True) (scripts/splatam.py:166-172): torch Adam, one group
+    per parameter, default eps."""
+    return torch.optim.Adam([{"params": [v], "name": k, "lr": lrs[k]} for k, v in params.items()])
+
+
+def track_frame_literal(params, variables, curr_data, time_idx, num_iters, cfg: TrackingConfig = TrackingConfig(),
+                        optimizer=None, losses_out=None, renderer=None):
+    """The unchanged tracking loop body of scripts/splatam.py:700-763 for one frame (use_gt_poses=False,
+    no depth-loss-threshold extension): get_loss(tracking=True) through two GaussianRasterizer calls,
+    loss.backward(), Adam over every parameter group, zero_grad, the best-candidate pose kept by loss
+    (:726-731) and written back after the last iteration (:760-763).  renderer: the GaussianRasterizer class
+    the caller imports (default splatam_amd's; diff_gaussian_rasterization's is the same drop-in).
+    Returns the optimizer."""
+    if optimizer is None:
+        optimizer = tracking_optimizer(params)
+    cand_rot = params["cam_unnorm_rots"][..., time_idx].detach().clone()
+    cand_tran = params["cam_trans"][..., time_idx].detach().clone()
+    current_min_loss = float(1e20)
+    for _ in range(num_iters):
+        loss, _radius, _m2d = get_loss_tracking(params, curr_data, time_idx, cfg, fast=False, fused=False,
+                                                variables=variables, renderer=renderer)
+        loss.backward()
+        optimizer.step()
+        optimizer.zero_grad(set_to_none=True)
+        with torch.no_grad():
+            if losses_out is not None:
+                losses_out.append(loss.detach())
+            if loss < current_min_loss:
+                current_min_loss = loss
+                cand_rot = params["cam_unnorm_rots"][..., time_idx].detach().clone()
+                cand_tran = params["cam_trans"][..., time_idx].detach().clone()
+    with torch.no_grad():
+        params["cam_unnorm_rots"][..., time_idx] = cand_rot
+        params["cam_trans"][..., time_idx] = cand_tran
+    return optimizer

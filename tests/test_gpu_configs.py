@@ -1,5 +1,5 @@
 """BASELINE.json configurations at full size, rasterizer vs the CPU oracle (fwd+bwd
-through the C ABI), same tolerances as tests/test_gpu_parity.py:
+through the C ABI):
 
   * config 1: 10k isotropic Gaussians, 320x240;
   * config 2: 100k isotropic Gaussians, 640x480 (Replica room0 intrinsics);
@@ -10,7 +10,18 @@ through the C ABI), same tolerances as tests/test_gpu_parity.py:
     high portrait, fx = fy = 625.22, 300k Gaussians (the tile grid
     is 30x40 instead of 40x30).
 
-The oracle runs single-threaded float32 C (~30 s for config 4)."""
+Criteria:
+  * integer work bit-exact against the float32 oracle (the reference's float32
+    arithmetic): num_rendered, every tile range, the sorted Gaussian-id list,
+    every radius, and n_contrib at every pixel without an alpha / T decision near
+    its threshold;
+  * forward RGB within 1e-4 * max(1, |ref|) at every pixel without such a decision
+    (and on >= 99.9 % overall), median depth equal except where T = 0.5 is crossed
+    near the threshold;
+  * gradients against the float64 oracle per tensor and per element
+    (harness.check_grad_accuracy), plus relative L2 <= 1e-4 against the float32 oracle.
+
+The oracle runs multi-threaded C (OpenMP; results independent of the thread count)."""
 import numpy as np
 import pytest
 
@@ -33,14 +44,37 @@ def test_baseline_config_parity(cuda, cfg):
     use_sh = scene.shs is not None
     dpix = np.random.RandomState(11).randn(3, c.H, c.W).astype(np.float32)
     gpu = harness.run_gpu(scene, dpix, use_sh=use_sh)
+    binning = harness.binning_gpu(scene, use_sh=use_sh)
     fr, ref = harness.run_oracle(scene, dpix, use_sh=use_sh)
-    # tile instances: every Gaussian with radius > 0 is duplicated over its tile rect
+    fr64, ref64 = harness.run_oracle(scene, dpix, use_sh=use_sh, dtype=np.float64, error_scale=True)
+
+    # ---- integer work: bit-exact -------------------------------------------------
     assert fr.num_rendered > 0 and int(fr.tiles_touched.sum()) == fr.num_rendered
+    assert binning["num_rendered"] == fr.num_rendered
+    np.testing.assert_array_equal(gpu["radii"], fr.radii)
+    np.testing.assert_array_equal(binning["radii"], fr.radii)
+    cnt = fr.ranges[:, 1] - fr.ranges[:, 0]
+    np.testing.assert_array_equal(binning["ranges"][:, 1] - binning["ranges"][:, 0], cnt)
+    np.testing.assert_array_equal(binning["ranges"][cnt > 0], fr.ranges[cnt > 0])  # empty tiles: any start
+    np.testing.assert_array_equal(binning["point_list"], fr.point_list)
+    settled = ~fr.unstable_pix
+    nc = binning["n_contrib"].reshape(c.H, c.W)
+    assert np.array_equal(nc[settled], fr.n_contrib[settled])
+
+    # ---- forward images -------------------------------------------------------------
     fwd = harness.compare_forward(gpu, fr)
     assert fwd["frac_bad"] <= 1e-3, fwd
-    assert fwd["radii_match"] >= 0.999, fwd
-    assert fwd["depth_match"] >= 0.995, fwd
+    col = np.asarray(gpu["color"], np.float64)
+    bad = (np.abs(col - fr.color) > 1e-4 * np.maximum(1.0, np.abs(fr.color))).any(axis=0)
+    assert not (bad & settled).any(), int((bad & settled).sum())
+    depth_ok = (np.asarray(gpu["depth"])[0] == fr.depth[0]) | fr.unstable_depth_pix | fr.unstable_pix
+    assert depth_ok.all(), int((~depth_ok).sum())
+
+    # ---- gradients --------------------------------------------------------------------
     errs = harness.compare_grads(gpu["grads"], ref)
-    bad = {k: v for k, v in errs.items() if v > 1e-4}
-    assert not bad, errs
-    print(cfg, fwd, {k: f"{v:.2e}" for k, v in errs.items()})
+    assert not {k: v for k, v in errs.items() if v > 1e-4}, errs
+    stable = ~(fr.unstable | fr64.unstable)
+    g, o = harness.check_grad_accuracy(gpu["grads"], ref, ref64, stable)
+    print(cfg, fwd, "unstable", int((~stable).sum()), {k: f"{v:.2e}" for k, v in errs.items()})
+    for k in g:
+        print(f"  {k}: gpu {g[k]}  oracle_f32 {o[k]}")
