@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=("auto", "on", "off"), default="auto")
     ap.add_argument("--graph", type=int, default=1, help="1: replay the tracking iterations as a HIP graph")
     ap.add_argument("--iters-per-graph", type=int, default=20)
+    ap.add_argument("--frame-iters", type=int, default=40,
+                    help="tracking iterations per frame (configs/replica/splatam.py:15); the timed loop runs whole "
+                         "frames: fresh optimizer, replays, best-candidate pose written back")
     ap.add_argument("--fuse-pose", type=int, default=1,
                     help="tracking: 1 = pose chain + Adam inside the per-Gaussian backward (one launch fewer), "
                          "0 = separate pose kernel")
@@ -143,13 +146,14 @@ def main():
         # HIP graph of S tracking iterations (splatam_amd/tracker.py); warm-up and timed
         # region are whole replays, so K is rounded up to a multiple of S
         from splatam_amd.tracker import GraphTracker
-        S = max(1, min(args.iters_per_graph, args.steps))
-        steps = -(-args.steps // S) * S
+        S = max(1, min(args.iters_per_graph, args.frame_iters))
+        FI = -(-args.frame_iters // S) * S  # iterations per frame, whole replays
+        steps = -(-args.steps // FI) * FI
         tracker = GraphTracker(params, curr, frame, iters_per_graph=S, timing=bool(args.timing),
                                fuse_pose=bool(args.fuse_pose),
                                warmup_iters=min(3, max(1, args.warmup)))
-        for _ in range(max(1, args.warmup // S)):
-            tracker.run()
+        for _ in range(max(1, -(-args.warmup // FI))):
+            tracker.track_frame(FI)
     else:
         for _ in range(args.warmup):
             step()
@@ -163,11 +167,11 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if tracker is not None:
-        per_bcast = max(1, args.bcast_every // tracker.iters) if args.bcast_every > 0 else 0
-        for r in range(steps // tracker.iters):
-            if world > 1 and per_bcast and r % per_bcast == 0:
+        per_bcast = max(1, args.bcast_every // FI) if args.bcast_every > 0 else 0
+        for f in range(steps // FI):
+            if world > 1 and per_bcast and f % per_bcast == 0:
                 sd.broadcast_map(params)       # map update -> RCCL broadcast over xGMI
-            tracker.run()
+            tracker.track_frame(FI)            # one frame: fresh optimizer, replays, best pose written back
     else:
         for i in range(steps):
             if world > 1 and args.bcast_every > 0 and i % args.bcast_every == 0:
@@ -258,8 +262,10 @@ def main():
             "metric": METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": steps,
             "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "execution": (f"HIP graph of {tracker.iters} tracking iterations, replayed; binning capacity "
-                          f"{tracker.capacity}, no overflow" if tracker is not None else "eager"),
+            "execution": (f"frames of {FI} tracking iterations: HIP graph of {tracker.iters} iterations replayed "
+                          f"{FI // tracker.iters}x per frame between the frame's optimizer reset and best-candidate "
+                          f"write-back; binning capacity {tracker.capacity}, no overflow" if tracker is not None
+                          else "eager"),
             "data": "synthetic (SURVEY.md 8(d) seeded scene; targets rendered at the unperturbed pose)",
             "config": {"workload": f"config {args.config}: {P} isotropic Gaussians, {W}x{H}, SplaTAM tracking "
                                    "iteration (RGB + depth/silhouette render fwd+bwd, masked L1, Adam on pose)",

@@ -1,6 +1,6 @@
 /*
  * gsr.h -- C ABI of the MI355X-native differentiable Gaussian rasterizer
- * (libgsr.so, built from splatam_amd/csrc/*.hip for gfx950).
+ * (libgsr.so, built from the splatam_amd/csrc HIP sources for gfx950).
  *
  * This is the drop-in boundary for the reference's torch extension `_C`
  * (hessian-diff-gaussian-rasterization-w-depth/ext.cpp:15-18).  Every entry
@@ -20,7 +20,10 @@
  *   - all work is enqueued on `stream`; gsr_forward synchronises the stream
  *     once to read num_rendered (rasterizer_impl.cu:282 does the same);
  *   - negative return values are errors; gsr_last_error() gives the message
- *     (thread-local).  No global state: re-entrant across devices/threads.
+ *     (thread-local).  Re-entrant across devices and threads: the only host-side
+ *     state is kept per device of the launch stream (the binning-capacity hint,
+ *     the stage timing) and per (thread, device) (the pinned num_rendered staging
+ *     word and its event).
  */
 #ifndef GSR_H
 #define GSR_H
@@ -32,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 1
+#define GSR_ABI_VERSION 2
 
 /* error codes */
 #define GSR_OK 0
@@ -130,14 +133,18 @@ int gsr_forward_dual(const gsr_settings* settings, const gsr_gaussians* gaussian
 
 /* Static-capacity, synchronisation-free gsr_forward_dual (capturable in a HIP
  * graph).  The binning buffer holds `capacity` instances; nothing waits on the
- * host.  The device counters are copied to `status` (device, 4 x u32:
- * [0] num_rendered, [1] prefiltered violation, [2] longest tile list) when the
- * stream reaches that point.  Outputs are valid iff status[0] <= capacity and
- * status[2] <= 4096 (the per-tile sort; longer lists need gsr_forward_dual);
- * otherwise every kernel after the scan skipped its work (no out-of-bounds
- * writes) and the call must be repeated with a larger capacity or in the
- * synchronous mode.  Returns `capacity`: pass it as num_rendered to
- * gsr_backward_dual (it sizes the buffer layouts). */
+ * host.  The device counters are merged into `status` (device, 4 x u32) when
+ * the stream reaches that point: [0] = max(num_rendered), [1] |= prefiltered
+ * violation, [2] = max(longest tile list), [3] = the longest list the per-tile
+ * sort handles (4096).  The row is sticky: an overflow in any call (e.g. any
+ * replay of a captured graph) stays visible until the caller zeroes the row.
+ * This call's outputs are valid iff its num_rendered <= capacity and its
+ * longest list <= 4096 (longer lists need gsr_forward_dual); otherwise every
+ * kernel after the scan skipped its work (no out-of-bounds writes), the fused
+ * optimizer steps of include/gsr_glue.h skip theirs, and the call must be
+ * repeated with a larger capacity or in the synchronous mode.  Returns
+ * `capacity`: pass it as num_rendered to gsr_backward_dual (it sizes the
+ * buffer layouts). */
 int gsr_forward_dual_static(const gsr_settings* settings, const gsr_gaussians* gaussians,
                             const float* colors2, int capacity, unsigned* status,
                             float* out_color, float* out_color2, float* out_depth, int* radii,
@@ -176,7 +183,9 @@ int gsr_abi_version(void);
  * below is bracketed by hipEvents recorded on the launch stream; read returns
  * accumulated milliseconds, launch counts and work units (P for per-Gaussian
  * stages, num_rendered for per-instance stages) since the last enable.
- * Process-wide (autograd runs backward on its own thread).  gsr_timing_read synchronises on the recorded events. */
+ * Per device: enable / read act on the calling thread's current device and
+ * cover launches on that device from any thread (autograd runs backward on its
+ * own thread).  gsr_timing_read synchronises on the recorded events. */
 #define GSR_STAGE_PREPROCESS 0 /* preprocess + tile-count scan  */
 #define GSR_STAGE_DUPLICATE 1  /* duplicateWithKeys              */
 #define GSR_STAGE_SORT 2       /* radix sort (all passes)        */

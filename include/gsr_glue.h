@@ -71,11 +71,29 @@ int gsr_track_transform_bwd(int P, const float* means_world, const float* unnorm
  * rounded from a float beta2 would be 1.3e-5 off).  adam_state: device, 15 floats [m_q 4, v_q 4, m_t 3, v_t 3, step],
  * zero-initialised by the caller per frame (SplaTAM re-creates the optimizer per
  * frame). */
+/* Optional per-iteration bookkeeping of the fused pose optimizer (may be NULL):
+ *   status / capacity: the static-mode status row of this iteration's forward and its binning
+ *       capacity; when the row shows an overflow ([0] > capacity, [2] > [3], or [1] != 0) the
+ *       Adam step is skipped -- pose and optimizer state stay as they were (the outputs of an
+ *       overflowing forward are invalid);
+ *   loss / best: scripts/splatam.py:726-731 best-candidate selection: after the step, if
+ *       *loss < best[0] then best[0] = *loss, best[1..4] = the updated quaternion and
+ *       best[5..7] = the updated translation (a NaN loss never replaces the candidate).  The
+ *       caller starts a frame with best[0] = 1e20 and writes best[1..7] back after its last
+ *       iteration (:760-763). */
+typedef struct gsr_pose_track {
+    const unsigned* status;
+    unsigned capacity;
+    const float* loss;
+    float* best;
+} gsr_pose_track;
+
 int gsr_track_transform_bwd_adam(int P, const float* means_world, const float* unnorm_rot, int scale_cols,
                                  float* cam_q, float* cam_t, int q_stride, const float* means_cam,
                                  const float* w2c, const float* dL_dmeans_cam, const float* dL_drot,
                                  const float* dL_ddepth_colors, double lr_q, double lr_t, double beta1,
-                                 double beta2, double eps, float* adam_state, float* scratch, void* stream);
+                                 double beta2, double eps, float* adam_state, float* scratch,
+                                 const gsr_pose_track* track, void* stream);
 
 /* im [3,H,W], depth_sil [3,H,W] (depth, silhouette, depth^2), gt_im [3,H,W], gt_depth [1,H,W].
  * loss: 1 float (device).  scratch: gsr_track_scratch_floats(H*W) floats. */
@@ -122,7 +140,9 @@ int gsr_track_forward_dual_static(const gsr_settings* settings, const gsr_gaussi
  * are those of the gsr_forward_dual(_static) call; means_world / unnorm_rot /
  * scale_cols / cam_q / cam_t / w2c those of gsr_track_transform_fwd.  scratch:
  * gsr_track_backward_scratch_floats(P) floats, zero-filled before first use,
- * left zero-filled. */
+ * left zero-filled.  The Adam step is skipped when the forward's own device
+ * counters show an overflow of num_rendered (its capacity); `track` (may be
+ * NULL) adds the best-candidate selection (its status / capacity are not used). */
 int gsr_track_backward_scratch_floats(int P);
 int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
                             const float* colors2, const float* dL_dout_color, const float* dL_dout_color2,
@@ -130,8 +150,8 @@ int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* g
                             const void* image_buffer, const float* means_world, const float* unnorm_rot,
                             int scale_cols, float* cam_q, float* cam_t, int q_stride, const float* w2c, double lr_q,
                             double lr_t, double beta1, double beta2, double eps, float* adam_state,
-                            float* dL_dcam_q, float* dL_dcam_t, float* scratch, gsr_alloc_fn alloc, void* alloc_ctx,
-                            void* stream);
+                            float* dL_dcam_q, float* dL_dcam_t, float* scratch, const gsr_pose_track* track,
+                            gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
 /* ------------------------------------------------------------------ mapping --
  * get_loss(mapping=True, do_ba=False) (scripts/splatam.py:220-353) with the
@@ -182,6 +202,10 @@ typedef struct gsr_map_adam {
     double lr[5];
     int step;
     double beta1, beta2, eps;
+    /* optional: the static-mode status row of this iteration's forward and its binning capacity;
+     * an overflow there (see gsr_pose_track) skips the step -- parameters and state unchanged */
+    const unsigned* status;
+    unsigned capacity;
 } gsr_map_adam;
 
 /* gsr_map_transform_bwd with the optimizer step fused in: the parameters are

@@ -268,10 +268,11 @@ def mark_visible(means3D, viewmatrix, projmatrix):
 
 def track_backward_dual(settings, means3D, radii, colors, colors2, scales, rotations, dL_dout_color, dL_dout_color2,
                         geomBuffer, R, binningBuffer, imageBuffer, means_world, unnorm_rot, scale_cols, cam_q_ptr,
-                        cam_t_ptr, q_stride, w2c, scratch, adam=None, dq_ptr=None, dt_ptr=None):
+                        cam_t_ptr, q_stride, w2c, scratch, adam=None, dq_ptr=None, dt_ptr=None, track=None):
     """gsr_track_backward_dual (include/gsr_glue.h): the tracking backward with the pose chain fused into
     the per-Gaussian backward.  adam = (lr_q, lr_t, beta1, beta2, eps, state tensor) applies the Adam step
-    to the pose in place; otherwise the pose gradient is written at dq_ptr / dt_ptr."""
+    to the pose in place; otherwise the pose gradient is written at dq_ptr / dt_ptr.  track: an optional
+    GsrPoseTrack (best-candidate selection; the Adam step is skipped on an overflowing forward)."""
     device = means3D.device
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     with torch.cuda.device(device):
@@ -293,7 +294,7 @@ def track_backward_dual(settings, means3D, radii, colors, colors2, scales, rotat
             imageBuffer.data_ptr(), means_world.data_ptr(), unnorm_rot.data_ptr(), int(scale_cols),
             cam_q_ptr, cam_t_ptr, int(q_stride), w2c.data_ptr(), float(lr_q), float(lr_t), float(b1), float(b2),
             float(eps), state.data_ptr() if state is not None else None, dq_ptr, dt_ptr, scratch.data_ptr(),
-            _ALLOC_CB, None, _stream(device))
+            ctypes.byref(track) if track is not None else None, _ALLOC_CB, None, _stream(device))
         _check(rc, "track_backward_dual")
         _tls.buffers = {}
 

@@ -37,7 +37,13 @@ class GsrGrads(ctypes.Structure):
 class GsrMapAdam(ctypes.Structure):
     """gsr_map_adam (include/gsr_glue.h)."""
     _fields_ = [("exp_avg", c_void_p * 5), ("exp_avg_sq", c_void_p * 5), ("lr", c_double * 5), ("step", c_int),
-                ("beta1", c_double), ("beta2", c_double), ("eps", c_double)]
+                ("beta1", c_double), ("beta2", c_double), ("eps", c_double), ("status", c_void_p),
+                ("capacity", ctypes.c_uint)]
+
+
+class GsrPoseTrack(ctypes.Structure):
+    """gsr_pose_track (include/gsr_glue.h)."""
+    _fields_ = [("status", c_void_p), ("capacity", ctypes.c_uint), ("loss", c_void_p), ("best", c_void_p)]
 
 
 class GsrAdamTensor(ctypes.Structure):
@@ -80,7 +86,8 @@ SIGNATURES = {
                                         c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "gsr_track_transform_bwd_adam": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                              c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_double,
-                                             c_double, c_double, c_double, c_void_p, c_void_p, c_void_p]),
+                                             c_double, c_double, c_double, c_void_p, c_void_p,
+                                             ctypes.POINTER(GsrPoseTrack), c_void_p]),
     "gsr_track_l1_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
                                  ctypes.c_float, ctypes.c_float, c_void_p, c_void_p, c_void_p]),
     "gsr_track_l1_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
@@ -97,8 +104,8 @@ SIGNATURES = {
     "gsr_track_backward_dual": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_int, c_void_p, c_void_p, c_int, c_void_p, c_double, c_double, c_double,
-                                        c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p, ALLOC_FN,
-                                        c_void_p, c_void_p]),
+                                        c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        ctypes.POINTER(GsrPoseTrack), ALLOC_FN, c_void_p, c_void_p]),
     # include/gsr_glue.h: fused SplaTAM mapping glue and optimizer
     "gsr_map_loss_scratch_floats": (c_int, [c_int, c_int]),
     "gsr_map_loss_state_floats": (c_int, [c_int, c_int]),
@@ -125,7 +132,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.gsr_abi_version() != 1:
+    if lib.gsr_abi_version() != 2:
         raise ImportError("libgsr.so ABI version mismatch")
     return lib
 

@@ -40,7 +40,7 @@ def flags():
 def _compile(src: str) -> str:
     obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
     srcp = os.path.join(CSRC, src)
-    deps = [srcp, os.path.join(ROOT, "include", "gsr.h")] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
+    deps = [srcp, os.path.join(ROOT, "include", "gsr.h"), os.path.join(ROOT, "include", "gsr_glue.h")] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
     cmd = [hipcc(), *flags(), "-c", srcp, "-o", obj]

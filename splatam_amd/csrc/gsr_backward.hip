@@ -536,7 +536,8 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         __syncthreads();
         if (threadIdx.x == 0) {
             const PoseAdam adam{pf.lr_q, pf.lr_t, pf.beta1, pf.beta2, (float)(1.0 - pf.beta1),
-                                (float)(1.0 - pf.beta2), (float)pf.eps, pf.adam_state, pf.cam_q, pf.cam_t};
+                                (float)(1.0 - pf.beta2), (float)pf.eps, pf.adam_state, pf.cam_q, pf.cam_t,
+                                pf.guard, pf.cap, pf.loss, pf.best};
             pose_fin(s_tot, pf.cam_q, pf.qs, pf.dq, pf.dt, adam);
         }
         return;

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/gsr.h"
+#include "../../include/gsr_glue.h"
 #include "gsr_common.h"
 
 using namespace gsr;
@@ -45,8 +46,32 @@ struct Pinned {  // per-thread staging of the device counters + the event after 
         if (ev) (void)hipEventDestroy(ev);
     }
 };
-thread_local Pinned g_pinned;
-std::atomic<double> g_inst_ratio{3.0};  // last num_rendered / P (binning capacity hint)
+// Host-side state is kept per device (the device of the launch stream), so one process (or one
+// thread) may serve several GPUs: the pinned counter staging + its event (per thread and device),
+// the binning-capacity hint (per device) and the stage timing (per device).
+constexpr int kMaxDevices = 64;
+int stream_device(hipStream_t s) {
+    thread_local hipStream_t last_s = nullptr;
+    thread_local int last_d = -1;
+    if (last_d >= 0 && s == last_s && s != nullptr) return last_d;
+    int d = 0;
+    if (hipStreamGetDevice(s, &d) != hipSuccess && hipGetDevice(&d) != hipSuccess) d = 0;
+    (void)hipGetLastError();
+    if (d < 0 || d >= kMaxDevices) d = 0;
+    last_s = s;
+    last_d = d;
+    return d;
+}
+int current_device() {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDevices) d = 0;
+    return d;
+}
+thread_local Pinned g_pinned[kMaxDevices];
+struct RatioHint {
+    std::atomic<double> v{3.0};  // last num_rendered / P (binning capacity hint)
+};
+RatioHint g_inst_ratio[kMaxDevices];
 
 Camera make_camera(const gsr_settings* s) {
     Camera c;
@@ -141,15 +166,12 @@ struct Timing {
         return e;
     }
 };
-// Global (not thread-local): torch runs autograd backward on its own thread.
-Timing g_timing;
+// Per device, not thread-local: torch runs autograd backward on its own thread.
+Timing g_timing[kMaxDevices];
 std::mutex g_timing_mu;
 
-// 4-word counter copies / resets as kernels: plain kernel nodes when captured in a
-// HIP graph (small memcpy / memset nodes misbehaved on re-replay here)
-__global__ void copy4_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src) {
-    if (threadIdx.x < 4) dst[threadIdx.x] = src ? src[threadIdx.x] : 0u;
-}
+// resets as kernels: plain kernel nodes when captured in a HIP graph (small memcpy /
+// memset nodes misbehaved on re-replay here)
 __global__ void zero_words_kernel(uint32_t* __restrict__ p, size_t n) {
     for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) p[k] = 0u;
 }
@@ -188,15 +210,18 @@ struct StageTimer {  // brackets the launches of one stage
     unsigned long long* kc = nullptr;  // in-kernel clock slot (stages whose kernel stamps itself)
     // in_kernel: the stage is one launch that takes kclock() and stamps itself
     // (kclock_begin / kclock_end), so no stamp kernels are added around it
-    StageTimer(int stage, long long units, hipStream_t s_, bool in_kernel = false) : s(s_), on(g_timing.on) {
+    Timing& T;
+    StageTimer(int stage, long long units, hipStream_t s_, bool in_kernel = false)
+        : s(s_), on(false), T(g_timing[stream_device(s_)]) {
+        on = T.on;
         if (!on) return;
-        if (g_timing.clock) {
+        if (T.clock) {
             on = false;
-            if ((g_timing.mask >> stage) & 1u) {
+            if ((T.mask >> stage) & 1u) {
                 if (in_kernel) {
-                    kc = g_timing.dclock + (size_t)KCLOCK_WORDS * stage;
+                    kc = T.dclock + (size_t)KCLOCK_WORDS * stage;
                 } else {
-                    dc = g_timing.dclock + (size_t)KCLOCK_WORDS * stage;
+                    dc = T.dclock + (size_t)KCLOCK_WORDS * stage;
                     hipLaunchKernelGGL(stamp_begin_kernel, dim3(1), dim3(1), 0, s, dc);
                 }
             }
@@ -205,7 +230,7 @@ struct StageTimer {  // brackets the launches of one stage
         rec.stage = stage; rec.units = units;
         {
             std::lock_guard<std::mutex> lk(g_timing_mu);
-            rec.a = g_timing.take(); rec.b = g_timing.take();
+            rec.a = T.take(); rec.b = T.take();
         }
         (void)record_event(rec.a, s);
     }
@@ -215,29 +240,30 @@ struct StageTimer {  // brackets the launches of one stage
         if (!on) return;
         (void)record_event(rec.b, s);
         std::lock_guard<std::mutex> lk(g_timing_mu);
-        g_timing.recs.push_back(rec);
+        T.recs.push_back(rec);
     }
 };
 
 // The speculative launches learn their work units only after the host sync.
-void g_timing_units(int stage, long long units) {
+void g_timing_units(int dev, int stage, long long units) {
     std::lock_guard<std::mutex> lk(g_timing_mu);
-    for (auto it = g_timing.recs.rbegin(); it != g_timing.recs.rend(); ++it)
+    Timing& T = g_timing[dev];
+    for (auto it = T.recs.rbegin(); it != T.recs.rend(); ++it)
         if (it->stage == stage) { it->units = units; break; }
 }
 
-void timing_drain() {  // caller holds g_timing_mu
-    for (auto& r : g_timing.recs) {
+void timing_drain(Timing& T) {  // caller holds g_timing_mu
+    for (auto& r : T.recs) {
         float ms = 0.f;
         if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
-            g_timing.ms[r.stage] += ms;
-            g_timing.launches[r.stage] += 1;
-            g_timing.units[r.stage] += r.units;
+            T.ms[r.stage] += ms;
+            T.launches[r.stage] += 1;
+            T.units[r.stage] += r.units;
         }
-        g_timing.pool.push_back(r.a);
-        g_timing.pool.push_back(r.b);
+        T.pool.push_back(r.a);
+        T.pool.push_back(r.b);
     }
-    g_timing.recs.clear();
+    T.recs.clear();
     (void)hipGetLastError();  // an event that was never recorded must not leave a sticky error for torch
 }
 
@@ -268,6 +294,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     if (colors2 && !out_color2) return fail(GSR_ERR_INVALID_ARG, "out_color2 required with colors2");
     if (colors2 && gaussians->P > 0 && !gaussians->means3D) return fail(GSR_ERR_INVALID_ARG, "means3D is required");
     hipStream_t stream = (hipStream_t)stream_;
+    const int dev = stream_device(stream);
+    Pinned& pin = g_pinned[dev];
     const Camera cam = make_camera(settings);
     GaussIn g = make_gauss(gaussians);
     g.colors2 = colors2;  // packed into the render records by preprocess (dual render)
@@ -304,15 +332,21 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     // scan launch does them, and the counters are final right after it
     const bool scan_in_duplicate = lds_hist && !force_radix;
     auto snapshot_counters = [&]() -> int {  // num_rendered & co. to pinned host memory (eager mode)
-        if (!g_pinned.p) {
-            if ((e = hipHostMalloc((void**)&g_pinned.p, 16, hipHostMallocDefault)) != hipSuccess)
+        if (!pin.p) {
+            if ((e = hipHostMalloc((void**)&pin.p, 16, hipHostMallocDefault)) != hipSuccess)
                 return hip_fail(e, "hipHostMalloc");
         }
-        if (!g_pinned.ev && (e = hipEventCreateWithFlags(&g_pinned.ev, hipEventDisableTiming)) != hipSuccess)
-            return hip_fail(e, "hipEventCreate");
-        if ((e = hipMemcpyAsync(g_pinned.p, geo.counters, 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+        if (!pin.ev) {  // created on the stream's device (the caller's current device is that device)
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            if (cur != dev) (void)hipSetDevice(dev);
+            e = hipEventCreateWithFlags(&pin.ev, hipEventDisableTiming);
+            if (cur != dev) (void)hipSetDevice(cur);
+            if (e != hipSuccess) return hip_fail(e, "hipEventCreate");
+        }
+        if ((e = hipMemcpyAsync(pin.p, geo.counters, 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
             return hip_fail(e, "copy num_rendered");
-        if ((e = hipEventRecord(g_pinned.ev, stream)) != hipSuccess) return hip_fail(e, "record num_rendered");
+        if ((e = hipEventRecord(pin.ev, stream)) != hipSuccess) return hip_fail(e, "record num_rendered");
         return GSR_OK;
     };
     if (P > 0) {
@@ -341,11 +375,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         if ((e = zero_async(ranges, sizeof(uint2) * (size_t)ntiles, stream)) != hipSuccess)
             return hip_fail(e, "memset ranges");
     }
-    if (P == 0) {  // rasterize_points.cu:67-81: zero outputs, forward not run
-        if (capacity > 0) {
-            hipLaunchKernelGGL(copy4_kernel, dim3(1), dim3(64), 0, stream, status, (const uint32_t*)nullptr);
-            if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "status");
-        }
+    if (P == 0) {  // rasterize_points.cu:67-81: zero outputs, forward not run (the sticky status keeps its rows)
         void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, BinLayout::make(0, W, H).total);
         if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
         if ((e = zero_async(out_color, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess ||
@@ -358,7 +388,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     // calls' instances-per-Gaussian ratio, so everything is enqueued before the
     // host waits on num_rendered (the reference blocks right after the scan,
     // rasterizer_impl.cu:282, leaving the GPU idle while it launches the rest).
-    const double ratio = g_inst_ratio.load(std::memory_order_relaxed);
+    const double ratio = g_inst_ratio[dev].v.load(std::memory_order_relaxed);
     const uint32_t cap = capacity > 0 ? (uint32_t)capacity
                                       : (uint32_t)std::min(2.0e9, std::max(1024.0, 1.5 * ratio * P));
     auto bin_ptrs = [&](void* bin, const BinLayout& BL, uint64_t** keys, uint32_t** vals, uint32_t*& gid,
@@ -403,17 +433,17 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     if (capacity > 0) {  // static mode: report, never wait (an overflow shows in status, outputs invalid)
         return (int)cap;
     }
-    if ((e = hipEventSynchronize(g_pinned.ev)) != hipSuccess) return hip_fail(e, "sync num_rendered");
-    const uint32_t I = g_pinned.p[0];
-    const uint32_t longest = g_pinned.p[2];
-    if (g_pinned.p[1] != 0)
+    if ((e = hipEventSynchronize(pin.ev)) != hipSuccess) return hip_fail(e, "sync num_rendered");
+    const uint32_t I = pin.p[0];
+    const uint32_t longest = pin.p[2];
+    if (pin.p[1] != 0)
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     if (I > 0x7fffffffu) return fail(GSR_ERR_INVALID_ARG, "num_rendered overflows int32");
-    g_inst_ratio.store(P > 0 ? std::max(0.05, (double)I / P) : 1.0, std::memory_order_relaxed);
+    g_inst_ratio[dev].v.store(P > 0 ? std::max(0.05, (double)I / P) : 1.0, std::memory_order_relaxed);
     const bool spec_ok = speculated && I <= cap && longest <= (uint32_t)TILE_SORT_CAP;
     if (spec_ok) {
-        g_timing_units(GSR_STAGE_SORT, I);
-        g_timing_units(GSR_STAGE_RENDER_FWD, I);
+        g_timing_units(dev, GSR_STAGE_SORT, I);
+        g_timing_units(dev, GSR_STAGE_RENDER_FWD, I);
         return (int)I;
     }
     // exact re-launch (capacity overflow, a tile longer than the LDS sort, or forced radix)
@@ -568,7 +598,13 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
             oc.dcolors = drgb;
             oc.dsh = nullptr;
         }
-        if ((e = launch_gauss_bwd(cam, gc, geo, radii, inst, rec, oc, guard, stream, pose)) != hipSuccess)
+        PoseFuse pc;
+        if (pose) {
+            pc = *pose;
+            pc.guard = geo.counters;
+        }
+        if ((e = launch_gauss_bwd(cam, gc, geo, radii, inst, rec, oc, guard, stream, pose ? &pc : nullptr)) !=
+            hipSuccess)
             return hip_fail(e, "gaussian backward");
         if (shs_staged && (e = launch_sh_bwd(cam, g, geo, radii, drgb, out.dmeans3D, out.dsh, guard, stream)) !=
                               hipSuccess)
@@ -605,8 +641,8 @@ int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* g
                             const void* image_buffer, const float* means_world, const float* unnorm_rot,
                             int scale_cols, float* cam_q, float* cam_t, int q_stride, const float* w2c, double lr_q,
                             double lr_t, double beta1, double beta2, double eps, float* adam_state,
-                            float* dL_dcam_q, float* dL_dcam_t, float* scratch, gsr_alloc_fn alloc, void* alloc_ctx,
-                            void* stream) {
+                            float* dL_dcam_q, float* dL_dcam_t, float* scratch, const gsr_pose_track* track,
+                            gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
     if (!gaussians || (scale_cols != 1 && scale_cols != 3) || q_stride < 1)
         return fail(GSR_ERR_INVALID_ARG, "track_backward_dual: bad sizes");
     if (!colors2 || !means_world || !unnorm_rot || !cam_q || !cam_t || !w2c || !scratch ||
@@ -616,6 +652,11 @@ int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* g
         return fail(GSR_ERR_INVALID_ARG, "track_backward_dual: anisotropic maps need the rendered rotations");
     PoseFuse pf{means_world, unnorm_rot, scale_cols, cam_q, cam_t, q_stride, w2c, scratch, adam_state,
                 lr_q, lr_t, beta1, beta2, eps, dL_dcam_q, dL_dcam_t};
+    pf.cap = (uint32_t)num_rendered;  // pf.guard = the forward's counters (backward_impl)
+    if (track) {
+        pf.loss = track->loss;
+        pf.best = track->best;
+    }
     gsr_grads none{};
     return backward_impl(settings, gaussians, radii, dL_dout_color, colors2, dL_dout_color2, num_rendered,
                          geom_buffer, binning_buffer, image_buffer, 1, &none, nullptr, 1, alloc, alloc_ctx, stream,
@@ -635,43 +676,43 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_timing_mu);
-    timing_drain();
-    g_timing.on = on != 0;
-    g_timing.clock = on >= GSR_TIMING_CLOCK;
-    g_timing.mask = (unsigned)on & 0xFFu;
-    for (int i = 0; i < GSR_NUM_STAGES; i++) { g_timing.ms[i] = 0.0; g_timing.launches[i] = 0; g_timing.units[i] = 0; }
-    if (g_timing.clock) {
+    Timing& T = g_timing[current_device()];
+    timing_drain(T);
+    T.on = on != 0;
+    T.clock = on >= GSR_TIMING_CLOCK;
+    T.mask = (unsigned)on & 0xFFu;
+    for (int i = 0; i < GSR_NUM_STAGES; i++) { T.ms[i] = 0.0; T.launches[i] = 0; T.units[i] = 0; }
+    if (T.clock) {
         hipError_t e;
-        if (!g_timing.dclock &&
-            (e = hipMalloc((void**)&g_timing.dclock, kclock_bytes())) != hipSuccess)
+        if (!T.dclock && (e = hipMalloc((void**)&T.dclock, kclock_bytes())) != hipSuccess)
             return hip_fail(e, "timing clock buffer");
-        if ((e = hipMemset(g_timing.dclock, 0, kclock_bytes())) != hipSuccess)
-            return hip_fail(e, "timing clock reset");
+        if ((e = hipMemset(T.dclock, 0, kclock_bytes())) != hipSuccess) return hip_fail(e, "timing clock reset");
     }
     return GSR_OK;
 }
 
 int gsr_timing_read(double* ms, long long* launches, long long* units, int n) {
     std::lock_guard<std::mutex> lk(g_timing_mu);
-    timing_drain();
-    if (g_timing.clock && g_timing.dclock) {
+    Timing& T = g_timing[current_device()];
+    timing_drain(T);
+    if (T.clock && T.dclock) {
         std::vector<unsigned long long> h((size_t)KCLOCK_WORDS * GSR_NUM_STAGES);
         int dev = 0, khz = 0;
         hipError_t e;
-        if ((e = hipMemcpy(h.data(), g_timing.dclock, kclock_bytes(), hipMemcpyDeviceToHost)) != hipSuccess)
+        if ((e = hipMemcpy(h.data(), T.dclock, kclock_bytes(), hipMemcpyDeviceToHost)) != hipSuccess)
             return hip_fail(e, "timing clock read");
         if ((e = hipGetDevice(&dev)) != hipSuccess ||
             (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev)) != hipSuccess || khz <= 0)
             return fail(GSR_ERR_HIP, "wall clock rate unavailable");
         for (int i = 0; i < GSR_NUM_STAGES; i++) {
-            g_timing.ms[i] = (double)h[(size_t)KCLOCK_WORDS * i + 1] / (double)khz;
-            g_timing.launches[i] = (long long)h[(size_t)KCLOCK_WORDS * i + 2];
+            T.ms[i] = (double)h[(size_t)KCLOCK_WORDS * i + 1] / (double)khz;
+            T.launches[i] = (long long)h[(size_t)KCLOCK_WORDS * i + 2];
         }
     }
     for (int i = 0; i < n && i < GSR_NUM_STAGES; i++) {
-        if (ms) ms[i] = g_timing.ms[i];
-        if (launches) launches[i] = g_timing.launches[i];
-        if (units) units[i] = g_timing.units[i];
+        if (ms) ms[i] = T.ms[i];
+        if (launches) launches[i] = T.launches[i];
+        if (units) units[i] = T.units[i];
     }
     return GSR_NUM_STAGES;
 }

@@ -926,6 +926,17 @@ struct BwdGuard {
         return counters[0] > cap_inst || counters[2] > counters[3];
     }
 };
+// Static-mode status rows are sticky across calls (HIP-graph replays): [0] and [2] keep the
+// maximum num_rendered / longest tile list seen, [1] ORs the prefiltered violations, [3] the
+// longest list the tile sort handles.  An overflow in any replay therefore stays visible until
+// the caller zeroes the row.
+__device__ __forceinline__ void status_merge(uint32_t* st, uint32_t n, uint32_t viol, uint32_t longest,
+                                             uint32_t sort_cap) {
+    if (n) atomicMax(st + 0, n);
+    if (viol) atomicOr(st + 1, viol);
+    if (longest) atomicMax(st + 2, longest);
+    if (sort_cap) atomicMax(st + 3, sort_cap);
+}
 // lds_hist: the colscan ran without its scan tail; every workgroup scans the
 // workgroup and tile totals (`tot`) itself, workgroup 0 writes ranges,
 // counters and `status` (static mode; may be null).
@@ -1002,6 +1013,10 @@ struct PoseFuse {
     double lr_q, lr_t, beta1, beta2, eps;
     float* dq;                 // gradient outputs when adam_state == nullptr
     float* dt;
+    const uint32_t* guard = nullptr;  // the forward's counters + capacity (Adam skipped on an overflow)
+    uint32_t cap = 0;
+    const float* loss = nullptr;      // best-candidate selection (PoseAdam::loss / best)
+    float* best = nullptr;
 };
 int pose_fuse_scratch_floats(int P);
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* inst,

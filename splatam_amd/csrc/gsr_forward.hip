@@ -336,11 +336,11 @@ __device__ void scan_counts_body(const uint32_t* __restrict__ wgsum, uint32_t* _
             if (pass == 0) {
                 counters[0] = s_carry;
                 counters[1] = s_viol;
-                if (status) { status[0] = s_carry; status[1] = s_viol; }
+                if (status) status_merge(status, s_carry, s_viol, 0u, 0u);
             } else {
                 counters[2] = s_max;
                 counters[3] = sort_cap;  // longest list the tile sort will handle (BwdGuard)
-                if (status) { status[2] = s_max; status[3] = sort_cap; }
+                if (status) status_merge(status, 0u, 0u, s_max, sort_cap);
             }
         }
         __syncthreads();
@@ -538,12 +538,7 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
                 geo.counters[1] = viol;
                 geo.counters[2] = vmax;
                 geo.counters[3] = sort_cap;
-                if (status) {
-                    status[0] = all;
-                    status[1] = viol;
-                    status[2] = vmax;
-                    status[3] = sort_cap;
-                }
+                if (status) status_merge(status, all, viol, vmax, sort_cap);
             }
         }
         base = pre;

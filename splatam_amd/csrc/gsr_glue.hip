@@ -216,7 +216,7 @@ int gsr_track_transform_bwd_adam(int P, const float* means_world, const float* u
                                  float* cam_q, float* cam_t, int q_stride, const float* means_cam, const float* w2c,
                                  const float* dL_dmeans_cam, const float* dL_drot, const float* dL_ddepth_colors,
                                  double lr_q, double lr_t, double beta1, double beta2, double eps, float* adam_state,
-                                 float* scratch, void* stream) {
+                                 float* scratch, const gsr_pose_track* track, void* stream) {
     if (P < 0 || (scale_cols != 1 && scale_cols != 3) || q_stride < 1)
         return fail(GSR_ERR_INVALID_ARG, "track_transform_bwd_adam: bad sizes");
     if (!cam_q || !cam_t || !adam_state || !scratch || !w2c ||
@@ -226,7 +226,9 @@ int gsr_track_transform_bwd_adam(int P, const float* means_world, const float* u
                        means_world, unnorm_rot, scale_cols, cam_q, q_stride, means_cam, w2c, dL_dmeans_cam, dL_drot,
                        dL_ddepth_colors, scratch, nullptr, nullptr,
                        PoseAdam{lr_q, lr_t, beta1, beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
-                                adam_state, cam_q, cam_t});
+                                adam_state, cam_q, cam_t, track ? track->status : nullptr,
+                                track ? track->capacity : 0u, track ? track->loss : nullptr,
+                                track ? track->best : nullptr});
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GSR_OK : hip_fail(e, "track_transform_bwd_adam");
 }

@@ -64,12 +64,24 @@ __device__ __forceinline__ float4 normalize4_bwd(float4 y, float norm, float4 dy
 
 __device__ __forceinline__ float4 load4(const float* p) { return make_float4(p[0], p[1], p[2], p[3]); }
 
+// Forward-state check of the fused optimizer steps: `st` is a forward's device counters or
+// its static-mode status row ([0] num_rendered, [1] prefiltered violation, [2] longest tile
+// list, [3] longest list the tile sort handled); the forward's outputs (and so the gradients)
+// are invalid when it overflowed its binning capacity `cap`.  st == nullptr: no check.
+__device__ __forceinline__ bool forward_overflowed(const uint32_t* st, uint32_t cap) {
+    return st && (st[0] > cap || st[2] > st[3] || st[1] != 0u);
+}
+
 struct PoseAdam {  // torch.optim.Adam (no weight decay, no amsgrad) on the frame's pose column
     double lr_q, lr_t, beta1, beta2;   // torch's hyperparameters are python floats (double)
     float w1, omb2, eps;               // 1 - beta1, 1 - beta2 rounded from double, like torch's scalars
     float* state;     // device: m_q[4], v_q[4], m_t[3], v_t[3], step
     float* q;         // the frame's quaternion column (stride qs), updated in place
     float* t;         // the frame's translation column (stride qs)
+    const uint32_t* guard = nullptr;  // forward counters / status row: skip the step on an overflow
+    uint32_t cap = 0;
+    const float* loss = nullptr;      // this iteration's loss (best-candidate selection), or nullptr
+    float* best = nullptr;            // [min loss, q 4, t 3]
 };
 
 // torch/optim/adam.py (foreach form): exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
@@ -103,6 +115,7 @@ __device__ void pose_fin(const float* S, const float* cq, int qs, float* dq, flo
     dc.x += S[12]; dc.y += S[13]; dc.z += S[14]; dc.w += S[15];
     const float4 g = normalize4_bwd(make_float4(ps.c[0], ps.c[1], ps.c[2], ps.c[3]), ps.qn, dc);
     if (adam.state) {  // optimizer step fused here: the pose gradient never leaves the kernel
+        if (forward_overflowed(adam.guard, adam.cap)) return;  // invalid gradients: pose and state unchanged
         float* st = adam.state;
         const float step = st[14] + 1.f;
         st[14] = step;
@@ -112,6 +125,16 @@ __device__ void pose_fin(const float* S, const float* cq, int qs, float* dq, flo
         const float gq[4] = {g.x, g.y, g.z, g.w};
         for (int k = 0; k < 4; k++) adam_update(adam.q[k * qs], gq[k], st[k], st[4 + k], ss_q, adam, bc2_sqrt);
         for (int k = 0; k < 3; k++) adam_update(adam.t[k * qs], S[k], st[8 + k], st[11 + k], ss_t, adam, bc2_sqrt);
+        // scripts/splatam.py:726-731: keep the pose after this step if this iteration's loss is the
+        // lowest so far (a NaN loss never is, like `loss < current_min_loss`)
+        if (adam.loss && adam.best) {
+            const float L = *adam.loss;
+            if (L < adam.best[0]) {
+                adam.best[0] = L;
+                for (int k = 0; k < 4; k++) adam.best[1 + k] = adam.q[k * qs];
+                for (int k = 0; k < 3; k++) adam.best[5 + k] = adam.t[k * qs];
+            }
+        }
         return;
     }
     dq[0] = g.x; dq[qs] = g.y; dq[2 * qs] = g.z; dq[3 * qs] = g.w;

@@ -330,6 +330,8 @@ struct MapAdam {  // the mapping optimizer's state, applied in place (NULL p: wr
     float* v[5];
     float step_size[5];
     float w1, beta2, omb2, bc2_sqrt, eps;
+    const uint32_t* guard;  // status row of the iteration's forward: skip the step on an overflow
+    uint32_t cap;
 };
 
 __device__ __forceinline__ float adam_apply(float* p, float g, float* m, float* v, float ss, const MapAdam& a) {
@@ -377,15 +379,17 @@ __device__ __forceinline__ void adam_apply_n(float* p, const float* g, float* m,
 // [z, 1, z^2] with z = w2c[2,:3] . m + w2c[2,3].  Colours pass through
 // unchanged (their gradient is only stepped when `adam` is set).
 __global__ void __launch_bounds__(GLUE_BLOCK)
-map_transform_bwd_kernel(int P, const float* __restrict__ ur, const float* __restrict__ lo,
-                         const float* __restrict__ ls, int scols, const float* __restrict__ cq, int qs,
+map_transform_bwd_kernel(int P, const float* ur, const float* lo, const float* ls, int scols, const float* __restrict__ cq, int qs,
                          const float* __restrict__ mc, const float* __restrict__ w2c, const float* __restrict__ gm,
                          const float* __restrict__ gr, const float* __restrict__ gd, const float* __restrict__ go,
                          const float* __restrict__ gs, float* __restrict__ dmeans, float* __restrict__ dur,
                          float* __restrict__ dlo, float* __restrict__ dls, const float* __restrict__ gcol, int ccols,
                          MapAdam adam) {
+    // ur / lo / ls alias adam.p[1..3] in the Adam variant (updated in place): no __restrict__,
+    // and every lane reads its own elements before it stores them
     const int i = blockIdx.x * GLUE_BLOCK + threadIdx.x;
     const bool step = adam.p[0] != nullptr;
+    if (step && forward_overflowed(adam.guard, adam.cap)) return;  // invalid gradients: nothing changes
     if (step && gcol && i < P) {  // colour parameters: element k * P + i (coalesced across the wave)
         constexpr int CU = 4;  // colour columns per round trip
         int k = 0;
@@ -567,6 +571,8 @@ int gsr_map_transform_bwd_adam(int P, float* means_world, float* unnorm_rot, flo
         a.step_size[k] = (float)(-adam->lr[k] / bc1);
     }
     fill_adam_common(adam->beta1, adam->beta2, adam->eps, adam->step, a.w1, a.beta2, a.omb2, a.bc2_sqrt, a.eps);
+    a.guard = adam->status;
+    a.cap = adam->capacity;
     hipLaunchKernelGGL(map_transform_bwd_kernel, dim3((P + GLUE_BLOCK - 1) / GLUE_BLOCK), dim3(GLUE_BLOCK), 0,
                        (hipStream_t)stream, P, unnorm_rot, logit_opac, log_scales, scale_cols, cam_q, q_stride,
                        means_cam, w2c, dL_dmeans_cam, dL_drot, dL_ddepth_colors, dL_dopac, dL_dscales, nullptr,

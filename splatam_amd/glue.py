@@ -31,6 +31,10 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+def _byref(s):
+    return ctypes.byref(s) if s is not None else None
+
+
 def _f32c(t: torch.Tensor, name: str) -> torch.Tensor:
     if t.device.type != "cuda":
         raise RuntimeError(f"{name}: the fused glue runs on ROCm devices only (no CPU fallback)")
@@ -41,14 +45,37 @@ def _f32c(t: torch.Tensor, name: str) -> torch.Tensor:
 
 class PoseAdam:
     """torch.optim.Adam (no weight decay / amsgrad) state for one frame's pose,
-    stepped inside the transform backward (gsr_track_transform_bwd_adam)."""
+    stepped inside the transform backward (gsr_track_transform_bwd_adam).
 
-    def __init__(self, device, lr_q=0.0004, lr_t=0.002, betas=(0.9, 0.999), eps=1e-8):
+    Optional per-iteration bookkeeping (gsr_pose_track): `status` / `capacity` -- the
+    static-mode status row of the iteration's forward (an overflow there skips the step);
+    `best` (device [8]: min loss, quaternion, translation) with the iteration's `loss` --
+    scripts/splatam.py:726-731's best-candidate selection, done on the device."""
+
+    def __init__(self, device, lr_q=0.0004, lr_t=0.002, betas=(0.9, 0.999), eps=1e-8, track_best=False):
         self.lr_q, self.lr_t, self.betas, self.eps = float(lr_q), float(lr_t), betas, float(eps)
         self.state = torch.zeros(15, dtype=torch.float32, device=device)
+        self.best = torch.full((8,), 1e20, dtype=torch.float32, device=device) if track_best else None
+        self.loss = None      # the current iteration's loss tensor (set before backward)
+        self.status = None    # the current iteration's status row
+        self.capacity = 0
 
     def reset(self):
+        """A fresh optimizer (SplaTAM re-creates it per frame) and candidate (current_min_loss = 1e20)."""
         self.state.zero_()
+        if self.best is not None:
+            self.best.fill_(1e20)
+
+    def track(self, loss_ptr=None):
+        """The gsr_pose_track of the current iteration, or None."""
+        from ._lib import GsrPoseTrack
+        if loss_ptr is None and self.loss is not None:
+            loss_ptr = self.loss.data_ptr()
+        if self.best is None and self.status is None:
+            return None
+        return GsrPoseTrack(status=self.status.data_ptr() if self.status is not None else None,
+                            capacity=int(self.capacity), loss=loss_ptr if self.best is not None else None,
+                            best=self.best.data_ptr() if self.best is not None else None)
 
 
 _SCRATCH: dict = {}
@@ -126,7 +153,7 @@ class _TrackTransform(torch.autograd.Function):
                 cam_trans.data_ptr() + 4 * t, T, means_cam.data_ptr(), w2c.data_ptr(), g_means.data_ptr(),
                 g_rot.data_ptr() if g_rot is not None else None, g_dcol.data_ptr() if g_dcol is not None else None,
                 opt.lr_q, opt.lr_t, float(opt.betas[0]), float(opt.betas[1]), opt.eps, opt.state.data_ptr(),
-                scratch.data_ptr(), _stream(means_world))
+                scratch.data_ptr(), _byref(opt.track()), _stream(means_world))
             _check(rc, "track_transform_bwd_adam")
             return none
         dq = torch.zeros_like(cam_rots)
@@ -221,6 +248,8 @@ class MapAdam:
         self.lr = [float(lrs[k]) for k in self.keys]
         self.betas, self.eps = (float(betas[0]), float(betas[1])), float(eps)
         self.step = 0
+        self.status = None  # the current iteration's static-mode status row: an overflow skips the step
+        self.capacity = 0
 
     def reset(self):
         for t in self.exp_avg + self.exp_avg_sq:
@@ -235,6 +264,8 @@ class MapAdam:
             s.exp_avg_sq[k] = self.exp_avg_sq[k].data_ptr()
             s.lr[k] = self.lr[k]
         s.step, s.beta1, s.beta2, s.eps = self.step, self.betas[0], self.betas[1], self.eps
+        s.status = self.status.data_ptr() if self.status is not None else None
+        s.capacity = int(self.capacity)
         return s
 
 
@@ -445,6 +476,7 @@ class _TrackIteration(torch.autograd.Function):
                                   img, im, ds, gt_im, gt_d, w2c)
             ctx.meta = (t, T, scols, int(n), cam, cfg)
             ctx.pose_adam = pose_adam
+            ctx.loss_ptr = loss.data_ptr()  # best-candidate selection reads this iteration's loss
             ctx.mark_non_differentiable(radii)
             ctx.set_materialize_grads(False)
             return loss, radii
@@ -471,6 +503,7 @@ class _TrackIteration(torch.autograd.Function):
                               im, ds, gt_im, gt_d, w2c)
         ctx.meta = (t, T, scols, int(n), cam, cfg)
         ctx.pose_adam = pose_adam
+        ctx.loss_ptr = loss.data_ptr()
         ctx.mark_non_differentiable(radii)
         ctx.set_materialize_grads(False)
         return loss, radii
@@ -502,7 +535,7 @@ class _TrackIteration(torch.autograd.Function):
             _C.track_backward_dual(cam, means, radii, rgb, dcol, scales, rot_in, dim, dds, geom, n, binning, img, mw,
                                    ur, scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c,
                                    scratch, adam=(opt.lr_q, opt.lr_t, float(opt.betas[0]), float(opt.betas[1]),
-                                                  opt.eps, opt.state))
+                                                  opt.eps, opt.state), track=opt.track(ctx.loss_ptr))
             return nones
         dq, dt = torch.zeros_like(cam_rots), torch.zeros_like(cam_trans)
         _C.track_backward_dual(cam, means, radii, rgb, dcol, scales, rot_in, dim, dds, geom, n, binning, img, mw, ur,

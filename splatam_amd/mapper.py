@@ -10,9 +10,13 @@ GraphMapper captures one frame's mapping -- the optimizer-state reset plus all
 `iters_per_graph` iterations -- into a torch.cuda.CUDAGraph: the Adam step runs
 inside the transform backward (gsr_map_transform_bwd_adam, step numbers 1..N
 baked into the captured launches), the rasterization uses the static-capacity
-dual forward, and the keyframe sequence is drawn once at construction with a
-seeded np.random.RandomState (the same distribution as the reference's draw).
-Each replay is one frame's mapping.  Densification / pruning (which change P)
+dual forward, and the keyframe sequence is drawn once at construction from
+numpy's global random stream (np.random.randint, the reference's own draw) or,
+with `seed`, from a seeded np.random.RandomState; a replay repeats it, so build
+one mapper per frame for fresh draws.
+Each replay is one frame's mapping.  An iteration whose forward overflows the
+binning capacity skips its Adam step on the device (its status row, sticky
+across replays, reports it).  Densification / pruning (which change P)
 are outside the graph, as they are outside the reference's inner loop body.
 """
 from __future__ import annotations
@@ -48,7 +52,7 @@ def probe_num_rendered(params, curr_data, time_idx) -> tuple[int, int]:
 
 class GraphMapper:
     def __init__(self, params: dict, keyframes: list, iters_per_graph: int = 60, cfg: MappingConfig = MappingConfig(),
-                 headroom: float = 1.5, min_extra: int = 65536, seed: int = 0, timing: bool = False):
+                 headroom: float = 1.5, min_extra: int = 65536, seed: int | None = None, timing: bool = False):
         if not keyframes:
             raise RuntimeError("GraphMapper needs at least one keyframe")
         for kf in keyframes:
@@ -67,9 +71,11 @@ class GraphMapper:
             raise RuntimeError(f"a tile list of {longest} > {TILE_SORT_CAP}: use the eager (synchronous) path")
         self.capacity = max(1, int(headroom * max(p[0] for p in probes)) + int(min_extra))
         self.iters = int(iters_per_graph)
-        self.sequence = np.random.RandomState(seed).randint(0, len(keyframes), size=self.iters).tolist()
+        rng = np.random if seed is None else np.random.RandomState(seed)
+        self.sequence = [int(rng.randint(0, len(keyframes))) for _ in range(self.iters)]  # splatam.py:851
         self.status = torch.zeros(self.iters, 4, dtype=torch.int32, device=dev)
         self.adam = MapAdam(params, cfg.lrs, color_key=key)
+        self.adam.capacity = self.capacity
         self.seed = torch.ones((), dtype=torch.float32, device=dev)           # static loss-gradient seed
         self.means2D = torch.zeros(params["means3D"].shape[0], 3, device=dev)  # no grad (no densification stats)
         side = torch.cuda.Stream(device=dev)
@@ -81,6 +87,7 @@ class GraphMapper:
             with torch.no_grad():
                 for k, v in snapshot.items():
                     params[k].copy_(v)
+            self.status.zero_()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         del snapshot
@@ -96,6 +103,7 @@ class GraphMapper:
 
     def _iteration(self, k: int):
         kf = self.keyframes[self.sequence[k]]
+        self.adam.status = self.status[k]  # this iteration's forward guards its Adam step
         loss, _, _ = _get_loss_mapping_fused(self.params, kf, kf["id"], self.cfg, adam=self.adam,
                                              capacity=self.capacity, status=self.status[k], means2D=self.means2D)
         torch.autograd.backward(loss, self.seed)
@@ -105,7 +113,11 @@ class GraphMapper:
         """Enqueue one frame's mapping (one graph launch, no host sync)."""
         self.graph.replay()
 
+    def reset_status(self):
+        self.status.zero_()
+
     def overflowed(self) -> bool:
+        """True if any iteration since the last reset_status() exceeded the binning capacity (one host sync)."""
         st = self.status.cpu()
         return bool((st[:, 0] > self.capacity).any() or (st[:, 2] > TILE_SORT_CAP).any() or (st[:, 1] != 0).any())
 

@@ -72,14 +72,19 @@ class _RasterizeGaussians(torch.autograd.Function):
 
 
 def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations,
-                             cov3Ds_precomp, raster_settings, capacity=0, status=None, grad2_channels=3):
+                             cov3Ds_precomp, raster_settings, capacity=0, status=None, grad2_channels=3,
+                             means2D_grad_sum=False):
     """Two GaussianRasterizer calls on identical geometry fused into one
     rasterization: SplaTAM renders RGB and the [z, 1, z^2]
     depth/silhouette image from the same means / scales / rotations / opacities
     and camera (scripts/splatam.py:255,259).  Returns (color, color2, radii,
     depth); each image is bitwise what a separate call returns, and the gradients
     of the shared inputs are the sums over both images, as autograd would
-    accumulate them over two calls (means2D receives that sum as well).
+    accumulate them over two calls.  means2D: the reference's densification statistics read the
+    gradient of the RGB render's own means2D (scripts/splatam.py:256), which one rasterization of
+    both images does not separate, so means2D receives no gradient unless means2D_grad_sum=True
+    asks for the sum over both images; callers that need the RGB-only statistic render the two
+    images with two GaussianRasterizer calls.
     capacity > 0: synchronisation-free static mode (gsr_forward_dual_static),
     for HIP-graph capture; check `status` (device int32[4]) afterwards.
     grad2_channels=1: the caller's loss reads only channel 0 of color2 (SplaTAM
@@ -91,13 +96,13 @@ def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opac
                                          empty if scales is None else scales,
                                          empty if rotations is None else rotations,
                                          empty if cov3Ds_precomp is None else cov3Ds_precomp, raster_settings,
-                                         capacity, status, grad2_channels)
+                                         capacity, status, grad2_channels, bool(means2D_grad_sum))
 
 
 class _RasterizeGaussiansDual(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings, capacity, status, grad2_channels):
+                raster_settings, capacity, status, grad2_channels, means2D_grad_sum):
         s = raster_settings
         num_rendered, color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth = _C.rasterize_gaussians_dual(
             s.bg, means3D, colors_precomp, colors2, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
@@ -106,6 +111,7 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
         ctx.grad2_channels = grad2_channels
+        ctx.means2D_grad_sum = means2D_grad_sum
         ctx.save_for_backward(colors_precomp, colors2, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
                               geomBuffer, binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii, depth)
@@ -122,7 +128,7 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
         if grad_color2 is None:
             grad_color2 = torch.zeros(3, s.image_height, s.image_width, device=means3D.device)
         n = ctx.needs_input_grad  # (means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations, cov3D)
-        needs = (n[1], n[3], n[4], n[5], n[0], n[8], n[2], n[6], n[7])
+        needs = (n[1] and ctx.means2D_grad_sum, n[3], n[4], n[5], n[0], n[8], n[2], n[6], n[7])
         (g_m2, g_col, g_col2, g_op, g_m3, g_cov, g_sh, g_sc, g_rot) = _C.rasterize_gaussians_dual_backward(
             s.bg, means3D, radii, colors_precomp, colors2, scales, rotations, s.scale_modifier, cov3Ds_precomp,
             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_color, grad_color2, sh, s.sh_degree, s.campos,
@@ -130,7 +136,7 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
             dl2_channels=ctx.grad2_channels if grad_color2 is not None else 3)
         if not n[0]:
             g_m3 = None
-        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None, None, None, None
+        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None, None, None, None, None
 
 
 class GaussianRasterizer(nn.Module):

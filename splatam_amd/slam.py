@@ -260,6 +260,10 @@ class MappingConfig:
     lrs: dict = field(default_factory=lambda: dict(means3D=0.0001, rgb_colors=0.0025, shs=0.0025,
                                                    unnorm_rotations=0.001, logit_opacities=0.05, log_scales=0.001,
                                                    cam_unnorm_rots=0.0, cam_trans=0.0))
+    # configs/replica/splatam.py:112 (True in the gaussian_splatting / post_splatam_opt configs): the
+    # densification statistics read means2D.grad of the RGB render alone (splatam.py:256,
+    # slam_external.py:100-104), which one dual rasterization does not provide
+    use_gaussian_splatting_densification: bool = False
 
 
 def _gaussian(window_size, sigma):
@@ -309,8 +313,11 @@ def _rendervar_colors(params, rv):
 
 def fused_mapping_eligible(params, curr_data, cfg: MappingConfig) -> bool:
     """The fused HIP glue covers SplaTAM's mapping configuration: Gaussians optimised, camera
-    fixed (do_ba=False), L1 + SSIM image loss, no silhouette mask, no outlier-depth rejection."""
+    fixed (do_ba=False), L1 + SSIM image loss, no silhouette mask, no outlier-depth rejection, and
+    no Gaussian-splatting densification (it needs the RGB render's own means2D gradient; the two
+    renders then run as two rasterizer calls, the literal path)."""
     return (cfg.use_l1 and not cfg.use_sil_for_loss and not cfg.ignore_outlier_depth_loss
+            and not cfg.use_gaussian_splatting_densification
             and params["means3D"].is_cuda and not params["cam_unnorm_rots"].requires_grad
             and not params["cam_trans"].requires_grad
             and curr_data["im"].dim() == 3 and curr_data["depth"].dim() == 3)

@@ -13,10 +13,20 @@ backward (gsr_track_transform_bwd_adam), so an iteration is the loss forward
 and backward only.  Capture requires a forward that never waits on the host: the dual forward runs
 in its static mode (gsr_forward_dual_static) with a binning capacity taken
 from an eager probe of the same frame times `headroom`.  Every captured
-iteration copies its binning counters into its own row of `status`;
-`overflowed()` reads them (one host sync) and reports whether any iteration
-exceeded the capacity (its outputs would then be invalid -- rebuild the
-tracker with more headroom and re-run the frame).
+iteration merges its binning counters into its own row of `status` (sticky
+across replays, include/gsr.h); `overflowed()` reads them (one host sync) and
+reports whether any iteration since the last `reset_status()` exceeded the
+capacity.  An overflowing iteration leaves the pose and the optimizer state
+untouched (its Adam step is skipped on the device), so the frame can be re-run
+from `begin_frame()` after rebuilding the tracker with more headroom.
+
+A frame (scripts/splatam.py:700-763) is `begin_frame()` (fresh optimizer,
+best candidate = the current pose with loss 1e20), `num_iters / iters_per_graph`
+replays, and `end_frame()`, which writes the best candidate pose back -- the
+pose after the step of the lowest-loss iteration (:726-731, :760-763), tracked
+on the device inside the captured backward.  `track_frame(num_iters)` does all
+three.  The warm-up iterations run at construction are undone (pose restored,
+optimizer reset).
 """
 from __future__ import annotations
 
@@ -67,15 +77,23 @@ class GraphTracker:
         # Adam on the pose fused into the transform backward (gsr_track_transform_bwd_adam): the
         # iteration is loss forward + backward only -- no .grad, zero_grad or optimizer kernels
         from .glue import PoseAdam
-        self.adam = PoseAdam(dev, lr_q=lrs[0], lr_t=lrs[1])
+        self.adam = PoseAdam(dev, lr_q=lrs[0], lr_t=lrs[1], track_best=True)
+        self.adam.capacity = self.capacity
         self.seed = torch.ones((), dtype=torch.float32, device=dev)          # static loss-gradient seed
         self.means2D = torch.zeros(params["means3D"].shape[0], 3, device=dev)  # no grad: tracking ignores it
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
+        q0, t0 = rots[..., time_idx].detach().clone(), trans[..., time_idx].detach().clone()
         with torch.cuda.stream(side):  # warm-up iterations (real tracking iterations) outside the capture
             for _ in range(max(1, warmup_iters)):
                 self._iteration(0)
+            with torch.no_grad():  # ... undone: the frame starts from its pose with a fresh optimizer
+                rots[..., time_idx] = q0
+                trans[..., time_idx] = t0
+            self.adam.reset()
+            self.status.zero_()
         torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
         if timing:  # device-clock stamps around render_bwd become graph nodes (accumulate over replays)
             from . import profiling
             torch.cuda.synchronize(dev)
@@ -87,6 +105,7 @@ class GraphTracker:
                 self.loss = self._iteration(k)
 
     def _iteration(self, k: int):
+        self.adam.status = self.status[k]  # this iteration's forward guards its Adam step
         if self.fuse_pose:
             from .glue import tracking_iteration
             loss, _ = tracking_iteration(self.params, self.curr, self.t, self.cfg, pose_adam=self.adam,
@@ -96,17 +115,46 @@ class GraphTracker:
         loss, _, _ = _get_loss_tracking_fused(self.params, self.curr, self.t, self.cfg, dual=True,
                                               capacity=self.capacity, status=self.status[k], pose_adam=self.adam,
                                               means2D=self.means2D, seed=self.seed)
+        self.adam.loss = loss  # best-candidate selection in the transform backward
         torch.autograd.backward(loss, self.seed)
+        self.adam.loss = None
         return loss.detach()
+
+    def begin_frame(self):
+        """initialize_optimizer + candidate = the current pose, current_min_loss = 1e20 (splatam.py:700-705)."""
+        with torch.no_grad():
+            self.adam.state.zero_()
+            self.adam.best[0] = 1e20
+            self.adam.best[1:5] = self.params["cam_unnorm_rots"][0, :, self.t]
+            self.adam.best[5:8] = self.params["cam_trans"][0, :, self.t]
+
+    def end_frame(self):
+        """Copy the best candidate pose back into the frame's column (splatam.py:760-763)."""
+        with torch.no_grad():
+            self.params["cam_unnorm_rots"][0, :, self.t] = self.adam.best[1:5]
+            self.params["cam_trans"][0, :, self.t] = self.adam.best[5:8]
+
+    def track_frame(self, num_iters: int):
+        """One frame's tracking: begin_frame, num_iters iterations (a multiple of iters_per_graph), end_frame."""
+        if num_iters % self.iters:
+            raise ValueError(f"num_iters {num_iters} is not a multiple of iters_per_graph {self.iters}")
+        self.begin_frame()
+        for _ in range(num_iters // self.iters):
+            self.run()
+        self.end_frame()
+
+    def reset_status(self):
+        self.status.zero_()
 
     def run(self):
         """Enqueue `iters_per_graph` tracking iterations (one graph launch, no host sync)."""
         self.graph.replay()
 
     def overflowed(self) -> bool:
-        """True if any iteration of the last replay exceeded the binning capacity (one host sync)."""
+        """True if any iteration since the last reset_status() exceeded the binning capacity (one host sync)."""
         st = self.status.cpu()
         return bool((st[:, 0] > self.capacity).any() or (st[:, 2] > TILE_SORT_CAP).any() or (st[:, 1] != 0).any())
 
     def num_rendered(self) -> list[int]:
+        """Per captured iteration: the largest num_rendered since the last reset_status()."""
         return [int(x) for x in self.status[:, 0].cpu()]

@@ -210,7 +210,8 @@ def test_dual_render_matches_two_calls_and_oracle(cuda, aniso):
     m3, op, col, col2, sc, ro = (leaf(scene.means3D), leaf(scene.opacities), leaf(scene.colors), leaf(colors2),
                                  leaf(scene.scales), leaf(scene.rotations))
     m2 = torch.zeros_like(m3, requires_grad=True)
-    im, im2, radii, depth = rasterize_gaussians_dual(m3, m2, None, col, col2, op, sc, ro, None, st)
+    im, im2, radii, depth = rasterize_gaussians_dual(m3, m2, None, col, col2, op, sc, ro, None, st,
+                                                     means2D_grad_sum=True)
     assert np.array_equal(im.detach().cpu().numpy(), a["color"])
     assert np.array_equal(im2.detach().cpu().numpy(), b["color"])
     assert np.array_equal(radii.cpu().numpy(), a["radii"])
@@ -226,6 +227,25 @@ def test_dual_render_matches_two_calls_and_oracle(cuda, aniso):
     for k, v in got.items():
         ref = ra[k].reshape(v.shape) + rb[k].reshape(v.shape)
         assert harness.rel_l2(v.detach().cpu().numpy(), ref) <= 1e-4, k
+    # by default the dual render gives means2D no gradient: the reference's densification statistics
+    # read the RGB render's own means2D gradient (scripts/splatam.py:256), which the sum is not
+    m2b = torch.zeros_like(m3, requires_grad=True)
+    im, im2, _, _ = rasterize_gaussians_dual(m3, m2b, None, col, col2, op, sc, ro, None, st)
+    ((im * torch.as_tensor(dpix, device=cuda)).sum() + (im2 * torch.as_tensor(dpix2, device=cuda)).sum()).backward()
+    assert m2b.grad is None
+
+
+def test_fused_mapping_refuses_densification(cuda):
+    """Gaussian-splatting densification needs the RGB render's own means2D gradient: the fused
+    (one-rasterization) mapping path declines it and the literal two-call path runs."""
+    from splatam_amd import slam
+    scene = make_scene(500, 64, 48, seed=3)
+    params = slam.init_mapping_params(scene, num_frames=1, device=cuda)
+    cam = slam.camera_settings(scene.cam, cuda)
+    curr = {"cam": cam, "w2c": torch.eye(4, device=cuda), "im": torch.rand(3, 48, 64, device=cuda),
+            "depth": torch.rand(1, 48, 64, device=cuda)}
+    assert slam.fused_mapping_eligible(params, curr, slam.MappingConfig())
+    assert not slam.fused_mapping_eligible(params, curr, slam.MappingConfig(use_gaussian_splatting_densification=True))
 
 
 def test_dual_render_skips_unneeded_gradients(cuda):
@@ -343,3 +363,28 @@ def test_block_masks_are_conservative(cuda, aniso):
     assert int(missed.sum()) == 0, int(missed.sum())
     kept = torch.stack([(mask[staged] >> b) & 1 for b in range(16)], 1).sum()
     assert int(kept) < 16 * int(staged.sum())  # it does cull
+
+
+def test_mark_visible_matches_oracle(cuda):
+    """GaussianRasterizer.markVisible (__init__.py:159-168 -> rasterize_points.cu:198-216 ->
+    checkFrustum, rasterizer_impl.cu:54-67): view_z > 0.001, against the oracle, including points
+    behind, on and just in front of the near limit and a non-identity view."""
+    from oracle import oracle
+    from splatam_amd.rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+    from splatam_amd.scenes import setup_camera
+    g = torch.Generator().manual_seed(21)
+    P = 5000
+    pts = torch.randn(P, 3, generator=g) * 2.0
+    pts[:16, 2] = torch.tensor([0.001, 0.0010001, 0.0009999, -0.001, 0.0, 1e-7, -1e-7, 0.002] * 2)
+    w2c = torch.eye(4)
+    w2c[:3, 3] = torch.tensor([0.1, -0.2, 0.3])
+    cam = setup_camera(64, 48, 50.0, 50.0, 31.5, 23.5, w2c=w2c)
+    st = GaussianRasterizationSettings(image_height=48, image_width=64, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+                                       bg=torch.zeros(3, device=cuda), scale_modifier=1.0,
+                                       viewmatrix=cam.viewmatrix.to(cuda), projmatrix=cam.projmatrix.to(cuda),
+                                       sh_degree=0, campos=cam.campos.to(cuda), prefiltered=False)
+    vis = GaussianRasterizer(st).markVisible(pts.to(cuda))
+    assert vis.dtype == torch.bool and vis.shape == (P,)
+    ref = oracle.mark_visible(pts.numpy(), cam.viewmatrix.numpy())
+    np.testing.assert_array_equal(vis.cpu().numpy(), ref)
+    assert 0 < int(vis.sum()) < P

@@ -61,7 +61,7 @@ def test_glue_equals_literal(cuda, aniso, mode):
     assert float((rad0 == rad1).float().mean()) >= 0.999
     assert float(l0) > 0.0 and float(r0.abs().sum()) > 0.0
     # means2D gradient of the RGB render (retained by the reference for densification stats);
-    # the dual rasterization returns the sum over both images instead (documented)
+    # the dual rasterization gives means2D no gradient unless asked for the sum (documented)
     if mode not in ("fused_dual", "fused_pose"):
         assert m1 is not None and float((m1 - m0).norm() / m0.norm()) <= 1e-3
 
@@ -101,20 +101,23 @@ def _pose_leaves(params):
 def test_graph_tracker_matches_eager_iterations(cuda, fuse_pose):
     """HIP-graph replay (static-capacity forward, pose Adam fused into the transform
     backward) follows the pose trajectory of the same number of eager iterations
-    with torch.optim.Adam (float rounding of the Adam update differs: 1e-6 abs)."""
+    with torch.optim.Adam (float rounding of the Adam update differs: 1e-6 abs).
+    The construction's warm-up iterations are undone (pose restored, optimizer reset)."""
     from splatam_amd.tracker import GraphTracker
     params, curr = _setup(cuda, False)
     S, W = 6, 2
     pe = _pose_leaves(params)
     opt = torch.optim.Adam([{"params": [pe["cam_unnorm_rots"]], "lr": 0.0004},
                             {"params": [pe["cam_trans"]], "lr": 0.002}], fused=True)
-    for _ in range(W + S):
+    for _ in range(S):
         opt.zero_grad(set_to_none=True)
         loss, _, _ = get_loss_tracking(pe, curr, 1)
         loss.backward()
         opt.step()
     pg = _pose_leaves(params)
     tr = GraphTracker(pg, curr, 1, iters_per_graph=S, warmup_iters=W, fuse_pose=fuse_pose)
+    assert torch.equal(pg["cam_unnorm_rots"].detach(), params["cam_unnorm_rots"])  # warm-up undone
+    assert torch.equal(pg["cam_trans"].detach(), params["cam_trans"])
     tr.run()
     torch.cuda.synchronize()
     assert not tr.overflowed()
@@ -128,11 +131,16 @@ def test_graph_tracker_matches_eager_iterations(cuda, fuse_pose):
 def test_graph_tracker_reports_overflow(cuda, fuse_pose):
     from splatam_amd.tracker import GraphTracker
     params, curr = _setup(cuda, False)
-    tr = GraphTracker(_pose_leaves(params), curr, 1, iters_per_graph=2, warmup_iters=1, headroom=0.5, min_extra=0,
+    p = _pose_leaves(params)
+    tr = GraphTracker(p, curr, 1, iters_per_graph=2, warmup_iters=1, headroom=0.5, min_extra=0,
                       fuse_pose=fuse_pose)
     tr.run()
     torch.cuda.synchronize()
     assert tr.overflowed()
+    # every iteration overflowed: its Adam step was skipped on the device (pose and state untouched)
+    assert torch.equal(p["cam_unnorm_rots"].detach(), params["cam_unnorm_rots"])
+    assert torch.equal(p["cam_trans"].detach(), params["cam_trans"])
+    assert float(tr.adam.state.abs().sum()) == 0.0
 
 
 @pytest.mark.parametrize("scale_cols", [1, 3])
