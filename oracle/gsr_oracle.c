@@ -67,6 +67,7 @@ typedef REAL real;
 
 static int g_threads = 0; /* 0: OpenMP default (OMP_NUM_THREADS / all cores) */
 void oracle_set_threads(int n) { g_threads = n < 0 ? 0 : n; }
+int oracle_threads(void);
 static int nthreads(void)
 {
 #ifdef _OPENMP
@@ -861,3 +862,4 @@ void oracle_mark_visible(int P, const real* means3D, const real* view, unsigned 
 }
 
 int oracle_real_size(void) { return (int)sizeof(real); }
+int oracle_threads(void) { return nthreads(); }

@@ -33,6 +33,12 @@ _libs: dict = {}
 _threads = 0  # 0: OpenMP default (OMP_NUM_THREADS or every core); results do not depend on it
 
 
+def threads() -> int:
+    """Threads the oracle's parallel loops use."""
+    lib = _lib(np.float32)[0]
+    return int(lib.oracle_threads())
+
+
 def set_threads(n: int) -> None:
     """Threads of the oracle's parallel loops (0 = OpenMP default).  The results are
     identical for any count (fixed-order per-instance sums, see gsr_oracle.c)."""
@@ -84,6 +90,7 @@ def _lib(dtype):
         lib.oracle_free_list.argtypes = [P(FwdOut)]
         lib.oracle_mark_visible.argtypes = [ctypes.c_int, P(real), P(real), P(ctypes.c_ubyte)]
         lib.oracle_set_threads.argtypes = [ctypes.c_int]
+        lib.oracle_threads.restype = ctypes.c_int
         lib.oracle_set_threads(_threads)
         _libs[key] = (lib, real, In, FwdOut, Grads)
     return _libs[key]

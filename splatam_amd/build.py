@@ -37,13 +37,13 @@ def flags():
             "-I", os.path.join(ROOT, "include"), "-I", CSRC]
 
 
-def _compile(src: str) -> str:
-    obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+def _compile(src: str, objdir: str = OBJDIR, extra=()) -> str:
+    obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
     srcp = os.path.join(CSRC, src)
     deps = [srcp, os.path.join(ROOT, "include", "gsr.h"), os.path.join(ROOT, "include", "gsr_glue.h")] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
-    cmd = [hipcc(), *flags(), "-c", srcp, "-o", obj]
+    cmd = [hipcc(), *flags(), *extra, "-c", srcp, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
@@ -63,6 +63,22 @@ def build(force: bool = False) -> str:
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
     return LIB
+
+
+def build_diag() -> str:
+    """Diagnostics library (tools/wgtime.py): libgsr with -DGSR_WGTIME=1 (per-workgroup render timelines),
+    built to splatam_amd/_build_diag/libgsr_diag.so; loaded only through GSR_LIB by the diagnostics tool."""
+    objdir = os.path.join(HERE, "_build_diag")
+    os.makedirs(objdir, exist_ok=True)
+    with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, objdir, ("-DGSR_WGTIME=1",)), SOURCES))
+    lib = os.path.join(objdir, "libgsr_diag.so")
+    if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in objs):
+        r = subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    return lib
 
 
 if __name__ == "__main__":

@@ -24,6 +24,7 @@
 #endif
 
 namespace gsr {
+GSR_WGTIME_TABLE
 
 // Per-pair geometric terms (hx, hy, hx dx, hx dy, hy dy[, G dL/dalpha]) with
 // h = G * dL/dG = (o * G) * dL/dalpha.
@@ -118,6 +119,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                   unsigned long long* clk) {
     static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
     kclock_begin(clk);
+    GSR_WGTIME_MARK(false);
     if (guard.overflow()) {  // invalid forward state (static-mode overflow): touch nothing
         kclock_end(clk);
         return;
@@ -349,6 +351,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
 #if GSR_ABLATE == 1
     if (ablate_sink == 1.2345f) inst[0] = ablate_sink;  // keeps the per-pair values alive (timing ablation)
 #endif
+    GSR_WGTIME_MARK(true);
     kclock_end(clk);
 }
 
@@ -615,5 +618,12 @@ hipError_t launch_selftest_reduce9(const float* in, float* out, hipStream_t s) {
     hipLaunchKernelGGL(selftest_reduce9_kernel, dim3(1), dim3(64), 0, s, in, out);
     return hipGetLastError();
 }
+
+#if GSR_WGTIME
+extern "C" int gsr_diag_wgtime_bwd(unsigned long long* host, int n) {
+    const size_t bytes = sizeof(unsigned long long) * 4 * (size_t)(n < GSR_WGTIME_MAX ? n : GSR_WGTIME_MAX);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgtime), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // namespace gsr

@@ -600,6 +600,31 @@ __device__ __forceinline__ RowGroup4 load_row_group4(const uint16_t* row_list, i
 // launch.  wall_clock64 runs at 100 MHz.
 constexpr int KCLOCK_GROUP_STRIDE = 32;  // u64 words (256 B)
 constexpr int KCLOCK_WORDS = 4 + 16 * KCLOCK_GROUP_STRIDE;
+// Diagnostics build only (-DGSR_WGTIME=1, tools/wgtime.py; never in libgsr.so): every render
+// workgroup records [start, end, HW_ID, XCC_ID] in its translation unit's g_wgtime table.
+#ifndef GSR_WGTIME
+#define GSR_WGTIME 0
+#endif
+#define GSR_WGTIME_MAX 16384
+#if GSR_WGTIME
+#define GSR_WGTIME_TABLE static __device__ unsigned long long g_wgtime[GSR_WGTIME_MAX][4];
+#define GSR_WGTIME_MARK(end_)                                                                              \
+    do {                                                                                                   \
+        if (end_) __syncthreads();                                                                         \
+        const unsigned b_ = blockIdx.y * gridDim.x + blockIdx.x;                                           \
+        if (threadIdx.x == 0 && b_ < GSR_WGTIME_MAX) {                                                     \
+            g_wgtime[b_][(end_) ? 1 : 0] = wall_clock64();                                                 \
+            if (!(end_)) {                                                                                 \
+                g_wgtime[b_][2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);                     \
+                g_wgtime[b_][3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);                    \
+            }                                                                                              \
+        }                                                                                                  \
+    } while (0)
+#else
+#define GSR_WGTIME_TABLE
+#define GSR_WGTIME_MARK(end_) do {} while (0)
+#endif
+
 __device__ __forceinline__ void kclock_begin(unsigned long long* clk) {
     if (clk && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
         __hip_atomic_store(&clk[0], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

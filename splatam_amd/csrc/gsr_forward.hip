@@ -15,6 +15,7 @@
 #include "gsr_common.h"
 
 namespace gsr {
+GSR_WGTIME_TABLE
 
 // ------------------------------------------------------------- preprocess --
 // LDS_HIST: per-tile instance counts go to a workgroup histogram in LDS and
@@ -927,6 +928,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
                   SpecGuard guard, unsigned long long* clk, TrackL1 l1) {
     static_assert(DUAL || !L1, "the tracking loss needs the depth / silhouette colour set");
     kclock_begin(clk);
+    GSR_WGTIME_MARK(false);
     if (guard.overflow()) {
         kclock_end(clk);
         return;
@@ -1119,8 +1121,16 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
             }
         }
     }
+    GSR_WGTIME_MARK(true);
     kclock_end(clk);
 }
+
+#if GSR_WGTIME
+extern "C" int gsr_diag_wgtime_fwd(unsigned long long* host, int n) {
+    const size_t bytes = sizeof(unsigned long long) * 4 * (size_t)(n < GSR_WGTIME_MAX ? n : GSR_WGTIME_MAX);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgtime), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int track_l1_fused_scratch_floats(int ntiles) { return 2 * ntiles + ARRIVE_GROUPED_WORDS; }
 
