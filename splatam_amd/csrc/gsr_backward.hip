@@ -143,12 +143,12 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     __shared__ uint32_t s_rmax[16];
     __shared__ __attribute__((aligned(16))) uint16_t s_list[16 * LS];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, row = (tid >> 4) & 3;
-    const int tile = blockIdx.y * cam.gx + blockIdx.x;
-    const int px = blockIdx.x * TILE_X + tile_px(tid);
-    const int py = blockIdx.y * TILE_Y + tile_py(tid);
+    const int tile = sched_tile(cam), tx = tile % cam.gx, ty = tile / cam.gx;
+    const int px = tx * TILE_X + tile_px(tid);
+    const int py = ty * TILE_Y + tile_py(tid);
     const bool inside = px < cam.W && py < cam.H;
     const int pid = py * cam.W + px;
-    const float x0 = (float)(blockIdx.x * TILE_X), y0 = (float)(blockIdx.y * TILE_Y);
+    const float x0 = (float)(tx * TILE_X), y0 = (float)(ty * TILE_Y);
     const int HW = cam.W * cam.H;
     const uint2 range = ranges[tile];
     const float T_final = inside ? final_T[pid] : 0.f;
@@ -180,7 +180,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {
         const uint32_t gk = pe_id(point_list[k]);
         const RenderRec r = load_rr(rr, gk);
-        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), blockIdx.x, blockIdx.y);
+        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), tx, ty);
         float2* dst = reinterpret_cast<float2*>(inst + (size_t)RS * u);
 #pragma unroll
         for (int m = 0; m < RS / 2; m++) dst[m] = make_float2(0.f, 0.f);
@@ -216,7 +216,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             const uint32_t gi = pe_id(pe);
             pm = pe_mask(pe);
             const RenderRec r = load_rr(rr, gi);
-            pu = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), blockIdx.x, blockIdx.y);
+            pu = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), tx, ty);
             pa = r.q0; pb = r.q1; pc = r.q2;
             if (DUAL) pd = r.q3;
         }
@@ -397,7 +397,7 @@ hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint6
                : (c1 ? (c2 ? bwd_variant<true, 0, 1, 1>() : bwd_variant<true, 0, 1, 0>())
                      : (c2 ? bwd_variant<true, 0, 0, 1>() : bwd_variant<true, 0, 0, 0>()));
     }
-    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rr, geo.blocksums,
+    hipLaunchKernelGGL(k, dim3(cam.gx * cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rr, geo.blocksums,
                        final_T, n_contrib, dL_dpix, dL_dpix2, inst, guard, clk);
     return hipGetLastError();
 }

@@ -115,12 +115,12 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
     __shared__ uint8_t s_mask[B];
     __shared__ __attribute__((aligned(16))) uint16_t s_list[4][B + 4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int tile = blockIdx.y * cam.gx + blockIdx.x;
-    const int px = blockIdx.x * TILE_X + tile_px(tid);
-    const int py = blockIdx.y * TILE_Y + tile_py(tid);
+    const int tile = sched_tile(cam), tx = tile % cam.gx, ty = tile / cam.gx;
+    const int px = tx * TILE_X + tile_px(tid);
+    const int py = ty * TILE_Y + tile_py(tid);
     const bool inside = px < cam.W && py < cam.H;
     const int pid = py * cam.W + px;
-    const float x0 = (float)(blockIdx.x * TILE_X), y0 = (float)(blockIdx.y * TILE_Y);
+    const float x0 = (float)(tx * TILE_X), y0 = (float)(ty * TILE_Y);
     const int HW = cam.W * cam.H;
     const uint2 range = ranges[tile];
     const float T_final = inside ? final_T[pid] : 0.f;
@@ -140,7 +140,7 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
     for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {
         const uint32_t gk = pe_id(point_list[k]);
         const RenderRec r = load_rr(rr, gk);
-        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), blockIdx.x, blockIdx.y);
+        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), tx, ty);
 #pragma unroll
         for (int m = 0; m < NVP / 4; m++) rec[(size_t)u * (NVP / 4) + m] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -158,7 +158,7 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
             const RenderRec r = load_rr(rr, gi);
             const float4 pa = r.q0, pb = r.q1;
             s_g[tid] = gi;
-            s_u[tid] = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), blockIdx.x, blockIdx.y);
+            s_u[tid] = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), tx, ty);
             s_a[tid] = pa;
             s_b[tid] = pb;
             s_c[tid] = make_float4(r.q2.x, r.q2.y, r.q2.z, __uint_as_float(clamp_bits[gi]));
@@ -278,7 +278,7 @@ hipError_t launch_render_bwd_power(const Camera& cam, const GaussIn& g, const ui
                                    BwdGuard guard, hipStream_t s) {
     const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
     const int has_scales = g.scales != nullptr;
-    const dim3 grid(cam.gx, cam.gy), block(TILE_PIX);
+    const dim3 grid(cam.gx * cam.gy), block(TILE_PIX);
 #define GSR_LAUNCH_POWER(NSH_)                                                                                      \
     hipLaunchKernelGGL(render_bwd_power_kernel<NSH_>, grid, block, 0, s, cam, has_scales, power, ranges, point_list, \
                        geo.rr, geo.blocksums, geo.clamp, (const float4*)jac, final_T,                                              \

@@ -72,6 +72,15 @@ struct RatioHint {
     std::atomic<double> v{3.0};  // last num_rendered / P (binning capacity hint)
 };
 RatioHint g_inst_ratio[kMaxDevices];
+std::atomic<int> g_cus[kMaxDevices];  // CU count per device (render schedule round size), 0 = unknown
+int device_cus(int dev) {
+    int n = g_cus[dev].load(std::memory_order_relaxed);
+    if (n > 0) return n;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    (void)hipGetLastError();
+    g_cus[dev].store(n, std::memory_order_relaxed);
+    return n;
+}
 
 Camera make_camera(const gsr_settings* s) {
     Camera c;
@@ -296,7 +305,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     hipStream_t stream = (hipStream_t)stream_;
     const int dev = stream_device(stream);
     Pinned& pin = g_pinned[dev];
-    const Camera cam = make_camera(settings);
+    Camera cam = make_camera(settings);
     GaussIn g = make_gauss(gaussians);
     g.colors2 = colors2;  // packed into the render records by preprocess (dual render)
     const int P = g.P, W = cam.W, H = cam.H;
@@ -312,6 +321,9 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     uint2* ranges = (uint2*)(ib + IL.ranges);
     uint32_t* tile_count = (uint32_t*)(ib + IL.tile_count);
     const int ntiles = cam.gx * cam.gy;
+    uint32_t* order = (uint32_t*)(ib + IL.order);
+    cam.tile_order = order;   // render schedule (tile_plan in the bucketed duplicate, else row-major)
+    cam.sched_cus = device_cus(dev);
     uint32_t* cursor = tile_count + (size_t)ntiles * TILE_CTR_STRIDE;
     hipError_t e;
     // tile counts: per-workgroup LDS histograms + column scan (transient count matrix in SCRATCH),
@@ -328,6 +340,12 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     }
     static const bool force_radix_env = getenv("GSR_FORCE_RADIX") && atoi(getenv("GSR_FORCE_RADIX")) != 0;
     const bool force_radix = force_radix_env && capacity <= 0;
+    // the bucketed duplicate's workgroup 0 writes the render schedule (tile_plan); the other paths
+    // render in row-major order
+    Camera cplan = cam;
+    cplan.tile_order_out = (lds_hist && !force_radix) ? order : nullptr;
+    if ((!lds_hist || force_radix) && P > 0 && (e = launch_identity_order(order, ntiles, stream)) != hipSuccess)
+        return hip_fail(e, "render schedule");
     // the bucketed duplicate does the instance / tile scans itself (lds_hist); otherwise a
     // scan launch does them, and the counters are final right after it
     const bool scan_in_duplicate = lds_hist && !force_radix;
@@ -415,7 +433,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         const SpecGuard guard{geo.counters, cap, (uint32_t)TILE_SORT_CAP};
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
-            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
+            if ((e = launch_duplicate_bucket(cplan, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
                                              ntiles, keys[0], GL.nb, guard, capacity > 0 ? status : nullptr,
                                              stream)) != hipSuccess)
                 return hip_fail(e, "duplicate");
@@ -456,7 +474,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     if (tile_sorted) {
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
-            if ((e = launch_duplicate_bucket(cam, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
+            if ((e = launch_duplicate_bucket(cplan, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
                                              ntiles, keys[0], GL.nb, none, nullptr, stream)) != hipSuccess)
                 return hip_fail(e, "duplicate");
         }
@@ -504,12 +522,14 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     if (!grads) return fail(GSR_ERR_INVALID_ARG, "grads required");
     if (num_rendered < 0) return fail(GSR_ERR_INVALID_ARG, "num_rendered must be >= 0");
     hipStream_t stream = (hipStream_t)stream_;
-    const Camera cam = make_camera(settings);
+    Camera cam = make_camera(settings);
     const GaussIn g = make_gauss(gaussians);
     const int P = g.P;
     if (P == 0) return GSR_OK;
     if (!geom_buffer || !image_buffer || !radii || !dL_dout_color)
         return fail(GSR_ERR_INVALID_ARG, "missing forward state");
+    // the forward's render schedule (a permutation of the tiles; any order gives the same results)
+    cam.tile_order = (const uint32_t*)((const char*)image_buffer + ImgLayout::make(cam.W, cam.H).order);
     const GeomLayout GL = GeomLayout::make(P);
     const ImgLayout IL = ImgLayout::make(cam.W, cam.H);
     const BinLayout BL = BinLayout::make(num_rendered, cam.W, cam.H);

@@ -71,6 +71,7 @@ struct ImgLayout {        // per-pixel / per-tile state ("imgBuffer")
     size_t final_T;       // f32   [N]
     size_t n_contrib;     // u32   [N]
     size_t ranges;        // uint2 [tiles]  [start, end) of each tile's sorted list
+    size_t order;         // u32   [tiles]  render schedule: workgroup i renders tile order[i] (tile_plan)
     size_t tile_count;    // u32   [2*tiles*TILE_CTR_STRIDE] instance counters, then bucket cursors (one memset)
     size_t total;
     static ImgLayout make(int W, int H) {
@@ -81,6 +82,7 @@ struct ImgLayout {        // per-pixel / per-tile state ("imgBuffer")
         L.final_T = o; o = align_up(o + 4 * (N ? N : 1), 256);
         L.n_contrib = o; o = align_up(o + 4 * (N ? N : 1), 256);
         L.ranges = o; o = align_up(o + 8 * (T ? T : 1), 256);
+        L.order = o; o = align_up(o + 4 * (T ? T : 1), 256);
         L.tile_count = o; o = align_up(o + 8 * (size_t)TILE_CTR_STRIDE * (T ? T : 1), 256);
         L.total = o;
         return L;
@@ -138,7 +140,17 @@ struct Camera {
     float scale_modifier;
     int sh_degree;
     int prefiltered;
+    // Render schedule: render workgroup i renders tile tile_order[i] (a permutation written by
+    // the binning's workgroup 0, tile_plan; nullptr = row-major).  sched_cus: the device's CU
+    // count, the round size of the plan.
+    const uint32_t* tile_order = nullptr;
+    uint32_t* tile_order_out = nullptr;
+    int sched_cus = 256;
 };
+// the tile a render workgroup (1D grid over the tiles) works on
+__device__ __forceinline__ int sched_tile(const Camera& cam) {
+    return cam.tile_order ? (int)cam.tile_order[blockIdx.x] : (int)blockIdx.x;
+}
 
 struct GaussIn {
     int P, M;
@@ -616,7 +628,8 @@ constexpr int KCLOCK_WORDS = 4 + 16 * KCLOCK_GROUP_STRIDE;
             g_wgtime[b_][(end_) ? 1 : 0] = wall_clock64();                                                 \
             if (!(end_)) {                                                                                 \
                 g_wgtime[b_][2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);                     \
-                g_wgtime[b_][3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);                    \
+                g_wgtime[b_][3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) |                   \
+                                  ((unsigned long long)sched_tile(cam) << 32);                             \
             }                                                                                              \
         }                                                                                                  \
     } while (0)
@@ -965,6 +978,8 @@ __device__ __forceinline__ void status_merge(uint32_t* st, uint32_t n, uint32_t 
 // lds_hist: the colscan ran without its scan tail; every workgroup scans the
 // workgroup and tile totals (`tot`) itself, workgroup 0 writes ranges,
 // counters and `status` (static mode; may be null).
+// Row-major render schedule (the paths that do not run tile_plan).
+hipError_t launch_identity_order(uint32_t* order, int ntiles, hipStream_t s);
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2* ranges, const uint32_t* tot,
                                    uint32_t* cursor, bool lds_hist, int ntiles, uint64_t* keys, int nb,
                                    SpecGuard guard, uint32_t* status, hipStream_t s);

@@ -433,6 +433,59 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
+// ---- render schedule ---------------------------------------------------------
+// All of a frame's render workgroups are resident at once (e.g. 1200 tiles on 256
+// CUs at 5 workgroups per CU), workgroup i is dispatched to XCD i mod 8 and, inside
+// it, round-robin over the XCD's CUs: workgroups i and i + ncu share a CU.  A render
+// kernel therefore lasts as long as its most loaded CU (measured: the per-CU sum of
+// tile work spread 0.81-1.18x of the mean with the row-major order, kernel span set
+// by the top; tools/wgtime.py).  tile_plan deals the tiles, in descending order of
+// list length (the render cost: 0.998 correlation with the tile's contributing
+// pairs), to workgroup slots in rounds of ncu, alternating direction (odd rounds
+// and the last, partial round reversed), so every CU's tiles add up to about the
+// same work (max/mean 1.07 on config 3).  Counting sort over length buckets of 4:
+// ties land in arbitrary order, which changes only which workgroup renders a tile,
+// never its results.
+constexpr int PLAN_BUCKETS = PRE_BLOCK, PLAN_SHIFT = 2;
+__device__ __forceinline__ uint32_t plan_bucket(uint32_t len) {  // descending length -> ascending bucket
+    return (uint32_t)(PLAN_BUCKETS - 1) - min(len >> PLAN_SHIFT, (uint32_t)(PLAN_BUCKETS - 1));
+}
+__device__ __forceinline__ uint32_t plan_slot(uint32_t p, uint32_t n, uint32_t ncu) {
+    const uint32_t rd = p / ncu, k = p - rd * ncu, base = rd * ncu, m = min(ncu, n - base);
+    return base + (((rd & 1u) || m < ncu) ? m - 1u - k : k);
+}
+// one workgroup of PRE_BLOCK threads; s_hist: PLAN_BUCKETS words of LDS
+__device__ void tile_plan(const uint32_t* __restrict__ tot, int ntiles, int ncu, uint32_t* __restrict__ order,
+                          uint32_t* s_hist, uint32_t* s_wsum) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    s_hist[tid] = 0u;
+    __syncthreads();
+    for (int u = tid; u < ntiles; u += PRE_BLOCK) atomicAdd(&s_hist[plan_bucket(tot[u])], 1u);
+    __syncthreads();
+    const uint32_t c = s_hist[tid];
+    const uint32_t incl = wave_incl_scan(c);
+    if (lane == 63) s_wsum[w] = incl;
+    __syncthreads();
+    uint32_t woff = 0;
+    for (int k = 0; k < w; k++) woff += s_wsum[k];
+    s_hist[tid] = woff + incl - c;  // exclusive: first position of the bucket
+    __syncthreads();
+    for (int u = tid; u < ntiles; u += PRE_BLOCK) {
+        const uint32_t p = atomicAdd(&s_hist[plan_bucket(tot[u])], 1u);
+        order[plan_slot(p, (uint32_t)ntiles, (uint32_t)ncu)] = (uint32_t)u;
+    }
+}
+
+__global__ void identity_order_kernel(uint32_t* __restrict__ order, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) order[i] = (uint32_t)i;
+}
+hipError_t launch_identity_order(uint32_t* order, int ntiles, hipStream_t s) {
+    if (ntiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(identity_order_kernel, dim3((ntiles + 255) / 256), dim3(256), 0, s, order, ntiles);
+    return hipGetLastError();
+}
+
 template <bool LDS_HIST>
 __global__ void __launch_bounds__(PRE_BLOCK)
 duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges, const uint32_t* __restrict__ tot,
@@ -541,6 +594,10 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
                 geo.counters[3] = sort_cap;
                 if (status) status_merge(status, all, viol, vmax, sort_cap);
             }
+        }
+        if (b == 0 && cam.tile_order_out) {
+            __shared__ uint32_t s_plan[PLAN_BUCKETS];
+            tile_plan(tot, ntiles, cam.sched_cus, cam.tile_order_out, s_plan, wsum);
         }
         base = pre;
         if (all > guard.cap_inst || vmax > guard.cap_tile) return;  // workgroup-uniform
@@ -946,10 +1003,10 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
     constexpr int LS = RENDER_BATCH + 4;  // row-list stride (u16)
     __shared__ __attribute__((aligned(16))) uint16_t s_list[16 * LS];
     const int tid = threadIdx.x, w = tid >> 6, row = (tid >> 4) & 3;
-    const int tile = blockIdx.y * cam.gx + blockIdx.x;
-    const int px = blockIdx.x * TILE_X + tile_px(tid);
-    const int py = blockIdx.y * TILE_Y + tile_py(tid);
-    const float x0 = (float)(blockIdx.x * TILE_X), y0 = (float)(blockIdx.y * TILE_Y);
+    const int tile = sched_tile(cam), tx = tile % cam.gx, ty = tile / cam.gx;
+    const int px = tx * TILE_X + tile_px(tid);
+    const int py = ty * TILE_Y + tile_py(tid);
+    const float x0 = (float)(tx * TILE_X), y0 = (float)(ty * TILE_Y);
     const bool inside = px < cam.W && py < cam.H;
     const v2f pix = v2f{(float)px, (float)py};
     const uint2 range = ranges[tile];
@@ -1141,7 +1198,7 @@ hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* p
                              unsigned long long* clk, const TrackL1* l1) {
     auto k = colors2 ? (l1 ? render_fwd_kernel<true, true> : render_fwd_kernel<true, false>)
                      : render_fwd_kernel<false, false>;
-    hipLaunchKernelGGL(k, dim3(cam.gx, cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, keys,
+    hipLaunchKernelGGL(k, dim3(cam.gx * cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, keys,
                        geo.rr, final_T,
                        n_contrib, out_color, out_color2, out_depth, guard, clk, l1 ? *l1 : TrackL1{});
     return hipGetLastError();

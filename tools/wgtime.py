@@ -27,7 +27,7 @@ def table(lib, name, n):
 
 
 def summarize(t, khz):
-    start, end, hwid, xcc = t[:, 0].astype(np.int64), t[:, 1].astype(np.int64), t[:, 2], t[:, 3]
+    start, end, hwid, xcc = t[:, 0].astype(np.int64), t[:, 1].astype(np.int64), t[:, 2], t[:, 3] & 0xFFFFFFFF
     t0 = start.min()
     us = lambda x: x / khz * 1e3  # noqa: E731
     dur = us(end - start)
@@ -80,8 +80,24 @@ def main():
     n = ((scene.cam.W + 15) // 16) * ((scene.cam.H + 15) // 16)
     khz = 100000  # wall_clock64: 100 MHz on MI300/MI355 (hipDeviceAttributeWallClockRate)
     res = {"config": a.config, "tiles": n}
+    raw = {}
     for k, name in (("render_fwd", "gsr_diag_wgtime_fwd"), ("render_bwd", "gsr_diag_wgtime_bwd")):
-        res[k] = summarize(table(lib, name, n), khz)
+        raw[k] = table(lib, name, n)
+        res[k] = summarize(raw[k], khz)
+    if a.out:  # per-tile work measures beside the raw timelines (offline analysis)
+        from splatam_amd import _C
+        from splatam_amd.glue import track_transform
+        from splatam_amd.layout import views
+        with torch.no_grad():
+            means, rots, dcol, opac, scales = track_transform(params, 0, w2c)
+            e = torch.Tensor([])
+            out = _C.rasterize_gaussians_dual(cam.bg, means, params["rgb_colors"], dcol, opac, scales, rots, 1.0, e,
+                                              cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy,
+                                              cam.image_height, cam.image_width, e, 0, cam.campos, False)
+            v = views(out[6], out[5], cam.image_width, cam.image_height, out[0])
+        np.savez(a.out.replace(".json", ".npz"), fwd=raw["render_fwd"], bwd=raw["render_bwd"],
+                 ranges=v["ranges"].cpu().numpy(), n_contrib=v["n_contrib"].cpu().numpy(),
+                 masks=v["block_masks"].cpu().numpy(), W=cam.image_width, H=cam.image_height)
     txt = json.dumps(res, indent=1)
     print(txt)
     if a.out:
