@@ -222,7 +222,9 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         }
     };
     fetch((int)bmax);
+    const uint32_t mean4 = sched_mean4(cam, guard.counters);
     for (int hi = (int)bmax; hi > 0; hi -= BB) {
+        prio_by_remaining(hi, mean4);
         const int cnt = min(BB, hi);
         if (tid < cnt) {
             s_u[tid] = pu;

@@ -147,6 +147,27 @@ struct Camera {
     uint32_t* tile_order_out = nullptr;
     int sched_cus = 256;
 };
+// Wave priority by remaining work (GSR_PRIO_SCHED): the instruction arbiter favours older
+// waves, so on a CU the last-dispatched tile used to run alone at the end at one wave per
+// SIMD; raising the priority of the waves with the most work left keeps the CU's tiles
+// finishing together (a dynamic longest-remaining-first among co-resident tiles).
+#ifndef GSR_PRIO_SCHED
+#define GSR_PRIO_SCHED 1
+#endif
+// Levels at 0.7 / 0.45 / 0.22 of the frame's mean tile list (`mean4` = 4 x mean, from num_rendered).
+__device__ __forceinline__ void prio_by_remaining(int remaining, uint32_t mean4) {
+#if GSR_PRIO_SCHED
+    const uint32_t r = 4u * (uint32_t)remaining;  // compare r / mean4 against 0.7, 0.45, 0.22 (x 100)
+    if (100u * r > 70u * mean4) __builtin_amdgcn_s_setprio(3);
+    else if (100u * r > 45u * mean4) __builtin_amdgcn_s_setprio(2);
+    else if (100u * r > 22u * mean4) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#endif
+}
+__device__ __forceinline__ uint32_t sched_mean4(const Camera& cam, const uint32_t* counters) {
+    const uint32_t nt = (uint32_t)(cam.gx * cam.gy);
+    return max(1u, (uint32_t)(4ull * counters[0] / (nt ? nt : 1u)));
+}
 // the tile a render workgroup (1D grid over the tiles) works on
 __device__ __forceinline__ int sched_tile(const Camera& cam) {
     return cam.tile_order ? (int)cam.tile_order[blockIdx.x] : (int)blockIdx.x;

@@ -1036,7 +1036,9 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         if (DUAL) pd = r.q3;
         pm = block_mask_exact(pa, pb, x0, y0);
     }
+    const uint32_t mean4 = sched_mean4(cam, guard.counters);
     for (uint32_t start = range.x; start < range.y; start += RENDER_BATCH) {
+        prio_by_remaining((int)(range.y - start), mean4);
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
         const int cnt = (int)min((uint32_t)RENDER_BATCH, range.y - start);
         if (tid < cnt) {
