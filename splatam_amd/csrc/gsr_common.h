@@ -857,6 +857,9 @@ __device__ __forceinline__ void wave_reduce2x9(const float (&v)[18], float (&r)[
 // ends up with NV values of entry e; further transposed steps split m while the
 // count stays even, plain DPP adds finish the rest.  Cost ~2.8 VALU per value
 // against 4 for four plain DPP steps per value.
+#ifndef GSR_DPP_BANKMASK
+#define GSR_DPP_BANKMASK 1
+#endif
 template <int NV>
 struct RowReduce {
     static constexpr int V = 4 * NV;
@@ -876,14 +879,49 @@ __device__ __forceinline__ void row_tstep(const float* c, float* out, bool hi) {
     }
 }
 
+// The same step for partners in the other half of a 4-lane-bank pair (row_ror:8: banks
+// {0,1} <-> {2,3}; row_half_mirror: banks {0,2} <-> {1,3}): two v_add_f32_dpp whose
+// bank masks write complementary lane halves -- lanes of the low half add the pair's c[i],
+// lanes of the high half c[i + N/2] -- instead of two selects and one DPP add per value.
+// One asm block per step: its leading s_nop 1 covers the VALU-write -> DPP-read hazard of
+// every input (the compiler does not see the DPP inside).  Requires full EXEC.
+#define GSR_DPP_PAIR(CTRL_STR, MLO, MHI)                                                                 \
+    "v_add_f32_dpp %0, %" #MLO ", %" #MLO " " CTRL_STR " row_mask:0xf bank_mask:0x3\n\t"
+template <int N>
+__device__ __forceinline__ void row_tstep_ror8(const float* c, float* out) {
+    static_assert(N % 2 == 0, "even value count");
+    asm volatile("s_nop 1" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < N / 2; i++)
+        asm volatile("v_add_f32_dpp %0, %1, %1 row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
+                     "v_add_f32_dpp %0, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xc"
+                     : "=&v"(out[i]) : "v"(c[i]), "v"(c[i + N / 2]));
+}
+template <int N>
+__device__ __forceinline__ void row_tstep_mirror(const float* c, float* out) {
+    static_assert(N % 2 == 0, "even value count");
+    asm volatile("s_nop 1" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < N / 2; i++)
+        asm volatile("v_add_f32_dpp %0, %1, %1 row_half_mirror row_mask:0xf bank_mask:0x5\n\t"
+                     "v_add_f32_dpp %0, %2, %2 row_half_mirror row_mask:0xf bank_mask:0xa"
+                     : "=&v"(out[i]) : "v"(c[i]), "v"(c[i + N / 2]));
+}
+#undef GSR_DPP_PAIR
+
 // r[i] = row total of value (entry row_entry(lane), m = row_m0<NV>(lane) + i)
 template <int NV>
 __device__ __forceinline__ void row_reduce(const float (&v)[4 * NV], float (&r)[RowReduce<NV>::R], int lane) {
     using RR = RowReduce<NV>;
     constexpr int V = RR::V;
     float a[V / 2], b[V / 4];
+#if GSR_DPP_BANKMASK
+    row_tstep_ror8<V>(v, a);                    // row_ror:8, bank-masked pair adds
+    row_tstep_mirror<V / 2>(a, b);              // row_half_mirror, bank-masked pair adds
+#else
     row_tstep<V, 0x128>(v, a, lane & 8);        // row_ror:8
     row_tstep<V / 2, 0x141>(a, b, lane & 4);    // row_half_mirror
+#endif
     if constexpr (RR::S == 2) {
 #pragma unroll
         for (int i = 0; i < RR::R; i++) {
