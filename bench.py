@@ -69,6 +69,9 @@ def parse():
                     help="also time the unchanged-caller path: SURVEY 8(d)'s unit through "
                          "diff_gaussian_rasterization.GaussianRasterizer, eager (the 'dropin' object)")
     ap.add_argument("--dropin-frames", type=int, default=3, help="dropin: timed frames of 40 iterations")
+    ap.add_argument("--fisher", choices=("on", "off"), default="on",
+                    help="also time the batched Fisher / EIG view scoring (backward_power 2) on the same map")
+    ap.add_argument("--fisher-k", type=int, default=16, help="fisher: poses per HIP-graph launch")
     ap.add_argument("--timing", type=int, default=1,
                     help="0: no device-clock timing of render_bwd in the graph (A/B check; no roofline)")
     return ap.parse_args()
@@ -219,6 +222,7 @@ def main():
                 else "hipEvents around each launch"}
 
     dropin = dropin_leg(args, scene, dev) if args.dropin == "on" else None
+    fisher = fisher_leg(args, scene, dev) if args.fisher == "on" else None
 
     # ---- CPU baseline: the float32 C oracle on one frame (rank 0, N=1) ------
     cpu = None
@@ -290,6 +294,7 @@ def main():
             "cpu_baseline": cpu,
             "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items()},
             "dropin": dropin,
+            "fisher": fisher,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -350,6 +355,50 @@ def dropin_leg(args, scene, dev, iters_per_frame: int = 40):
                            "alg_bytes_per_launch": int(alg),
                            "frac": round(alg / (rb["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 5) if rb["avg_us"] else None},
             "stages_us": {k: round(v["avg_us"], 2) for k, v in st.items()}}
+
+
+def fisher_leg(args, scene, dev, launches: int = 6):
+    """Fisher / EIG view scoring (scripts/ros_handler.py:807-902) on the bench map:
+    the visited-pose Hessian sum H = sum_k [dL/dmeans_cam, dL/dopacity] of backward_power=2 renders seeded
+    with 1e-3, K poses per HIP-graph launch (fisher.BatchedFisher), against the per-pose eager path."""
+    import math
+    from splatam_amd.fisher import BatchedFisher, FisherScorer
+    from splatam_amd.slam import camera_settings, init_tracking_params
+    params = init_tracking_params(scene, num_frames=1, device=dev)
+    cam = camera_settings(scene.cam, dev)
+    sc = FisherScorer(params, cam)
+    K = max(1, args.fisher_k)
+
+    def pose(k):  # a ring of views around the frame's camera: 0.5 deg yaw steps, 1 cm translations
+        a = math.radians(0.5 * (k - K / 2))
+        w = torch.eye(4, device=dev)
+        w[0, 0], w[0, 2], w[2, 0], w[2, 2] = math.cos(a), math.sin(a), -math.sin(a), math.cos(a)
+        w[:3, 3] = torch.tensor([0.01 * math.sin(k), 0.01 * math.cos(k), 0.0], device=dev)
+        return w
+
+    poses = [pose(k) for k in range(K)]
+    bf = BatchedFisher(sc, K, mode="sum", probe_w2cs=poses)
+    bf.hessian_sum(poses)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(launches):
+        bf.hessian_sum(poses)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if bf.overflowed():
+        return {"error": "binning capacity overflow"}
+    sc.hessian(poses[0])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for w in poses[:4]:
+        sc.hessian(w)
+    torch.cuda.synchronize()
+    de = (time.perf_counter() - t1) / 4
+    return {"value": round(K * launches / dt, 2), "unit": "poses/s", "poses_per_launch": K,
+            "ms_per_pose": round(1000 * dt / (K * launches), 4), "eager_ms_per_pose": round(1000 * de, 4),
+            "workload": f"H_train of {K} visited poses per HIP-graph launch over the {scene.P}-Gaussian "
+                        f"{scene.cam.W}x{scene.cam.H} map: static forward + backward_power=2 per pose, "
+                        "H accumulated on the device"}
 
 
 def render_bwd_roofline(rb, I_avg, P, W, H, graph: bool):

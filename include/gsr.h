@@ -150,6 +150,14 @@ int gsr_forward_dual_static(const gsr_settings* settings, const gsr_gaussians* g
                             float* out_color, float* out_color2, float* out_depth, int* radii,
                             gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
+/* Static-capacity, synchronisation-free gsr_forward (one colour set): the
+ * gsr_forward_dual_static contract (capacity, sticky status row, returns
+ * `capacity` for gsr_backward's num_rendered) for a single render -- e.g. the
+ * HIP-graph-captured Fisher scoring of a batch of poses (backward_power 2). */
+int gsr_forward_static(const gsr_settings* settings, const gsr_gaussians* gaussians, int capacity,
+                       unsigned* status, float* out_color, float* out_depth, int* radii,
+                       gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
 /* Backward of gsr_forward_dual (power 1): every geometric gradient in `grads`
  * is the sum of the two renders' (as autograd would accumulate it over two
  * calls), grads->dcolors is d/dcolors of the first set and dcolors2 [P,3]

@@ -95,10 +95,12 @@ def _gaussians(means3D, sh, colors, opacity, scales, rotations, cov3D_precomp, d
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                        prefiltered):
+                        prefiltered, capacity=0, status=None):
     """RasterizeGaussiansCUDA (rasterize_points.cu:35-115).
 
     Returns (num_rendered, color[3,H,W], radii[P] int32, geomBuffer, binningBuffer, imgBuffer, depth[1,H,W]).
+    capacity > 0 selects gsr_forward_static (no host synchronisation, HIP-graph capturable; `status` is a
+    device int32[4] receiving the sticky counters, and num_rendered is the capacity).
     """
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
@@ -121,8 +123,15 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         out_depth = torch.empty(1, H, W, **f32)
         radii = torch.empty(P, dtype=torch.int32, device=device)
         _begin(device)
-        n = lib.gsr_forward(ctypes.byref(s), ctypes.byref(g), out_color.data_ptr(), out_depth.data_ptr(),
-                            radii.data_ptr(), _ALLOC_CB, None, _stream(device))
+        if capacity > 0:
+            if status is None or status.device != device or status.numel() < 4:
+                raise RuntimeError("static forward needs a device status tensor of 4 int32")
+            n = lib.gsr_forward_static(ctypes.byref(s), ctypes.byref(g), int(capacity), status.data_ptr(),
+                                       out_color.data_ptr(), out_depth.data_ptr(), radii.data_ptr(), _ALLOC_CB, None,
+                                       _stream(device))
+        else:
+            n = lib.gsr_forward(ctypes.byref(s), ctypes.byref(g), out_color.data_ptr(), out_depth.data_ptr(),
+                                radii.data_ptr(), _ALLOC_CB, None, _stream(device))
         _check(n, "rasterize_gaussians")
         bufs = _tls.buffers
         return (int(n), out_color, radii, bufs[0], bufs[1], bufs[2], out_depth)

@@ -63,6 +63,8 @@ SIGNATURES = {
                              c_void_p]),
     "gsr_forward_dual": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p, ALLOC_FN, c_void_p, c_void_p]),
+    "gsr_forward_static": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_int, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, ALLOC_FN, c_void_p, c_void_p]),
     "gsr_forward_dual_static": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p, c_int,
                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ALLOC_FN, c_void_p,
                                         c_void_p]),

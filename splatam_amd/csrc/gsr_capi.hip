@@ -757,6 +757,14 @@ int gsr_forward_dual(const gsr_settings* settings, const gsr_gaussians* gaussian
                         stream);
 }
 
+int gsr_forward_static(const gsr_settings* settings, const gsr_gaussians* gaussians, int capacity, unsigned* status,
+                       float* out_color, float* out_depth, int* radii, gsr_alloc_fn alloc, void* alloc_ctx,
+                       void* stream) {
+    if (capacity <= 0 || !status) return fail(GSR_ERR_INVALID_ARG, "static mode needs capacity > 0 and status");
+    return forward_impl(settings, gaussians, nullptr, out_color, nullptr, out_depth, radii, alloc, alloc_ctx, stream,
+                        capacity, status);
+}
+
 int gsr_forward_dual_static(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
                             int capacity, unsigned* status, float* out_color, float* out_color2, float* out_depth,
                             int* radii, gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {

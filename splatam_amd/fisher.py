@@ -20,6 +20,12 @@ the device and exchanged once with an all-gather.  Each pose's render +
 power-2 backward runs through the HIP rasterizer (gsr_forward / gsr_backward
 with power = 2: gauss_jac, render_bwd_power, gauss_bwd_power) and only the two
 gradients H needs are requested.
+
+BatchedFisher renders a batch of K poses per host launch: the K transforms, static-
+capacity forwards (gsr_forward_static), power-2 backwards and the per-pose reductions
+(H accumulation for the visited poses, or the EIG score of each candidate) are captured
+once into a HIP graph and replayed with the poses written into a device [K,4,4] tensor.
+Every pose's Hessian is bitwise the per-pose FisherScorer.hessian's.
 """
 from __future__ import annotations
 
@@ -32,6 +38,13 @@ from .rasterizer import GaussianRasterizer
 
 SEED = 1e-3      # im.backward(gradient=torch.ones_like(im) * 1e-3)  (ros_handler.py:888)
 H_EPS = 0.1      # torch.reciprocal(H_train + 0.1)                   (ros_handler.py:829)
+
+
+def camera_points(means: torch.Tensor, w2c: torch.Tensor) -> torch.Tensor:
+    """(rel_w2c @ pts4.T).T[:, :3] (ros_handler.py:863-866) as means @ R^T + t: the same values up to
+    float32 rounding, without the K=P product of the homogeneous form; shared by the per-pose and the
+    batched paths, so both see bitwise the same camera-frame points."""
+    return torch.addmm(w2c[:3, 3], means, w2c[:3, :3].t()).contiguous()
 
 
 class FisherScorer:
@@ -56,9 +69,8 @@ class FisherScorer:
             return self._hessian_fn(w2c)
         means = self.params["means3D"].detach()
         w2c = w2c.to(means.device).float()
-        with torch.no_grad():  # (rel_w2c @ pts4.T).T[:, :3]
-            pts4 = torch.cat((means, torch.ones(means.shape[0], 1, device=means.device)), dim=1)
-            pts = (w2c @ pts4.T).T[:, :3].contiguous()
+        with torch.no_grad():
+            pts = camera_points(means, w2c)
         pts.requires_grad_(True)
         opac = self.opacities.detach().clone().requires_grad_(True)
         means2D = torch.zeros_like(pts)
@@ -68,13 +80,19 @@ class FisherScorer:
         im.backward(gradient=torch.full_like(im, SEED))
         return torch.cat([pts.grad.reshape(pts.shape[0], -1), opac.grad.reshape(pts.shape[0], -1)], dim=1)
 
-    def fit_visited(self, w2cs) -> torch.Tensor:
+    def fit_visited(self, w2cs, batch: "BatchedFisher | None" = None) -> torch.Tensor:
         """compute_H_visited_inv over all visited poses: each rank sums the Hessians of its shard
-        (poses r, r+W, ...), one all-reduce merges them.  Returns (and keeps) H_train_inv."""
+        (poses r, r+W, ...), one all-reduce merges them.  Returns (and keeps) H_train_inv.
+        batch: a BatchedFisher(mode="sum") -- the shard is rendered K poses per graph launch."""
         r, w = sd.world()
         H = None
-        for j in range(r, len(w2cs), w):
-            h = self.hessian(w2cs[j])
+        mine = [w2cs[j] for j in range(r, len(w2cs), w)]
+        if batch is not None:
+            for c in range(0, len(mine), batch.K):
+                h = batch.hessian_sum(mine[c:c + batch.K])
+                H = h.clone() if H is None else H + h
+        for w2c in ([] if batch is not None else mine):
+            h = self.hessian(w2c)
             H = h if H is None else H + h
         if H is None:  # this rank has no pose: contribute zeros of the right shape
             P = self.params["means3D"].shape[0]
@@ -83,9 +101,10 @@ class FisherScorer:
         self.H_train_inv = torch.reciprocal(H + H_EPS)
         return self.H_train_inv
 
-    def eig_scores(self, w2cs) -> torch.Tensor:
+    def eig_scores(self, w2cs, batch: "BatchedFisher | None" = None) -> torch.Tensor:
         """compute_eig_score for every candidate pose: sum(H(pose) * H_train_inv).  The batch is
-        sharded over ranks; returns all scores (float64, in pose order) on every rank."""
+        sharded over ranks; returns all scores (float64, in pose order) on every rank.
+        batch: a BatchedFisher(mode="scores") -- K candidate poses per graph launch."""
         if self.H_train_inv is None:
             raise RuntimeError("fit_visited() first (H_train_inv)")
         r, w = sd.world()
@@ -93,7 +112,12 @@ class FisherScorer:
         per = -(-n // w) if n else 0
         dev = self.H_train_inv.device
         local = torch.zeros(max(per, 1), dtype=torch.float64, device=dev)
-        for k, j in enumerate(range(r, n, w)):
+        mine = list(range(r, n, w))
+        if batch is not None:
+            for c in range(0, len(mine), batch.K):
+                idx = mine[c:c + batch.K]
+                local[c:c + len(idx)] = batch.scores([w2cs[j] for j in idx], self.H_train_inv)
+        for k, j in enumerate([] if batch is not None else mine):
             local[k] = (self.hessian(w2cs[j]) * self.H_train_inv).sum().double()
         if w == 1:
             return local[:n]
@@ -104,3 +128,112 @@ class FisherScorer:
             idx = list(range(rr, n, w))
             out[idx] = gathered[rr][:len(idx)]
         return out
+
+
+class BatchedFisher:
+    """K poses of FisherScorer's Hessian per HIP-graph launch.
+
+    mode "sum": `hessian_sum(w2cs)` returns sum_k H(w2c_k) (compute_H_visited_inv's H_train before the
+    all-reduce); mode "scores": `scores(w2cs, H_inv)` returns [sum(H(w2c_k) * H_inv) for k] (float64 like
+    FisherScorer.eig_scores).  Fewer than K poses pad the batch with weight-0 slots.  The binning capacity
+    comes from eager probes of `probe_w2cs` times `headroom`; `overflowed()` reports (sticky) whether a
+    replay exceeded it (results then invalid: rebuild with more headroom)."""
+
+    def __init__(self, scorer: FisherScorer, K: int, mode: str = "sum", probe_w2cs=None, headroom: float = 1.5,
+                 min_extra: int = 65536):
+        from . import _C
+        if scorer._hessian_fn is not None:
+            raise RuntimeError("BatchedFisher renders through the rasterizer (no hessian_fn override)")
+        if mode not in ("sum", "scores"):
+            raise ValueError("mode is 'sum' or 'scores'")
+        self.sc, self.K, self.mode = scorer, int(K), mode
+        cam = scorer.cam
+        means = scorer.params["means3D"].detach().contiguous()
+        dev = means.device
+        self.means = means
+        P = means.shape[0]
+        self.w2c = torch.eye(4, device=dev).repeat(self.K, 1, 1).contiguous()
+        self.weight = torch.zeros(self.K, device=dev)
+        self.H_inv = torch.zeros(P, 4, device=dev)
+        self.status = torch.zeros(self.K, 4, dtype=torch.int32, device=dev)
+        self.seed = torch.full((3, cam.image_height, cam.image_width), SEED, device=dev)  # ros_handler.py:888
+        self.e = torch.Tensor([])
+        probes = list(probe_w2cs) if probe_w2cs is not None else [torch.eye(4, device=dev)]
+        n = 0
+        with torch.no_grad():
+            for w in probes:
+                pts = camera_points(means, w.to(dev).float())
+                n = max(n, self._forward(_C, pts, 0)[0])
+        self.capacity = max(1, int(headroom * n) + int(min_extra))
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            self._body(_C)  # warm-up (allocator pools, kernels) outside the capture
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        self.status.zero_()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=side):
+            self._body(_C)
+
+    def _forward(self, _C, pts, capacity):
+        sc, cam = self.sc, self.sc.cam
+        return _C.rasterize_gaussians(cam.bg, pts, sc.colors.detach(), sc.opacities.detach(), sc.scales.detach(),
+                                      sc.rotations.detach(), cam.scale_modifier, self.e, cam.viewmatrix,
+                                      cam.projmatrix, cam.tanfovx, cam.tanfovy, cam.image_height, cam.image_width,
+                                      self.e, cam.sh_degree, cam.campos, cam.prefiltered, capacity=capacity,
+                                      status=self.status[self._k] if capacity else None)
+
+    def _hessian(self, _C, k):
+        sc, cam = self.sc, self.sc.cam
+        self._k = k
+        pts = camera_points(self.means, self.w2c[k])
+        n, color, radii, geom, binning, img, depth = self._forward(_C, pts, self.capacity)
+        g = _C.rasterize_gaussians_backward(cam.bg, pts, radii, sc.colors.detach(), sc.scales.detach(),
+                                            sc.rotations.detach(), cam.scale_modifier, self.e, cam.viewmatrix,
+                                            cam.projmatrix, cam.tanfovx, cam.tanfovy, self.seed, self.e,
+                                            cam.sh_degree, cam.campos, geom, n, binning, img, 2)
+        return torch.cat([g[3].reshape(pts.shape[0], -1), g[2].reshape(pts.shape[0], -1)], dim=1)
+
+    def _body(self, _C):
+        self._k = 0
+        with torch.no_grad():
+            if self.mode == "sum":
+                self.out = torch.zeros_like(self.H_inv)
+                for k in range(self.K):
+                    self.out.add_(self._hessian(_C, k) * self.weight[k])
+            else:
+                self.out = torch.zeros(self.K, dtype=torch.float32, device=self.H_inv.device)
+                for k in range(self.K):
+                    self.out[k] = (self._hessian(_C, k) * self.H_inv).sum()
+
+    def _load(self, w2cs):
+        if len(w2cs) > self.K:
+            raise ValueError(f"at most {self.K} poses per launch")
+        with torch.no_grad():
+            self.weight.zero_()
+            for k, w in enumerate(w2cs):
+                self.w2c[k].copy_(w)
+                self.weight[k] = 1.0
+
+    def hessian_sum(self, w2cs) -> torch.Tensor:
+        """sum over the (<= K) poses of H(w2c) [P,4] (one graph launch)."""
+        if self.mode != "sum":
+            raise RuntimeError("built for mode='scores'")
+        self._load(w2cs)
+        self.graph.replay()
+        return self.out
+
+    def scores(self, w2cs, H_inv) -> torch.Tensor:
+        """sum(H(w2c_k) * H_inv) for each of the (<= K) poses, float64 (one graph launch)."""
+        if self.mode != "scores":
+            raise RuntimeError("built for mode='sum'")
+        self._load(w2cs)
+        with torch.no_grad():
+            self.H_inv.copy_(H_inv)
+        self.graph.replay()
+        return self.out[:len(w2cs)].double()
+
+    def overflowed(self) -> bool:
+        st = self.status.cpu()
+        return bool((st[:, 0] > self.capacity).any() or (st[:, 2] > st[:, 3]).any() or (st[:, 1] != 0).any())

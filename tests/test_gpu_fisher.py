@@ -47,3 +47,31 @@ def test_fisher_hessian_matches_oracle(cuda, aniso):
     hinv = sc.fit_visited([w2c.to(cuda), torch.eye(4, device=cuda)])
     s = sc.eig_scores([w2c.to(cuda)])
     torch.testing.assert_close(s[0], (torch.tensor(H, device=cuda) * hinv).sum().double(), rtol=1e-6, atol=0)
+
+
+def test_batched_fisher_matches_per_pose(cuda):
+    """BatchedFisher (K poses per HIP-graph launch, static forwards, power-2 backwards) gives bitwise the
+    per-pose FisherScorer Hessians: their sum over visited poses (incl. a partial batch) and the EIG score
+    of every candidate."""
+    from splatam_amd.fisher import BatchedFisher
+    scene = make_scene(3000, 96, 72, seed=22)
+    params = init_tracking_params(scene, num_frames=1, device=cuda)
+    cam = camera_settings(scene.cam, cuda)
+    sc = FisherScorer(params, cam)
+    poses = [_pose(d, [0.01 * d, -0.005 * d, 0.02]).to(cuda) for d in (-4.0, -2.0, 0.0, 1.5, 3.0)]
+    K = 3
+    bs = BatchedFisher(sc, K, mode="sum", probe_w2cs=poses)
+    ref = [sc.hessian(w) for w in poses]
+    got = bs.hessian_sum(poses[:3]).clone()
+    assert torch.equal(got, (ref[0] + ref[1]) + ref[2])
+    got2 = bs.hessian_sum(poses[3:])  # partial batch: the third slot has weight 0
+    assert torch.equal(got2, ref[3] + ref[4])
+    torch.cuda.synchronize()
+    assert not bs.overflowed()
+    hinv = sc.fit_visited(poses)
+    hinv_b = sc.fit_visited(poses, batch=bs)
+    torch.testing.assert_close(hinv_b, hinv, rtol=1e-6, atol=0)  # chunked sum order differs
+    bsc = BatchedFisher(sc, K, mode="scores", probe_w2cs=poses)
+    s_ref = sc.eig_scores(poses)
+    s_b = sc.eig_scores(poses, batch=bsc)
+    assert torch.equal(s_b, s_ref)
