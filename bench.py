@@ -337,6 +337,34 @@ def dropin_leg(args, scene, dev, iters_per_frame: int = 40):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     iters = (nf - 1) * iters_per_frame
+    # SURVEY 8(d)'s unit on its own: 2 x (GaussianRasterizer(...) + backward) from Python, eager, every
+    # rasterizer input a leaf requiring grad, no caller glue (the rest of the loop body above is caller code)
+    with torch.no_grad():
+        tg = transform_to_frame(params, 0, False, False)
+        rv1 = transformed_params2rendervar(params, tg)
+        rv2 = transformed_params2depthplussilhouette(params, w2c, tg)
+    leaf = lambda d: {k: v.detach().clone().requires_grad_(True) for k, v in d.items()}  # noqa: E731
+    rv1, rv2 = leaf(rv1), leaf(rv2)
+    g1 = torch.randn(3, H, W, device=dev)
+    g2 = torch.randn(3, H, W, device=dev)
+
+    def unit():
+        for d in (rv1, rv2):
+            for v in d.values():
+                v.grad = None
+        im_, _, _ = R(cam)(**rv1)
+        ds_, _, _ = R(cam)(**rv2)
+        ((im_ * g1).sum() + (ds_ * g2).sum()).backward()
+
+    for _ in range(5):
+        unit()
+    torch.cuda.synchronize()
+    nu = 60
+    t1 = time.perf_counter()
+    for _ in range(nu):
+        unit()
+    torch.cuda.synchronize()
+    du = (time.perf_counter() - t1) / nu
     profiling.enable_timing(True)  # separate pass: hipEvents around every stage
     track_frame_literal(params, variables, curr, 0, 10, renderer=R)
     torch.cuda.synchronize()
@@ -354,7 +382,11 @@ def dropin_leg(args, scene, dev, iters_per_frame: int = 40):
             "render_bwd": {"avg_us": round(rb["avg_us"], 2), "launches_per_step": 2,
                            "alg_bytes_per_launch": int(alg),
                            "frac": round(alg / (rb["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 5) if rb["avg_us"] else None},
-            "stages_us": {k: round(v["avg_us"], 2) for k, v in st.items()}}
+            "stages_us": {k: round(v["avg_us"], 2) for k, v in st.items()},
+            "raster_unit": {"value": round(1.0 / du, 3), "unit": "frames/s", "ms_per_step": round(1000 * du, 4),
+                            "path": "SURVEY 8(d) unit alone: 2x diff_gaussian_rasterization.GaussianRasterizer "
+                                    "(RGB, depth/silhouette) + backward from Python, eager, every input a leaf "
+                                    "requiring grad; the difference to ms_per_step is the caller's torch glue"}}
 
 
 def fisher_leg(args, scene, dev, launches: int = 6):

@@ -139,19 +139,22 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree,
-                                 campos, geomBuffer, R, binningBuffer, imageBuffer, power=1):
+                                 campos, geomBuffer, R, binningBuffer, imageBuffer, power=1, needs=None):
     """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:117-196).
 
     Returns (dmeans2D[P,3], dcolors[P,3], dopacity[P,1], dmeans3D[P,3], dcov3D[P,6], dsh[P,M,3],
-    dscales[P,3], drotations[P,4]).
+    dscales[P,3], drotations[P,4]).  `needs` (8 bools in that order, power == 1 only) skips the
+    gradients nobody wants: they come back as None and their per-pair sums are not formed.
     """
     device = means3D.device
     P = means3D.size(0)
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     M = sh.size(1) if (sh is not None and sh.numel() > 0 and sh.size(0) != 0) else 0
     f32 = dict(dtype=torch.float32, device=device)
-    out = [torch.empty(P, 3, **f32), torch.empty(P, 3, **f32), torch.empty(P, 1, **f32), torch.empty(P, 3, **f32),
-           torch.empty(P, 6, **f32), torch.empty(P, M, 3, **f32), torch.empty(P, 3, **f32), torch.empty(P, 4, **f32)]
+    needs = [True] * 8 if (needs is None or int(power) != 1) else list(needs)
+    needs[3] = True  # dmeans3D is always produced
+    shapes = [(P, 3), (P, 3), (P, 1), (P, 3), (P, 6), (P, M, 3), (P, 3), (P, 4)]
+    out = [torch.empty(*sh_, **f32) if nd else None for sh_, nd in zip(shapes, needs)]
     if P == 0:
         return tuple(out)
     with torch.cuda.device(device):
@@ -161,7 +164,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         g, keep_g, _ = _gaussians(means3D, sh, colors, None, scales, rotations, cov3D_precomp, device)
         dpix = _dev_f32(dL_dout_color, device, "dL_dout_color")
         radii_c = radii.to(device=device, dtype=torch.int32).contiguous()
-        grads = GsrGrads(*[o.data_ptr() if o.numel() > 0 else None for o in out])
+        grads = GsrGrads(*[o.data_ptr() if (o is not None and o.numel() > 0) else None for o in out])
         _begin(device)
         rc = lib.gsr_backward(ctypes.byref(s), ctypes.byref(g), radii_c.data_ptr(), dpix.data_ptr(), int(R),
                               geomBuffer.data_ptr(), binningBuffer.data_ptr() if binningBuffer.numel() else None,

@@ -81,5 +81,22 @@ def build_diag() -> str:
     return lib
 
 
+def build_variant(tag: str, defines=()) -> str:
+    """Timing-experiment library (tools/ablate.sh): libgsr built with extra -D flags into
+    splatam_amd/_build_<tag>/libgsr_<tag>.so; loaded only through GSR_LIB."""
+    objdir = os.path.join(HERE, f"_build_{tag}")
+    os.makedirs(objdir, exist_ok=True)
+    extra = tuple(f"-D{d}" for d in defines)
+    with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, objdir, extra), SOURCES))
+    lib = os.path.join(objdir, f"libgsr_{tag}.so")
+    if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in objs):
+        r = subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    return lib
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv))

@@ -73,8 +73,11 @@ __device__ __forceinline__ void reduce_store(const float (&v)[4 * N], int lane, 
 }
 
 // Gaussians staged per batch: the per-row partial sums take 16 x batch x NV floats of LDS
+#ifndef GSR_BWD_BB
+#define GSR_BWD_BB 64  // batch of the variants with <= 6 sums (timing experiments may override)
+#endif
 template <int NV>
-constexpr int bwd_batch() { return NV <= 6 ? 64 : 32; }
+constexpr int bwd_batch() { return NV <= 6 ? GSR_BWD_BB : 32; }
 
 // DUAL: the pass also carries a second colour set (colors2, dL_dpix2) composited
 // with the same alpha / T (one dual forward): the per-pair dL/dalpha is the sum
@@ -197,6 +200,11 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     float ablate_sink = 0.f;
 #endif
     const int my_e = row_entry(lane);
+    // Block slots start zero; after every batch the entry totals re-zero exactly the slots they read
+    // (the ones a row list can have written: the entry's mask blocks), and the pad entry's slots
+    // only ever receive zeros, so no per-batch clear is needed.
+    for (int q = tid; q < 16 * SL * NV / 4; q += TILE_PIX)
+        reinterpret_cast<float4*>(s_acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     float* acc_row = s_acc + (4 * w + row) * SL * NV;
     const uint16_t* my_list = s_list + (4 * w + row) * LS;
     if (tid == 0) {
@@ -234,8 +242,6 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             if (DUAL) s_d[tid] = pd;
             s_mask[tid] = (uint16_t)pm;  // the instance's exact 4x4-block mask (sorted list entry)
         }
-        for (int q = tid; q < 16 * SL * NV / 4; q += TILE_PIX)
-            reinterpret_cast<float4*>(s_acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         __syncthreads();
         fetch(hi - BB);  // prefetch the next batch
         // entries j with pos = hi-1-j >= rmax lie behind every pixel of the block
@@ -331,22 +337,33 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             }
         }
         __syncthreads();
-        if (tid < cnt) {
-            float c[NV];
+        // Entry totals: TPE threads per entry, thread q of an entry owns values m = q, q + TPE, ...
+        // and adds the entry's block slots in ascending block order (deterministic), visiting only
+        // the blocks of its mask; the TPE threads store adjacent floats of the packed record.
+        constexpr int TPE = TILE_PIX / BB, NQ = (RS + TPE - 1) / TPE;
+        int t_ = tid;
+        asm volatile("" : "+v"(t_));  // addresses formed here, not hoisted across the batch loop (VGPRs)
+        const int e = t_ / TPE, q = t_ % TPE;
+        if (GSR_ABLATE != 2 && e < cnt) {
+            float c[NQ];
 #pragma unroll
-            for (int m = 0; m < NV; m++) c[m] = 0.f;
-            const uint32_t mask = s_mask[tid];
-            for (int b = 0; b < 16; b++) {  // fixed block order: deterministic
-                if (!((mask >> b) & 1u)) continue;
-                const float* src = s_acc + (b * SL + tid) * NV;
+            for (int i = 0; i < NQ; i++) c[i] = 0.f;
+            uint32_t mm = s_mask[e];
+            while (mm) {
+                const int b = __builtin_ctz(mm);
+                mm &= mm - 1u;
+                float* src = s_acc + (b * SL + e) * NV;
 #pragma unroll
-                for (int m = 0; m < NV; m++) c[m] += src[m];
+                for (int i = 0; i < NQ; i++)
+                    if (q + TPE * i < NV) {
+                        c[i] += src[q + TPE * i];
+                        src[q + TPE * i] = 0.f;
+                    }
             }
-            const uint32_t u = s_u[tid];  // packed record (RecLayout): the NV sums, zero pad
-            float2* dst = reinterpret_cast<float2*>(inst + (size_t)RS * u);
+            float* dst = inst + (size_t)RS * s_u[e];  // packed record (RecLayout): the NV sums, zero pad
 #pragma unroll
-            for (int m = 0; m < RS / 2; m++)
-                dst[m] = make_float2(2 * m < NV ? c[2 * m] : 0.f, 2 * m + 1 < NV ? c[2 * m + 1] : 0.f);
+            for (int i = 0; i < NQ; i++)
+                if (q + TPE * i < RS) dst[q + TPE * i] = c[i];
         }
         __syncthreads();
     }

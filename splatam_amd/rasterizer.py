@@ -62,11 +62,17 @@ class _RasterizeGaussians(torch.autograd.Function):
         s = ctx.raster_settings
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer,
          imgBuffer) = ctx.saved_tensors
+        # inputs: (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, ...);
+        # outputs of the binding: (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drotations)
+        n = ctx.needs_input_grad
+        needs = (n[1], n[3], n[4], True, n[7], n[2], n[5], n[6])
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh, grad_scales,
          grad_rotations) = _C.rasterize_gaussians_backward(
             s.bg, means3D, radii, colors_precomp, scales, rotations, s.scale_modifier, cov3Ds_precomp, s.viewmatrix,
             s.projmatrix, s.tanfovx, s.tanfovy, grad_out_color, sh, s.sh_degree, s.campos, geomBuffer,
-            ctx.num_rendered, binningBuffer, imgBuffer, ctx.backward_power)
+            ctx.num_rendered, binningBuffer, imgBuffer, ctx.backward_power, needs=needs)
+        if not n[0]:
+            grad_means3D = None
         return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales, grad_rotations,
                 grad_cov3Ds_precomp, None, None)
 

@@ -80,7 +80,7 @@ class RecordingC:
         u8 = torch.zeros(16, dtype=torch.uint8)
         return (7, torch.zeros(3, H, W), torch.zeros(P, dtype=torch.int32), u8, u8, u8, torch.zeros(1, H, W))
 
-    def rasterize_gaussians_backward(self, *args):
+    def rasterize_gaussians_backward(self, *args, needs=None):  # `needs`: keyword-only extension
         self.calls.append(("rasterize_gaussians_backward", [_describe(a) for a in args]))
         P = args[1].shape[0]
         M = args[13].shape[1] if args[13].numel() else 0

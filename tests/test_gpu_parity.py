@@ -275,6 +275,30 @@ def test_dual_render_skips_unneeded_gradients(cuda):
     assert res[1][2] is None
 
 
+def test_single_render_skips_unneeded_gradients(cuda):
+    """GaussianRasterizer forms only the gradients autograd asks for (ctx.needs_input_grad):
+    with only means3D / colors requiring grad, their gradients are bitwise those of the
+    all-inputs call and the other inputs receive None."""
+    from splatam_amd.rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+    scene = make_scene(3000, 128, 96, seed=31, anisotropic=True)
+    c = scene.cam
+    st = GaussianRasterizationSettings(96, 128, c.tanfovx, c.tanfovy, torch.zeros(3, device=cuda), 1.0,
+                                       c.viewmatrix.to(cuda), c.projmatrix.to(cuda), 0, c.campos.to(cuda), False)
+    g1 = torch.as_tensor(np.random.RandomState(9).randn(3, 96, 128).astype(np.float32), device=cuda)
+    res = []
+    for lean in (False, True):
+        t = lambda x, rg: x.detach().to(cuda).clone().requires_grad_(rg)  # noqa: E731
+        m3, col = t(scene.means3D, True), t(scene.colors, True)
+        op, sc, ro = t(scene.opacities, not lean), t(scene.scales, not lean), t(scene.rotations, not lean)
+        m2 = torch.zeros_like(m3, requires_grad=not lean)
+        im, _, _ = GaussianRasterizer(st)(means3D=m3, means2D=m2, opacities=op, colors_precomp=col, scales=sc,
+                                          rotations=ro)
+        (im * g1).sum().backward()
+        res.append((m3.grad.cpu(), col.grad.cpu(), op.grad, sc.grad, ro.grad, m2.grad))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert all(g is not None for g in res[0][2:]) and all(g is None for g in res[1][2:])
+
+
 def test_dual_render_depth_channel_only_gradient(cuda):
     """grad2_channels=1 (SplaTAM tracking: the loss reads only the depth channel
     of the depth/silhouette render) matches the 3-channel backward when the
