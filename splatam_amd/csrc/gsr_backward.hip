@@ -109,8 +109,11 @@ constexpr int bwd_nv() { return 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2
 // 5 waves per SIMD (96 VGPRs; the wide variants reduce in two passes to fit), except
 // the dual variants with a 3-channel second gradient (mapping-style), which spill
 // at 96 VGPRs and run at 4
+#ifndef GSR_BWD_WIDE_WAVES
+#define GSR_BWD_WIDE_WAVES 5
+#endif
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2>
-constexpr int bwd_waves() { return (DUAL && Q2 == 3) ? 4 : 5; }
+constexpr int bwd_waves() { return (DUAL && Q2 == 3) ? 4 : ((OPAC && COL1) ? GSR_BWD_WIDE_WAVES : 5); }
 
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3>
 __global__ void __launch_bounds__(TILE_PIX, (bwd_waves<DUAL, OPAC, COL1, COL2, Q2>()))
@@ -214,28 +217,37 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         s_c[BB] = z;
         if (DUAL) s_d[BB] = z;
     }
-    // Batch staging: thread t < batch holds entry t's render record (already in its
-    // LDS form) for the next batch while the current one is rasterised.
+    // Batch staging, software-pipelined two batches deep: thread t < batch holds entry t's
+    // render record (already in its LDS form) and block-sum word for the next batch, and the
+    // sorted list entry for the batch after it, so neither dependent load (list entry ->
+    // record) is waited on while a batch is rasterised; the instance slot is formed at staging.
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
-    uint32_t pu = 0, pm = 0;
-    auto fetch = [&](int hi_) {
+    uint32_t pbs = 0, pm = 0, prh = 0;  // prh: tile-rect hi (q3.w) when q3 is not staged
+    PointEntry pn = 0;
+    auto fetch_entry = [&](int hi_) {
+        if (tid < min(BB, hi_)) pn = point_list[range.x + (uint32_t)(hi_ - 1 - tid)];
+    };
+    auto fetch_rec = [&](int hi_) {
         if (tid < min(BB, hi_)) {
-            const PointEntry pe = point_list[range.x + (uint32_t)(hi_ - 1 - tid)];
-            const uint32_t gi = pe_id(pe);
-            pm = pe_mask(pe);
+            const uint32_t gi = pe_id(pn);
+            pm = pe_mask(pn);
             const RenderRec r = load_rr(rr, gi);
-            pu = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), tx, ty);
+            pbs = blocksums[gi / PRE_BLOCK];
             pa = r.q0; pb = r.q1; pc = r.q2;
             if (DUAL) pd = r.q3;
+            else prh = __float_as_uint(r.q3.w);
         }
     };
-    fetch((int)bmax);
+    fetch_entry((int)bmax);
+    fetch_rec((int)bmax);
+    fetch_entry((int)bmax - BB);
     const uint32_t mean4 = sched_mean4(cam, guard.counters);
     for (int hi = (int)bmax; hi > 0; hi -= BB) {
         prio_by_remaining(hi, mean4);
         const int cnt = min(BB, hi);
         if (tid < cnt) {
-            s_u[tid] = pu;
+            s_u[tid] = instance_slot(make_uint2(__float_as_uint(pc.w), DUAL ? __float_as_uint(pd.w) : prh),
+                                     pbs + __float_as_uint(pb.w), tx, ty);
             s_a[tid] = pa;
             s_b[tid] = pb;
             s_c[tid] = pc;
@@ -243,7 +255,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             s_mask[tid] = (uint16_t)pm;  // the instance's exact 4x4-block mask (sorted list entry)
         }
         __syncthreads();
-        fetch(hi - BB);  // prefetch the next batch
+        fetch_rec(hi - BB);        // records of the next batch (list entries loaded a batch ago)
+        fetch_entry(hi - 2 * BB);  // list entries of the batch after it
         // entries j with pos = hi-1-j >= rmax lie behind every pixel of the block
         const int jmin[4] = {hi - rm[0], hi - rm[1], hi - rm[2], hi - rm[3]};
         const int n = build_row_lists(s_mask, cnt, w, jmin, s_list + 4 * w * LS, LS, (uint16_t)BB);
