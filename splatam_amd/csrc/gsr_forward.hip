@@ -1015,7 +1015,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
     float C3 = 0.f, C4 = 0.f, C5 = 0.f;
     uint32_t last = 0;
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
-    uint32_t pm = 0, pg = 0;  // the staged entry's 4x4-block mask and Gaussian id
+    uint32_t pg = 0, pgn = 0;  // the staged entry's Gaussian id, the id of the entry a batch later
     if (keys != nullptr) {
         // the tile's bucket is sorted here; the sorted ids land in point_list and are read
         // back below by this same workgroup (guard: every list is <= TILE_SORT_CAP)
@@ -1029,19 +1029,30 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         s_c[RENDER_BATCH] = pa;
         if (DUAL) s_d[RENDER_BATCH] = pa;
     }
-    if (range.x + tid < range.y) {
-        pg = pe_id(point_list[range.x + tid]);
-        const RenderRec r = load_rr(rr, pg);
-        pa = r.q0; pb = r.q1; pc = r.q2;
-        if (DUAL) pd = r.q3;
-        pm = block_mask_exact(pa, pb, x0, y0);
-    }
+    // Batch staging pipelined two deep: the sorted id of an entry is loaded a batch before its
+    // render record, and the record's block mask is formed at staging, so no dependent load is
+    // waited on while a batch is rasterised.
+    auto fetch_id = [&](uint32_t s0) {
+        if (s0 + tid < range.y) pgn = pe_id(point_list[s0 + tid]);
+    };
+    auto fetch_rec = [&](uint32_t s0) {
+        if (s0 + tid < range.y) {
+            pg = pgn;
+            const RenderRec r = load_rr(rr, pg);
+            pa = r.q0; pb = r.q1; pc = r.q2;
+            if (DUAL) pd = r.q3;
+        }
+    };
+    fetch_id(range.x);
+    fetch_rec(range.x);
+    fetch_id(range.x + RENDER_BATCH);
     const uint32_t mean4 = sched_mean4(cam, guard.counters);
     for (uint32_t start = range.x; start < range.y; start += RENDER_BATCH) {
         prio_by_remaining((int)(range.y - start), mean4);
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
         const int cnt = (int)min((uint32_t)RENDER_BATCH, range.y - start);
         if (tid < cnt) {
+            const uint32_t pm = block_mask_exact(pa, pb, x0, y0);
             s_a[tid] = pa;
             s_b[tid] = pb;
             s_c[tid] = pc;
@@ -1050,16 +1061,8 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
             point_list[start + tid] = ((PointEntry)pm << 32) | pg;  // the mask, for render_bwd
         }
         __syncthreads();
-        {   // prefetch the next batch while this one is rasterised
-            const uint32_t k = start + RENDER_BATCH + tid;
-            if (k < range.y) {
-                pg = pe_id(point_list[k]);
-                const RenderRec r = load_rr(rr, pg);
-                pa = r.q0; pb = r.q1; pc = r.q2;
-                if (DUAL) pd = r.q3;
-                pm = block_mask_exact(pa, pb, x0, y0);
-            }
-        }
+        fetch_rec(start + RENDER_BATCH);      // records of the next batch (ids loaded a batch ago)
+        fetch_id(start + 2 * RENDER_BATCH);   // ids of the batch after it
         const int jmin0[4] = {0, 0, 0, 0};
         const int n = build_row_lists(s_mask, cnt, w, jmin0, s_list + 4 * w * LS, LS, (uint16_t)RENDER_BATCH);
         const uint16_t* my_list = s_list + (4 * w + row) * LS;
