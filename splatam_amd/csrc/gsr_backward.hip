@@ -25,6 +25,14 @@
 
 namespace gsr {
 GSR_WGTIME_TABLE
+#ifndef GSR_STEPSTAT
+#define GSR_STEPSTAT 0  // diagnostics build only (tools/stepstat.py): render_bwd step statistics
+#endif
+#if GSR_STEPSTAT
+// [wave-steps, wave-steps with a contributing pair, contributing (lane, entry) pairs, pad (lane, entry) slots,
+//  batches x waves]
+static __device__ unsigned long long g_stepstat[8];
+#endif
 
 // Per-pair geometric terms (hx, hy, hx dx, hx dy, hy dy[, G dL/dalpha]) with
 // h = G * dL/dG = (o * G) * dL/dalpha.
@@ -73,11 +81,73 @@ __device__ __forceinline__ void reduce_store(const float (&v)[4 * N], int lane, 
 }
 
 // Gaussians staged per batch: the per-row partial sums take 16 x batch x NV floats of LDS
+// Entries staged per batch, and the batch's budget of per-(entry, block) LDS slots: each entry
+// owns popcount(block mask) consecutive slots of NV floats (about 3 on average, at most 16), so a
+// batch of BB entries is cut short when its masks need more than BS slots.
 #ifndef GSR_BWD_BB
-#define GSR_BWD_BB 64  // batch of the variants with <= 6 sums (timing experiments may override)
+#define GSR_BWD_BB 128  // batch of the variants with <= 6 sums (timing experiments may override)
 #endif
 template <int NV>
-constexpr int bwd_batch() { return NV <= 6 ? GSR_BWD_BB : 32; }
+constexpr int bwd_batch() { return NV <= 6 ? GSR_BWD_BB : 64; }
+template <int NV>
+constexpr int bwd_slots() { return NV <= 6 ? 4 * GSR_BWD_BB : 256; }
+
+// Per-wave row lists of one batch: row r of wave w (tile block b = 4w + r) lists the entries j
+// (< cnt) whose block mask has bit b and that lie before the block's last contributor (j >=
+// jmin[r]), as (j | slot << 16) with slot = the entry's slot for block b; every wave also forms
+// the batch's slot bases (exclusive scan of the masks' popcounts, redundantly per wave) and
+// returns cnt = the longest prefix of the cmax staged entries whose slots fit in `budget`.
+// Lists are padded to a common multiple of 4 with `pad`.  Wave 0 publishes the bases.
+struct SlotLists {
+    int len, cnt;
+};
+__device__ __forceinline__ SlotLists build_row_slot_lists(const uint16_t* s_mask, uint16_t* s_base, int cmax,
+                                                         int budget, int w, const int (&jmin)[4], uint32_t* list,
+                                                         int stride, uint32_t pad) {
+    const int lane = __lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t below_w = (1u << (4 * w)) - 1u;  // blocks of the waves before this one
+    int n[4] = {0, 0, 0, 0};
+    uint32_t carry = 0;
+    int cnt = 0;
+    for (int c = 0; c < cmax; c += 64) {
+        const int j = c + lane;
+        const uint32_t mf = j < cmax ? (uint32_t)s_mask[j] : 0u;
+        const uint32_t pc = __popc(mf);
+        // inclusive prefix of the popcounts (0..16) bit by bit: ballots + mbcnt (no lane shuffles,
+        // whose hoisted address registers spilled), the chunk total from the ballots' popcounts
+        uint32_t incl = carry, tot = 0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const uint64_t bk = __ballot((pc >> k) & 1u);
+            incl += (uint32_t)__popcll(bk & (lt | (1ull << lane))) << k;
+            tot += (uint32_t)__popcll(bk) << k;
+        }
+        const uint32_t base = incl - pc;
+        const bool fits = j < cmax && incl <= (uint32_t)budget;
+        cnt += __popcll(__ballot(fits));
+        carry += tot;
+        if (w == 0 && fits) s_base[j] = (uint16_t)base;
+        const uint32_t m = (mf >> (4 * w)) & 0xFu;
+        const uint32_t sb = base + __popc(mf & below_w);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const bool bit = fits && ((m >> r) & 1u) && j >= jmin[r];
+            const uint64_t bal = __ballot(bit);
+            if (bit) list[r * stride + n[r] + __popcll(bal & lt)] = (uint32_t)j | ((sb + __popc(m & ((1u << r) - 1u))) << 16);
+            n[r] += __popcll(bal);
+        }
+    }
+    const int len = (max(max(n[0], n[1]), max(n[2], n[3])) + 3) & ~3;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+        for (int p = n[r] + lane; p < len; p += 64) list[r * stride + p] = pad;
+    return {len, cnt};
+}
+// Four consecutive (j | slot << 16) words of this lane's row list.
+__device__ __forceinline__ uint4 load_slot_group4(const uint32_t* row_list, int i) {
+    return *reinterpret_cast<const uint4*>(&row_list[i]);
+}
 
 // DUAL: the pass also carries a second colour set (colors2, dL_dpix2) composited
 // with the same alpha / T (one dual forward): the per-pair dL/dalpha is the sum
@@ -133,21 +203,22 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     static_assert(Q2 == 1 || Q2 == 3, "Q2 is 1 or 3 channels");
     constexpr int NV = bwd_nv<DUAL, OPAC, COL1, COL2, Q2>();
     constexpr int O_OP = 5, O_C1 = 5 + (OPAC ? 1 : 0), O_C2 = O_C1 + (COL1 ? 3 : 0);
-    constexpr int BB = bwd_batch<NV>();
+    constexpr int BB = bwd_batch<NV>(), BS = bwd_slots<NV>();
     constexpr int RS = (NV + 1) & ~1;  // record stride (floats)
-    constexpr int LS = BB + 4;  // row-list stride (u16)
-    // entry BB is a dummy (opacity 0, never blends) that pads the row lists; its
-    // per-block slots absorb the pad entries' (zero) sums
-    constexpr int SL = BB + 1;  // per-block slot count
+    constexpr int LS = BB + 4;  // row-list stride (u32)
+    // entry BB is a dummy (opacity 0, never blends) that pads the row lists; its slot BS
+    // absorbs the pad entries' (zero) sums
+    constexpr int SL = BB + 1;
     __shared__ float4 s_a[SL];
     __shared__ float4 s_b[SL];
     __shared__ float4 s_c[SL];
     __shared__ float4 s_d[DUAL ? SL : 1];
     __shared__ uint32_t s_u[BB];
     __shared__ uint16_t s_mask[BB];
-    __shared__ __attribute__((aligned(16))) float s_acc[16 * SL * NV];
+    __shared__ uint16_t s_base[BB];
+    __shared__ __attribute__((aligned(16))) float s_acc[(BS + 1) * NV];
     __shared__ uint32_t s_rmax[16];
-    __shared__ __attribute__((aligned(16))) uint16_t s_list[16 * LS];
+    __shared__ __attribute__((aligned(16))) uint32_t s_list[16 * LS];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, row = (tid >> 4) & 3;
     const int tile = sched_tile(cam), tx = tile % cam.gx, ty = tile / cam.gx;
     const int px = tx * TILE_X + tile_px(tid);
@@ -203,13 +274,11 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     float ablate_sink = 0.f;
 #endif
     const int my_e = row_entry(lane);
-    // Block slots start zero; after every batch the entry totals re-zero exactly the slots they read
-    // (the ones a row list can have written: the entry's mask blocks), and the pad entry's slots
-    // only ever receive zeros, so no per-batch clear is needed.
-    for (int q = tid; q < 16 * SL * NV / 4; q += TILE_PIX)
-        reinterpret_cast<float4*>(s_acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    float* acc_row = s_acc + (4 * w + row) * SL * NV;
-    const uint16_t* my_list = s_list + (4 * w + row) * LS;
+    // Slots start zero; after every batch the entry totals re-zero exactly the slots they read
+    // (every slot a row list can have written), and the pad slot only ever receives zeros, so no
+    // per-batch clear is needed.
+    for (int q = tid; q < (BS + 1) * NV; q += TILE_PIX) s_acc[q] = 0.f;
+    const uint32_t* my_list = s_list + (4 * w + row) * LS;
     if (tid == 0) {
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
         s_a[BB] = z;
@@ -238,31 +307,53 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             else prh = __float_as_uint(r.q3.w);
         }
     };
+#if GSR_STEPSTAT
+    unsigned long long st_steps = 0, st_csteps = 0, st_ok = 0, st_pads = 0, st_batches = 0;
+#endif
     fetch_entry((int)bmax);
     fetch_rec((int)bmax);
     fetch_entry((int)bmax - BB);
     const uint32_t mean4 = sched_mean4(cam, guard.counters);
-    for (int hi = (int)bmax; hi > 0; hi -= BB) {
+    int hi_pf = (int)bmax;  // the batch start the staged registers hold
+    for (int hi = (int)bmax; hi > 0;) {
         prio_by_remaining(hi, mean4);
-        const int cnt = min(BB, hi);
-        if (tid < cnt) {
-            s_u[tid] = instance_slot(make_uint2(__float_as_uint(pc.w), DUAL ? __float_as_uint(pd.w) : prh),
+        if (hi != hi_pf) {  // the previous batch was cut by its slot budget: re-fetch (rare)
+            fetch_entry(hi);
+            fetch_rec(hi);
+            fetch_entry(hi - BB);
+        }
+        const int cmax = min(BB, hi);
+        int ts_ = tid;
+        asm volatile("" : "+v"(ts_));  // staging addresses formed here, not hoisted across the batch loop
+        if (ts_ < cmax) {
+            s_u[ts_] = instance_slot(make_uint2(__float_as_uint(pc.w), DUAL ? __float_as_uint(pd.w) : prh),
                                      pbs + __float_as_uint(pb.w), tx, ty);
-            s_a[tid] = pa;
-            s_b[tid] = pb;
-            s_c[tid] = pc;
-            if (DUAL) s_d[tid] = pd;
-            s_mask[tid] = (uint16_t)pm;  // the instance's exact 4x4-block mask (sorted list entry)
+            s_a[ts_] = pa;
+            s_b[ts_] = pb;
+            s_c[ts_] = pc;
+            if (DUAL) s_d[ts_] = pd;
+            s_mask[ts_] = (uint16_t)pm;  // the instance's exact 4x4-block mask (sorted list entry)
         }
         __syncthreads();
         fetch_rec(hi - BB);        // records of the next batch (list entries loaded a batch ago)
         fetch_entry(hi - 2 * BB);  // list entries of the batch after it
+        hi_pf = hi - BB;
         // entries j with pos = hi-1-j >= rmax lie behind every pixel of the block
         const int jmin[4] = {hi - rm[0], hi - rm[1], hi - rm[2], hi - rm[3]};
-        const int n = build_row_lists(s_mask, cnt, w, jmin, s_list + 4 * w * LS, LS, (uint16_t)BB);
+        const SlotLists sl = build_row_slot_lists(s_mask, s_base, cmax, BS, w, jmin, s_list + 4 * w * LS, LS,
+                                                  (uint32_t)BB | ((uint32_t)BS << 16));
+        const int n = sl.len, cnt = sl.cnt;
         const int jlo = hi - (int)last;  // pos = hi-1-j < last  <=>  j >= jlo
+#if GSR_STEPSTAT
+        st_batches++;
+#endif
         for (int i = 0; i < n; i += 4) {
-            const RowGroup4 gq = load_row_group4(my_list, i);
+            const uint4 gw = load_slot_group4(my_list, i);
+            RowGroup4 gq;
+            gq.j[0] = (int)(gw.x & 0xFFFFu);
+            gq.j[1] = (int)(gw.y & 0xFFFFu);
+            gq.j[2] = (int)(gw.z & 0xFFFFu);
+            gq.j[3] = (int)(gw.w & 0xFFFFu);
             v2f d[4];
             float G[4], araw[4], alpha[4];
             bool ok[4];
@@ -282,6 +373,20 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 alpha[k] = ok[k] ? alpha[k] : 0.f;
                 any = any || ok[k];
             }
+#if GSR_STEPSTAT
+            st_steps++;
+            {
+                uint64_t pads = 0, oks = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    pads += __popcll(__ballot(gq.j[k] == BB));
+                    oks += __popcll(__ballot(ok[k]));
+                }
+                st_pads += pads;
+                st_ok += oks;
+                st_csteps += __ballot(any) != 0ull;
+            }
+#endif
             if (__ballot(any) == 0ull) continue;  // slots stay zero
             // serial part (in list order): T and A, then dL/dalpha and dchannel/dcolor
             float dLa[4], dch[4];
@@ -314,8 +419,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             // h = G * dL/dG = (o * G) * dL/dalpha.  gauss_bwd turns them into the reference's
             // per-pair quantities (backward.cu:1020-1038): dmean2D = -ddel * (Q [hx, hy]),
             // dconic = -0.5 * (hxx, hxy, hyy); both are linear in the sums (Q is per Gaussian).
-            const int je = my_e == 0 ? gq.j[0] : (my_e == 1 ? gq.j[1] : (my_e == 2 ? gq.j[2] : gq.j[3]));
-            float* dst = acc_row + je * NV;
+            const uint32_t we = my_e == 0 ? gw.x : (my_e == 1 ? gw.y : (my_e == 2 ? gw.z : gw.w));
+            float* dst = s_acc + (we >> 16) * NV;  // the (entry, block) slot
             if constexpr (NV <= 6) {  // one reduction over all values
                 float v[4 * NV];
 #pragma unroll
@@ -351,8 +456,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         }
         __syncthreads();
         // Entry totals: TPE threads per entry, thread q of an entry owns values m = q, q + TPE, ...
-        // and adds the entry's block slots in ascending block order (deterministic), visiting only
-        // the blocks of its mask; the TPE threads store adjacent floats of the packed record.
+        // and adds the entry's consecutive block slots in ascending block order (deterministic);
+        // the TPE threads store adjacent floats of the packed record.
         constexpr int TPE = TILE_PIX / BB, NQ = (RS + TPE - 1) / TPE;
         int t_ = tid;
         asm volatile("" : "+v"(t_));  // addresses formed here, not hoisted across the batch loop (VGPRs)
@@ -361,11 +466,9 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             float c[NQ];
 #pragma unroll
             for (int i = 0; i < NQ; i++) c[i] = 0.f;
-            uint32_t mm = s_mask[e];
-            while (mm) {
-                const int b = __builtin_ctz(mm);
-                mm &= mm - 1u;
-                float* src = s_acc + (b * SL + e) * NV;
+            const int nb = __popc((uint32_t)s_mask[e]);
+            float* src = s_acc + (int)s_base[e] * NV;
+            for (int b = 0; b < nb; b++, src += NV) {
 #pragma unroll
                 for (int i = 0; i < NQ; i++)
                     if (q + TPE * i < NV) {
@@ -379,9 +482,19 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 if (q + TPE * i < RS) dst[q + TPE * i] = c[i];
         }
         __syncthreads();
+        hi -= cnt;
     }
 #if GSR_ABLATE == 1
     if (ablate_sink == 1.2345f) inst[0] = ablate_sink;  // keeps the per-pair values alive (timing ablation)
+#endif
+#if GSR_STEPSTAT
+    if (lane == 0) {
+        atomicAdd(&g_stepstat[0], st_steps);
+        atomicAdd(&g_stepstat[1], st_csteps);
+        atomicAdd(&g_stepstat[2], st_ok);
+        atomicAdd(&g_stepstat[3], st_pads);
+        atomicAdd(&g_stepstat[4], st_batches);
+    }
 #endif
     GSR_WGTIME_MARK(true);
     kclock_end(clk);
@@ -651,6 +764,14 @@ hipError_t launch_selftest_reduce9(const float* in, float* out, hipStream_t s) {
     return hipGetLastError();
 }
 
+#if GSR_STEPSTAT
+extern "C" int gsr_diag_stepstat_bwd(unsigned long long* host) {  // copies and clears the counters
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stepstat), sizeof(g_stepstat), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stepstat), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+#endif
 #if GSR_WGTIME
 extern "C" int gsr_diag_wgtime_bwd(unsigned long long* host, int n) {
     const size_t bytes = sizeof(unsigned long long) * 4 * (size_t)(n < GSR_WGTIME_MAX ? n : GSR_WGTIME_MAX);
