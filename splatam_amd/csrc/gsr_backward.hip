@@ -419,7 +419,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             // h = G * dL/dG = (o * G) * dL/dalpha.  gauss_bwd turns them into the reference's
             // per-pair quantities (backward.cu:1020-1038): dmean2D = -ddel * (Q [hx, hy]),
             // dconic = -0.5 * (hxx, hxy, hyy); both are linear in the sums (Q is per Gaussian).
-            const uint32_t we = my_e == 0 ? gw.x : (my_e == 1 ? gw.y : (my_e == 2 ? gw.z : gw.w));
+            const uint32_t wlo = (my_e & 1) ? gw.y : gw.x, whi = (my_e & 1) ? gw.w : gw.z;  // selects, no branches
+            const uint32_t we = (my_e & 2) ? whi : wlo;
             float* dst = s_acc + (we >> 16) * NV;  // the (entry, block) slot
             if constexpr (NV <= 6) {  // one reduction over all values
                 float v[4 * NV];
