@@ -20,6 +20,10 @@ def main(src, tag):
         for f in glob.glob(f"{src}/pmc_{c}/**/run_counter_collection.csv", recursive=True):
             for r in csv.DictReader(open(f)):
                 pmc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    bench = None
+    for line in open(f"{src}/bench.log"):
+        if line.startswith("{"):
+            bench = json.loads(line)
     summary = {}
     for k, d in pmc.items():
         fetch = sum(d["FETCH_SIZE"]) / max(len(d["FETCH_SIZE"]), 1)
@@ -29,19 +33,30 @@ def main(src, tag):
         summary[k] = {"FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write,
                       "hbm_bytes_per_launch": int((2.0 * fetch + write) * 1024),
                       "avg_duration_ns_trace": float(rows[k]["AverageNs"]) if k in rows else None}
-    bench = None
-    for line in open(f"{src}/bench.log"):
-        if line.startswith("{"):
-            bench = json.loads(line)
+        if k == "render_bwd_kernel" and bench is not None and bench.get("roofline"):
+            # profiles/traffic_calibration.json: 64-B record gathers are counted 1:1 by FETCH_SIZE,
+            # coalesced streams at half: calibrated bytes = FETCH + streamed/2 + WRITE, the streamed
+            # reads being the sorted list entries (8 B / instance) and the per-pixel inputs
+            # (final_T, n_contrib, 3 + 1 gradient channels: 24 B / pixel)
+            cfg = bench["config"]
+            inst = float(bench["roofline"]["num_rendered_avg"])
+            streamed = 8.0 * inst + 24.0 * cfg["width"] * cfg["height"]
+            summary[k]["streamed_read_bytes_alg"] = int(streamed)
+            summary[k]["hbm_bytes_calibrated"] = int((fetch + write) * 1024 + streamed / 2)
+
     out = {"tag": tag, "kernels": summary, "bench": bench,
            "note": "FETCH_SIZE/WRITE_SIZE in KB per dispatch from separate rocprofv3 --pmc passes of "
-                   "bench.py; hbm_bytes_per_launch = 2 * FETCH_SIZE + WRITE_SIZE (the gfx950 FETCH_SIZE "
-                   "correction of MI355X_MICROARCH.md HBM; gather widths are uncalibrated there)."}
+                   "bench.py; hbm_bytes_per_launch = 2 * FETCH_SIZE + WRITE_SIZE (the guide's streaming-read "
+                   "correction applied to everything: an upper bound); hbm_bytes_calibrated (render_bwd) = "
+                   "FETCH_SIZE + streamed/2 + WRITE_SIZE per profiles/traffic_calibration.json."}
     json.dump(out, open(f"{dst}/{tag}_summary.json", "w"), indent=1)
     rb = summary.get("render_bwd_kernel")
     headline = bench is not None and str(bench.get("metric", "")).startswith("rasterize fwd+bwd")
     if rb and headline:  # bench.py's roofline.traffic of the headline (tracking) workload
-        json.dump({"kernel": "render_bwd_kernel", "hbm_bytes_per_launch": rb["hbm_bytes_per_launch"],
+        json.dump({"kernel": "render_bwd_kernel", "hbm_bytes_per_launch": rb.get("hbm_bytes_calibrated",
+                                                                                 rb["hbm_bytes_per_launch"]),
+                   "uncalibrated_2fetch_plus_write": rb["hbm_bytes_per_launch"],
+                   "calibration": "profiles/traffic_calibration.json",
                    "source": f"profiles/{tag}_summary.json"}, open(f"{dst}/render_bwd_pmc.json", "w"), indent=1)
     shutil.copy(f"{src}/bench.log", f"{dst}/{tag}_bench.log")
     print(json.dumps(out["kernels"], indent=1))
