@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 2
+#define GSR_ABI_VERSION 3
 
 /* error codes */
 #define GSR_OK 0
@@ -149,6 +149,30 @@ int gsr_forward_dual_static(const gsr_settings* settings, const gsr_gaussians* g
                             const float* colors2, int capacity, unsigned* status,
                             float* out_color, float* out_color2, float* out_depth, int* radii,
                             gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
+/* Geometry-reuse forward (SURVEY.md 8(f) row 1 for unchanged callers): the
+ * second of two gsr_forward calls on identical geometry and camera -- SplaTAM's
+ * RGB then depth/silhouette Renderer calls (scripts/splatam.py:255,259), each
+ * through RasterizeGaussiansCUDA (rasterize_points.cu:35-115) -- skips
+ * preprocess, binning and the tile sort: the new geometry buffer is the
+ * previous one with the colours of `gaussians` (colors_precomp, required; no
+ * SH) written into its render records, the binning and image buffers of the
+ * previous call are reused in place (their content is what this call would
+ * compute), radii are copied.  The caller guarantees (gsr_bitwise_equal on
+ * the device, identity of the unchanged tensors on the host) that means3D,
+ * scales, rotations, opacities and every setting equal those of the call that
+ * produced prev_geom / binning_buffer / image_buffer, which must still be
+ * alive.  Returns num_rendered (the previous call's) or a negative error. */
+int gsr_forward_reuse(const gsr_settings* settings, const gsr_gaussians* gaussians, int num_rendered,
+                      const void* prev_geom, void* binning_buffer, void* image_buffer, const int* prev_radii,
+                      float* out_color, float* out_depth, int* radii,
+                      gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
+/* Sets *flag (device int, zeroed by the caller) to non-zero when any of the
+ * `npairs` (<= 8) float arrays a[k][0..n[k]) and b[k][0..n[k]) differ bitwise.
+ * Enqueued on `stream`; the host reads the flag after a stream sync. */
+int gsr_bitwise_equal(int npairs, const float* const* a, const float* const* b, const long long* n, int* flag,
+                      void* stream);
 
 /* Static-capacity, synchronisation-free gsr_forward (one colour set): the
  * gsr_forward_dual_static contract (capacity, sticky status row, returns

@@ -15,7 +15,9 @@ ROCm device, these functions raise.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
+import weakref
 
 import torch
 
@@ -93,6 +95,94 @@ def _gaussians(means3D, sh, colors, opacity, scales, rotations, cov3D_precomp, d
     return g, keep, M
 
 
+# ---------------------------------------------------------------------------------------------
+# Geometry reuse across consecutive calls (SURVEY.md 8(f) row 1 for unchanged callers): SplaTAM
+# renders RGB and then the depth/silhouette image of the same Gaussians from the same camera
+# (scripts/splatam.py:255,259), two RasterizeGaussiansCUDA calls whose preprocess, binning and
+# tile sort are identical.  The second call reuses the first call's geometry / binning / image
+# buffers (gsr_forward_reuse) when
+#   * means3D and the camera tensors are the same storage at the same version, the scalar
+#     settings and P are equal, the colours are precomputed (no SH) and no cov3D is given,
+#   * the first call's buffers and its rotations / opacities / scales are still alive and
+#     unmodified (weak references + tensor versions), and
+#   * this call's rotations / opacities / scales equal the first call's bitwise (one device
+#     comparison, gsr_bitwise_equal, read back with the host sync the reference also makes).
+# GSR_GEOM_CACHE=0 disables it.
+_GEOM_CACHE = os.environ.get("GSR_GEOM_CACHE", "1") != "0"
+REUSE_STATS = {"hits": 0, "misses": 0}  # eligible calls that did / did not reuse (diagnostics, tests)
+
+
+class _Prev:
+    """The last eager single-call forward on a (thread, device)."""
+    __slots__ = ("key", "shared", "shared_versions", "others", "versions", "bufs", "radii", "num_rendered")
+
+
+def _try_reuse(key, shared, others, P):
+    """The previous call's state if this call may reuse it (host checks + one device comparison).
+    key: device, stream and scalar settings; shared: tensors that must be the very same objects
+    (means3D, bg, viewmatrix, projmatrix, campos) at the same versions."""
+    prev = getattr(_tls, "prev", {}).get(key[0])
+    if prev is None or prev.key != key:
+        return _miss("key")
+    for k, (r, v, t) in enumerate(zip(prev.shared, prev.shared_versions, shared)):
+        if (r is None) != (t is None):
+            return _miss(f"shared{k}_none")
+        if t is not None and r() is None:
+            return _miss(f"shared{k}_dead")
+        if t is not None and r() is not t:
+            return _miss(f"shared{k}_other")
+        if t is not None and t._version != v:
+            return _miss(f"shared{k}_version")
+    po = [r() for r in prev.others]
+    bufs = [r() for r in prev.bufs]
+    radii = prev.radii()
+    if any(t is None for t in po) or any(b is None for b in bufs) or radii is None:
+        return _miss("dead")
+    if any(t._version != v for t, v in zip(po, prev.versions)):
+        return _miss("version")
+    if any(a is None or a.shape != b.shape for a, b in zip(others, po)):
+        return _miss("shape")
+    flag = _flag(key[0])
+    flag.zero_()
+    arr_a = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in others])
+    arr_b = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in po])
+    arr_n = (ctypes.c_longlong * 3)(*[t.numel() for t in others])
+    _check(lib.gsr_bitwise_equal(3, arr_a, arr_b, arr_n, flag.data_ptr(), key[1]), "bitwise_equal")
+    if int(flag.item()) != 0:
+        return _miss("content")
+    return prev, bufs, radii
+
+
+def _miss(reason):
+    REUSE_STATS[reason] = REUSE_STATS.get(reason, 0) + 1
+    return None
+
+
+def _flag(device):
+    flags = getattr(_tls, "flags", None)
+    if flags is None:
+        flags = _tls.flags = {}
+    f = flags.get(device)
+    if f is None:
+        f = flags[device] = torch.zeros(1, dtype=torch.int32, device=device)
+    return f
+
+
+def _remember(key, shared, others, bufs, radii, num_rendered):
+    if not hasattr(_tls, "prev"):
+        _tls.prev = {}
+    p = _Prev()
+    p.key = key
+    p.shared = [None if t is None else weakref.ref(t) for t in shared]
+    p.shared_versions = [None if t is None else t._version for t in shared]
+    p.others = [weakref.ref(t) for t in others]
+    p.versions = [t._version for t in others]
+    p.bufs = [weakref.ref(b) for b in bufs]
+    p.radii = weakref.ref(radii)
+    p.num_rendered = num_rendered
+    _tls.prev[key[0]] = p
+
+
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
                         prefiltered, capacity=0, status=None):
@@ -122,6 +212,27 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         out_color = torch.empty(3, H, W, **f32)
         out_depth = torch.empty(1, H, W, **f32)
         radii = torch.empty(P, dtype=torch.int32, device=device)
+        stream = _stream(device)
+        reusable = (_GEOM_CACHE and capacity <= 0 and keep_g[2] is not None and keep_g[1] is None and
+                    keep_g[6] is None and None not in (keep_g[3], keep_g[4], keep_g[5]))
+        if reusable:
+            others = (keep_g[5], keep_g[3], keep_g[4])  # rotations, opacities, scales as passed down
+            # identity of the caller's own tensors (SplaTAM's viewmatrix / projmatrix are transposed
+            # views, so the contiguous copies passed down are new objects on every call)
+            shared = (means3D, background, viewmatrix, projmatrix, campos)
+            key = (device, stream, P, H, W, float(tan_fovx), float(tan_fovy), float(scale_modifier), int(degree),
+                   bool(prefiltered))
+            hit = _try_reuse(key, shared, others, P)
+            REUSE_STATS["hits" if hit is not None else "misses"] += 1
+            if hit is not None:
+                prev, bufs, prev_radii = hit
+                _begin(device)
+                n = lib.gsr_forward_reuse(ctypes.byref(s), ctypes.byref(g), int(prev.num_rendered), bufs[0].data_ptr(),
+                                          bufs[1].data_ptr(), bufs[2].data_ptr(), prev_radii.data_ptr(),
+                                          out_color.data_ptr(), out_depth.data_ptr(), radii.data_ptr(), _ALLOC_CB, None,
+                                          stream)
+                _check(n, "rasterize_gaussians (geometry reuse)")
+                return (int(n), out_color, radii, _tls.buffers[0], bufs[1], bufs[2], out_depth)
         _begin(device)
         if capacity > 0:
             if status is None or status.device != device or status.numel() < 4:
@@ -131,9 +242,11 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                                        _stream(device))
         else:
             n = lib.gsr_forward(ctypes.byref(s), ctypes.byref(g), out_color.data_ptr(), out_depth.data_ptr(),
-                                radii.data_ptr(), _ALLOC_CB, None, _stream(device))
+                                radii.data_ptr(), _ALLOC_CB, None, stream)
         _check(n, "rasterize_gaussians")
         bufs = _tls.buffers
+        if reusable:
+            _remember(key, shared, others, (bufs[0], bufs[1], bufs[2]), radii, int(n))
         return (int(n), out_color, radii, bufs[0], bufs[1], bufs[2], out_depth)
 
 

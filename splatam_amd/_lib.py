@@ -71,6 +71,10 @@ SIGNATURES = {
     "gsr_backward_dual": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, ctypes.POINTER(GsrGrads),
                                   c_void_p, c_int, ALLOC_FN, c_void_p, c_void_p]),
+    "gsr_forward_reuse": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_int, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ALLOC_FN, c_void_p,
+                                  c_void_p]),
+    "gsr_bitwise_equal": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gsr_mark_visible": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gsr_geom_buffer_bytes": (c_size_t, [c_int]),
     "gsr_binning_buffer_bytes": (c_size_t, [c_int, c_int, c_int]),
@@ -134,7 +138,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.gsr_abi_version() != 2:
+    if lib.gsr_abi_version() != 3:
         raise ImportError("libgsr.so ABI version mismatch")
     return lib
 

@@ -749,6 +749,69 @@ int gsr_forward(const gsr_settings* settings, const gsr_gaussians* gaussians, fl
     return forward_impl(settings, gaussians, nullptr, out_color, nullptr, out_depth, radii, alloc, alloc_ctx, stream);
 }
 
+int gsr_forward_reuse(const gsr_settings* settings, const gsr_gaussians* gaussians, int num_rendered,
+                      const void* prev_geom, void* binning_buffer, void* image_buffer, const int* prev_radii,
+                      float* out_color, float* out_depth, int* radii, gsr_alloc_fn alloc, void* alloc_ctx,
+                      void* stream_) {
+    int rc = validate(settings, gaussians, true);
+    if (rc != GSR_OK) return rc;
+    if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
+    if (!gaussians->colors_precomp || (gaussians->shs && gaussians->M > 0))
+        return fail(GSR_ERR_INVALID_ARG, "geometry reuse needs precomputed colours (no SH)");
+    if (gaussians->P <= 0 || num_rendered < 0 || !prev_geom || !binning_buffer || !image_buffer || !prev_radii ||
+        !out_color || !out_depth || !radii)
+        return fail(GSR_ERR_INVALID_ARG, "geometry reuse needs the previous call's state and the outputs");
+    hipStream_t stream = (hipStream_t)stream_;
+    const int dev = stream_device(stream);
+    Camera cam = make_camera(settings);
+    const GaussIn g = make_gauss(gaussians);
+    const int P = g.P;
+    const GeomLayout GL = GeomLayout::make(P);
+    const ImgLayout IL = ImgLayout::make(cam.W, cam.H);
+    void* geom = obtain(alloc, alloc_ctx, GSR_BUF_GEOM, GL.total);
+    if (!geom) return fail(GSR_ERR_ALLOC, "allocator returned NULL (geom buffer)");
+    const GeomPtrs geo = GeomPtrs::at(geom, GL);
+    char* ib = (char*)image_buffer;
+    cam.tile_order = (const uint32_t*)(ib + IL.order);
+    cam.sched_cus = device_cus(dev);
+    hipError_t e;
+    {
+        StageTimer t(GSR_STAGE_PREPROCESS, P, stream);
+        if ((e = hipMemcpyAsync(geom, prev_geom, GL.total, hipMemcpyDeviceToDevice, stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(radii, prev_radii, sizeof(int) * (size_t)P, hipMemcpyDeviceToDevice, stream)) !=
+                hipSuccess)
+            return hip_fail(e, "copy previous geometry");
+        if ((e = launch_recolour(P, g.colors, geo, stream)) != hipSuccess) return hip_fail(e, "recolour");
+    }
+    // the previous render_fwd left point_list sorted (with its block masks): no sort, any list length
+    const SpecGuard guard{geo.counters, (uint32_t)num_rendered, 0xFFFFFFFFu};
+    {
+        StageTimer t(GSR_STAGE_RENDER_FWD, num_rendered, stream, true);
+        if ((e = launch_render_fwd(cam, (const uint2*)(ib + IL.ranges), (uint64_t*)binning_buffer, nullptr, geo,
+                                   nullptr, (float*)(ib + IL.final_T), (uint32_t*)(ib + IL.n_contrib), out_color,
+                                   nullptr, out_depth, guard, stream, t.kclock())) != hipSuccess)
+            return hip_fail(e, "render");
+    }
+    return num_rendered;
+}
+
+int gsr_bitwise_equal(int npairs, const float* const* a, const float* const* b, const long long* n, int* flag,
+                      void* stream) {
+    if (npairs < 0 || npairs > 8 || (npairs > 0 && (!a || !b || !n)) || !flag)
+        return fail(GSR_ERR_INVALID_ARG, "gsr_bitwise_equal: 0..8 pairs and a flag");
+    EqualPairs q{};
+    q.npairs = npairs;
+    for (int k = 0; k < npairs; k++) {
+        if (n[k] < 0 || (n[k] > 0 && (!a[k] || !b[k]))) return fail(GSR_ERR_INVALID_ARG, "gsr_bitwise_equal: pair");
+        q.a[k] = a[k];
+        q.b[k] = b[k];
+        q.n[k] = n[k];
+    }
+    hipError_t e = launch_bitwise_equal(q, flag, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "bitwise_equal");
+    return GSR_OK;
+}
+
 int gsr_forward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
                      float* out_color, float* out_color2, float* out_depth, int* radii, gsr_alloc_fn alloc,
                      void* alloc_ctx, void* stream) {

@@ -1069,6 +1069,15 @@ hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* p
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
                              unsigned long long* clk = nullptr, const TrackL1* l1 = nullptr);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* vis, hipStream_t s);
+// geometry reuse (gsr_forward_reuse): the render records' colours replaced by `colors` [P,3]
+hipError_t launch_recolour(int P, const float* colors, GeomPtrs geo, hipStream_t s);
+struct EqualPairs {
+    int npairs;
+    const float* a[8];
+    const float* b[8];
+    long long n[8];
+};
+hipError_t launch_bitwise_equal(const EqualPairs& q, int* flag, hipStream_t s);
 // Per-(tile, Gaussian) instance record of the power-1 backward: the per-pair sums
 // the launched render_bwd variant forms, packed (no slots for absent terms):
 // [hx, hy, hxx, hxy, hyy | G dL/dalpha (o_op) | dch dp (o_c1, 3) | dch dq (o_c2, n_c2)]

@@ -1209,6 +1209,40 @@ hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* p
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------- geometry reuse --
+// gsr_forward_reuse: the copied render records get this call's colours (preprocess writes the
+// colours only for Gaussians that touch a tile: the same condition here, tiles[i] != 0)
+__global__ void recolour_kernel(int P, const float* __restrict__ colors, float4* __restrict__ rr,
+                                const uint32_t* __restrict__ tiles) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P || tiles[i] == 0u) return;
+    float4* q2 = rr + (size_t)RR_F4 * i + 2;
+    const float4 old = *q2;
+    *q2 = make_float4(colors[3 * i], colors[3 * i + 1], colors[3 * i + 2], old.w);
+}
+hipError_t launch_recolour(int P, const float* colors, GeomPtrs geo, hipStream_t s) {
+    if (P <= 0) return hipSuccess;
+    hipLaunchKernelGGL(recolour_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, colors, geo.rr, geo.tiles);
+    return hipGetLastError();
+}
+// flag |= 1 when a[k][i] != b[k][i] bitwise for any pair k (grid-stride over the pairs' elements)
+__global__ void bitwise_equal_kernel(EqualPairs q, int* flag) {
+    bool diff = false;
+    for (int k = 0; k < q.npairs; k++) {
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(q.a[k]);
+        const uint32_t* b = reinterpret_cast<const uint32_t*>(q.b[k]);
+        for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < q.n[k];
+             i += (long long)gridDim.x * blockDim.x)
+            diff = diff || a[i] != b[i];
+    }
+    if (__ballot(diff) != 0ull && __lane_id() == 0) atomicOr(flag, 1);
+}
+hipError_t launch_bitwise_equal(const EqualPairs& q, int* flag, hipStream_t s) {
+    if (q.npairs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(bitwise_equal_kernel, dim3(1024), dim3(256), 0, s, q, flag);
+    return hipGetLastError();
+}
+
 // ----------------------------------------------------------- mark visible --
 __global__ void mark_visible_kernel(int P, const float* __restrict__ means3D, const float* __restrict__ view,
                                     uint8_t* __restrict__ vis) {

@@ -412,3 +412,65 @@ def test_mark_visible_matches_oracle(cuda):
     ref = oracle.mark_visible(pts.numpy(), cam.viewmatrix.numpy())
     np.testing.assert_array_equal(vis.cpu().numpy(), ref)
     assert 0 < int(vis.sum()) < P
+
+
+def _geom_pair(cuda, seed, perturb_second=False, cache=True):
+    """SplaTAM's two Renderer calls (scripts/splatam.py:255,259): same means3D tensor and camera,
+    rotations / opacities / scales recomputed (new tensors, equal values), different colours."""
+    from splatam_amd import _C
+    from splatam_amd.rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+    scene = make_scene(4000, 160, 120, seed=seed, anisotropic=True)
+    c = scene.cam
+    st = GaussianRasterizationSettings(120, 160, c.tanfovx, c.tanfovy, torch.zeros(3, device=cuda), 1.0,
+                                       c.viewmatrix.to(cuda), c.projmatrix.to(cuda), 0, c.campos.to(cuda), False)
+    rs = np.random.RandomState(seed)
+    g1 = torch.as_tensor(rs.randn(3, 120, 160).astype(np.float32), device=cuda)
+    g2 = torch.as_tensor(rs.randn(3, 120, 160).astype(np.float32), device=cuda)
+    old = _C._GEOM_CACHE
+    _C._GEOM_CACHE = cache
+    try:
+        m3 = scene.means3D.to(cuda).requires_grad_(True)
+        u_rot = scene.rotations.to(cuda).requires_grad_(True)
+        lo = torch.logit(scene.opacities.to(cuda).clamp(1e-4, 1 - 1e-4)).requires_grad_(True)
+        ls = torch.log(scene.scales.to(cuda)).requires_grad_(True)
+        col = scene.colors.to(cuda).requires_grad_(True)
+        outs = []
+        rendervars = []  # held like get_loss holds its two rendervar dicts (slam_helpers.py:124-139,234-249)
+        for k in range(2):
+            z = m3[:, 2:3]
+            rendervars.append(dict(
+                means3D=m3, means2D=torch.zeros_like(m3, requires_grad=True), opacities=torch.sigmoid(lo),
+                colors_precomp=col if k == 0 else torch.cat([z, torch.ones_like(z), z * z], 1),
+                scales=torch.exp(ls) * (1.001 if (perturb_second and k == 1) else 1.0),
+                rotations=torch.nn.functional.normalize(u_rot)))
+        for k in range(2):
+            outs.append(GaussianRasterizer(st)(**rendervars[k]))
+        ((outs[0][0] * g1).sum() + (outs[1][0] * g2).sum()).backward()
+        res = [o[0].detach().cpu() for o in outs] + [o[1].cpu() for o in outs] + [o[2].detach().cpu() for o in outs]
+        res += [t.grad.cpu() for t in (m3, u_rot, lo, ls, col)]
+        return res
+    finally:
+        _C._GEOM_CACHE = old
+
+
+def test_geometry_reuse_matches_two_full_calls(cuda):
+    """The second of two calls on identical geometry reuses the first call's preprocess / binning
+    (gsr_forward_reuse): images, radii, depth and every gradient bitwise those of two full calls."""
+    from splatam_amd import _C
+    hits = _C.REUSE_STATS["hits"]
+    a = _geom_pair(cuda, 41, cache=True)
+    assert _C.REUSE_STATS["hits"] == hits + 1, _C.REUSE_STATS  # the second call took the reuse path
+    b = _geom_pair(cuda, 41, cache=False)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def test_geometry_reuse_refused_on_changed_geometry(cuda):
+    """Scales differing in the second call (bitwise comparison on the device) -> full forward."""
+    from splatam_amd import _C
+    hits, content = _C.REUSE_STATS["hits"], _C.REUSE_STATS.get("content", 0)
+    a = _geom_pair(cuda, 43, perturb_second=True, cache=True)
+    assert _C.REUSE_STATS["hits"] == hits and _C.REUSE_STATS["content"] == content + 1, _C.REUSE_STATS
+    b = _geom_pair(cuda, 43, perturb_second=True, cache=False)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
