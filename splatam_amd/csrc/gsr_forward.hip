@@ -1011,8 +1011,9 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
     const v2f pix = v2f{(float)px, (float)py};
     const uint2 range = ranges[tile];
     bool done = !inside;
-    float T = 1.f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 15.0f;  // forward.cu:308 median-depth default
-    float C3 = 0.f, C4 = 0.f, C5 = 0.f;
+    float T = 1.f, C2 = 0.f, D = 15.0f;  // forward.cu:308 median-depth default
+    float C5 = 0.f;
+    v2f C01 = v2f{0.f, 0.f}, C34 = v2f{0.f, 0.f};  // channel pairs: one v_pk_fma_f32 per pair and Gaussian
     uint32_t last = 0;
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
     uint32_t pg = 0, pgn = 0;  // the staged entry's Gaussian id, the id of the entry a batch later
@@ -1052,7 +1053,9 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
         const int cnt = (int)min((uint32_t)RENDER_BATCH, range.y - start);
         if (tid < cnt) {
-            const uint32_t pm = block_mask_exact(pa, pb, x0, y0);
+            float xs = x0, ys = y0;
+            asm volatile("" : "+v"(xs), "+v"(ys));  // block bounds formed here, not hoisted (VGPRs)
+            const uint32_t pm = block_mask_exact(pa, pb, xs, ys);
             s_a[tid] = pa;
             s_b[tid] = pb;
             s_c[tid] = pc;
@@ -1093,12 +1096,10 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
                 if (DUAL) c2 = s_d[gq.j[k]];
                 if (blend) {
                     const float wgt = alpha[k] * T;
-                    C0 += c.x * wgt;
-                    C1 += c.y * wgt;
+                    C01 = __builtin_elementwise_fma(v2f{c.x, c.y}, v2f{wgt, wgt}, C01);
                     C2 += c.z * wgt;
                     if (DUAL) {
-                        C3 += c2.x * wgt;
-                        C4 += c2.y * wgt;
+                        C34 = __builtin_elementwise_fma(v2f{c2.x, c2.y}, v2f{wgt, wgt}, C34);
                         C5 += c2.z * wgt;
                     }
                     if (T > 0.5f && test_T < 0.5f) D = depth[k];  // median depth (forward.cu:368-372)
@@ -1109,6 +1110,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         }
         __syncthreads();
     }
+    const float C0 = C01.x, C1 = C01.y, C3 = C34.x, C4 = C34.y;
     if (inside) {
         const int pid = py * cam.W + px;
         const int HW = cam.W * cam.H;
