@@ -83,8 +83,12 @@ def setup_dist(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        backend = os.environ.get("GSR_DIST_BACKEND", "nccl")  # nccl = RCCL; gloo only to rehearse ranks on one GPU
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -99,7 +103,7 @@ def img_n_contrib_sum(img_buffer: torch.Tensor, W: int, H: int) -> int:
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     if args.config is None:
         args.config = 4 if args.workload == "mapping" else 3
@@ -166,7 +170,7 @@ def main():
     if tracker is None:
         profiling.enable_timing(True)
     else:  # reset the device-clock accumulators the captured stamps add to
-        profiling.enable_timing(clock_stages=("render_bwd",))
+        profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if tracker is not None:
@@ -498,7 +502,7 @@ def main_mapping(args, world, rank, dev):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    profiling.enable_timing(clock_stages=("render_bwd",))
+    profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps // S):

@@ -764,9 +764,16 @@ __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, E
 //                for every other chunk (staged in LDS), the number of that chunk's
 //                keys below it -- exact, as the keys are unique in a tile.
 // The result equals a stable (tile, depth) radix order (ids break depth ties).
+#ifndef GSR_FWD_ABLATE
+#define GSR_FWD_ABLATE 0  // timing ablations (tools/ablate.sh); 0 in every real build
+#endif
 __device__ __forceinline__ void tile_sort_bucket(uint64_t* __restrict__ src, uint32_t cnt,
                                                  PointEntry* __restrict__ dst, uint64_t* sk) {
     auto emit = [&](uint32_t i, uint32_t gi) { dst[i] = (PointEntry)gi; };
+    if (GSR_FWD_ABLATE == 1) {  // timing only: the bucket copied unsorted (wrong order)
+        for (uint32_t i = threadIdx.x; i < cnt; i += TILE_SORT_THREADS) emit(i, (uint32_t)src[i]);
+        return;
+    }
     if (cnt <= 1) {
         if (cnt == 1 && threadIdx.x == 0) emit(0, (uint32_t)src[0]);
         return;

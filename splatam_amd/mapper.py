@@ -93,7 +93,7 @@ class GraphMapper:
         del snapshot
         if timing:
             from . import profiling
-            profiling.enable_timing(clock_stages=("render_bwd",))
+            profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
         self.graph = torch.cuda.CUDAGraph()
         self.stream = side
         with torch.cuda.graph(self.graph, stream=side):

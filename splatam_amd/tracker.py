@@ -94,10 +94,10 @@ class GraphTracker:
             self.status.zero_()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
-        if timing:  # device-clock stamps around render_bwd become graph nodes (accumulate over replays)
+        if timing:  # device-clock stamps of render_bwd / render_fwd (in-kernel) (accumulate over replays)
             from . import profiling
             torch.cuda.synchronize(dev)
-            profiling.enable_timing(clock_stages=("render_bwd",))
+            profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
         self.graph = torch.cuda.CUDAGraph()
         self.stream = side
         with torch.cuda.graph(self.graph, stream=side):  # capture on the warm-up stream (autograd nodes live there)
