@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--dropin-frames", type=int, default=3, help="dropin: timed frames of 40 iterations")
     ap.add_argument("--fisher", choices=("on", "off"), default="on",
                     help="also time the batched Fisher / EIG view scoring (backward_power 2) on the same map")
+    ap.add_argument("--mapping", choices=("auto", "on", "off"), default="auto",
+                    help="also time the mapping workload (config 4) into a 'mapping' object (auto: N=1 only)")
+    ap.add_argument("--mapping-steps", type=int, default=100, help="mapping leg: timed iterations")
     ap.add_argument("--fisher-k", type=int, default=16, help="fisher: poses per HIP-graph launch")
     ap.add_argument("--timing", type=int, default=1,
                     help="0: no device-clock timing of render_bwd in the graph (A/B check; no roofline)")
@@ -227,6 +230,9 @@ def main():
 
     dropin = dropin_leg(args, scene, dev) if args.dropin == "on" else None
     fisher = fisher_leg(args, scene, dev) if args.fisher == "on" else None
+    mapping = None
+    if args.mapping == "on" or (args.mapping == "auto" and world == 1):
+        mapping = mapping_leg(args, dev)
 
     # ---- CPU baseline: the float32 C oracle on one frame (rank 0, N=1) ------
     cpu = None
@@ -299,6 +305,7 @@ def main():
             "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items()},
             "dropin": dropin,
             "fisher": fisher,
+            "mapping": mapping,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -457,6 +464,26 @@ def render_bwd_roofline(rb, I_avg, P, W, H, graph: bool):
 
 
 def main_mapping(args, world, rank, dev):
+    line = run_mapping(args, world, rank, dev)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def mapping_leg(args, dev):
+    """BASELINE config 4 (the mapping workload) inside the default bench line, so the round-end driver run
+    records it too: the same measurement as `--workload mapping` (rank 0, N=1 only)."""
+    import copy
+    a = copy.copy(args)
+    a.config, a.steps, a.warmup = 4, max(20, args.mapping_steps), 20
+    line = run_mapping(a, 1, 0, dev)
+    keep = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "execution", "config", "roofline",
+            "stages_us")
+    return {k: line[k] for k in keep}
+
+
+def run_mapping(args, world, rank, dev):
     """SplaTAM mapping iterations (scripts/splatam.py:842-905, get_loss mapping=True): one step = one
     iteration = transform + RGB(SH) and depth/silhouette render fwd+bwd (one dual rasterization) +
     0.8 L1 + 0.2 (1 - SSIM) + masked depth L1 + Adam on every Gaussian parameter; replayed as a HIP
@@ -520,25 +547,24 @@ def main_mapping(args, world, rank, dev):
     value = steps * world / elapsed
     nr = mapper.num_rendered()
     roofline = render_bwd_roofline(stages["render_bwd"], sum(nr) / len(nr), P, W, H, graph=True)
-    if rank == 0:
-        line = {
-            "metric": f"mapping iterations/sec @{W}x{H}, {P // 1000}k anisotropic Gaussians, SH degree "
-                      f"{scene.sh_degree}", "value": round(value, 3), "unit": "iterations/s", "n_gpus": world,
-            "steps": steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / steps, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "execution": f"HIP graph of {S} mapping iterations (one frame, fresh Adam), replayed; binning "
-                         f"capacity {mapper.capacity}, no overflow",
-            "data": f"synthetic (SURVEY.md 8(d) seeded scene; {K} keyframe targets rendered from a perturbed map)",
-            "config": {"workload": f"config {args.config}: {P} Gaussians, {W}x{H}, SplaTAM mapping iteration "
-                                   "(SH colour + depth/silhouette render fwd+bwd, L1 + SSIM + depth L1, Adam on "
-                                   "all Gaussian parameters)", "gaussians": P, "width": W, "height": H,
-                       "keyframes": K, "parallelism": f"frame-sharded x{world}"},
-            "roofline": roofline,
-            "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items()},
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    line = {
+        "metric": f"mapping iterations/sec @{W}x{H}, {P // 1000}k anisotropic Gaussians, SH degree "
+                  f"{scene.sh_degree}", "value": round(value, 3), "unit": "iterations/s", "n_gpus": world,
+        "steps": steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "execution": f"HIP graph of {S} mapping iterations (one frame, fresh Adam), replayed; binning "
+                     f"capacity {mapper.capacity}, no overflow",
+        "data": f"synthetic (SURVEY.md 8(d) seeded scene; {K} keyframe targets rendered from a perturbed map)",
+        "config": {"workload": f"config {args.config}: {P} Gaussians, {W}x{H}, SplaTAM mapping iteration "
+                               "(SH colour + depth/silhouette render fwd+bwd, L1 + SSIM + depth L1, Adam on "
+                               "all Gaussian parameters)", "gaussians": P, "width": W, "height": H,
+                   "keyframes": K, "parallelism": f"frame-sharded x{world}"},
+        "roofline": roofline,
+        "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items()},
+    }
+    del mapper, params, kfs
+    torch.cuda.empty_cache()
+    return line
 
 
 if __name__ == "__main__":

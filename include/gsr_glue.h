@@ -128,6 +128,34 @@ int gsr_track_forward_dual_static(const gsr_settings* settings, const gsr_gaussi
                                   float* dL_dim, float* dL_ddepth_sil, float* scratch, gsr_alloc_fn alloc,
                                   void* alloc_ctx, void* stream);
 
+/* gsr_track_transform_fwd fused into gsr_track_forward_dual_static (SURVEY.md 8(f) row 3:
+ * "transform-to-frame plus the [z,1,z^2] colours fused into preprocess"): the rasterizer's
+ * preprocess forms each Gaussian's camera-frame rendervars from the world-frame map and the
+ * frame's pose itself, so the transform is not a launch of its own and its outputs are not read
+ * back.  Same results, bit for bit, as gsr_track_transform_fwd(xform -> gaussians->means3D,
+ * ->rotations, colors2, ->opacities, ->scales) followed by gsr_track_forward_dual_static with
+ * those arrays: here they are OUTPUTS (written by the forward, device [P,3] / [P,4] / [P,3] /
+ * [P,1] / [P,3]) for the backward (gsr_track_backward_dual).  gaussians->colors_precomp: the
+ * RGB colours [P,3] (input); shs and cov3D_precomp must be NULL. */
+typedef struct gsr_track_xform {
+    const float* means_world;  /* [P,3] */
+    const float* unnorm_rot;   /* [P,4] */
+    const float* logit_opac;   /* [P,1] */
+    const float* log_scales;   /* [P,scale_cols] */
+    int scale_cols;            /* 1 (isotropic, tiled to 3) or 3 */
+    const float* cam_q;        /* the frame's quaternion, element k at cam_q[k * q_stride] */
+    const float* cam_t;        /* the frame's translation, likewise */
+    int q_stride;
+    const float* w2c;          /* [4,4] row-major: depth colours */
+} gsr_track_xform;
+
+int gsr_track_forward_dual_static_xf(const gsr_settings* settings, const gsr_gaussians* gaussians, float* colors2,
+                                     const gsr_track_xform* xform, int capacity, unsigned* status, float* out_color,
+                                     float* out_color2, float* out_depth, int* radii, const float* gt_im,
+                                     const float* gt_depth, float sil_thres, float w_im, float w_depth,
+                                     const float* dL_dloss, float* loss, float* dL_dim, float* dL_ddepth_sil,
+                                     float* scratch, gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
 /* Tracking backward with the pose chain fused into the rasterizer's per-Gaussian
  * backward: gsr_backward_dual's render backward (depth channel of the second
  * image, no opacity / colour sums), then one per-Gaussian kernel whose

@@ -21,7 +21,7 @@ import weakref
 
 import torch
 
-from ._lib import ALLOC_FN, GsrGaussians, GsrGrads, GsrSettings, lib
+from ._lib import ALLOC_FN, GsrGaussians, GsrGrads, GsrSettings, GsrTrackXform, lib
 
 _tls = threading.local()
 
@@ -425,10 +425,13 @@ def track_backward_dual(settings, means3D, radii, colors, colors2, scales, rotat
 
 
 def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scales, rotations, capacity, status, gt_im,
-                              gt_depth, sil_thres, w_im, w_depth, seed, scratch):
+                              gt_depth, sil_thres, w_im, w_depth, seed, scratch, xform=None):
     """gsr_track_forward_dual_static (include/gsr_glue.h): the static dual forward with SplaTAM's
     tracking L1 loss and its gradient images formed in the render epilogue.  Returns (num_rendered=capacity,
-    color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth, loss, dL_dim, dL_ddepth_sil)."""
+    color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth, loss, dL_dim, dL_ddepth_sil).
+    xform = (means_world, unnorm_rot, logit_opac, log_scales, scale_cols, cam_q_ptr, cam_t_ptr, q_stride, w2c):
+    gsr_track_forward_dual_static_xf -- the tracking transform runs inside preprocess and means3D,
+    colors2, opacity, scales and rotations are its OUTPUTS (preallocated contiguous float32)."""
     st = settings
     device = means3D.device
     P = means3D.size(0)
@@ -449,6 +452,23 @@ def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scale
         if status is None or status.device != device or status.numel() < 4:
             raise RuntimeError("static dual forward needs a device status tensor of 4 int32")
         _begin(device)
+        if xform is not None:
+            outs = (means3D, colors2, opacity, scales, rotations)
+            if any(t is None or not t.is_contiguous() or t.dtype != torch.float32 or t.device != device for t in outs):
+                raise RuntimeError("track_forward_dual_static_xf: the rendervar outputs must be contiguous float32 "
+                                   "tensors on the device")
+            mw, ur, lo, ls, scols, q_ptr, t_ptr, qs, w2c = xform
+            xf = GsrTrackXform(means_world=mw.data_ptr(), unnorm_rot=ur.data_ptr(), logit_opac=lo.data_ptr(),
+                               log_scales=ls.data_ptr(), scale_cols=int(scols), cam_q=q_ptr, cam_t=t_ptr,
+                               q_stride=int(qs), w2c=w2c.data_ptr())
+            n = lib.gsr_track_forward_dual_static_xf(
+                ctypes.byref(s), ctypes.byref(g), _ptr(c2), ctypes.byref(xf), int(capacity), status.data_ptr(),
+                out_color.data_ptr(), out_color2.data_ptr(), out_depth.data_ptr(), radii.data_ptr() if P else None,
+                gi.data_ptr(), gd.data_ptr(), float(sil_thres), float(w_im), float(w_depth), sd.data_ptr(),
+                loss.data_ptr(), dim.data_ptr(), dds.data_ptr(), scratch.data_ptr(), _ALLOC_CB, None, _stream(device))
+            _check(n, "track_forward_dual_static_xf")
+            bufs = _tls.buffers
+            return (int(n), out_color, out_color2, radii, bufs[0], bufs[1], bufs[2], out_depth, loss, dim, dds)
         n = lib.gsr_track_forward_dual_static(
             ctypes.byref(s), ctypes.byref(g), _ptr(c2), int(capacity), status.data_ptr(), out_color.data_ptr(),
             out_color2.data_ptr(), out_depth.data_ptr(), radii.data_ptr() if P else None, gi.data_ptr(),

@@ -41,6 +41,13 @@ class GsrMapAdam(ctypes.Structure):
                 ("capacity", ctypes.c_uint)]
 
 
+class GsrTrackXform(ctypes.Structure):
+    """gsr_track_xform (include/gsr_glue.h)."""
+    _fields_ = [("means_world", c_void_p), ("unnorm_rot", c_void_p), ("logit_opac", c_void_p),
+                ("log_scales", c_void_p), ("scale_cols", c_int), ("cam_q", c_void_p), ("cam_t", c_void_p),
+                ("q_stride", c_int), ("w2c", c_void_p)]
+
+
 class GsrPoseTrack(ctypes.Structure):
     """gsr_pose_track (include/gsr_glue.h)."""
     _fields_ = [("status", c_void_p), ("capacity", ctypes.c_uint), ("loss", c_void_p), ("best", c_void_p)]
@@ -106,6 +113,11 @@ SIGNATURES = {
                                               c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_void_p, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
                                               c_void_p, c_void_p, ALLOC_FN, c_void_p, c_void_p]),
+    "gsr_track_forward_dual_static_xf": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p,
+                                                 ctypes.POINTER(GsrTrackXform), c_int, c_void_p, c_void_p, c_void_p,
+                                                 c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float,
+                                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ALLOC_FN, c_void_p,
+                                                 c_void_p]),
     "gsr_track_backward_scratch_floats": (c_int, [c_int]),
     "gsr_track_backward_dual": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -308,7 +308,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         }
     };
 #if GSR_STEPSTAT
-    unsigned long long st_steps = 0, st_csteps = 0, st_ok = 0, st_pads = 0, st_batches = 0;
+    unsigned long long st_steps = 0, st_csteps = 0, st_ok = 0, st_pads = 0, st_batches = 0, st_items = 0, st_dead = 0;
 #endif
     fetch_entry((int)bmax);
     fetch_rec((int)bmax);
@@ -385,6 +385,16 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 st_pads += pads;
                 st_ok += oks;
                 st_csteps += __ballot(any) != 0ull;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {  // (row, entry) items: listed, and listed with no contributing pixel
+                    const uint64_t okb = __ballot(ok[k]), padb = __ballot(gq.j[k] == BB);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const bool listed = ((padb >> (16 * r)) & 0xFFFFull) == 0ull;
+                        st_items += listed;
+                        st_dead += listed && ((okb >> (16 * r)) & 0xFFFFull) == 0ull;
+                    }
+                }
             }
 #endif
             if (__ballot(any) == 0ull) continue;  // slots stay zero
@@ -495,6 +505,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         atomicAdd(&g_stepstat[2], st_ok);
         atomicAdd(&g_stepstat[3], st_pads);
         atomicAdd(&g_stepstat[4], st_batches);
+        atomicAdd(&g_stepstat[5], st_items);
+        atomicAdd(&g_stepstat[6], st_dead);
     }
 #endif
     GSR_WGTIME_MARK(true);

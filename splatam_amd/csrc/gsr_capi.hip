@@ -295,7 +295,7 @@ size_t gsr_image_buffer_bytes(int W, int H) { return ImgLayout::make(W, H).total
 static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
                         float* out_color, float* out_color2, float* out_depth, int* radii, gsr_alloc_fn alloc,
                         void* alloc_ctx, void* stream_, int capacity = 0, uint32_t* status = nullptr,
-                        const TrackL1* l1 = nullptr) {
+                        const TrackL1* l1 = nullptr, const TrackXf* xf = nullptr) {
     int rc = validate(settings, gaussians, true);
     if (rc != GSR_OK) return rc;
     if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
@@ -308,6 +308,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     Camera cam = make_camera(settings);
     GaussIn g = make_gauss(gaussians);
     g.colors2 = colors2;  // packed into the render records by preprocess (dual render)
+    if (xf) g.xf = *xf;   // tracking transform fused into preprocess (g's arrays are then its outputs)
     const int P = g.P, W = cam.W, H = cam.H;
     const GeomLayout GL = GeomLayout::make(P);
     const ImgLayout IL = ImgLayout::make(W, H);
@@ -651,6 +652,34 @@ int gsr_track_forward_dual_static(const gsr_settings* settings, const gsr_gaussi
     const TrackL1 l1{gt_im, gt_depth, sil_thres, w_im, w_depth, dL_dloss, dL_dim, dL_ddepth_sil, scratch, loss};
     return forward_impl(settings, gaussians, colors2, out_color, out_color2, out_depth, radii, alloc, alloc_ctx,
                         stream, capacity, status, &l1);
+}
+
+int gsr_track_forward_dual_static_xf(const gsr_settings* settings, const gsr_gaussians* gaussians, float* colors2,
+                                     const gsr_track_xform* xform, int capacity, unsigned* status, float* out_color,
+                                     float* out_color2, float* out_depth, int* radii, const float* gt_im,
+                                     const float* gt_depth, float sil_thres, float w_im, float w_depth,
+                                     const float* dL_dloss, float* loss, float* dL_dim, float* dL_ddepth_sil,
+                                     float* scratch, gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
+    if (!xform || !gaussians) return fail(GSR_ERR_INVALID_ARG, "track_forward_dual_static_xf: null pointer");
+    const gsr_track_xform& x = *xform;
+    if ((x.scale_cols != 1 && x.scale_cols != 3) || x.q_stride < 1)
+        return fail(GSR_ERR_INVALID_ARG, "track_forward_dual_static_xf: bad sizes");
+    if (gaussians->P > 0 && (!x.means_world || !x.unnorm_rot || !x.logit_opac || !x.log_scales || !x.cam_q ||
+                             !x.cam_t || !x.w2c || !gaussians->means3D || !gaussians->rotations ||
+                             !gaussians->opacities || !gaussians->scales || !colors2))
+        return fail(GSR_ERR_INVALID_ARG, "track_forward_dual_static_xf: null pointer");
+    if (gaussians->shs || gaussians->cov3D_precomp)
+        return fail(GSR_ERR_INVALID_ARG, "track_forward_dual_static_xf: precomputed colours, scales / rotations only");
+    if (!colors2) return fail(GSR_ERR_INVALID_ARG, "colors2 required");
+    if (capacity <= 0 || !status) return fail(GSR_ERR_INVALID_ARG, "static mode needs capacity > 0 and status");
+    if (!gt_im || !gt_depth || !dL_dloss || !loss || !dL_dim || !dL_ddepth_sil || !scratch)
+        return fail(GSR_ERR_INVALID_ARG, "track_forward_dual_static_xf: null pointer");
+    TrackXf xf;
+    xf.mw = x.means_world; xf.ur = x.unnorm_rot; xf.lo = x.logit_opac; xf.ls = x.log_scales;
+    xf.scols = x.scale_cols; xf.cq = x.cam_q; xf.ct = x.cam_t; xf.qs = x.q_stride; xf.w2c = x.w2c;
+    const TrackL1 l1{gt_im, gt_depth, sil_thres, w_im, w_depth, dL_dloss, dL_dim, dL_ddepth_sil, scratch, loss};
+    return forward_impl(settings, gaussians, colors2, out_color, out_color2, out_depth, radii, alloc, alloc_ctx,
+                        stream, capacity, status, &l1, &xf);
 }
 
 int gsr_track_backward_scratch_floats(int P) { return pose_fuse_scratch_floats(P < 1 ? 1 : P); }

@@ -173,7 +173,24 @@ __device__ __forceinline__ int sched_tile(const Camera& cam) {
     return cam.tile_order ? (int)cam.tile_order[blockIdx.x] : (int)blockIdx.x;
 }
 
+// SplaTAM's tracking transform (gsr_track_transform_fwd) fused into preprocess: the world-frame
+// map + the frame's pose in; preprocess forms the camera-frame rendervars itself and also writes
+// them to GaussIn's means3D / rotations / opacities / scales / colors2 (then outputs) for the
+// backward.  mw == nullptr: no transform (GaussIn holds the rendervars).
+struct TrackXf {
+    const float* mw = nullptr;  // means_world [P,3]
+    const float* ur = nullptr;  // unnorm_rotations [P,4]
+    const float* lo = nullptr;  // logit_opacities [P,1]
+    const float* ls = nullptr;  // log_scales [P,scols]
+    int scols = 1;
+    const float* cq = nullptr;  // the frame's quaternion column (stride qs)
+    const float* ct = nullptr;  // the frame's translation column (stride qs)
+    int qs = 1;
+    const float* w2c = nullptr;  // [16] row-major (depth colours)
+};
+
 struct GaussIn {
+    TrackXf xf;
     int P, M;
     const float* means3D;
     const float* shs;

@@ -12,7 +12,7 @@
 //               LDS batches, block-wide early exit
 #include <cstdlib>
 
-#include "gsr_common.h"
+#include "gsr_glue_common.h"  // (includes gsr_common.h) track_xform_one: the transform-fused preprocess
 
 namespace gsr {
 GSR_WGTIME_TABLE
@@ -23,7 +23,9 @@ GSR_WGTIME_TABLE
 // atomics: ~680k scattered global atomics cost ~30 us on MI355X whatever their
 // contention, tools/micro/atomics.hip).  Otherwise: global atomics on padded
 // per-tile counters (fallback for > MAX_LDS_TILES tiles).
-template <bool LDS_HIST>
+// XF: SplaTAM's tracking transform fused in (g.xf, TrackXf): the camera-frame rendervars are
+// formed here from the world-frame map and the pose, and stored to g's arrays for the backward.
+template <bool LDS_HIST, bool XF>
 __global__ void __launch_bounds__(PRE_BLOCK)
 preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __restrict__ counts, int ntiles) {
 #pragma clang fp contract(off)
@@ -39,7 +41,19 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     float4 q1;
     if (i < g.P) {
         int radius = 0;
-        float3 p = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
+        float3 p;
+        float xs[3], xc2[3], xop = 0.f;
+        float4 xq;
+        if (XF) {  // gsr_track_transform_fwd's outputs, formed in registers (and stored for the backward)
+            const Pose ps = make_pose(g.xf.cq, g.xf.ct, g.xf.qs);
+            float m[3];
+            track_xform_one(g.xf, ps, i, m, xq, xc2, xop, xs, const_cast<float*>(g.means3D),
+                            const_cast<float*>(g.rotations), const_cast<float*>(g.colors2),
+                            const_cast<float*>(g.opacities), const_cast<float*>(g.scales));
+            p = make_float3(m[0], m[1], m[2]);
+        } else {
+            p = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
+        }
         float4 hom = xform4x4(p, cam.proj);
         float pw = 1.0f / (hom.w + 0.0000001f);
         float3 pv = xform4x3(p, cam.view);
@@ -53,8 +67,10 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
 #pragma unroll
                 for (int k = 0; k < 6; k++) cov3[k] = g.cov3D[6 * i + k];
             } else {
-                float3 s = make_float3(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2]);
-                float4 q = make_float4(g.rotations[4 * i], g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3]);
+                float3 s = XF ? make_float3(xs[0], xs[1], xs[2])
+                              : make_float3(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2]);
+                float4 q = XF ? xq : make_float4(g.rotations[4 * i], g.rotations[4 * i + 1], g.rotations[4 * i + 2],
+                                                 g.rotations[4 * i + 3]);
                 cov3d_fwd(s, cam.scale_modifier, q, cov3);
             }
             cov2d_fwd(p, cam.focal_x, cam.focal_y, cam.tan_fovx, cam.tan_fovy, cov3, cam.view, pj);
@@ -83,7 +99,9 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                 }
                 radius = (int)rad;
                 float c2[3] = {0.f, 0.f, 0.f};
-                if (g.colors2) {
+                if (XF) {
+                    c2[0] = xc2[0]; c2[1] = xc2[1]; c2[2] = xc2[2];
+                } else if (g.colors2) {
                     c2[0] = g.colors2[3 * i]; c2[1] = g.colors2[3 * i + 1]; c2[2] = g.colors2[3 * i + 2];
                 }
                 const uint32_t rlo = (uint32_t)x0 | ((uint32_t)y0 << 16), rhi = (uint32_t)x1 | ((uint32_t)y1 << 16);
@@ -91,7 +109,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                 rr[0] = make_float4(px, py, K_AC * ca, K_AC * cc);  // render-record conic form
                 rr[2] = make_float4(rgb[0], rgb[1], rgb[2], __uint_as_float(rlo));
                 rr[3] = make_float4(c2[0], c2[1], c2[2], __uint_as_float(rhi));
-                q1 = make_float4(K_B * cb, g.opacities[i], pv.z, 0.f);  // .w: workgroup-local instance offset, below
+                q1 = make_float4(K_B * cb, XF ? xop : g.opacities[i], pv.z, 0.f);  // .w: workgroup-local instance offset, below
                 geo.bin[i] = make_uint4(rlo, rhi, __float_as_uint(pv.z), tiles);
                 if (!g.sh_staged) geo.clamp[i] = clamped;
                 for (int ty = y0; ty < y1; ty++)  // per-tile instance counts -> bucket ranges
@@ -129,12 +147,11 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
 hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* counts,
                              bool lds_hist, int ntiles, int nb, hipStream_t s) {
     if (nb == 0) return hipSuccess;
-    if (lds_hist)
-        hipLaunchKernelGGL(preprocess_kernel<true>, dim3(nb), dim3(PRE_BLOCK), sizeof(uint32_t) * ntiles, s, cam, g,
-                           geo, radii, counts, ntiles);
-    else
-        hipLaunchKernelGGL(preprocess_kernel<false>, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, g, geo, radii, counts,
-                           ntiles);
+    const bool xf = g.xf.mw != nullptr;
+    auto k = lds_hist ? (xf ? preprocess_kernel<true, true> : preprocess_kernel<true, false>)
+                      : (xf ? preprocess_kernel<false, true> : preprocess_kernel<false, false>);
+    hipLaunchKernelGGL(k, dim3(nb), dim3(PRE_BLOCK), lds_hist ? sizeof(uint32_t) * ntiles : 0, s, cam, g, geo, radii,
+                       counts, ntiles);
     return hipGetLastError();
 }
 

@@ -39,23 +39,11 @@ track_transform_fwd_kernel(int P, const float* __restrict__ mw, const float* __r
     const int i = blockIdx.x * GLUE_BLOCK + threadIdx.x;
     if (i >= P) return;
     const Pose ps = make_pose(cq, ct, qs);
-    const float p0 = mw[3 * i], p1 = mw[3 * i + 1], p2 = mw[3 * i + 2];
-    float m[3];
-#pragma unroll
-    for (int r = 0; r < 3; r++) m[r] = ps.R[r][0] * p0 + ps.R[r][1] * p1 + ps.R[r][2] * p2 + ps.t[r];
-    mc[3 * i] = m[0]; mc[3 * i + 1] = m[1]; mc[3 * i + 2] = m[2];
-    float un_norm;
-    float4 q = normalize4(load4(ur + 4 * i), un_norm);          // F.normalize(unnorm_rotations)
-    if (scols != 1) {                                          // anisotropic: compose with the camera
-        float o_norm;
-        q = normalize4(quat_mult(ps.c, q), o_norm);
-    }
-    rot[4 * i] = q.x; rot[4 * i + 1] = q.y; rot[4 * i + 2] = q.z; rot[4 * i + 3] = q.w;
-    const float z = w2c[8] * m[0] + w2c[9] * m[1] + w2c[10] * m[2] + w2c[11];
-    dcol[3 * i] = z; dcol[3 * i + 1] = 1.f; dcol[3 * i + 2] = z * z;
-    opac[i] = 1.f / (1.f + expf(-lo[i]));
-#pragma unroll
-    for (int k = 0; k < 3; k++) scl[3 * i + k] = expf(ls[scols == 1 ? i : 3 * i + k]);
+    TrackXf x;
+    x.mw = mw; x.ur = ur; x.lo = lo; x.ls = ls; x.scols = scols; x.w2c = w2c;
+    float m[3], c2[3], op, s[3];
+    float4 q;
+    track_xform_one(x, ps, i, m, q, c2, op, s, mc, rot, dcol, opac, scl);
 }
 
 // Pose gradient in one launch: every workgroup publishes its partial of the 16

@@ -64,6 +64,36 @@ __device__ __forceinline__ float4 normalize4_bwd(float4 y, float norm, float4 dy
 
 __device__ __forceinline__ float4 load4(const float* p) { return make_float4(p[0], p[1], p[2], p[3]); }
 
+// One Gaussian of transform_to_frame + the rendervar builders (slam_helpers.py:124-139,196-213,
+// 252-304): camera-frame mean m, rendervar rotation q, depth colours c2 = [z, 1, z^2], opacity op,
+// scales s -- returned and stored at mc / rot / dcol / opac / scl.  Shared by
+// track_transform_fwd_kernel and the transform-fused preprocess (same code, same bits).
+__device__ __forceinline__ void track_xform_one(const TrackXf& x, const Pose& ps, int i, float (&m)[3], float4& q,
+                                                float (&c2)[3], float& op, float (&s)[3], float* mc, float* rot,
+                                                float* dcol, float* opac, float* scl) {
+    const float p0 = x.mw[3 * i], p1 = x.mw[3 * i + 1], p2 = x.mw[3 * i + 2];
+#pragma unroll
+    for (int r = 0; r < 3; r++) m[r] = ps.R[r][0] * p0 + ps.R[r][1] * p1 + ps.R[r][2] * p2 + ps.t[r];
+    mc[3 * i] = m[0]; mc[3 * i + 1] = m[1]; mc[3 * i + 2] = m[2];
+    float un_norm;
+    q = normalize4(load4(x.ur + 4 * i), un_norm);              // F.normalize(unnorm_rotations)
+    if (x.scols != 1) {                                          // anisotropic: compose with the camera
+        float o_norm;
+        q = normalize4(quat_mult(ps.c, q), o_norm);
+    }
+    rot[4 * i] = q.x; rot[4 * i + 1] = q.y; rot[4 * i + 2] = q.z; rot[4 * i + 3] = q.w;
+    const float z = x.w2c[8] * m[0] + x.w2c[9] * m[1] + x.w2c[10] * m[2] + x.w2c[11];
+    c2[0] = z; c2[1] = 1.f; c2[2] = z * z;
+    dcol[3 * i] = c2[0]; dcol[3 * i + 1] = c2[1]; dcol[3 * i + 2] = c2[2];
+    op = 1.f / (1.f + expf(-x.lo[i]));
+    opac[i] = op;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        s[k] = expf(x.ls[x.scols == 1 ? i : 3 * i + k]);
+        scl[3 * i + k] = s[k];
+    }
+}
+
 // Forward-state check of the fused optimizer steps: `st` is a forward's device counters or
 // its static-mode status row ([0] num_rendered, [1] prefiltered violation, [2] longest tile
 // list, [3] longest list the tile sort handled); the forward's outputs (and so the gradients)

@@ -16,10 +16,15 @@ path: these raise on non-ROCm tensors.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
 from ._lib import lib
+
+# tracking transform fused into the rasterizer's preprocess in the static tracking iteration
+# (gsr_track_forward_dual_static_xf); GSR_XF_FUSED=0 runs it as its own launch (A/B, parity tests)
+_XF_FUSED = os.environ.get("GSR_XF_FUSED", "1") != "0"
 
 
 def _check(rc: int, what: str):
@@ -455,16 +460,34 @@ class _TrackIteration(torch.autograd.Function):
         f32 = dict(dtype=torch.float32, device=dev)
         means, rot, dcol = torch.empty(P, 3, **f32), torch.empty(P, 4, **f32), torch.empty(P, 3, **f32)
         opac, scales = torch.empty(P, 1, **f32), torch.empty(P, 3, **f32)
+        rgb = _f32c(params["rgb_colors"].detach(), "rgb_colors")
+        gt_im, gt_d = _f32c(curr["im"], "gt_im"), _f32c(curr["depth"], "gt_depth")
+        H, W = cam.image_height, cam.image_width
+        ctx.pre = None
+        if seed is not None and capacity > 0 and _XF_FUSED:
+            # static mode, static seed: the transform inside preprocess (gsr_track_forward_dual_static_xf),
+            # loss + gradient images in the render epilogue
+            seed = _f32c(seed, "seed")
+            scratch = _scratch(mw, lib.gsr_track_forward_scratch_floats(W, H))
+            xform = (mw, ur, lo, ls, scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c)
+            (n, im, ds, radii, geom, binning, img, _, loss, dim, dds) = _C.track_forward_dual_static(
+                cam, means, rgb, dcol, opac, scales, rot, capacity, status, gt_im, gt_d, cfg.sil_thres, cfg.w_im,
+                cfg.w_depth, seed, scratch, xform=xform)
+            ctx.pre = (dim, dds, seed)
+            ctx.save_for_backward(cam_rots, cam_trans, mw, ur, means, rot, dcol, scales, rgb, radii, geom, binning,
+                                  img, im, ds, gt_im, gt_d, w2c)
+            ctx.meta = (t, T, scols, int(n), cam, cfg)
+            ctx.pose_adam = pose_adam
+            ctx.loss_ptr = loss.data_ptr()
+            ctx.mark_non_differentiable(radii)
+            ctx.set_materialize_grads(False)
+            return loss, radii
         rc = lib.gsr_track_transform_fwd(P, mw.data_ptr(), ur.data_ptr(), lo.data_ptr(), ls.data_ptr(), scols,
                                          cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c.data_ptr(),
                                          means.data_ptr(), rot.data_ptr(), dcol.data_ptr(), opac.data_ptr(),
                                          scales.data_ptr(), _stream(mw))
         _check(rc, "track_transform_fwd")
-        rgb = _f32c(params["rgb_colors"].detach(), "rgb_colors")
         empty = torch.Tensor([])
-        gt_im, gt_d = _f32c(curr["im"], "gt_im"), _f32c(curr["depth"], "gt_depth")
-        H, W = cam.image_height, cam.image_width
-        ctx.pre = None
         if seed is not None and capacity > 0:  # static mode, static seed: loss + gradient images in the render epilogue
             seed = _f32c(seed, "seed")
             scratch = _scratch(mw, lib.gsr_track_forward_scratch_floats(W, H))

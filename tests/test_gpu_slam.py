@@ -226,3 +226,36 @@ def test_render_epilogue_l1_matches_separate_kernel(cuda, aniso):
     assert torch.equal(r0, r1)
     torch.testing.assert_close(q1, q0, rtol=1e-6, atol=1e-9)
     torch.testing.assert_close(t1, t0, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("aniso", [False, True])
+def test_transform_fused_preprocess_bitwise(cuda, aniso, monkeypatch):
+    """gsr_track_forward_dual_static_xf (the tracking transform inside preprocess)
+    against gsr_track_transform_fwd + gsr_track_forward_dual_static: loss, radii, the camera-frame
+    rendervars the forward writes for the backward, and the pose gradients bitwise equal; on a strided
+    pose column (t = 1 of T = 2) with a non-identity w2c."""
+    from splatam_amd import glue
+    from splatam_amd.slam import TrackingConfig
+    params, curr = _setup(cuda, aniso)
+    w2c = torch.eye(4, device=cuda)
+    w2c[:3, 3] = torch.tensor([0.05, -0.02, 0.1], device=cuda)
+    curr = dict(curr, w2c=w2c)
+    seed = torch.ones((), device=cuda)
+    outs = []
+    for fused in (False, True):
+        monkeypatch.setattr(glue, "_XF_FUSED", fused)
+        p = _pose_leaves(params)
+        status = torch.zeros(4, dtype=torch.int32, device=cuda)
+        loss, radii = glue.tracking_iteration(p, curr, 1, TrackingConfig(), capacity=400000, status=status, seed=seed)
+        saved = loss.grad_fn.saved_tensors  # (.., means, rot, dcol, scales, ..)
+        rv = [saved[k].clone() for k in (4, 5, 6, 7)]
+        torch.autograd.backward(loss, seed)
+        outs.append((loss.detach().clone(), radii.clone(), rv, p["cam_unnorm_rots"].grad.clone(),
+                     p["cam_trans"].grad.clone()))
+        assert int(status[1]) == 0 and 0 < int(status[0]) <= 400000
+    (l0, r0, v0, q0, t0), (l1, r1, v1, q1, t1) = outs
+    assert torch.equal(l0, l1) and torch.equal(r0, r1)
+    for a, b in zip(v0, v1):
+        assert torch.equal(a, b)
+    assert torch.equal(q0, q1) and torch.equal(t0, t1)
+    assert float(q1[..., 1].abs().sum()) > 0.0

@@ -40,10 +40,11 @@ def main():
     torch.autograd.backward([im, im2], [g, g2])
     torch.cuda.synchronize()
     assert fn(buf) == 0
-    steps, csteps, ok, pads, batches = (int(buf[i]) for i in range(5))
+    steps, csteps, ok, pads, batches, items, dead = (int(buf[i]) for i in range(7))
     out = {"config": cfg, "wave_steps": steps, "contributing_step_share": csteps / max(steps, 1),
            "contributing_pairs": ok, "contributing_pairs_per_step": ok / max(steps, 1),
-           "pair_slots": 256 * steps, "pad_share": pads / max(256 * steps, 1), "wave_batches": batches}
+           "pair_slots": 256 * steps, "pad_share": pads / max(256 * steps, 1), "wave_batches": batches,
+           "row_items": items, "row_items_without_contribution": dead, "dead_item_share": dead / max(items, 1)}
     print(json.dumps(out))
 
 
