@@ -22,6 +22,9 @@
 #ifndef GSR_ABLATE
 #define GSR_ABLATE 0  // timing ablations (tools/ablate.sh); 0 in every real build
 #endif
+#ifndef GSR_POSE_TAIL
+#define GSR_POSE_TAIL 2  // levels of the fused pose reduction's last-workgroup sum (1 or 2)
+#endif
 
 namespace gsr {
 GSR_WGTIME_TABLE
@@ -651,6 +654,54 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         block_sum<POSE_PARTS>(v, s_red, s_tot);
         __syncthreads();
         if (threadIdx.x < POSE_PARTS) st_agent(pf.part + POSE_PARTS * blockIdx.x + threadIdx.x, s_tot[threadIdx.x]);
+#if GSR_ABLATE == 3
+        return;  // timing ablation: no pose tail (invalid pose update)
+#endif
+#if GSR_POSE_TAIL == 1
+        // One-level fixed-order sum: the last workgroup to arrive (grouped arrival counters) reads
+        // all partials as one coalesced float stream (thread t: floats t, t + 256, ... = value
+        // k = t % 16 of the partials t / 16, t / 16 + 16, ... in order, 40 loads in flight per round
+        // trip), then adds the 16 classes of each value in order through LDS.  Three serial memory
+        // round trips (publish, arrive, gather) instead of the two-level tail's six.
+        {
+            const int nb = gridDim.x;
+            if (!last_block_arrive_grouped(reinterpret_cast<uint32_t*>(pf.part + POSE_PARTS * nb))) return;
+#if GSR_ABLATE == 4
+            return;  // timing ablation: arrival only
+#endif
+            static_assert(256 % POSE_PARTS == 0, "a thread keeps one value index");
+            constexpr int CH = 40;
+            const int total = POSE_PARTS * nb;
+            float acc = 0.f;
+            for (int f0 = threadIdx.x; f0 < total; f0 += CH * 256) {
+                float buf[CH];
+#pragma unroll
+                for (int u = 0; u < CH; u++) {
+                    const int f = f0 + 256 * u;
+                    buf[u] = f < total ? ld_agent(pf.part + f) : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < CH; u++) acc += buf[u];
+            }
+            __shared__ float s_cls[256];
+            s_cls[threadIdx.x] = acc;
+            __syncthreads();
+            if (threadIdx.x < POSE_PARTS) {
+                float t = 0.f;
+#pragma unroll
+                for (int c = 0; c < 256 / POSE_PARTS; c++) t += s_cls[threadIdx.x + POSE_PARTS * c];
+                s_tot[threadIdx.x] = t;
+            }
+            __syncthreads();
+            if (GSR_ABLATE != 5 && threadIdx.x == 0) {  // (5: timing ablation, no pose_fin)
+                const PoseAdam adam{pf.lr_q, pf.lr_t, pf.beta1, pf.beta2, (float)(1.0 - pf.beta1),
+                                    (float)(1.0 - pf.beta2), (float)pf.eps, pf.adam_state, pf.cam_q, pf.cam_t,
+                                    pf.guard, pf.cap, pf.loss, pf.best};
+                pose_fin(s_tot, pf.cam_q, pf.qs, pf.dq, pf.dt, adam);
+            }
+            return;
+        }
+#endif
         // Two-level fixed-order sum of the ~1200 workgroup partials: the last workgroup of each
         // of the 16 arrival groups (b = g mod 16) adds its group's partials (one per thread)
         // and publishes the group sum; the last group then adds the 16 group sums.  (One

@@ -503,8 +503,16 @@ hipError_t launch_identity_order(uint32_t* order, int ntiles, hipStream_t s) {
     return hipGetLastError();
 }
 
+// GSR_DUP_OCC: minimum waves per SIMD (8 = <= 64 VGPRs, two workgroups per CU) spills and measured
+// slower (21.7 vs 19.0 us at config 3), so no bound by default
+#ifndef GSR_DUP_OCC
+#define GSR_DUP_OCC 1
+#endif
+#ifndef GSR_NO_PLAN
+#define GSR_NO_PLAN 0  // timing experiment: row-major render order instead of tile_plan
+#endif
 template <bool LDS_HIST>
-__global__ void __launch_bounds__(PRE_BLOCK)
+__global__ void __launch_bounds__(PRE_BLOCK, GSR_DUP_OCC)
 duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges, const uint32_t* __restrict__ tot,
                         uint32_t* __restrict__ cursor, int ntiles, uint64_t* __restrict__ keys,
                         SpecGuard guard, uint32_t sort_cap, uint32_t* __restrict__ status) {
@@ -613,8 +621,12 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
             }
         }
         if (b == 0 && cam.tile_order_out) {
+#if GSR_NO_PLAN
+            for (int u = tid; u < ntiles; u += PRE_BLOCK) cam.tile_order_out[u] = (uint32_t)u;
+#else
             __shared__ uint32_t s_plan[PLAN_BUCKETS];
             tile_plan(tot, ntiles, cam.sched_cus, cam.tile_order_out, s_plan, wsum);
+#endif
         }
         base = pre;
         if (all > guard.cap_inst || vmax > guard.cap_tile) return;  // workgroup-uniform

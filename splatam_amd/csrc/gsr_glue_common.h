@@ -126,11 +126,58 @@ __device__ __forceinline__ void adam_update(float& p, float g, float& m, float& 
     p = p + neg_step * (m / denom);
 }
 
+// beta^n for the Adam bias corrections, formed in double like torch's python floats: by
+// squaring (n = the step count, an integer; within a few double ulps of pow(), so the float
+// scalars derived from it are the same) -- 1 us faster than the device pow() on the one thread
+// that runs the pose step (GSR_POW_INT=0: pow())
+#ifndef GSR_POW_INT
+#define GSR_POW_INT 1
+#endif
+__device__ __forceinline__ double adam_pow(double b, float step) {
+#if GSR_POW_INT
+    double r = 1.0;
+    for (unsigned n = (unsigned)step; n; n >>= 1) {
+        if (n & 1u) r *= b;
+        b *= b;
+    }
+    return r;
+#else
+    return pow(b, (double)step);
+#endif
+}
+
 // The pose chain on the 16 summed terms S: dR -> dn (build_rotation) -> dc
 // (its own normalisation) -> dq (F.normalize), dt = S[0..2]; then either the
 // gradient is written (dq, dt) or the Adam step is applied in place.
+// Runs in one thread at the end of a launch, so every input (pose, optimizer state, guard
+// counters, loss, best candidate) is loaded up front in one memory round trip, and every
+// result stored at the end: element-wise updates through possibly aliasing pointers had
+// serialised ~6 dependent round trips (~5 us of the fused pose backward).
 __device__ void pose_fin(const float* S, const float* cq, int qs, float* dq, float* dt, const PoseAdam& adam) {
-    const Pose ps = make_pose(cq, nullptr, qs);
+    float qv[4], qa[4] = {0.f, 0.f, 0.f, 0.f}, ta[3] = {0.f, 0.f, 0.f}, st[15];
+    uint32_t gd[4] = {0u, 0u, 0u, 0u};
+    float L = 0.f, b0 = 0.f;
+    const bool fused = adam.state != nullptr;
+    const bool track = fused && adam.loss && adam.best;
+#pragma unroll
+    for (int k = 0; k < 4; k++) qv[k] = cq[k * qs];
+    if (fused) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) qa[k] = adam.q[k * qs];
+#pragma unroll
+        for (int k = 0; k < 3; k++) ta[k] = adam.t[k * qs];
+#pragma unroll
+        for (int k = 0; k < 15; k++) st[k] = adam.state[k];
+        if (adam.guard) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) gd[k] = adam.guard[k];
+        }
+        if (track) {
+            L = *adam.loss;
+            b0 = adam.best[0];
+        }
+    }
+    const Pose ps = make_pose(qv, nullptr, 1);
     // dR[j][k] = S[3 + 3j + k]; R = build_rotation(n), n = (r, x, y, z)
     const float r = ps.n[0], x = ps.n[1], y = ps.n[2], z = ps.n[3];
     const float d00 = S[3], d01 = S[4], d02 = S[5], d10 = S[6], d11 = S[7], d12 = S[8], d20 = S[9], d21 = S[10],
@@ -144,26 +191,33 @@ __device__ void pose_fin(const float* S, const float* cq, int qs, float* dq, flo
     float4 dc = normalize4_bwd(make_float4(ps.n[0], ps.n[1], ps.n[2], ps.n[3]), ps.cn, dn);
     dc.x += S[12]; dc.y += S[13]; dc.z += S[14]; dc.w += S[15];
     const float4 g = normalize4_bwd(make_float4(ps.c[0], ps.c[1], ps.c[2], ps.c[3]), ps.qn, dc);
-    if (adam.state) {  // optimizer step fused here: the pose gradient never leaves the kernel
-        if (forward_overflowed(adam.guard, adam.cap)) return;  // invalid gradients: pose and state unchanged
-        float* st = adam.state;
+    if (fused) {  // optimizer step fused here: the pose gradient never leaves the kernel
+        // forward_overflowed on the preloaded counters: invalid gradients, pose and state unchanged
+        if (adam.guard && (gd[0] > adam.cap || gd[2] > gd[3] || gd[1] != 0u)) return;
         const float step = st[14] + 1.f;
         st[14] = step;
-        const double bc1 = 1.0 - pow(adam.beta1, (double)step);
-        const float bc2_sqrt = (float)sqrt(1.0 - pow(adam.beta2, (double)step));
+        const double bc1 = 1.0 - adam_pow(adam.beta1, step);
+        const float bc2_sqrt = (float)sqrt(1.0 - adam_pow(adam.beta2, step));
         const float ss_q = (float)(-adam.lr_q / bc1), ss_t = (float)(-adam.lr_t / bc1);
         const float gq[4] = {g.x, g.y, g.z, g.w};
-        for (int k = 0; k < 4; k++) adam_update(adam.q[k * qs], gq[k], st[k], st[4 + k], ss_q, adam, bc2_sqrt);
-        for (int k = 0; k < 3; k++) adam_update(adam.t[k * qs], S[k], st[8 + k], st[11 + k], ss_t, adam, bc2_sqrt);
+#pragma unroll
+        for (int k = 0; k < 4; k++) adam_update(qa[k], gq[k], st[k], st[4 + k], ss_q, adam, bc2_sqrt);
+#pragma unroll
+        for (int k = 0; k < 3; k++) adam_update(ta[k], S[k], st[8 + k], st[11 + k], ss_t, adam, bc2_sqrt);
+#pragma unroll
+        for (int k = 0; k < 4; k++) adam.q[k * qs] = qa[k];
+#pragma unroll
+        for (int k = 0; k < 3; k++) adam.t[k * qs] = ta[k];
+#pragma unroll
+        for (int k = 0; k < 15; k++) adam.state[k] = st[k];
         // scripts/splatam.py:726-731: keep the pose after this step if this iteration's loss is the
         // lowest so far (a NaN loss never is, like `loss < current_min_loss`)
-        if (adam.loss && adam.best) {
-            const float L = *adam.loss;
-            if (L < adam.best[0]) {
-                adam.best[0] = L;
-                for (int k = 0; k < 4; k++) adam.best[1 + k] = adam.q[k * qs];
-                for (int k = 0; k < 3; k++) adam.best[5 + k] = adam.t[k * qs];
-            }
+        if (track && L < b0) {
+            adam.best[0] = L;
+#pragma unroll
+            for (int k = 0; k < 4; k++) adam.best[1 + k] = qa[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) adam.best[5 + k] = ta[k];
         }
         return;
     }

@@ -15,6 +15,6 @@ for G in "$G1" "$G2" "$G3"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $G --kernel-include-regex 'render_' -T \
      -d "$ROOT/$OUT/sq$i" -o run --output-format csv \
-     -- python "$ROOT/bench.py" --steps 20 --warmup 20 --cpu-baseline off --dropin off "$@" > "$ROOT/$OUT/sq$i.log" 2>&1
+     -- python "$ROOT/bench.py" --steps 20 --warmup 20 --cpu-baseline off --dropin off --fisher off --mapping off "$@" > "$ROOT/$OUT/sq$i.log" 2>&1
 done
 echo pmc_sq done
