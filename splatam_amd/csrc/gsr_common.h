@@ -724,6 +724,28 @@ __device__ __forceinline__ float ld_agent(const float* p) {
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The last workgroup's fixed-order gather of per-workgroup partials: thread t adds values
+// k < N of part[stride * b + k] for b = t, t + nt, t + 2 nt, ... in that order -- the same
+// sums, bit for bit, as the plain loop (v starts at +0, and the out-of-range slots add +0),
+// but CH partials' loads are in flight per memory round trip (the plain loop waited for each
+// agent-scope load before issuing the next iteration's).
+template <int N, int CH>
+__device__ __forceinline__ void gather_partials(const float* part, int stride, int nb, int t, int nt,
+                                                float (&v)[N]) {
+    for (int b0 = t; b0 < nb; b0 += CH * nt) {
+        float buf[CH][N];
+#pragma unroll
+        for (int u = 0; u < CH; u++) {
+            const int b = b0 + u * nt;
+#pragma unroll
+            for (int k = 0; k < N; k++) buf[u][k] = b < nb ? ld_agent(part + (size_t)stride * b + k) : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < CH; u++)
+#pragma unroll
+            for (int k = 0; k < N; k++) v[k] += buf[u][k];
+    }
+}
 // Same for large grids: 16 group counters (workgroup id mod 16, 64 B apart)
 // and a top counter, so no single address takes more than ~nb/16 atomics
 // (same-address atomics serialise: one counter for 1024 workgroups cost

@@ -508,6 +508,9 @@ hipError_t launch_identity_order(uint32_t* order, int ntiles, hipStream_t s) {
 #ifndef GSR_DUP_OCC
 #define GSR_DUP_OCC 1
 #endif
+#ifndef GSR_L1_CH
+#define GSR_L1_CH 8  // tracking-loss epilogue: partials in flight per round trip of the last workgroup
+#endif
 #ifndef GSR_NO_PLAN
 #define GSR_NO_PLAN 0  // timing experiment: row-major render order instead of tile_plan
 #endif
@@ -1207,9 +1210,11 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         if (tid < 2) st_agent(l1.part + 2 * tile + tid, s_tot[tid]);
         if (last_block_arrive_grouped(reinterpret_cast<uint32_t*>(l1.part + 2 * nb))) {
             v[0] = v[1] = v[2] = v[3] = 0.f;
-            for (int b = tid; b < nb; b += TILE_PIX) {
-                v[0] += ld_agent(l1.part + 2 * b);
-                v[1] += ld_agent(l1.part + 2 * b + 1);
+            {
+                float v2[2] = {0.f, 0.f};
+                gather_partials<2, GSR_L1_CH>(l1.part, 2, nb, tid, TILE_PIX, v2);
+                v[0] = v2[0];
+                v[1] = v2[1];
             }
             wave_reduce_n<4>(v, r);
             if ((lane & 15) == 0) s_red[w * 4 + row4] = r[0];

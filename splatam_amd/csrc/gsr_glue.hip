@@ -80,9 +80,7 @@ track_transform_bwd_kernel(int P, const float* __restrict__ mw, const float* __r
     // last workgroup: fixed-order sum of the partials
 #pragma unroll
     for (int k = 0; k < POSE_PARTS; k++) v[k] = 0.f;
-    for (int b = threadIdx.x; b < nb; b += GLUE_BLOCK)
-#pragma unroll
-        for (int k = 0; k < POSE_PARTS; k++) v[k] += ld_agent(part + POSE_PARTS * b + k);
+    gather_partials<POSE_PARTS, 2>(part, POSE_PARTS, nb, threadIdx.x, GLUE_BLOCK, v);
     __syncthreads();
     block_sum<POSE_PARTS>(v, s_red, s_tot);
     __syncthreads();
@@ -125,9 +123,11 @@ track_l1_kernel(int HW, const float* __restrict__ im, const float* __restrict__ 
     const int nb = gridDim.x;
     if (!last_block_arrive_grouped(reinterpret_cast<uint32_t*>(part + 4 * nb))) return;
     v[0] = v[1] = v[2] = v[3] = 0.f;
-    for (int b = threadIdx.x; b < nb; b += GLUE_BLOCK) {
-        v[0] += ld_agent(part + 4 * b);
-        v[1] += ld_agent(part + 4 * b + 1);
+    {
+        float v2[2] = {0.f, 0.f};
+        gather_partials<2, 4>(part, 4, nb, threadIdx.x, GLUE_BLOCK, v2);
+        v[0] = v2[0];
+        v[1] = v2[1];
     }
     __syncthreads();
     block_sum<4>(v, s_red, s_tot);

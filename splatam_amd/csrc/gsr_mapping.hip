@@ -197,9 +197,7 @@ map_loss_fwd_kernel(int H, int W, const float* __restrict__ im, const float* __r
     if (!last_block_arrive_grouped(reinterpret_cast<uint32_t*>(part + MAP_PARTS * nb))) return;
 #pragma unroll
     for (int k = 0; k < MAP_PARTS; k++) v[k] = 0.f;
-    for (int i = threadIdx.x; i < nb; i += SS_BLOCK)
-#pragma unroll
-        for (int k = 0; k < MAP_PARTS; k++) v[k] += ld_agent(part + MAP_PARTS * i + k);
+    gather_partials<MAP_PARTS, 8>(part, MAP_PARTS, nb, threadIdx.x, SS_BLOCK, v);
     __syncthreads();
     block_sum<MAP_PARTS>(v, s_red, s_tot);
     __syncthreads();
