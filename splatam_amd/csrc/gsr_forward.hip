@@ -471,23 +471,37 @@ __device__ __forceinline__ uint32_t plan_slot(uint32_t p, uint32_t n, uint32_t n
     const uint32_t rd = p / ncu, k = p - rd * ncu, base = rd * ncu, m = min(ncu, n - base);
     return base + (((rd & 1u) || m < ncu) ? m - 1u - k : k);
 }
-// one workgroup of PRE_BLOCK threads; s_hist: PLAN_BUCKETS words of LDS
+// one workgroup of NT threads (PLAN_BUCKETS / NT consecutive buckets per thread); s_hist:
+// PLAN_BUCKETS words of LDS, s_wsum: NT / 64
+template <int NT>
 __device__ void tile_plan(const uint32_t* __restrict__ tot, int ntiles, int ncu, uint32_t* __restrict__ order,
                           uint32_t* s_hist, uint32_t* s_wsum) {
+    constexpr int BPT = PLAN_BUCKETS / NT;
+    static_assert(BPT * NT == PLAN_BUCKETS, "buckets per thread");
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    s_hist[tid] = 0u;
+#pragma unroll
+    for (int k = 0; k < BPT; k++) s_hist[tid * BPT + k] = 0u;
     __syncthreads();
-    for (int u = tid; u < ntiles; u += PRE_BLOCK) atomicAdd(&s_hist[plan_bucket(tot[u])], 1u);
+    for (int u = tid; u < ntiles; u += NT) atomicAdd(&s_hist[plan_bucket(tot[u])], 1u);
     __syncthreads();
-    const uint32_t c = s_hist[tid];
-    const uint32_t incl = wave_incl_scan(c);
+    uint32_t c[BPT], cs = 0;
+#pragma unroll
+    for (int k = 0; k < BPT; k++) {
+        c[k] = s_hist[tid * BPT + k];
+        cs += c[k];
+    }
+    const uint32_t incl = wave_incl_scan(cs);
     if (lane == 63) s_wsum[w] = incl;
     __syncthreads();
-    uint32_t woff = 0;
-    for (int k = 0; k < w; k++) woff += s_wsum[k];
-    s_hist[tid] = woff + incl - c;  // exclusive: first position of the bucket
+    uint32_t run = incl - cs;
+    for (int k = 0; k < w; k++) run += s_wsum[k];
+#pragma unroll
+    for (int k = 0; k < BPT; k++) {  // exclusive: first position of each bucket
+        s_hist[tid * BPT + k] = run;
+        run += c[k];
+    }
     __syncthreads();
-    for (int u = tid; u < ntiles; u += PRE_BLOCK) {
+    for (int u = tid; u < ntiles; u += NT) {
         const uint32_t p = atomicAdd(&s_hist[plan_bucket(tot[u])], 1u);
         order[plan_slot(p, (uint32_t)ntiles, (uint32_t)ncu)] = (uint32_t)u;
     }
@@ -503,11 +517,15 @@ hipError_t launch_identity_order(uint32_t* order, int ntiles, hipStream_t s) {
     return hipGetLastError();
 }
 
-// GSR_DUP_OCC: minimum waves per SIMD (8 = <= 64 VGPRs, two workgroups per CU) spills and measured
-// slower (21.7 vs 19.0 us at config 3), so no bound by default
-#ifndef GSR_DUP_OCC
-#define GSR_DUP_OCC 1
+// DUP_T lanes per workgroup, each placing the instances of DUP_G consecutive Gaussians of a
+// preprocess workgroup's PRE_BLOCK: at 1024 lanes (98 VGPRs, one workgroup per CU) a frame's ~300
+// workgroups took two dispatch rounds on 37 CUs; at 512 two workgroups share a CU (one round).
+// Forcing 1024-lane workgroups to 64 VGPRs instead spilled and was slower.
+#ifndef GSR_DUP_THREADS
+#define GSR_DUP_THREADS 512
 #endif
+constexpr int DUP_T = GSR_DUP_THREADS, DUP_G = PRE_BLOCK / DUP_T;
+static_assert(DUP_G * DUP_T == PRE_BLOCK && DUP_T % 64 == 0, "duplicate workgroup shape");
 #ifndef GSR_L1_CH
 #define GSR_L1_CH 8  // tracking-loss epilogue: partials in flight per round trip of the last workgroup
 #endif
@@ -515,7 +533,7 @@ hipError_t launch_identity_order(uint32_t* order, int ntiles, hipStream_t s) {
 #define GSR_NO_PLAN 0  // timing experiment: row-major render order instead of tile_plan
 #endif
 template <bool LDS_HIST>
-__global__ void __launch_bounds__(PRE_BLOCK, GSR_DUP_OCC)
+__global__ void __launch_bounds__(DUP_T)
 duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges, const uint32_t* __restrict__ tot,
                         uint32_t* __restrict__ cursor, int ntiles, uint64_t* __restrict__ keys,
                         SpecGuard guard, uint32_t sort_cap, uint32_t* __restrict__ status) {
@@ -524,12 +542,17 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
     extern __shared__ uint32_t s_cur[];
     __shared__ uint32_t s_incl[PRE_BLOCK];
     __shared__ uint32_t s_x0[PRE_BLOCK], s_y0[PRE_BLOCK], s_w[PRE_BLOCK], s_depth[PRE_BLOCK];
-    __shared__ uint32_t wsum[PRE_BLOCK / 64];
+    __shared__ uint32_t wsum[DUP_T / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int i = blockIdx.x * PRE_BLOCK + tid;
-    // the Gaussian's tile count and rect, loaded ahead of the prologue's loads (one round trip)
-    const uint32_t t = (i < P) ? geo.tiles[i] : 0u;
-    const uint4 r = (i < P) ? geo.bin[i] : make_uint4(0u, 0u, 0u, 0u);  // (rect lo, rect hi, depth bits, tiles)
+    const int i0 = blockIdx.x * PRE_BLOCK + DUP_G * tid;  // this lane's Gaussians i0 .. i0 + DUP_G - 1
+    // the Gaussians' tile counts and rects, loaded ahead of the prologue's loads (one round trip)
+    uint32_t t[DUP_G];
+    uint4 r[DUP_G];
+#pragma unroll
+    for (int g = 0; g < DUP_G; g++) {
+        t[g] = (i0 + g < P) ? geo.tiles[i0 + g] : 0u;
+        r[g] = (i0 + g < P) ? geo.bin[i0 + g] : make_uint4(0u, 0u, 0u, 0u);  // (rect lo, rect hi, depth bits, tiles)
+    }
     uint32_t base;
     if (LDS_HIST) {
         // The scans of scan_counts_body, redone by every workgroup (the inputs are
@@ -537,10 +560,10 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         // workgroup totals, num_rendered, the prefiltered flag, and the exclusive
         // scan of the tile totals (bucket starts).  Workgroup 0 publishes them
         // (ranges, counters, status) for the later launches and the host.
-        constexpr int TPT = 4;  // tiles per thread kept in registers (<= 4096 tiles), else staged in LDS
-        __shared__ uint32_t s_red[5][PRE_BLOCK / 64];
+        constexpr int TPT = 4;  // tiles per thread kept in registers (<= 4 DUP_T tiles), else staged in LDS
+        __shared__ uint32_t s_red[5][DUP_T / 64];
         const uint32_t b = blockIdx.x, nb = gridDim.x;
-        const int per = (ntiles + PRE_BLOCK - 1) / PRE_BLOCK;  // contiguous tiles per thread
+        const int per = (ntiles + DUP_T - 1) / DUP_T;  // contiguous tiles per thread
         const int t0 = min(ntiles, tid * per), t1 = min(ntiles, t0 + per);
         const bool in_regs = per <= TPT;
         uint32_t tv[TPT], cv[TPT];
@@ -551,7 +574,7 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
             cv[k] = ok ? cursor[(size_t)b * ntiles + t0 + k] : 0u;
         }
         uint32_t pre = 0, all = 0, viol = 0, vmax = 0;
-        for (uint32_t k = tid; k < nb; k += PRE_BLOCK) {
+        for (uint32_t k = tid; k < nb; k += DUP_T) {
             const uint32_t v = geo.wgsum[k];
             viol |= v >> 31;
             all += v & 0x7fffffffu;
@@ -588,7 +611,7 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         uint32_t woff = 0;
         pre = all = viol = vmax = 0;
 #pragma unroll
-        for (int k = 0; k < PRE_BLOCK / 64; k++) {
+        for (int k = 0; k < DUP_T / 64; k++) {
             pre += s_red[0][k];
             all += s_red[1][k];
             viol |= s_red[2][k];
@@ -625,10 +648,10 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         }
         if (b == 0 && cam.tile_order_out) {
 #if GSR_NO_PLAN
-            for (int u = tid; u < ntiles; u += PRE_BLOCK) cam.tile_order_out[u] = (uint32_t)u;
+            for (int u = tid; u < ntiles; u += DUP_T) cam.tile_order_out[u] = (uint32_t)u;
 #else
             __shared__ uint32_t s_plan[PLAN_BUCKETS];
-            tile_plan(tot, ntiles, cam.sched_cus, cam.tile_order_out, s_plan, wsum);
+            tile_plan<DUP_T>(tot, ntiles, cam.sched_cus, cam.tile_order_out, s_plan, wsum);
 #endif
         }
         base = pre;
@@ -637,23 +660,33 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         if (guard.overflow()) return;
         base = geo.blocksums[blockIdx.x];
     }
-    uint32_t incl = wave_incl_scan(t);
+    uint32_t tsum = 0;
+#pragma unroll
+    for (int g = 0; g < DUP_G; g++) {
+        tsum += t[g];
+        const int q = DUP_G * tid + g;
+        if (t[g]) {
+            s_x0[q] = r[g].x & 0xFFFFu;
+            s_y0[q] = r[g].x >> 16;
+            s_w[q] = (r[g].y & 0xFFFFu) - (r[g].x & 0xFFFFu);
+            s_depth[q] = r[g].z;
+        }
+    }
+    uint32_t incl = wave_incl_scan(tsum);
+    __syncthreads();  // (wsum is also tile_plan's scratch)
     if (lane == 63) wsum[w] = incl;
-    if (t) {
-        s_x0[tid] = r.x & 0xFFFFu;
-        s_y0[tid] = r.x >> 16;
-        s_w[tid] = (r.y & 0xFFFFu) - (r.x & 0xFFFFu);
-        s_depth[tid] = r.z;
+    __syncthreads();
+    uint32_t run = incl - tsum;
+    for (int k = 0; k < w; k++) run += wsum[k];
+#pragma unroll
+    for (int g = 0; g < DUP_G; g++) {  // Gaussian order: the workgroup-local instance offsets of preprocess
+        if (i0 + g < P) geo.offsets[i0 + g] = base + run;
+        run += t[g];
+        s_incl[DUP_G * tid + g] = run;
     }
     __syncthreads();
-    uint32_t woff = 0;
-    for (int k = 0; k < w; k++) woff += wsum[k];
-    incl += woff;
-    s_incl[tid] = incl;
-    if (i < P) geo.offsets[i] = base + incl - t;
-    __syncthreads();
     const uint32_t total = s_incl[PRE_BLOCK - 1];
-    for (uint32_t e = tid; e < total; e += PRE_BLOCK) {
+    for (uint32_t e = tid; e < total; e += DUP_T) {
         int lo = 0, hi = PRE_BLOCK - 1;
         while (lo < hi) {
             int mid = (lo + hi) >> 1;
@@ -674,10 +707,10 @@ hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2
                                    SpecGuard guard, uint32_t* status, hipStream_t s) {
     if (nb == 0) return hipSuccess;
     if (lds_hist)
-        hipLaunchKernelGGL(duplicate_bucket_kernel<true>, dim3(nb), dim3(PRE_BLOCK), sizeof(uint32_t) * ntiles, s, cam,
+        hipLaunchKernelGGL(duplicate_bucket_kernel<true>, dim3(nb), dim3(DUP_T), sizeof(uint32_t) * ntiles, s, cam,
                            P, geo, ranges, tot, cursor, ntiles, keys, guard, (uint32_t)TILE_SORT_CAP, status);
     else
-        hipLaunchKernelGGL(duplicate_bucket_kernel<false>, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, ranges, tot,
+        hipLaunchKernelGGL(duplicate_bucket_kernel<false>, dim3(nb), dim3(DUP_T), 0, s, cam, P, geo, ranges, tot,
                            cursor, ntiles, keys, guard, (uint32_t)TILE_SORT_CAP, status);
     return hipGetLastError();
 }
