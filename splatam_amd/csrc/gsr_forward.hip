@@ -30,10 +30,21 @@ __global__ void __launch_bounds__(PRE_BLOCK)
 preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __restrict__ counts, int ntiles) {
 #pragma clang fp contract(off)
     extern __shared__ uint32_t s_hist[];
-    if (LDS_HIST) {
-        for (int t = threadIdx.x; t < ntiles; t += PRE_BLOCK) s_hist[t] = 0u;
-        __syncthreads();
+    __shared__ float s_pose[16];  // XF: the frame's pose (R 9, t 3, F.normalize(q) 4), formed once by wave 0
+    if (XF && threadIdx.x < 64) {
+        const Pose ps = make_pose(g.xf.cq, g.xf.ct, g.xf.qs);
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int k = 0; k < 9; k++) s_pose[k] = ps.R[k / 3][k % 3];
+#pragma unroll
+            for (int k = 0; k < 3; k++) s_pose[9 + k] = ps.t[k];
+#pragma unroll
+            for (int k = 0; k < 4; k++) s_pose[12 + k] = ps.c[k];
+        }
     }
+    if (LDS_HIST)
+        for (int t = threadIdx.x; t < ntiles; t += PRE_BLOCK) s_hist[t] = 0u;
+    if (LDS_HIST || XF) __syncthreads();
     const int i = blockIdx.x * PRE_BLOCK + threadIdx.x;
     if (i == 0) geo.counters[4] = 0u;  // tile_colscan_kernel's arrival counter (next launch)
     uint32_t tiles = 0;
@@ -45,7 +56,13 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
         float xs[3], xc2[3], xop = 0.f;
         float4 xq;
         if (XF) {  // gsr_track_transform_fwd's outputs, formed in registers (and stored for the backward)
-            const Pose ps = make_pose(g.xf.cq, g.xf.ct, g.xf.qs);
+            Pose ps;  // (track_xform_one reads R, t and c)
+#pragma unroll
+            for (int k = 0; k < 9; k++) ps.R[k / 3][k % 3] = s_pose[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) ps.t[k] = s_pose[9 + k];
+#pragma unroll
+            for (int k = 0; k < 4; k++) ps.c[k] = s_pose[12 + k];
             float m[3];
             track_xform_one(g.xf, ps, i, m, xq, xc2, xop, xs, const_cast<float*>(g.means3D),
                             const_cast<float*>(g.rotations), const_cast<float*>(g.colors2),
