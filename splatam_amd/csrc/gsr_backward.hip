@@ -90,10 +90,13 @@ __device__ __forceinline__ void reduce_store(const float (&v)[4 * N], int lane, 
 #ifndef GSR_BWD_BB
 #define GSR_BWD_BB 128  // batch of the variants with <= 6 sums (timing experiments may override)
 #endif
+#ifndef GSR_BWD_WBB
+#define GSR_BWD_WBB 96  // batch of the wide variants (> 6 sums): 96 measured faster than 64 (mapping render_bwd 362 -> 326 us) at 5 waves/SIMD; 128 drops to 4
+#endif
 template <int NV>
-constexpr int bwd_batch() { return NV <= 6 ? GSR_BWD_BB : 64; }
+constexpr int bwd_batch() { return NV <= 6 ? GSR_BWD_BB : GSR_BWD_WBB; }
 template <int NV>
-constexpr int bwd_slots() { return NV <= 6 ? 4 * GSR_BWD_BB : 256; }
+constexpr int bwd_slots() { return NV <= 6 ? 4 * GSR_BWD_BB : 4 * GSR_BWD_WBB; }
 
 // Per-wave row lists of one batch: row r of wave w (tile block b = 4w + r) lists the entries j
 // (< cnt) whose block mask has bit b and that lie before the block's last contributor (j >=
