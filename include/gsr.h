@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 3
+#define GSR_ABI_VERSION 4
 
 /* error codes */
 #define GSR_OK 0

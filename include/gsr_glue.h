@@ -135,7 +135,9 @@ int gsr_track_forward_dual_static(const gsr_settings* settings, const gsr_gaussi
  * back.  Same results, bit for bit, as gsr_track_transform_fwd(xform -> gaussians->means3D,
  * ->rotations, colors2, ->opacities, ->scales) followed by gsr_track_forward_dual_static with
  * those arrays: here they are OUTPUTS (written by the forward, device [P,3] / [P,4] / [P,3] /
- * [P,1] / [P,3]) for the backward (gsr_track_backward_dual).  gaussians->colors_precomp: the
+ * [P,1] / [P,3]) for the backward (gsr_track_backward_dual), unless store_rendervars is 0: then
+ * nothing is written to them (storing them cost preprocess ~6 us at 300 k Gaussians) and the
+ * backward recomputes the geometric ones from the world-frame map (its log_scales argument).  gaussians->colors_precomp: the
  * RGB colours [P,3] (input); shs and cov3D_precomp must be NULL. */
 typedef struct gsr_track_xform {
     const float* means_world;  /* [P,3] */
@@ -147,6 +149,8 @@ typedef struct gsr_track_xform {
     const float* cam_t;        /* the frame's translation, likewise */
     int q_stride;
     const float* w2c;          /* [4,4] row-major: depth colours */
+    int store_rendervars;      /* 1: write the rendervars (outputs below); 0: do not -- the
+                                  backward then recomputes them (gsr_track_backward_dual log_scales) */
 } gsr_track_xform;
 
 int gsr_track_forward_dual_static_xf(const gsr_settings* settings, const gsr_gaussians* gaussians, float* colors2,
@@ -170,7 +174,11 @@ int gsr_track_forward_dual_static_xf(const gsr_settings* settings, const gsr_gau
  * gsr_track_backward_scratch_floats(P) floats, zero-filled before first use,
  * left zero-filled.  The Adam step is skipped when the forward's own device
  * counters show an overflow of num_rendered (its capacity); `track` (may be
- * NULL) adds the best-candidate selection (its status / capacity are not used). */
+ * NULL) adds the best-candidate selection (its status / capacity are not used).
+ * log_scales [P, scale_cols] (may be NULL): recompute each Gaussian's camera-frame mean, rotation
+ * and scale from means_world / unnorm_rot / log_scales and the frame's (pre-step) pose instead of
+ * reading gaussians->means3D / rotations / scales -- for a forward that did not store them
+ * (gsr_track_forward_dual_static_xf with store_rendervars = 0); bitwise the same values. */
 int gsr_track_backward_scratch_floats(int P);
 int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
                             const float* colors2, const float* dL_dout_color, const float* dL_dout_color2,
@@ -179,7 +187,7 @@ int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* g
                             int scale_cols, float* cam_q, float* cam_t, int q_stride, const float* w2c, double lr_q,
                             double lr_t, double beta1, double beta2, double eps, float* adam_state,
                             float* dL_dcam_q, float* dL_dcam_t, float* scratch, const gsr_pose_track* track,
-                            gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+                            const float* log_scales, gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
 /* ------------------------------------------------------------------ mapping --
  * get_loss(mapping=True, do_ba=False) (scripts/splatam.py:220-353) with the

@@ -393,11 +393,14 @@ def mark_visible(means3D, viewmatrix, projmatrix):
 
 def track_backward_dual(settings, means3D, radii, colors, colors2, scales, rotations, dL_dout_color, dL_dout_color2,
                         geomBuffer, R, binningBuffer, imageBuffer, means_world, unnorm_rot, scale_cols, cam_q_ptr,
-                        cam_t_ptr, q_stride, w2c, scratch, adam=None, dq_ptr=None, dt_ptr=None, track=None):
+                        cam_t_ptr, q_stride, w2c, scratch, adam=None, dq_ptr=None, dt_ptr=None, track=None,
+                        log_scales=None):
     """gsr_track_backward_dual (include/gsr_glue.h): the tracking backward with the pose chain fused into
     the per-Gaussian backward.  adam = (lr_q, lr_t, beta1, beta2, eps, state tensor) applies the Adam step
     to the pose in place; otherwise the pose gradient is written at dq_ptr / dt_ptr.  track: an optional
-    GsrPoseTrack (best-candidate selection; the Adam step is skipped on an overflowing forward)."""
+    GsrPoseTrack (best-candidate selection; the Adam step is skipped on an overflowing forward).
+    log_scales: recompute the rendervars (means3D / rotations / scales) from the world-frame map
+    instead of reading them (a forward run with store_rendervars = 0)."""
     device = means3D.device
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     with torch.cuda.device(device):
@@ -419,7 +422,8 @@ def track_backward_dual(settings, means3D, radii, colors, colors2, scales, rotat
             imageBuffer.data_ptr(), means_world.data_ptr(), unnorm_rot.data_ptr(), int(scale_cols),
             cam_q_ptr, cam_t_ptr, int(q_stride), w2c.data_ptr(), float(lr_q), float(lr_t), float(b1), float(b2),
             float(eps), state.data_ptr() if state is not None else None, dq_ptr, dt_ptr, scratch.data_ptr(),
-            ctypes.byref(track) if track is not None else None, _ALLOC_CB, None, _stream(device))
+            ctypes.byref(track) if track is not None else None,
+            log_scales.data_ptr() if log_scales is not None else None, _ALLOC_CB, None, _stream(device))
         _check(rc, "track_backward_dual")
         _tls.buffers = {}
 
@@ -429,9 +433,10 @@ def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scale
     """gsr_track_forward_dual_static (include/gsr_glue.h): the static dual forward with SplaTAM's
     tracking L1 loss and its gradient images formed in the render epilogue.  Returns (num_rendered=capacity,
     color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth, loss, dL_dim, dL_ddepth_sil).
-    xform = (means_world, unnorm_rot, logit_opac, log_scales, scale_cols, cam_q_ptr, cam_t_ptr, q_stride, w2c):
-    gsr_track_forward_dual_static_xf -- the tracking transform runs inside preprocess and means3D,
-    colors2, opacity, scales and rotations are its OUTPUTS (preallocated contiguous float32)."""
+    xform = (means_world, unnorm_rot, logit_opac, log_scales, scale_cols, cam_q_ptr, cam_t_ptr, q_stride, w2c,
+    store): gsr_track_forward_dual_static_xf -- the tracking transform runs inside preprocess and means3D,
+    colors2, opacity, scales and rotations are its OUTPUTS (preallocated contiguous float32; written only
+    when store is true)."""
     st = settings
     device = means3D.device
     P = means3D.size(0)
@@ -457,10 +462,10 @@ def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scale
             if any(t is None or not t.is_contiguous() or t.dtype != torch.float32 or t.device != device for t in outs):
                 raise RuntimeError("track_forward_dual_static_xf: the rendervar outputs must be contiguous float32 "
                                    "tensors on the device")
-            mw, ur, lo, ls, scols, q_ptr, t_ptr, qs, w2c = xform
+            mw, ur, lo, ls, scols, q_ptr, t_ptr, qs, w2c, store = xform
             xf = GsrTrackXform(means_world=mw.data_ptr(), unnorm_rot=ur.data_ptr(), logit_opac=lo.data_ptr(),
                                log_scales=ls.data_ptr(), scale_cols=int(scols), cam_q=q_ptr, cam_t=t_ptr,
-                               q_stride=int(qs), w2c=w2c.data_ptr())
+                               q_stride=int(qs), w2c=w2c.data_ptr(), store_rendervars=int(bool(store)))
             n = lib.gsr_track_forward_dual_static_xf(
                 ctypes.byref(s), ctypes.byref(g), _ptr(c2), ctypes.byref(xf), int(capacity), status.data_ptr(),
                 out_color.data_ptr(), out_color2.data_ptr(), out_depth.data_ptr(), radii.data_ptr() if P else None,

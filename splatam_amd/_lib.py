@@ -45,7 +45,7 @@ class GsrTrackXform(ctypes.Structure):
     """gsr_track_xform (include/gsr_glue.h)."""
     _fields_ = [("means_world", c_void_p), ("unnorm_rot", c_void_p), ("logit_opac", c_void_p),
                 ("log_scales", c_void_p), ("scale_cols", c_int), ("cam_q", c_void_p), ("cam_t", c_void_p),
-                ("q_stride", c_int), ("w2c", c_void_p)]
+                ("q_stride", c_int), ("w2c", c_void_p), ("store_rendervars", c_int)]
 
 
 class GsrPoseTrack(ctypes.Structure):
@@ -123,7 +123,7 @@ SIGNATURES = {
                                         c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_int, c_void_p, c_void_p, c_int, c_void_p, c_double, c_double, c_double,
                                         c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
-                                        ctypes.POINTER(GsrPoseTrack), ALLOC_FN, c_void_p, c_void_p]),
+                                        ctypes.POINTER(GsrPoseTrack), c_void_p, ALLOC_FN, c_void_p, c_void_p]),
     # include/gsr_glue.h: fused SplaTAM mapping glue and optimizer
     "gsr_map_loss_scratch_floats": (c_int, [c_int, c_int]),
     "gsr_map_loss_state_floats": (c_int, [c_int, c_int]),
@@ -150,7 +150,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.gsr_abi_version() != 3:
+    if lib.gsr_abi_version() != 4:
         raise ImportError("libgsr.so ABI version mismatch")
     return lib
 

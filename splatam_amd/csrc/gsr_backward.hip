@@ -581,6 +581,25 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     float dsh[48];
 #pragma unroll
     for (int k = 0; k < 48; k++) dsh[k] = 0.f;
+    // the Gaussian's geometry: recomputed from the world-frame map and the pre-step pose (tracking
+    // forward that did not store its rendervars, PoseFuse::ls) or read from GaussIn
+    GaussGeom gg;
+    gg.m = make_float3(0.f, 0.f, 0.f);
+    gg.s = make_float3(0.f, 0.f, 0.f);
+    gg.q = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (live && (POSE || radii[i] > 0)) {  // (the pose sums need every live Gaussian's mean)
+        if (POSE && pf.ls) {
+            TrackXf x;
+            x.mw = pf.means_world; x.ur = pf.unnorm_rot; x.ls = pf.ls; x.scols = pf.scols;
+            const Pose ps = make_pose(pf.cam_q, pf.cam_t, pf.qs);
+            float m[3], sv[3];
+            track_xform_geom(x, ps, i, m, gg.q, sv);
+            gg.m = make_float3(m[0], m[1], m[2]);
+            gg.s = make_float3(sv[0], sv[1], sv[2]);
+        } else {
+            gg = load_geom(g, i);
+        }
+    }
     if (live && radii[i] > 0 && !guard.overflow()) {  // overflow: zero gradients, no record reads
         const uint32_t off = geo.offsets[i], cnt = geo.tiles[i];
         // fixed-order sum of the Gaussian's instance records (deterministic)
@@ -626,7 +645,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         // the conic is recomputed exactly as preprocess computed it (the render record keeps
         // only its exp2-scaled form)
         float ca, cb, cc;
-        gaussian_conic(cam, g, i, ca, cb, cc);
+        gaussian_conic(cam, g, gg, i, ca, cb, cc);
         const float ddelx = (float)(0.5 * cam.W), ddely = (float)(0.5 * cam.H);  // backward.cu:935-936
         const float hx = g2[0], hy = g2[1];
         g2[0] = -(ca * hx + cb * hy) * ddelx;
@@ -635,7 +654,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         g2[3] *= -0.5f;
         g2[4] *= -0.5f;
         const unsigned clamped = geo.clamp[i];
-        gauss_chain(cam, g, i, g2, clamped, dmean, dcov, dscale, drot, dsh, nsh);
+        gauss_chain(cam, g, gg, i, g2, clamped, dmean, dcov, dscale, drot, dsh, nsh);
     }
     if constexpr (POSE) {
         // tracking: the pose sums of this Gaussian (track_transform_bwd_kernel's, gsr_glue.hip), then
@@ -651,9 +670,11 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
 #pragma unroll
             for (int k = 0; k < 4; k++) c[k] = ps.c[k];
         }
-        if (live)
-            pose_partials(v, i, dmean, dcol2, pf.scols != 1 ? drot : nullptr, pf.means_world, pf.unnorm_rot,
-                          g.means3D, pf.w2c, c);
+        if (live) {
+            const float mci[3] = {gg.m.x, gg.m.y, gg.m.z};
+            pose_partials_m(v, i, dmean, dcol2, pf.scols != 1 ? drot : nullptr, pf.means_world, pf.unnorm_rot, mci,
+                            pf.w2c, c);
+        }
         block_sum<POSE_PARTS>(v, s_red, s_tot);
         __syncthreads();
         if (threadIdx.x < POSE_PARTS) st_agent(pf.part + POSE_PARTS * blockIdx.x + threadIdx.x, s_tot[threadIdx.x]);

@@ -677,6 +677,7 @@ int gsr_track_forward_dual_static_xf(const gsr_settings* settings, const gsr_gau
     TrackXf xf;
     xf.mw = x.means_world; xf.ur = x.unnorm_rot; xf.lo = x.logit_opac; xf.ls = x.log_scales;
     xf.scols = x.scale_cols; xf.cq = x.cam_q; xf.ct = x.cam_t; xf.qs = x.q_stride; xf.w2c = x.w2c;
+    xf.store = x.store_rendervars != 0;
     const TrackL1 l1{gt_im, gt_depth, sil_thres, w_im, w_depth, dL_dloss, dL_dim, dL_ddepth_sil, scratch, loss};
     return forward_impl(settings, gaussians, colors2, out_color, out_color2, out_depth, radii, alloc, alloc_ctx,
                         stream, capacity, status, &l1, &xf);
@@ -691,7 +692,7 @@ int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* g
                             int scale_cols, float* cam_q, float* cam_t, int q_stride, const float* w2c, double lr_q,
                             double lr_t, double beta1, double beta2, double eps, float* adam_state,
                             float* dL_dcam_q, float* dL_dcam_t, float* scratch, const gsr_pose_track* track,
-                            gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
+                            const float* log_scales, gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
     if (!gaussians || (scale_cols != 1 && scale_cols != 3) || q_stride < 1)
         return fail(GSR_ERR_INVALID_ARG, "track_backward_dual: bad sizes");
     if (!colors2 || !means_world || !unnorm_rot || !cam_q || !cam_t || !w2c || !scratch ||
@@ -702,6 +703,7 @@ int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* g
     PoseFuse pf{means_world, unnorm_rot, scale_cols, cam_q, cam_t, q_stride, w2c, scratch, adam_state,
                 lr_q, lr_t, beta1, beta2, eps, dL_dcam_q, dL_dcam_t};
     pf.cap = (uint32_t)num_rendered;  // pf.guard = the forward's counters (backward_impl)
+    pf.ls = log_scales;               // recompute the rendervars (forward without stored rendervars)
     if (track) {
         pf.loss = track->loss;
         pf.best = track->best;

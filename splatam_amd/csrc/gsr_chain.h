@@ -5,21 +5,43 @@
 
 namespace gsr {
 
+// The geometric inputs of Gaussian i: mean, and scale / rotation (when no cov3D is given) -- loaded
+// from GaussIn, or recomputed from the world-frame map by the tracking backward (TrackXf).
+struct GaussGeom {
+    float3 m;
+    float3 s;
+    float4 q;
+};
+__device__ __forceinline__ GaussGeom load_geom(const GaussIn& g, int i) {
+    GaussGeom r;
+    r.m = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
+    if (g.scales && g.rotations) {
+        r.s = make_float3(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2]);
+        r.q = make_float4(g.rotations[4 * i], g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3]);
+    } else {
+        r.s = make_float3(0.f, 0.f, 0.f);
+        r.q = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    return r;
+}
+
 // Conic of Gaussian i as preprocess computed it (same helpers, same inputs).
-__device__ inline void gaussian_conic(const Camera& cam, const GaussIn& g, int i, float& ca, float& cb, float& cc) {
-    const float3 m = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
+__device__ inline void gaussian_conic(const Camera& cam, const GaussIn& g, const GaussGeom& gg, int i, float& ca,
+                                      float& cb, float& cc) {
+    const float3 m = gg.m;
     float c3[6];
     if (g.cov3D) {
 #pragma unroll
         for (int k = 0; k < 6; k++) c3[k] = g.cov3D[6 * i + k];
     } else {
-        float3 s = make_float3(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2]);
-        float4 q = make_float4(g.rotations[4 * i], g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3]);
-        cov3d_fwd(s, cam.scale_modifier, q, c3);
+        cov3d_fwd(gg.s, cam.scale_modifier, gg.q, c3);
     }
     Proj pj;
     cov2d_fwd(m, cam.focal_x, cam.focal_y, cam.tan_fovx, cam.tan_fovy, c3, cam.view, pj);
     (void)conic_of(pj, ca, cb, cc);
+}
+__device__ inline void gaussian_conic(const Camera& cam, const GaussIn& g, int i, float& ca, float& cb, float& cc) {
+    gaussian_conic(cam, g, load_geom(g, i), i, ca, cb, cc);
 }
 
 // SH backward (backward.cu:20-139) for one Gaussian: sh = its 3*M coefficients
@@ -92,18 +114,17 @@ __device__ __forceinline__ void sh_chain_bwd(const Camera& cam, float3 m, const 
 // ------------------------------------------------------ per-Gaussian chain --
 // g2: [0..1] dL/dmean2D (NDC units), [2..4] dL/dconic (A, B/2, C), [5] dL/dopacity,
 // [6..8] dL/dcolor.  Outputs: dmean3D[3], dcov3D[6], dscale[3], drot[4], dsh[3*nsh].
-__device__ inline void gauss_chain(const Camera& cam, const GaussIn& g, int i, const float g2[9], unsigned clamped,
-                            float dmean[3], float dcov[6], float dscale[3], float drot[4], float* dsh_out, int nsh) {
+__device__ inline void gauss_chain(const Camera& cam, const GaussIn& g, const GaussGeom& gg, int i, const float g2[9],
+                                   unsigned clamped, float dmean[3], float dcov[6], float dscale[3], float drot[4],
+                                   float* dsh_out, int nsh) {
     const float fx = cam.focal_x, fy = cam.focal_y;
-    const float3 m = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
+    const float3 m = gg.m;
     float c3[6];
     if (g.cov3D) {
 #pragma unroll
         for (int k = 0; k < 6; k++) c3[k] = g.cov3D[6 * i + k];
     } else {
-        float3 s = make_float3(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2]);
-        float4 q = make_float4(g.rotations[4 * i], g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3]);
-        cov3d_fwd(s, cam.scale_modifier, q, c3);
+        cov3d_fwd(gg.s, cam.scale_modifier, gg.q, c3);
     }
     // computeCov2DCUDA (backward.cu:144-274)
     Proj pj;
@@ -169,12 +190,11 @@ __device__ inline void gauss_chain(const Camera& cam, const GaussIn& g, int i, c
 #pragma unroll
     for (int k = 0; k < 4; k++) drot[k] = 0.f;
     if (g.scales) {
-        const float4 q = make_float4(g.rotations[4 * i], g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3]);
+        const float4 q = gg.q;
         const float r = q.x, x = q.y, y = q.z, z = q.w;
         float R[3][3];
         rot_from_quat(q, R);
-        const float s[3] = {cam.scale_modifier * g.scales[3 * i], cam.scale_modifier * g.scales[3 * i + 1],
-                            cam.scale_modifier * g.scales[3 * i + 2]};
+        const float s[3] = {cam.scale_modifier * gg.s.x, cam.scale_modifier * gg.s.y, cam.scale_modifier * gg.s.z};
         const float Gs[3][3] = {{dcov[0], 0.5f * dcov[1], 0.5f * dcov[2]},
                                 {0.5f * dcov[1], dcov[3], 0.5f * dcov[4]},
                                 {0.5f * dcov[2], 0.5f * dcov[4], dcov[5]}};
@@ -196,6 +216,11 @@ __device__ inline void gauss_chain(const Camera& cam, const GaussIn& g, int i, c
         drot[2] = 2.f * x * (dR[0][1] + dR[1][0]) + 2.f * r * (dR[0][2] - dR[2][0]) + 2.f * z * (dR[1][2] + dR[2][1]) - 4.f * y * (dR[0][0] + dR[2][2]);
         drot[3] = 2.f * r * (dR[1][0] - dR[0][1]) + 2.f * x * (dR[0][2] + dR[2][0]) + 2.f * y * (dR[1][2] + dR[2][1]) - 4.f * z * (dR[0][0] + dR[1][1]);
     }
+}
+__device__ inline void gauss_chain(const Camera& cam, const GaussIn& g, int i, const float g2[9], unsigned clamped,
+                                   float dmean[3], float dcov[6], float dscale[3], float drot[4], float* dsh_out,
+                                   int nsh) {
+    gauss_chain(cam, g, load_geom(g, i), i, g2, clamped, dmean, dcov, dscale, drot, dsh_out, nsh);
 }
 
 }  // namespace gsr

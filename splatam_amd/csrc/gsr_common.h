@@ -187,6 +187,7 @@ struct TrackXf {
     const float* ct = nullptr;  // the frame's translation column (stride qs)
     int qs = 1;
     const float* w2c = nullptr;  // [16] row-major (depth colours)
+    int store = 1;               // 0: the rendervars are not stored (the tracking backward recomputes them)
 };
 
 struct GaussIn {
@@ -1164,6 +1165,10 @@ struct PoseFuse {
     uint32_t cap = 0;
     const float* loss = nullptr;      // best-candidate selection (PoseAdam::loss / best)
     float* best = nullptr;
+    // log_scales [P, scols]: recompute each Gaussian's camera-frame mean / rotation / scale from the
+    // world-frame map and the (pre-step) pose instead of reading GaussIn's arrays (the forward ran the
+    // transform inside preprocess without storing them); nullptr: read GaussIn
+    const float* ls = nullptr;
 };
 int pose_fuse_scratch_floats(int P);
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* inst,

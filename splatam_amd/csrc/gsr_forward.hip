@@ -12,7 +12,7 @@
 //               LDS batches, block-wide early exit
 #include <cstdlib>
 
-#include "gsr_glue_common.h"  // (includes gsr_common.h) track_xform_one: the transform-fused preprocess
+#include "gsr_glue_common.h"  // (includes gsr_common.h) track_xform_compute / _store: the transform-fused preprocess
 
 namespace gsr {
 GSR_WGTIME_TABLE
@@ -56,7 +56,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
         float xs[3], xc2[3], xop = 0.f;
         float4 xq;
         if (XF) {  // gsr_track_transform_fwd's outputs, formed in registers (and stored for the backward)
-            Pose ps;  // (track_xform_one reads R, t and c)
+            Pose ps;  // (track_xform_compute reads R, t and c)
 #pragma unroll
             for (int k = 0; k < 9; k++) ps.R[k / 3][k % 3] = s_pose[k];
 #pragma unroll
@@ -64,9 +64,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
 #pragma unroll
             for (int k = 0; k < 4; k++) ps.c[k] = s_pose[12 + k];
             float m[3];
-            track_xform_one(g.xf, ps, i, m, xq, xc2, xop, xs, const_cast<float*>(g.means3D),
-                            const_cast<float*>(g.rotations), const_cast<float*>(g.colors2),
-                            const_cast<float*>(g.opacities), const_cast<float*>(g.scales));
+            track_xform_compute(g.xf, ps, i, m, xq, xc2, xop, xs);  // (stored below, after every load)
             p = make_float3(m[0], m[1], m[2]);
         } else {
             p = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
@@ -139,6 +137,12 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
         radii[i] = radius;
         geo.tiles[i] = tiles;
         if (tiles == 0) geo.bin[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (XF && g.xf.store) {  // the rendervars for the backward (the same values as gsr_track_transform_fwd's)
+            const float m[3] = {p.x, p.y, p.z};
+            track_xform_store(i, m, xq, xc2, xop, xs, const_cast<float*>(g.means3D), const_cast<float*>(g.rotations),
+                              const_cast<float*>(g.colors2), const_cast<float*>(g.opacities),
+                              const_cast<float*>(g.scales));
+        }
     }
     // workgroup scan of tiles touched: the local instance offset goes into the render
     // record (q1.w; the render kernels add the scanned workgroup base, blocksums[i >> 10]),

@@ -43,7 +43,8 @@ track_transform_fwd_kernel(int P, const float* __restrict__ mw, const float* __r
     x.mw = mw; x.ur = ur; x.lo = lo; x.ls = ls; x.scols = scols; x.w2c = w2c;
     float m[3], c2[3], op, s[3];
     float4 q;
-    track_xform_one(x, ps, i, m, q, c2, op, s, mc, rot, dcol, opac, scl);
+    track_xform_compute(x, ps, i, m, q, c2, op, s);
+    track_xform_store(i, m, q, c2, op, s, mc, rot, dcol, opac, scl);
 }
 
 // Pose gradient in one launch: every workgroup publishes its partial of the 16

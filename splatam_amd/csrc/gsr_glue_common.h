@@ -66,32 +66,49 @@ __device__ __forceinline__ float4 load4(const float* p) { return make_float4(p[0
 
 // One Gaussian of transform_to_frame + the rendervar builders (slam_helpers.py:124-139,196-213,
 // 252-304): camera-frame mean m, rendervar rotation q, depth colours c2 = [z, 1, z^2], opacity op,
-// scales s -- returned and stored at mc / rot / dcol / opac / scl.  Shared by
-// track_transform_fwd_kernel and the transform-fused preprocess (same code, same bits).
-__device__ __forceinline__ void track_xform_one(const TrackXf& x, const Pose& ps, int i, float (&m)[3], float4& q,
-                                                float (&c2)[3], float& op, float (&s)[3], float* mc, float* rot,
-                                                float* dcol, float* opac, float* scl) {
+// scales s.  Shared by track_transform_fwd_kernel and the transform-fused preprocess (same code,
+// same bits).  Loads only: the stores (track_xform_store) go after every other global load of the
+// calling kernel -- a load issued after a store waits for the store's completion too (vmcnt
+// counts both on gfx950), which serialised ~5 store round trips in preprocess (6 us).
+// The geometric part (mean, rotation, scale) alone: also what the tracking backward recomputes
+// (PoseFuse::ls) instead of reading stored rendervars -- the same expressions, so the same bits.
+__device__ __forceinline__ void track_xform_geom(const TrackXf& x, const Pose& ps, int i, float (&m)[3], float4& q,
+                                                 float (&s)[3]) {
     const float p0 = x.mw[3 * i], p1 = x.mw[3 * i + 1], p2 = x.mw[3 * i + 2];
+    const float4 ur = load4(x.ur + 4 * i);
+    float lsv[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) lsv[k] = x.ls[x.scols == 1 ? i : 3 * i + k];
 #pragma unroll
     for (int r = 0; r < 3; r++) m[r] = ps.R[r][0] * p0 + ps.R[r][1] * p1 + ps.R[r][2] * p2 + ps.t[r];
-    mc[3 * i] = m[0]; mc[3 * i + 1] = m[1]; mc[3 * i + 2] = m[2];
     float un_norm;
-    q = normalize4(load4(x.ur + 4 * i), un_norm);              // F.normalize(unnorm_rotations)
+    q = normalize4(ur, un_norm);                                 // F.normalize(unnorm_rotations)
     if (x.scols != 1) {                                          // anisotropic: compose with the camera
         float o_norm;
         q = normalize4(quat_mult(ps.c, q), o_norm);
     }
-    rot[4 * i] = q.x; rot[4 * i + 1] = q.y; rot[4 * i + 2] = q.z; rot[4 * i + 3] = q.w;
+#pragma unroll
+    for (int k = 0; k < 3; k++) s[k] = expf(lsv[k]);
+}
+__device__ __forceinline__ void track_xform_compute(const TrackXf& x, const Pose& ps, int i, float (&m)[3],
+                                                    float4& q, float (&c2)[3], float& op, float (&s)[3]) {
+    const float lo = x.lo[i];
+    track_xform_geom(x, ps, i, m, q, s);
     const float z = x.w2c[8] * m[0] + x.w2c[9] * m[1] + x.w2c[10] * m[2] + x.w2c[11];
     c2[0] = z; c2[1] = 1.f; c2[2] = z * z;
+    op = 1.f / (1.f + expf(-lo));
+}
+__device__ __forceinline__ void track_xform_store(int i, const float (&m)[3], float4 q, const float (&c2)[3], float op,
+                                                  const float (&s)[3], float* mc, float* rot, float* dcol,
+                                                  float* opac, float* scl) {
+#ifndef GSR_XF_NOSTORE
+    mc[3 * i] = m[0]; mc[3 * i + 1] = m[1]; mc[3 * i + 2] = m[2];
+    rot[4 * i] = q.x; rot[4 * i + 1] = q.y; rot[4 * i + 2] = q.z; rot[4 * i + 3] = q.w;
     dcol[3 * i] = c2[0]; dcol[3 * i + 1] = c2[1]; dcol[3 * i + 2] = c2[2];
-    op = 1.f / (1.f + expf(-x.lo[i]));
     opac[i] = op;
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-        s[k] = expf(x.ls[x.scols == 1 ? i : 3 * i + k]);
-        scl[3 * i + k] = s[k];
-    }
+    for (int k = 0; k < 3; k++) scl[3 * i + k] = s[k];
+#endif
 }
 
 // Forward-state check of the fused optimizer steps: `st` is a forward's device counters or
@@ -229,14 +246,14 @@ __device__ void pose_fin(const float* S, const float* cq, int qs, float* dq, flo
 // One Gaussian's contribution to the 16 pose sums (sum g, sum g p^T, sum dquat_mult^T dr):
 // g = dL/dmeans_cam, gd = dL/d[z, 1, z^2] (or NULL), gr = dL/drotation of an anisotropic map
 // (or NULL), c = F.normalize(cam quaternion) (used with gr only).
-__device__ __forceinline__ void pose_partials(float (&v)[POSE_PARTS], int i, const float g_in[3], const float* gd,
+__device__ __forceinline__ void pose_partials_m(float (&v)[POSE_PARTS], int i, const float g_in[3], const float* gd,
                                               const float* gr, const float* __restrict__ mw,
-                                              const float* __restrict__ ur, const float* __restrict__ mc,
+                                              const float* __restrict__ ur, const float (&mci)[3],
                                               const float* __restrict__ w2c, const float c[4]) {
     float g0 = g_in[0], g1 = g_in[1], g2 = g_in[2];
     if (gd) {  // colours [z, 1, z^2]: dz = dc0 + 2 z dc2, z = w2c[2,:3] . m + w2c[2,3]
         const float wz0 = w2c[8], wz1 = w2c[9], wz2 = w2c[10];
-        const float z = wz0 * mc[3 * i] + wz1 * mc[3 * i + 1] + wz2 * mc[3 * i + 2] + w2c[11];
+        const float z = wz0 * mci[0] + wz1 * mci[1] + wz2 * mci[2] + w2c[11];
         const float dz = gd[0] + 2.f * z * gd[2];
         g0 += dz * wz0; g1 += dz * wz1; g2 += dz * wz2;
     }
@@ -257,6 +274,14 @@ __device__ __forceinline__ void pose_partials(float (&v)[POSE_PARTS], int i, con
         v[14] += -d.x * u.z + d.y * u.w + d.z * u.x - d.w * u.y;
         v[15] += -d.x * u.w - d.y * u.z + d.z * u.y + d.w * u.x;
     }
+}
+
+__device__ __forceinline__ void pose_partials(float (&v)[POSE_PARTS], int i, const float g_in[3], const float* gd,
+                                              const float* gr, const float* __restrict__ mw,
+                                              const float* __restrict__ ur, const float* __restrict__ mc,
+                                              const float* __restrict__ w2c, const float c[4]) {
+    const float mci[3] = {mc[3 * i], mc[3 * i + 1], mc[3 * i + 2]};
+    pose_partials_m(v, i, g_in, gd, gr, mw, ur, mci, w2c, c);
 }
 
 // Sums `v` over the workgroup (4 waves) into out[0..N) in a fixed order.

@@ -25,6 +25,9 @@ from ._lib import lib
 # tracking transform fused into the rasterizer's preprocess in the static tracking iteration
 # (gsr_track_forward_dual_static_xf); GSR_XF_FUSED=0 runs it as its own launch (A/B, parity tests)
 _XF_FUSED = os.environ.get("GSR_XF_FUSED", "1") != "0"
+# ... without storing the camera-frame rendervars (the backward recomputes them from the world-frame
+# map: gsr_track_backward_dual log_scales); True stores them (tests compare them with the separate transform)
+_XF_STORE = False
 
 
 def _check(rc: int, what: str):
@@ -469,7 +472,8 @@ class _TrackIteration(torch.autograd.Function):
             # loss + gradient images in the render epilogue
             seed = _f32c(seed, "seed")
             scratch = _scratch(mw, lib.gsr_track_forward_scratch_floats(W, H))
-            xform = (mw, ur, lo, ls, scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c)
+            xform = (mw, ur, lo, ls, scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c,
+                     _XF_STORE)
             (n, im, ds, radii, geom, binning, img, _, loss, dim, dds) = _C.track_forward_dual_static(
                 cam, means, rgb, dcol, opac, scales, rot, capacity, status, gt_im, gt_d, cfg.sil_thres, cfg.w_im,
                 cfg.w_depth, seed, scratch, xform=xform)
@@ -479,6 +483,7 @@ class _TrackIteration(torch.autograd.Function):
             ctx.meta = (t, T, scols, int(n), cam, cfg)
             ctx.pose_adam = pose_adam
             ctx.loss_ptr = loss.data_ptr()
+            ctx.log_scales = None if _XF_STORE else ls  # rendervars not stored: the backward recomputes them
             ctx.mark_non_differentiable(radii)
             ctx.set_materialize_grads(False)
             return loss, radii
@@ -500,6 +505,7 @@ class _TrackIteration(torch.autograd.Function):
             ctx.meta = (t, T, scols, int(n), cam, cfg)
             ctx.pose_adam = pose_adam
             ctx.loss_ptr = loss.data_ptr()  # best-candidate selection reads this iteration's loss
+            ctx.log_scales = None
             ctx.mark_non_differentiable(radii)
             ctx.set_materialize_grads(False)
             return loss, radii
@@ -527,6 +533,7 @@ class _TrackIteration(torch.autograd.Function):
         ctx.meta = (t, T, scols, int(n), cam, cfg)
         ctx.pose_adam = pose_adam
         ctx.loss_ptr = loss.data_ptr()
+        ctx.log_scales = None
         ctx.mark_non_differentiable(radii)
         ctx.set_materialize_grads(False)
         return loss, radii
@@ -558,12 +565,13 @@ class _TrackIteration(torch.autograd.Function):
             _C.track_backward_dual(cam, means, radii, rgb, dcol, scales, rot_in, dim, dds, geom, n, binning, img, mw,
                                    ur, scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c,
                                    scratch, adam=(opt.lr_q, opt.lr_t, float(opt.betas[0]), float(opt.betas[1]),
-                                                  opt.eps, opt.state), track=opt.track(ctx.loss_ptr))
+                                                  opt.eps, opt.state), track=opt.track(ctx.loss_ptr),
+                                   log_scales=ctx.log_scales)
             return nones
         dq, dt = torch.zeros_like(cam_rots), torch.zeros_like(cam_trans)
         _C.track_backward_dual(cam, means, radii, rgb, dcol, scales, rot_in, dim, dds, geom, n, binning, img, mw, ur,
                                scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c, scratch,
-                               dq_ptr=dq.data_ptr() + 4 * t, dt_ptr=dt.data_ptr() + 4 * t)
+                               dq_ptr=dq.data_ptr() + 4 * t, dt_ptr=dt.data_ptr() + 4 * t, log_scales=ctx.log_scales)
         return (dq, dt) + (None,) * 9
 
 
