@@ -494,16 +494,25 @@ __device__ __forceinline__ uint32_t plan_slot(uint32_t p, uint32_t n, uint32_t n
 }
 // one workgroup of NT threads (PLAN_BUCKETS / NT consecutive buckets per thread); s_hist:
 // PLAN_BUCKETS words of LDS, s_wsum: NT / 64
-template <int NT>
+// TPT > 0: the tile totals come from registers, tv[k] = total of tile t0 + k (t0 + k < t1) -- no
+// reload of `tot` after the caller's stores (a load issued after a store waits for it too)
+template <int NT, int TPT = 0>
 __device__ void tile_plan(const uint32_t* __restrict__ tot, int ntiles, int ncu, uint32_t* __restrict__ order,
-                          uint32_t* s_hist, uint32_t* s_wsum) {
+                          uint32_t* s_hist, uint32_t* s_wsum, const uint32_t* tv = nullptr, int t0 = 0,
+                          int t1 = 0) {
     constexpr int BPT = PLAN_BUCKETS / NT;
     static_assert(BPT * NT == PLAN_BUCKETS, "buckets per thread");
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 #pragma unroll
     for (int k = 0; k < BPT; k++) s_hist[tid * BPT + k] = 0u;
     __syncthreads();
-    for (int u = tid; u < ntiles; u += NT) atomicAdd(&s_hist[plan_bucket(tot[u])], 1u);
+    if constexpr (TPT > 0) {
+#pragma unroll
+        for (int k = 0; k < TPT; k++)
+            if (t0 + k < t1) atomicAdd(&s_hist[plan_bucket(tv[k])], 1u);
+    } else {
+        for (int u = tid; u < ntiles; u += NT) atomicAdd(&s_hist[plan_bucket(tot[u])], 1u);
+    }
     __syncthreads();
     uint32_t c[BPT], cs = 0;
 #pragma unroll
@@ -522,9 +531,18 @@ __device__ void tile_plan(const uint32_t* __restrict__ tot, int ntiles, int ncu,
         run += c[k];
     }
     __syncthreads();
-    for (int u = tid; u < ntiles; u += NT) {
-        const uint32_t p = atomicAdd(&s_hist[plan_bucket(tot[u])], 1u);
-        order[plan_slot(p, (uint32_t)ntiles, (uint32_t)ncu)] = (uint32_t)u;
+    if constexpr (TPT > 0) {
+#pragma unroll
+        for (int k = 0; k < TPT; k++)
+            if (t0 + k < t1) {
+                const uint32_t p = atomicAdd(&s_hist[plan_bucket(tv[k])], 1u);
+                order[plan_slot(p, (uint32_t)ntiles, (uint32_t)ncu)] = (uint32_t)(t0 + k);
+            }
+    } else {
+        for (int u = tid; u < ntiles; u += NT) {
+            const uint32_t p = atomicAdd(&s_hist[plan_bucket(tot[u])], 1u);
+            order[plan_slot(p, (uint32_t)ntiles, (uint32_t)ncu)] = (uint32_t)u;
+        }
     }
 }
 
@@ -672,7 +690,10 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
             for (int u = tid; u < ntiles; u += DUP_T) cam.tile_order_out[u] = (uint32_t)u;
 #else
             __shared__ uint32_t s_plan[PLAN_BUCKETS];
-            tile_plan<DUP_T>(tot, ntiles, cam.sched_cus, cam.tile_order_out, s_plan, wsum);
+            if (in_regs)
+                tile_plan<DUP_T, TPT>(tot, ntiles, cam.sched_cus, cam.tile_order_out, s_plan, wsum, tv, t0, t1);
+            else
+                tile_plan<DUP_T>(tot, ntiles, cam.sched_cus, cam.tile_order_out, s_plan, wsum);
 #endif
         }
         base = pre;
@@ -1204,6 +1225,19 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         __syncthreads();
     }
     const float C0 = C01.x, C1 = C01.y, C3 = C34.x, C4 = C34.y;
+    // the loss epilogue's inputs are loaded before the image stores: a load issued after a store
+    // also waits for the store's completion (vmcnt counts both)
+    float l1_seed = 0.f, l1_gd = 0.f, l1_gi[3] = {0.f, 0.f, 0.f};
+    if constexpr (L1) {
+        if (inside) {
+            const int pid = py * cam.W + px;
+            const int HW = cam.W * cam.H;
+            l1_seed = l1.seed[0];
+            l1_gd = l1.gt_depth[pid];
+#pragma unroll
+            for (int c = 0; c < 3; c++) l1_gi[c] = l1.gt_im[c * HW + pid];
+        }
+    }
     if (inside) {
         const int pid = py * cam.W + px;
         const int HW = cam.W * cam.H;
@@ -1229,15 +1263,13 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         if (inside) {
             const int pid = py * cam.W + px;
             const int HW = cam.W * cam.H;
-            const float g = l1.seed[0];
+            const float g = l1_seed;
             const float im[3] = {C0 + T * cam.bg[0], C1 + T * cam.bg[1], C2 + T * cam.bg[2]};
             const float d = C3 + T * cam.bg[0], sil = C4 + T * cam.bg[1], dsq = C5 + T * cam.bg[2];
-            const float gd = l1.gt_depth[pid];
+            const float gd = l1_gd;
             const float unc = dsq - d * d;
             const bool m = gd > 0.f && !isnan(d) && !isnan(unc) && sil > l1.sil_thres;
-            float gi[3];
-#pragma unroll
-            for (int c = 0; c < 3; c++) gi[c] = l1.gt_im[c * HW + pid];
+            const float gi[3] = {l1_gi[0], l1_gi[1], l1_gi[2]};
             if (m) {
                 v[0] = fabsf(gi[0] - im[0]) + fabsf(gi[1] - im[1]) + fabsf(gi[2] - im[2]);
                 v[1] = fabsf(gd - d);
