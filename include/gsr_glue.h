@@ -244,6 +244,18 @@ typedef struct gsr_map_adam {
     unsigned capacity;
 } gsr_map_adam;
 
+/* gsr_backward_dual with the mapping optimizer's colour group (sh_adam->exp_avg[4] / exp_avg_sq[4] /
+ * lr[4], step, betas, eps, status) applied to the SH coefficients gaussians->shs in place inside the
+ * SH backward stage, instead of writing grads->dsh (which may be NULL) for
+ * gsr_map_transform_bwd_adam to step: the 192-B-per-Gaussian gradient never makes the HBM round
+ * trip.  Same element update (bitwise) as gsr_map_transform_bwd_adam's; call that one afterwards
+ * with dL_dcolors = NULL.  Needs staged SH colours (M == (sh_degree+1)^2). */
+int gsr_backward_dual_sh_adam(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
+                              const float* colors2, const float* dL_dout_color, const float* dL_dout_color2,
+                              int num_rendered, const void* geom_buffer, const void* binning_buffer,
+                              const void* image_buffer, const gsr_grads* grads, float* dcolors2, int dl2_channels,
+                              const gsr_map_adam* sh_adam, gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
 /* gsr_map_transform_bwd with the optimizer step fused in: the parameters are
  * updated in place, no gradient is written.  dL_dcolors (the rasterizer's
  * gradient of the colour parameters, [P, color_cols]) steps `colors`; NULL

@@ -334,12 +334,14 @@ def rasterize_gaussians_dual(background, means3D, colors, colors2, opacity, scal
 def rasterize_gaussians_dual_backward(background, means3D, radii, colors, colors2, scales, rotations, scale_modifier,
                                       cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
                                       dL_dout_color2, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
-                                      needs=None, dl2_channels=3):
+                                      needs=None, dl2_channels=3, sh_adam=None):
     """gsr_backward_dual.  Returns (dmeans2D, dcolors, dcolors2, dopacity, dmeans3D, dcov3D, dsh, dscales,
     drotations); geometric gradients are the sums over both colour sets.  `needs` (9 bools in that
     order, default all) skips the gradients nobody wants: they come back as None and the kernels do
     not form their per-pair sums.  dl2_channels=1 promises dL_dout_color2[1:] == 0 (only the depth
-    channel is differentiated): those channels are not read and dcolors2[:, 1:] comes back zero."""
+    channel is differentiated): those channels are not read and dcolors2[:, 1:] comes back zero.
+    sh_adam: a GsrMapAdam (the mapping optimizer, colour group = index 4, step = the upcoming one): the
+    colour Adam step is applied to `sh` in place (gsr_backward_dual_sh_adam) and dsh comes back None."""
     device = means3D.device
     P = means3D.size(0)
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
@@ -347,6 +349,8 @@ def rasterize_gaussians_dual_backward(background, means3D, radii, colors, colors
     f32 = dict(dtype=torch.float32, device=device)
     needs = [True] * 9 if needs is None else list(needs)
     needs[4] = True  # dmeans3D is always produced
+    if sh_adam is not None:
+        needs[6] = False  # dsh: consumed by the fused colour Adam step
     shapes = [(P, 3), (P, 3), (P, 3), (P, 1), (P, 3), (P, 6), (P, M, 3), (P, 3), (P, 4)]
     res = [torch.empty(*sh_, **f32) if nd else None for sh_, nd in zip(shapes, needs)]
     out = [res[0], res[1], res[3], res[4], res[5], res[6], res[7], res[8]]
@@ -363,13 +367,21 @@ def rasterize_gaussians_dual_backward(background, means3D, radii, colors, colors
         radii_c = radii.to(device=device, dtype=torch.int32).contiguous()
         grads = GsrGrads(*[o.data_ptr() if (o is not None and o.numel() > 0) else None for o in out])
         _begin(device)
-        rc = lib.gsr_backward_dual(ctypes.byref(s), ctypes.byref(g), radii_c.data_ptr(), _ptr(c2), dpix.data_ptr(),
-                                   dpix2.data_ptr(), int(R), geomBuffer.data_ptr(),
-                                   binningBuffer.data_ptr() if binningBuffer.numel() else None,
-                                   imageBuffer.data_ptr(), ctypes.byref(grads),
-                                   dcolors2.data_ptr() if dcolors2 is not None else None, int(dl2_channels),
-                                   _ALLOC_CB, None,
-                                   _stream(device))
+        if sh_adam is not None:
+            if keep_g[1] is None or keep_g[1].data_ptr() != sh.data_ptr():
+                raise RuntimeError("sh_adam steps the SH coefficients in place: sh must be contiguous float32")
+            rc = lib.gsr_backward_dual_sh_adam(
+                ctypes.byref(s), ctypes.byref(g), radii_c.data_ptr(), _ptr(c2), dpix.data_ptr(), dpix2.data_ptr(),
+                int(R), geomBuffer.data_ptr(), binningBuffer.data_ptr() if binningBuffer.numel() else None,
+                imageBuffer.data_ptr(), ctypes.byref(grads), dcolors2.data_ptr() if dcolors2 is not None else None,
+                int(dl2_channels), ctypes.byref(sh_adam), _ALLOC_CB, None, _stream(device))
+        else:
+            rc = lib.gsr_backward_dual(ctypes.byref(s), ctypes.byref(g), radii_c.data_ptr(), _ptr(c2),
+                                       dpix.data_ptr(), dpix2.data_ptr(), int(R), geomBuffer.data_ptr(),
+                                       binningBuffer.data_ptr() if binningBuffer.numel() else None,
+                                       imageBuffer.data_ptr(), ctypes.byref(grads),
+                                       dcolors2.data_ptr() if dcolors2 is not None else None, int(dl2_channels),
+                                       _ALLOC_CB, None, _stream(device))
         _check(rc, "rasterize_gaussians_dual_backward")
         _tls.buffers = {}
         return (out[0], out[1], dcolors2, *out[2:])

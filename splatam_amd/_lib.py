@@ -118,6 +118,10 @@ SIGNATURES = {
                                                  c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float,
                                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ALLOC_FN, c_void_p,
                                                  c_void_p]),
+    "gsr_backward_dual_sh_adam": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p,
+                                          c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                          ctypes.POINTER(GsrGrads), c_void_p, c_int, ctypes.POINTER(GsrMapAdam),
+                                          ALLOC_FN, c_void_p, c_void_p]),
     "gsr_track_backward_scratch_floats": (c_int, [c_int]),
     "gsr_track_backward_dual": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -514,7 +514,7 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
                          int num_rendered, const void* geom_buffer, const void* binning_buffer,
                          const void* image_buffer, int power, const gsr_grads* grads, float* dcolors2,
                          int dl2_channels, gsr_alloc_fn alloc, void* alloc_ctx, void* stream_,
-                         const PoseFuse* pose = nullptr) {
+                         const PoseFuse* pose = nullptr, const ShAdam* sh_adam = nullptr) {
     int rc = validate(settings, gaussians, false);
     if (dl2_channels != 1 && dl2_channels != 3) return fail(GSR_ERR_INVALID_ARG, "dl2_channels must be 1 or 3");
     if (rc != GSR_OK) return rc;
@@ -627,8 +627,9 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
         if ((e = launch_gauss_bwd(cam, gc, geo, radii, inst, rec, oc, guard, stream, pose ? &pc : nullptr)) !=
             hipSuccess)
             return hip_fail(e, "gaussian backward");
-        if (shs_staged && (e = launch_sh_bwd(cam, g, geo, radii, drgb, out.dmeans3D, out.dsh, guard, stream)) !=
-                              hipSuccess)
+        if (sh_adam && !shs_staged) return fail(GSR_ERR_INVALID_ARG, "sh_adam needs staged SH colours (M == (D+1)^2)");
+        if (shs_staged && (e = launch_sh_bwd(cam, g, geo, radii, drgb, out.dmeans3D, out.dsh, guard, stream,
+                                             sh_adam ? *sh_adam : ShAdam{})) != hipSuccess)
             return hip_fail(e, "sh backward");
     }
     return GSR_OK;
@@ -885,6 +886,33 @@ int gsr_backward_dual(const gsr_settings* settings, const gsr_gaussians* gaussia
     return backward_impl(settings, gaussians, radii, dL_dout_color, colors2, dL_dout_color2, num_rendered,
                          geom_buffer, binning_buffer, image_buffer, 1, grads, dcolors2, dl2_channels, alloc, alloc_ctx,
                          stream);
+}
+
+int gsr_backward_dual_sh_adam(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
+                              const float* colors2, const float* dL_dout_color, const float* dL_dout_color2,
+                              int num_rendered, const void* geom_buffer, const void* binning_buffer,
+                              const void* image_buffer, const gsr_grads* grads, float* dcolors2, int dl2_channels,
+                              const gsr_map_adam* sh_adam, gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
+    if (!colors2) return fail(GSR_ERR_INVALID_ARG, "colors2 required");
+    if (!sh_adam || !gaussians || !gaussians->shs || sh_adam->step < 1 || !sh_adam->exp_avg[4] ||
+        !sh_adam->exp_avg_sq[4])
+        return fail(GSR_ERR_INVALID_ARG, "backward_dual_sh_adam: SH colours and the colour group's state required");
+    // the scalars exactly as gsr_map_transform_bwd_adam forms them (python floats -> float)
+    ShAdam sa;
+    const double bc1 = 1.0 - pow(sh_adam->beta1, (double)sh_adam->step);
+    sa.m = sh_adam->exp_avg[4];
+    sa.v = sh_adam->exp_avg_sq[4];
+    sa.ss = (float)(-sh_adam->lr[4] / bc1);
+    sa.w1 = (float)(1.0 - sh_adam->beta1);
+    sa.beta2 = (float)sh_adam->beta2;
+    sa.omb2 = (float)(1.0 - sh_adam->beta2);
+    sa.bc2_sqrt = (float)sqrt(1.0 - pow(sh_adam->beta2, (double)sh_adam->step));
+    sa.eps = (float)sh_adam->eps;
+    sa.guard = sh_adam->status;
+    sa.cap = sh_adam->capacity;
+    return backward_impl(settings, gaussians, radii, dL_dout_color, colors2, dL_dout_color2, num_rendered,
+                         geom_buffer, binning_buffer, image_buffer, 1, grads, dcolors2, dl2_channels, alloc, alloc_ctx,
+                         stream, nullptr, &sa);
 }
 
 }  // extern "C"

@@ -1178,8 +1178,34 @@ hipError_t launch_selftest_reduce9(const float* in, float* out, hipStream_t s);
 // gsr_sh.hip: SH colour stages with LDS-staged, coalesced coefficient traffic
 bool sh_staged(const Camera& cam, const GaussIn& g);
 hipError_t launch_sh_eval(const Camera& cam, const GaussIn& g, GeomPtrs geo, hipStream_t s);
+// torch.optim.Adam's element update (foreach form: exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2)
+// .addcmul_(g, g, 1-b2); p.addcdiv_(exp_avg, sqrt(exp_avg_sq)/sqrt(bc2) + eps, -lr/bc1)) -- the one
+// definition the mapping step and the SH-stage colour step share, with no FP contraction (each
+// operation rounded, like torch's separate kernels): the two kernels had contracted differently and
+// diverged by an ulp from the second step on.
+__device__ __forceinline__ float adam_update_elem(float p, float g, float& m, float& v, float ss, float w1, float beta2,
+                                           float omb2, float bc2_sqrt, float eps) {
+#pragma clang fp contract(off)
+    const float mm = m + w1 * (g - m);
+    float v2 = v * beta2;
+    v2 = v2 + omb2 * g * g;
+    const float denom = sqrtf(v2) / bc2_sqrt + eps;
+    m = mm;
+    v = v2;
+    return p + ss * (mm / denom);
+}
+
+// The mapping optimizer's colour group applied to the SH coefficients inside sh_bwd (m == nullptr: none):
+// torch.optim.Adam's element update with the scalars formed on the host like the other fused steps.
+struct ShAdam {
+    float* m = nullptr;
+    float* v = nullptr;
+    float ss = 0.f, w1 = 0.f, beta2 = 0.f, omb2 = 0.f, bc2_sqrt = 1.f, eps = 0.f;
+    const uint32_t* guard = nullptr;  // the forward's status row / counters: skip the step on an overflow
+    uint32_t cap = 0;
+};
 hipError_t launch_sh_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* drgb,
-                         float* dmeans3D, float* dsh, BwdGuard guard, hipStream_t s);
+                         float* dmeans3D, float* dsh, BwdGuard guard, hipStream_t s, const ShAdam& sa = ShAdam{});
 // error reporting shared by the C entry points (gsr_last_error)
 int fail(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* where);

@@ -334,13 +334,9 @@ struct MapAdam {  // the mapping optimizer's state, applied in place (NULL p: wr
 
 __device__ __forceinline__ float adam_apply(float* p, float g, float* m, float* v, float ss, const MapAdam& a) {
     float mm = *m, vv = *v;
-    mm = mm + a.w1 * (g - mm);
-    vv = vv * a.beta2;
-    vv = vv + a.omb2 * g * g;
-    const float denom = sqrtf(vv) / a.bc2_sqrt + a.eps;
+    const float np = adam_update_elem(*p, g, mm, vv, ss, a.w1, a.beta2, a.omb2, a.bc2_sqrt, a.eps);
     *m = mm;
     *v = vv;
-    const float np = *p + ss * (mm / denom);
     *p = np;
     return np;
 }
@@ -361,13 +357,10 @@ __device__ __forceinline__ void adam_apply_n(float* p, const float* g, float* m,
 #pragma unroll
     for (int k = 0; k < N; k++) {
         float mm = mv[k], v2 = vv[k];
-        mm = mm + a.w1 * (g[k] - mm);
-        v2 = v2 * a.beta2;
-        v2 = v2 + a.omb2 * g[k] * g[k];
-        const float denom = sqrtf(v2) / a.bc2_sqrt + a.eps;
+        const float np = adam_update_elem(pv[k], g[k], mm, v2, ss, a.w1, a.beta2, a.omb2, a.bc2_sqrt, a.eps);
         m[k * stride] = mm;
         v[k * stride] = v2;
-        p[k * stride] = pv[k] + ss * (mm / denom);
+        p[k * stride] = np;
     }
 }
 

@@ -66,6 +66,47 @@ __device__ __forceinline__ void unstage_rows(float* __restrict__ dst, const floa
     }
 }
 
+// The colour Adam step over the workgroup's [n x ROW] block, gradients from the LDS rows: the
+// parameters (the SH coefficients the block staged, updated in place), exp_avg and exp_avg_sq move
+// as float4 streams.  The element update is adam_update_elem, as in map_transform_bwd's colour step, so
+// fusing it here changes no bit of the optimizer's result.
+template <int NSH>
+__device__ __forceinline__ void adam_rows(float* p, float* m, float* v, const float* s, int n, const ShAdam& a) {
+    using T = ShTile<NSH>;
+    const int total = n * T::ROW;
+    auto elem = [&](float& pp, float g, float& mm_, float& vv_) {
+        pp = adam_update_elem(pp, g, mm_, vv_, a.ss, a.w1, a.beta2, a.omb2, a.bc2_sqrt, a.eps);
+    };
+    const bool vec = T::ROW % 4 == 0 && ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(m) |
+                                          reinterpret_cast<uintptr_t>(v)) & 15u) == 0;
+    if (vec) {
+        float4* p4 = reinterpret_cast<float4*>(p);
+        float4* m4 = reinterpret_cast<float4*>(m);
+        float4* v4 = reinterpret_cast<float4*>(v);
+        for (int e4 = threadIdx.x; 4 * e4 < total; e4 += SH_BLOCK) {
+            const int e = 4 * e4, r = e / T::ROW, c = e - r * T::ROW;
+            const float* q = s + r * T::PITCH + c;
+            float4 pv = p4[e4], mv = m4[e4], vv = v4[e4];
+            elem(pv.x, q[0], mv.x, vv.x);
+            elem(pv.y, q[1], mv.y, vv.y);
+            elem(pv.z, q[2], mv.z, vv.z);
+            elem(pv.w, q[3], mv.w, vv.w);
+            m4[e4] = mv;
+            v4[e4] = vv;
+            p4[e4] = pv;
+        }
+    } else {
+        for (int e = threadIdx.x; e < total; e += SH_BLOCK) {
+            const int r = e / T::ROW, c = e - r * T::ROW;
+            float pv = p[e], mv = m[e], vv = v[e];
+            elem(pv, s[r * T::PITCH + c], mv, vv);
+            m[e] = mv;
+            v[e] = vv;
+            p[e] = pv;
+        }
+    }
+}
+
 template <int NSH>
 __global__ void __launch_bounds__(SH_BLOCK) sh_eval_kernel(Camera cam, GaussIn g, GeomPtrs geo) {
     using T = ShTile<NSH>;
@@ -88,7 +129,7 @@ __global__ void __launch_bounds__(SH_BLOCK) sh_eval_kernel(Camera cam, GaussIn g
 template <int NSH>
 __global__ void __launch_bounds__(SH_BLOCK)
 sh_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float* __restrict__ drgb,
-              float* __restrict__ dmeans3D, float* __restrict__ dsh, BwdGuard guard) {
+              float* __restrict__ dmeans3D, float* __restrict__ dsh, BwdGuard guard, ShAdam sa) {
     using T = ShTile<NSH>;
     __shared__ float s_sh[SH_BLOCK * T::PITCH];
     const int base = blockIdx.x * SH_BLOCK;
@@ -114,7 +155,14 @@ sh_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii
         }
     }
     __syncthreads();
-    if (dsh) unstage_rows<NSH>(dsh + (size_t)T::ROW * base, s_sh, n);
+    if (sa.m) {  // the colour Adam step in place of the dsh round trip through HBM
+        const uint32_t* st = sa.guard;
+        if (st && (st[0] > sa.cap || st[2] > st[3] || st[1] != 0u)) return;  // overflowing forward: no step
+        const size_t o = (size_t)T::ROW * base;
+        adam_rows<NSH>(const_cast<float*>(g.shs) + o, sa.m + o, sa.v + o, s_sh, n, sa);
+    } else if (dsh) {
+        unstage_rows<NSH>(dsh + (size_t)T::ROW * base, s_sh, n);
+    }
 }
 
 template <int NSH>
@@ -125,9 +173,9 @@ hipError_t launch_sh_eval_t(const Camera& cam, const GaussIn& g, GeomPtrs geo, h
 
 template <int NSH>
 hipError_t launch_sh_bwd_t(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* drgb,
-                           float* dmeans3D, float* dsh, BwdGuard guard, hipStream_t s) {
+                           float* dmeans3D, float* dsh, BwdGuard guard, hipStream_t s, const ShAdam& sa) {
     hipLaunchKernelGGL(sh_bwd_kernel<NSH>, dim3((g.P + SH_BLOCK - 1) / SH_BLOCK), dim3(SH_BLOCK), 0, s, cam, g, geo,
-                       radii, drgb, dmeans3D, dsh, guard);
+                       radii, drgb, dmeans3D, dsh, guard, sa);
     return hipGetLastError();
 }
 
@@ -150,13 +198,13 @@ hipError_t launch_sh_eval(const Camera& cam, const GaussIn& g, GeomPtrs geo, hip
 }
 
 hipError_t launch_sh_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* drgb,
-                         float* dmeans3D, float* dsh, BwdGuard guard, hipStream_t s) {
+                         float* dmeans3D, float* dsh, BwdGuard guard, hipStream_t s, const ShAdam& sa) {
     if (g.P == 0) return hipSuccess;
     switch (cam.sh_degree) {
-        case 0: return launch_sh_bwd_t<1>(cam, g, geo, radii, drgb, dmeans3D, dsh, guard, s);
-        case 1: return launch_sh_bwd_t<4>(cam, g, geo, radii, drgb, dmeans3D, dsh, guard, s);
-        case 2: return launch_sh_bwd_t<9>(cam, g, geo, radii, drgb, dmeans3D, dsh, guard, s);
-        default: return launch_sh_bwd_t<16>(cam, g, geo, radii, drgb, dmeans3D, dsh, guard, s);
+        case 0: return launch_sh_bwd_t<1>(cam, g, geo, radii, drgb, dmeans3D, dsh, guard, s, sa);
+        case 1: return launch_sh_bwd_t<4>(cam, g, geo, radii, drgb, dmeans3D, dsh, guard, s, sa);
+        case 2: return launch_sh_bwd_t<9>(cam, g, geo, radii, drgb, dmeans3D, dsh, guard, s, sa);
+        default: return launch_sh_bwd_t<16>(cam, g, geo, radii, drgb, dmeans3D, dsh, guard, s, sa);
     }
 }
 

@@ -79,7 +79,7 @@ class _RasterizeGaussians(torch.autograd.Function):
 
 def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations,
                              cov3Ds_precomp, raster_settings, capacity=0, status=None, grad2_channels=3,
-                             means2D_grad_sum=False):
+                             means2D_grad_sum=False, sh_adam=None):
     """Two GaussianRasterizer calls on identical geometry fused into one
     rasterization: SplaTAM renders RGB and the [z, 1, z^2]
     depth/silhouette image from the same means / scales / rotations / opacities
@@ -95,20 +95,23 @@ def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opac
     for HIP-graph capture; check `status` (device int32[4]) afterwards.
     grad2_channels=1: the caller's loss reads only channel 0 of color2 (SplaTAM
     tracking uses the depth, not the silhouette or depth^2, in its loss), so the
-    backward skips the other two channels; their incoming gradient must be zero."""
+    backward skips the other two channels; their incoming gradient must be zero.
+    sh_adam: the mapping optimizer (glue.MapAdam) whose colour group steps `sh` in place inside the
+    backward (gsr_backward_dual_sh_adam); `sh` then receives no gradient (the caller's own colour step,
+    gsr_map_transform_bwd_adam, sees none and leaves the colours to this one)."""
     empty = torch.Tensor([])
     return _RasterizeGaussiansDual.apply(means3D, means2D, empty if sh is None else sh,
                                          empty if colors_precomp is None else colors_precomp, colors2, opacities,
                                          empty if scales is None else scales,
                                          empty if rotations is None else rotations,
                                          empty if cov3Ds_precomp is None else cov3Ds_precomp, raster_settings,
-                                         capacity, status, grad2_channels, bool(means2D_grad_sum))
+                                         capacity, status, grad2_channels, bool(means2D_grad_sum), sh_adam)
 
 
 class _RasterizeGaussiansDual(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings, capacity, status, grad2_channels, means2D_grad_sum):
+                raster_settings, capacity, status, grad2_channels, means2D_grad_sum, sh_adam=None):
         s = raster_settings
         num_rendered, color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth = _C.rasterize_gaussians_dual(
             s.bg, means3D, colors_precomp, colors2, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
@@ -118,6 +121,7 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
         ctx.num_rendered = num_rendered
         ctx.grad2_channels = grad2_channels
         ctx.means2D_grad_sum = means2D_grad_sum
+        ctx.sh_adam = sh_adam
         ctx.save_for_backward(colors_precomp, colors2, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
                               geomBuffer, binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii, depth)
@@ -135,14 +139,18 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
             grad_color2 = torch.zeros(3, s.image_height, s.image_width, device=means3D.device)
         n = ctx.needs_input_grad  # (means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations, cov3D)
         needs = (n[1] and ctx.means2D_grad_sum, n[3], n[4], n[5], n[0], n[8], n[2], n[6], n[7])
+        sa = None
+        if ctx.sh_adam is not None:  # the colour group's upcoming step (the transform backward counts it)
+            sa = ctx.sh_adam.struct()
+            sa.step = ctx.sh_adam.step + 1
         (g_m2, g_col, g_col2, g_op, g_m3, g_cov, g_sh, g_sc, g_rot) = _C.rasterize_gaussians_dual_backward(
             s.bg, means3D, radii, colors_precomp, colors2, scales, rotations, s.scale_modifier, cov3Ds_precomp,
             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_color, grad_color2, sh, s.sh_degree, s.campos,
             geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, needs=needs,
-            dl2_channels=ctx.grad2_channels if grad_color2 is not None else 3)
+            dl2_channels=ctx.grad2_channels if grad_color2 is not None else 3, sh_adam=sa)
         if not n[0]:
             g_m3 = None
-        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None, None, None, None, None
+        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None, None, None, None, None, None
 
 
 class GaussianRasterizer(nn.Module):

@@ -323,6 +323,9 @@ def fused_mapping_eligible(params, curr_data, cfg: MappingConfig) -> bool:
             and curr_data["im"].dim() == 3 and curr_data["depth"].dim() == 3)
 
 
+_SH_ADAM_FUSED = True  # False: the colour step in gsr_map_transform_bwd_adam (A/B, parity tests)
+
+
 def _get_loss_mapping_fused(params, curr_data, iter_time_idx, cfg: MappingConfig, adam=None, capacity=0, status=None,
                             means2D=None):
     """The fused mapping iteration; capacity > 0: static-capacity rasterization (HIP-graph capturable),
@@ -333,8 +336,12 @@ def _get_loss_mapping_fused(params, curr_data, iter_time_idx, cfg: MappingConfig
     if means2D is None:
         means2D = torch.zeros(means.shape[0], 3, device=means.device, requires_grad=True)
     sh, colors = (col, None) if key == "shs" else (None, col)
+    # SH colours: the mapping optimizer's colour step runs inside the rasterizer's SH backward stage
+    # (gsr_backward_dual_sh_adam) instead of after a round trip of the gradient through HBM
+    sh_adam = adam if (adam is not None and sh is not None and _SH_ADAM_FUSED) else None
     im, depth_sil, radius, _ = rasterize_gaussians_dual(means, means2D, sh, colors, dcol, opac, scales, rots, None,
-                                                        curr_data["cam"], capacity, status, grad2_channels=1)
+                                                        curr_data["cam"], capacity, status, grad2_channels=1,
+                                                        sh_adam=sh_adam)
     loss = mapping_loss(im, depth_sil, curr_data["im"], curr_data["depth"], cfg.w_im, cfg.w_depth)
     return loss, radius, means2D
 

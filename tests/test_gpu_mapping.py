@@ -334,3 +334,34 @@ def test_fused_adam_through_gaussian_surgery(cuda):
     for k in base:
         assert runs[0][k].shape == runs[1][k].shape
         torch.testing.assert_close(runs[0][k].detach(), runs[1][k].detach(), rtol=1e-6, atol=1e-7)
+
+
+def test_sh_colour_adam_fused_bitwise(cuda, monkeypatch):
+    """The colour group's Adam step inside the rasterizer's SH backward stage
+    (gsr_backward_dual_sh_adam) against the same step in gsr_map_transform_bwd_adam after the
+    gradient's HBM round trip: parameters and optimizer moments bitwise equal after three
+    iterations (same element update, same gradients)."""
+    _, params, cam = _map_params(cuda, True, True)
+    curr = _scene_targets(params, cam, cuda)
+    cfg = slam.MappingConfig()
+    key = slam.color_key(params)
+    assert key == "shs"
+    keys = GAUSS_KEYS + (key,)
+    out = []
+    for fused in (False, True):
+        monkeypatch.setattr(slam, "_SH_ADAM_FUSED", fused)
+        p = {k: v.clone() for k, v in params.items()}
+        for k in keys:
+            p[k].requires_grad_(True)
+        adam = MapAdam(p, cfg.lrs, color_key=key)
+        for _ in range(3):
+            loss, _, _ = slam.get_loss_mapping(p, curr, 1, cfg, fused=True, adam=adam)
+            loss.backward()
+        assert adam.step == 3
+        out.append(({k: p[k].detach().clone() for k in keys}, [t.clone() for t in adam.exp_avg + adam.exp_avg_sq]))
+    (p0, s0), (p1, s1) = out
+    for k in keys:
+        assert torch.equal(p0[k], p1[k]), k
+        assert float((p1[k] - params[k]).abs().max()) > 0.0, k
+    for a, b in zip(s0, s1):
+        assert torch.equal(a, b)
