@@ -23,10 +23,16 @@ def header_functions():
 
 
 def header_struct_fields(name):
-    txt = open(HEADER).read()
+    txt = open(HEADER).read() + open(os.path.join(os.path.dirname(HEADER), "gsr_glue.h")).read()
     body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), txt, re.S).group(1)
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
-    return [re.findall(r"(\w+)$", d.strip())[0] for d in body.split(";") if d.strip()]
+    # "type name", "type name[N]" or "type a, b, c" per declaration
+    names = []
+    for d in body.split(";"):
+        for part in d.strip().split(","):
+            if part.strip():
+                names.append(re.findall(r"(\w+)(?:\[\d+\])?$", part.strip())[0])
+    return names
 
 
 def test_library_exports_every_header_symbol():
@@ -41,7 +47,8 @@ def test_library_exports_every_header_symbol():
 
 
 @pytest.mark.parametrize("cname,pyname", [("gsr_settings", "GsrSettings"), ("gsr_gaussians", "GsrGaussians"),
-                                          ("gsr_grads", "GsrGrads")])
+                                          ("gsr_grads", "GsrGrads"), ("gsr_track_xform", "GsrTrackXform"),
+                                          ("gsr_pose_track", "GsrPoseTrack"), ("gsr_map_adam", "GsrMapAdam")])
 def test_ctypes_structs_match_header(cname, pyname):
     from splatam_amd import _lib
     fields = header_struct_fields(cname)
