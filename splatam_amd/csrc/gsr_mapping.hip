@@ -448,16 +448,50 @@ map_transform_bwd_kernel(int P, const float* ur, const float* lo, const float* l
         if (dls) for (int k = 0; k < scols; k++) dls[scols * i + k] = dsc[k];
         return;
     }
-    adam_apply_n<3>(adam.p[0] + 3 * i, dp, adam.m[0] + 3 * i, adam.v[0] + 3 * i, 1, adam.step_size[0], adam);
+    // The four groups' parameters and moments are all loaded before the first store: a load issued
+    // after a store waits for the store too (vmcnt counts both on gfx950), so the group-by-group
+    // form serialised one store round trip per group.  Same element update, same results.
     const float duv[4] = {du.x, du.y, du.z, du.w};
-    adam_apply_n<4>(adam.p[1] + 4 * i, duv, adam.m[1] + 4 * i, adam.v[1] + 4 * i, 1, adam.step_size[1], adam);
-    adam_apply(adam.p[2] + i, dl, adam.m[2] + i, adam.v[2] + i, adam.step_size[2], adam);
-    if (scols == 3)
-        adam_apply_n<3>(adam.p[3] + 3 * i, dsc, adam.m[3] + 3 * i, adam.v[3] + 3 * i, 1, adam.step_size[3], adam);
-    else
-        for (int k = 0; k < scols; k++)
-            adam_apply(adam.p[3] + scols * i + k, dsc[k], adam.m[3] + scols * i + k, adam.v[3] + scols * i + k,
-                       adam.step_size[3], adam);
+    float pv[11], mv[11], vv[11], gv[11];
+    float* const p0 = adam.p[0] + 3 * i;
+    float* const p1 = adam.p[1] + 4 * i;
+    float* const p2 = adam.p[2] + i;
+    float* const p3 = adam.p[3] + scols * i;
+    float* const m0 = adam.m[0] + 3 * i;
+    float* const m1 = adam.m[1] + 4 * i;
+    float* const m2 = adam.m[2] + i;
+    float* const m3 = adam.m[3] + scols * i;
+    float* const v0 = adam.v[0] + 3 * i;
+    float* const v1 = adam.v[1] + 4 * i;
+    float* const v2 = adam.v[2] + i;
+    float* const v3 = adam.v[3] + scols * i;
+#pragma unroll
+    for (int k = 0; k < 3; k++) { pv[k] = p0[k]; mv[k] = m0[k]; vv[k] = v0[k]; gv[k] = dp[k]; }
+#pragma unroll
+    for (int k = 0; k < 4; k++) { pv[3 + k] = p1[k]; mv[3 + k] = m1[k]; vv[3 + k] = v1[k]; gv[3 + k] = duv[k]; }
+    pv[7] = *p2; mv[7] = *m2; vv[7] = *v2; gv[7] = dl;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const bool on = k < scols;
+        pv[8 + k] = on ? p3[k] : 0.f;
+        mv[8 + k] = on ? m3[k] : 0.f;
+        vv[8 + k] = on ? v3[k] : 0.f;
+        gv[8 + k] = dsc[k];
+    }
+#pragma unroll
+    for (int e = 0; e < 11; e++) {
+        const float ss = adam.step_size[e < 3 ? 0 : (e < 7 ? 1 : (e < 8 ? 2 : 3))];
+        pv[e] = adam_update_elem(pv[e], gv[e], mv[e], vv[e], ss, adam.w1, adam.beta2, adam.omb2, adam.bc2_sqrt,
+                                 adam.eps);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) { p0[k] = pv[k]; m0[k] = mv[k]; v0[k] = vv[k]; }
+#pragma unroll
+    for (int k = 0; k < 4; k++) { p1[k] = pv[3 + k]; m1[k] = mv[3 + k]; v1[k] = vv[3 + k]; }
+    *p2 = pv[7]; *m2 = mv[7]; *v2 = vv[7];
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+        if (k < scols) { p3[k] = pv[8 + k]; m3[k] = mv[8 + k]; v3[k] = vv[8 + k]; }
 }
 
 int map_loss_blocks(int H, int W, dim3& grid) {
