@@ -33,6 +33,19 @@ __device__ __forceinline__ void stage_rows(float* s, const float* __restrict__ s
     const int total = n * T::ROW;
     if (T::ROW % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
         const float4* s4 = reinterpret_cast<const float4*>(src);
+        if (n == SH_BLOCK) {  // full block: every lane's ROW/4 loads issued before the first LDS store
+            constexpr int IT = T::ROW / 4 > 0 ? T::ROW / 4 : 1;  // float4 per lane (ROW % 4 == 0 here)
+            float4 v[IT];
+#pragma unroll
+            for (int k = 0; k < IT; k++) v[k] = s4[threadIdx.x + k * SH_BLOCK];
+#pragma unroll
+            for (int k = 0; k < IT; k++) {
+                const int e = 4 * (threadIdx.x + k * SH_BLOCK), r = e / T::ROW, c = e - r * T::ROW;
+                float* d = s + r * T::PITCH + c;
+                d[0] = v[k].x; d[1] = v[k].y; d[2] = v[k].z; d[3] = v[k].w;
+            }
+            return;
+        }
         for (int e4 = threadIdx.x; 4 * e4 < total; e4 += SH_BLOCK) {
             const float4 v = s4[e4];
             const int e = 4 * e4, r = e / T::ROW, c = e - r * T::ROW;  // ROW % 4 == 0: no row straddle
@@ -83,7 +96,33 @@ __device__ __forceinline__ void adam_rows(float* p, float* m, float* v, const fl
         float4* p4 = reinterpret_cast<float4*>(p);
         float4* m4 = reinterpret_cast<float4*>(m);
         float4* v4 = reinterpret_cast<float4*>(v);
-        for (int e4 = threadIdx.x; 4 * e4 < total; e4 += SH_BLOCK) {
+        constexpr int U = 4;  // float4 groups per round trip: U loads of p, m and v in flight before the stores
+        int e4 = threadIdx.x;
+        for (; 4 * (e4 + (U - 1) * SH_BLOCK) < total; e4 += U * SH_BLOCK) {
+            float4 pv[U], mv[U], vv[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                pv[u] = p4[e4 + u * SH_BLOCK];
+                mv[u] = m4[e4 + u * SH_BLOCK];
+                vv[u] = v4[e4 + u * SH_BLOCK];
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int e = 4 * (e4 + u * SH_BLOCK), r = e / T::ROW, c = e - r * T::ROW;
+                const float* q = s + r * T::PITCH + c;
+                elem(pv[u].x, q[0], mv[u].x, vv[u].x);
+                elem(pv[u].y, q[1], mv[u].y, vv[u].y);
+                elem(pv[u].z, q[2], mv[u].z, vv[u].z);
+                elem(pv[u].w, q[3], mv[u].w, vv[u].w);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                m4[e4 + u * SH_BLOCK] = mv[u];
+                v4[e4 + u * SH_BLOCK] = vv[u];
+                p4[e4 + u * SH_BLOCK] = pv[u];
+            }
+        }
+        for (; 4 * e4 < total; e4 += SH_BLOCK) {
             const int e = 4 * e4, r = e / T::ROW, c = e - r * T::ROW;
             const float* q = s + r * T::PITCH + c;
             float4 pv = p4[e4], mv = m4[e4], vv = v4[e4];
@@ -113,11 +152,14 @@ __global__ void __launch_bounds__(SH_BLOCK) sh_eval_kernel(Camera cam, GaussIn g
     __shared__ float s_sh[SH_BLOCK * T::PITCH];
     const int base = blockIdx.x * SH_BLOCK;
     const int n = min(SH_BLOCK, g.P - base);
+    const int i = base + threadIdx.x;
+    const bool act = (int)threadIdx.x < n;
+    // the lane's mean is loaded with the staging stream, not after it
+    const float3 p = act ? make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2])
+                         : make_float3(0.f, 0.f, 0.f);
     stage_rows<NSH>(s_sh, g.shs + (size_t)T::ROW * base, n);
     __syncthreads();
-    if ((int)threadIdx.x >= n) return;
-    const int i = base + threadIdx.x;
-    const float3 p = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
+    if (!act) return;
     float rgb[3];
     unsigned clamped = 0;
     sh_fwd(cam.sh_degree, p, cam.campos, s_sh + threadIdx.x * T::PITCH, rgb, clamped);
