@@ -19,6 +19,12 @@ namespace gsr {
 namespace {
 
 constexpr int SH_BLOCK = 256;
+#ifndef GSR_SH_EVAL_BLOCK
+#define GSR_SH_EVAL_BLOCK 64
+#endif
+// sh_eval: one wave per workgroup (12.5 KB of LDS at D = 3): the waves of a CU stage and evaluate
+// independently instead of in barrier-coupled groups of four
+constexpr int SH_EVAL_BLOCK = GSR_SH_EVAL_BLOCK;
 
 template <int NSH>
 struct ShTile {
@@ -27,33 +33,33 @@ struct ShTile {
 };
 
 // Global [n x ROW] block (contiguous: M == NSH) -> LDS rows.
-template <int NSH>
+template <int NSH, int BLK = SH_BLOCK>
 __device__ __forceinline__ void stage_rows(float* s, const float* __restrict__ src, int n) {
     using T = ShTile<NSH>;
     const int total = n * T::ROW;
     if (T::ROW % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
         const float4* s4 = reinterpret_cast<const float4*>(src);
-        if (n == SH_BLOCK) {  // full block: every lane's ROW/4 loads issued before the first LDS store
+        if (n == BLK) {  // full block: every lane's ROW/4 loads issued before the first LDS store
             constexpr int IT = T::ROW / 4 > 0 ? T::ROW / 4 : 1;  // float4 per lane (ROW % 4 == 0 here)
             float4 v[IT];
 #pragma unroll
-            for (int k = 0; k < IT; k++) v[k] = s4[threadIdx.x + k * SH_BLOCK];
+            for (int k = 0; k < IT; k++) v[k] = s4[threadIdx.x + k * BLK];
 #pragma unroll
             for (int k = 0; k < IT; k++) {
-                const int e = 4 * (threadIdx.x + k * SH_BLOCK), r = e / T::ROW, c = e - r * T::ROW;
+                const int e = 4 * (threadIdx.x + k * BLK), r = e / T::ROW, c = e - r * T::ROW;
                 float* d = s + r * T::PITCH + c;
                 d[0] = v[k].x; d[1] = v[k].y; d[2] = v[k].z; d[3] = v[k].w;
             }
             return;
         }
-        for (int e4 = threadIdx.x; 4 * e4 < total; e4 += SH_BLOCK) {
+        for (int e4 = threadIdx.x; 4 * e4 < total; e4 += BLK) {
             const float4 v = s4[e4];
             const int e = 4 * e4, r = e / T::ROW, c = e - r * T::ROW;  // ROW % 4 == 0: no row straddle
             float* d = s + r * T::PITCH + c;
             d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
         }
     } else {
-        for (int e = threadIdx.x; e < total; e += SH_BLOCK) {
+        for (int e = threadIdx.x; e < total; e += BLK) {
             const int r = e / T::ROW, c = e - r * T::ROW;
             s[r * T::PITCH + c] = src[e];
         }
@@ -147,17 +153,17 @@ __device__ __forceinline__ void adam_rows(float* p, float* m, float* v, const fl
 }
 
 template <int NSH>
-__global__ void __launch_bounds__(SH_BLOCK) sh_eval_kernel(Camera cam, GaussIn g, GeomPtrs geo) {
+__global__ void __launch_bounds__(SH_EVAL_BLOCK) sh_eval_kernel(Camera cam, GaussIn g, GeomPtrs geo) {
     using T = ShTile<NSH>;
-    __shared__ float s_sh[SH_BLOCK * T::PITCH];
-    const int base = blockIdx.x * SH_BLOCK;
-    const int n = min(SH_BLOCK, g.P - base);
+    __shared__ float s_sh[SH_EVAL_BLOCK * T::PITCH];
+    const int base = blockIdx.x * SH_EVAL_BLOCK;
+    const int n = min(SH_EVAL_BLOCK, g.P - base);
     const int i = base + threadIdx.x;
     const bool act = (int)threadIdx.x < n;
     // the lane's mean is loaded with the staging stream, not after it
     const float3 p = act ? make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2])
                          : make_float3(0.f, 0.f, 0.f);
-    stage_rows<NSH>(s_sh, g.shs + (size_t)T::ROW * base, n);
+    stage_rows<NSH, SH_EVAL_BLOCK>(s_sh, g.shs + (size_t)T::ROW * base, n);
     __syncthreads();
     if (!act) return;
     float rgb[3];
@@ -209,7 +215,7 @@ sh_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii
 
 template <int NSH>
 hipError_t launch_sh_eval_t(const Camera& cam, const GaussIn& g, GeomPtrs geo, hipStream_t s) {
-    hipLaunchKernelGGL(sh_eval_kernel<NSH>, dim3((g.P + SH_BLOCK - 1) / SH_BLOCK), dim3(SH_BLOCK), 0, s, cam, g, geo);
+    hipLaunchKernelGGL(sh_eval_kernel<NSH>, dim3((g.P + SH_EVAL_BLOCK - 1) / SH_EVAL_BLOCK), dim3(SH_EVAL_BLOCK), 0, s, cam, g, geo);
     return hipGetLastError();
 }
 

@@ -19,5 +19,5 @@ import csv, glob, sys
 for v in ("base", "var", "base2"):
     f = glob.glob(f"{sys.argv[1]}/{v}/**/run_kernel_stats.csv", recursive=True)[0]
     rows = {r["Name"].split("(")[0][:40]: float(r["AverageNs"]) / 1e3 for r in csv.DictReader(open(f))}
-    print(v, {k: round(x, 2) for k, x in rows.items() if any(s in k for s in ("render", "gauss", "dupl", "prepro", "colscan"))})
+    print(v, {k: round(x, 2) for k, x in rows.items() if any(s in k for s in ("render", "gauss", "dupl", "prepro", "colscan", "sh_", "map_"))})
 PY
