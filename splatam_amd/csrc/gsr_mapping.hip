@@ -484,14 +484,31 @@ map_transform_bwd_kernel(int P, const float* ur, const float* lo, const float* l
         pv[e] = adam_update_elem(pv[e], gv[e], mv[e], vv[e], ss, adam.w1, adam.beta2, adam.omb2, adam.bc2_sqrt,
                                  adam.eps);
     }
+    // stores grouped by array (adjacent elements of one array in a row), so they merge into
+    // dwordx3 / dwordx4 stores: interleaving p / m / v stores (possibly aliasing) kept them dwords
 #pragma unroll
-    for (int k = 0; k < 3; k++) { p0[k] = pv[k]; m0[k] = mv[k]; v0[k] = vv[k]; }
+    for (int k = 0; k < 3; k++) p0[k] = pv[k];
 #pragma unroll
-    for (int k = 0; k < 4; k++) { p1[k] = pv[3 + k]; m1[k] = mv[3 + k]; v1[k] = vv[3 + k]; }
+    for (int k = 0; k < 3; k++) m0[k] = mv[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) v0[k] = vv[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) p1[k] = pv[3 + k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) m1[k] = mv[3 + k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v1[k] = vv[3 + k];
     *p2 = pv[7]; *m2 = mv[7]; *v2 = vv[7];
+    if (scols == 3) {
 #pragma unroll
-    for (int k = 0; k < 3; k++)
-        if (k < scols) { p3[k] = pv[8 + k]; m3[k] = mv[8 + k]; v3[k] = vv[8 + k]; }
+        for (int k = 0; k < 3; k++) p3[k] = pv[8 + k];
+#pragma unroll
+        for (int k = 0; k < 3; k++) m3[k] = mv[8 + k];
+#pragma unroll
+        for (int k = 0; k < 3; k++) v3[k] = vv[8 + k];
+    } else {
+        *p3 = pv[8]; *m3 = mv[8]; *v3 = vv[8];
+    }
 }
 
 int map_loss_blocks(int H, int W, dim3& grid) {
