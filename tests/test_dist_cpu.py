@@ -72,7 +72,9 @@ def _fisher_worker(rank, world, port, q):
         c[0, 3] = 0.5 * j
     hinv = sc.fit_visited(visited)
     scores = sc.eig_scores(cands)
-    q.put((rank, hinv.clone(), scores.clone()))
+    # plain lists: a tensor on a multiprocessing queue is shared through the sender's file
+    # descriptors, which vanish when the sender exits before the parent reads it
+    q.put((rank, hinv.tolist(), scores.tolist()))
     dist.destroy_process_group()
 
 
@@ -105,5 +107,5 @@ def test_fisher_scoring_sharded_world2():
     hinv = ref.fit_visited(visited)
     scores = ref.eig_scores(cands)
     for _, h, s in res:
-        assert torch.allclose(h, hinv) and torch.allclose(s, scores)
+        assert torch.allclose(torch.tensor(h, dtype=hinv.dtype), hinv) and torch.allclose(torch.tensor(s, dtype=scores.dtype), scores)
     assert bool((scores[1:] > scores[:-1]).all())
