@@ -31,6 +31,9 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
 #pragma clang fp contract(off)
     extern __shared__ uint32_t s_hist[];
     __shared__ float s_pose[16];  // XF: the frame's pose (R 9, t 3, F.normalize(q) 4), formed once by wave 0
+    const int i = blockIdx.x * PRE_BLOCK + threadIdx.x;
+    XfRaw xr{};  // XF: the Gaussian's transform inputs, in flight while wave 0 forms the pose
+    if (XF && i < g.P) xr = track_xform_load(g.xf, i, true);
     if (XF && threadIdx.x < 64) {
         const Pose ps = make_pose(g.xf.cq, g.xf.ct, g.xf.qs);
         if (threadIdx.x == 0) {
@@ -45,7 +48,6 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     if (LDS_HIST)
         for (int t = threadIdx.x; t < ntiles; t += PRE_BLOCK) s_hist[t] = 0u;
     if (LDS_HIST || XF) __syncthreads();
-    const int i = blockIdx.x * PRE_BLOCK + threadIdx.x;
     if (i == 0) geo.counters[4] = 0u;  // tile_colscan_kernel's arrival counter (next launch)
     uint32_t tiles = 0;
     bool violation = false;  // prefiltered set but the point is culled (auxiliary.h:154-160)
@@ -64,7 +66,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
 #pragma unroll
             for (int k = 0; k < 4; k++) ps.c[k] = s_pose[12 + k];
             float m[3];
-            track_xform_compute(g.xf, ps, i, m, xq, xc2, xop, xs);  // (stored below, after every load)
+            track_xform_compute_raw(g.xf, xr, ps, m, xq, xc2, xop, xs);  // (stored below, after every load)
             p = make_float3(m[0], m[1], m[2]);
         } else {
             p = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);

@@ -41,7 +41,9 @@ __device__ __forceinline__ Pose make_pose(const float* q, const float* t, int st
 }
 
 // quat_mult(a, b) (slam_helpers.py), (w, x, y, z)
+// (contraction off here and in normalize4: the same bits in every kernel that inlines them)
 __device__ __forceinline__ float4 quat_mult(const float a[4], float4 b) {
+#pragma clang fp contract(off)
     return make_float4(a[0] * b.x - a[1] * b.y - a[2] * b.z - a[3] * b.w,
                        a[0] * b.y + a[1] * b.x + a[2] * b.w - a[3] * b.z,
                        a[0] * b.z - a[1] * b.w + a[2] * b.x + a[3] * b.y,
@@ -49,6 +51,7 @@ __device__ __forceinline__ float4 quat_mult(const float a[4], float4 b) {
 }
 
 __device__ __forceinline__ float4 normalize4(float4 v, float& norm) {
+#pragma clang fp contract(off)
     norm = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
     const float d = fmaxf(norm, kNormEps);
     return make_float4(v.x / d, v.y / d, v.z / d, v.w / d);
@@ -72,31 +75,55 @@ __device__ __forceinline__ float4 load4(const float* p) { return make_float4(p[0
 // counts both on gfx950), which serialised ~5 store round trips in preprocess (6 us).
 // The geometric part (mean, rotation, scale) alone: also what the tracking backward recomputes
 // (PoseFuse::ls) instead of reading stored rendervars -- the same expressions, so the same bits.
-__device__ __forceinline__ void track_xform_geom(const TrackXf& x, const Pose& ps, int i, float (&m)[3], float4& q,
-                                                 float (&s)[3]) {
-    const float p0 = x.mw[3 * i], p1 = x.mw[3 * i + 1], p2 = x.mw[3 * i + 2];
-    const float4 ur = load4(x.ur + 4 * i);
-    float lsv[3];
+// The transform's per-Gaussian inputs, loaded ahead of the arithmetic (the transform-fused
+// preprocess issues them before its pose barrier, overlapping the pose's own loads).
+struct XfRaw {
+    float p[3];
+    float4 ur;
+    float ls[3];
+    float lo;
+};
+__device__ __forceinline__ XfRaw track_xform_load(const TrackXf& x, int i, bool with_opacity) {
+    XfRaw r;
+    r.p[0] = x.mw[3 * i]; r.p[1] = x.mw[3 * i + 1]; r.p[2] = x.mw[3 * i + 2];
+    r.ur = load4(x.ur + 4 * i);
 #pragma unroll
-    for (int k = 0; k < 3; k++) lsv[k] = x.ls[x.scols == 1 ? i : 3 * i + k];
+    for (int k = 0; k < 3; k++) r.ls[k] = x.ls[x.scols == 1 ? i : 3 * i + k];
+    r.lo = with_opacity ? x.lo[i] : 0.f;
+    return r;
+}
+__device__ __forceinline__ void track_xform_geom_raw(const XfRaw& r, int scols, const Pose& ps, float (&m)[3],
+                                                     float4& q, float (&s)[3]) {
+    // contraction off: the same bits in every kernel that inlines this (the forward's transform,
+    // the transform-fused preprocess, the backward's recomputation), whatever the surrounding code
+#pragma clang fp contract(off)
 #pragma unroll
-    for (int r = 0; r < 3; r++) m[r] = ps.R[r][0] * p0 + ps.R[r][1] * p1 + ps.R[r][2] * p2 + ps.t[r];
+    for (int k = 0; k < 3; k++) m[k] = ps.R[k][0] * r.p[0] + ps.R[k][1] * r.p[1] + ps.R[k][2] * r.p[2] + ps.t[k];
     float un_norm;
-    q = normalize4(ur, un_norm);                                 // F.normalize(unnorm_rotations)
-    if (x.scols != 1) {                                          // anisotropic: compose with the camera
+    q = normalize4(r.ur, un_norm);                               // F.normalize(unnorm_rotations)
+    if (scols != 1) {                                            // anisotropic: compose with the camera
         float o_norm;
         q = normalize4(quat_mult(ps.c, q), o_norm);
     }
 #pragma unroll
-    for (int k = 0; k < 3; k++) s[k] = expf(lsv[k]);
+    for (int k = 0; k < 3; k++) s[k] = expf(r.ls[k]);
+}
+__device__ __forceinline__ void track_xform_geom(const TrackXf& x, const Pose& ps, int i, float (&m)[3], float4& q,
+                                                 float (&s)[3]) {
+    track_xform_geom_raw(track_xform_load(x, i, false), x.scols, ps, m, q, s);
+}
+__device__ __forceinline__ void track_xform_compute_raw(const TrackXf& x, const XfRaw& r, const Pose& ps,
+                                                        float (&m)[3], float4& q, float (&c2)[3], float& op,
+                                                        float (&s)[3]) {
+#pragma clang fp contract(off)
+    track_xform_geom_raw(r, x.scols, ps, m, q, s);
+    const float z = x.w2c[8] * m[0] + x.w2c[9] * m[1] + x.w2c[10] * m[2] + x.w2c[11];
+    c2[0] = z; c2[1] = 1.f; c2[2] = z * z;
+    op = 1.f / (1.f + expf(-r.lo));
 }
 __device__ __forceinline__ void track_xform_compute(const TrackXf& x, const Pose& ps, int i, float (&m)[3],
                                                     float4& q, float (&c2)[3], float& op, float (&s)[3]) {
-    const float lo = x.lo[i];
-    track_xform_geom(x, ps, i, m, q, s);
-    const float z = x.w2c[8] * m[0] + x.w2c[9] * m[1] + x.w2c[10] * m[2] + x.w2c[11];
-    c2[0] = z; c2[1] = 1.f; c2[2] = z * z;
-    op = 1.f / (1.f + expf(-lo));
+    track_xform_compute_raw(x, track_xform_load(x, i, true), ps, m, q, c2, op, s);
 }
 __device__ __forceinline__ void track_xform_store(int i, const float (&m)[3], float4 q, const float (&c2)[3], float op,
                                                   const float (&s)[3], float* mc, float* rot, float* dcol,
