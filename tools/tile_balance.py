@@ -143,6 +143,12 @@ def main():
         rng = v["ranges"].cpu().numpy().astype(np.int64)
         nc = v["n_contrib"].cpu().numpy().reshape(H, W).astype(np.int64)
         cull = instance_culling(out[3], v, W, H, R, s.P)
+        # gauss_bwd: a lane sums its Gaussian's instance records, RU = 4 per memory round trip;
+        # a wave of 64 consecutive Gaussians waits for its longest lane
+        per_g = torch.bincount(v["point_list"].long()[:R], minlength=s.P).cpu().numpy()
+        pad = (-s.P) % 64
+        wv = np.concatenate([per_g, np.zeros(pad, np.int64)]).reshape(-1, 64)
+        wave_trips = np.ceil(wv.max(1) / 4.0)
     gx, gy = (W + 15) // 16, (H + 15) // 16
     ncp = np.zeros((gy * 16, gx * 16), np.int64)
     ncp[:H, :W] = nc
@@ -156,6 +162,10 @@ def main():
     order = np.sort(bmax)[::-1]
     print("top-16 bwd trip counts", order[:16].tolist())
     print("trip/list ratio mean", float((bmax / np.maximum(length, 1)).mean()))
+    stats("inst/gauss", per_g)
+    stats("wave_max", wv.max(1))
+    print(f"gauss_bwd record round trips per wave: mean {wave_trips.mean():.2f} "
+          f"(balanced {np.ceil(wv.sum(1) / 64 / 4).mean():.2f})")
     for k, val in cull.items():
         print(f"{k:34s} {val:.4f}")
 
