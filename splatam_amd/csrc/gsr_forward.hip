@@ -227,8 +227,14 @@ tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t*
     }
     s_part[q][tl] = sum;
     __syncthreads();
-    uint32_t run = 0;
-    for (int k = 0; k < q; k++) run += s_part[k][tl];
+    {  // wave w scans tile w's CS_PARTS part sums (lane = part) in place: exclusive prefixes
+        static_assert(CS_PARTS == 64, "one wave per tile column (CS_TILES waves)");
+        const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const uint32_t v = s_part[lane][w];
+        s_part[lane][w] = wave_incl_scan(v) - v;
+    }
+    __syncthreads();
+    uint32_t run = s_part[q][tl];
     if (t < ntiles) {
         if (in_regs) {
 #pragma unroll
