@@ -41,18 +41,19 @@ __device__ __forceinline__ Pose make_pose(const float* q, const float* t, int st
 }
 
 // quat_mult(a, b) (slam_helpers.py), (w, x, y, z)
-// (contraction off here and in normalize4: the same bits in every kernel that inlines them)
+// (explicit FMAs, contraction off here and in normalize4: the same bits in every kernel that inlines them)
 __device__ __forceinline__ float4 quat_mult(const float a[4], float4 b) {
 #pragma clang fp contract(off)
-    return make_float4(a[0] * b.x - a[1] * b.y - a[2] * b.z - a[3] * b.w,
-                       a[0] * b.y + a[1] * b.x + a[2] * b.w - a[3] * b.z,
-                       a[0] * b.z - a[1] * b.w + a[2] * b.x + a[3] * b.y,
-                       a[0] * b.w + a[1] * b.z - a[2] * b.y + a[3] * b.x);
+    // explicit fused multiply-adds (fixed, not left to the contraction of the caller's context)
+    return make_float4(__builtin_fmaf(-a[3], b.w, __builtin_fmaf(-a[2], b.z, __builtin_fmaf(-a[1], b.y, a[0] * b.x))),
+                       __builtin_fmaf(-a[3], b.z, __builtin_fmaf(a[2], b.w, __builtin_fmaf(a[1], b.x, a[0] * b.y))),
+                       __builtin_fmaf(a[3], b.y, __builtin_fmaf(a[2], b.x, __builtin_fmaf(-a[1], b.w, a[0] * b.z))),
+                       __builtin_fmaf(a[3], b.x, __builtin_fmaf(-a[2], b.y, __builtin_fmaf(a[1], b.z, a[0] * b.w))));
 }
 
 __device__ __forceinline__ float4 normalize4(float4 v, float& norm) {
 #pragma clang fp contract(off)
-    norm = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
+    norm = sqrtf(__builtin_fmaf(v.w, v.w, __builtin_fmaf(v.z, v.z, __builtin_fmaf(v.y, v.y, v.x * v.x))));
     const float d = fmaxf(norm, kNormEps);
     return make_float4(v.x / d, v.y / d, v.z / d, v.w / d);
 }
@@ -94,11 +95,13 @@ __device__ __forceinline__ XfRaw track_xform_load(const TrackXf& x, int i, bool 
 }
 __device__ __forceinline__ void track_xform_geom_raw(const XfRaw& r, int scols, const Pose& ps, float (&m)[3],
                                                      float4& q, float (&s)[3]) {
-    // contraction off: the same bits in every kernel that inlines this (the forward's transform,
-    // the transform-fused preprocess, the backward's recomputation), whatever the surrounding code
+    // explicit fused multiply-adds, contraction off otherwise: the same bits in every kernel that
+    // inlines this (the forward's transform, the transform-fused preprocess, the backward's
+    // recomputation), whatever the surrounding code
 #pragma clang fp contract(off)
 #pragma unroll
-    for (int k = 0; k < 3; k++) m[k] = ps.R[k][0] * r.p[0] + ps.R[k][1] * r.p[1] + ps.R[k][2] * r.p[2] + ps.t[k];
+    for (int k = 0; k < 3; k++)
+        m[k] = __builtin_fmaf(ps.R[k][2], r.p[2], __builtin_fmaf(ps.R[k][1], r.p[1], __builtin_fmaf(ps.R[k][0], r.p[0], ps.t[k])));
     float un_norm;
     q = normalize4(r.ur, un_norm);                               // F.normalize(unnorm_rotations)
     if (scols != 1) {                                            // anisotropic: compose with the camera
@@ -117,7 +120,7 @@ __device__ __forceinline__ void track_xform_compute_raw(const TrackXf& x, const 
                                                         float (&s)[3]) {
 #pragma clang fp contract(off)
     track_xform_geom_raw(r, x.scols, ps, m, q, s);
-    const float z = x.w2c[8] * m[0] + x.w2c[9] * m[1] + x.w2c[10] * m[2] + x.w2c[11];
+    const float z = __builtin_fmaf(x.w2c[10], m[2], __builtin_fmaf(x.w2c[9], m[1], __builtin_fmaf(x.w2c[8], m[0], x.w2c[11])));
     c2[0] = z; c2[1] = 1.f; c2[2] = z * z;
     op = 1.f / (1.f + expf(-r.lo));
 }
