@@ -86,6 +86,8 @@ def build_variant(tag: str, defines=()) -> str:
     splatam_amd/_build_<tag>/libgsr_<tag>.so; loaded only through GSR_LIB."""
     objdir = os.path.join(HERE, f"_build_{tag}")
     os.makedirs(objdir, exist_ok=True)
+    if isinstance(defines, dict):  # {"NAME": "value"} -> NAME=value (iterating a dict would drop the values)
+        defines = [f"{k}={v}" for k, v in defines.items()]
     extra = tuple(f"-D{d}" for d in defines)
     with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
         objs = list(ex.map(lambda s: _compile(s, objdir, extra), SOURCES))
