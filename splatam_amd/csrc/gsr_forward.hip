@@ -185,7 +185,10 @@ hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, 
 // are loaded once, all in flight, and kept in registers for the offset pass
 // (the previous 64-tile x 16-segment shape ran 19 workgroups of two dependent
 // load passes: 16.5 us at config 3).
-constexpr int CS_TILES = 16, CS_PARTS = 64, CS_RQ = 16;
+#ifndef GSR_CS_TILES
+#define GSR_CS_TILES 16
+#endif
+constexpr int CS_TILES = GSR_CS_TILES, CS_PARTS = 1024 / CS_TILES, CS_RQ = CS_PARTS == 64 ? 16 : 32;
 template <bool AGENT_TILES>
 __device__ void scan_counts_body(const uint32_t* __restrict__ wgsum, uint32_t* __restrict__ blocksums, uint32_t nb,
                                  const uint32_t* __restrict__ tile_count, uint32_t tile_stride, uint32_t ntiles,
@@ -227,11 +230,18 @@ tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t*
     }
     s_part[q][tl] = sum;
     __syncthreads();
-    {  // wave w scans tile w's CS_PARTS part sums (lane = part) in place: exclusive prefixes
-        static_assert(CS_PARTS == 64, "one wave per tile column (CS_TILES waves)");
+    {  // each wave scans 64 / CS_PARTS tile columns' part sums (lane = part) in place: exclusive prefixes
+        static_assert(CS_PARTS == 64 || CS_PARTS == 32, "one or two tile columns per wave");
+        constexpr int CPW = 64 / CS_PARTS;  // columns per wave
         const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        const uint32_t v = s_part[lane][w];
-        s_part[lane][w] = wave_incl_scan(v) - v;
+        const int part = lane % CS_PARTS, colw = CPW * w + lane / CS_PARTS;
+        const uint32_t v = s_part[part][colw];
+        uint32_t inc = wave_incl_scan(v);
+        if (CPW == 2) {  // the upper half-wave's column starts after the lower column's total
+            const uint32_t lo_tot = (uint32_t)__shfl((int)inc, 31);
+            if (lane >= 32) inc -= lo_tot;
+        }
+        s_part[part][colw] = inc - v;
     }
     __syncthreads();
     uint32_t run = s_part[q][tl];
