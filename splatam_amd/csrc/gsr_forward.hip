@@ -185,10 +185,14 @@ hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, 
 // are loaded once, all in flight, and kept in registers for the offset pass
 // (the previous 64-tile x 16-segment shape ran 19 workgroups of two dependent
 // load passes: 16.5 us at config 3).
-#ifndef GSR_CS_TILES
-#define GSR_CS_TILES 16
-#endif
-constexpr int CS_TILES = GSR_CS_TILES, CS_PARTS = 1024 / CS_TILES, CS_RQ = CS_PARTS == 64 ? 16 : 32;
+// Two shapes: 16 tiles x 64 parts (64-B row segments) for count matrices of <= 512 rows, 32 x 32
+// (128-B segments, <= 32 rows per thread) above: 5.2 vs 5.8 us at config 3 (293 rows), 19.1 vs
+// 16.2 us at config 4 (977 rows).
+constexpr int CS_THREADS = 1024, CS_ROWS_SMALL = 512;
+template <int CT>
+struct ColscanShape {
+    static constexpr int TILES = CT, PARTS = CS_THREADS / CT, RQ = PARTS == 64 ? 16 : 32;
+};
 template <bool AGENT_TILES>
 __device__ void scan_counts_body(const uint32_t* __restrict__ wgsum, uint32_t* __restrict__ blocksums, uint32_t nb,
                                  const uint32_t* __restrict__ tile_count, uint32_t tile_stride, uint32_t ntiles,
@@ -204,10 +208,11 @@ constexpr int SCAN_ITEMS = 4;
 // path) every duplicate_bucket workgroup does those scans itself in its
 // prologue, which removes this launch's serial tail (arrival + one-workgroup
 // scan: ~10 us of latency at config 3).
-template <bool TAIL>
-__global__ void __launch_bounds__(CS_TILES * CS_PARTS)
+template <bool TAIL, int CT>
+__global__ void __launch_bounds__(CS_THREADS)
 tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t* __restrict__ tot, GeomPtrs geo,
                     uint2* __restrict__ ranges, uint32_t sort_cap, uint32_t* __restrict__ status) {
+    constexpr int CS_TILES = ColscanShape<CT>::TILES, CS_PARTS = ColscanShape<CT>::PARTS, CS_RQ = ColscanShape<CT>::RQ;
     __shared__ uint32_t s_part[CS_PARTS][CS_TILES];
     const int tl = threadIdx.x % CS_TILES, q = threadIdx.x / CS_TILES;
     const int t = blockIdx.x * CS_TILES + tl;
@@ -274,10 +279,12 @@ tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t*
 
 hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, GeomPtrs geo, uint2* ranges,
                                uint32_t* status, bool tail, hipStream_t s) {
-    static_assert(CS_TILES * CS_PARTS == SCAN_THREADS, "the last colscan workgroup runs the scan body");
-    hipLaunchKernelGGL(tail ? tile_colscan_kernel<true> : tile_colscan_kernel<false>,
-                       dim3((ntiles + CS_TILES - 1) / CS_TILES), dim3(CS_TILES * CS_PARTS), 0, s,
-                       counts, nb, ntiles, tot, geo, ranges, (uint32_t)TILE_SORT_CAP, status);
+    static_assert(CS_THREADS == SCAN_THREADS, "the last colscan workgroup runs the scan body");
+    const int ct = nb <= CS_ROWS_SMALL ? 16 : 32;
+    auto k = tail ? (ct == 16 ? tile_colscan_kernel<true, 16> : tile_colscan_kernel<true, 32>)
+                  : (ct == 16 ? tile_colscan_kernel<false, 16> : tile_colscan_kernel<false, 32>);
+    hipLaunchKernelGGL(k, dim3((ntiles + ct - 1) / ct), dim3(CS_THREADS), 0, s, counts, nb, ntiles, tot, geo, ranges,
+                       (uint32_t)TILE_SORT_CAP, status);
     return hipGetLastError();
 }
 
