@@ -566,10 +566,17 @@ hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint6
     return hipGetLastError();
 }
 
-template <bool POSE>
+// SHL: per-lane SH chain (g.shs may be set).  Without it (colours precomputed, or SH handled by
+// the staged sh_bwd_kernel) g.shs is NULL at compile time, and the 48-float dsh array and the SH
+// chain drop out of the kernel (mapping variant: 142 -> fewer VGPRs, more waves per SIMD).
+template <bool POSE, bool SHL>
 __global__ void __launch_bounds__(256)
 gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float* __restrict__ inst,
                  RecLayout rec, GradsOut out, BwdGuard guard, PoseFuse pf) {
+    if constexpr (!SHL) {
+        g.shs = nullptr;
+        g.M = 0;
+    }
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (!POSE && i >= g.P) return;  // (POSE: every lane takes part in the workgroup sum)
     const bool live = i < g.P;
@@ -805,7 +812,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     if (out.drot)
 #pragma unroll
         for (int k = 0; k < 4; k++) out.drot[4 * i + k] = drot[k];
-    if (out.dsh && g.M > 0) {
+    if (SHL && out.dsh && g.M > 0) {
         float* d = out.dsh + (size_t)3 * g.M * i;
 #pragma unroll
         for (int k = 0; k < 48; k++)
@@ -820,12 +827,11 @@ int pose_fuse_scratch_floats(int P) { return POSE_PARTS * ((P + 255) / 256) + AR
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* inst,
                             RecLayout rec, const GradsOut& out, BwdGuard guard, hipStream_t s, const PoseFuse* pose) {
     if (g.P == 0) return hipSuccess;
-    if (pose)
-        hipLaunchKernelGGL(gauss_bwd_kernel<true>, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii, inst,
-                           rec, out, guard, *pose);
-    else
-        hipLaunchKernelGGL(gauss_bwd_kernel<false>, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii,
-                           inst, rec, out, guard, PoseFuse{});
+    const bool shl = g.shs != nullptr;
+    auto k = pose ? (shl ? gauss_bwd_kernel<true, true> : gauss_bwd_kernel<true, false>)
+                  : (shl ? gauss_bwd_kernel<false, true> : gauss_bwd_kernel<false, false>);
+    hipLaunchKernelGGL(k, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii, inst, rec, out, guard,
+                       pose ? *pose : PoseFuse{});
     return hipGetLastError();
 }
 
