@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -152,18 +153,17 @@ def main():
 
     tracker = None
     steps = args.steps
+    FI = max(1, args.frame_iters)
     if args.graph:
-        # HIP graph of S tracking iterations (splatam_amd/tracker.py); warm-up and timed
-        # region are whole replays, so K is rounded up to a multiple of S
+        # HIP graph of S tracking iterations (splatam_amd/tracker.py).  Exactly `steps` iterations are
+        # timed: frames of FI iterations (fresh optimizer, best-candidate write-back), the last one
+        # partial when FI does not divide steps; S divides both so every frame is whole replays.
         from splatam_amd.tracker import GraphTracker
-        S = max(1, min(args.iters_per_graph, args.frame_iters))
-        FI = -(-args.frame_iters // S) * S  # iterations per frame, whole replays
-        steps = -(-args.steps // FI) * FI
+        S = math.gcd(math.gcd(max(1, args.iters_per_graph), FI), max(1, steps))
+        # warm-up: W eager tracking iterations plus one priming replay, all undone (pose restored,
+        # optimizer reset) before the timed frames
         tracker = GraphTracker(params, curr, frame, iters_per_graph=S, timing=bool(args.timing),
-                               fuse_pose=bool(args.fuse_pose),
-                               warmup_iters=min(3, max(1, args.warmup)))
-        for _ in range(max(1, -(-args.warmup // FI))):
-            tracker.track_frame(FI)
+                               fuse_pose=bool(args.fuse_pose), warmup_iters=max(1, args.warmup), prime=True)
     else:
         for _ in range(args.warmup):
             step()
@@ -178,10 +178,14 @@ def main():
     t0 = time.perf_counter()
     if tracker is not None:
         per_bcast = max(1, args.bcast_every // FI) if args.bcast_every > 0 else 0
-        for f in range(steps // FI):
+        done, f = 0, 0
+        while done < steps:
             if world > 1 and per_bcast and f % per_bcast == 0:
                 sd.broadcast_map(params)       # map update -> RCCL broadcast over xGMI
-            tracker.track_frame(FI)            # one frame: fresh optimizer, replays, best pose written back
+            n = min(FI, steps - done)
+            tracker.track_frame(n)             # one frame: fresh optimizer, replays, best pose written back
+            done += n
+            f += 1
     else:
         for i in range(steps):
             if world > 1 and args.bcast_every > 0 and i % args.bcast_every == 0:
@@ -290,10 +294,11 @@ def main():
             "metric": METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": steps,
             "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "execution": (f"frames of {FI} tracking iterations: HIP graph of {tracker.iters} iterations replayed "
-                          f"{FI // tracker.iters}x per frame between the frame's optimizer reset and best-candidate "
-                          f"write-back; binning capacity {tracker.capacity}, no overflow" if tracker is not None
-                          else "eager"),
+            "execution": (f"{steps} timed tracking iterations in frames of up to {FI} (fresh optimizer per "
+                          f"frame, best-candidate pose written back): HIP graph of {tracker.iters} iterations "
+                          f"replayed {-(-steps // tracker.iters)}x; warm-up {args.warmup} eager iterations + one "
+                          f"priming replay, undone; binning capacity {tracker.capacity}, no overflow"
+                          if tracker is not None else "eager"),
             "data": "synthetic (SURVEY.md 8(d) seeded scene; targets rendered at the unperturbed pose)",
             "config": {"workload": f"config {args.config}: {P} isotropic Gaussians, {W}x{H}, SplaTAM tracking "
                                    "iteration (RGB + depth/silhouette render fwd+bwd, masked L1, Adam on pose)",
@@ -425,9 +430,10 @@ def fisher_leg(args, scene, dev, launches: int = 6):
     bf = BatchedFisher(sc, K, mode="sum", probe_w2cs=poses)
     bf.hessian_sum(poses)
     torch.cuda.synchronize()
+    bf.status.zero_()
     t0 = time.perf_counter()
     for _ in range(launches):
-        bf.hessian_sum(poses)
+        bf.hessian_sum(poses, check=False)  # the sticky status rows are checked once after the timed launches
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if bf.overflowed():
@@ -521,10 +527,10 @@ def run_mapping(args, world, rank, dev):
         del truth
     for k in ("means3D", "unnorm_rotations", "logit_opacities", "log_scales", key):
         params[k].requires_grad_(True)
-    S = max(1, min(args.iters_per_graph, args.steps))
-    steps = -(-args.steps // S) * S
+    steps = max(1, args.steps)
+    S = math.gcd(max(1, args.iters_per_graph), steps)  # exactly `steps` timed iterations, whole replays
     mapper = GraphMapper(params, kfs, iters_per_graph=S, cfg=MappingConfig(), timing=bool(args.timing))
-    for _ in range(max(1, args.warmup // S)):
+    for _ in range(max(1, -(-args.warmup // S))):  # >= W untimed iterations (whole replays)
         mapper.run()
     torch.cuda.synchronize()
     if world > 1:

@@ -207,6 +207,11 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix,
 size_t gsr_geom_buffer_bytes(int P);
 size_t gsr_binning_buffer_bytes(int num_rendered, int image_width, int image_height);
 size_t gsr_image_buffer_bytes(int image_width, int image_height);
+/* Byte offset, inside a geometry buffer of P Gaussians, of the forward's device counters
+ * (4 x u32, the status-row layout of gsr_forward_dual_static: num_rendered, prefiltered
+ * violation, longest tile list, sort cap).  Passed as gsr_map_adam.status, they make the
+ * fused optimizer steps guard on that one call's forward instead of a sticky status row. */
+size_t gsr_geom_counters_offset(int P);
 
 const char* gsr_last_error(void);
 int gsr_abi_version(void);

@@ -238,14 +238,17 @@ typedef struct gsr_map_adam {
     double lr[5];
     int step;
     double beta1, beta2, eps;
-    /* optional: the static-mode status row of this iteration's forward and its binning capacity;
-     * an overflow there (see gsr_pose_track) skips the step -- parameters and state unchanged */
+    /* optional: the counters of this iteration's static-mode forward and its binning capacity;
+     * an overflow there (see gsr_pose_track) skips the step -- parameters and state unchanged.
+     * Point it at the forward's own counters (geom_buffer + gsr_geom_counters_offset(P)); a
+     * sticky status row would skip every later step once any earlier call overflowed.
+     * gsr_backward_dual_sh_adam ignores it and guards on its own forward's counters. */
     const unsigned* status;
     unsigned capacity;
 } gsr_map_adam;
 
 /* gsr_backward_dual with the mapping optimizer's colour group (sh_adam->exp_avg[4] / exp_avg_sq[4] /
- * lr[4], step, betas, eps, status) applied to the SH coefficients gaussians->shs in place inside the
+ * lr[4], step, betas, eps) applied to the SH coefficients gaussians->shs in place inside the
  * SH backward stage, instead of writing grads->dsh (which may be NULL) for
  * gsr_map_transform_bwd_adam to step: the 192-B-per-Gaussian gradient never makes the HBM round
  * trip.  Same element update (bitwise) as gsr_map_transform_bwd_adam's; call that one afterwards

@@ -201,3 +201,29 @@ def check_grad_accuracy(gpu_grads, ref32, ref64, stable):
             bad[k] = why
     assert not bad, dict(failed=bad, gpu=g, oracle_f32=o)
     return g, o
+
+
+def unstable_grad_stats(gpu_grads, ref32, ref64, unstable):
+    """The Gaussians check_grad_accuracy excludes (a pair of theirs sits near an alpha / T
+    decision, so a float32 implementation may legitimately include or drop it): per gradient
+    tensor, relative L2 error against float64 over that subset and the 99 % quantile of the
+    per-element ratio r (as in grad_accuracy), for the product and for the float32 oracle.
+    Returns {tensor: dict(gpu_rel_l2, f32_rel_l2, gpu_q99, f32_q99)}."""
+    out = {}
+    if not unstable.any():
+        return out
+    for k, v in gpu_grads.items():
+        if k not in ref64 or k not in ref32 or not isinstance(ref64[k], np.ndarray) or v.size == 0:
+            continue
+        P = v.shape[0]
+        x = np.asarray(v, np.float64).reshape(P, -1)[unstable]
+        o = np.asarray(ref32[k], np.float64).reshape(P, -1)[unstable]
+        b = np.asarray(ref64[k], np.float64).reshape(P, -1)[unstable]
+        if not b.any():
+            continue
+        s = np.asarray(ref64["scale"][k], np.float64).reshape(P, -1)[unstable]
+        den = 1e-4 * np.abs(b) + s + 1e-30
+        out[k] = dict(gpu_rel_l2=rel_l2(x, b), f32_rel_l2=rel_l2(o, b),
+                      gpu_q99=float(np.quantile(np.abs(x - b) / den, 0.99)),
+                      f32_q99=float(np.quantile(np.abs(o - b) / den, 0.99)))
+    return out

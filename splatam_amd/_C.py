@@ -114,7 +114,8 @@ REUSE_STATS = {"hits": 0, "misses": 0}  # eligible calls that did / did not reus
 
 class _Prev:
     """The last eager single-call forward on a (thread, device)."""
-    __slots__ = ("key", "shared", "shared_versions", "others", "versions", "bufs", "radii", "num_rendered")
+    __slots__ = ("key", "shared", "shared_versions", "others", "versions", "bufs", "radii", "radii_version",
+                 "num_rendered")
 
 
 def _try_reuse(key, shared, others, P):
@@ -138,8 +139,8 @@ def _try_reuse(key, shared, others, P):
     radii = prev.radii()
     if any(t is None for t in po) or any(b is None for b in bufs) or radii is None:
         return _miss("dead")
-    if any(t._version != v for t, v in zip(po, prev.versions)):
-        return _miss("version")
+    if any(t._version != v for t, v in zip(po, prev.versions)) or radii._version != prev.radii_version:
+        return _miss("version")  # (radii: copied into this call's, so an in-place edit must miss)
     if any(a is None or a.shape != b.shape for a, b in zip(others, po)):
         return _miss("shape")
     flag = _flag(key[0])
@@ -179,6 +180,7 @@ def _remember(key, shared, others, bufs, radii, num_rendered):
     p.versions = [t._version for t in others]
     p.bufs = [weakref.ref(b) for b in bufs]
     p.radii = weakref.ref(radii)
+    p.radii_version = radii._version
     p.num_rendered = num_rendered
     _tls.prev[key[0]] = p
 

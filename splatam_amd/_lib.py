@@ -84,6 +84,7 @@ SIGNATURES = {
     "gsr_bitwise_equal": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gsr_mark_visible": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gsr_geom_buffer_bytes": (c_size_t, [c_int]),
+    "gsr_geom_counters_offset": (c_size_t, [c_int]),
     "gsr_binning_buffer_bytes": (c_size_t, [c_int, c_int, c_int]),
     "gsr_image_buffer_bytes": (c_size_t, [c_int, c_int]),
     "gsr_last_error": (ctypes.c_char_p, []),

@@ -285,6 +285,7 @@ int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 const char* gsr_last_error(void) { return g_last_error.c_str(); }
 
 size_t gsr_geom_buffer_bytes(int P) { return GeomLayout::make(P).total; }
+size_t gsr_geom_counters_offset(int P) { return GeomLayout::make(P).counters; }
 size_t gsr_binning_buffer_bytes(int num_rendered, int W, int H) { return BinLayout::make(num_rendered, W, H).total; }
 size_t gsr_image_buffer_bytes(int W, int H) { return ImgLayout::make(W, H).total; }
 
@@ -525,6 +526,8 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     hipStream_t stream = (hipStream_t)stream_;
     Camera cam = make_camera(settings);
     const GaussIn g = make_gauss(gaussians);
+    if (sh_adam && (power != 1 || !sh_staged(cam, g)))  // checked before any work is enqueued
+        return fail(GSR_ERR_INVALID_ARG, "sh_adam needs staged SH colours (M == (D+1)^2) and power 1");
     const int P = g.P;
     if (P == 0) return GSR_OK;
     if (!geom_buffer || !image_buffer || !radii || !dL_dout_color)
@@ -627,9 +630,15 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
         if ((e = launch_gauss_bwd(cam, gc, geo, radii, inst, rec, oc, guard, stream, pose ? &pc : nullptr)) !=
             hipSuccess)
             return hip_fail(e, "gaussian backward");
-        if (sh_adam && !shs_staged) return fail(GSR_ERR_INVALID_ARG, "sh_adam needs staged SH colours (M == (D+1)^2)");
-        if (shs_staged && (e = launch_sh_bwd(cam, g, geo, radii, drgb, out.dmeans3D, out.dsh, guard, stream,
-                                             sh_adam ? *sh_adam : ShAdam{})) != hipSuccess)
+        // the colour step guards on this call's own forward counters (not a sticky status row: an
+        // overflow in an earlier replay must not skip the steps of later valid iterations)
+        ShAdam sa = sh_adam ? *sh_adam : ShAdam{};
+        if (sh_adam) {
+            sa.guard = geo.counters;
+            sa.cap = (uint32_t)num_rendered;
+        }
+        if (shs_staged && (e = launch_sh_bwd(cam, g, geo, radii, drgb, out.dmeans3D, out.dsh, guard, stream, sa)) !=
+                              hipSuccess)
             return hip_fail(e, "sh backward");
     }
     return GSR_OK;
@@ -908,8 +917,7 @@ int gsr_backward_dual_sh_adam(const gsr_settings* settings, const gsr_gaussians*
     sa.omb2 = (float)(1.0 - sh_adam->beta2);
     sa.bc2_sqrt = (float)sqrt(1.0 - pow(sh_adam->beta2, (double)sh_adam->step));
     sa.eps = (float)sh_adam->eps;
-    sa.guard = sh_adam->status;
-    sa.cap = sh_adam->capacity;
+    // sa.guard / sa.cap: the forward's own counters (backward_impl); sh_adam->status is not read
     return backward_impl(settings, gaussians, radii, dL_dout_color, colors2, dL_dout_color2, num_rendered,
                          geom_buffer, binning_buffer, image_buffer, 1, grads, dcolors2, dl2_channels, alloc, alloc_ctx,
                          stream, nullptr, &sa);

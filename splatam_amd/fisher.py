@@ -89,7 +89,10 @@ class FisherScorer:
         mine = [w2cs[j] for j in range(r, len(w2cs), w)]
         if batch is not None:
             for c in range(0, len(mine), batch.K):
-                h = batch.hessian_sum(mine[c:c + batch.K])
+                chunk = mine[c:c + batch.K]
+                h = batch.hessian_sum(chunk)
+                if h is None:  # a pose exceeded the graph's binning capacity: the eager path re-sizes
+                    h = sum(self.hessian(w2c) for w2c in chunk)
                 H = h.clone() if H is None else H + h
         for w2c in ([] if batch is not None else mine):
             h = self.hessian(w2c)
@@ -116,7 +119,10 @@ class FisherScorer:
         if batch is not None:
             for c in range(0, len(mine), batch.K):
                 idx = mine[c:c + batch.K]
-                local[c:c + len(idx)] = batch.scores([w2cs[j] for j in idx], self.H_train_inv)
+                sc = batch.scores([w2cs[j] for j in idx], self.H_train_inv)
+                if sc is None:  # capacity overflow in the graph: score this chunk on the eager path
+                    sc = torch.stack([(self.hessian(w2cs[j]) * self.H_train_inv).sum().double() for j in idx])
+                local[c:c + len(idx)] = sc
         for k, j in enumerate([] if batch is not None else mine):
             local[k] = (self.hessian(w2cs[j]) * self.H_train_inv).sum().double()
         if w == 1:
@@ -216,24 +222,37 @@ class BatchedFisher:
                 self.w2c[k].copy_(w)
                 self.weight[k] = 1.0
 
-    def hessian_sum(self, w2cs) -> torch.Tensor:
-        """sum over the (<= K) poses of H(w2c) [P,4] (one graph launch)."""
+    def hessian_sum(self, w2cs, check: bool = True) -> torch.Tensor | None:
+        """sum over the (<= K) poses of H(w2c) [P,4] (one graph launch).  With `check` (one host sync)
+        returns None when a pose of this launch exceeded the binning capacity (its Hessian would be
+        missing from the sum): the caller re-renders the chunk eagerly or rebuilds with more headroom."""
         if self.mode != "sum":
             raise RuntimeError("built for mode='scores'")
         self._load(w2cs)
+        if check:
+            self.status.zero_()
         self.graph.replay()
+        if check and self.overflowed(len(w2cs)):
+            return None
         return self.out
 
-    def scores(self, w2cs, H_inv) -> torch.Tensor:
-        """sum(H(w2c_k) * H_inv) for each of the (<= K) poses, float64 (one graph launch)."""
+    def scores(self, w2cs, H_inv, check: bool = True) -> torch.Tensor | None:
+        """sum(H(w2c_k) * H_inv) for each of the (<= K) poses, float64 (one graph launch); None on a
+        capacity overflow of any of them (see hessian_sum)."""
         if self.mode != "scores":
             raise RuntimeError("built for mode='sum'")
         self._load(w2cs)
         with torch.no_grad():
             self.H_inv.copy_(H_inv)
+        if check:
+            self.status.zero_()
         self.graph.replay()
+        if check and self.overflowed(len(w2cs)):
+            return None
         return self.out[:len(w2cs)].double()
 
-    def overflowed(self) -> bool:
-        st = self.status.cpu()
+    def overflowed(self, n: int | None = None) -> bool:
+        """True if a replay since the last status reset exceeded the capacity in one of the first `n`
+        slots (default: all K; padded slots render the previous poses and are not results)."""
+        st = self.status[: self.K if n is None else n].cpu()
         return bool((st[:, 0] > self.capacity).any() or (st[:, 2] > st[:, 3]).any() or (st[:, 1] != 0).any())

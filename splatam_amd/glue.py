@@ -256,13 +256,19 @@ class MapAdam:
         self.lr = [float(lrs[k]) for k in self.keys]
         self.betas, self.eps = (float(betas[0]), float(betas[1])), float(eps)
         self.step = 0
-        self.status = None  # the current iteration's static-mode status row: an overflow skips the step
+        self.status = None  # the current iteration's static-mode status row (reporting; see `guard`)
         self.capacity = 0
+        # (geom_buffer, counters offset, capacity) of the current iteration's static forward, set by
+        # rasterize_gaussians_dual(guard_sink=...): the fused steps guard on that call's own counters.
+        # The host `step` still advances when the device skips an overflowing iteration's step, so
+        # after an overflow the frame must be re-run from reset() (GraphMapper.run(check=True) raises).
+        self.guard = None
 
     def reset(self):
         for t in self.exp_avg + self.exp_avg_sq:
             t.zero_()
         self.step = 0
+        self.guard = None
 
     def struct(self):
         from ._lib import GsrMapAdam
@@ -272,8 +278,12 @@ class MapAdam:
             s.exp_avg_sq[k] = self.exp_avg_sq[k].data_ptr()
             s.lr[k] = self.lr[k]
         s.step, s.beta1, s.beta2, s.eps = self.step, self.betas[0], self.betas[1], self.eps
-        s.status = self.status.data_ptr() if self.status is not None else None
-        s.capacity = int(self.capacity)
+        if self.guard is not None:
+            geom, off, cap = self.guard
+            s.status, s.capacity = geom.data_ptr() + off, cap
+        else:
+            s.status = self.status.data_ptr() if self.status is not None else None
+            s.capacity = int(self.capacity)
         return s
 
 

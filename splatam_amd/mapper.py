@@ -109,9 +109,17 @@ class GraphMapper:
         torch.autograd.backward(loss, self.seed)
         return loss.detach()
 
-    def run(self):
-        """Enqueue one frame's mapping (one graph launch, no host sync)."""
+    def run(self, check: bool = False):
+        """Enqueue one frame's mapping (one graph launch, no host sync).  An iteration whose forward
+        overflowed skips its own Adam step (the steps guard on that forward's counters), but the bias
+        corrections of the later steps still count it; with `check` the replay ends with one host sync
+        and raises on any overflow, so the caller can rebuild with more headroom and re-map the frame."""
+        if check:
+            self.reset_status()
         self.graph.replay()
+        if check and self.overflowed():
+            raise RuntimeError(f"binning capacity {self.capacity} exceeded during mapping: rebuild the mapper "
+                               "with more headroom and re-run the frame")
 
     def reset_status(self):
         self.status.zero_()

@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 
 from . import _C
+from ._lib import lib
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -79,7 +80,7 @@ class _RasterizeGaussians(torch.autograd.Function):
 
 def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations,
                              cov3Ds_precomp, raster_settings, capacity=0, status=None, grad2_channels=3,
-                             means2D_grad_sum=False, sh_adam=None):
+                             means2D_grad_sum=False, sh_adam=None, guard_sink=None):
     """Two GaussianRasterizer calls on identical geometry fused into one
     rasterization: SplaTAM renders RGB and the [z, 1, z^2]
     depth/silhouette image from the same means / scales / rotations / opacities
@@ -105,18 +106,23 @@ def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opac
                                          empty if scales is None else scales,
                                          empty if rotations is None else rotations,
                                          empty if cov3Ds_precomp is None else cov3Ds_precomp, raster_settings,
-                                         capacity, status, grad2_channels, bool(means2D_grad_sum), sh_adam)
+                                         capacity, status, grad2_channels, bool(means2D_grad_sum), sh_adam,
+                                         guard_sink)
 
 
 class _RasterizeGaussiansDual(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings, capacity, status, grad2_channels, means2D_grad_sum, sh_adam=None):
+                raster_settings, capacity, status, grad2_channels, means2D_grad_sum, sh_adam=None, guard_sink=None):
         s = raster_settings
         num_rendered, color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth = _C.rasterize_gaussians_dual(
             s.bg, means3D, colors_precomp, colors2, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
             s.campos, s.prefiltered, capacity=capacity, status=status)
+        if guard_sink is not None and capacity > 0:
+            # the fused optimizer steps of this iteration guard on this forward's own counters
+            # (the geometry buffer stays referenced until the next iteration replaces it)
+            guard_sink.guard = (geomBuffer, int(lib.gsr_geom_counters_offset(means3D.shape[0])), int(num_rendered))
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
         ctx.grad2_channels = grad2_channels
@@ -150,7 +156,7 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
             dl2_channels=ctx.grad2_channels if grad_color2 is not None else 3, sh_adam=sa)
         if not n[0]:
             g_m3 = None
-        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None, None, None, None, None, None
+        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None, None, None, None, None, None, None
 
 
 class GaussianRasterizer(nn.Module):

@@ -341,7 +341,7 @@ def _get_loss_mapping_fused(params, curr_data, iter_time_idx, cfg: MappingConfig
     sh_adam = adam if (adam is not None and sh is not None and _SH_ADAM_FUSED) else None
     im, depth_sil, radius, _ = rasterize_gaussians_dual(means, means2D, sh, colors, dcol, opac, scales, rots, None,
                                                         curr_data["cam"], capacity, status, grad2_channels=1,
-                                                        sh_adam=sh_adam)
+                                                        sh_adam=sh_adam, guard_sink=adam)
     loss = mapping_loss(im, depth_sil, curr_data["im"], curr_data["depth"], cfg.w_im, cfg.w_depth)
     return loss, radius, means2D
 

@@ -59,7 +59,8 @@ def probe_num_rendered(params, curr_data, time_idx) -> tuple[int, int]:
 class GraphTracker:
     def __init__(self, params: dict, curr_data: dict, time_idx: int, iters_per_graph: int = 20,
                  cfg: TrackingConfig = TrackingConfig(), lrs=(0.0004, 0.002), headroom: float = 1.5,
-                 warmup_iters: int = 3, min_extra: int = 65536, timing: bool = False, fuse_pose: bool = False):
+                 warmup_iters: int = 3, min_extra: int = 65536, timing: bool = False, fuse_pose: bool = False,
+                 prime: bool = False):
         if not fused_eligible(params, curr_data, cfg):
             raise RuntimeError("GraphTracker needs the fused tracking configuration (only the pose requires grad)")
         self.params, self.curr, self.t, self.cfg = params, curr_data, time_idx, cfg
@@ -103,6 +104,17 @@ class GraphTracker:
         with torch.cuda.graph(self.graph, stream=side):  # capture on the warm-up stream (autograd nodes live there)
             for k in range(self.iters):
                 self.loss = self._iteration(k)
+        if prime:  # one replay (graph upload, first-launch costs), undone like the warm-up iterations
+            self.graph.replay()
+            with torch.no_grad():
+                rots[..., time_idx] = q0
+                trans[..., time_idx] = t0
+            self.adam.reset()
+            self.status.zero_()
+            torch.cuda.synchronize(dev)
+            if timing:
+                from . import profiling
+                profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
 
     def _iteration(self, k: int):
         self.adam.status = self.status[k]  # this iteration's forward guards its Adam step
@@ -134,14 +146,23 @@ class GraphTracker:
             self.params["cam_unnorm_rots"][0, :, self.t] = self.adam.best[1:5]
             self.params["cam_trans"][0, :, self.t] = self.adam.best[5:8]
 
-    def track_frame(self, num_iters: int):
-        """One frame's tracking: begin_frame, num_iters iterations (a multiple of iters_per_graph), end_frame."""
+    def track_frame(self, num_iters: int, check: bool = False):
+        """One frame's tracking: begin_frame, num_iters iterations (a multiple of iters_per_graph), end_frame.
+
+        An iteration whose forward overflowed skips its own pose step (the fused steps guard on that
+        forward's counters, not on the sticky status rows), so later iterations are unaffected; with
+        `check` the frame ends with one host sync and raises if any iteration of it overflowed."""
         if num_iters % self.iters:
             raise ValueError(f"num_iters {num_iters} is not a multiple of iters_per_graph {self.iters}")
+        if check:
+            self.reset_status()
         self.begin_frame()
         for _ in range(num_iters // self.iters):
             self.run()
         self.end_frame()
+        if check and self.overflowed():
+            raise RuntimeError(f"binning capacity {self.capacity} exceeded while tracking frame {self.t}: "
+                               "rebuild the tracker with more headroom and re-run the frame")
 
     def reset_status(self):
         self.status.zero_()

@@ -30,6 +30,14 @@ from splatam_amd.scenes import config_scene, make_scene
 
 pytestmark = pytest.mark.gpu
 
+# Upper bounds on the oracle's near-threshold sets (fractions; measured on these seeded scenes:
+# Gaussians 0.40 / 1.03 / 2.38 / 8.12 / 1.61 % of the visible ones, pixels <= 0.124 %).  A Gaussian is
+# excluded from the per-element gradient check when any pixel it contributes to has a decision near its
+# threshold (oracle/gsr_oracle.c ALPHA_BAND / T_BAND, forward.cu:311-381): one such pixel excludes every
+# Gaussian composited in front of its terminating pair, hence the larger share at config 4 (~80 per pixel).
+UNSTABLE_MAX = {1: 0.01, 2: 0.015, 3: 0.03, 4: 0.10, "habitat": 0.02}
+UNSTABLE_PIX_MAX = 0.002
+
 
 def _scene(cfg):
     if cfg == "habitat":
@@ -58,6 +66,10 @@ def test_baseline_config_parity(cuda, cfg):
     np.testing.assert_array_equal(binning["ranges"][cnt > 0], fr.ranges[cnt > 0])  # empty tiles: any start
     np.testing.assert_array_equal(binning["point_list"], fr.point_list)
     settled = ~fr.unstable_pix
+    # pixels with an alpha / T decision near its threshold: reported and bounded (the oracle's count on
+    # these seeded scenes is deterministic; the bound guards against a widened exclusion)
+    n_upix = int(fr.unstable_pix.astype(bool).sum())
+    assert n_upix <= UNSTABLE_PIX_MAX * c.W * c.H, (cfg, n_upix, c.W * c.H)
     nc = binning["n_contrib"].reshape(c.H, c.W)
     assert np.array_equal(nc[settled], fr.n_contrib[settled])
 
@@ -74,7 +86,21 @@ def test_baseline_config_parity(cuda, cfg):
     errs = harness.compare_grads(gpu["grads"], ref)
     assert not {k: v for k, v in errs.items() if v > 1e-4}, errs
     stable = ~(fr.unstable | fr64.unstable)
+    visible = int((fr.radii > 0).sum())
+    n_unstable = int((~stable).sum())
     g, o = harness.check_grad_accuracy(gpu["grads"], ref, ref64, stable)
-    print(cfg, fwd, "unstable", int((~stable).sum()), {k: f"{v:.2e}" for k, v in errs.items()})
+    print(f"config {cfg}: {n_unstable} of {visible} visible Gaussians excluded from the per-element check "
+          f"({n_unstable / max(visible, 1):.3%}), {n_upix} near-threshold pixels; forward {fwd}; "
+          f"rel L2 vs f32 {({k: f'{v:.2e}' for k, v in errs.items()})}")
     for k in g:
         print(f"  {k}: gpu {g[k]}  oracle_f32 {o[k]}")
+    assert n_unstable <= UNSTABLE_MAX[cfg] * visible, (cfg, n_unstable, visible)
+    # the excluded Gaussians are checked too, against the float32 oracle's own error on the same subset:
+    # a float32 rasterizer may flip the near-threshold pairs, but no worse than the reference arithmetic
+    # (measured r3a: the product's subset errors equal the float32 oracle's to 1-7 %, all configs)
+    us = harness.unstable_grad_stats(gpu["grads"], ref, ref64, ~stable)
+    for k, d in us.items():
+        print(f"  unstable {k}: {d}")
+    worse = {k: d for k, d in us.items()
+             if d["gpu_rel_l2"] > max(1e-4, 1.5 * d["f32_rel_l2"]) or d["gpu_q99"] > max(1e-3, 1.5 * d["f32_q99"])}
+    assert not worse, worse
