@@ -237,6 +237,8 @@ def main():
     mapping = None
     if args.mapping == "on" or (args.mapping == "auto" and world == 1):
         mapping = mapping_leg(args, dev)
+        if args.dropin == "on":
+            mapping["dropin"] = dropin_mapping_leg(args, dev)
 
     # ---- CPU baseline: the float32 C oracle on one frame (rank 0, N=1) ------
     cpu = None
@@ -407,6 +409,67 @@ def dropin_leg(args, scene, dev, iters_per_frame: int = 40):
                                     "to ms_per_step is the caller's torch glue"}}
 
 
+def mapping_keyframes(params, cam, K, rank, dev):
+    """K keyframe targets (cam / im / depth / w2c / id): the map with perturbed colours rendered at each
+    keyframe's pose (the synthetic stand-in for the dataset frames the reference maps against)."""
+    from splatam_amd.rasterizer import GaussianRasterizer
+    from splatam_amd.slam import _rendervar_colors, color_key, transform_to_frame, \
+        transformed_params2depthplussilhouette, transformed_params2rendervar
+    key = color_key(params)
+    w2c = torch.eye(4, device=dev)
+    g = torch.Generator().manual_seed(1234)
+    kfs = []
+    with torch.no_grad():
+        truth = dict(params)
+        truth[key] = params[key] * 0.9 + 0.05 * torch.rand(params[key].shape, generator=g).to(dev)
+        for j in range(K):
+            t = rank * K + j
+            tg = transform_to_frame(truth, t, False, False)
+            im, _, _ = GaussianRasterizer(cam)(**_rendervar_colors(truth, transformed_params2rendervar(truth, tg)))
+            ds, _, _ = GaussianRasterizer(cam)(**transformed_params2depthplussilhouette(truth, w2c, tg))
+            kfs.append({"cam": cam, "w2c": w2c, "im": im.clamp(0, 1), "depth": ds[0:1].clone(), "id": t})
+    return kfs
+
+
+def dropin_mapping_leg(args, dev, iters: int = 20):
+    """The unchanged mapping loop (scripts/splatam.py:841-905) at config 4: every parameter an
+    nn.Parameter, a fresh torch.optim.Adam per frame over every group (eps 1e-15), per iteration a random
+    keyframe, the literal get_loss(mapping=True) with two diff_gaussian_rasterization.GaussianRasterizer
+    calls (SH colours, [z,1,z^2]), L1 + SSIM (torch conv2d) + masked depth L1, loss.backward(), step --
+    eager, one Python iteration at a time, beside the HIP-graph mapping number."""
+    import numpy as np
+    import diff_gaussian_rasterization as dgr
+    from splatam_amd.scenes import config_scene
+    from splatam_amd.slam import MappingConfig, as_parameters, camera_settings, init_mapping_params, \
+        map_frame_literal, tracking_variables
+    scene = config_scene(4)
+    P, W, H = scene.P, scene.cam.W, scene.cam.H
+    K = max(1, args.keyframes)
+    base = init_mapping_params(scene, num_frames=K, device=dev)
+    cam = camera_settings(scene.cam, dev, sh_degree=scene.sh_degree)
+    kfs = mapping_keyframes(base, cam, K, 0, dev)
+    params = as_parameters(base)
+    del base
+    variables = tracking_variables(P, dev)
+    cfg = MappingConfig()
+    rng = np.random.RandomState(0)
+    map_frame_literal(params, variables, kfs, 3, cfg, renderer=dgr.GaussianRasterizer, rng=rng)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    map_frame_literal(params, variables, kfs, iters, cfg, renderer=dgr.GaussianRasterizer, rng=rng)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del params, variables, kfs
+    torch.cuda.empty_cache()
+    return {"value": round(iters / dt, 3), "unit": "iterations/s", "ms_per_step": round(1000 * dt / iters, 4),
+            "iterations": iters,
+            "path": f"unchanged scripts/splatam.py mapping loop body at config 4 ({P} Gaussians, SH degree "
+                    f"{scene.sh_degree}, {W}x{H}, {K} keyframes): literal get_loss(mapping=True) with 2x "
+                    "diff_gaussian_rasterization.GaussianRasterizer, torch L1 + calc_ssim + masked depth L1, "
+                    "loss.backward(), torch.optim.Adam over every group (fresh per frame), eager; pruning and "
+                    "densification off"}
+
+
 def fisher_leg(args, scene, dev, launches: int = 6):
     """Fisher / EIG view scoring (scripts/ros_handler.py:807-902) on the bench map:
     the visited-pose Hessian sum H = sum_k [dL/dmeans_cam, dL/dopacity] of backward_power=2 renders seeded
@@ -498,11 +561,8 @@ def run_mapping(args, world, rank, dev):
     from splatam_amd import dist as sd
     from splatam_amd import profiling
     from splatam_amd.mapper import GraphMapper
-    from splatam_amd.rasterizer import GaussianRasterizer
     from splatam_amd.scenes import config_scene
-    from splatam_amd.slam import MappingConfig, _rendervar_colors, camera_settings, color_key, \
-        init_mapping_params, transform_to_frame, transformed_params2depthplussilhouette, \
-        transformed_params2rendervar
+    from splatam_amd.slam import MappingConfig, camera_settings, color_key, init_mapping_params
 
     scene = config_scene(args.config)
     P, W, H = scene.P, scene.cam.W, scene.cam.H
@@ -512,19 +572,7 @@ def run_mapping(args, world, rank, dev):
     cam = camera_settings(scene.cam, dev, sh_degree=scene.sh_degree)
     w2c = torch.eye(4, device=dev)
     key = color_key(params)
-    # keyframe targets: the map with perturbed colours rendered at each keyframe's pose
-    g = torch.Generator().manual_seed(1234)
-    kfs = []
-    with torch.no_grad():
-        truth = dict(params)
-        truth[key] = params[key] * 0.9 + 0.05 * torch.rand(params[key].shape, generator=g).to(dev)
-        for j in range(K):
-            t = rank * K + j
-            tg = transform_to_frame(truth, t, False, False)
-            im, _, _ = GaussianRasterizer(cam)(**_rendervar_colors(truth, transformed_params2rendervar(truth, tg)))
-            ds, _, _ = GaussianRasterizer(cam)(**transformed_params2depthplussilhouette(truth, w2c, tg))
-            kfs.append({"cam": cam, "w2c": w2c, "im": im.clamp(0, 1), "depth": ds[0:1].clone(), "id": t})
-        del truth
+    kfs = mapping_keyframes(params, cam, K, rank, dev)  # keyframe targets: the map with perturbed colours
     for k in ("means3D", "unnorm_rotations", "logit_opacities", "log_scales", key):
         params[k].requires_grad_(True)
     steps = max(1, args.steps)

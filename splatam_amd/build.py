@@ -17,6 +17,7 @@ CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 OBJDIR = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libgsr.so")
+DIAG = os.path.join(HERE, "_diag")  # experiment / diagnostics libraries that travel to the GPU box
 SOURCES = ["gsr_forward.hip", "gsr_backward.hip", "gsr_backward_power.hip", "gsr_capi.hip", "gsr_glue.hip",
            "gsr_mapping.hip", "gsr_sh.hip"]
 ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
@@ -97,7 +98,11 @@ def build_variant(tag: str, defines=()) -> str:
                            capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    return lib
+    # the _build_<tag> trees stay on this machine (.gpurunignore); the experiment's library travels to the
+    # GPU box from splatam_amd/_diag/ (delete that directory when the experiment is done)
+    os.makedirs(DIAG, exist_ok=True)
+    shutil.copy2(lib, os.path.join(DIAG, f"libgsr_{tag}.so"))
+    return os.path.join(DIAG, f"libgsr_{tag}.so")
 
 
 if __name__ == "__main__":

@@ -36,6 +36,32 @@ GSR_WGTIME_TABLE
 //  batches x waves]
 static __device__ unsigned long long g_stepstat[8];
 #endif
+#ifndef GSR_PHASE
+#define GSR_PHASE 0  // diagnostics build only (tools/phase_bwd.py): per-wave s_memtime cycles per render_bwd phase
+#endif
+#if GSR_PHASE
+// per-wave shader-clock cycles summed over all waves: [0] prologue (pixel inputs, row maxima, zero records
+// behind the last contributors, first staging loads), [1] batch staging stores + barrier, [2] row / slot list
+// build, [3] row walk, [4] barrier after the walk, [5] entry totals + record stores, [6] barrier after the
+// totals, [7] batches x waves
+static __device__ unsigned long long g_phase[8];
+#define PHASE_T0() unsigned long long ph_t = __builtin_amdgcn_s_memtime(); unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define PHASE_MARK(k)                                                           \
+    do {                                                                        \
+        const unsigned long long ph_n = __builtin_amdgcn_s_memtime();           \
+        ph_acc[k] += ph_n - ph_t;                                               \
+        ph_t = ph_n;                                                            \
+    } while (0)
+#define PHASE_FLUSH()                                                           \
+    do {                                                                        \
+        if ((threadIdx.x & 63) == 0)                                            \
+            for (int k_ = 0; k_ < 8; k_++) atomicAdd(&g_phase[k_], ph_acc[k_]); \
+    } while (0)
+#else
+#define PHASE_T0() do {} while (0)
+#define PHASE_MARK(k) do {} while (0)
+#define PHASE_FLUSH() do {} while (0)
+#endif
 
 // Per-pair geometric terms (hx, hy, hx dx, hx dy, hy dy[, G dL/dalpha]) with
 // h = G * dL/dG = (o * G) * dL/dalpha.
@@ -206,6 +232,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         kclock_end(clk);
         return;
     }
+    PHASE_T0();
     static_assert(Q2 == 1 || Q2 == 3, "Q2 is 1 or 3 channels");
     constexpr int NV = bwd_nv<DUAL, OPAC, COL1, COL2, Q2>();
     constexpr int O_OP = 5, O_C1 = 5 + (OPAC ? 1 : 0), O_C2 = O_C1 + (COL1 ? 3 : 0);
@@ -321,6 +348,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     fetch_entry((int)bmax - BB);
     const uint32_t mean4 = sched_mean4(cam, guard.counters);
     int hi_pf = (int)bmax;  // the batch start the staged registers hold
+    PHASE_MARK(0);
     for (int hi = (int)bmax; hi > 0;) {
         prio_by_remaining(hi, mean4);
         if (hi != hi_pf) {  // the previous batch was cut by its slot budget: re-fetch (rare)
@@ -341,6 +369,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             s_mask[ts_] = (uint16_t)pm;  // the instance's exact 4x4-block mask (sorted list entry)
         }
         __syncthreads();
+        PHASE_MARK(1);
         fetch_rec(hi - BB);        // records of the next batch (list entries loaded a batch ago)
         fetch_entry(hi - 2 * BB);  // list entries of the batch after it
         hi_pf = hi - BB;
@@ -349,6 +378,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         const SlotLists sl = build_row_slot_lists(s_mask, s_base, cmax, BS, w, jmin, s_list + 4 * w * LS, LS,
                                                   (uint32_t)BB | ((uint32_t)BS << 16));
         const int n = sl.len, cnt = sl.cnt;
+        PHASE_MARK(2);
         const int jlo = hi - (int)last;  // pos = hi-1-j < last  <=>  j >= jlo
 #if GSR_STEPSTAT
         st_batches++;
@@ -471,7 +501,9 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 }
             }
         }
+        PHASE_MARK(3);
         __syncthreads();
+        PHASE_MARK(4);
         // Entry totals: TPE threads per entry, thread q of an entry owns values m = q, q + TPE, ...
         // and adds the entry's consecutive block slots in ascending block order (deterministic);
         // the TPE threads store adjacent floats of the packed record.
@@ -498,9 +530,15 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             for (int i = 0; i < NQ; i++)
                 if (q + TPE * i < RS) dst[q + TPE * i] = c[i];
         }
+        PHASE_MARK(5);
         __syncthreads();
+        PHASE_MARK(6);
+#if GSR_PHASE
+        ph_acc[7]++;
+#endif
         hi -= cnt;
     }
+    PHASE_FLUSH();
 #if GSR_ABLATE == 1
     if (ablate_sink == 1.2345f) inst[0] = ablate_sink;  // keeps the per-pair values alive (timing ablation)
 #endif
@@ -864,6 +902,14 @@ extern "C" int gsr_diag_stepstat_bwd(unsigned long long* host) {  // copies and 
         return -1;
     const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_stepstat), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+#endif
+#if GSR_PHASE
+extern "C" int gsr_diag_phase_bwd(unsigned long long* host) {  // copies and clears the phase cycles
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), sizeof(g_phase), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
 }
 #endif
 #if GSR_WGTIME

@@ -347,7 +347,7 @@ def _get_loss_mapping_fused(params, curr_data, iter_time_idx, cfg: MappingConfig
 
 
 def get_loss_mapping(params, curr_data, iter_time_idx, cfg: MappingConfig = MappingConfig(), fused=True,
-                     adam=None, loss_dtype=None):
+                     adam=None, loss_dtype=None, variables=None, renderer=None):
     """scripts/splatam.py:220-353 with mapping=True, do_ba=False: two renders (RGB or SH colours, and
     [z,1,z^2]), masked mean depth L1 and 0.8 L1 + 0.2 (1 - SSIM) on the image.
 
@@ -355,7 +355,9 @@ def get_loss_mapping(params, curr_data, iter_time_idx, cfg: MappingConfig = Mapp
     gsr_track_transform_fwd + gsr_map_transform_bwd, both renders share one rasterization, and the
     loss is the fused SSIM/L1 kernel pair; `adam` (glue.MapAdam) then applies the mapping optimizer's
     step inside the transform backward.  fused=False is the literal statement of the reference
-    (loss_dtype=torch.float64 evaluates its loss terms in double: a tighter test reference)."""
+    (loss_dtype=torch.float64 evaluates its loss terms in double: a tighter test reference; renderer: the
+    GaussianRasterizer class the caller imports; variables: the densification statistics, updated like
+    splatam.py:257,349-351)."""
     if fused and fused_mapping_eligible(params, curr_data, cfg):
         return _get_loss_mapping_fused(params, curr_data, iter_time_idx, cfg, adam)
     if adam is not None:
@@ -364,8 +366,9 @@ def get_loss_mapping(params, curr_data, iter_time_idx, cfg: MappingConfig = Mapp
     rendervar = _rendervar_colors(params, transformed_params2rendervar(params, tg))
     depth_sil_rendervar = transformed_params2depthplussilhouette(params, curr_data["w2c"], tg, fast=False)
     rendervar["means2D"].retain_grad()
-    im, radius, _ = GaussianRasterizer(raster_settings=curr_data["cam"])(**rendervar)
-    depth_sil, _, _ = GaussianRasterizer(raster_settings=curr_data["cam"])(**depth_sil_rendervar)
+    Renderer = GaussianRasterizer if renderer is None else renderer
+    im, radius, _ = Renderer(raster_settings=curr_data["cam"])(**rendervar)
+    depth_sil, _, _ = Renderer(raster_settings=curr_data["cam"])(**depth_sil_rendervar)
     gt_im, gt_depth = curr_data["im"], curr_data["depth"]
     if loss_dtype is not None:
         im, depth_sil, gt_im, gt_depth = (t.to(loss_dtype) for t in (im, depth_sil, gt_im, gt_depth))
@@ -377,7 +380,36 @@ def get_loss_mapping(params, curr_data, iter_time_idx, cfg: MappingConfig = Mapp
     loss_depth = torch.abs(gt_depth - depth)[mask].mean()
     loss_im = 0.8 * l1_loss_v1(im, gt_im) + 0.2 * (1.0 - calc_ssim(im, gt_im))
     loss = cfg.w_im * loss_im + cfg.w_depth * loss_depth
+    if variables is not None:  # splatam.py:257,349-351
+        variables["means2D"] = rendervar["means2D"]
+        seen = radius > 0
+        variables["max_2D_radius"][seen] = torch.max(radius[seen], variables["max_2D_radius"][seen])
+        variables["seen"] = seen
     return loss, radius, rendervar["means2D"]
+
+
+def map_frame_literal(params, variables, keyframes, num_iters, cfg: MappingConfig = MappingConfig(), optimizer=None,
+                      renderer=None, rng=None, losses_out=None):
+    """The unchanged mapping loop body of scripts/splatam.py:841-905 for one frame (prune_gaussians and
+    densification off, no progress reports): a fresh torch Adam over every parameter group
+    (initialize_optimizer, :842), then per iteration a keyframe drawn with np.random.randint (:851),
+    get_loss(mapping=True) through two GaussianRasterizer calls, loss.backward(), optimizer.step(),
+    zero_grad.  keyframes: dicts with cam / im / depth / w2c / id.  Returns the optimizer."""
+    import numpy as np
+    rng = np.random if rng is None else rng
+    if optimizer is None:
+        optimizer = mapping_optimizer(params, cfg, fused=False)
+    for _ in range(num_iters):
+        kf = keyframes[int(rng.randint(0, len(keyframes)))]
+        loss, _radius, _m2d = get_loss_mapping(params, kf, kf["id"], cfg, fused=False, variables=variables,
+                                               renderer=renderer)
+        loss.backward()
+        with torch.no_grad():
+            optimizer.step()
+            optimizer.zero_grad(set_to_none=True)
+        if losses_out is not None:
+            losses_out.append(loss.detach())
+    return optimizer
 
 
 def init_mapping_params(scene: Scene, num_frames: int, device, pose_noise=(0.5, 0.01), seed=0):

@@ -12,6 +12,6 @@ run_one() {  # name lib
   fi
 }
 BASE=splatam_amd/libgsr.so
-VAR=splatam_amd/_build_$TAG/libgsr_$TAG.so
+VAR=splatam_amd/_diag/libgsr_$TAG.so
 run_one base $BASE && run_one var $VAR && run_one base2 $BASE || exit 1
 grep -o '"value": [0-9.]*\|"avg_us": [0-9.]*' "$OUT"/*.log

@@ -8,7 +8,7 @@ mkdir -p "$ROOT/$OUT"
 cd /tmp && export TMPDIR=/tmp
 for v in base var base2; do
   L=$ROOT/splatam_amd/libgsr.so
-  [ $v = var ] && L=$ROOT/splatam_amd/_build_$TAG/libgsr_$TAG.so
+  [ $v = var ] && L=$ROOT/splatam_amd/_diag/libgsr_$TAG.so
   GSR_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/$v" -o run --output-format csv \
       -- python "$ROOT/bench.py" --steps 40 --warmup 20 --cpu-baseline off --dropin off --fisher off --mapping off "$@" \
       > "$ROOT/$OUT/$v.log" 2>&1 || { echo "$v failed"; tail -20 "$ROOT/$OUT/$v.log"; exit 1; }
