@@ -340,6 +340,325 @@ gauss_bwd_power_kernel(GaussIn g, GeomPtrs geo, const int* __restrict__ radii, c
     }
 }
 
+// ---------------------------------------------- Fisher-selective backward --
+// The fork's Fisher / EIG scoring reads only transformed_pts.grad and opacities.grad of a
+// backward_power render (scripts/ros_handler.py:884-889).  Without SH (colours precomputed) a
+// pair's dL/dmeans3D is linear in its 2D terms u = h (dx, dy, dx^2, dx dy, dy^2), h = G dL/dG:
+// backward.cu:1020-1038 forms dmean2D = -(Q h d) ddel and dconic = -1/2 h d d^T, and the
+// per-Gaussian chain (computeCov2D / projection backward) maps those linearly to dmean3D.  With
+// the conic and the NDC factor folded in, dmean3D_r = h * (M_r . (dx, dy, dx^2, dx dy, dy^2)) for a
+// 3x5 matrix M per Gaussian (gauss_mpack_kernel), so a pair forms 4 values (3 mean components and
+// G dL/dalpha), each raised to `power`, instead of the full path's 22 + 3 nsh.  The tile walk is
+// render_bwd_kernel's: per-row lists of the 4x4-pixel blocks an entry's ellipse reaches (exact
+// masks from the forward), compact per-(entry, block) slots, the transposed in-row reduction, one
+// 16-B record per (tile, Gaussian) instance at its unsorted slot.
+constexpr int MPACK_F4 = 4;  // M (15 floats, row-major) + 1 pad
+
+__global__ void __launch_bounds__(256)
+gauss_mpack_kernel(Camera cam, GaussIn g, const int* __restrict__ radii, float4* __restrict__ mp) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.P || radii[i] <= 0) return;
+    const GaussGeom gg = load_geom(g, i);
+    float J[3][5];
+#pragma unroll 1
+    for (int kk = 0; kk < 5; kk++) {  // column kk <- unit dmean2D.x/.y, dconic.A/.B/.C
+        float g2[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        g2[kk] = 1.f;
+        float dmean[3], dcov[6], dscale[3], drot[4], dsh[48];
+        gauss_chain(cam, g, gg, i, g2, 0u, dmean, dcov, dscale, drot, dsh, 0);
+#pragma unroll
+        for (int r = 0; r < 3; r++) J[r][kk] = dmean[r];
+    }
+    float ca, cb, cc;
+    gaussian_conic(cam, g, gg, i, ca, cb, cc);
+    const float ddelx = (float)(0.5 * cam.W), ddely = (float)(0.5 * cam.H);  // backward.cu:935-936
+    float M[16];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        M[5 * r] = -(J[r][0] * ca * ddelx + J[r][1] * cb * ddely);
+        M[5 * r + 1] = -(J[r][0] * cb * ddelx + J[r][1] * cc * ddely);
+        M[5 * r + 2] = -0.5f * J[r][2];
+        M[5 * r + 3] = -0.5f * J[r][3];
+        M[5 * r + 4] = -0.5f * J[r][4];
+    }
+    M[15] = 0.f;
+#pragma unroll
+    for (int q = 0; q < MPACK_F4; q++) mp[(size_t)MPACK_F4 * i + q] = make_float4(M[4 * q], M[4 * q + 1], M[4 * q + 2], M[4 * q + 3]);
+}
+
+template <bool POW2>
+__device__ __forceinline__ float pow_sel(float x, float p) { return POW2 ? x * x : powf(x, p); }
+
+template <bool POW2>
+__global__ void __launch_bounds__(TILE_PIX, 5)
+render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ ranges,
+                         const PointEntry* __restrict__ point_list, const float4* __restrict__ rr,
+                         const uint32_t* __restrict__ blocksums, const float4* __restrict__ mp,
+                         const float* __restrict__ final_T, const uint32_t* __restrict__ n_contrib,
+                         const float* __restrict__ dL_dpix, float* __restrict__ inst, BwdGuard guard) {
+    if (guard.overflow()) return;  // invalid forward state (static-mode overflow): touch nothing
+    constexpr int NV = 4, BB = 128, BS = 4 * BB, LS = BB + 4, SL = BB + 1;
+    __shared__ float4 s_a[SL];
+    __shared__ float4 s_b[SL];
+    __shared__ float4 s_c[SL];
+    __shared__ float4 s_m[MPACK_F4 * SL];
+    __shared__ uint32_t s_u[BB];
+    __shared__ uint16_t s_mask[BB];
+    __shared__ uint16_t s_base[BB];
+    __shared__ float4 s_acc4[BS + 1];
+    __shared__ uint32_t s_rmax[16];
+    __shared__ __attribute__((aligned(16))) uint32_t s_list[16 * LS];
+    float* s_acc = reinterpret_cast<float*>(s_acc4);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, row = (tid >> 4) & 3;
+    const int tile = sched_tile(cam), tx = tile % cam.gx, ty = tile / cam.gx;
+    const int px = tx * TILE_X + tile_px(tid);
+    const int py = ty * TILE_Y + tile_py(tid);
+    const bool inside = px < cam.W && py < cam.H;
+    const int pid = py * cam.W + px;
+    const int HW = cam.W * cam.H;
+    const uint2 range = ranges[tile];
+    const float T_final = inside ? final_T[pid] : 0.f;
+    const uint32_t last = inside ? n_contrib[pid] : 0u;
+    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
+    if (inside) {
+        dp0 = dL_dpix[pid];
+        dp1 = dL_dpix[HW + pid];
+        dp2 = dL_dpix[2 * HW + pid];
+    }
+    uint32_t rmax = last;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, o));
+    if ((lane & 15) == 0) s_rmax[4 * w + row] = rmax;
+    __syncthreads();
+    uint32_t bmax = 0;
+#pragma unroll
+    for (int b = 0; b < 16; b++) bmax = max(bmax, s_rmax[b]);
+    const int rm[4] = {(int)s_rmax[4 * w], (int)s_rmax[4 * w + 1], (int)s_rmax[4 * w + 2], (int)s_rmax[4 * w + 3]};
+    for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {  // behind every last contributor
+        const uint32_t gk = pe_id(point_list[k]);
+        const RenderRec r = load_rr(rr, gk);
+        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), tx, ty);
+        reinterpret_cast<float4*>(inst)[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // background term of dL/dalpha (backward.cu:1014): -T_final / (1 - alpha) * (bg . dL/dpix)
+    const float Tbg = -T_final * (cam.bg[0] * dp0 + cam.bg[1] * dp1 + cam.bg[2] * dp2);
+    const v2f pix = v2f{(float)px, (float)py};
+    const v2f dp01 = v2f{dp0, dp1};
+    float T = T_final, A = 0.f;
+    const int my_e = row_entry(lane);
+    for (int q = tid; q < BS + 1; q += TILE_PIX) s_acc4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const uint32_t* my_list = s_list + (4 * w + row) * LS;
+    if (tid == 0) {
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        s_a[BB] = z;
+        s_b[BB] = z;
+        s_c[BB] = z;
+#pragma unroll
+        for (int q = 0; q < MPACK_F4; q++) s_m[MPACK_F4 * BB + q] = z;
+    }
+    // staging pipelined two batches deep (render_bwd_kernel): records + M of the next batch in
+    // registers, sorted list entries of the batch after it
+    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pm4[MPACK_F4] = {pa, pa, pa, pa};
+    uint32_t pbs = 0, pmask = 0, prh = 0, pgi = 0;
+    PointEntry pn = 0;
+    auto fetch_entry = [&](int hi_) {
+        if (tid < min(BB, hi_)) pn = point_list[range.x + (uint32_t)(hi_ - 1 - tid)];
+    };
+    auto fetch_rec = [&](int hi_) {
+        if (tid < min(BB, hi_)) {
+            const uint32_t gi = pe_id(pn);
+            pmask = pe_mask(pn);
+            const RenderRec r = load_rr(rr, gi);
+            pbs = blocksums[gi / PRE_BLOCK];
+            pa = r.q0; pb = r.q1; pc = r.q2;
+            prh = __float_as_uint(r.q3.w);
+            pgi = gi;
+        }
+    };
+    // the M rows are loaded after the walk (in flight during the entry totals), so they occupy no
+    // registers while the batch is rasterised (16 VGPRs: the kernel spilled at 96)
+    auto fetch_m = [&](int hi_) {
+        if (tid < min(BB, hi_)) {
+#pragma unroll
+            for (int q = 0; q < MPACK_F4; q++) pm4[q] = mp[(size_t)MPACK_F4 * pgi + q];
+        }
+    };
+    fetch_entry((int)bmax);
+    fetch_rec((int)bmax);
+    fetch_m((int)bmax);
+    fetch_entry((int)bmax - BB);
+    const uint32_t mean4 = sched_mean4(cam, guard.counters);
+    int hi_pf = (int)bmax;
+    for (int hi = (int)bmax; hi > 0;) {
+        prio_by_remaining(hi, mean4);
+        if (hi != hi_pf) {  // the previous batch was cut by its slot budget: re-fetch (rare)
+            fetch_entry(hi);
+            fetch_rec(hi);
+            fetch_m(hi);
+            fetch_entry(hi - BB);
+        }
+        const int cmax = min(BB, hi);
+        int ts_ = tid;
+        asm volatile("" : "+v"(ts_));
+        if (ts_ < cmax) {
+            s_u[ts_] = instance_slot(make_uint2(__float_as_uint(pc.w), prh), pbs + __float_as_uint(pb.w), tx, ty);
+            s_a[ts_] = pa;
+            s_b[ts_] = pb;
+            s_c[ts_] = pc;
+#pragma unroll
+            for (int q = 0; q < MPACK_F4; q++) s_m[MPACK_F4 * ts_ + q] = pm4[q];
+            s_mask[ts_] = (uint16_t)pmask;
+        }
+        __syncthreads();
+        fetch_rec(hi - BB);
+        fetch_entry(hi - 2 * BB);
+        hi_pf = hi - BB;
+        const int jmin[4] = {hi - rm[0], hi - rm[1], hi - rm[2], hi - rm[3]};
+        const SlotLists sl = build_row_slot_lists(s_mask, s_base, cmax, BS, w, jmin, s_list + 4 * w * LS, LS,
+                                                  (uint32_t)BB | ((uint32_t)BS << 16));
+        const int n = sl.len, cnt = sl.cnt;
+        const int jlo = hi - (int)last;  // pos = hi-1-j < last  <=>  j >= jlo
+        for (int i = 0; i < n; i += 4) {
+            const uint4 gw = load_slot_group4(my_list, i);
+            int jj[4];
+            jj[0] = (int)(gw.x & 0xFFFFu);
+            jj[1] = (int)(gw.y & 0xFFFFu);
+            jj[2] = (int)(gw.z & 0xFFFFu);
+            jj[3] = (int)(gw.w & 0xFFFFu);
+            v2f d[4];
+            float G[4], araw[4], alpha[4];
+            bool ok[4];
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float4 a = s_a[jj[k]], b = s_b[jj[k]];
+                d[k] = pix_delta(a, pix);
+                const float p2 = eval_p2(a, b, d[k]);
+                G[k] = __builtin_amdgcn_exp2f(fminf(p2, 0.f));
+                araw[k] = b.y * G[k];
+                alpha[k] = fminf(0.99f, araw[k]);
+                ok[k] = jj[k] >= jlo && p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;
+                alpha[k] = ok[k] ? alpha[k] : 0.f;
+                any = any || ok[k];
+            }
+            if (__ballot(any) == 0ull) continue;  // slots stay zero
+            // per pair, in list order: T and A, dL/dalpha; dL/dmeans3D = h * (M . (dx, dy, dx^2, dx dy,
+            // dy^2)) with h = G dL/dG, dL/dopacity = G dL/dalpha, each powered (0 on non-contributing pairs)
+            float v[4 * NV];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float4 c = s_c[jj[k]];
+                const v2f t = v2f{c.x, c.y} * dp01;
+                const float cd = __builtin_fmaf(c.z, dp2, t.x + t.y);
+                const float inv = __builtin_amdgcn_rcpf(1.f - alpha[k]);
+                const float Tn = T * inv;                      // backward.cu:978
+                const float e = cd - A;
+                const bool o = ok[k];
+                const float dLa = o ? __builtin_fmaf(Tbg, inv, e * Tn) : 0.f;
+                T = o ? Tn : T;
+                A = __builtin_fmaf(alpha[k], e, A);
+                const float4 m0 = s_m[MPACK_F4 * jj[k]], m1 = s_m[MPACK_F4 * jj[k] + 1];
+                const float4 m2 = s_m[MPACK_F4 * jj[k] + 2], m3 = s_m[MPACK_F4 * jj[k] + 3];
+                const float dx = d[k].x, dy = d[k].y;
+                const float xx = dx * dx, xy = dx * dy, yy = dy * dy;
+                const float h = araw[k] * dLa;
+                const float q0 = m0.x * dx + m0.y * dy + m0.z * xx + m0.w * xy + m1.x * yy;
+                const float q1 = m1.y * dx + m1.z * dy + m1.w * xx + m2.x * xy + m2.y * yy;
+                const float q2 = m2.z * dx + m2.w * dy + m3.x * xx + m3.y * xy + m3.z * yy;
+                v[NV * k] = o ? pow_sel<POW2>(h * q0, power) : 0.f;
+                v[NV * k + 1] = o ? pow_sel<POW2>(h * q1, power) : 0.f;
+                v[NV * k + 2] = o ? pow_sel<POW2>(h * q2, power) : 0.f;
+                v[NV * k + 3] = o ? pow_sel<POW2>(G[k] * dLa, power) : 0.f;
+                asm volatile("" ::: "memory");  // one entry's rows in registers at a time (hoisting them spilled)
+            }
+            const uint32_t wlo = (my_e & 1) ? gw.y : gw.x, whi = (my_e & 1) ? gw.w : gw.z;
+            const uint32_t we = (my_e & 2) ? whi : wlo;
+            float r[RowReduce<NV>::R];
+            row_reduce<NV>(v, r, lane);
+            if ((lane & RowReduce<NV>::WRITER_MASK) == 0) {
+                float* p = s_acc + (we >> 16) * NV + row_m0<NV>(lane);
+#pragma unroll
+                for (int m = 0; m < RowReduce<NV>::R; m++) p[m] = r[m];
+            }
+        }
+        fetch_m(hi_pf);  // M rows of the next batch (its records were loaded after the staging barrier)
+        __syncthreads();
+        // entry totals: 2 threads per entry, each adds 2 values over the entry's block slots in block
+        // order (deterministic), re-zeroes them, stores its half of the 16-B record
+        int t_ = tid;
+        asm volatile("" : "+v"(t_));
+        const int e = t_ >> 1, q = t_ & 1;
+        if (e < cnt) {
+            float c0 = 0.f, c1 = 0.f;
+            const int nb = __popc((uint32_t)s_mask[e]);
+            float2* src = reinterpret_cast<float2*>(s_acc + (int)s_base[e] * NV) + q;
+            for (int b = 0; b < nb; b++, src += 2) {
+                const float2 x = *src;
+                c0 += x.x;
+                c1 += x.y;
+                *src = make_float2(0.f, 0.f);
+            }
+            reinterpret_cast<float2*>(inst)[2 * (size_t)s_u[e] + q] = make_float2(c0, c1);
+        }
+        __syncthreads();
+        hi -= cnt;
+    }
+}
+
+// One lane per Gaussian: fixed-order sum of its 16-B instance records (deterministic) straight
+// into dL/dmeans3D and dL/dopacity (nullptr: skipped).
+__global__ void __launch_bounds__(256)
+gauss_bwd_fisher_kernel(int P, GeomPtrs geo, const int* __restrict__ radii, const float4* __restrict__ rec,
+                        float* __restrict__ dmeans3D, float* __restrict__ dopacity, BwdGuard guard) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (radii[i] > 0 && !guard.overflow()) {
+        const uint32_t off = geo.offsets[i], cnt = geo.tiles[i];
+        constexpr int RU = 4;  // RU records' loads per memory round trip, added in instance order
+        for (uint32_t e0 = 0; e0 < cnt; e0 += RU) {
+            float4 v[RU];
+#pragma unroll
+            for (int k = 0; k < RU; k++) v[k] = e0 + k < cnt ? rec[off + e0 + k] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int k = 0; k < RU; k++)
+                if (e0 + k < cnt) {
+                    s.x += v[k].x;
+                    s.y += v[k].y;
+                    s.z += v[k].z;
+                    s.w += v[k].w;
+                }
+        }
+    }
+    dmeans3D[3 * i] = s.x;
+    dmeans3D[3 * i + 1] = s.y;
+    dmeans3D[3 * i + 2] = s.z;
+    if (dopacity) dopacity[i] = s.w;
+}
+
+hipError_t launch_gauss_mpack(const Camera& cam, const GaussIn& g, const int* radii, float* mpack, hipStream_t s) {
+    if (g.P == 0) return hipSuccess;
+    hipLaunchKernelGGL(gauss_mpack_kernel, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, radii, (float4*)mpack);
+    return hipGetLastError();
+}
+
+hipError_t launch_render_bwd_fisher(const Camera& cam, const uint2* ranges, const uint64_t* point_list, GeomPtrs geo,
+                                    const float* mpack, const float* final_T, const uint32_t* n_contrib,
+                                    const float* dL_dpix, int power, float* rec, BwdGuard guard, hipStream_t s) {
+    auto k = power == 2 ? render_bwd_fisher_kernel<true> : render_bwd_fisher_kernel<false>;
+    hipLaunchKernelGGL(k, dim3(cam.gx * cam.gy), dim3(TILE_PIX), 0, s, cam, (float)power, ranges, point_list, geo.rr,
+                       geo.blocksums, (const float4*)mpack, final_T, n_contrib, dL_dpix, rec, guard);
+    return hipGetLastError();
+}
+
+hipError_t launch_gauss_bwd_fisher(int P, GeomPtrs geo, const int* radii, const float* rec, float* dmeans3D,
+                                   float* dopacity, BwdGuard guard, hipStream_t s) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(gauss_bwd_fisher_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, geo, radii,
+                       (const float4*)rec, dmeans3D, dopacity, guard);
+    return hipGetLastError();
+}
+
 hipError_t launch_gauss_bwd_power(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii,
                                   const float* rec, const GradsOut& out, BwdGuard guard, hipStream_t s) {
     if (g.P == 0) return hipSuccess;

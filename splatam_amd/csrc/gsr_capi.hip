@@ -546,9 +546,41 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     GradsOut out{grads->dmeans2D, grads->dcolors, grads->dopacity, grads->dmeans3D,
                  grads->dcov3D,   grads->dsh,     grads->dscales,  grads->drotations};
     if (!out.dmeans3D && !pose) return fail(GSR_ERR_INVALID_ARG, "dmeans3D output pointer required");
+    if (power != 1 && !out.dmeans2D && !out.dcolors && !out.dcov3D && !out.dscales && !out.drot && !out.dsh) {
+        // Fisher-selective path: only dL/dmeans3D (+ dL/dopacity), the gradients the fork's Fisher
+        // scoring reads (scripts/ros_handler.py:884-889)
+        if (g.shs) return fail(GSR_ERR_INVALID_ARG, "backward_power != 1 with only dmeans3D / dopacity requested "
+                                                    "needs precomputed colours (no SH)");
+        if (num_rendered > 0 && !binning_buffer) return fail(GSR_ERR_INVALID_ARG, "missing binning buffer");
+        if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
+        const size_t mp_bytes = align_up(sizeof(float) * MPACK_FLOATS * (size_t)P, 256);
+        const size_t rec_bytes = sizeof(float) * 4 * (size_t)num_rendered;
+        char* scratch = (char*)obtain(alloc, alloc_ctx, GSR_BUF_SCRATCH, mp_bytes + rec_bytes);
+        if (!scratch) return fail(GSR_ERR_ALLOC, "allocator returned NULL (backward scratch)");
+        float* mpack = (float*)scratch;
+        float* rec = (float*)(scratch + mp_bytes);
+        const BwdGuard guard{geo.counters, (uint32_t)num_rendered};
+        {
+            StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
+            if ((e = launch_gauss_mpack(cam, g, radii, mpack, stream)) != hipSuccess)
+                return hip_fail(e, "gaussian chain matrix");
+        }
+        if (num_rendered > 0) {
+            const uint64_t* point_list = (const uint64_t*)((const char*)binning_buffer + BL.point_list);
+            StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream);
+            if ((e = launch_render_bwd_fisher(cam, ranges, point_list, geo, mpack, final_T, n_contrib, dL_dout_color,
+                                              power, rec, guard, stream)) != hipSuccess)
+                return hip_fail(e, "render backward (fisher)");
+        }
+        StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
+        if ((e = launch_gauss_bwd_fisher(P, geo, radii, rec, out.dmeans3D, out.dopacity, guard, stream)) != hipSuccess)
+            return hip_fail(e, "gaussian backward (fisher)");
+        return GSR_OK;
+    }
     if (power != 1) {
         if (!out.dmeans2D || !out.dcolors || !out.dopacity || !out.dcov3D || !out.dscales || !out.drot)
-            return fail(GSR_ERR_INVALID_ARG, "backward_power != 1 needs every gradient output pointer");
+            return fail(GSR_ERR_INVALID_ARG, "backward_power != 1 needs every gradient output pointer, or only "
+                                             "dmeans3D (+ dopacity)");
         // per-pair powf before summation (renderCUDAFused, backward.cu:850-1140): gsr_backward_power.hip
         const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
         const int nvp = power_record_floats(nsh);

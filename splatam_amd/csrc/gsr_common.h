@@ -641,6 +641,63 @@ __device__ __forceinline__ RowGroup4 load_row_group4(const uint16_t* row_list, i
     return g;
 }
 
+// Per-wave row lists of one batch: row r of wave w (tile block b = 4w + r) lists the entries j
+// (< cnt) whose block mask has bit b and that lie before the block's last contributor (j >=
+// jmin[r]), as (j | slot << 16) with slot = the entry's slot for block b; every wave also forms
+// the batch's slot bases (exclusive scan of the masks' popcounts, redundantly per wave) and
+// returns cnt = the longest prefix of the cmax staged entries whose slots fit in `budget`.
+// Lists are padded to a common multiple of 4 with `pad`.  Wave 0 publishes the bases.
+struct SlotLists {
+    int len, cnt;
+};
+__device__ __forceinline__ SlotLists build_row_slot_lists(const uint16_t* s_mask, uint16_t* s_base, int cmax,
+                                                         int budget, int w, const int (&jmin)[4], uint32_t* list,
+                                                         int stride, uint32_t pad) {
+    const int lane = __lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t below_w = (1u << (4 * w)) - 1u;  // blocks of the waves before this one
+    int n[4] = {0, 0, 0, 0};
+    uint32_t carry = 0;
+    int cnt = 0;
+    for (int c = 0; c < cmax; c += 64) {
+        const int j = c + lane;
+        const uint32_t mf = j < cmax ? (uint32_t)s_mask[j] : 0u;
+        const uint32_t pc = __popc(mf);
+        // inclusive prefix of the popcounts (0..16) bit by bit: ballots + mbcnt (no lane shuffles,
+        // whose hoisted address registers spilled), the chunk total from the ballots' popcounts
+        uint32_t incl = carry, tot = 0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const uint64_t bk = __ballot((pc >> k) & 1u);
+            incl += (uint32_t)__popcll(bk & (lt | (1ull << lane))) << k;
+            tot += (uint32_t)__popcll(bk) << k;
+        }
+        const uint32_t base = incl - pc;
+        const bool fits = j < cmax && incl <= (uint32_t)budget;
+        cnt += __popcll(__ballot(fits));
+        carry += tot;
+        if (w == 0 && fits) s_base[j] = (uint16_t)base;
+        const uint32_t m = (mf >> (4 * w)) & 0xFu;
+        const uint32_t sb = base + __popc(mf & below_w);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const bool bit = fits && ((m >> r) & 1u) && j >= jmin[r];
+            const uint64_t bal = __ballot(bit);
+            if (bit) list[r * stride + n[r] + __popcll(bal & lt)] = (uint32_t)j | ((sb + __popc(m & ((1u << r) - 1u))) << 16);
+            n[r] += __popcll(bal);
+        }
+    }
+    const int len = (max(max(n[0], n[1]), max(n[2], n[3])) + 3) & ~3;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+        for (int p = n[r] + lane; p < len; p += 64) list[r * stride + p] = pad;
+    return {len, cnt};
+}
+// Four consecutive (j | slot << 16) words of this lane's row list.
+__device__ __forceinline__ uint4 load_slot_group4(const uint32_t* row_list, int i) {
+    return *reinterpret_cast<const uint4*>(&row_list[i]);
+}
+
 // In-kernel device-clock timing of one launch (graph-capturable, no extra
 // kernels): clk = [start, sum of durations, launches, groups done, then 16 group
 // counters KCLOCK_GROUP_STRIDE words apart].  The first workgroup stamps the
@@ -1219,6 +1276,15 @@ hipError_t launch_render_bwd_power(const Camera& cam, const GaussIn& g, const ui
                                    const uint64_t* point_list, GeomPtrs geo, const float* jac, const float* final_T,
                                    const uint32_t* n_contrib, const float* dL_dpix, int power, float* rec,
                                    BwdGuard guard, hipStream_t s);
+// Fisher-selective backward_power path (dL/dmeans3D + dL/dopacity only, colours precomputed):
+// gauss_mpack (3x5 chain matrix per Gaussian, MPACK_FLOATS), render_bwd_fisher (4-float records), sums
+constexpr int MPACK_FLOATS = 16;
+hipError_t launch_gauss_mpack(const Camera& cam, const GaussIn& g, const int* radii, float* mpack, hipStream_t s);
+hipError_t launch_render_bwd_fisher(const Camera& cam, const uint2* ranges, const uint64_t* point_list, GeomPtrs geo,
+                                    const float* mpack, const float* final_T, const uint32_t* n_contrib,
+                                    const float* dL_dpix, int power, float* rec, BwdGuard guard, hipStream_t s);
+hipError_t launch_gauss_bwd_fisher(int P, GeomPtrs geo, const int* radii, const float* rec, float* dmeans3D,
+                                   float* dopacity, BwdGuard guard, hipStream_t s);
 hipError_t launch_gauss_bwd_power(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii,
                                   const float* rec, const GradsOut& out, BwdGuard guard, hipStream_t s);
 
