@@ -51,8 +51,11 @@ def run_oracle(scene, dL_dcolor=None, *, bg=(0.0, 0.0, 0.0), use_sh=False, use_c
 
 
 def run_gpu(scene, dL_dcolor=None, *, device="cuda:0", bg=(0.0, 0.0, 0.0), use_sh=False, use_cov=False, power=1,
-            scale_modifier=1.0, backward=True):
-    """Runs the product rasterizer (splatam_amd.GaussianRasterizer) and returns numpy results."""
+            scale_modifier=1.0, backward=True, grads_for=None):
+    """Runs the product rasterizer (splatam_amd.GaussianRasterizer) and returns numpy results.
+    grads_for: names of the inputs that require grad (means3D, means2D, opacities, colors, shs, cov3D,
+    scales, rotations; default all) -- the others are passed detached and get no gradient."""
+    want = (lambda k: True) if grads_for is None else (lambda k: k in grads_for)  # noqa: E731
     from splatam_amd.rasterizer import GaussianRasterizationSettings, GaussianRasterizer
     c = scene.cam
     dev = torch.device(device)
@@ -61,20 +64,21 @@ def run_gpu(scene, dL_dcolor=None, *, device="cuda:0", bg=(0.0, 0.0, 0.0), use_s
         bg=torch.tensor(bg, dtype=torch.float32, device=dev), scale_modifier=scale_modifier,
         viewmatrix=c.viewmatrix.to(dev), projmatrix=c.projmatrix.to(dev), sh_degree=scene.sh_degree if use_sh else 0,
         campos=c.campos.to(dev), prefiltered=False)
-    leaf = lambda t: t.detach().to(dev).clone().requires_grad_(True)  # noqa: E731
-    means3D = leaf(scene.means3D)
-    means2D = torch.zeros_like(means3D, requires_grad=True)
-    opac = leaf(scene.opacities)
+    def leaf(t, name):
+        return t.detach().to(dev).clone().requires_grad_(want(name))
+    means3D = leaf(scene.means3D, "means3D")
+    means2D = torch.zeros_like(means3D, requires_grad=want("means2D"))
+    opac = leaf(scene.opacities, "opacities")
     kw = {}
     if use_sh:
-        kw["shs"] = leaf(scene.shs)
+        kw["shs"] = leaf(scene.shs, "shs")
     else:
-        kw["colors_precomp"] = leaf(scene.colors)
+        kw["colors_precomp"] = leaf(scene.colors, "colors")
     if use_cov:
-        kw["cov3D_precomp"] = leaf(cov3d_from(scene.scales, scene.rotations, 1.0))
+        kw["cov3D_precomp"] = leaf(cov3d_from(scene.scales, scene.rotations, 1.0), "cov3D")
     else:
-        kw["scales"] = leaf(scene.scales)
-        kw["rotations"] = leaf(scene.rotations)
+        kw["scales"] = leaf(scene.scales, "scales")
+        kw["rotations"] = leaf(scene.rotations, "rotations")
     ras = GaussianRasterizer(st, backward_power=power)
     color, radii, depth = ras(means3D=means3D, means2D=means2D, opacities=opac, **kw)
     out = dict(color=color.detach().cpu().numpy(), depth=depth.detach().cpu().numpy(),
@@ -93,7 +97,7 @@ def run_gpu(scene, dL_dcolor=None, *, device="cuda:0", bg=(0.0, 0.0, 0.0), use_s
         else:
             g["dscales"] = kw["scales"].grad
             g["drot"] = kw["rotations"].grad
-        out["grads"] = {k: v.detach().cpu().numpy() for k, v in g.items()}
+        out["grads"] = {k: v.detach().cpu().numpy() for k, v in g.items() if v is not None}
     return out
 
 

@@ -258,15 +258,23 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:117-196).
 
     Returns (dmeans2D[P,3], dcolors[P,3], dopacity[P,1], dmeans3D[P,3], dcov3D[P,6], dsh[P,M,3],
-    dscales[P,3], drotations[P,4]).  `needs` (8 bools in that order, power == 1 only) skips the
-    gradients nobody wants: they come back as None and their per-pair sums are not formed.
+    dscales[P,3], drotations[P,4]).  `needs` (8 bools in that order) skips the gradients nobody
+    wants: they come back as None and their per-pair sums are not formed.  With power != 1 it is
+    honoured only for the Fisher-selective request -- dmeans3D (+ dopacity) of a render with
+    precomputed colours (scripts/ros_handler.py:884-889 reads no other gradient) -- which runs the
+    4-value-per-pair kernel; any other power != 1 request forms every gradient.
     """
     device = means3D.device
     P = means3D.size(0)
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     M = sh.size(1) if (sh is not None and sh.numel() > 0 and sh.size(0) != 0) else 0
     f32 = dict(dtype=torch.float32, device=device)
-    needs = [True] * 8 if (needs is None or int(power) != 1) else list(needs)
+    if needs is not None and int(power) != 1:
+        fisher = M == 0 and colors is not None and colors.numel() > 0 and \
+            not any(bool(needs[k]) for k in (0, 1, 4, 5, 6, 7))
+        if not fisher:
+            needs = None
+    needs = [True] * 8 if needs is None else list(needs)
     needs[3] = True  # dmeans3D is always produced
     shapes = [(P, 3), (P, 3), (P, 1), (P, 3), (P, 6), (P, M, 3), (P, 3), (P, 4)]
     out = [torch.empty(*sh_, **f32) if nd else None for sh_, nd in zip(shapes, needs)]

@@ -458,7 +458,7 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
     }
     // staging pipelined two batches deep (render_bwd_kernel): records + M of the next batch in
     // registers, sorted list entries of the batch after it
-    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pm4[MPACK_F4] = {pa, pa, pa, pa};
+    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pm0 = pa, pm1 = pa, pm2 = pa, pm3 = pa;
     uint32_t pbs = 0, pmask = 0, prh = 0, pgi = 0;
     PointEntry pn = 0;
     auto fetch_entry = [&](int hi_) {
@@ -479,8 +479,11 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
     // registers while the batch is rasterised (16 VGPRs: the kernel spilled at 96)
     auto fetch_m = [&](int hi_) {
         if (tid < min(BB, hi_)) {
-#pragma unroll
-            for (int q = 0; q < MPACK_F4; q++) pm4[q] = mp[(size_t)MPACK_F4 * pgi + q];
+            const float4* m = mp + (size_t)MPACK_F4 * pgi;
+            pm0 = m[0];
+            pm1 = m[1];
+            pm2 = m[2];
+            pm3 = m[3];
         }
     };
     fetch_entry((int)bmax);
@@ -505,8 +508,10 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
             s_a[ts_] = pa;
             s_b[ts_] = pb;
             s_c[ts_] = pc;
-#pragma unroll
-            for (int q = 0; q < MPACK_F4; q++) s_m[MPACK_F4 * ts_ + q] = pm4[q];
+            s_m[MPACK_F4 * ts_] = pm0;
+            s_m[MPACK_F4 * ts_ + 1] = pm1;
+            s_m[MPACK_F4 * ts_ + 2] = pm2;
+            s_m[MPACK_F4 * ts_ + 3] = pm3;
             s_mask[ts_] = (uint16_t)pmask;
         }
         __syncthreads();

@@ -18,8 +18,9 @@ ranks (one process per GPU): H_train is the all-reduce (sum) of the per-rank
 partial sums (RCCL over xGMI, 16 B per Gaussian), candidate scores are formed on
 the device and exchanged once with an all-gather.  Each pose's render +
 power-2 backward runs through the HIP rasterizer (gsr_forward / gsr_backward
-with power = 2: gauss_jac, render_bwd_power, gauss_bwd_power) and only the two
-gradients H needs are requested.
+with power = 2) and only the two gradients H needs are requested, which selects
+the Fisher kernels (gauss_mpack, render_bwd_fisher, gauss_bwd_fisher: 4 powered
+values per pixel-Gaussian pair instead of the full path's 22).
 
 BatchedFisher renders a batch of K poses per host launch: the K transforms, static-
 capacity forwards (gsr_forward_static), power-2 backwards and the per-pose reductions
@@ -37,6 +38,9 @@ from . import dist as sd
 from .rasterizer import GaussianRasterizer
 
 SEED = 1e-3      # im.backward(gradient=torch.ones_like(im) * 1e-3)  (ros_handler.py:888)
+# the gradients H reads (ros_handler.py:884-889): dmeans3D and dopacity -- the Fisher-selective
+# backward_power kernel (gsr_backward_power.hip render_bwd_fisher_kernel), 4 values per pair
+FISHER_NEEDS = (False, False, True, True, False, False, False, False)
 H_EPS = 0.1      # torch.reciprocal(H_train + 0.1)                   (ros_handler.py:829)
 
 
@@ -198,7 +202,8 @@ class BatchedFisher:
         g = _C.rasterize_gaussians_backward(cam.bg, pts, radii, sc.colors.detach(), sc.scales.detach(),
                                             sc.rotations.detach(), cam.scale_modifier, self.e, cam.viewmatrix,
                                             cam.projmatrix, cam.tanfovx, cam.tanfovy, self.seed, self.e,
-                                            cam.sh_degree, cam.campos, geom, n, binning, img, 2)
+                                            cam.sh_degree, cam.campos, geom, n, binning, img, 2,
+                                            needs=FISHER_NEEDS)
         return torch.cat([g[3].reshape(pts.shape[0], -1), g[2].reshape(pts.shape[0], -1)], dim=1)
 
     def _body(self, _C):

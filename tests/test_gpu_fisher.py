@@ -75,3 +75,43 @@ def test_batched_fisher_matches_per_pose(cuda):
     s_ref = sc.eig_scores(poses)
     s_b = sc.eig_scores(poses, batch=bsc)
     assert torch.equal(s_b, s_ref)
+
+
+@pytest.mark.parametrize("power,aniso,bg", [(2, False, (0.0, 0.0, 0.0)), (2, True, (0.3, 0.1, 0.6)),
+                                            (3, True, (0.0, 0.0, 0.0))])
+def test_fisher_selective_path(cuda, power, aniso, bg):
+    """The Fisher-selective backward (only dmeans3D + dopacity requested: render_bwd_fisher_kernel, 4 powered
+    values per pair) against the full backward_power path (every gradient requested: 22 values per pair) and
+    the float32 oracle's fused mode (backward.cu:850-1140, per-pair powf), on a random-sign seed image with
+    a background colour.  The two GPU paths sum the same per-pair terms in different orders and the
+    selective one folds the chain into a 3x5 matrix per Gaussian, so they agree to float32 rounding."""
+    scene = make_scene(4000, 128, 96, seed=23 + power, anisotropic=aniso)
+    dpix = np.random.RandomState(5).randn(3, scene.cam.H, scene.cam.W).astype(np.float32) * 1e-2
+    sel = harness.run_gpu(scene, dpix, device=cuda, bg=bg, power=power, grads_for=("means3D", "opacities"))
+    full = harness.run_gpu(scene, dpix, device=cuda, bg=bg, power=power)
+    assert set(sel["grads"]) == {"dmeans3D", "dopacity"}
+    _, ref = harness.run_oracle(scene, dpix, bg=bg, power=power, mode=oracle.FUSED)
+    for k in ("dmeans3D", "dopacity"):
+        r_full = harness.rel_l2(sel["grads"][k], full["grads"][k])
+        r_ref = harness.rel_l2(sel["grads"][k], ref[k].reshape(sel["grads"][k].shape))
+        print(f"power {power} {k}: rel L2 vs full path {r_full:.2e}, vs oracle {r_ref:.2e}")
+        assert r_full <= 2e-6, (k, r_full)
+        assert r_ref <= 1e-4, (k, r_ref)
+    if power % 2 == 0:
+        assert (sel["grads"]["dmeans3D"] >= 0).all() and (sel["grads"]["dopacity"] >= 0).all()
+
+
+def test_fisher_selective_config3(cuda):
+    """Full-size BASELINE config 3 (300k Gaussians, 640x480): the selective Hessian of a seeded power-2
+    render vs the full power path and the float32 oracle."""
+    from splatam_amd.scenes import config_scene
+    scene = config_scene(3)
+    dpix = np.full((3, scene.cam.H, scene.cam.W), 1e-3, np.float32)
+    sel = harness.run_gpu(scene, dpix, device=cuda, power=2, grads_for=("means3D", "opacities"))
+    full = harness.run_gpu(scene, dpix, device=cuda, power=2)
+    _, ref = harness.run_oracle(scene, dpix, power=2, mode=oracle.FUSED)
+    for k in ("dmeans3D", "dopacity"):
+        r_full = harness.rel_l2(sel["grads"][k], full["grads"][k])
+        r_ref = harness.rel_l2(sel["grads"][k], ref[k].reshape(sel["grads"][k].shape))
+        print(f"config 3 {k}: rel L2 vs full path {r_full:.2e}, vs oracle {r_ref:.2e}")
+        assert r_full <= 2e-6 and r_ref <= 1e-4, (k, r_full, r_ref)
