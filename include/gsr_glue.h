@@ -284,6 +284,18 @@ typedef struct gsr_adam_tensor {
 int gsr_adam_step(int n_tensors, const gsr_adam_tensor* tensors, int step, double beta1, double beta2, double eps,
                   void* stream);
 
+/* Fisher / EIG view scoring glue (scripts/ros_handler.py:847-902).
+ * gsr_points_to_camera: pts [P,3] = the Gaussians' means [P,3] in a candidate camera frame,
+ *     (rel_w2c @ [means, 1]^T)^T[:, :3] (ros_handler.py:863-866); w2c [4,4] row-major (device),
+ *     each coordinate summed left to right without contraction.
+ * gsr_fisher_accumulate: H [P,4] (16-byte aligned) += [dmeans3D [P,3], dopacity [P,1]] * (*weight)
+ *     (weight: device scalar), product and sum each rounded -- torch's
+ *     H.add_(torch.cat([pts.grad, opacities.grad], 1) * w) in one launch (the visited-pose sum of
+ *     compute_H_visited_inv, ros_handler.py:807-829). */
+int gsr_points_to_camera(int P, const float* means, const float* w2c, float* pts, void* stream);
+int gsr_fisher_accumulate(int P, const float* dmeans3D, const float* dopacity, const float* weight, float* H,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -570,11 +570,15 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
                 const float q0 = m0.x * dx + m0.y * dy + m0.z * xx + m0.w * xy + m1.x * yy;
                 const float q1 = m1.y * dx + m1.z * dy + m1.w * xx + m2.x * xy + m2.y * yy;
                 const float q2 = m2.z * dx + m2.w * dy + m3.x * xx + m3.y * xy + m3.z * yy;
-                v[NV * k] = o ? pow_sel<POW2>(h * q0, power) : 0.f;
-                v[NV * k + 1] = o ? pow_sel<POW2>(h * q1, power) : 0.f;
-                v[NV * k + 2] = o ? pow_sel<POW2>(h * q2, power) : 0.f;
-                v[NV * k + 3] = o ? pow_sel<POW2>(G[k] * dLa, power) : 0.f;
-                asm volatile("" ::: "memory");  // one entry's rows in registers at a time (hoisting them spilled)
+                float x0 = pow_sel<POW2>(h * q0, power), x1 = pow_sel<POW2>(h * q1, power);
+                float x2 = pow_sel<POW2>(h * q2, power), x3 = pow_sel<POW2>(G[k] * dLa, power);
+                // the entry's values formed here, unconditionally (no branch around the M reads), and its
+                // M rows dead before the next entry's are read: all four entries' rows live at once spilled
+                asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)::"memory");
+                v[NV * k] = o ? x0 : 0.f;
+                v[NV * k + 1] = o ? x1 : 0.f;
+                v[NV * k + 2] = o ? x2 : 0.f;
+                v[NV * k + 3] = o ? x3 : 0.f;
             }
             const uint32_t wlo = (my_e & 1) ? gw.y : gw.x, whi = (my_e & 1) ? gw.w : gw.z;
             const uint32_t we = (my_e & 2) ? whi : wlo;

@@ -152,6 +152,33 @@ track_l1_bwd_kernel(int HW, const float* __restrict__ im, const float* __restric
     dds[2 * HW + p] = 0.f;
 }
 
+// Fisher scoring glue (scripts/ros_handler.py:863-866, 884-889): the Gaussians' means moved into a
+// candidate camera frame, and the visited-pose Hessian sum.
+__global__ void __launch_bounds__(GLUE_BLOCK)
+points_to_camera_kernel(int P, const float* __restrict__ means, const float* __restrict__ w2c, float* __restrict__ pts) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float m0 = means[3 * i], m1 = means[3 * i + 1], m2 = means[3 * i + 2];
+#pragma unroll
+    for (int r = 0; r < 3; r++)  // (rel_w2c @ [m, 1]^T)[r], left to right
+        pts[3 * i + r] = ((w2c[4 * r] * m0 + w2c[4 * r + 1] * m1) + w2c[4 * r + 2] * m2) + w2c[4 * r + 3];
+}
+__global__ void __launch_bounds__(GLUE_BLOCK)
+fisher_accumulate_kernel(int P, const float* __restrict__ dm, const float* __restrict__ dop, const float* __restrict__ w,
+                         float* __restrict__ H) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float s = *w;
+    float4 h = reinterpret_cast<float4*>(H)[i];
+    h.x = h.x + dm[3 * i] * s;  // torch: H.add_(torch.cat([dm, dop], 1) * w), each op rounded
+    h.y = h.y + dm[3 * i + 1] * s;
+    h.z = h.z + dm[3 * i + 2] * s;
+    h.w = h.w + dop[i] * s;
+    reinterpret_cast<float4*>(H)[i] = h;
+}
+
 int blocks_for(int n) { return n <= 0 ? 1 : std::min(GLUE_MAX_BLOCKS, (n + GLUE_BLOCK - 1) / GLUE_BLOCK); }
 // the pose reduction's last workgroup reads 16 partials per workgroup: fewer, fuller workgroups
 constexpr int POSE_MAX_BLOCKS = 256;
@@ -261,6 +288,28 @@ int gsr_track_l1_bwd(int H, int W, const float* im, const float* depth_sil, cons
                        dL_dim, dL_ddepth_sil);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GSR_OK : hip_fail(e, "track_l1_bwd");
+}
+
+int gsr_points_to_camera(int P, const float* means, const float* w2c, float* pts, void* stream) {
+    if (P < 0) return fail(GSR_ERR_INVALID_ARG, "points_to_camera: bad size");
+    if (P == 0) return GSR_OK;
+    if (!means || !w2c || !pts) return fail(GSR_ERR_INVALID_ARG, "points_to_camera: null pointer");
+    hipLaunchKernelGGL(points_to_camera_kernel, dim3((P + GLUE_BLOCK - 1) / GLUE_BLOCK), dim3(GLUE_BLOCK), 0,
+                       (hipStream_t)stream, P, means, w2c, pts);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? GSR_OK : hip_fail(e, "points_to_camera");
+}
+
+int gsr_fisher_accumulate(int P, const float* dmeans3D, const float* dopacity, const float* weight, float* H,
+                          void* stream) {
+    if (P < 0) return fail(GSR_ERR_INVALID_ARG, "fisher_accumulate: bad size");
+    if (P == 0) return GSR_OK;
+    if (!dmeans3D || !dopacity || !weight || !H) return fail(GSR_ERR_INVALID_ARG, "fisher_accumulate: null pointer");
+    if (((uintptr_t)H & 15u) != 0) return fail(GSR_ERR_INVALID_ARG, "fisher_accumulate: H must be 16-byte aligned");
+    hipLaunchKernelGGL(fisher_accumulate_kernel, dim3((P + GLUE_BLOCK - 1) / GLUE_BLOCK), dim3(GLUE_BLOCK), 0,
+                       (hipStream_t)stream, P, dmeans3D, dopacity, weight, H);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? GSR_OK : hip_fail(e, "fisher_accumulate");
 }
 
 }  // extern "C"

@@ -45,10 +45,20 @@ H_EPS = 0.1      # torch.reciprocal(H_train + 0.1)                   (ros_handle
 
 
 def camera_points(means: torch.Tensor, w2c: torch.Tensor) -> torch.Tensor:
-    """(rel_w2c @ pts4.T).T[:, :3] (ros_handler.py:863-866) as means @ R^T + t: the same values up to
-    float32 rounding, without the K=P product of the homogeneous form; shared by the per-pose and the
-    batched paths, so both see bitwise the same camera-frame points."""
-    return torch.addmm(w2c[:3, 3], means, w2c[:3, :3].t()).contiguous()
+    """(rel_w2c @ pts4.T).T[:, :3] (ros_handler.py:863-866) in one launch (gsr_points_to_camera: each
+    coordinate summed left to right; a [P,3] x [3,3] addmm took a 22 us hipBLASLt kernel); shared by the
+    per-pose and the batched paths, so both see bitwise the same camera-frame points."""
+    from ._lib import lib
+    if means.device.type != "cuda":
+        raise RuntimeError("Fisher scoring runs on ROCm devices only (no CPU fallback)")
+    means = means.detach().float().contiguous()
+    w2c = w2c.detach().to(means.device).float().contiguous()
+    pts = torch.empty_like(means)
+    rc = lib.gsr_points_to_camera(means.shape[0], means.data_ptr(), w2c.data_ptr(), pts.data_ptr(),
+                                  torch.cuda.current_stream(means.device).cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"gsr_points_to_camera: {lib.gsr_last_error().decode(errors='replace')}")
+    return pts
 
 
 class FisherScorer:
@@ -194,7 +204,8 @@ class BatchedFisher:
                                       self.e, cam.sh_degree, cam.campos, cam.prefiltered, capacity=capacity,
                                       status=self.status[self._k] if capacity else None)
 
-    def _hessian(self, _C, k):
+    def _grads(self, _C, k):
+        """(dL/dmeans_cam [P,3], dL/dopacity [P,1]) of pose slot k (power-2 backward, Fisher kernels)."""
         sc, cam = self.sc, self.sc.cam
         self._k = k
         pts = camera_points(self.means, self.w2c[k])
@@ -204,19 +215,28 @@ class BatchedFisher:
                                             cam.projmatrix, cam.tanfovx, cam.tanfovy, self.seed, self.e,
                                             cam.sh_degree, cam.campos, geom, n, binning, img, 2,
                                             needs=FISHER_NEEDS)
-        return torch.cat([g[3].reshape(pts.shape[0], -1), g[2].reshape(pts.shape[0], -1)], dim=1)
+        return g[3], g[2]
 
     def _body(self, _C):
+        from ._lib import lib
         self._k = 0
         with torch.no_grad():
             if self.mode == "sum":
                 self.out = torch.zeros_like(self.H_inv)
+                P = self.out.shape[0]
+                stream = torch.cuda.current_stream(self.out.device).cuda_stream
                 for k in range(self.K):
-                    self.out.add_(self._hessian(_C, k) * self.weight[k])
+                    dm, dop = self._grads(_C, k)
+                    # out += [dm, dop] * weight[k] in one launch (bitwise torch's add_(cat(...) * w))
+                    rc = lib.gsr_fisher_accumulate(P, dm.data_ptr(), dop.data_ptr(),
+                                                   self.weight.data_ptr() + 4 * k, self.out.data_ptr(), stream)
+                    if rc != 0:
+                        raise RuntimeError(f"gsr_fisher_accumulate: {lib.gsr_last_error().decode(errors='replace')}")
             else:
                 self.out = torch.zeros(self.K, dtype=torch.float32, device=self.H_inv.device)
                 for k in range(self.K):
-                    self.out[k] = (self._hessian(_C, k) * self.H_inv).sum()
+                    dm, dop = self._grads(_C, k)
+                    self.out[k] = (torch.cat([dm, dop.reshape(-1, 1)], dim=1) * self.H_inv).sum()
 
     def _load(self, w2cs):
         if len(w2cs) > self.K:
