@@ -157,6 +157,15 @@ constexpr int bwd_nv() { return 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2
 #ifndef GSR_BWD_WIDE_WAVES
 #define GSR_BWD_WIDE_WAVES 5
 #endif
+#ifndef GSR_TOT_UNROLL
+// entry totals: block slots whose LDS loads are issued together.  4 measured 1-2 us SLOWER than 1 on
+// config 3 (dual lean 72.2-72.7 -> 73.9-74.5 us, single-image full-gradient 87.7-88.5 -> 89-90 us):
+// the totals phase is not latency-bound by its LDS reads
+#define GSR_TOT_UNROLL 1
+#endif
+#ifndef GSR_PACK_C
+#define GSR_PACK_C 1  // DUAL, Q2 = 1: the second colour set's one channel staged in s_c.w (no s_d array)
+#endif
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2>
 constexpr int bwd_waves() { return (DUAL && Q2 == 3) ? 4 : ((OPAC && COL1) ? GSR_BWD_WIDE_WAVES : 5); }
 
@@ -185,10 +194,13 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     // entry BB is a dummy (opacity 0, never blends) that pads the row lists; its slot BS
     // absorbs the pad entries' (zero) sums
     constexpr int SL = BB + 1;
+    // PACKC: the dual render's second colour set needs only channel 0 (Q2 = 1): staged as s_c.w (the
+    // tile-rect half s_c.w carried is consumed at staging), so a pair reads one colour float4, not two
+    constexpr bool PACKC = GSR_PACK_C && DUAL && Q2 == 1;
     __shared__ float4 s_a[SL];
     __shared__ float4 s_b[SL];
     __shared__ float4 s_c[SL];
-    __shared__ float4 s_d[DUAL ? SL : 1];
+    __shared__ float4 s_d[(DUAL && !PACKC) ? SL : 1];
     __shared__ uint32_t s_u[BB];
     __shared__ uint16_t s_mask[BB];
     __shared__ uint16_t s_base[BB];
@@ -260,7 +272,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         s_a[BB] = z;
         s_b[BB] = z;
         s_c[BB] = z;
-        if (DUAL) s_d[BB] = z;
+        if (DUAL && !PACKC) s_d[BB] = z;
     }
     // Batch staging, software-pipelined two batches deep: thread t < batch holds entry t's
     // render record (already in its LDS form) and block-sum word for the next batch, and the
@@ -279,8 +291,12 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             const RenderRec r = load_rr(rr, gi);
             pbs = blocksums[gi / PRE_BLOCK];
             pa = r.q0; pb = r.q1; pc = r.q2;
-            if (DUAL) pd = r.q3;
-            else prh = __float_as_uint(r.q3.w);
+            if (DUAL && !PACKC) {
+                pd = r.q3;
+            } else {
+                prh = __float_as_uint(r.q3.w);
+                if (PACKC) pd.x = r.q3.x;
+            }
         }
     };
 #if GSR_STEPSTAT
@@ -303,12 +319,12 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         int ts_ = tid;
         asm volatile("" : "+v"(ts_));  // staging addresses formed here, not hoisted across the batch loop
         if (ts_ < cmax) {
-            s_u[ts_] = instance_slot(make_uint2(__float_as_uint(pc.w), DUAL ? __float_as_uint(pd.w) : prh),
+            s_u[ts_] = instance_slot(make_uint2(__float_as_uint(pc.w), (DUAL && !PACKC) ? __float_as_uint(pd.w) : prh),
                                      pbs + __float_as_uint(pb.w), tx, ty);
             s_a[ts_] = pa;
             s_b[ts_] = pb;
-            s_c[ts_] = pc;
-            if (DUAL) s_d[ts_] = pd;
+            s_c[ts_] = PACKC ? make_float4(pc.x, pc.y, pc.z, pd.x) : pc;
+            if (DUAL && !PACKC) s_d[ts_] = pd;
             s_mask[ts_] = (uint16_t)pm;  // the instance's exact 4x4-block mask (sorted list entry)
         }
         __syncthreads();
@@ -384,7 +400,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 const float4 c = s_c[gq.j[k]];
                 float cd;
                 if (DUAL && Q2 == 1) {
-                    const float c2x = s_d[gq.j[k]].x;
+                    const float c2x = PACKC ? c.w : s_d[gq.j[k]].x;
                     const v2f t = v2f{c.x, c.y} * dp01;
                     cd = __builtin_fmaf(c.z, dp2, __builtin_fmaf(c2x, dq0, t.x + t.y));
                 } else if (DUAL) {
@@ -460,12 +476,24 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             for (int i = 0; i < NQ; i++) c[i] = 0.f;
             const int nb = __popc((uint32_t)s_mask[e]);
             float* src = s_acc + (int)s_base[e] * NV;
-            for (int b = 0; b < nb; b++, src += NV) {
+            // GSR_TOT_UNROLL block slots' loads per LDS round trip, added in block order (the same sums)
+            constexpr int TU = GSR_TOT_UNROLL;
+            for (int b = 0; b < nb; b += TU, src += TU * NV) {
+                float x[TU][NQ];
 #pragma unroll
-                for (int i = 0; i < NQ; i++)
-                    if (q + TPE * i < NV) {
-                        c[i] += src[q + TPE * i];
-                        src[q + TPE * i] = 0.f;
+                for (int u = 0; u < TU; u++)
+#pragma unroll
+                    for (int i = 0; i < NQ; i++)
+                        x[u][i] = (b + u < nb && q + TPE * i < NV) ? src[u * NV + q + TPE * i] : 0.f;
+#pragma unroll
+                for (int u = 0; u < TU; u++)
+                    if (b + u < nb) {
+#pragma unroll
+                        for (int i = 0; i < NQ; i++)
+                            if (q + TPE * i < NV) {
+                                c[i] += x[u][i];
+                                src[u * NV + q + TPE * i] = 0.f;
+                            }
                     }
             }
             float* dst = inst + (size_t)RS * s_u[e];  // packed record (RecLayout): the NV sums, zero pad
