@@ -168,7 +168,7 @@ int gsr_forward_reuse(const gsr_settings* settings, const gsr_gaussians* gaussia
                       float* out_color, float* out_depth, int* radii,
                       gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
-/* Sets *flag (device int, zeroed by the caller) to non-zero when any of the
+/* Zeroes *flag (device int) and sets it to non-zero when any of the
  * `npairs` (<= 8) float arrays a[k][0..n[k]) and b[k][0..n[k]) differ bitwise.
  * Enqueued on `stream`; the host reads the flag after a stream sync. */
 int gsr_bitwise_equal(int npairs, const float* const* a, const float* const* b, const long long* n, int* flag,

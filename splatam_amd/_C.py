@@ -63,6 +63,36 @@ def _dev_f32(t: torch.Tensor, device, name: str) -> torch.Tensor | None:
     return t.contiguous()
 
 
+# The camera tensors (bg, viewmatrix, projmatrix, campos) are the same objects on every call of an
+# iteration, and SplaTAM passes the matrices as transposed views (utils/recon_helpers.py setup_camera):
+# each call's .contiguous() was a copy kernel (8 launches per RGB + depth fwd+bwd unit).  The copy is
+# reused while the source tensor object is alive and unmodified (weak reference + version counter, which
+# views share with their base), on the same stream, and never during stream capture (a captured graph must
+# re-copy on replay).  GSR_CAM_CACHE=0 disables it.
+_CAM_CACHE = os.environ.get("GSR_CAM_CACHE", "1") != "0"
+
+
+def _cam_f32(t: torch.Tensor, device, name: str, stream: int) -> torch.Tensor | None:
+    if t is None or t.numel() == 0:
+        return None
+    if t.dtype == torch.float32 and t.device == device and t.is_contiguous():
+        return t
+    if not _CAM_CACHE or torch.cuda.is_current_stream_capturing():
+        return _dev_f32(t, device, name)
+    cache = getattr(_tls, "cam_cache", None)
+    if cache is None:
+        cache = _tls.cam_cache = {}
+    e = cache.get(id(t))
+    if e is not None and e[0]() is t and e[1] == t._version and e[2] == stream and e[3].device == device:
+        return e[3]
+    c = _dev_f32(t, device, name)
+    if len(cache) >= 64:
+        for k in [k for k, v in cache.items() if v[0]() is None]:
+            del cache[k]
+    cache[id(t)] = (weakref.ref(t), t._version, stream, c)
+    return c
+
+
 def _ptr(t):
     return None if t is None else t.data_ptr()
 
@@ -72,9 +102,11 @@ def _stream(device) -> int:
 
 
 def _settings(bg, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, scale_modifier, degree, prefiltered,
-              device):
-    keep = [_dev_f32(bg, device, "bg"), _dev_f32(viewmatrix, device, "viewmatrix"),
-            _dev_f32(projmatrix, device, "projmatrix"), _dev_f32(campos, device, "campos")]
+              device, stream=None):
+    if stream is None:
+        stream = _stream(device)
+    keep = [_cam_f32(bg, device, "bg", stream), _cam_f32(viewmatrix, device, "viewmatrix", stream),
+            _cam_f32(projmatrix, device, "projmatrix", stream), _cam_f32(campos, device, "campos", stream)]
     s = GsrSettings(image_height=int(H), image_width=int(W), tan_fovx=float(tan_fovx), tan_fovy=float(tan_fovy),
                     bg=_ptr(keep[0]), scale_modifier=float(scale_modifier), viewmatrix=_ptr(keep[1]),
                     projmatrix=_ptr(keep[2]), sh_degree=int(degree), campos=_ptr(keep[3]),
@@ -143,8 +175,7 @@ def _try_reuse(key, shared, others, P):
         return _miss("version")  # (radii: copied into this call's, so an in-place edit must miss)
     if any(a is None or a.shape != b.shape for a, b in zip(others, po)):
         return _miss("shape")
-    flag = _flag(key[0])
-    flag.zero_()
+    flag = _flag(key[0])  # (zeroed by gsr_bitwise_equal)
     arr_a = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in others])
     arr_b = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in po])
     arr_n = (ctypes.c_longlong * 3)(*[t.numel() for t in others])
@@ -208,13 +239,13 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         return (0, torch.zeros(3, H, W, **f32), torch.zeros(0, dtype=torch.int32, device=device), empty,
                 empty.clone(), empty.clone(), torch.zeros(1, H, W, **f32))
     with torch.cuda.device(device):
+        stream = _stream(device)
         s, keep_s = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, scale_modifier,
-                              degree, prefiltered, device)
+                              degree, prefiltered, device, stream)
         g, keep_g, _ = _gaussians(means3D, sh, colors, opacity, scales, rotations, cov3D_precomp, device)
         out_color = torch.empty(3, H, W, **f32)
         out_depth = torch.empty(1, H, W, **f32)
         radii = torch.empty(P, dtype=torch.int32, device=device)
-        stream = _stream(device)
         reusable = (_GEOM_CACHE and capacity <= 0 and keep_g[2] is not None and keep_g[1] is None and
                     keep_g[6] is None and None not in (keep_g[3], keep_g[4], keep_g[5]))
         if reusable:
@@ -241,7 +272,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                 raise RuntimeError("static forward needs a device status tensor of 4 int32")
             n = lib.gsr_forward_static(ctypes.byref(s), ctypes.byref(g), int(capacity), status.data_ptr(),
                                        out_color.data_ptr(), out_depth.data_ptr(), radii.data_ptr(), _ALLOC_CB, None,
-                                       _stream(device))
+                                       stream)
         else:
             n = lib.gsr_forward(ctypes.byref(s), ctypes.byref(g), out_color.data_ptr(), out_depth.data_ptr(),
                                 radii.data_ptr(), _ALLOC_CB, None, stream)
@@ -281,8 +312,9 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     if P == 0:
         return tuple(out)
     with torch.cuda.device(device):
+        stream = _stream(device)
         s, keep_s = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, scale_modifier,
-                              degree, False, device)
+                              degree, False, device, stream)
         # opacities are not an input of the backward (rasterize_points.cu:117-139): they live in geomBuffer
         g, keep_g, _ = _gaussians(means3D, sh, colors, None, scales, rotations, cov3D_precomp, device)
         dpix = _dev_f32(dL_dout_color, device, "dL_dout_color")
@@ -292,7 +324,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         rc = lib.gsr_backward(ctypes.byref(s), ctypes.byref(g), radii_c.data_ptr(), dpix.data_ptr(), int(R),
                               geomBuffer.data_ptr(), binningBuffer.data_ptr() if binningBuffer.numel() else None,
                               imageBuffer.data_ptr(), int(power), ctypes.byref(grads), _ALLOC_CB, None,
-                              _stream(device))
+                              stream)
         _check(rc, "rasterize_gaussians_backward")
         _tls.buffers = {}  # scratch is released to torch's caching allocator (stream-ordered)
         return tuple(out)

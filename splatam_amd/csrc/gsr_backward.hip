@@ -163,6 +163,12 @@ constexpr int bwd_nv() { return 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2
 // the totals phase is not latency-bound by its LDS reads
 #define GSR_TOT_UNROLL 1
 #endif
+#ifndef GSR_LIST_PF
+#define GSR_LIST_PF 0  // render_bwd row walk: next step's list words prefetched (experiment)
+#endif
+#ifndef GSR_C_EARLY
+#define GSR_C_EARLY 0  // render_bwd row walk: colour reads issued with the geometry reads (experiment)
+#endif
 #ifndef GSR_PACK_C
 #define GSR_PACK_C 1  // DUAL, Q2 = 1: the second colour set's one channel staged in s_c.w (no s_d array)
 #endif
@@ -342,8 +348,18 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
 #if GSR_STEPSTAT
         st_batches++;
 #endif
+#if GSR_LIST_PF
+        // the next step's list words are read while this step computes (one LDS round trip fewer
+        // on each step's dependent chain); reads past n stay inside the row's list (stride BB + 4)
+        uint4 gw_pf = load_slot_group4(my_list, 0);
+#endif
         for (int i = 0; i < n; i += 4) {
+#if GSR_LIST_PF
+            const uint4 gw = gw_pf;
+            gw_pf = load_slot_group4(my_list, i + 4);
+#else
             const uint4 gw = load_slot_group4(my_list, i);
+#endif
             RowGroup4 gq;
             gq.j[0] = (int)(gw.x & 0xFFFFu);
             gq.j[1] = (int)(gw.y & 0xFFFFu);
@@ -353,6 +369,11 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             float G[4], araw[4], alpha[4];
             bool ok[4];
             bool any = false;
+#if GSR_C_EARLY
+            float4 ce[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) ce[k] = s_c[gq.j[k]];
+#endif
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const float4 a = s_a[gq.j[k]], b = s_b[gq.j[k]];
@@ -397,7 +418,11 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             float dLa[4], dch[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
+#if GSR_C_EARLY
+                const float4 c = ce[k];
+#else
                 const float4 c = s_c[gq.j[k]];
+#endif
                 float cd;
                 if (DUAL && Q2 == 1) {
                     const float c2x = PACKC ? c.w : s_d[gq.j[k]].x;

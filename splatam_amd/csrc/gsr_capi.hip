@@ -880,7 +880,8 @@ int gsr_bitwise_equal(int npairs, const float* const* a, const float* const* b, 
         q.b[k] = b[k];
         q.n[k] = n[k];
     }
-    hipError_t e = launch_bitwise_equal(q, flag, (hipStream_t)stream);
+    hipError_t e = zero_async(flag, sizeof(int), (hipStream_t)stream);  // (kernel: valid under capture too)
+    if (e == hipSuccess) e = launch_bitwise_equal(q, flag, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "bitwise_equal");
     return GSR_OK;
 }
