@@ -139,8 +139,11 @@ def _gaussians(means3D, sh, colors, opacity, scales, rotations, cov3D_precomp, d
 #     unmodified (weak references + tensor versions), and
 #   * this call's rotations / opacities / scales equal the first call's bitwise (one device
 #     comparison, gsr_bitwise_equal, read back with the host sync the reference also makes).
-# GSR_GEOM_CACHE=0 disables it.
-_GEOM_CACHE = os.environ.get("GSR_GEOM_CACHE", "1") != "0"
+# Off by default (GSR_GEOM_CACHE=1 enables it): it saves ~60 us of device work per pair of calls, but
+# its comparison read-back is a second host synchronisation per pair, and the unchanged caller is
+# host-bound -- SURVEY 8(d)'s unit took 0.65-0.68 ms with it against 0.48-0.55 ms without on the same
+# box (profiles/r3_unit_ab.txt).
+_GEOM_CACHE = os.environ.get("GSR_GEOM_CACHE", "0") == "1"
 REUSE_STATS = {"hits": 0, "misses": 0}  # eligible calls that did / did not reuse (diagnostics, tests)
 
 

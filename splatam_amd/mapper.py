@@ -9,11 +9,15 @@ uniformly from the mapping window (np.random.randint, splatam.py:851).
 GraphMapper captures one frame's mapping -- the optimizer-state reset plus all
 `iters_per_graph` iterations -- into a torch.cuda.CUDAGraph: the Adam step runs
 inside the transform backward (gsr_map_transform_bwd_adam, step numbers 1..N
-baked into the captured launches), the rasterization uses the static-capacity
-dual forward, and the keyframe sequence is drawn once at construction from
-numpy's global random stream (np.random.randint, the reference's own draw) or,
-with `seed`, from a seeded np.random.RandomState; a replay repeats it, so build
-one mapper per frame for fresh draws.
+baked into the captured launches) and the rasterization uses the static-capacity
+dual forward.  The keyframes are drawn per replay, like the reference draws per
+iteration: every `run()` draws `iters_per_graph` indices from numpy's global random
+stream (np.random.randint, the reference's own draw; `seed`: a seeded
+np.random.RandomState) and gathers the drawn keyframes' target image, depth and
+camera pose into per-iteration slots the captured iterations read (three gathers
+per replay, enqueued before it; the keyframes must share one camera settings object,
+one w2c and one image size -- otherwise the sequence drawn at construction is baked
+into the graph, `redraw` False).  `sequence` is the last replay's draw.
 Each replay is one frame's mapping.  An iteration whose forward overflows the
 binning capacity skips its Adam step on the device (its status row, sticky
 across replays, reports it).  Densification / pruning (which change P)
@@ -71,8 +75,16 @@ class GraphMapper:
             raise RuntimeError(f"a tile list of {longest} > {TILE_SORT_CAP}: use the eager (synchronous) path")
         self.capacity = max(1, int(headroom * max(p[0] for p in probes)) + int(min_extra))
         self.iters = int(iters_per_graph)
-        rng = np.random if seed is None else np.random.RandomState(seed)
-        self.sequence = [int(rng.randint(0, len(keyframes))) for _ in range(self.iters)]  # splatam.py:851
+        self.rng = np.random if seed is None else np.random.RandomState(seed)
+        kf0 = keyframes[0]
+        self.redraw = all(kf["cam"] is kf0["cam"] and kf["w2c"] is kf0["w2c"] and kf["im"].shape == kf0["im"].shape
+                          and kf["depth"].shape == kf0["depth"].shape for kf in keyframes)
+        if self.redraw:
+            self._make_slots(params, keyframes, dev)
+            self.sequence = [0] * self.iters  # warm-up / capture content; run() draws before every replay
+            self._load(self.sequence)
+        else:
+            self.sequence = [int(self.rng.randint(0, len(keyframes))) for _ in range(self.iters)]  # splatam.py:851
         self.status = torch.zeros(self.iters, 4, dtype=torch.int32, device=dev)
         self.adam = MapAdam(params, cfg.lrs, color_key=key)
         self.adam.capacity = self.capacity
@@ -101,19 +113,73 @@ class GraphMapper:
             for k in range(self.iters):
                 self.loss = self._iteration(k)
 
+    def _make_slots(self, params, keyframes, dev):
+        """Per-iteration keyframe slots read by the captured iterations: target image / depth, and the
+        camera pose columns (a params view whose cam_unnorm_rots / cam_trans hold iteration k's pose in
+        column k; the Gaussian tensors are the mapped ones)."""
+        K = self.iters
+        self._kf_im = torch.stack([kf["im"] for kf in keyframes]).contiguous()
+        self._kf_depth = torch.stack([kf["depth"] for kf in keyframes]).contiguous()
+        self._kf_ids = [int(kf["id"]) for kf in keyframes]
+        self._slot_im = torch.empty((K,) + tuple(keyframes[0]["im"].shape), device=dev)
+        self._slot_depth = torch.empty((K,) + tuple(keyframes[0]["depth"].shape), device=dev)
+        cr, ct = params["cam_unnorm_rots"], params["cam_trans"]
+        self._slot_params = dict(params)
+        self._slot_params["cam_unnorm_rots"] = torch.empty(cr.shape[:-1] + (K,), dtype=cr.dtype, device=dev)
+        self._slot_params["cam_trans"] = torch.empty(ct.shape[:-1] + (K,), dtype=ct.dtype, device=dev)
+        kf0 = keyframes[0]
+        self._slot_kfs = [{"cam": kf0["cam"], "w2c": kf0["w2c"], "im": self._slot_im[k], "depth": self._slot_depth[k],
+                           "id": k} for k in range(K)]
+        self._idx_host = torch.empty(2, K, dtype=torch.int64, pin_memory=True)
+        self._idx_dev = torch.empty(2, K, dtype=torch.int64, device=dev)
+        self._idx_event = None
+
+    def _load(self, seq):
+        """Gather the keyframes of `seq` (one index per iteration) into the slots, on the current stream."""
+        if self._idx_event is not None:  # the pinned index buffer of the previous load has been read
+            self._idx_event.synchronize()
+        self._idx_host[0] = torch.tensor(seq, dtype=torch.int64)
+        self._idx_host[1] = torch.tensor([self._kf_ids[j] for j in seq], dtype=torch.int64)
+        self._idx_dev.copy_(self._idx_host, non_blocking=True)
+        self._idx_event = torch.cuda.Event()
+        self._idx_event.record()
+        with torch.no_grad():
+            torch.index_select(self._kf_im, 0, self._idx_dev[0], out=self._slot_im)
+            torch.index_select(self._kf_depth, 0, self._idx_dev[0], out=self._slot_depth)
+            p = self.params
+            torch.index_select(p["cam_unnorm_rots"].detach(), -1, self._idx_dev[1],
+                               out=self._slot_params["cam_unnorm_rots"])
+            torch.index_select(p["cam_trans"].detach(), -1, self._idx_dev[1], out=self._slot_params["cam_trans"])
+
     def _iteration(self, k: int):
-        kf = self.keyframes[self.sequence[k]]
+        if self.redraw:
+            kf, params, t = self._slot_kfs[k], self._slot_params, k
+        else:
+            kf = self.keyframes[self.sequence[k]]
+            params, t = self.params, kf["id"]
         self.adam.status = self.status[k]  # this iteration's forward guards its Adam step
-        loss, _, _ = _get_loss_mapping_fused(self.params, kf, kf["id"], self.cfg, adam=self.adam,
-                                             capacity=self.capacity, status=self.status[k], means2D=self.means2D)
+        loss, _, _ = _get_loss_mapping_fused(params, kf, t, self.cfg, adam=self.adam, capacity=self.capacity,
+                                             status=self.status[k], means2D=self.means2D)
         torch.autograd.backward(loss, self.seed)
         return loss.detach()
 
-    def run(self, check: bool = False):
-        """Enqueue one frame's mapping (one graph launch, no host sync).  An iteration whose forward
-        overflowed skips its own Adam step (the steps guard on that forward's counters), but the bias
-        corrections of the later steps still count it; with `check` the replay ends with one host sync
-        and raises on any overflow, so the caller can rebuild with more headroom and re-map the frame."""
+    def run(self, check: bool = False, sequence=None):
+        """Enqueue one frame's mapping (one graph launch, no host sync).  With `redraw` the keyframe of
+        every iteration is drawn now (splatam.py:851; `sequence` overrides the draw) and gathered into the
+        slots.  An iteration whose forward overflowed skips its own Adam step (the steps guard on that
+        forward's counters), but the bias corrections of the later steps still count it; with `check`
+        the replay ends with one host sync and raises on any overflow, so the caller can rebuild with
+        more headroom and re-map the frame."""
+        if self.redraw:
+            n = len(self.keyframes)
+            seq = [int(self.rng.randint(0, n)) for _ in range(self.iters)] if sequence is None else \
+                [int(j) for j in sequence]
+            if len(seq) != self.iters or not all(0 <= j < n for j in seq):
+                raise ValueError(f"sequence: {self.iters} keyframe indices in [0, {n})")
+            self.sequence = seq
+            self._load(seq)
+        elif sequence is not None:
+            raise RuntimeError("this mapper bakes its keyframe sequence into the graph (redraw False)")
         if check:
             self.reset_status()
         self.graph.replay()

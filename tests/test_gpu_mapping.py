@@ -3,6 +3,7 @@ the fused SSIM/L1 loss kernels, the mapping transform backward, the fused Adam
 step and the whole fused iteration against the literal restatement of
 scripts/splatam.py:220-353 (mapping=True) in splatam_amd.slam, whose torch glue
 is itself pinned to the reference's utils/*.py by tests/test_glue_cpu.py."""
+import numpy as np
 import pytest
 import torch
 
@@ -273,8 +274,9 @@ def _keyframes(params, cam, cuda, K=3):
 
 @pytest.mark.parametrize("sh", [False, True])
 def test_graph_mapper_matches_eager_iterations(cuda, sh):
-    """Two replays of a 6-iteration mapping graph (fresh optimizer per replay, keyframes
-    drawn at construction) follow the same 2 x 6 eager fused iterations with MapAdam."""
+    """Two replays of a 6-iteration mapping graph (fresh optimizer per replay, keyframes drawn per
+    replay and gathered into the captured iterations' slots) follow the same 2 x 6 eager fused
+    iterations with MapAdam over the drawn keyframes."""
     from splatam_amd.mapper import GraphMapper
     _, params, cam = _map_params(cuda, True, sh)
     kfs = _keyframes(params, cam, cuda)
@@ -285,17 +287,23 @@ def test_graph_mapper_matches_eager_iterations(cuda, sh):
     for k in keys:
         g_p[k].requires_grad_(True)
         e_p[k].requires_grad_(True)
-    mapper = GraphMapper(g_p, kfs, iters_per_graph=6)
+    mapper = GraphMapper(g_p, kfs, iters_per_graph=6, seed=7)
+    assert mapper.redraw
     for k in keys:  # construction (warm-up) leaves the parameters untouched
         assert torch.equal(g_p[k].detach(), params[k]), k
-    mapper.run()
-    mapper.run()
+    seqs = []
+    for _ in range(2):
+        mapper.run()
+        seqs.append(list(mapper.sequence))
     torch.cuda.synchronize()
     assert not mapper.overflowed()
+    rs = np.random.RandomState(7)  # the reference's per-iteration draws (splatam.py:851)
+    assert seqs == [[int(rs.randint(0, len(kfs))) for _ in range(6)] for _ in range(2)]
+    assert seqs[0] != seqs[1] and len(set(seqs[0] + seqs[1])) > 1
     adam = MapAdam(e_p, slam.MappingConfig().lrs, color_key=key)
-    for _ in range(2):
+    for seq in seqs:
         adam.reset()
-        for j in mapper.sequence:
+        for j in seq:
             kf = kfs[j]
             loss, _, _ = slam.get_loss_mapping(e_p, kf, kf["id"], fused=True, adam=adam)
             loss.backward()

@@ -49,7 +49,7 @@ def main():
         torch.cuda.synchronize()
     dev_us = sum(e.self_device_time_total for e in prof.key_averages()) / a.iters
     ours = sum(e.self_device_time_total for e in prof.key_averages() if "gsr::" in e.key or "rocclr_copy" in e.key)
-    lines = [f"wall per iteration (no profiler): {wall * 1e3:.3f} ms  (GSR_GEOM_CACHE={os.environ.get('GSR_GEOM_CACHE', '1')})",
+    lines = [f"wall per iteration (no profiler): {wall * 1e3:.3f} ms  (GSR_GEOM_CACHE={os.environ.get('GSR_GEOM_CACHE', '0')})",
              f"device time per iteration: {dev_us:.1f} us (all kernels), {ours / a.iters:.1f} us (libgsr kernels + copies)",
              prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=40),
              prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=25)]

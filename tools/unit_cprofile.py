@@ -16,6 +16,7 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=300)
+    ap.add_argument("--no-profile", action="store_true")
     a = ap.parse_args()
     import diff_gaussian_rasterization as dgr
     from splatam_amd.scenes import config_scene
@@ -53,6 +54,8 @@ def main():
         unit()
     torch.cuda.synchronize()
     print(f"unit {1e3 * (time.perf_counter() - t0) / a.n:.4f} ms (no profiler)")
+    if a.no_profile:
+        return
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(a.n):
