@@ -157,18 +157,6 @@ constexpr int bwd_nv() { return 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2
 #ifndef GSR_BWD_WIDE_WAVES
 #define GSR_BWD_WIDE_WAVES 5
 #endif
-#ifndef GSR_TOT_UNROLL
-// entry totals: block slots whose LDS loads are issued together.  4 measured 1-2 us SLOWER than 1 on
-// config 3 (dual lean 72.2-72.7 -> 73.9-74.5 us, single-image full-gradient 87.7-88.5 -> 89-90 us):
-// the totals phase is not latency-bound by its LDS reads
-#define GSR_TOT_UNROLL 1
-#endif
-#ifndef GSR_LIST_PF
-#define GSR_LIST_PF 0  // render_bwd row walk: next step's list words prefetched (experiment)
-#endif
-#ifndef GSR_C_EARLY
-#define GSR_C_EARLY 0  // render_bwd row walk: colour reads issued with the geometry reads (experiment)
-#endif
 #ifndef GSR_PACK_C
 #define GSR_PACK_C 1  // DUAL, Q2 = 1: the second colour set's one channel staged in s_c.w (no s_d array)
 #endif
@@ -348,18 +336,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
 #if GSR_STEPSTAT
         st_batches++;
 #endif
-#if GSR_LIST_PF
-        // the next step's list words are read while this step computes (one LDS round trip fewer
-        // on each step's dependent chain); reads past n stay inside the row's list (stride BB + 4)
-        uint4 gw_pf = load_slot_group4(my_list, 0);
-#endif
         for (int i = 0; i < n; i += 4) {
-#if GSR_LIST_PF
-            const uint4 gw = gw_pf;
-            gw_pf = load_slot_group4(my_list, i + 4);
-#else
             const uint4 gw = load_slot_group4(my_list, i);
-#endif
             RowGroup4 gq;
             gq.j[0] = (int)(gw.x & 0xFFFFu);
             gq.j[1] = (int)(gw.y & 0xFFFFu);
@@ -369,11 +347,6 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             float G[4], araw[4], alpha[4];
             bool ok[4];
             bool any = false;
-#if GSR_C_EARLY
-            float4 ce[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) ce[k] = s_c[gq.j[k]];
-#endif
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const float4 a = s_a[gq.j[k]], b = s_b[gq.j[k]];
@@ -418,11 +391,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             float dLa[4], dch[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-#if GSR_C_EARLY
-                const float4 c = ce[k];
-#else
                 const float4 c = s_c[gq.j[k]];
-#endif
                 float cd;
                 if (DUAL && Q2 == 1) {
                     const float c2x = PACKC ? c.w : s_d[gq.j[k]].x;
@@ -501,24 +470,12 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             for (int i = 0; i < NQ; i++) c[i] = 0.f;
             const int nb = __popc((uint32_t)s_mask[e]);
             float* src = s_acc + (int)s_base[e] * NV;
-            // GSR_TOT_UNROLL block slots' loads per LDS round trip, added in block order (the same sums)
-            constexpr int TU = GSR_TOT_UNROLL;
-            for (int b = 0; b < nb; b += TU, src += TU * NV) {
-                float x[TU][NQ];
+            for (int b = 0; b < nb; b++, src += NV) {
 #pragma unroll
-                for (int u = 0; u < TU; u++)
-#pragma unroll
-                    for (int i = 0; i < NQ; i++)
-                        x[u][i] = (b + u < nb && q + TPE * i < NV) ? src[u * NV + q + TPE * i] : 0.f;
-#pragma unroll
-                for (int u = 0; u < TU; u++)
-                    if (b + u < nb) {
-#pragma unroll
-                        for (int i = 0; i < NQ; i++)
-                            if (q + TPE * i < NV) {
-                                c[i] += x[u][i];
-                                src[u * NV + q + TPE * i] = 0.f;
-                            }
+                for (int i = 0; i < NQ; i++)
+                    if (q + TPE * i < NV) {
+                        c[i] += src[q + TPE * i];
+                        src[q + TPE * i] = 0.f;
                     }
             }
             float* dst = inst + (size_t)RS * s_u[e];  // packed record (RecLayout): the NV sums, zero pad
