@@ -117,12 +117,19 @@ __device__ __forceinline__ void reduce_store(const float (&v)[4 * N], int lane, 
 #define GSR_BWD_BB 128  // batch of the variants with <= 6 sums (timing experiments may override)
 #endif
 #ifndef GSR_BWD_WBB
-#define GSR_BWD_WBB 96  // batch of the wide variants (> 6 sums): 96 measured faster than 64 (mapping render_bwd 362 -> 326 us) at 5 waves/SIMD; 128 drops to 4
+// batch of the wide variants (> 6 sums): 96 measured faster than 64 (mapping render_bwd 362 -> 326 us) at 5
+// waves/SIMD; 128 entries with a 384-slot budget (the 96-entry batch's s_acc; 2.7 blocks per entry on
+// average) stay at 5 waves/SIMD and measured 3 % faster again (single-image full gradient 88 -> 85.5 us,
+// config-4 dual 425 -> 410 us; profiles/r3_ab_render_bwd.txt); 448 slots drop the mapping variant to 4
+#define GSR_BWD_WBB 128
 #endif
 template <int NV>
 constexpr int bwd_batch() { return NV <= 6 ? GSR_BWD_BB : GSR_BWD_WBB; }
+#ifndef GSR_BWD_WBS
+#define GSR_BWD_WBS 384  // slot budget of the wide variants' batches
+#endif
 template <int NV>
-constexpr int bwd_slots() { return NV <= 6 ? 4 * GSR_BWD_BB : 4 * GSR_BWD_WBB; }
+constexpr int bwd_slots() { return NV <= 6 ? 4 * GSR_BWD_BB : GSR_BWD_WBS; }
 
 // DUAL: the pass also carries a second colour set (colors2, dL_dpix2) composited
 // with the same alpha / T (one dual forward): the per-pair dL/dalpha is the sum
