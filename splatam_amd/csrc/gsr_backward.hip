@@ -114,7 +114,9 @@ __device__ __forceinline__ void reduce_store(const float (&v)[4 * N], int lane, 
 // owns popcount(block mask) consecutive slots of NV floats (about 3 on average, at most 16), so a
 // batch of BB entries is cut short when its masks need more than BS slots.
 #ifndef GSR_BWD_BB
-#define GSR_BWD_BB 128  // batch of the variants with <= 6 sums (timing experiments may override)
+// batch of the variants with <= 6 sums (timing experiments may override); 144 and 160 entries (512 /
+// 576 slots, still 5 waves/SIMD) measured 3-4 us slower on the config-3 tracking launch (r3 ab5)
+#define GSR_BWD_BB 128
 #endif
 #ifndef GSR_BWD_WBB
 // batch of the wide variants (> 6 sums): 96 measured faster than 64 (mapping render_bwd 362 -> 326 us) at 5
@@ -128,8 +130,11 @@ constexpr int bwd_batch() { return NV <= 6 ? GSR_BWD_BB : GSR_BWD_WBB; }
 #ifndef GSR_BWD_WBS
 #define GSR_BWD_WBS 384  // slot budget of the wide variants' batches
 #endif
+#ifndef GSR_BWD_BS
+#define GSR_BWD_BS (4 * GSR_BWD_BB)  // slot budget of the batches of the variants with <= 6 sums
+#endif
 template <int NV>
-constexpr int bwd_slots() { return NV <= 6 ? 4 * GSR_BWD_BB : GSR_BWD_WBS; }
+constexpr int bwd_slots() { return NV <= 6 ? GSR_BWD_BS : GSR_BWD_WBS; }
 
 // DUAL: the pass also carries a second colour set (colors2, dL_dpix2) composited
 // with the same alpha / T (one dual forward): the per-pair dL/dalpha is the sum
