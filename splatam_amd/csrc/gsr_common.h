@@ -201,7 +201,7 @@ struct GaussIn {
     const float* rotations;
     const float* cov3D;
     const float* colors2;  // second precomputed colour set of a dual render (else nullptr)
-    int sh_staged;         // SH colours already in rr[2].xyz / clamp (sh_eval_kernel, gsr_sh.hip)
+    int sh_staged;         // SH colours already in bin[i].xyz / clamp (sh_eval_kernel, gsr_sh.hip)
 };
 
 struct GeomPtrs {

@@ -41,9 +41,9 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     if (!XF && i < g.P) {
         if (g.colors) {
             pre_rgb[0] = g.colors[3 * i]; pre_rgb[1] = g.colors[3 * i + 1]; pre_rgb[2] = g.colors[3 * i + 2];
-        } else if (g.sh_staged) {  // sh_eval_kernel wrote rgb and the clamp bits
-            const float4 c = geo.rr[(size_t)RR_F4 * i + 2];
-            pre_rgb[0] = c.x; pre_rgb[1] = c.y; pre_rgb[2] = c.z;
+        } else if (g.sh_staged) {  // sh_eval_kernel wrote rgb (in bin[i], overwritten below) and the clamp bits
+            const uint4 c = geo.bin[i];
+            pre_rgb[0] = __uint_as_float(c.x); pre_rgb[1] = __uint_as_float(c.y); pre_rgb[2] = __uint_as_float(c.z);
         }
         pre_op = g.opacities[i];
         if (g.colors2) {
@@ -125,8 +125,8 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                 if (XF && g.colors) {
                     rgb[0] = g.colors[3 * i]; rgb[1] = g.colors[3 * i + 1]; rgb[2] = g.colors[3 * i + 2];
                 } else if (XF && g.sh_staged) {
-                    const float4 c = geo.rr[(size_t)RR_F4 * i + 2];
-                    rgb[0] = c.x; rgb[1] = c.y; rgb[2] = c.z;
+                    const uint4 c = geo.bin[i];
+                    rgb[0] = __uint_as_float(c.x); rgb[1] = __uint_as_float(c.y); rgb[2] = __uint_as_float(c.z);
                 } else if (!g.colors && !g.sh_staged) {
                     sh_fwd(cam.sh_degree, p, cam.campos, g.shs + (size_t)3 * g.M * i, rgb, clamped);
                 }

@@ -7,8 +7,8 @@
 // lane works on its own LDS row (row stride 3*NSH + 1 floats: odd, so the 64
 // lanes of a wave hit 64 distinct banks).
 //
-//   sh_eval_kernel  computeColorFromSH (forward.cu:20-73) -> render-record rgb
-//                   (rr[2].xyz) and the clamp bits, before preprocess;
+//   sh_eval_kernel  computeColorFromSH (forward.cu:20-73) -> rgb (handed to preprocess
+//                   in the binning record bin[i]) and the clamp bits, before preprocess;
 //   sh_bwd_kernel   the SH part of preprocessCUDA's backward (backward.cu:20-139):
 //                   dsh (staged in LDS, written as one float4 stream) and the
 //                   view-direction term added to dL/dmeans3D, after gauss_bwd has
@@ -19,12 +19,9 @@ namespace gsr {
 namespace {
 
 constexpr int SH_BLOCK = 256;
-#ifndef GSR_SH_EVAL_BLOCK
-#define GSR_SH_EVAL_BLOCK 64
-#endif
 // sh_eval: one wave per workgroup (12.5 KB of LDS at D = 3): the waves of a CU stage and evaluate
-// independently instead of in barrier-coupled groups of four
-constexpr int SH_EVAL_BLOCK = GSR_SH_EVAL_BLOCK;
+// independently instead of in barrier-coupled groups of four (GSR_SH_EVAL_WAVES: several such waves
+// per workgroup, each with its own LDS rows and no workgroup barrier)
 
 template <int NSH>
 struct ShTile {
@@ -34,7 +31,8 @@ struct ShTile {
 
 // Global [n x ROW] block (contiguous: M == NSH) -> LDS rows.
 template <int NSH, int BLK = SH_BLOCK>
-__device__ __forceinline__ void stage_rows(float* s, const float* __restrict__ src, int n) {
+__device__ __forceinline__ void stage_rows(float* s, const float* __restrict__ src, int n, int tix = -1) {
+    const int tt = tix < 0 ? (int)threadIdx.x : tix;  // the staging thread's index among BLK
     using T = ShTile<NSH>;
     const int total = n * T::ROW;
     if (T::ROW % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
@@ -43,23 +41,23 @@ __device__ __forceinline__ void stage_rows(float* s, const float* __restrict__ s
             constexpr int IT = T::ROW / 4 > 0 ? T::ROW / 4 : 1;  // float4 per lane (ROW % 4 == 0 here)
             float4 v[IT];
 #pragma unroll
-            for (int k = 0; k < IT; k++) v[k] = s4[threadIdx.x + k * BLK];
+            for (int k = 0; k < IT; k++) v[k] = s4[tt + k * BLK];
 #pragma unroll
             for (int k = 0; k < IT; k++) {
-                const int e = 4 * (threadIdx.x + k * BLK), r = e / T::ROW, c = e - r * T::ROW;
+                const int e = 4 * (tt + k * BLK), r = e / T::ROW, c = e - r * T::ROW;
                 float* d = s + r * T::PITCH + c;
                 d[0] = v[k].x; d[1] = v[k].y; d[2] = v[k].z; d[3] = v[k].w;
             }
             return;
         }
-        for (int e4 = threadIdx.x; 4 * e4 < total; e4 += BLK) {
+        for (int e4 = tt; 4 * e4 < total; e4 += BLK) {
             const float4 v = s4[e4];
             const int e = 4 * e4, r = e / T::ROW, c = e - r * T::ROW;  // ROW % 4 == 0: no row straddle
             float* d = s + r * T::PITCH + c;
             d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
         }
     } else {
-        for (int e = threadIdx.x; e < total; e += BLK) {
+        for (int e = tt; e < total; e += BLK) {
             const int r = e / T::ROW, c = e - r * T::ROW;
             s[r * T::PITCH + c] = src[e];
         }
@@ -152,24 +150,40 @@ __device__ __forceinline__ void adam_rows(float* p, float* m, float* v, const fl
     }
 }
 
+#ifndef GSR_SH_EVAL_WAVES
+#define GSR_SH_EVAL_WAVES 1  // waves per sh_eval workgroup, each staging and evaluating its own 64 Gaussians
+#endif
 template <int NSH>
-__global__ void __launch_bounds__(SH_EVAL_BLOCK) sh_eval_kernel(Camera cam, GaussIn g, GeomPtrs geo) {
+__global__ void __launch_bounds__(64 * GSR_SH_EVAL_WAVES) sh_eval_kernel(Camera cam, GaussIn g, GeomPtrs geo) {
     using T = ShTile<NSH>;
-    __shared__ float s_sh[SH_EVAL_BLOCK * T::PITCH];
-    const int base = blockIdx.x * SH_EVAL_BLOCK;
-    const int n = min(SH_EVAL_BLOCK, g.P - base);
-    const int i = base + threadIdx.x;
-    const bool act = (int)threadIdx.x < n;
+    __shared__ float s_all[GSR_SH_EVAL_WAVES * 64 * T::PITCH];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float* s_sh = s_all + wv * 64 * T::PITCH;
+    const int base = (blockIdx.x * GSR_SH_EVAL_WAVES + wv) * 64;
+    const int n = min(64, g.P - base);
+    if (n <= 0) return;
+    const int i = base + lane;
+    const bool act = lane < n;
     // the lane's mean is loaded with the staging stream, not after it
     const float3 p = act ? make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2])
                          : make_float3(0.f, 0.f, 0.f);
-    stage_rows<NSH, SH_EVAL_BLOCK>(s_sh, g.shs + (size_t)T::ROW * base, n);
-    __syncthreads();
+    if (GSR_SH_EVAL_WAVES == 1) {
+        stage_rows<NSH, 64>(s_sh, g.shs + (size_t)T::ROW * base, n);
+        __syncthreads();
+    } else {  // wave-local staging: the wave's 64 rows, no workgroup barrier (each wave reads only its own)
+        stage_rows<NSH, 64>(s_sh, g.shs + (size_t)T::ROW * base, n, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     if (!act) return;
     float rgb[3];
     unsigned clamped = 0;
     sh_fwd(cam.sh_degree, p, cam.campos, s_sh + threadIdx.x * T::PITCH, rgb, clamped);
-    geo.rr[(size_t)RR_F4 * i + 2] = make_float4(rgb[0], rgb[1], rgb[2], 0.f);  // .w: tile rect, by preprocess
+    // handed to preprocess through bin[i] (dense 16-B rows, one full line per 4 Gaussians; preprocess
+    // reads it first and overwrites it with the binning record) instead of the render record's rgb slot
+    // (16 B every 64 B: partial-line writes here, 64-B line reads there)
+    geo.bin[i] = make_uint4(__float_as_uint(rgb[0]), __float_as_uint(rgb[1]), __float_as_uint(rgb[2]), 0u);
     geo.clamp[i] = clamped;
 }
 
@@ -215,7 +229,8 @@ sh_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii
 
 template <int NSH>
 hipError_t launch_sh_eval_t(const Camera& cam, const GaussIn& g, GeomPtrs geo, hipStream_t s) {
-    hipLaunchKernelGGL(sh_eval_kernel<NSH>, dim3((g.P + SH_EVAL_BLOCK - 1) / SH_EVAL_BLOCK), dim3(SH_EVAL_BLOCK), 0, s, cam, g, geo);
+    constexpr int per = 64 * GSR_SH_EVAL_WAVES;
+    hipLaunchKernelGGL(sh_eval_kernel<NSH>, dim3((g.P + per - 1) / per), dim3(per), 0, s, cam, g, geo);
     return hipGetLastError();
 }
 
