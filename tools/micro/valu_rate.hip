@@ -31,6 +31,17 @@ __global__ void __launch_bounds__(256) valu_kernel(float* out, unsigned long lon
             } else if (MIX == 3) {  // fma + exp (transcendental)
                 a[k] = __builtin_fmaf(a[k], b, c);
                 a[k] = __builtin_amdgcn_exp2f(a[k]);
+            } else if (MIX >= 4) {  // fma, then (after the unrolled fmas) a lane-half swap per pair + add/sub
+                a[k] = __builtin_fmaf(a[k], b, c);
+            }
+        }
+        if (MIX >= 4) {  // v_permlane32_swap (MIX 4) / v_permlane16_swap (MIX 5): one per two chains
+#pragma unroll
+            for (int k = 0; k < 8; k += 2) {
+                const auto r = MIX == 4 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(a[k]), __float_as_uint(a[k + 1]), false, false)
+                                        : __builtin_amdgcn_permlane16_swap(__float_as_uint(a[k]), __float_as_uint(a[k + 1]), false, false);
+                a[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+                a[k + 1] = __uint_as_float(r[0]) - __uint_as_float(r[1]);
             }
         }
         asm volatile("" ::: "memory");
@@ -51,12 +62,12 @@ int main() {
     unsigned long long* cyc;
     hipMalloc(&out, sizeof(float) * 256 * cus * maxw);
     hipMalloc(&cyc, sizeof(unsigned long long) * 4 * cus * maxw);
-    const char* names[4] = {"fma", "fma+dpp_add", "fma+cndmask", "fma+exp"};
-    const int per_iter[4] = {8, 16, 24, 16};  // VALU instructions per loop iteration (checked in the ISA, -fno-slp-vectorize)
-    for (int mix = 0; mix < 4; mix++) {
+    const char* names[6] = {"fma", "fma+dpp_add", "fma+cndmask", "fma+exp", "fma+pl32swap", "fma+pl16swap"};
+    const int per_iter[6] = {8, 16, 24, 16, 20, 20};  // VALU instructions per loop iteration (checked in the ISA, -fno-slp-vectorize)
+    for (int mix = 0; mix < 6; mix++) {
         for (int w = 1; w <= maxw; w++) {
             const int blocks = cus * w;
-            auto k = mix == 0 ? valu_kernel<0> : mix == 1 ? valu_kernel<1> : mix == 2 ? valu_kernel<2> : valu_kernel<3>;
+            auto k = mix == 0 ? valu_kernel<0> : mix == 1 ? valu_kernel<1> : mix == 2 ? valu_kernel<2> : mix == 3 ? valu_kernel<3> : mix == 4 ? valu_kernel<4> : valu_kernel<5>;
             hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, out, cyc, 1.0f);  // warm-up
             hipEvent_t e0, e1;
             hipEventCreate(&e0);
