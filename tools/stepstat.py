@@ -9,7 +9,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["GSR_LIB"] = os.path.join(ROOT, "splatam_amd", "_diag", "libgsr_stepstat.so")
+os.environ["GSR_LIB"] = os.environ.get("GSR_LIB") or os.path.join(ROOT, "splatam_amd", "_diag", "libgsr_stepstat.so")
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
