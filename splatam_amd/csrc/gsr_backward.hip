@@ -423,7 +423,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 const bool o = ok[k];
                 dLa[k] = o ? __builtin_fmaf(Tbg, inv, e * Tn) : 0.f;
                 dch[k] = alpha[k] * Tn;                 // 0 when masked
-                T = o ? Tn : T;                         // (select: keeps T exact whatever rcp(1) returns)
+                T = Tn;  // masked pairs: alpha = 0 and v_rcp_f32(1) == 1 exactly (tools/micro/rcp_one.hip)
                 A = __builtin_fmaf(alpha[k], e, A);     // unchanged when masked
             }
             // Per pair: (hx, hy, hx*dx, hx*dy, hy*dy, G*dL/dalpha, dch*dL/dpix, dch*dL/dpix2) with

@@ -560,7 +560,7 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
                 const float e = cd - A;
                 const bool o = ok[k];
                 const float dLa = o ? __builtin_fmaf(Tbg, inv, e * Tn) : 0.f;
-                T = o ? Tn : T;
+                T = Tn;  // masked pairs: alpha = 0, v_rcp_f32(1) == 1 exactly
                 A = __builtin_fmaf(alpha[k], e, A);
                 const float4 m0 = s_m[MPACK_F4 * jj[k]], m1 = s_m[MPACK_F4 * jj[k] + 1];
                 const float4 m2 = s_m[MPACK_F4 * jj[k] + 2], m3 = s_m[MPACK_F4 * jj[k] + 3];
