@@ -358,7 +358,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             v2f d[4];
             float G[4], araw[4], alpha[4];
             bool ok[4];
-            bool any = false;
+            [[maybe_unused]] bool any = false;  // (step statistics only)
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const float4 a = s_a[gq.j[k]], b = s_b[gq.j[k]];
@@ -398,7 +398,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 }
             }
 #endif
-            if (__ballot(any) == 0ull) continue;  // slots stay zero
+            // (no wave-uniform skip of steps without a contributing pair: 0.04 % of steps, and the test
+            // cost 2 VALU + a branch per step; config-4 dual 396 -> 387 us without it)
             // serial part (in list order): T and A, then dL/dalpha and dchannel/dcolor
             float dLa[4], dch[4];
 #pragma unroll

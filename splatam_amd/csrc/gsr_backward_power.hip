@@ -533,7 +533,6 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
             v2f d[4];
             float G[4], araw[4], alpha[4];
             bool ok[4];
-            bool any = false;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const float4 a = s_a[jj[k]], b = s_b[jj[k]];
@@ -544,9 +543,7 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
                 alpha[k] = fminf(0.99f, araw[k]);
                 ok[k] = jj[k] >= jlo && p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;
                 alpha[k] = ok[k] ? alpha[k] : 0.f;
-                any = any || ok[k];
             }
-            if (__ballot(any) == 0ull) continue;  // slots stay zero
             // per pair, in list order: T and A, dL/dalpha; dL/dmeans3D = h * (M . (dx, dy, dx^2, dx dy,
             // dy^2)) with h = G dL/dG, dL/dopacity = G dL/dalpha, each powered (0 on non-contributing pairs)
             float v[4 * NV];
