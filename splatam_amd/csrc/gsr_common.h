@@ -17,7 +17,10 @@ namespace gsr {
 constexpr int TILE_X = 16;  // config.h:16-17 (BLOCK_X/BLOCK_Y); parity needs 16x16 tiles
 constexpr int TILE_Y = 16;
 constexpr int TILE_PIX = TILE_X * TILE_Y;
-constexpr int PRE_BLOCK = 1024;      // Gaussians per preprocess / duplicate workgroup (one count-matrix row)
+#ifndef GSR_PRE_BLOCK
+#define GSR_PRE_BLOCK 1024
+#endif
+constexpr int PRE_BLOCK = GSR_PRE_BLOCK;  // Gaussians per preprocess / duplicate workgroup (one count-matrix row)
 constexpr int MAX_LDS_TILES = 16384; // tile histogram in LDS up to 64 KB; global atomics beyond
 constexpr int SORT_THREADS = 256;
 constexpr int SORT_ITEMS = 8;        // keys per thread per radix pass

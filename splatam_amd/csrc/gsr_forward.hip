@@ -536,7 +536,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // same work (max/mean 1.07 on config 3).  Counting sort over length buckets of 4:
 // ties land in arbitrary order, which changes only which workgroup renders a tile,
 // never its results.
-constexpr int PLAN_BUCKETS = PRE_BLOCK, PLAN_SHIFT = 2;
+constexpr int PLAN_BUCKETS = 1024, PLAN_SHIFT = 2;
 __device__ __forceinline__ uint32_t plan_bucket(uint32_t len) {  // descending length -> ascending bucket
     return (uint32_t)(PLAN_BUCKETS - 1) - min(len >> PLAN_SHIFT, (uint32_t)(PLAN_BUCKETS - 1));
 }
@@ -613,7 +613,7 @@ hipError_t launch_identity_order(uint32_t* order, int ntiles, hipStream_t s) {
 // workgroups took two dispatch rounds on 37 CUs; at 512 two workgroups share a CU (one round).
 // Forcing 1024-lane workgroups to 64 VGPRs instead spilled and was slower.
 #ifndef GSR_DUP_THREADS
-#define GSR_DUP_THREADS 512
+#define GSR_DUP_THREADS (GSR_PRE_BLOCK < 512 ? GSR_PRE_BLOCK : 512)
 #endif
 constexpr int DUP_T = GSR_DUP_THREADS, DUP_G = PRE_BLOCK / DUP_T;
 static_assert(DUP_G * DUP_T == PRE_BLOCK && DUP_T % 64 == 0, "duplicate workgroup shape");
