@@ -251,7 +251,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {
         const uint32_t gk = pe_id(point_list[k]);
         const RenderRec r = load_rr(rr, gk);
-        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), tx, ty);
+        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk, cam.pre_shift), tx, ty);
         float2* dst = reinterpret_cast<float2*>(inst + (size_t)RS * u);
 #pragma unroll
         for (int m = 0; m < RS / 2; m++) dst[m] = make_float2(0.f, 0.f);
@@ -295,7 +295,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             const uint32_t gi = pe_id(pn);
             pm = pe_mask(pn);
             const RenderRec r = load_rr(rr, gi);
-            pbs = blocksums[gi / PRE_BLOCK];
+            pbs = blocksums[gi >> cam.pre_shift];
             pa = r.q0; pb = r.q1; pc = r.q2;
             if (DUAL && !PACKC) {
                 pd = r.q3;

@@ -140,7 +140,7 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
     for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {
         const uint32_t gk = pe_id(point_list[k]);
         const RenderRec r = load_rr(rr, gk);
-        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), tx, ty);
+        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk, cam.pre_shift), tx, ty);
 #pragma unroll
         for (int m = 0; m < NVP / 4; m++) rec[(size_t)u * (NVP / 4) + m] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -158,7 +158,7 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
             const RenderRec r = load_rr(rr, gi);
             const float4 pa = r.q0, pb = r.q1;
             s_g[tid] = gi;
-            s_u[tid] = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi), tx, ty);
+            s_u[tid] = instance_slot(rr_rect(r), rr_offset(r, blocksums, gi, cam.pre_shift), tx, ty);
             s_a[tid] = pa;
             s_b[tid] = pb;
             s_c[tid] = make_float4(r.q2.x, r.q2.y, r.q2.z, __uint_as_float(clamp_bits[gi]));
@@ -437,7 +437,7 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
     for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {  // behind every last contributor
         const uint32_t gk = pe_id(point_list[k]);
         const RenderRec r = load_rr(rr, gk);
-        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk), tx, ty);
+        const uint32_t u = instance_slot(rr_rect(r), rr_offset(r, blocksums, gk, cam.pre_shift), tx, ty);
         reinterpret_cast<float4*>(inst)[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     // background term of dL/dalpha (backward.cu:1014): -T_final / (1 - alpha) * (bg . dL/dpix)
@@ -469,7 +469,7 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
             const uint32_t gi = pe_id(pn);
             pmask = pe_mask(pn);
             const RenderRec r = load_rr(rr, gi);
-            pbs = blocksums[gi / PRE_BLOCK];
+            pbs = blocksums[gi >> cam.pre_shift];
             pa = r.q0; pb = r.q1; pc = r.q2;
             prh = __float_as_uint(r.q3.w);
             pgi = gi;

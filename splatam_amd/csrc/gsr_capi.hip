@@ -278,6 +278,10 @@ void timing_drain(Timing& T) {  // caller holds g_timing_mu
 
 }  // namespace
 
+namespace gsr {
+int geom_pre_shift(int P) { return pre_shift_for(P, device_cus(current_device())); }
+}  // namespace gsr
+
 extern "C" {
 
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
@@ -312,6 +316,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     if (xf) g.xf = *xf;   // tracking transform fused into preprocess (g's arrays are then its outputs)
     const int P = g.P, W = cam.W, H = cam.H;
     const GeomLayout GL = GeomLayout::make(P);
+    cam.pre_shift = GL.shift;
     const ImgLayout IL = ImgLayout::make(W, H);
     void* geom = obtain(alloc, alloc_ctx, GSR_BUF_GEOM, GL.total);
     void* img = obtain(alloc, alloc_ctx, GSR_BUF_IMAGE, IL.total);
@@ -535,6 +540,7 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     // the forward's render schedule (a permutation of the tiles; any order gives the same results)
     cam.tile_order = (const uint32_t*)((const char*)image_buffer + ImgLayout::make(cam.W, cam.H).order);
     const GeomLayout GL = GeomLayout::make(P);
+    cam.pre_shift = GL.shift;
     const ImgLayout IL = ImgLayout::make(cam.W, cam.H);
     const BinLayout BL = BinLayout::make(num_rendered, cam.W, cam.H);
     const GeomPtrs geo = GeomPtrs::at(const_cast<void*>(geom_buffer), GL);
@@ -840,6 +846,7 @@ int gsr_forward_reuse(const gsr_settings* settings, const gsr_gaussians* gaussia
     const GaussIn g = make_gauss(gaussians);
     const int P = g.P;
     const GeomLayout GL = GeomLayout::make(P);
+    cam.pre_shift = GL.shift;
     const ImgLayout IL = ImgLayout::make(cam.W, cam.H);
     void* geom = obtain(alloc, alloc_ctx, GSR_BUF_GEOM, GL.total);
     if (!geom) return fail(GSR_ERR_ALLOC, "allocator returned NULL (geom buffer)");

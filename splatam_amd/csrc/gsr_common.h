@@ -17,10 +17,14 @@ namespace gsr {
 constexpr int TILE_X = 16;  // config.h:16-17 (BLOCK_X/BLOCK_Y); parity needs 16x16 tiles
 constexpr int TILE_Y = 16;
 constexpr int TILE_PIX = TILE_X * TILE_Y;
-#ifndef GSR_PRE_BLOCK
-#define GSR_PRE_BLOCK 1024
-#endif
-constexpr int PRE_BLOCK = GSR_PRE_BLOCK;  // Gaussians per preprocess / duplicate workgroup (one count-matrix row)
+// Count-matrix rows (one preprocess / duplicate workgroup each): 1024 Gaussians, or 512 when rows of 1024
+// would put fewer than two on every CU -- config 3's 293 rows on 256 CUs left 37 CUs with two workgroups'
+// work (tracking preprocess 20.3 -> 16.7 us with 586 rows of 512); config 4's 977 rows stay at 1024 (its
+// count matrix would double: column scan 16 -> 31 us).  The choice is a pure function of (P, CU count):
+// GeomLayout::make and every kernel read it as a shift (Camera::pre_shift).
+constexpr int PRE_BLOCK = 1024;  // the largest row (workgroup size bound, LDS arrays)
+__host__ __device__ inline int pre_shift_for(int P, int cus) { return ((P + 1023) >> 10) < 2 * cus ? 9 : 10; }
+int geom_pre_shift(int P);  // pre_shift_for(P, CU count of the current device) (gsr_capi.hip)
 constexpr int MAX_LDS_TILES = 16384; // tile histogram in LDS up to 64 KB; global atomics beyond
 constexpr int SORT_THREADS = 256;
 constexpr int SORT_ITEMS = 8;        // keys per thread per radix pass
@@ -52,11 +56,14 @@ struct GeomLayout {       // per-Gaussian state ("geomBuffer")
     size_t counters;      // u32    [8]  [0]=num_rendered [1]=prefiltered violation [2]=longest tile list
                           //             [3]=sort cap [4]=colscan arrival counter
     size_t total;
-    int nb;
-    static GeomLayout make(int P) {
+    int nb;     // count-matrix rows
+    int shift;  // log2 Gaussians per row
+    static GeomLayout make(int P) { return make(P, geom_pre_shift(P)); }
+    static GeomLayout make(int P, int shift) {
         GeomLayout L;
         size_t o = 0, p = (size_t)(P > 0 ? P : 1);
-        L.nb = (P + PRE_BLOCK - 1) / PRE_BLOCK;
+        L.shift = shift;
+        L.nb = (P + (1 << shift) - 1) >> shift;
         L.rr = o; o = align_up(o + 16 * RR_F4 * p, 256);
         L.clamp = o; o = align_up(o + 4 * p, 256);
         L.bin = o; o = align_up(o + 16 * p, 256);
@@ -149,6 +156,7 @@ struct Camera {
     const uint32_t* tile_order = nullptr;
     uint32_t* tile_order_out = nullptr;
     int sched_cus = 256;
+    int pre_shift = 10;  // log2 Gaussians per count-matrix row (GeomLayout::shift)
 };
 // Wave priority by remaining work (GSR_PRIO_SCHED): the instruction arbiter favours older
 // waves, so on a CU the last-dispatched tile used to run alone at the end at one wave per
@@ -236,8 +244,8 @@ __device__ __forceinline__ uint2 rr_rect(const RenderRec& r) {
     return make_uint2(__float_as_uint(r.q2.w), __float_as_uint(r.q3.w));
 }
 // instance offset of Gaussian i: scanned workgroup base + workgroup-local part (q1.w)
-__device__ __forceinline__ uint32_t rr_offset(const RenderRec& r, const uint32_t* blocksums, uint32_t i) {
-    return blocksums[i / PRE_BLOCK] + __float_as_uint(r.q1.w);
+__device__ __forceinline__ uint32_t rr_offset(const RenderRec& r, const uint32_t* blocksums, uint32_t i, int shift) {
+    return blocksums[i >> shift] + __float_as_uint(r.q1.w);
 }
 
 // ------------------------------------------------------------ device math --

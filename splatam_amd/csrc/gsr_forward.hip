@@ -31,7 +31,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
 #pragma clang fp contract(off)
     extern __shared__ uint32_t s_hist[];
     __shared__ float s_pose[16];  // XF: the frame's pose (R 9, t 3, F.normalize(q) 4), formed once by wave 0
-    const int i = blockIdx.x * PRE_BLOCK + threadIdx.x;
+    const int i = (blockIdx.x << cam.pre_shift) + threadIdx.x;  // blockDim.x = 1 << pre_shift
     XfRaw xr{};  // XF: the Gaussian's transform inputs, in flight while wave 0 forms the pose
     if (XF && i < g.P) xr = track_xform_load(g.xf, i, true);
     // the per-Gaussian inputs used only once the rect is known (colour, opacity, second colour set)
@@ -62,7 +62,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
         }
     }
     if (LDS_HIST)
-        for (int t = threadIdx.x; t < ntiles; t += PRE_BLOCK) s_hist[t] = 0u;
+        for (int t = threadIdx.x; t < ntiles; t += blockDim.x) s_hist[t] = 0u;
     if (LDS_HIST || XF) __syncthreads();
     if (i == 0) geo.counters[4] = 0u;  // tile_colscan_kernel's arrival counter (next launch)
     uint32_t tiles = 0;
@@ -168,7 +168,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
         }
     }
     // workgroup scan of tiles touched: the local instance offset goes into the render
-    // record (q1.w; the render kernels add the scanned workgroup base, blocksums[i >> 10]),
+    // record (q1.w; the render kernels add the scanned workgroup base, blocksums[i >> pre_shift]),
     // the workgroup total into wgsum (input of the two-level scan)
     __shared__ uint32_t wsum[PRE_BLOCK / 64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -189,9 +189,9 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     }
     // top bit: prefiltered violation anywhere in the workgroup (folded into counters[1] by the scan)
     const bool viol = __syncthreads_or(violation);
-    if (threadIdx.x == PRE_BLOCK - 1) geo.wgsum[blockIdx.x] = (woff + incl) | (viol ? 0x80000000u : 0u);
+    if (threadIdx.x == blockDim.x - 1) geo.wgsum[blockIdx.x] = (woff + incl) | (viol ? 0x80000000u : 0u);
     if (LDS_HIST)
-        for (int t = threadIdx.x; t < ntiles; t += PRE_BLOCK) counts[(size_t)blockIdx.x * ntiles + t] = s_hist[t];
+        for (int t = threadIdx.x; t < ntiles; t += blockDim.x) counts[(size_t)blockIdx.x * ntiles + t] = s_hist[t];
 }
 
 hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* counts,
@@ -200,8 +200,8 @@ hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, 
     const bool xf = g.xf.mw != nullptr;
     auto k = lds_hist ? (xf ? preprocess_kernel<true, true> : preprocess_kernel<true, false>)
                       : (xf ? preprocess_kernel<false, true> : preprocess_kernel<false, false>);
-    hipLaunchKernelGGL(k, dim3(nb), dim3(PRE_BLOCK), lds_hist ? sizeof(uint32_t) * ntiles : 0, s, cam, g, geo, radii,
-                       counts, ntiles);
+    hipLaunchKernelGGL(k, dim3(nb), dim3(1 << cam.pre_shift), lds_hist ? sizeof(uint32_t) * ntiles : 0, s, cam, g,
+                       geo, radii, counts, ntiles);
     return hipGetLastError();
 }
 
@@ -215,7 +215,10 @@ hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, 
 // Two shapes: 16 tiles x 64 parts (64-B row segments) for count matrices of <= 512 rows, 32 x 32
 // (128-B segments, <= 32 rows per thread) above: 5.2 vs 5.8 us at config 3 (293 rows), 19.1 vs
 // 16.2 us at config 4 (977 rows).
-constexpr int CS_THREADS = 1024, CS_ROWS_SMALL = 512;
+#ifndef GSR_CS_ROWS_SMALL
+#define GSR_CS_ROWS_SMALL 640  // (config 3 has 586 rows of 512 Gaussians)
+#endif
+constexpr int CS_THREADS = 1024, CS_ROWS_SMALL = GSR_CS_ROWS_SMALL;
 template <int CT>
 struct ColscanShape {
     static constexpr int TILES = CT, PARTS = CS_THREADS / CT, RQ = PARTS == 64 ? 16 : 32;
@@ -461,8 +464,8 @@ duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, u
     __shared__ uint32_t s_incl[PRE_BLOCK];   // inclusive scan of tiles touched
     __shared__ uint32_t s_x0[PRE_BLOCK], s_y0[PRE_BLOCK], s_w[PRE_BLOCK], s_depth[PRE_BLOCK];
     __shared__ uint32_t wsum[PRE_BLOCK / 64];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int i = blockIdx.x * PRE_BLOCK + tid;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, R = (int)blockDim.x;  // R = 1 << pre_shift
+    const int i = (blockIdx.x << cam.pre_shift) + tid;
     uint32_t t = (i < P) ? geo.tiles[i] : 0u;
     uint32_t incl = wave_incl_scan(t);
     if (lane == 63) wsum[w] = incl;
@@ -481,10 +484,10 @@ duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, u
     const uint32_t base = geo.blocksums[blockIdx.x];  // exclusive scan of workgroup totals
     if (i < P) geo.offsets[i] = base + incl - t;
     __syncthreads();
-    const uint32_t total = s_incl[PRE_BLOCK - 1];
-    for (uint32_t e = tid; e < total; e += PRE_BLOCK) {
+    const uint32_t total = s_incl[R - 1];
+    for (uint32_t e = tid; e < total; e += R) {
         // owner j: first Gaussian whose inclusive sum exceeds e
-        int lo = 0, hi = PRE_BLOCK - 1;
+        int lo = 0, hi = R - 1;
         while (lo < hi) {
             int mid = (lo + hi) >> 1;
             if (s_incl[mid] > e) hi = mid; else lo = mid + 1;
@@ -495,7 +498,7 @@ duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, u
         const uint32_t ty = s_y0[lo] + local / wdt;
         const uint32_t tx = s_x0[lo] + local % wdt;
         const uint32_t u = base + e;
-        const uint32_t gi = blockIdx.x * PRE_BLOCK + lo;
+        const uint32_t gi = (blockIdx.x << cam.pre_shift) + lo;
         keys[u] = ((uint64_t)(ty * (uint32_t)cam.gx + tx) << 32) | (uint64_t)s_depth[lo];
         gid[u] = gi;
     }
@@ -504,7 +507,7 @@ duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, u
 hipError_t launch_duplicate(const Camera& cam, int P, GeomPtrs geo, uint64_t* keys, uint32_t* gid,
                             int nb, hipStream_t s) {
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(duplicate_kernel, dim3(nb), dim3(PRE_BLOCK), 0, s, cam, P, geo, keys, gid);
+    hipLaunchKernelGGL(duplicate_kernel, dim3(nb), dim3(1 << cam.pre_shift), 0, s, cam, P, geo, keys, gid);
     return hipGetLastError();
 }
 
@@ -608,34 +611,31 @@ hipError_t launch_identity_order(uint32_t* order, int ntiles, hipStream_t s) {
     return hipGetLastError();
 }
 
-// DUP_T lanes per workgroup, each placing the instances of DUP_G consecutive Gaussians of a
-// preprocess workgroup's PRE_BLOCK: at 1024 lanes (98 VGPRs, one workgroup per CU) a frame's ~300
-// workgroups took two dispatch rounds on 37 CUs; at 512 two workgroups share a CU (one round).
-// Forcing 1024-lane workgroups to 64 VGPRs instead spilled and was slower.
-#ifndef GSR_DUP_THREADS
-#define GSR_DUP_THREADS (GSR_PRE_BLOCK < 512 ? GSR_PRE_BLOCK : 512)
-#endif
-constexpr int DUP_T = GSR_DUP_THREADS, DUP_G = PRE_BLOCK / DUP_T;
-static_assert(DUP_G * DUP_T == PRE_BLOCK && DUP_T % 64 == 0, "duplicate workgroup shape");
+// DUP_T lanes per workgroup, each placing the instances of DUP_G consecutive Gaussians of a count-matrix
+// row (DUP_G = 2 for rows of 1024, 1 for rows of 512): at 1024 lanes (98 VGPRs, one workgroup per CU) a
+// frame's ~300 workgroups took two dispatch rounds on 37 CUs; at 512 two workgroups share a CU (one
+// round).  Forcing 1024-lane workgroups to 64 VGPRs instead spilled and was slower.
+constexpr int DUP_T = 512;
 #ifndef GSR_L1_CH
 #define GSR_L1_CH 8  // tracking-loss epilogue: partials in flight per round trip of the last workgroup
 #endif
 #ifndef GSR_NO_PLAN
 #define GSR_NO_PLAN 0  // timing experiment: row-major render order instead of tile_plan
 #endif
-template <bool LDS_HIST>
+template <bool LDS_HIST, int DUP_G>
 __global__ void __launch_bounds__(DUP_T)
 duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges, const uint32_t* __restrict__ tot,
                         uint32_t* __restrict__ cursor, int ntiles, uint64_t* __restrict__ keys,
                         SpecGuard guard, uint32_t sort_cap, uint32_t* __restrict__ status) {
     // LDS_HIST: cursor = the column-scanned count matrix; this workgroup's
     // instances of tile t go to start[t] + cursor[block][t] + (LDS rank)
+    constexpr int ROW = DUP_G * DUP_T;  // Gaussians per count-matrix row (1 << cam.pre_shift)
     extern __shared__ uint32_t s_cur[];
-    __shared__ uint32_t s_incl[PRE_BLOCK];
-    __shared__ uint32_t s_x0[PRE_BLOCK], s_y0[PRE_BLOCK], s_w[PRE_BLOCK], s_depth[PRE_BLOCK];
+    __shared__ uint32_t s_incl[ROW];
+    __shared__ uint32_t s_x0[ROW], s_y0[ROW], s_w[ROW], s_depth[ROW];
     __shared__ uint32_t wsum[DUP_T / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int i0 = blockIdx.x * PRE_BLOCK + DUP_G * tid;  // this lane's Gaussians i0 .. i0 + DUP_G - 1
+    const int i0 = blockIdx.x * ROW + DUP_G * tid;  // this lane's Gaussians i0 .. i0 + DUP_G - 1
     // the Gaussians' tile counts and rects, loaded ahead of the prologue's loads (one round trip)
     uint32_t t[DUP_G];
     uint4 r[DUP_G];
@@ -779,9 +779,9 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         s_incl[DUP_G * tid + g] = run;
     }
     __syncthreads();
-    const uint32_t total = s_incl[PRE_BLOCK - 1];
+    const uint32_t total = s_incl[ROW - 1];
     for (uint32_t e = tid; e < total; e += DUP_T) {
-        int lo = 0, hi = PRE_BLOCK - 1;
+        int lo = 0, hi = ROW - 1;
         while (lo < hi) {
             int mid = (lo + hi) >> 1;
             if (s_incl[mid] > e) hi = mid; else lo = mid + 1;
@@ -791,7 +791,7 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         const uint32_t tile = (s_y0[lo] + local / wdt) * (uint32_t)cam.gx + s_x0[lo] + local % wdt;
         const uint32_t pos = LDS_HIST ? atomicAdd(&s_cur[tile], 1u)
                                       : ranges[tile].x + atomicAdd(&cursor[tile * TILE_CTR_STRIDE], 1u);
-        const uint32_t gi = blockIdx.x * PRE_BLOCK + lo;
+        const uint32_t gi = blockIdx.x * ROW + lo;
         keys[pos] = ((uint64_t)s_depth[lo] << 32) | (uint64_t)gi;
     }
 }
@@ -800,12 +800,11 @@ hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2
                                    uint32_t* cursor, bool lds_hist, int ntiles, uint64_t* keys, int nb,
                                    SpecGuard guard, uint32_t* status, hipStream_t s) {
     if (nb == 0) return hipSuccess;
-    if (lds_hist)
-        hipLaunchKernelGGL(duplicate_bucket_kernel<true>, dim3(nb), dim3(DUP_T), sizeof(uint32_t) * ntiles, s, cam,
-                           P, geo, ranges, tot, cursor, ntiles, keys, guard, (uint32_t)TILE_SORT_CAP, status);
-    else
-        hipLaunchKernelGGL(duplicate_bucket_kernel<false>, dim3(nb), dim3(DUP_T), 0, s, cam, P, geo, ranges, tot,
-                           cursor, ntiles, keys, guard, (uint32_t)TILE_SORT_CAP, status);
+    const bool g2 = cam.pre_shift == 10;  // rows of 1024: two Gaussians per lane; of 512: one
+    auto k = lds_hist ? (g2 ? duplicate_bucket_kernel<true, 2> : duplicate_bucket_kernel<true, 1>)
+                      : (g2 ? duplicate_bucket_kernel<false, 2> : duplicate_bucket_kernel<false, 1>);
+    hipLaunchKernelGGL(k, dim3(nb), dim3(DUP_T), lds_hist ? sizeof(uint32_t) * ntiles : 0, s, cam, P, geo, ranges,
+                       tot, cursor, ntiles, keys, guard, (uint32_t)TILE_SORT_CAP, status);
     return hipGetLastError();
 }
 
