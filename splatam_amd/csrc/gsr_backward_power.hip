@@ -389,8 +389,14 @@ gauss_mpack_kernel(Camera cam, GaussIn g, const int* __restrict__ radii, float4*
 template <bool POW2>
 __device__ __forceinline__ float pow_sel(float x, float p) { return POW2 ? x * x : powf(x, p); }
 
+#ifndef GSR_FISHER_WAVES
+#define GSR_FISHER_WAVES 4  // 128 VGPRs: room for a step's records and the next entry's M rows in flight
+#endif
+#ifndef GSR_FISHER_PF
+#define GSR_FISHER_PF 1  // a step's geometry / colour records loaded up front, the next entry's M rows a pair ahead
+#endif
 template <bool POW2>
-__global__ void __launch_bounds__(TILE_PIX, 5)
+__global__ void __launch_bounds__(TILE_PIX, GSR_FISHER_WAVES)
 render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ ranges,
                          const PointEntry* __restrict__ point_list, const float4* __restrict__ rr,
                          const uint32_t* __restrict__ blocksums, const float4* __restrict__ mp,
@@ -533,9 +539,23 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
             v2f d[4];
             float G[4], araw[4], alpha[4];
             bool ok[4];
+#if GSR_FISHER_PF
+            // one LDS round trip for the step's four geometry records (the compiler otherwise waits on each
+            // entry's reads in turn: the kernel was LDS-latency-bound, SQ_WAIT_ANY 59 % of wave cycles)
+            float4 ra[4], rb[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
+                ra[k] = s_a[jj[k]];
+                rb[k] = s_b[jj[k]];
+            }
+#endif
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+#if GSR_FISHER_PF
+                const float4 a = ra[k], b = rb[k];
+#else
                 const float4 a = s_a[jj[k]], b = s_b[jj[k]];
+#endif
                 d[k] = pix_delta(a, pix);
                 const float p2 = eval_p2(a, b, d[k]);
                 G[k] = __builtin_amdgcn_exp2f(fminf(p2, 0.f));
@@ -547,9 +567,27 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
             // per pair, in list order: T and A, dL/dalpha; dL/dmeans3D = h * (M . (dx, dy, dx^2, dx dy,
             // dy^2)) with h = G dL/dG, dL/dopacity = G dL/dalpha, each powered (0 on non-contributing pairs)
             float v[4 * NV];
+#if GSR_FISHER_PF
+            float4 rc[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) rc[k] = s_c[jj[k]];
+            float4 nm0 = s_m[MPACK_F4 * jj[0]], nm1 = s_m[MPACK_F4 * jj[0] + 1];
+            float4 nm2 = s_m[MPACK_F4 * jj[0] + 2], nm3 = s_m[MPACK_F4 * jj[0] + 3];
+#endif
 #pragma unroll
             for (int k = 0; k < 4; k++) {
+#if GSR_FISHER_PF
+                const float4 c = rc[k];
+                const float4 m0 = nm0, m1 = nm1, m2 = nm2, m3 = nm3;
+                if (k < 3) {  // the next entry's M rows, in flight while this entry's values are formed
+                    nm0 = s_m[MPACK_F4 * jj[k + 1]];
+                    nm1 = s_m[MPACK_F4 * jj[k + 1] + 1];
+                    nm2 = s_m[MPACK_F4 * jj[k + 1] + 2];
+                    nm3 = s_m[MPACK_F4 * jj[k + 1] + 3];
+                }
+#else
                 const float4 c = s_c[jj[k]];
+#endif
                 const v2f t = v2f{c.x, c.y} * dp01;
                 const float cd = __builtin_fmaf(c.z, dp2, t.x + t.y);
                 const float inv = __builtin_amdgcn_rcpf(1.f - alpha[k]);
@@ -559,8 +597,10 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
                 const float dLa = o ? __builtin_fmaf(Tbg, inv, e * Tn) : 0.f;
                 T = Tn;  // masked pairs: alpha = 0, v_rcp_f32(1) == 1 exactly
                 A = __builtin_fmaf(alpha[k], e, A);
+#if !GSR_FISHER_PF
                 const float4 m0 = s_m[MPACK_F4 * jj[k]], m1 = s_m[MPACK_F4 * jj[k] + 1];
                 const float4 m2 = s_m[MPACK_F4 * jj[k] + 2], m3 = s_m[MPACK_F4 * jj[k] + 3];
+#endif
                 const float dx = d[k].x, dy = d[k].y;
                 const float xx = dx * dx, xy = dx * dy, yy = dy * dy;
                 const float h = araw[k] * dLa;

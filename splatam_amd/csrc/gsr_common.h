@@ -991,31 +991,31 @@ __device__ __forceinline__ void row_tstep(const float* c, float* out, bool hi) {
 // {0,1} <-> {2,3}; row_half_mirror: banks {0,2} <-> {1,3}): two v_add_f32_dpp whose
 // bank masks write complementary lane halves -- lanes of the low half add the pair's c[i],
 // lanes of the high half c[i + N/2] -- instead of two selects and one DPP add per value.
-// One asm block per step: its leading s_nop 1 covers the VALU-write -> DPP-read hazard of
-// every input (the compiler does not see the DPP inside).  Requires full EXEC.
-#define GSR_DPP_PAIR(CTRL_STR, MLO, MHI)                                                                 \
-    "v_add_f32_dpp %0, %" #MLO ", %" #MLO " " CTRL_STR " row_mask:0xf bank_mask:0x3\n\t"
+// Each pair is its own asm block and starts with s_nop 1: the VALU-write -> DPP-read hazard of its
+// inputs needs 2 wait states, and the compiler, which does not see the DPP inside, may schedule the
+// VALU that writes an input right before any of the blocks (a single s_nop ahead of the first block
+// once let a select land between two blocks and the DPP read the stale register: the Fisher kernel's
+// opacity column at 4 waves/SIMD).  Requires full EXEC.
 template <int N>
 __device__ __forceinline__ void row_tstep_ror8(const float* c, float* out) {
     static_assert(N % 2 == 0, "even value count");
-    asm volatile("s_nop 1" ::: "memory");
 #pragma unroll
     for (int i = 0; i < N / 2; i++)
-        asm volatile("v_add_f32_dpp %0, %1, %1 row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
+        asm volatile("s_nop 1\n\t"
+                     "v_add_f32_dpp %0, %1, %1 row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
                      "v_add_f32_dpp %0, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xc"
                      : "=&v"(out[i]) : "v"(c[i]), "v"(c[i + N / 2]));
 }
 template <int N>
 __device__ __forceinline__ void row_tstep_mirror(const float* c, float* out) {
     static_assert(N % 2 == 0, "even value count");
-    asm volatile("s_nop 1" ::: "memory");
 #pragma unroll
     for (int i = 0; i < N / 2; i++)
-        asm volatile("v_add_f32_dpp %0, %1, %1 row_half_mirror row_mask:0xf bank_mask:0x5\n\t"
+        asm volatile("s_nop 1\n\t"
+                     "v_add_f32_dpp %0, %1, %1 row_half_mirror row_mask:0xf bank_mask:0x5\n\t"
                      "v_add_f32_dpp %0, %2, %2 row_half_mirror row_mask:0xf bank_mask:0xa"
                      : "=&v"(out[i]) : "v"(c[i]), "v"(c[i + N / 2]));
 }
-#undef GSR_DPP_PAIR
 
 // r[i] = row total of value (entry row_entry(lane), m = row_m0<NV>(lane) + i)
 template <int NV>
