@@ -616,6 +616,9 @@ hipError_t launch_identity_order(uint32_t* order, int ntiles, hipStream_t s) {
 // frame's ~300 workgroups took two dispatch rounds on 37 CUs; at 512 two workgroups share a CU (one
 // round).  Forcing 1024-lane workgroups to 64 VGPRs instead spilled and was slower.
 constexpr int DUP_T = 512;
+#ifndef GSR_DUP_LOOP_MAX
+#define GSR_DUP_LOOP_MAX 8  // rows whose Gaussians touch at most this many tiles place instances per lane
+#endif
 #ifndef GSR_L1_CH
 #define GSR_L1_CH 8  // tracking-loss epilogue: partials in flight per round trip of the last workgroup
 #endif
@@ -633,7 +636,7 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
     extern __shared__ uint32_t s_cur[];
     __shared__ uint32_t s_incl[ROW];
     __shared__ uint32_t s_x0[ROW], s_y0[ROW], s_w[ROW], s_depth[ROW];
-    __shared__ uint32_t wsum[DUP_T / 64];
+    __shared__ uint32_t wsum[DUP_T / 64], s_tmax[DUP_T / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int i0 = blockIdx.x * ROW + DUP_G * tid;  // this lane's Gaussians i0 .. i0 + DUP_G - 1
     // the Gaussians' tile counts and rects, loaded ahead of the prologue's loads (one round trip)
@@ -754,10 +757,11 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         if (guard.overflow()) return;
         base = geo.blocksums[blockIdx.x];
     }
-    uint32_t tsum = 0;
+    uint32_t tsum = 0, tmax = 0;
 #pragma unroll
     for (int g = 0; g < DUP_G; g++) {
         tsum += t[g];
+        tmax = max(tmax, t[g]);
         const int q = DUP_G * tid + g;
         if (t[g]) {
             s_x0[q] = r[g].x & 0xFFFFu;
@@ -767,16 +771,38 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         }
     }
     uint32_t incl = wave_incl_scan(tsum);
+    tmax = wave_max_u32(tmax);
     __syncthreads();  // (wsum is also tile_plan's scratch)
     if (lane == 63) wsum[w] = incl;
+    if (lane == 0) s_tmax[w] = tmax;
     __syncthreads();
     uint32_t run = incl - tsum;
     for (int k = 0; k < w; k++) run += wsum[k];
+#pragma unroll
+    for (int k = 0; k < DUP_T / 64; k++) tmax = max(tmax, s_tmax[k]);
 #pragma unroll
     for (int g = 0; g < DUP_G; g++) {  // Gaussian order: the workgroup-local instance offsets of preprocess
         if (i0 + g < P) geo.offsets[i0 + g] = base + run;
         run += t[g];
         s_incl[DUP_G * tid + g] = run;
+    }
+    if (tmax <= (uint32_t)GSR_DUP_LOOP_MAX) {
+        // few tiles per Gaussian in this row (config 3: at most 4): every lane places its own Gaussians'
+        // instances (<= GSR_DUP_LOOP_MAX loop trips) instead of one binary search over the row's
+        // inclusive sums per instance; the slots within a tile bucket still come from the LDS cursors
+        // (the bucket order is the sort's input, any order)
+#pragma unroll
+        for (int g = 0; g < DUP_G; g++) {
+            const uint32_t x0 = r[g].x & 0xFFFFu, y0 = r[g].x >> 16, wdt = (r[g].y & 0xFFFFu) - x0;
+            const uint32_t gi = (uint32_t)(i0 + g);
+            for (uint32_t k = 0; k < t[g]; k++) {
+                const uint32_t tile = (y0 + k / wdt) * (uint32_t)cam.gx + x0 + k % wdt;
+                const uint32_t pos = LDS_HIST ? atomicAdd(&s_cur[tile], 1u)
+                                              : ranges[tile].x + atomicAdd(&cursor[tile * TILE_CTR_STRIDE], 1u);
+                keys[pos] = ((uint64_t)r[g].z << 32) | (uint64_t)gi;
+            }
+        }
+        return;
     }
     __syncthreads();
     const uint32_t total = s_incl[ROW - 1];
