@@ -788,7 +788,7 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
     }
     if (tmax <= (uint32_t)GSR_DUP_LOOP_MAX) {
         // few tiles per Gaussian in this row (config 3: at most 4; mapping duplicate 50.4 -> 48.1 us at 16 or
-        // 64, tracking 13.4 -> 11.9 at 8): every lane places its own Gaussians
+        // 64, tracking 13.4 -> 11.9 at 8): every lane places its own Gaussians'
         // instances (<= GSR_DUP_LOOP_MAX loop trips) instead of one binary search over the row's
         // inclusive sums per instance; the slots within a tile bucket still come from the LDS cursors
         // (the bucket order is the sort's input, any order)
