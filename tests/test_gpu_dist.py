@@ -31,3 +31,38 @@ def test_bench_two_ranks(cuda):
     # value = frames of both ranks / max-over-ranks wall time
     assert abs(b["value"] - 2 * 40 / (b["ms_per_step"] * 40 / 1e3)) <= 0.01 * b["value"]
     assert b["roofline"]["launches_timed"] == 40 and b["roofline"]["avg_us"] > 0
+
+
+_RCCL_SCRIPT = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+from splatam_amd import dist as sd
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", device_id=torch.device("cuda", 0))  # bench.py's call (RCCL)
+p = {"means3D": torch.arange(12., device="cuda").reshape(4, 3), "rgb_colors": torch.ones(4, 3, device="cuda")}
+n = sd.broadcast_map(p, keys=("means3D", "rgb_colors"))
+for k in ("means3D", "rgb_colors"):  # the collectives the helpers issue when world > 1, issued directly
+    dist.broadcast(p[k].data, src=0)
+dist.barrier()
+t = torch.full((3,), 2.0, device="cuda")
+dist.all_reduce(t, op=dist.ReduceOp.SUM)
+x = torch.tensor([0.25], dtype=torch.float64, device="cuda")
+dist.all_reduce(x, op=dist.ReduceOp.MAX)
+m = sd.max_over_ranks(float(x), device=torch.device("cuda", 0))
+print("RCCL", dist.get_backend(), dist.get_world_size(), n, t.tolist(), m, float(p["means3D"].sum()))
+dist.destroy_process_group()
+"""
+
+
+def test_rccl_single_rank(cuda):
+    """bench.py's RCCL calls (init_process_group("nccl", device_id), map broadcast, barrier, all-reduce,
+    max over ranks) on this box's one GPU with one rank: the nccl backend is RCCL on ROCm, and this is the
+    code path the driver's multi-GPU runs take (two ranks cannot share one device under RCCL)."""
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT="29531")
+    r = subprocess.run([sys.executable, "-c", _RCCL_SCRIPT, ROOT], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("RCCL")][-1]
+    print(line)
+    f = line.split()
+    assert f[1] == "nccl" and f[2] == "1" and f[-1] == "66.0"
