@@ -203,7 +203,9 @@ int gsr_backward_dual(const gsr_settings* settings, const gsr_gaussians* gaussia
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix,
                      const float* projmatrix, uint8_t* visible, void* stream);
 
-/* Byte sizes of the opaque buffers (for tests and pre-sizing). */
+/* Byte sizes of the opaque buffers (for tests and pre-sizing).  The geometry buffer's size (and the
+ * counters' offset) depends on P and on the current device's CU count: its per-row scan arrays hold one
+ * entry per 512 or 1024 Gaussians (rows of 512 when rows of 1024 would leave fewer than two per CU). */
 size_t gsr_geom_buffer_bytes(int P);
 size_t gsr_binning_buffer_bytes(int num_rendered, int image_width, int image_height);
 size_t gsr_image_buffer_bytes(int image_width, int image_height);
