@@ -11,7 +11,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["GSR_LIB"] = os.path.join(ROOT, "splatam_amd", "_build_diag", "libgsr_diag.so")
+os.environ["GSR_LIB"] = os.environ.get("GSR_LIB") or os.path.join(ROOT, "splatam_amd", "_build_diag", "libgsr_diag.so")
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
