@@ -312,10 +312,11 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     fetch_rec((int)bmax);
     fetch_entry((int)bmax - BB);
     const uint32_t mean4 = sched_mean4(cam, guard.counters);
+    const bool multi_round = sched_multi_round(cam);
     int hi_pf = (int)bmax;  // the batch start the staged registers hold
     PHASE_MARK(0);
     for (int hi = (int)bmax; hi > 0;) {
-        prio_by_remaining(hi, mean4);
+        prio_by_remaining(hi, mean4, multi_round);
         if (hi != hi_pf) {  // the previous batch was cut by its slot budget: re-fetch (rare)
             fetch_entry(hi);
             fetch_rec(hi);

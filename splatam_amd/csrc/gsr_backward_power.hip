@@ -499,7 +499,7 @@ render_bwd_fisher_kernel(Camera cam, float power, const uint2* __restrict__ rang
     const uint32_t mean4 = sched_mean4(cam, guard.counters);
     int hi_pf = (int)bmax;
     for (int hi = (int)bmax; hi > 0;) {
-        prio_by_remaining(hi, mean4);
+        prio_by_remaining(hi, mean4, sched_multi_round(cam));
         if (hi != hi_pf) {  // the previous batch was cut by its slot budget: re-fetch (rare)
             fetch_entry(hi);
             fetch_rec(hi);

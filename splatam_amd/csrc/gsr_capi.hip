@@ -539,6 +539,7 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
         return fail(GSR_ERR_INVALID_ARG, "missing forward state");
     // the forward's render schedule (a permutation of the tiles; any order gives the same results)
     cam.tile_order = (const uint32_t*)((const char*)image_buffer + ImgLayout::make(cam.W, cam.H).order);
+    cam.sched_cus = device_cus(current_device());  // (wave priority levels: one or several dispatch rounds)
     const GeomLayout GL = GeomLayout::make(P);
     cam.pre_shift = GL.shift;
     const ImgLayout IL = ImgLayout::make(cam.W, cam.H);

@@ -165,16 +165,21 @@ struct Camera {
 #ifndef GSR_PRIO_SCHED
 #define GSR_PRIO_SCHED 1
 #endif
-// Levels at 0.7 / 0.45 / 0.22 of the frame's mean tile list (`mean4` = 4 x mean, from num_rendered).
-__device__ __forceinline__ void prio_by_remaining(int remaining, uint32_t mean4) {
+// Levels at 70 / 45 / 22 % of the frame's mean tile list (`mean4` = 4 x mean, from num_rendered) when every tile
+// is resident at once (config 3: 1200 tiles, 1280 workgroup slots; 200 / 100 / 50 % measured 3 us slower
+// there), and at 200 / 100 / 50 % when the tiles take several dispatch rounds (config 4: 3225 tiles; the
+// single-round levels measured 392 against 383 us for render_bwd): `multi` = more tiles than 5 per CU.
+__device__ __forceinline__ void prio_by_remaining(int remaining, uint32_t mean4, bool multi) {
 #if GSR_PRIO_SCHED
-    const uint32_t r = 4u * (uint32_t)remaining;  // compare r / mean4 against 0.7, 0.45, 0.22 (x 100)
-    if (100u * r > 70u * mean4) __builtin_amdgcn_s_setprio(3);
-    else if (100u * r > 45u * mean4) __builtin_amdgcn_s_setprio(2);
-    else if (100u * r > 22u * mean4) __builtin_amdgcn_s_setprio(1);
+    const uint32_t r = 4u * (uint32_t)remaining;  // compare r / mean4 against the level thresholds (x 100)
+    const uint32_t t3 = multi ? 200u : 70u, t2 = multi ? 100u : 45u, t1 = multi ? 50u : 22u;
+    if (100u * r > t3 * mean4) __builtin_amdgcn_s_setprio(3);
+    else if (100u * r > t2 * mean4) __builtin_amdgcn_s_setprio(2);
+    else if (100u * r > t1 * mean4) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
 #endif
 }
+__device__ __forceinline__ bool sched_multi_round(const Camera& cam) { return cam.gx * cam.gy > 5 * cam.sched_cus; }
 __device__ __forceinline__ uint32_t sched_mean4(const Camera& cam, const uint32_t* counters) {
     const uint32_t nt = (uint32_t)(cam.gx * cam.gy);
     return max(1u, (uint32_t)(4ull * counters[0] / (nt ? nt : 1u)));

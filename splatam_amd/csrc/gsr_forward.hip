@@ -1240,8 +1240,9 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
     fetch_rec(range.x);
     fetch_id(range.x + RENDER_BATCH);
     const uint32_t mean4 = sched_mean4(cam, guard.counters);
+    const bool multi_round = sched_multi_round(cam);
     for (uint32_t start = range.x; start < range.y; start += RENDER_BATCH) {
-        prio_by_remaining((int)(range.y - start), mean4);
+        prio_by_remaining((int)(range.y - start), mean4, multi_round);
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
         const int cnt = (int)min((uint32_t)RENDER_BATCH, range.y - start);
         if (tid < cnt) {
