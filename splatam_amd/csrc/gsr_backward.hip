@@ -169,11 +169,18 @@ constexpr int bwd_nv() { return 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2
 #ifndef GSR_BWD_WIDE_WAVES
 #define GSR_BWD_WIDE_WAVES 5
 #endif
+#ifndef GSR_BWD_MAP_WAVES
+#define GSR_BWD_MAP_WAVES 4
+#endif
+#ifndef GSR_BWD_SPLIT6
+#define GSR_BWD_SPLIT6 1  // wide variants: the first reduction pass carries G dL/dalpha with the 5 geometric sums
+// (6 + 6 instead of 5 + 7 sums for mapping: 84 instead of 96 DPP adds per step, render_bwd 312 -> 303 us at config 4)
+#endif
 #ifndef GSR_PACK_C
 #define GSR_PACK_C 1  // DUAL, Q2 = 1: the second colour set's one channel staged in s_c.w (no s_d array)
 #endif
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2>
-constexpr int bwd_waves() { return (DUAL && Q2 == 3) ? 4 : ((OPAC && COL1) ? GSR_BWD_WIDE_WAVES : 5); }
+constexpr int bwd_waves() { return (DUAL && Q2 == 3) ? GSR_BWD_MAP_WAVES : ((OPAC && COL1) ? GSR_BWD_WIDE_WAVES : 5); }
 
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3>
 __global__ void __launch_bounds__(TILE_PIX, (bwd_waves<DUAL, OPAC, COL1, COL2, Q2>()))
@@ -448,23 +455,24 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
 #else
                 reduce_store<NV>(v, lane, dst, true);
 #endif
-            } else {  // wide variants: geometric, then opacity + colour sums (register pressure)
-                constexpr int NB = NV - 5;
+            } else {  // wide variants: geometric (+ opacity), then colour sums (register pressure)
+                constexpr bool OP_A = OPAC && GSR_BWD_SPLIT6;
+                constexpr int NA = 5 + (OP_A ? 1 : 0), NB = NV - NA;
                 {
-                    float v[4 * 5];
+                    float v[4 * NA];
 #pragma unroll
-                    for (int k = 0; k < 4; k++) pair_geom<false>(v + 5 * k, araw[k], dLa[k], G[k], d[k]);
-                    reduce_store<5>(v, lane, dst, true);
+                    for (int k = 0; k < 4; k++) pair_geom<OP_A>(v + NA * k, araw[k], dLa[k], G[k], d[k]);
+                    reduce_store<NA>(v, lane, dst, true);
                 }
                 {
                     float v[4 * NB];
+                    constexpr int OB = (OPAC && !OP_A) ? 1 : 0;
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
-                        if (OPAC) v[NB * k] = G[k] * dLa[k];
-                        pair_colours<COL1, COL2, Q2>(v + NB * k + (OPAC ? 1 : 0), dch[k], dp01, dp2, dq0, dq01,
-                                                     dq2);
+                        if (OB) v[NB * k] = G[k] * dLa[k];
+                        pair_colours<COL1, COL2, Q2>(v + NB * k + OB, dch[k], dp01, dp2, dq0, dq01, dq2);
                     }
-                    reduce_store<NB>(v, lane, dst + 5, true);
+                    reduce_store<NB>(v, lane, dst + NA, true);
                 }
             }
         }
