@@ -37,12 +37,15 @@ namespace {
 
 // ------------------------------------------------------------- SSIM tiles --
 constexpr int SS_TW = 64;                 // output tile width (one wave per row)
-constexpr int SS_TH = 16;                 // output tile height
+#ifndef GSR_SS_TH
+#define GSR_SS_TH 16
+#endif
+constexpr int SS_TH = GSR_SS_TH;          // output tile height
 constexpr int SS_R = 5;                   // window radius (window_size 11)
 constexpr int SS_IW = SS_TW + 2 * SS_R;   // 74
-constexpr int SS_IH = SS_TH + 2 * SS_R;   // 26
+constexpr int SS_IH = SS_TH + 2 * SS_R;   // 26 at 16 rows
 constexpr int SS_BLOCK = 256;
-constexpr int SS_ROWS_PER_THREAD = SS_TH / (SS_BLOCK / SS_TW);  // 4
+constexpr int SS_ROWS_PER_THREAD = SS_TH / (SS_BLOCK / SS_TW);  // 4 at 16 rows
 constexpr float SS_C1 = 0.01f * 0.01f;
 constexpr float SS_C2 = 0.03f * 0.03f;
 constexpr int MAP_PARTS = 4;  // sum ssim, sum |x - y|, sum masked |d - gt|, mask count
@@ -65,25 +68,39 @@ Window make_window() {
     return win;
 }
 
-__device__ __forceinline__ bool map_mask(int pid, int HW, const float* ds, const float* gt_depth) {
-    const float d = ds[pid], dsq = ds[2 * HW + pid];
+__device__ __forceinline__ bool map_mask_v(float d, float dsq, float gt_depth) {
     const float unc = dsq - d * d;
-    return gt_depth[pid] > 0.f && !isnan(d) && !isnan(unc);
+    return gt_depth > 0.f && !isnan(d) && !isnan(unc);
 }
 
 __device__ __forceinline__ float sgn(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
 
 // Loads NM maps' (TH + 10) x (TW + 10) halo tiles of channel plane `c` into LDS,
 // zero outside the image (conv2d zero padding).
+// Every load of the thread's elements is issued before the first LDS store: a load-then-store
+// loop waits one HBM round trip per element (the halo phase set the kernels' time).
 template <int NM>
 __device__ __forceinline__ void load_halo(float (*dst)[SS_IH][SS_IW], const float* const (&src)[NM], int H, int W,
                                           int x0, int y0) {
-    for (int e = threadIdx.x; e < SS_IH * SS_IW; e += SS_BLOCK) {
+    constexpr int NE = (SS_IH * SS_IW + SS_BLOCK - 1) / SS_BLOCK;
+    float v[NE][NM];
+#pragma unroll
+    for (int i = 0; i < NE; i++) {
+        const int e = (int)threadIdx.x + i * SS_BLOCK;
         const int r = e / SS_IW, cc = e - r * SS_IW;
         const int y = y0 - SS_R + r, x = x0 - SS_R + cc;
-        const bool in = y >= 0 && y < H && x >= 0 && x < W;
+        const bool in = e < SS_IH * SS_IW && y >= 0 && y < H && x >= 0 && x < W;
 #pragma unroll
-        for (int m = 0; m < NM; m++) dst[m][r][cc] = in ? src[m][y * W + x] : 0.f;
+        for (int m = 0; m < NM; m++) v[i][m] = in ? src[m][y * W + x] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NE; i++) {
+        const int e = (int)threadIdx.x + i * SS_BLOCK;
+        if (e < SS_IH * SS_IW) {
+            const int r = e / SS_IW, cc = e - r * SS_IW;
+#pragma unroll
+            for (int m = 0; m < NM; m++) dst[m][r][cc] = v[i][m];
+        }
     }
 }
 
@@ -148,17 +165,31 @@ map_loss_fwd_kernel(int H, int W, const float* __restrict__ im, const float* __r
     const int HW = H * W, c = blockIdx.z;
     const int x0 = blockIdx.x * SS_TW, y0 = blockIdx.y * SS_TH;
     const float* const src[2] = {im + (size_t)c * HW, gt_im + (size_t)c * HW};
+    const int col = threadIdx.x % SS_TW, r0 = (threadIdx.x / SS_TW) * SS_ROWS_PER_THREAD;
+    const int x = x0 + col;
+    // the depth term's inputs (channel-0 workgroups), loaded up front: a load issued after the
+    // gmap stores would wait for them (vmcnt counts both)
+    float pd[SS_ROWS_PER_THREAD], pdsq[SS_ROWS_PER_THREAD], pgd[SS_ROWS_PER_THREAD];
+#pragma unroll
+    for (int j = 0; j < SS_ROWS_PER_THREAD; j++) {
+        const int y = y0 + r0 + j;
+        pd[j] = pdsq[j] = pgd[j] = 0.f;
+        if (c == 0 && x < W && y < H) {
+            const int pid = y * W + x;
+            pd[j] = ds[pid];
+            pdsq[j] = ds[2 * HW + pid];
+            pgd[j] = gt_d[pid];
+        }
+    }
     load_halo<2>(s_in, src, H, W, x0, y0);
     __syncthreads();
     horizontal_pass<2, 5>(s_in, s_h, win, [](const float (&i)[2], float (&o)[5]) {
         o[0] = i[0]; o[1] = i[1]; o[2] = i[0] * i[0]; o[3] = i[1] * i[1]; o[4] = i[0] * i[1];
     });
     __syncthreads();
-    const int col = threadIdx.x % SS_TW, r0 = (threadIdx.x / SS_TW) * SS_ROWS_PER_THREAD;
     float mo[SS_ROWS_PER_THREAD][5];
     vertical_pass<5>(s_h, win, col, r0, mo);
     float v[MAP_PARTS] = {0.f, 0.f, 0.f, 0.f};
-    const int x = x0 + col;
 #pragma unroll
     for (int j = 0; j < SS_ROWS_PER_THREAD; j++) {
         const int y = y0 + r0 + j;
@@ -181,12 +212,9 @@ map_loss_fwd_kernel(int H, int W, const float* __restrict__ im, const float* __r
         gmap[6 * (size_t)HW + o] = g2;
         v[0] += ssim;
         v[1] += fabsf(s_in[0][r0 + j + SS_R][col + SS_R] - s_in[1][r0 + j + SS_R][col + SS_R]);
-        if (c == 0) {
-            const int pid = y * W + x;
-            if (map_mask(pid, HW, ds, gt_d)) {
-                v[2] += fabsf(gt_d[pid] - ds[pid]);
-                v[3] += 1.f;
-            }
+        if (c == 0 && map_mask_v(pd[j], pdsq[j], pgd[j])) {
+            v[2] += fabsf(pgd[j] - pd[j]);
+            v[3] += 1.f;
         }
     }
     block_sum<MAP_PARTS>(v, s_red, s_tot);
@@ -222,13 +250,32 @@ map_loss_bwd_kernel(int H, int W, const float* __restrict__ im, const float* __r
     const int x0 = blockIdx.x * SS_TW, y0 = blockIdx.y * SS_TH;
     const float* const src[3] = {gmap + (size_t)c * HW, gmap + 3 * (size_t)HW + (size_t)c * HW,
                                  gmap + 6 * (size_t)HW + (size_t)c * HW};
+    const int col = threadIdx.x % SS_TW, r0 = (threadIdx.x / SS_TW) * SS_ROWS_PER_THREAD;
+    const int x = x0 + col;
+    // the epilogue's per-pixel inputs, loaded up front (ahead of the gradient stores)
+    float pxi[SS_ROWS_PER_THREAD], pyi[SS_ROWS_PER_THREAD];
+    float pd[SS_ROWS_PER_THREAD], pdsq[SS_ROWS_PER_THREAD], pgd[SS_ROWS_PER_THREAD];
+#pragma unroll
+    for (int j = 0; j < SS_ROWS_PER_THREAD; j++) {
+        const int y = y0 + r0 + j;
+        pxi[j] = pyi[j] = pd[j] = pdsq[j] = pgd[j] = 0.f;
+        if (x < W && y < H) {
+            const int pid = y * W + x;
+            pxi[j] = im[(size_t)c * HW + pid];
+            pyi[j] = gt_im[(size_t)c * HW + pid];
+            if (c == 0) {
+                pd[j] = ds[pid];
+                pdsq[j] = ds[2 * HW + pid];
+                pgd[j] = gt_d[pid];
+            }
+        }
+    }
     load_halo<3>(s_in, src, H, W, x0, y0);
     __syncthreads();
     horizontal_pass<3, 3>(s_in, s_h, win, [](const float (&i)[3], float (&o)[3]) {
         o[0] = i[0]; o[1] = i[1]; o[2] = i[2];
     });
     __syncthreads();
-    const int col = threadIdx.x % SS_TW, r0 = (threadIdx.x / SS_TW) * SS_ROWS_PER_THREAD;
     float bl[SS_ROWS_PER_THREAD][3];
     vertical_pass<3>(s_h, win, col, r0, bl);
     const float g = dloss[0];
@@ -237,17 +284,16 @@ map_loss_bwd_kernel(int H, int W, const float* __restrict__ im, const float* __r
     const float g_l1 = g * w_im * (0.8f / n);
     const float count = fwd_out[0];
     const float g_d = g * w_depth / count;
-    const int x = x0 + col;
 #pragma unroll
     for (int j = 0; j < SS_ROWS_PER_THREAD; j++) {
         const int y = y0 + r0 + j;
         if (x >= W || y >= H) continue;
         const int pid = y * W + x;
         const size_t o = (size_t)c * HW + pid;
-        const float xi = im[o], yi = gt_im[o];
+        const float xi = pxi[j], yi = pyi[j];
         dim[o] = g_ssim * (bl[j][0] + 2.f * xi * bl[j][1] + yi * bl[j][2]) + g_l1 * sgn(xi - yi);
         if (c == 0) {  // d|gt - d|/dd = -sgn(gt - d), over the masked mean
-            dds[pid] = map_mask(pid, HW, ds, gt_d) ? g_d * neg_sgn(gt_d[pid] - ds[pid]) : 0.f;
+            dds[pid] = map_mask_v(pd[j], pdsq[j], pgd[j]) ? g_d * neg_sgn(pgd[j] - pd[j]) : 0.f;
             dds[HW + pid] = 0.f;
             dds[2 * HW + pid] = 0.f;
         }
