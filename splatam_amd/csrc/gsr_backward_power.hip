@@ -167,9 +167,20 @@ render_bwd_power_kernel(Camera cam, int has_scales, int power, const uint2* __re
         for (int q = tid; q < 4 * B * NVP / 4; q += TILE_PIX)
             reinterpret_cast<float4*>(s_acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         __syncthreads();
-        for (int q = tid; q < cnt * JF4; q += TILE_PIX) {
-            const int item = q / JF4, part = q - item * JF4;
-            s_j[q] = jac[(size_t)s_g[item] * JF4 + part];
+        {  // every Jacobian-pack load issued before the first LDS store (one round trip, not one per float4)
+            constexpr int NJ = (B * JF4 + TILE_PIX - 1) / TILE_PIX;
+            float4 jv[NJ];
+#pragma unroll
+            for (int i = 0; i < NJ; i++) {
+                const int q = min(tid + i * TILE_PIX, cnt * JF4 - 1);  // clamped: loads without a branch
+                const int item = q / JF4, part = q - item * JF4;
+                jv[i] = jac[(size_t)s_g[item] * JF4 + part];
+            }
+#pragma unroll
+            for (int i = 0; i < NJ; i++) {
+                const int q = tid + i * TILE_PIX;
+                if (q < cnt * JF4) s_j[q] = jv[i];
+            }
         }
         __syncthreads();
         const int n = build_wave_list(s_mask, cnt, w, hi - (int)wmax, s_list[w]);

@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from splatam_amd import profiling  # noqa: E402
-from splatam_amd.rasterizer import GaussianRasterizer, rasterize_gaussians_dual  # noqa: E402
+from splatam_amd.rasterizer import GaussianRasterizer, rasterize_gaussians, rasterize_gaussians_dual  # noqa: E402
 from splatam_amd.scenes import config_scene  # noqa: E402
 from splatam_amd.slam import camera_settings  # noqa: E402
 
@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", choices=("dual_lean", "dual", "single"), default="dual_lean",
+    ap.add_argument("--mode", choices=("dual_lean", "dual", "single", "power"), default="dual_lean",
                     help="dual_lean: one dual rasterization, grads for means3D + depth colours only, depth "
                          "channel of the second image differentiated (tracking)")
     a = ap.parse_args()
@@ -47,7 +47,11 @@ def main():
     ds.requires_grad_(True)
 
     def it():
-        if a.mode == "single":
+        if a.mode == "power":  # drop-in backward_power=2 (hessian_diff_gaussian_rasterization_w_depth)
+            m2 = torch.zeros_like(m3, requires_grad=True)
+            im, _, _ = rasterize_gaussians(m3, m2, torch.Tensor([]), col, op, sc, ro, torch.Tensor([]), cam, 2)
+            im.backward(g)
+        elif a.mode == "single":
             for c in (col, ds):
                 m2 = torch.zeros_like(m3, requires_grad=True)
                 im, _, _ = ras(means3D=m3, means2D=m2, opacities=op, colors_precomp=c, scales=sc, rotations=ro)
