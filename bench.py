@@ -76,6 +76,9 @@ def parse():
                     help="also time the mapping workload (config 4) into a 'mapping' object (auto: N=1 only)")
     ap.add_argument("--mapping-steps", type=int, default=100, help="mapping leg: timed iterations")
     ap.add_argument("--fisher-k", type=int, default=16, help="fisher: poses per HIP-graph launch")
+    ap.add_argument("--configs", choices=("auto", "on", "off"), default="auto",
+                    help="BASELINE configs 1 (forward only) and 2 (fwd+bwd RGB + depth) on the GPU and the CPU "
+                         "oracle beside the headline (auto: N=1 only)")
     ap.add_argument("--timing", type=int, default=1,
                     help="0: no device-clock timing of render_bwd in the graph (A/B check; no roofline)")
     return ap.parse_args()
@@ -178,12 +181,14 @@ def main():
     t0 = time.perf_counter()
     if tracker is not None:
         per_bcast = max(1, args.bcast_every // FI) if args.bcast_every > 0 else 0
-        done, f = 0, 0
+        done, f, n_bcast = 0, 0, 0
         while done < steps:
             if world > 1 and per_bcast and f % per_bcast == 0:
                 sd.broadcast_map(params)       # map update -> RCCL broadcast over xGMI
+                n_bcast += 1
             n = min(FI, steps - done)
-            tracker.track_frame(n)             # one frame: fresh optimizer, replays, best pose written back
+            tracker.track_frame(n, check=False)  # one frame: fresh optimizer, replays, best pose written back
+            #   (overflow checked once after the timed loop, below)
             done += n
             f += 1
     else:
@@ -203,6 +208,35 @@ def main():
     elapsed = sd.max_over_ranks(t1 - t0, device=dev)
     frames = steps * world
     value = frames / elapsed
+    # the same timed frames without the broadcast, and the broadcast alone
+    bcast_split = None
+    if world > 1 and tracker is not None:
+        dist.barrier()
+        torch.cuda.synchronize()
+        tb0 = time.perf_counter()
+        done = 0
+        while done < steps:
+            n = min(FI, steps - done)
+            tracker.track_frame(n, check=False)
+            done += n
+        torch.cuda.synchronize()
+        dist.barrier()
+        el_nb = sd.max_over_ranks(time.perf_counter() - tb0, device=dev)
+        nb = 5
+        dist.barrier()
+        torch.cuda.synchronize()
+        tc0 = time.perf_counter()
+        for _ in range(nb):
+            sd.broadcast_map(params)
+        torch.cuda.synchronize()
+        dist.barrier()
+        el_b = sd.max_over_ranks(time.perf_counter() - tc0, device=dev)
+        if tracker.overflowed():
+            raise SystemExit("binning capacity overflow during the no-broadcast replays: measurement invalid")
+        bcast_split = {"value_no_broadcast": round(frames / el_nb, 3), "ms_per_step_no_broadcast":
+                       round(1000.0 * el_nb / steps, 4), "broadcast_ms": round(1000.0 * el_b / nb, 4),
+                       "broadcasts_in_timed_region": n_bcast,
+                       "broadcast_bytes": int(sum(params[k].numel() * params[k].element_size() for k in sd.MAP_KEYS))}
 
     # ---- roofline of the dominant kernel (render backward) ------------------
     rb = stages["render_bwd"]
@@ -233,6 +267,13 @@ def main():
                 else "hipEvents around each launch"}
 
     dropin = dropin_leg(args, scene, dev) if args.dropin == "on" else None
+    configs = None
+    if args.configs == "on" or (args.configs == "auto" and world == 1):
+        configs = configs_leg(dev, want_cpu=rank == 0 and args.cpu_baseline != "off")
+        stream = hbm_stream_gbs()
+        if stream:
+            roofline["peak_measured"] = {"copy_gbs": stream["copy_gbs"], "triad_gbs": stream["triad_gbs"],
+                                         "source": "tools/micro/stream (1 GiB float4 streams, best of 20)"}
     fisher = fisher_leg(args, scene, dev) if args.fisher == "on" else None
     mapping = None
     if args.mapping == "on" or (args.mapping == "auto" and world == 1):
@@ -313,10 +354,134 @@ def main():
             "dropin": dropin,
             "fisher": fisher,
             "mapping": mapping,
+            "configs": configs,
+            "broadcast": bcast_split,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def configs_leg(dev, want_cpu: bool):
+    """BASELINE.json configs 1 and 2 in SURVEY 8(d)'s unit (1 frame = the RGB render plus the [z, 1, z^2]
+    depth/silhouette render of the same Gaussians and camera): config 1 (10k isotropic, 320x240) forward
+    only, config 2 (100k isotropic, 640x480, Replica room0 intrinsics) forward + backward of both renders
+    with seeded N(0,1) pixel gradients.  GPU, two ways: `unit` = SURVEY's own measurement, 2 x
+    diff_gaussian_rasterization.GaussianRasterizer (+ backward) from Python with a synchronize around the
+    timed frames (every input a leaf requiring grad), and `fused` = one rasterize_gaussians_dual call (+ its
+    backward) per frame, eager.  CPU: the float32 C oracle on the same frame, every host thread, 1 warm-up +
+    median of 3 (config 1: 10 frames per sample)."""
+    import numpy as np
+    import diff_gaussian_rasterization as dgr
+    from splatam_amd.rasterizer import rasterize_gaussians_dual
+    from splatam_amd.scenes import config_scene
+    from splatam_amd.slam import camera_settings, init_tracking_params, transform_to_frame, \
+        transformed_params2depthplussilhouette, transformed_params2rendervar
+    out = {}
+    for cfg, fwd_only in ((1, True), (2, False)):
+        scene = config_scene(cfg)
+        P, W, H = scene.P, scene.cam.W, scene.cam.H
+        params = init_tracking_params(scene, num_frames=1, device=dev)
+        cam = camera_settings(scene.cam, dev)
+        w2c = torch.eye(4, device=dev)
+        with torch.no_grad():
+            tg = transform_to_frame(params, 0, False, False)
+            rv1 = transformed_params2rendervar(params, tg)
+            rv2 = transformed_params2depthplussilhouette(params, w2c, tg)
+        leaf = lambda d: {k: v.detach().clone().requires_grad_(not fwd_only) for k, v in d.items()}  # noqa: E731
+        rv1, rv2 = leaf(rv1), leaf(rv2)
+        rv2["means3D"] = rv1["means3D"]
+        gen = torch.Generator().manual_seed(0)
+        g1 = torch.randn(3, H, W, generator=gen).to(dev)
+        g2 = torch.randn(3, H, W, generator=gen).to(dev)
+        R = dgr.GaussianRasterizer
+
+        def unit():
+            if fwd_only:
+                with torch.no_grad():
+                    R(cam)(**rv1)
+                    R(cam)(**rv2)
+                return
+            for d in (rv1, rv2):
+                for v in d.values():
+                    v.grad = None
+            im, _, _ = R(cam)(**rv1)
+            ds, _, _ = R(cam)(**rv2)
+            ((im * g1).sum() + (ds * g2).sum()).backward()
+
+        def fused():
+            if fwd_only:
+                with torch.no_grad():
+                    rasterize_gaussians_dual(rv1["means3D"], rv1["means2D"], None, rv1["colors_precomp"],
+                                             rv2["colors_precomp"], rv1["opacities"], rv1["scales"],
+                                             rv1["rotations"], None, cam)
+                return
+            for d in (rv1, rv2):
+                for v in d.values():
+                    v.grad = None
+            im, ds, _, _ = rasterize_gaussians_dual(rv1["means3D"], rv1["means2D"], None, rv1["colors_precomp"],
+                                                    rv2["colors_precomp"], rv1["opacities"], rv1["scales"],
+                                                    rv1["rotations"], None, cam)
+            ((im * g1).sum() + (ds * g2).sum()).backward()
+
+        res = {"workload": f"config {cfg}: {P} isotropic Gaussians, {W}x{H}, "
+                           + ("forward only" if fwd_only else "forward + backward") + " of RGB + depth/silhouette"}
+        for name, fn in (("unit", unit), ("fused", fused)):
+            for _ in range(5):
+                fn()
+            torch.cuda.synchronize()
+            n = 200 if fwd_only else 100
+            t0 = time.perf_counter()
+            for _ in range(n):
+                fn()
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / n
+            res[name] = {"value": round(1.0 / dt, 2), "unit": "frames/s", "ms_per_frame": round(1000 * dt, 4)}
+        if want_cpu:
+            from oracle import oracle as orc
+            c = scene.cam
+            common = dict(view=c.viewmatrix.numpy(), proj=c.projmatrix.numpy(), campos=c.campos.numpy(),
+                          tanfovx=c.tanfovx, tanfovy=c.tanfovy, H=H, W=W)
+            inputs = [tuple(r[k].detach().cpu().numpy() for k in ("means3D", "opacities", "colors_precomp", "scales",
+                                                                   "rotations")) for r in (rv1, rv2)]
+            dps = [g1.cpu().numpy(), g2.cpu().numpy()]
+            reps = 10 if fwd_only else 1
+
+            def cpu_frame():
+                for _ in range(reps):
+                    for (m, o, col, sc, ro), dp in zip(inputs, dps):
+                        fr = orc.forward(m, o, colors=col, scales=sc, rotations=ro, **common)
+                        if not fwd_only:
+                            orc.backward(fr, dp)
+
+            cpu_frame()
+            times = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                cpu_frame()
+                times.append((time.perf_counter() - t0) / reps)
+            tc = sorted(times)[1]
+            res["cpu"] = {"value": round(1.0 / tc, 4), "unit": "frames/s", "cores": orc.threads(), "kind": "port",
+                          "sample": f"{reps} frame(s) per sample through oracle/gsr_oracle.c float32, 1 warm-up + "
+                                    f"median of 3: {', '.join(f'{t:.4f}' for t in times)} s per frame"}
+        out[str(cfg)] = res
+        del params, rv1, rv2
+        torch.cuda.empty_cache()
+    return out
+
+
+def hbm_stream_gbs():
+    """STREAM-style copy / triad on this GPU (tools/micro/stream, built in-tree): the measured HBM peak the
+    roofline's spec peak is compared with; None when the binary is absent."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "micro", "stream")
+    if not os.path.exists(exe):
+        return None
+    try:
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+        return json.loads(r.stdout.strip().split("\n")[-1])
+    except Exception:
+        return None
 
 
 def dropin_leg(args, scene, dev, iters_per_frame: int = 40):
@@ -493,14 +658,12 @@ def fisher_leg(args, scene, dev, launches: int = 6):
     bf = BatchedFisher(sc, K, mode="sum", probe_w2cs=poses)
     bf.hessian_sum(poses)
     torch.cuda.synchronize()
-    bf.status.zero_()
     t0 = time.perf_counter()
     for _ in range(launches):
-        bf.hessian_sum(poses, check=False)  # the sticky status rows are checked once after the timed launches
+        if bf.hessian_sum(poses) is None:  # the default (checked) call: one host sync per launch
+            return {"error": "binning capacity overflow"}
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    if bf.overflowed():
-        return {"error": "binning capacity overflow"}
     sc.hessian(poses[0])
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -508,11 +671,73 @@ def fisher_leg(args, scene, dev, launches: int = 6):
         sc.hessian(w)
     torch.cuda.synchronize()
     de = (time.perf_counter() - t1) / 4
+    dropin = fisher_dropin(params, cam, poses, dev)
     return {"value": round(K * launches / dt, 2), "unit": "poses/s", "poses_per_launch": K,
             "ms_per_pose": round(1000 * dt / (K * launches), 4), "eager_ms_per_pose": round(1000 * de, 4),
+            "dropin": dropin,
             "workload": f"H_train of {K} visited poses per HIP-graph launch over the {scene.P}-Gaussian "
                         f"{scene.cam.W}x{scene.cam.H} map: static forward + backward_power=2 per pose, "
                         "H accumulated on the device"}
+
+
+def fisher_dropin(params, cam, poses, dev):
+    """The reference's own Fisher caller, unchanged (scripts/ros_handler.py:839-902 compute_Hessian with
+    return_points=True): per pose the map is moved into the candidate frame by torch glue, every rendervar
+    is made to require grad, hessian_diff_gaussian_rasterization_w_depth.GaussianRasterizer(..,
+    backward_power=2) renders, im.backward(1e-3 * ones) runs the full-gradient power-2 backward, and H =
+    [transformed_pts.grad, opacities.grad].  Eager, one pose at a time; the render-backward kernels' own
+    time is read from the stage timers in a separate pass."""
+    import torch.nn.functional as F
+    from hessian_diff_gaussian_rasterization_w_depth import GaussianRasterizer as Renderer
+    from splatam_amd import profiling
+
+    def compute_hessian(rel_w2c):
+        with torch.no_grad():
+            pts = params["means3D"]
+            pts_ones = torch.ones(pts.shape[0], 1, device=dev).float()
+            pts4 = torch.cat((pts, pts_ones), dim=1)
+            transformed_pts = (rel_w2c @ pts4.T).T[:, :3]
+            rgb_colors = params["rgb_colors"]
+            rotations = F.normalize(params["unnorm_rotations"])
+            opacities = torch.sigmoid(params["logit_opacities"])
+            scales = torch.exp(params["log_scales"])
+            if scales.shape[-1] == 1:
+                scales = torch.tile(scales, (1, 3))
+        num_points = transformed_pts.shape[0]
+        rendervar = {"means3D": transformed_pts.requires_grad_(True),
+                     "colors_precomp": rgb_colors.detach().clone().requires_grad_(True),
+                     "rotations": rotations.requires_grad_(True), "opacities": opacities.requires_grad_(True),
+                     "scales": scales.requires_grad_(True),
+                     "means2D": torch.zeros_like(transformed_pts, requires_grad=True, device=dev) + 0}
+        rendervar["means2D"].retain_grad()
+        im, _, _ = Renderer(raster_settings=cam, backward_power=2)(**rendervar)
+        im.backward(gradient=torch.ones_like(im) * 1e-3)
+        cur_H = torch.cat([transformed_pts.grad.detach().reshape(num_points, -1),
+                           opacities.grad.detach().reshape(num_points, -1)], dim=1)
+        for v in rendervar.values():
+            v.grad.fill_(0.)
+        return cur_H
+
+    for w in poses[:2]:
+        compute_hessian(w)
+    torch.cuda.synchronize()
+    n = len(poses)
+    t0 = time.perf_counter()
+    for w in poses:
+        compute_hessian(w)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / n
+    profiling.enable_timing(True)
+    for w in poses[:4]:
+        compute_hessian(w)
+    torch.cuda.synchronize()
+    st = profiling.read_timing()
+    profiling.enable_timing(False)
+    return {"value": round(1.0 / dt, 2), "unit": "poses/s", "ms_per_pose": round(1000 * dt, 4),
+            "render_bwd_us": round(st["render_bwd"]["avg_us"], 2), "gauss_bwd_us": round(st["gauss_bwd"]["avg_us"], 2),
+            "path": "unchanged scripts/ros_handler.py compute_Hessian: torch glue + hessian_diff_gaussian_"
+                    "rasterization_w_depth.GaussianRasterizer(backward_power=2) with every rendervar requiring "
+                    "grad + im.backward(1e-3), eager, one pose at a time"}
 
 
 def render_bwd_roofline(rb, I_avg, P, W, H, graph: bool):
@@ -579,7 +804,7 @@ def run_mapping(args, world, rank, dev):
     S = math.gcd(max(1, args.iters_per_graph), steps)  # exactly `steps` timed iterations, whole replays
     mapper = GraphMapper(params, kfs, iters_per_graph=S, cfg=MappingConfig(), timing=bool(args.timing))
     for _ in range(max(1, -(-args.warmup // S))):  # >= W untimed iterations (whole replays)
-        mapper.run()
+        mapper.run()  # checked: raises on an overflow
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -587,7 +812,7 @@ def run_mapping(args, world, rank, dev):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps // S):
-        mapper.run()
+        mapper.run(check=False)  # no host sync inside the timed region; overflowed() read after it
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -245,6 +245,12 @@ typedef struct gsr_map_adam {
      * gsr_backward_dual_sh_adam ignores it and guards on its own forward's counters. */
     const unsigned* status;
     unsigned capacity;
+    /* optional device word, zero at the start of a frame (torch.optim.Adam's fresh state): a step
+     * skipped because its forward overflowed sets it, and every later fused step (colour group,
+     * transform backward) is skipped while it is set -- so the device never applies a step whose
+     * bias corrections assume a step count the skipped one did not reach.  The caller re-runs the
+     * frame from fresh state (splatam_amd.glue.MapAdam.reset) after reading it as non-zero. */
+    unsigned* halted;
 } gsr_map_adam;
 
 /* gsr_backward_dual with the mapping optimizer's colour group (sh_adam->exp_avg[4] / exp_avg_sq[4] /

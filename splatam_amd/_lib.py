@@ -38,7 +38,7 @@ class GsrMapAdam(ctypes.Structure):
     """gsr_map_adam (include/gsr_glue.h)."""
     _fields_ = [("exp_avg", c_void_p * 5), ("exp_avg_sq", c_void_p * 5), ("lr", c_double * 5), ("step", c_int),
                 ("beta1", c_double), ("beta2", c_double), ("eps", c_double), ("status", c_void_p),
-                ("capacity", ctypes.c_uint)]
+                ("capacity", ctypes.c_uint), ("halted", c_void_p)]
 
 
 class GsrTrackXform(ctypes.Structure):
@@ -158,7 +158,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.gsr_abi_version() != 4:
+    if lib.gsr_abi_version() != 5:
         raise ImportError("libgsr.so ABI version mismatch")
     return lib
 

@@ -15,6 +15,7 @@
 //               per-Gaussian chain rule (backward.cu:144-274 cov2D,
 //               412-475 cov3D, 480-530 projection, 20-139 SH).
 #include <cstdlib>
+#include <utility>
 
 #include "gsr_chain.h"
 #include "gsr_glue_common.h"
@@ -125,16 +126,17 @@ __device__ __forceinline__ void reduce_store(const float (&v)[4 * N], int lane, 
 // config-4 dual 425 -> 410 us; profiles/r3_ab_render_bwd.txt); 448 slots drop the mapping variant to 4
 #define GSR_BWD_WBB 128
 #endif
-template <int NV>
-constexpr int bwd_batch() { return NV <= 6 ? GSR_BWD_BB : GSR_BWD_WBB; }
+template <int NV, int MOM = 0>
+constexpr int bwd_batch() { return MOM ? 128 : (NV <= 6 ? GSR_BWD_BB : GSR_BWD_WBB); }
 #ifndef GSR_BWD_WBS
 #define GSR_BWD_WBS 384  // slot budget of the wide variants' batches
 #endif
 #ifndef GSR_BWD_BS
 #define GSR_BWD_BS (4 * GSR_BWD_BB)  // slot budget of the batches of the variants with <= 6 sums
 #endif
-template <int NV>
-constexpr int bwd_slots() { return NV <= 6 ? GSR_BWD_BS : GSR_BWD_WBS; }
+// the moment variants (backward_power == 2): 19 / 37 sums per slot; 256 / 128 slots keep 4 workgroups per CU
+template <int NV, int MOM = 0>
+constexpr int bwd_slots() { return MOM == 1 ? 256 : (MOM == 2 ? 128 : (NV <= 6 ? GSR_BWD_BS : GSR_BWD_WBS)); }
 
 // DUAL: the pass also carries a second colour set (colors2, dL_dpix2) composited
 // with the same alpha / T (one dual forward): the per-pair dL/dalpha is the sum
@@ -161,8 +163,72 @@ constexpr int bwd_slots() { return NV <= 6 ? GSR_BWD_BS : GSR_BWD_WBS; }
 // Gaussian) instance at its unsorted position.
 // 5 workgroups per CU (<= 96 VGPRs): a 640x480 frame's 1200 tiles are all resident
 // at once, so there is no second dispatch round behind the slowest tiles.
-template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2>
-constexpr int bwd_nv() { return 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2 : 0); }
+// MOM (backward_power == 2, gauss_bwd_mom_kernel): the pair's second moments instead of its values --
+// 1: colours precomputed, 19 sums (u u^T upper triangle of the 5 geometric terms, (G dL/dalpha)^2,
+// (dch dL/dpix_c)^2); 2: SH colours, 37 sums (+ the colour terms' cross moments with u and each other).
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2, int MOM = 0>
+constexpr int bwd_nv() { return MOM == 1 ? 19 : (MOM == 2 ? 37 : 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2 : 0)); }
+// Moment q of the MOM layout as the product b_i b_j of the pair's base values b = (u0..u4, G dL/dalpha,
+// dch dL/dpix_0..2): [0, 15) u_i u_j (i <= j, row-major), 15 b5 b5, then MOM 1: b_{6+c}^2; MOM 2: the 6
+// colour products (c <= d, row-major), then u_i b_{6+c} (i-major).
+__host__ __device__ constexpr int mom_i(int mom, int q) {
+    if (q < 15) {
+        int i = 0, r = q;
+        while (r >= 5 - i) r -= 5 - i++;
+        return i;
+    }
+    if (q == 15) return 5;
+    if (mom == 1) return 6 + (q - 16);
+    if (q < 22) {
+        int i = 0, r = q - 16;
+        while (r >= 3 - i) r -= 3 - i++;
+        return 6 + i;
+    }
+    return (q - 22) / 3;
+}
+__host__ __device__ constexpr int mom_j(int mom, int q) {
+    if (q < 15) {
+        int i = 0, r = q;
+        while (r >= 5 - i) r -= 5 - i++;
+        return i + r;
+    }
+    if (q == 15) return 5;
+    if (mom == 1) return 6 + (q - 16);
+    if (q < 22) {
+        int i = 0, r = q - 16;
+        while (r >= 3 - i) r -= 3 - i++;
+        return 6 + i + r;
+    }
+    return 6 + (q - 22) % 3;
+}
+static_assert(mom_i(1, 14) == 4 && mom_j(1, 14) == 4 && mom_i(1, 5) == 1 && mom_j(1, 5) == 1 && mom_j(1, 18) == 8, "");
+static_assert(mom_i(2, 20) == 7 && mom_j(2, 20) == 8 && mom_i(2, 36) == 4 && mom_j(2, 36) == 8, "");
+template <int MOM, int Q>
+struct MomIJ {  // (frontend-evaluated: every register-array index below is a compile-time constant)
+    static constexpr int i = mom_i(MOM, Q), j = mom_j(MOM, Q);
+};
+// One reduction pass over moments [Q0, Q0 + N) of the step's four entries (base values b[k][0..8]).
+template <int MOM, int Q0, int... Q>
+__device__ __forceinline__ void mom_products(const float (&b)[4][9], float* v, std::integer_sequence<int, Q...>) {
+    constexpr int N = sizeof...(Q);
+#pragma unroll
+    for (int k = 0; k < 4; k++) ((v[N * k + Q] = b[k][MomIJ<MOM, Q0 + Q>::i] * b[k][MomIJ<MOM, Q0 + Q>::j]), ...);
+}
+template <int MOM, int Q0, int N>
+__device__ __forceinline__ void mom_pass(const float (&b)[4][9], int lane, float* dst) {
+    float v[4 * N];
+    mom_products<MOM, Q0>(b, v, std::make_integer_sequence<int, N>{});
+    reduce_store<N>(v, lane, dst + Q0, true);
+}
+// The moments as a symmetric 9 x 9 matrix (entries MOM 1 does not form stay 0).
+template <int MOM, int... Q>
+__device__ __forceinline__ void mom_matrix(const float* S, float (&Sm)[9][9], std::integer_sequence<int, Q...>) {
+#pragma unroll
+    for (int a = 0; a < 9; a++)
+#pragma unroll
+        for (int c = 0; c < 9; c++) Sm[a][c] = 0.f;
+    ((Sm[MomIJ<MOM, Q>::i][MomIJ<MOM, Q>::j] = S[Q], Sm[MomIJ<MOM, Q>::j][MomIJ<MOM, Q>::i] = S[Q]), ...);
+}
 // 5 waves per SIMD (96 VGPRs; the wide variants reduce in two passes to fit), except
 // the dual variants with a 3-channel second gradient (mapping-style), which spill
 // at 96 VGPRs and run at 4
@@ -179,11 +245,13 @@ constexpr int bwd_nv() { return 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2
 #ifndef GSR_PACK_C
 #define GSR_PACK_C 1  // DUAL, Q2 = 1: the second colour set's one channel staged in s_c.w (no s_d array)
 #endif
-template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2>
-constexpr int bwd_waves() { return (DUAL && Q2 == 3) ? GSR_BWD_MAP_WAVES : ((OPAC && COL1) ? GSR_BWD_WIDE_WAVES : 5); }
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2, int MOM = 0>
+constexpr int bwd_waves() {
+    return MOM ? 4 : ((DUAL && Q2 == 3) ? GSR_BWD_MAP_WAVES : ((OPAC && COL1) ? GSR_BWD_WIDE_WAVES : 5));
+}
 
-template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3>
-__global__ void __launch_bounds__(TILE_PIX, (bwd_waves<DUAL, OPAC, COL1, COL2, Q2>()))
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3, int MOM = 0>
+__global__ void __launch_bounds__(TILE_PIX, (bwd_waves<DUAL, OPAC, COL1, COL2, Q2, MOM>()))
 render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry* __restrict__ point_list,
                   const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
                   const float* __restrict__ final_T,
@@ -191,6 +259,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                   const float* __restrict__ dL_dpix2, float* __restrict__ inst, BwdGuard guard,
                   unsigned long long* clk) {
     static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
+    static_assert(!MOM || (!DUAL && OPAC && COL1), "the moment variants form every single-image gradient");
     kclock_begin(clk);
     GSR_WGTIME_MARK(false);
     if (guard.overflow()) {  // invalid forward state (static-mode overflow): touch nothing
@@ -199,9 +268,9 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     }
     PHASE_T0();
     static_assert(Q2 == 1 || Q2 == 3, "Q2 is 1 or 3 channels");
-    constexpr int NV = bwd_nv<DUAL, OPAC, COL1, COL2, Q2>();
-    constexpr int O_OP = 5, O_C1 = 5 + (OPAC ? 1 : 0), O_C2 = O_C1 + (COL1 ? 3 : 0);
-    constexpr int BB = bwd_batch<NV>(), BS = bwd_slots<NV>();
+    constexpr int NV = bwd_nv<DUAL, OPAC, COL1, COL2, Q2, MOM>();
+    constexpr int O_C1 = 5 + (OPAC ? 1 : 0);
+    constexpr int BB = bwd_batch<NV, MOM>(), BS = bwd_slots<NV, MOM>();
     constexpr int RS = (NV + 1) & ~1;  // record stride (floats)
     constexpr int LS = BB + 4;  // row-list stride (u32)
     // entry BB is a dummy (opacity 0, never blends) that pads the row lists; its slot BS
@@ -263,14 +332,17 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
 #pragma unroll
         for (int m = 0; m < RS / 2; m++) dst[m] = make_float2(0.f, 0.f);
     }
-    // background term of dL/dalpha, -T_final / (1 - alpha) * (bg . dL/dpix) (backward.cu:1014):
-    // a per-pixel constant times 1 / (1 - alpha); exactly 0 when bg = 0
+    // background term of dL/dalpha, -T_final / (1 - alpha) * (bg . dL/dpix) (backward.cu:1014), folded
+    // into the accumulator: with A' = A - Tbg / T (Tbg = -T_final bg.dL/dpix, T the transmittance in
+    // front of the current Gaussian), dL/dalpha = T_n (c . dL/dpix - A') and A' follows A's own recurrence
+    // A' <- A' + alpha (c . dL/dpix - A') (T_n = T / (1 - alpha)), from A'_0 = bg . dL/dpix: the colour
+    // behind the last Gaussian is the background.  Bitwise the plain recurrence when bg = 0.
     float bg_dot = cam.bg[0] * dp0 + cam.bg[1] * dp1 + cam.bg[2] * dp2;
     if (DUAL) bg_dot += cam.bg[0] * dq0 + cam.bg[1] * dq1 + cam.bg[2] * dq2;
-    const float Tbg = -T_final * bg_dot;
     const v2f pix = v2f{(float)px, (float)py};
     const v2f dp01 = v2f{dp0, dp1}, dq01 = v2f{dq0, dq1};
-    float T = T_final, A = 0.f;
+    const v2f dp2q0 = v2f{dp2, dq0};  // (PACKC) the colour dot's second packed pair
+    float T = T_final, A = bg_dot;
 #if GSR_ABLATE == 1
     float ablate_sink = 0.f;
 #endif
@@ -348,38 +420,51 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         hi_pf = hi - BB;
         // entries j with pos = hi-1-j >= rmax lie behind every pixel of the block
         const int jmin[4] = {hi - rm[0], hi - rm[1], hi - rm[2], hi - rm[3]};
+        // list words: (LDS byte offset of entry j's staged record, 16 j) | (byte offset of its slot) << 16
+        static_assert(16 * BB < 65536 && (BS + 1) * NV * 4 < 65536, "list words hold 16-bit byte offsets");
         const SlotLists sl = build_row_slot_lists(s_mask, s_base, cmax, BS, w, jmin, s_list + 4 * w * LS, LS,
-                                                  (uint32_t)BB | ((uint32_t)BS << 16));
+                                                  (uint32_t)(16 * BB) | ((uint32_t)(BS * NV * 4) << 16), 16u,
+                                                  (uint32_t)(NV * 4));
         const int n = sl.len, cnt = sl.cnt;
         PHASE_MARK(2);
-        const int jlo = hi - (int)last;  // pos = hi-1-j < last  <=>  j >= jlo
+        const int jlo16 = 16 * (hi - (int)last);  // pos = hi-1-j < last  <=>  j >= jlo  <=>  16 j >= 16 jlo
 #if GSR_STEPSTAT
         st_batches++;
 #endif
         for (int i = 0; i < n; i += 4) {
             const uint4 gw = load_slot_group4(my_list, i);
-            RowGroup4 gq;
-            gq.j[0] = (int)(gw.x & 0xFFFFu);
-            gq.j[1] = (int)(gw.y & 0xFFFFu);
-            gq.j[2] = (int)(gw.z & 0xFFFFu);
-            gq.j[3] = (int)(gw.w & 0xFFFFu);
+            // this lane's entry slot (the reduction's writer lanes): the high half of its entry's word,
+            // read from LDS instead of selected from gw
+            const uint32_t soff = reinterpret_cast<const uint16_t*>(my_list + i + my_e)[1];
+            int jb[4];  // byte offsets 16 j of the step's entries in s_a / s_b / s_c / s_d
+            jb[0] = (int)(gw.x & 0xFFFFu);
+            jb[1] = (int)(gw.y & 0xFFFFu);
+            jb[2] = (int)(gw.z & 0xFFFFu);
+            jb[3] = (int)(gw.w & 0xFFFFu);
+            auto rec = [&](const float4* arr, int k) {
+                return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(arr) + jb[k]);
+            };
             v2f d[4];
             float G[4], araw[4], alpha[4];
             bool ok[4];
             [[maybe_unused]] bool any = false;  // (step statistics only)
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const float4 a = s_a[gq.j[k]], b = s_b[gq.j[k]];
+                const float4 a = rec(s_a, k), b = rec(s_b, k);
                 d[k] = pix_delta(a, pix);
                 const float p2 = eval_p2(a, b, d[k]);                       // log2(e) * power
-                G[k] = __builtin_amdgcn_exp2f(fminf(p2, 0.f));             // finite for every lane
-                araw[k] = b.y * G[k];
+                // position in the tile list before the pixel's last contributor, power <= 0, alpha >= 1/255
+                // (alpha = min(0.99, araw) >= 1/255 <=> araw >= 1/255); the pad entry has opacity 0.
+                // Non-contributing pairs continue with alpha 0: T and A then pass through unchanged
+                // (1 / (1 - 0) == 1 exactly).  Without the opacity sum the mask is applied to araw (a
+                // masked pair's h = araw dL/dalpha is then 0, and G may even be inf there); with it,
+                // G dL/dalpha needs a finite G and a masked dL/dalpha.
+                G[k] = __builtin_amdgcn_exp2f(OPAC ? fminf(p2, 0.f) : p2);
+                const float ar = b.y * G[k];
+                ok[k] = jb[k] >= jlo16 && p2 <= 0.0f && ar >= 1.0f / 255.0f;
+                araw[k] = (OPAC || ok[k]) ? ar : 0.f;
                 alpha[k] = fminf(0.99f, araw[k]);
-                // position in the tile list before the pixel's last contributor; the pad entry
-                // has alpha 0.  Non-contributing pairs continue with alpha 0: T and A then pass
-                // through unchanged (1 / (1 - 0) == 1 exactly) and only dL/dalpha needs a mask.
-                ok[k] = gq.j[k] >= jlo && p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;
-                alpha[k] = ok[k] ? alpha[k] : 0.f;
+                if (OPAC) alpha[k] = ok[k] ? alpha[k] : 0.f;
                 any = any || ok[k];
             }
 #if GSR_STEPSTAT
@@ -388,7 +473,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 uint64_t pads = 0, oks = 0;
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    pads += __popcll(__ballot(gq.j[k] == BB));
+                    pads += __popcll(__ballot(jb[k] == 16 * BB));
                     oks += __popcll(__ballot(ok[k]));
                 }
                 st_pads += pads;
@@ -396,7 +481,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 st_csteps += __ballot(any) != 0ull;
 #pragma unroll
                 for (int k = 0; k < 4; k++) {  // (row, entry) items: listed, and listed with no contributing pixel
-                    const uint64_t okb = __ballot(ok[k]), padb = __ballot(gq.j[k] == BB);
+                    const uint64_t okb = __ballot(ok[k]), padb = __ballot(jb[k] == 16 * BB);
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         const bool listed = ((padb >> (16 * r)) & 0xFFFFull) == 0ull;
@@ -412,14 +497,17 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             float dLa[4], dch[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const float4 c = s_c[gq.j[k]];
+                const float4 c = rec(s_c, k);
                 float cd;
-                if (DUAL && Q2 == 1) {
-                    const float c2x = PACKC ? c.w : s_d[gq.j[k]].x;
+                if (DUAL && Q2 == 1 && PACKC) {  // (c.x, c.y) . dp01 + (c.z, c.w) . (dp2, dq0): pk_mul + pk_fma + add
+                    const v2f t = __builtin_elementwise_fma(v2f{c.z, c.w}, dp2q0, v2f{c.x, c.y} * dp01);
+                    cd = t.x + t.y;
+                } else if (DUAL && Q2 == 1) {
+                    const float c2x = rec(s_d, k).x;
                     const v2f t = v2f{c.x, c.y} * dp01;
                     cd = __builtin_fmaf(c.z, dp2, __builtin_fmaf(c2x, dq0, t.x + t.y));
                 } else if (DUAL) {
-                    const float4 c2 = s_d[gq.j[k]];
+                    const float4 c2 = rec(s_d, k);
                     const v2f t = v2f{c.x, c.y} * dp01 + v2f{c2.x, c2.y} * dq01;
                     cd = __builtin_fmaf(c.z, dp2, __builtin_fmaf(c2.z, dq2, t.x + t.y));
                 } else {
@@ -429,8 +517,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 const float inv = __builtin_amdgcn_rcpf(1.f - alpha[k]);   // v_rcp_f32 (~1 ulp)
                 const float Tn = T * inv;                                   // T / (1 - alpha), backward.cu:978
                 const float e = cd - A;
-                const bool o = ok[k];
-                dLa[k] = o ? __builtin_fmaf(Tbg, inv, e * Tn) : 0.f;
+                const float x = e * Tn;
+                dLa[k] = (OPAC && !ok[k]) ? 0.f : x;    // (without OPAC: h = araw dLa is 0 when masked)
                 dch[k] = alpha[k] * Tn;                 // 0 when masked
                 T = Tn;  // masked pairs: alpha = 0 and v_rcp_f32(1) == 1 exactly (tools/micro/rcp_one.hip)
                 A = __builtin_fmaf(alpha[k], e, A);     // unchanged when masked
@@ -439,10 +527,30 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             // h = G * dL/dG = (o * G) * dL/dalpha.  gauss_bwd turns them into the reference's
             // per-pair quantities (backward.cu:1020-1038): dmean2D = -ddel * (Q [hx, hy]),
             // dconic = -0.5 * (hxx, hxy, hyy); both are linear in the sums (Q is per Gaussian).
-            const uint32_t wlo = (my_e & 1) ? gw.y : gw.x, whi = (my_e & 1) ? gw.w : gw.z;  // selects, no branches
-            const uint32_t we = (my_e & 2) ? whi : wlo;
-            float* dst = s_acc + (we >> 16) * NV;  // the (entry, block) slot
-            if constexpr (NV <= 6) {  // one reduction over all values
+            float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(s_acc) + soff);  // the (entry, block) slot
+            if constexpr (MOM > 0) {  // backward_power == 2: the pair's second moments (gauss_bwd_mom_kernel)
+                float b[4][9];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    pair_geom<true>(b[k], araw[k], dLa[k], G[k], d[k]);  // u0..u4, G dL/dalpha
+                    pair_colours<true, false, Q2>(b[k] + 6, dch[k], dp01, dp2, dq0, dq01, dq2);
+                }
+                // passes of 4 moments (the reduction's cost is per value, so the pass size only sets
+                // how many products are live at once next to the 36 base values)
+                mom_pass<MOM, 0, 4>(b, lane, dst);
+                mom_pass<MOM, 4, 4>(b, lane, dst);
+                mom_pass<MOM, 8, 4>(b, lane, dst);
+                mom_pass<MOM, 12, 4>(b, lane, dst);
+                if constexpr (MOM == 1) {
+                    mom_pass<MOM, 16, 3>(b, lane, dst);
+                } else {
+                    mom_pass<MOM, 16, 4>(b, lane, dst);
+                    mom_pass<MOM, 20, 4>(b, lane, dst);
+                    mom_pass<MOM, 24, 4>(b, lane, dst);
+                    mom_pass<MOM, 28, 4>(b, lane, dst);
+                    mom_pass<MOM, 32, 5>(b, lane, dst);
+                }
+            } else if constexpr (NV <= 6) {  // one reduction over all values
                 float v[4 * NV];
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
@@ -845,6 +953,190 @@ hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, c
                   : (shl ? gauss_bwd_kernel<false, true> : gauss_bwd_kernel<false, false>);
     hipLaunchKernelGGL(k, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii, inst, rec, out, guard,
                        pose ? *pose : PoseFuse{});
+    return hipGetLastError();
+}
+
+// ------------------------------------------------ backward_power == 2 --
+// renderCUDAFused (backward.cu:850-1140) squares every per-pair output before summing it.  Every
+// output of a pair is linear in the pair's base values b = (u, G dL/dalpha, dch dL/dpix) with a
+// per-Gaussian coefficient row n (the chain, the conic and the NDC factor folded in), so
+//   sum_p (n . b_p)^2 = n (sum_p b_p b_p^T) n^T:
+// render_bwd forms the second moments sum_p b_p b_p^T (MOM layout, 19 or 37 sums per instance),
+// and this kernel applies the quadratic forms once per Gaussian, in double.
+hipError_t launch_render_bwd_moments(const Camera& cam, const uint2* ranges, const uint64_t* point_list, GeomPtrs geo,
+                                     const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, bool sh,
+                                     float* inst, BwdGuard guard, hipStream_t s) {
+    auto k = sh ? render_bwd_kernel<false, true, true, false, 3, 2> : render_bwd_kernel<false, true, true, false, 3, 1>;
+    hipLaunchKernelGGL(k, dim3(cam.gx * cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list, geo.rr, geo.blocksums,
+                       final_T, n_contrib, dL_dpix, nullptr, inst, guard, nullptr);
+    return hipGetLastError();
+}
+int moments_record_floats(bool sh) { return sh ? 38 : 20; }
+
+template <int MOM>
+__global__ void __launch_bounds__(256)
+gauss_bwd_mom_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii,
+                     const float* __restrict__ inst, GradsOut out, BwdGuard guard) {
+    constexpr int NV = MOM == 1 ? 19 : 37, RS = (NV + 1) & ~1;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.P) return;
+    const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
+    float S[NV];
+#pragma unroll
+    for (int q = 0; q < NV; q++) S[q] = 0.f;
+    const bool live = radii[i] > 0 && !guard.overflow();
+    if (live) {  // fixed-order sum of the Gaussian's instance records (deterministic)
+        const uint32_t off = geo.offsets[i], cnt = geo.tiles[i];
+        for (uint32_t e = 0; e < cnt; e++) {
+            const float2* r = reinterpret_cast<const float2*>(inst + (size_t)RS * (off + e));
+            float2 v[RS / 2];
+#pragma unroll
+            for (int m = 0; m < RS / 2; m++) v[m] = r[m];
+#pragma unroll
+            for (int m = 0; m < NV / 2; m++) {
+                S[2 * m] += v[m].x;
+                S[2 * m + 1] += v[m].y;
+            }
+            if (NV % 2) S[NV - 1] += v[NV / 2].x;
+        }
+    }
+    float Sm[9][9];
+    mom_matrix<MOM>(S, Sm, std::make_integer_sequence<int, NV>{});
+    float o_m2[2] = {0.f, 0.f}, o_mean[3] = {0.f, 0.f, 0.f}, o_cov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f},
+          o_scale[3] = {0.f, 0.f, 0.f}, o_rot[4] = {0.f, 0.f, 0.f, 0.f}, ysq[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) ysq[k] = 0.f;
+    unsigned clamped = 0u;
+    // sum_ab n_a n_b Sm[a][b] over the geometric terms a, b in [A0, 5) and, with nw, the masked colours
+    // (double: the terms of a quadratic form may cancel)
+    auto qform = [&](const float (&n)[5], const float* nw, int A0) -> float {
+        double acc = 0.0;
+#pragma unroll
+        for (int a = 0; a < 5; a++)
+#pragma unroll
+            for (int c = 0; c < 5; c++)
+                if (a >= A0 && c >= A0) acc += (double)n[a] * (double)n[c] * (double)Sm[a][c];
+        if (MOM == 2 && nw) {
+#pragma unroll
+            for (int a = 0; a < 5; a++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) acc += 2.0 * (double)n[a] * (double)nw[c] * (double)Sm[a][6 + c];
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+#pragma unroll
+                for (int e = 0; e < 3; e++) acc += (double)nw[c] * (double)nw[e] * (double)Sm[6 + c][6 + e];
+        }
+        return (float)acc;
+    };
+    if (live) {
+        const GaussGeom gg = load_geom(g, i);
+        float ca, cb, cc;
+        gaussian_conic(cam, g, gg, i, ca, cb, cc);
+        const float ddx = (float)(0.5 * cam.W), ddy = (float)(0.5 * cam.H);  // backward.cu:935-936
+        // chain input g2 = Lm u: dmean2D (NDC units) from (hx, hy), dconic = -u_conic / 2 (backward.cu:1020-1038)
+        const float L0[2] = {-ca * ddx, -cb * ddx}, L1[2] = {-cb * ddy, -cc * ddy};
+        {
+            const float n0[5] = {L0[0], L0[1], 0.f, 0.f, 0.f}, n1[5] = {L1[0], L1[1], 0.f, 0.f, 0.f};
+            o_m2[0] = qform(n0, nullptr, 0);
+            o_m2[1] = qform(n1, nullptr, 0);
+        }
+        // coefficient rows n = (chain column) Lm, accumulated one unit chain input at a time
+        float nm[3][5], nc[6][5], ns[3][5], nr[4][5], nw[3][3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+#pragma unroll
+            for (int b = 0; b < 5; b++) nm[r][b] = 0.f;
+#pragma unroll
+            for (int c = 0; c < 3; c++) nw[r][c] = 0.f;
+        }
+#pragma unroll 1
+        for (int kk = 0; kk < (MOM == 2 ? 8 : 5); kk++) {
+            const int in = kk < 5 ? kk : kk + 1;
+            float g2[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            g2[in] = 1.f;
+            float dmean[3], dcov[6], dscale[3], drot[4], dsh[48];
+            gauss_chain(cam, g, gg, i, g2, 0u, dmean, dcov, dscale, drot, dsh, nsh);
+            // (selects with constant indices: no dynamic register-array indexing)
+#pragma unroll
+            for (int b = 0; b < 5; b++) {
+                const float lk = kk == 0 ? (b == 0 ? L0[0] : (b == 1 ? L0[1] : 0.f))
+                                         : kk == 1 ? (b == 0 ? L1[0] : (b == 1 ? L1[1] : 0.f))
+                                                   : (kk == b ? -0.5f : 0.f);
+#pragma unroll
+                for (int r = 0; r < 3; r++) nm[r][b] = __builtin_fmaf(dmean[r], lk, nm[r][b]);
+                if (b >= 2) {  // cov3D / scale / rotation depend on the conic terms only
+#pragma unroll
+                    for (int r = 0; r < 6; r++) nc[r][b] = kk == b ? -0.5f * dcov[r] : (kk < 2 ? 0.f : nc[r][b]);
+#pragma unroll
+                    for (int r = 0; r < 3; r++) ns[r][b] = kk == b ? -0.5f * dscale[r] : (kk < 2 ? 0.f : ns[r][b]);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) nr[r][b] = kk == b ? -0.5f * drot[r] : (kk < 2 ? 0.f : nr[r][b]);
+                }
+            }
+            if (MOM == 2 && kk >= 5) {
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+#pragma unroll
+                    for (int r = 0; r < 3; r++) nw[r][c] = (kk - 5 == c) ? dmean[r] : nw[r][c];  // view-direction term
+                if (kk == 5)
+#pragma unroll
+                    for (int k = 0; k < 16; k++) ysq[k] = k < nsh ? dsh[3 * k] * dsh[3 * k] : 0.f;
+            }
+        }
+        clamped = g.shs ? geo.clamp[i] : 0u;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            float w3[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) w3[c] = ((clamped >> c) & 1u) ? 0.f : nw[r][c];
+            o_mean[r] = qform(nm[r], w3, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 6; r++) o_cov[r] = qform(nc[r], nullptr, 2);
+        if (g.scales) {  // the reference forms no scale / rotation gradient from a precomputed cov3D
+#pragma unroll
+            for (int r = 0; r < 3; r++) o_scale[r] = qform(ns[r], nullptr, 2);
+#pragma unroll
+            for (int r = 0; r < 4; r++) o_rot[r] = qform(nr[r], nullptr, 2);
+        }
+    }
+    if (out.dmeans2D) {
+        out.dmeans2D[3 * i] = o_m2[0];
+        out.dmeans2D[3 * i + 1] = o_m2[1];
+        out.dmeans2D[3 * i + 2] = 0.f;
+    }
+    if (out.dcolors)
+#pragma unroll
+        for (int c = 0; c < 3; c++) out.dcolors[3 * i + c] = Sm[6 + c][6 + c];
+    if (out.dopacity) out.dopacity[i] = Sm[5][5];
+#pragma unroll
+    for (int r = 0; r < 3; r++) out.dmeans3D[3 * i + r] = o_mean[r];
+    if (out.dcov3D)
+#pragma unroll
+        for (int r = 0; r < 6; r++) out.dcov3D[6 * i + r] = o_cov[r];
+    if (out.dscales)
+#pragma unroll
+        for (int r = 0; r < 3; r++) out.dscales[3 * i + r] = o_scale[r];
+    if (out.drot)
+#pragma unroll
+        for (int r = 0; r < 4; r++) out.drot[4 * i + r] = o_rot[r];
+    if (out.dsh && g.M > 0) {  // dsh[k][c] = Y_k dRGB_c per pair: Y_k^2 sum (dRGB_c)^2, 0 where the colour clamped
+        float* d = out.dsh + (size_t)3 * g.M * i;
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                if (k < g.M) d[3 * k + c] = !((clamped >> c) & 1u) ? ysq[k] * Sm[6 + c][6 + c] : 0.f;
+        for (int k = 16; k < g.M; k++)
+            for (int c = 0; c < 3; c++) d[3 * k + c] = 0.f;
+    }
+}
+
+hipError_t launch_gauss_bwd_moments(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii,
+                                    const float* inst, const GradsOut& out, BwdGuard guard, hipStream_t s) {
+    if (g.P == 0) return hipSuccess;
+    auto k = g.shs ? gauss_bwd_mom_kernel<2> : gauss_bwd_mom_kernel<1>;
+    hipLaunchKernelGGL(k, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii, inst, out, guard);
     return hipGetLastError();
 }
 

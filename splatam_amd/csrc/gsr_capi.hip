@@ -584,6 +584,35 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
             return hip_fail(e, "gaussian backward (fisher)");
         return GSR_OK;
     }
+    if (power == 2) {
+        // backward_power == 2 (the fork's Fisher / Hessian scoring, scripts/ros_handler.py:839-902): each
+        // pair's squared outputs are quadratic forms of its base values, so render_bwd forms per-instance
+        // second moments and gauss_bwd_mom applies the forms per Gaussian (gsr_backward.hip).  Outputs
+        // not requested (NULL) are skipped; dmeans3D is always formed.
+        const bool sh = g.shs != nullptr;
+        if (sh && (cam.sh_degree < 0 || cam.sh_degree > 3))
+            return fail(GSR_ERR_INVALID_ARG, "unsupported sh_degree for backward_power != 1");
+        if (num_rendered > 0 && !binning_buffer) return fail(GSR_ERR_INVALID_ARG, "missing binning buffer");
+        if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
+        const size_t rec_bytes = sizeof(float) * (size_t)moments_record_floats(sh) * (size_t)num_rendered;
+        float* rec = nullptr;
+        if (rec_bytes > 0) {
+            rec = (float*)obtain(alloc, alloc_ctx, GSR_BUF_SCRATCH, rec_bytes);
+            if (!rec) return fail(GSR_ERR_ALLOC, "allocator returned NULL (backward scratch)");
+        }
+        const BwdGuard guard{geo.counters, (uint32_t)num_rendered};
+        if (num_rendered > 0) {
+            const uint64_t* point_list = (const uint64_t*)((const char*)binning_buffer + BL.point_list);
+            StageTimer t(GSR_STAGE_RENDER_BWD, num_rendered, stream);
+            if ((e = launch_render_bwd_moments(cam, ranges, point_list, geo, final_T, n_contrib, dL_dout_color, sh, rec,
+                                               guard, stream)) != hipSuccess)
+                return hip_fail(e, "render backward (moments)");
+        }
+        StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
+        if ((e = launch_gauss_bwd_moments(cam, g, geo, radii, rec, out, guard, stream)) != hipSuccess)
+            return hip_fail(e, "gaussian backward (moments)");
+        return GSR_OK;
+    }
     if (power != 1) {
         if (!out.dmeans2D || !out.dcolors || !out.dopacity || !out.dcov3D || !out.dscales || !out.drot)
             return fail(GSR_ERR_INVALID_ARG, "backward_power != 1 needs every gradient output pointer, or only "
@@ -958,6 +987,7 @@ int gsr_backward_dual_sh_adam(const gsr_settings* settings, const gsr_gaussians*
     sa.omb2 = (float)(1.0 - sh_adam->beta2);
     sa.bc2_sqrt = (float)sqrt(1.0 - pow(sh_adam->beta2, (double)sh_adam->step));
     sa.eps = (float)sh_adam->eps;
+    sa.halted = sh_adam->halted;
     // sa.guard / sa.cap: the forward's own counters (backward_impl); sh_adam->status is not read
     return backward_impl(settings, gaussians, radii, dL_dout_color, colors2, dL_dout_color2, num_rendered,
                          geom_buffer, binning_buffer, image_buffer, 1, grads, dcolors2, dl2_channels, alloc, alloc_ctx,

@@ -430,10 +430,13 @@ __device__ __forceinline__ v2f pix_delta(float4 sa, v2f pix) {
 #pragma clang fp contract(off)
     return v2f{sa.x, sa.y} - pix;
 }
+// p2 = dx (A' dx + B' dy) + C' dy^2: one packed multiply and three single ops (v_pk_mul, 2 fma, mul)
+// after the packed delta; the forward and the backward evaluate the same expression, so their
+// alpha decisions agree bit for bit.
 __device__ __forceinline__ float eval_p2(float4 sa, float4 sb, v2f d) {
 #pragma clang fp contract(off)
     const v2f t = v2f{sa.z, sa.w} * d;  // (A' dx, C' dy)
-    return __builtin_fmaf(sb.x * d.x, d.y, __builtin_fmaf(t.x, d.x, t.y * d.y));
+    return __builtin_fmaf(__builtin_fmaf(sb.x, d.y, t.x), d.x, t.y * d.y);
 }
 
 // Pixel of thread tid within its 16x16 tile: wave w covers the 8x8 quadrant
@@ -666,9 +669,12 @@ __device__ __forceinline__ RowGroup4 load_row_group4(const uint16_t* row_list, i
 struct SlotLists {
     int len, cnt;
 };
+// jmul / smul scale the stored j and slot (the walk may take them as LDS byte offsets: j * record
+// size, slot * slot size; both must stay below 2^16).
 __device__ __forceinline__ SlotLists build_row_slot_lists(const uint16_t* s_mask, uint16_t* s_base, int cmax,
                                                          int budget, int w, const int (&jmin)[4], uint32_t* list,
-                                                         int stride, uint32_t pad) {
+                                                         int stride, uint32_t pad, uint32_t jmul = 1u,
+                                                         uint32_t smul = 1u) {
     const int lane = __lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
     const uint32_t below_w = (1u << (4 * w)) - 1u;  // blocks of the waves before this one
@@ -699,7 +705,9 @@ __device__ __forceinline__ SlotLists build_row_slot_lists(const uint16_t* s_mask
         for (int r = 0; r < 4; r++) {
             const bool bit = fits && ((m >> r) & 1u) && j >= jmin[r];
             const uint64_t bal = __ballot(bit);
-            if (bit) list[r * stride + n[r] + __popcll(bal & lt)] = (uint32_t)j | ((sb + __popc(m & ((1u << r) - 1u))) << 16);
+            if (bit)
+                list[r * stride + n[r] + __popcll(bal & lt)] =
+                    (uint32_t)j * jmul | ((sb + __popc(m & ((1u << r) - 1u))) * smul << 16);
             n[r] += __popcll(bal);
         }
     }
@@ -1276,6 +1284,7 @@ struct ShAdam {
     float ss = 0.f, w1 = 0.f, beta2 = 0.f, omb2 = 0.f, bc2_sqrt = 1.f, eps = 0.f;
     const uint32_t* guard = nullptr;  // the forward's status row / counters: skip the step on an overflow
     uint32_t cap = 0;
+    uint32_t* halted = nullptr;       // gsr_map_adam.halted (sticky skip)
 };
 hipError_t launch_sh_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* drgb,
                          float* dmeans3D, float* dsh, BwdGuard guard, hipStream_t s, const ShAdam& sa = ShAdam{});
@@ -1283,6 +1292,13 @@ hipError_t launch_sh_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, cons
 int fail(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* where);
 // backward_power != 1 (the vendored renderCUDAFused semantics, backward.cu:850-1140)
+// backward_power == 2 through per-instance second moments (gsr_backward.hip, gauss_bwd_mom_kernel)
+int moments_record_floats(bool sh);
+hipError_t launch_render_bwd_moments(const Camera& cam, const uint2* ranges, const uint64_t* point_list, GeomPtrs geo,
+                                     const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, bool sh,
+                                     float* inst, BwdGuard guard, hipStream_t s);
+hipError_t launch_gauss_bwd_moments(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii,
+                                    const float* inst, const GradsOut& out, BwdGuard guard, hipStream_t s);
 constexpr int JAC_FLOATS = 84;  // per-Gaussian linear chain pack, see gsr_backward_power.hip
 constexpr int JAC_CONIC = 80;   // conic (A, B, C) inside the pack
 int power_record_floats(int nsh);  // values stored per instance record

@@ -950,7 +950,8 @@ __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, E
 //                keys below it -- exact, as the keys are unique in a tile.
 // The result equals a stable (tile, depth) radix order (ids break depth ties).
 #ifndef GSR_FWD_ABLATE
-#define GSR_FWD_ABLATE 0  // timing ablations (tools/ablate.sh); 0 in every real build
+#define GSR_FWD_ABLATE 0  // timing ablations (tools/ablate.sh; results invalid): 1 no per-tile sort, 2 no walk,
+                          // 4 no tracking-loss epilogue.  0 in every real build
 #endif
 __device__ __forceinline__ void tile_sort_bucket(uint64_t* __restrict__ src, uint32_t cnt,
                                                  PointEntry* __restrict__ dst, uint64_t* sk) {
@@ -1263,7 +1264,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         const int n = build_row_lists(s_mask, cnt, w, jmin0, s_list + 4 * w * LS, LS, (uint16_t)RENDER_BATCH);
         const uint16_t* my_list = s_list + (4 * w + row) * LS;
         const uint32_t pos0 = start - range.x;
-        for (int i = 0; i < n; i += 4) {
+        for (int i = 0; i < (GSR_FWD_ABLATE == 2 ? 0 : n); i += 4) {
             if (__ballot(!done) == 0ull) break;
             const RowGroup4 gq = load_row_group4(my_list, i);
             float alpha[4], depth[4];
@@ -1309,7 +1310,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
     // the loss epilogue's inputs are loaded before the image stores: a load issued after a store
     // also waits for the store's completion (vmcnt counts both)
     float l1_seed = 0.f, l1_gd = 0.f, l1_gi[3] = {0.f, 0.f, 0.f};
-    if constexpr (L1) {
+    if constexpr (L1 && GSR_FWD_ABLATE != 4) {
         if (inside) {
             const int pid = py * cam.W + px;
             const int HW = cam.W * cam.H;
@@ -1334,7 +1335,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
             out_color2[2 * HW + pid] = C5 + T * cam.bg[2];
         }
     }
-    if constexpr (L1) {
+    if constexpr (L1 && GSR_FWD_ABLATE != 4) {
         // get_loss(tracking=True) on this pixel (gsr_glue.hip track_l1_kernel, same expressions on the
         // values just written): mask = gt_depth > 0 & !isnan(depth) & !isnan(depth_sq - depth^2) &
         // silhouette > thres; sums of |gt - x| over the mask; dL/dx = -sgn(gt - x) * w * dL/dloss

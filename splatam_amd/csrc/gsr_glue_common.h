@@ -148,6 +148,16 @@ __device__ __forceinline__ void track_xform_store(int i, const float (&m)[3], fl
 __device__ __forceinline__ bool forward_overflowed(const uint32_t* st, uint32_t cap) {
     return st && (st[0] > cap || st[2] > st[3] || st[1] != 0u);
 }
+// The fused mapping steps' skip decision: the forward overflowed, or an earlier step of the frame
+// was skipped (`halted`, gsr_map_adam.halted: sticky until the caller resets the optimizer).  A skip
+// caused by an overflow sets `halted` (a plain vector store from one lane per workgroup; every
+// workgroup of a launch takes the same decision from the same counters).
+__device__ __forceinline__ bool fused_step_skipped(const uint32_t* st, uint32_t cap, uint32_t* halted) {
+    if (halted && *reinterpret_cast<volatile uint32_t*>(halted) != 0u) return true;
+    if (!forward_overflowed(st, cap)) return false;
+    if (halted && threadIdx.x == 0) *halted = 1u;
+    return true;
+}
 
 struct PoseAdam {  // torch.optim.Adam (no weight decay, no amsgrad) on the frame's pose column
     double lr_q, lr_t, beta1, beta2;   // torch's hyperparameters are python floats (double)

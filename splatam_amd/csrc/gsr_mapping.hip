@@ -376,6 +376,7 @@ struct MapAdam {  // the mapping optimizer's state, applied in place (NULL p: wr
     float w1, beta2, omb2, bc2_sqrt, eps;
     const uint32_t* guard;  // status row of the iteration's forward: skip the step on an overflow
     uint32_t cap;
+    uint32_t* halted;       // gsr_map_adam.halted (sticky skip), or nullptr
 };
 
 __device__ __forceinline__ float adam_apply(float* p, float g, float* m, float* v, float ss, const MapAdam& a) {
@@ -426,7 +427,7 @@ map_transform_bwd_kernel(int P, const float* ur, const float* lo, const float* l
     // and every lane reads its own elements before it stores them
     const int i = blockIdx.x * GLUE_BLOCK + threadIdx.x;
     const bool step = adam.p[0] != nullptr;
-    if (step && forward_overflowed(adam.guard, adam.cap)) return;  // invalid gradients: nothing changes
+    if (step && fused_step_skipped(adam.guard, adam.cap, adam.halted)) return;  // invalid gradients: nothing changes
     if (step && gcol && i < P) {  // colour parameters: element k * P + i (coalesced across the wave)
         constexpr int CU = 4;  // colour columns per round trip
         int k = 0;
@@ -661,6 +662,7 @@ int gsr_map_transform_bwd_adam(int P, float* means_world, float* unnorm_rot, flo
     fill_adam_common(adam->beta1, adam->beta2, adam->eps, adam->step, a.w1, a.beta2, a.omb2, a.bc2_sqrt, a.eps);
     a.guard = adam->status;
     a.cap = adam->capacity;
+    a.halted = adam->halted;
     hipLaunchKernelGGL(map_transform_bwd_kernel, dim3((P + GLUE_BLOCK - 1) / GLUE_BLOCK), dim3(GLUE_BLOCK), 0,
                        (hipStream_t)stream, P, unnorm_rot, logit_opac, log_scales, scale_cols, cam_q, q_stride,
                        means_cam, w2c, dL_dmeans_cam, dL_drot, dL_ddepth_colors, dL_dopac, dL_dscales, nullptr,

@@ -14,14 +14,14 @@
 //                   view-direction term added to dL/dmeans3D, after gauss_bwd has
 //                   written dL/dcolor into a scratch array.
 #include "gsr_chain.h"
+#include "gsr_glue_common.h"
 
 namespace gsr {
 namespace {
 
 constexpr int SH_BLOCK = 256;
 // sh_eval: one wave per workgroup (12.5 KB of LDS at D = 3): the waves of a CU stage and evaluate
-// independently instead of in barrier-coupled groups of four (GSR_SH_EVAL_WAVES: several such waves
-// per workgroup, each with its own LDS rows and no workgroup barrier)
+// independently instead of in barrier-coupled groups of four
 
 template <int NSH>
 struct ShTile {
@@ -150,16 +150,12 @@ __device__ __forceinline__ void adam_rows(float* p, float* m, float* v, const fl
     }
 }
 
-#ifndef GSR_SH_EVAL_WAVES
-#define GSR_SH_EVAL_WAVES 1  // waves per sh_eval workgroup, each staging and evaluating its own 64 Gaussians
-#endif
 template <int NSH>
-__global__ void __launch_bounds__(64 * GSR_SH_EVAL_WAVES) sh_eval_kernel(Camera cam, GaussIn g, GeomPtrs geo) {
+__global__ void __launch_bounds__(64) sh_eval_kernel(Camera cam, GaussIn g, GeomPtrs geo) {
     using T = ShTile<NSH>;
-    __shared__ float s_all[GSR_SH_EVAL_WAVES * 64 * T::PITCH];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float* s_sh = s_all + wv * 64 * T::PITCH;
-    const int base = (blockIdx.x * GSR_SH_EVAL_WAVES + wv) * 64;
+    __shared__ float s_sh[64 * T::PITCH];
+    const int lane = threadIdx.x;
+    const int base = blockIdx.x * 64;
     const int n = min(64, g.P - base);
     if (n <= 0) return;
     const int i = base + lane;
@@ -167,19 +163,12 @@ __global__ void __launch_bounds__(64 * GSR_SH_EVAL_WAVES) sh_eval_kernel(Camera 
     // the lane's mean is loaded with the staging stream, not after it
     const float3 p = act ? make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2])
                          : make_float3(0.f, 0.f, 0.f);
-    if (GSR_SH_EVAL_WAVES == 1) {
-        stage_rows<NSH, 64>(s_sh, g.shs + (size_t)T::ROW * base, n);
-        __syncthreads();
-    } else {  // wave-local staging: the wave's 64 rows, no workgroup barrier (each wave reads only its own)
-        stage_rows<NSH, 64>(s_sh, g.shs + (size_t)T::ROW * base, n, lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
+    stage_rows<NSH, 64>(s_sh, g.shs + (size_t)T::ROW * base, n);
+    __syncthreads();
     if (!act) return;
     float rgb[3];
     unsigned clamped = 0;
-    sh_fwd(cam.sh_degree, p, cam.campos, s_sh + threadIdx.x * T::PITCH, rgb, clamped);
+    sh_fwd(cam.sh_degree, p, cam.campos, s_sh + lane * T::PITCH, rgb, clamped);
     // handed to preprocess through bin[i] (dense 16-B rows, one full line per 4 Gaussians; preprocess
     // reads it first and overwrites it with the binning record) instead of the render record's rgb slot
     // (16 B every 64 B: partial-line writes here, 64-B line reads there)
@@ -218,8 +207,7 @@ sh_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii
     }
     __syncthreads();
     if (sa.m) {  // the colour Adam step in place of the dsh round trip through HBM
-        const uint32_t* st = sa.guard;
-        if (st && (st[0] > sa.cap || st[2] > st[3] || st[1] != 0u)) return;  // overflowing forward: no step
+        if (fused_step_skipped(sa.guard, sa.cap, sa.halted)) return;  // overflowing forward (or an earlier skip): no step
         const size_t o = (size_t)T::ROW * base;
         adam_rows<NSH>(const_cast<float*>(g.shs) + o, sa.m + o, sa.v + o, s_sh, n, sa);
     } else if (dsh) {
@@ -229,7 +217,7 @@ sh_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii
 
 template <int NSH>
 hipError_t launch_sh_eval_t(const Camera& cam, const GaussIn& g, GeomPtrs geo, hipStream_t s) {
-    constexpr int per = 64 * GSR_SH_EVAL_WAVES;
+    constexpr int per = 64;
     hipLaunchKernelGGL(sh_eval_kernel<NSH>, dim3((g.P + per - 1) / per), dim3(per), 0, s, cam, g, geo);
     return hipGetLastError();
 }

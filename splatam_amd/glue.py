@@ -260,15 +260,24 @@ class MapAdam:
         self.capacity = 0
         # (geom_buffer, counters offset, capacity) of the current iteration's static forward, set by
         # rasterize_gaussians_dual(guard_sink=...): the fused steps guard on that call's own counters.
-        # The host `step` still advances when the device skips an overflowing iteration's step, so
-        # after an overflow the frame must be re-run from reset() (GraphMapper.run(check=True) raises).
         self.guard = None
+        # gsr_map_adam.halted: set on the device when a step is skipped because its forward overflowed;
+        # every later fused step of the frame is then skipped too (the host `step` keeps counting, so a
+        # later step would otherwise apply bias corrections for a step count the state never reached).
+        # reset() clears it; halted() reads it (one host sync).
+        self.halted_word = torch.zeros(1, dtype=torch.int32, device=params[self.keys[0]].device)
 
     def reset(self):
         for t in self.exp_avg + self.exp_avg_sq:
             t.zero_()
         self.step = 0
         self.guard = None
+        self.halted_word.zero_()
+
+    def halted(self) -> bool:
+        """True if a fused step of this frame was skipped (forward overflow): the frame must be re-run
+        from reset() with more binning capacity.  One host sync."""
+        return bool(self.halted_word.item() != 0)
 
     def struct(self):
         from ._lib import GsrMapAdam
@@ -284,6 +293,7 @@ class MapAdam:
         else:
             s.status = self.status.data_ptr() if self.status is not None else None
             s.capacity = int(self.capacity)
+        s.halted = self.halted_word.data_ptr()
         return s
 
 

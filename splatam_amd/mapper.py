@@ -163,13 +163,15 @@ class GraphMapper:
         torch.autograd.backward(loss, self.seed)
         return loss.detach()
 
-    def run(self, check: bool = False, sequence=None):
-        """Enqueue one frame's mapping (one graph launch, no host sync).  With `redraw` the keyframe of
-        every iteration is drawn now (splatam.py:851; `sequence` overrides the draw) and gathered into the
-        slots.  An iteration whose forward overflowed skips its own Adam step (the steps guard on that
-        forward's counters), but the bias corrections of the later steps still count it; with `check`
-        the replay ends with one host sync and raises on any overflow, so the caller can rebuild with
-        more headroom and re-map the frame."""
+    def run(self, check: bool = True, sequence=None):
+        """Enqueue one frame's mapping (one graph launch).  With `redraw` the keyframe of every iteration
+        is drawn now (splatam.py:851; `sequence` overrides the draw) and gathered into the slots.  An
+        iteration whose forward overflowed skips its Adam step, and so does every later iteration of the
+        frame (MapAdam.halted_word, sticky on the device), so the parameters are those of the last good
+        iteration and no step uses mismatched bias corrections.  `check` (the default) ends the replay
+        with one host sync and raises on an overflow, so the caller can rebuild with more headroom and
+        re-map the frame; check=False (timing loops) enqueues without a sync -- read overflowed()
+        afterwards."""
         if self.redraw:
             n = len(self.keyframes)
             seq = [int(self.rng.randint(0, n)) for _ in range(self.iters)] if sequence is None else \
@@ -191,9 +193,11 @@ class GraphMapper:
         self.status.zero_()
 
     def overflowed(self) -> bool:
-        """True if any iteration since the last reset_status() exceeded the binning capacity (one host sync)."""
+        """True if any iteration since the last reset_status() exceeded the binning capacity, or the last
+        replay's optimizer halted (one host sync)."""
         st = self.status.cpu()
-        return bool((st[:, 0] > self.capacity).any() or (st[:, 2] > TILE_SORT_CAP).any() or (st[:, 1] != 0).any())
+        return bool((st[:, 0] > self.capacity).any() or (st[:, 2] > TILE_SORT_CAP).any() or (st[:, 1] != 0).any()
+                    or self.adam.halted())
 
     def num_rendered(self) -> list[int]:
         return [int(x) for x in self.status[:, 0].cpu()]

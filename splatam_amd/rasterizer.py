@@ -119,10 +119,18 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
             s.bg, means3D, colors_precomp, colors2, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
             s.campos, s.prefiltered, capacity=capacity, status=status)
-        if guard_sink is not None and capacity > 0:
-            # the fused optimizer steps of this iteration guard on this forward's own counters
-            # (the geometry buffer stays referenced until the next iteration replaces it)
-            guard_sink.guard = (geomBuffer, int(lib.gsr_geom_counters_offset(means3D.shape[0])), int(num_rendered))
+        if guard_sink is not None:
+            if capacity > 0:
+                # the fused optimizer steps of this iteration guard on this forward's own counters
+                # (the geometry buffer stays referenced until the next iteration replaces it); the
+                # geometry layout depends on the device's CU count, so the offset is taken on its device
+                with torch.cuda.device(means3D.device):
+                    off = int(lib.gsr_geom_counters_offset(means3D.shape[0]))
+                guard_sink.guard = (geomBuffer, off, int(num_rendered))
+            else:
+                # an eager forward (no static capacity) never overflows silently: no stale guard from an
+                # earlier static forward may decide this iteration's optimizer steps
+                guard_sink.guard = None
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
         ctx.grad2_channels = grad2_channels

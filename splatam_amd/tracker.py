@@ -146,12 +146,14 @@ class GraphTracker:
             self.params["cam_unnorm_rots"][0, :, self.t] = self.adam.best[1:5]
             self.params["cam_trans"][0, :, self.t] = self.adam.best[5:8]
 
-    def track_frame(self, num_iters: int, check: bool = False):
+    def track_frame(self, num_iters: int, check: bool = True):
         """One frame's tracking: begin_frame, num_iters iterations (a multiple of iters_per_graph), end_frame.
 
         An iteration whose forward overflowed skips its own pose step (the fused steps guard on that
-        forward's counters, not on the sticky status rows), so later iterations are unaffected; with
-        `check` the frame ends with one host sync and raises if any iteration of it overflowed."""
+        forward's counters, not on the sticky status rows; the pose optimizer's step count lives on the
+        device, so later iterations are consistent).  `check` (the default) ends the frame with one host
+        sync and raises if any iteration of it overflowed -- the frozen pose is never returned silently;
+        check=False (timing loops) skips the sync: read overflowed() afterwards."""
         if num_iters % self.iters:
             raise ValueError(f"num_iters {num_iters} is not a multiple of iters_per_graph {self.iters}")
         if check:

@@ -95,23 +95,29 @@ def test_fisher_selective_path(cuda, power, aniso, bg):
         r_full = harness.rel_l2(sel["grads"][k], full["grads"][k])
         r_ref = harness.rel_l2(sel["grads"][k], ref[k].reshape(sel["grads"][k].shape))
         print(f"power {power} {k}: rel L2 vs full path {r_full:.2e}, vs oracle {r_ref:.2e}")
-        assert r_full <= 2e-6, (k, r_full)
+        assert r_full <= 2e-5, (k, r_full)  # (power 2: the full path sums second moments; see config 3)
         assert r_ref <= 1e-4, (k, r_ref)
     if power % 2 == 0:
         assert (sel["grads"]["dmeans3D"] >= 0).all() and (sel["grads"]["dopacity"] >= 0).all()
 
 
 def test_fisher_selective_config3(cuda):
-    """Full-size BASELINE config 3 (300k Gaussians, 640x480): the selective Hessian of a seeded power-2
-    render vs the full power path and the float32 oracle."""
+    """Full-size BASELINE config 3 (300k Gaussians, 640x480), the drop-in compute_Hessian request
+    (scripts/ros_handler.py:873-885: every rendervar requires grad, backward_power=2, seed 1e-3): every
+    gradient of the full power-2 path (per-instance second moments, gauss_bwd_mom_kernel) against the
+    float32 oracle's fused mode (per-pair powf, backward.cu:850-1140) at 1e-4 relative L2, and the
+    selective Hessian (dmeans3D + dopacity only) against both."""
     from splatam_amd.scenes import config_scene
     scene = config_scene(3)
     dpix = np.full((3, scene.cam.H, scene.cam.W), 1e-3, np.float32)
     sel = harness.run_gpu(scene, dpix, device=cuda, power=2, grads_for=("means3D", "opacities"))
     full = harness.run_gpu(scene, dpix, device=cuda, power=2)
     _, ref = harness.run_oracle(scene, dpix, power=2, mode=oracle.FUSED)
+    errs = harness.compare_grads(full["grads"], ref)
+    print("config 3 full power-2 path vs oracle:", {k: f"{v:.2e}" for k, v in errs.items()})
+    assert not {k: v for k, v in errs.items() if v > 1e-4}, errs
     for k in ("dmeans3D", "dopacity"):
         r_full = harness.rel_l2(sel["grads"][k], full["grads"][k])
         r_ref = harness.rel_l2(sel["grads"][k], ref[k].reshape(sel["grads"][k].shape))
         print(f"config 3 {k}: rel L2 vs full path {r_full:.2e}, vs oracle {r_ref:.2e}")
-        assert r_full <= 2e-6 and r_ref <= 1e-4, (k, r_full, r_ref)
+        assert r_full <= 2e-5 and r_ref <= 1e-4, (k, r_full, r_ref)

@@ -101,6 +101,23 @@ def test_track_frame_best_candidate(cuda, fuse_pose):
         print("best iteration", ties, "of", N)
 
 
+def test_track_frame_raises_on_overflow_by_default(cuda):
+    """The default track_frame() call never returns a frozen pose silently: an overflowing frame raises."""
+    from splatam_amd.tracker import GraphTracker
+    scene = make_scene(5000, 160, 120, seed=3)
+    params, curr = _frames(cuda, scene, 2)
+    p = _pose_leaves(params)
+    tr = GraphTracker(p, curr[1], 1, iters_per_graph=3, warmup_iters=1, fuse_pose=True, headroom=1.25, min_extra=0)
+    with torch.no_grad():
+        p["log_scales"].add_(1.0)
+    with pytest.raises(RuntimeError, match="capacity"):
+        tr.track_frame(3)
+    with torch.no_grad():
+        p["log_scales"].sub_(1.0)
+    tr.track_frame(3)  # a good frame passes the default check
+    assert not tr.overflowed()
+
+
 def test_status_is_sticky_and_overflow_freezes_pose(cuda):
     """Replay 1 overflows (the map grows in place), replay 2 does not: the status still reports the
     overflow until reset_status(); during replay 1 the pose did not move."""

@@ -315,6 +315,55 @@ def test_graph_mapper_matches_eager_iterations(cuda, sh):
         assert float(close.float().mean()) >= 0.995, (k, float(close.float().mean()))
 
 
+def test_graph_mapper_overflow_halts_and_raises(cuda):
+    """An overflowing mapping forward skips its Adam step and halts every later step of the frame
+    (MapAdam.halted_word, sticky on the device), so the parameters stay those of the last good
+    iteration; run() checks by default and raises, run(check=False) leaves overflowed() to report it."""
+    from splatam_amd.mapper import GraphMapper
+    _, params, cam = _map_params(cuda, True, False)
+    kfs = _keyframes(params, cam, cuda)
+    key = slam.color_key(params)
+    keys = GAUSS_KEYS + (key,)
+    p = {k: v.clone() for k, v in params.items()}
+    for k in keys:
+        p[k].requires_grad_(True)
+    mapper = GraphMapper(p, kfs, iters_per_graph=4, seed=3, headroom=1.0, min_extra=0)
+    with torch.no_grad():
+        p["log_scales"].add_(1.0)  # 2.7x larger footprints: far more tile instances than the capacity
+    before = {k: p[k].detach().clone() for k in keys}
+    with pytest.raises(RuntimeError, match="capacity"):
+        mapper.run()
+    for k in keys:
+        assert torch.equal(p[k].detach(), before[k]), k
+    assert mapper.adam.halted()
+    mapper.run(check=False)
+    torch.cuda.synchronize()
+    assert mapper.overflowed()
+
+
+def test_map_adam_halted_skips_later_steps(cuda):
+    """A set halted word (an earlier skipped step of the frame) makes the fused steps of a valid
+    iteration skip too: nothing moves until reset()."""
+    _, params, cam = _map_params(cuda, True, False)
+    kfs = _keyframes(params, cam, cuda, K=1)
+    key = slam.color_key(params)
+    keys = GAUSS_KEYS + (key,)
+    p = {k: v.clone() for k, v in params.items()}
+    for k in keys:
+        p[k].requires_grad_(True)
+    adam = MapAdam(p, slam.MappingConfig().lrs, color_key=key)
+    adam.halted_word.fill_(1)
+    loss, _, _ = slam.get_loss_mapping(p, kfs[0], 0, fused=True, adam=adam)
+    loss.backward()
+    for k in keys:
+        assert torch.equal(p[k].detach(), params[k]), k
+    adam.reset()
+    assert not adam.halted()
+    loss, _, _ = slam.get_loss_mapping(p, kfs[0], 0, fused=True, adam=adam)
+    loss.backward()
+    assert not torch.equal(p["means3D"].detach(), params["means3D"])
+
+
 def test_fused_adam_through_gaussian_surgery(cuda):
     """FusedAdam keeps torch's state layout, so SplaTAM's optimizer surgery (remove_points /
     cat_params_to_optimizer, slam_external.py:122-163) works on it: after pruning and
