@@ -83,7 +83,7 @@ def build_diag() -> str:
 
 
 def build_variant(tag: str, defines=()) -> str:
-    """Timing-experiment library (tools/ablate.sh): libgsr built with extra -D flags into
+    """Timing-experiment library (tools/gpu_round.sh ab= / abbench= steps): libgsr built with extra -D flags into
     splatam_amd/_build_<tag>/libgsr_<tag>.so; loaded only through GSR_LIB."""
     objdir = os.path.join(HERE, f"_build_{tag}")
     os.makedirs(objdir, exist_ok=True)
@@ -105,5 +105,41 @@ def build_variant(tag: str, defines=()) -> str:
     return os.path.join(DIAG, f"libgsr_{tag}.so")
 
 
+def build_from_rev(rev: str, tag: str) -> str:
+    """A/B baseline without macros in the sources: libgsr built from the csrc/ and include/ trees of git
+    revision `rev` (exported to a scratch directory) into splatam_amd/_diag/libgsr_<tag>.so, which
+    tools/gpu_round.sh's ab= / abbench= steps load through GSR_LIB."""
+    import tempfile
+    work = tempfile.mkdtemp(prefix=f"gsr_{tag}_")
+    for sub in ("splatam_amd/csrc", "include"):
+        r = subprocess.run(f"git -C {ROOT} archive {rev} {sub} | tar -x -C {work}", shell=True,
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"git archive {rev} {sub} failed: {r.stderr}")
+    csrc, inc = os.path.join(work, "splatam_amd", "csrc"), os.path.join(work, "include")
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(work, os.path.splitext(src)[0] + ".o")
+        base = flags()
+        base = [f for i, f in enumerate(base) if f != "-I" and (i == 0 or base[i - 1] != "-I")]  # (drop -I pairs)
+        cmd = [hipcc(), *base, "-I", inc, "-I", csrc, "-c", os.path.join(csrc, src), "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src} at {rev}:\n{r.stderr}")
+        objs.append(obj)
+    os.makedirs(DIAG, exist_ok=True)
+    lib = os.path.join(DIAG, f"libgsr_{tag}.so")
+    r = subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    shutil.rmtree(work, ignore_errors=True)
+    return lib
+
+
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
+    if "--from-rev" in sys.argv:  # python -m splatam_amd.build --from-rev REV TAG
+        i = sys.argv.index("--from-rev")
+        print(build_from_rev(sys.argv[i + 1], sys.argv[i + 2]))
+    else:
+        print(build(force="--force" in sys.argv))

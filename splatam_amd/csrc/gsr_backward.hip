@@ -18,51 +18,15 @@
 #include <utility>
 
 #include "gsr_chain.h"
+#include "gsr_diag.h"
 #include "gsr_glue_common.h"
 
-#ifndef GSR_ABLATE
-#define GSR_ABLATE 0  // timing ablations (tools/ablate.sh); 0 in every real build
-#endif
 #ifndef GSR_POSE_TAIL
 #define GSR_POSE_TAIL 2  // levels of the fused pose reduction's last-workgroup sum (1 or 2)
 #endif
 
 namespace gsr {
 GSR_WGTIME_TABLE
-#ifndef GSR_STEPSTAT
-#define GSR_STEPSTAT 0  // diagnostics build only (tools/stepstat.py): render_bwd step statistics
-#endif
-#if GSR_STEPSTAT
-// [wave-steps, wave-steps with a contributing pair, contributing (lane, entry) pairs, pad (lane, entry) slots,
-//  batches x waves]
-static __device__ unsigned long long g_stepstat[8];
-#endif
-#ifndef GSR_PHASE
-#define GSR_PHASE 0  // diagnostics build only (tools/phase_bwd.py): per-wave s_memtime cycles per render_bwd phase
-#endif
-#if GSR_PHASE
-// per-wave shader-clock cycles summed over all waves: [0] prologue (pixel inputs, row maxima, zero records
-// behind the last contributors, first staging loads), [1] batch staging stores + barrier, [2] row / slot list
-// build, [3] row walk, [4] barrier after the walk, [5] entry totals + record stores, [6] barrier after the
-// totals, [7] batches x waves
-static __device__ unsigned long long g_phase[8];
-#define PHASE_T0() unsigned long long ph_t = __builtin_amdgcn_s_memtime(); unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
-#define PHASE_MARK(k)                                                           \
-    do {                                                                        \
-        const unsigned long long ph_n = __builtin_amdgcn_s_memtime();           \
-        ph_acc[k] += ph_n - ph_t;                                               \
-        ph_t = ph_n;                                                            \
-    } while (0)
-#define PHASE_FLUSH()                                                           \
-    do {                                                                        \
-        if ((threadIdx.x & 63) == 0)                                            \
-            for (int k_ = 0; k_ < 8; k_++) atomicAdd(&g_phase[k_], ph_acc[k_]); \
-    } while (0)
-#else
-#define PHASE_T0() do {} while (0)
-#define PHASE_MARK(k) do {} while (0)
-#define PHASE_FLUSH() do {} while (0)
-#endif
 
 // Per-pair geometric terms (hx, hy, hx dx, hx dy, hy dy[, G dL/dalpha]) with
 // h = G * dL/dG = (o * G) * dL/dalpha.
@@ -163,71 +127,80 @@ constexpr int bwd_slots() { return MOM == 1 ? 256 : (MOM == 2 ? 128 : (NV <= 6 ?
 // Gaussian) instance at its unsorted position.
 // 5 workgroups per CU (<= 96 VGPRs): a 640x480 frame's 1200 tiles are all resident
 // at once, so there is no second dispatch round behind the slowest tiles.
-// MOM (backward_power == 2, gauss_bwd_mom_kernel): the pair's second moments instead of its values --
-// 1: colours precomputed, 19 sums (u u^T upper triangle of the 5 geometric terms, (G dL/dalpha)^2,
-// (dch dL/dpix_c)^2); 2: SH colours, 37 sums (+ the colour terms' cross moments with u and each other).
+// MOM (backward_power == 2, gauss_bwd_mom_kernel): the pair's second moments instead of its values.
+// The geometric terms are u = h (dx, dy, dx^2, dx dy, dy^2) (h = G dL/dG), so u_i u_j = h^2 dx^a dy^b
+// with a + b in {2, 3, 4}: 12 distinct monomial moments instead of 15 products.  Layout:
+//   [0, 12)  sum h^2 dx^a dy^b, monomial t: (2,0) (1,1) (0,2) | (3,0) (2,1) (1,2) (0,3) | (4,0) (3,1) (2,2) (1,3) (0,4)
+//   12       sum (G dL/dalpha)^2
+//   MOM 1 (colours precomputed, 16 sums): [13, 16) sum (dch dL/dpix_c)^2
+//   MOM 2 (SH colours, 34 sums): [13, 19) sum dch^2 dL/dpix_c dL/dpix_d (c <= d, row-major),
+//                                [19, 34) sum u_i dch dL/dpix_c (i-major)
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2, int MOM = 0>
-constexpr int bwd_nv() { return MOM == 1 ? 19 : (MOM == 2 ? 37 : 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2 : 0)); }
-// Moment q of the MOM layout as the product b_i b_j of the pair's base values b = (u0..u4, G dL/dalpha,
-// dch dL/dpix_0..2): [0, 15) u_i u_j (i <= j, row-major), 15 b5 b5, then MOM 1: b_{6+c}^2; MOM 2: the 6
-// colour products (c <= d, row-major), then u_i b_{6+c} (i-major).
-__host__ __device__ constexpr int mom_i(int mom, int q) {
-    if (q < 15) {
-        int i = 0, r = q;
-        while (r >= 5 - i) r -= 5 - i++;
-        return i;
-    }
-    if (q == 15) return 5;
-    if (mom == 1) return 6 + (q - 16);
-    if (q < 22) {
-        int i = 0, r = q - 16;
-        while (r >= 3 - i) r -= 3 - i++;
-        return 6 + i;
-    }
-    return (q - 22) / 3;
+constexpr int bwd_nv() { return MOM == 1 ? 16 : (MOM == 2 ? 34 : 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2 : 0)); }
+__host__ __device__ constexpr int mono_t(int a, int b) {  // monomial index of dx^a dy^b, a + b in {2, 3, 4}
+    return a + b == 2 ? 2 - a : (a + b == 3 ? 3 + (3 - a) : 7 + (4 - a));
 }
-__host__ __device__ constexpr int mom_j(int mom, int q) {
-    if (q < 15) {
-        int i = 0, r = q;
-        while (r >= 5 - i) r -= 5 - i++;
-        return i + r;
-    }
-    if (q == 15) return 5;
-    if (mom == 1) return 6 + (q - 16);
-    if (q < 22) {
-        int i = 0, r = q - 16;
-        while (r >= 3 - i) r -= 3 - i++;
-        return 6 + i + r;
-    }
-    return 6 + (q - 22) % 3;
+__host__ __device__ constexpr int u_a(int i) { return i == 0 ? 1 : (i == 2 ? 2 : (i == 3 ? 1 : 0)); }  // u_i ~ dx^a dy^b
+__host__ __device__ constexpr int u_b(int i) { return i == 1 ? 1 : (i == 3 ? 1 : (i == 4 ? 2 : 0)); }
+__host__ __device__ constexpr int ww_q(int c, int d) {  // MOM 2 index of the colour product (c, d), any order
+    return c > d ? 13 + (d == 0 ? c : (d == 1 ? 2 + c : 5)) : 13 + (c == 0 ? d : (c == 1 ? 2 + d : 5));
 }
-static_assert(mom_i(1, 14) == 4 && mom_j(1, 14) == 4 && mom_i(1, 5) == 1 && mom_j(1, 5) == 1 && mom_j(1, 18) == 8, "");
-static_assert(mom_i(2, 20) == 7 && mom_j(2, 20) == 8 && mom_i(2, 36) == 4 && mom_j(2, 36) == 8, "");
-template <int MOM, int Q>
-struct MomIJ {  // (frontend-evaluated: every register-array index below is a compile-time constant)
-    static constexpr int i = mom_i(MOM, Q), j = mom_j(MOM, Q);
+static_assert(mono_t(2, 0) == 0 && mono_t(0, 2) == 2 && mono_t(0, 3) == 6 && mono_t(4, 0) == 7 && mono_t(0, 4) == 11, "");
+static_assert(ww_q(0, 0) == 13 && ww_q(2, 1) == 17 && ww_q(2, 2) == 18, "");
+// Per-entry quantities the moments are formed from
+struct MomIn {
+    float m20, m11, m02;  // h^2 dx^2, h^2 dx dy, h^2 dy^2
+    float dx, dy, xx, xy, yy;
+    float o2, c2;         // (G dL/dalpha)^2, dch^2
+    float hc[3];          // h dch dL/dpix_c (MOM 2)
 };
-// One reduction pass over moments [Q0, Q0 + N) of the step's four entries (base values b[k][0..8]).
+// moment Q of one entry (per-pixel constants: dp2[c] = dL/dpix_c^2, dpp[6] = the c <= d products)
+template <int MOM, int Q>
+__device__ __forceinline__ float mom_val(const MomIn& e, const float (&dp2)[3], const float (&dpp)[6]) {
+    if constexpr (Q < 3) return Q == 0 ? e.m20 : (Q == 1 ? e.m11 : e.m02);
+    else if constexpr (Q < 5) return e.m20 * (Q == 3 ? e.dx : e.dy);
+    else if constexpr (Q < 7) return e.m02 * (Q == 5 ? e.dx : e.dy);
+    else if constexpr (Q < 10) return e.m20 * (Q == 7 ? e.xx : (Q == 8 ? e.xy : e.yy));
+    else if constexpr (Q < 12) return e.m02 * (Q == 10 ? e.xy : e.yy);
+    else if constexpr (Q == 12) return e.o2;
+    else if constexpr (MOM == 1) return e.c2 * dp2[Q - 13];
+    else if constexpr (Q < 19) return e.c2 * dpp[Q - 13];
+    else {
+        constexpr int i = (Q - 19) / 3, c = (Q - 19) % 3;
+        const float mono = i == 0 ? e.dx : (i == 1 ? e.dy : (i == 2 ? e.xx : (i == 3 ? e.xy : e.yy)));
+        return e.hc[c] * mono;
+    }
+}
+// One reduction pass over moments [Q0, Q0 + N) of the step's four entries.
 template <int MOM, int Q0, int... Q>
-__device__ __forceinline__ void mom_products(const float (&b)[4][9], float* v, std::integer_sequence<int, Q...>) {
+__device__ __forceinline__ void mom_values(const MomIn (&e)[4], const float (&dp2)[3], const float (&dpp)[6], float* v,
+                                           std::integer_sequence<int, Q...>) {
     constexpr int N = sizeof...(Q);
 #pragma unroll
-    for (int k = 0; k < 4; k++) ((v[N * k + Q] = b[k][MomIJ<MOM, Q0 + Q>::i] * b[k][MomIJ<MOM, Q0 + Q>::j]), ...);
+    for (int k = 0; k < 4; k++) ((v[N * k + Q] = mom_val<MOM, Q0 + Q>(e[k], dp2, dpp)), ...);
 }
 template <int MOM, int Q0, int N>
-__device__ __forceinline__ void mom_pass(const float (&b)[4][9], int lane, float* dst) {
+__device__ __forceinline__ void mom_pass(const MomIn (&e)[4], const float (&dp2)[3], const float (&dpp)[6], int lane,
+                                         float* dst) {
     float v[4 * N];
-    mom_products<MOM, Q0>(b, v, std::make_integer_sequence<int, N>{});
+    mom_values<MOM, Q0>(e, dp2, dpp, v, std::make_integer_sequence<int, N>{});
     reduce_store<N>(v, lane, dst + Q0, true);
 }
-// The moments as a symmetric 9 x 9 matrix (entries MOM 1 does not form stay 0).
-template <int MOM, int... Q>
-__device__ __forceinline__ void mom_matrix(const float* S, float (&Sm)[9][9], std::integer_sequence<int, Q...>) {
-#pragma unroll
-    for (int a = 0; a < 9; a++)
-#pragma unroll
-        for (int c = 0; c < 9; c++) Sm[a][c] = 0.f;
-    ((Sm[MomIJ<MOM, Q>::i][MomIJ<MOM, Q>::j] = S[Q], Sm[MomIJ<MOM, Q>::j][MomIJ<MOM, Q>::i] = S[Q]), ...);
+// The moments as the symmetric 9 x 9 matrix of the base values b = (u0..u4, G dL/dalpha, dch dL/dpix_0..2)
+// (MOM 1 forms no colour cross moments: those entries stay 0).
+template <int MOM, int IJ>
+struct MomSlot {  // (frontend-evaluated: every register-array index below is a compile-time constant)
+    static constexpr int i = IJ / 9, j = IJ % 9;
+    static constexpr int q = (i < 5 && j < 5) ? mono_t(u_a(i) + u_a(j), u_b(i) + u_b(j))
+                             : (i == 5 && j == 5) ? 12
+                             : (i >= 6 && j >= 6) ? (MOM == 1 ? (i == j ? 13 + (i - 6) : -1) : ww_q(i - 6, j - 6))
+                             : (MOM == 2 && i < 5 && j >= 6) ? 19 + 3 * i + (j - 6)
+                             : (MOM == 2 && j < 5 && i >= 6) ? 19 + 3 * j + (i - 6)
+                                                             : -1;
+};
+template <int MOM, int... IJ>
+__device__ __forceinline__ void mom_matrix(const float* S, float (&Sm)[9][9], std::integer_sequence<int, IJ...>) {
+    ((Sm[MomSlot<MOM, IJ>::i][MomSlot<MOM, IJ>::j] = MomSlot<MOM, IJ>::q >= 0 ? S[MomSlot<MOM, IJ>::q >= 0 ? MomSlot<MOM, IJ>::q : 0] : 0.f), ...);
 }
 // 5 waves per SIMD (96 VGPRs; the wide variants reduce in two passes to fit), except
 // the dual variants with a 3-channel second gradient (mapping-style), which spill
@@ -261,12 +234,12 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
     static_assert(!MOM || (!DUAL && OPAC && COL1), "the moment variants form every single-image gradient");
     kclock_begin(clk);
-    GSR_WGTIME_MARK(false);
+    RenderDiag dg;  // (diagnostics builds only, gsr_diag.h)
+    dg.begin();
     if (guard.overflow()) {  // invalid forward state (static-mode overflow): touch nothing
         kclock_end(clk);
         return;
     }
-    PHASE_T0();
     static_assert(Q2 == 1 || Q2 == 3, "Q2 is 1 or 3 channels");
     constexpr int NV = bwd_nv<DUAL, OPAC, COL1, COL2, Q2, MOM>();
     constexpr int O_C1 = 5 + (OPAC ? 1 : 0);
@@ -342,10 +315,11 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     const v2f pix = v2f{(float)px, (float)py};
     const v2f dp01 = v2f{dp0, dp1}, dq01 = v2f{dq0, dq1};
     const v2f dp2q0 = v2f{dp2, dq0};  // (PACKC) the colour dot's second packed pair
+    // (MOM) per-pixel products of the colour gradient the colour moments need
+    [[maybe_unused]] const float mdp2[3] = {dp0 * dp0, dp1 * dp1, dp2 * dp2};
+    [[maybe_unused]] const float mdpp[6] = {dp0 * dp0, dp0 * dp1, dp0 * dp2, dp1 * dp1, dp1 * dp2, dp2 * dp2};
     float T = T_final, A = bg_dot;
-#if GSR_ABLATE == 1
-    float ablate_sink = 0.f;
-#endif
+    [[maybe_unused]] float ablate_sink = 0.f;  // (timing ablation 1)
     const int my_e = row_entry(lane);
     // Slots start zero; after every batch the entry totals re-zero exactly the slots they read
     // (every slot a row list can have written), and the pad slot only ever receives zeros, so no
@@ -384,16 +358,13 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             }
         }
     };
-#if GSR_STEPSTAT
-    unsigned long long st_steps = 0, st_csteps = 0, st_ok = 0, st_pads = 0, st_batches = 0, st_items = 0, st_dead = 0;
-#endif
     fetch_entry((int)bmax);
     fetch_rec((int)bmax);
     fetch_entry((int)bmax - BB);
     const uint32_t mean4 = sched_mean4(cam, guard.counters);
     const bool multi_round = sched_multi_round(cam);
     int hi_pf = (int)bmax;  // the batch start the staged registers hold
-    PHASE_MARK(0);
+    dg.phase(0);
     for (int hi = (int)bmax; hi > 0;) {
         prio_by_remaining(hi, mean4, multi_round);
         if (hi != hi_pf) {  // the previous batch was cut by its slot budget: re-fetch (rare)
@@ -414,7 +385,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             s_mask[ts_] = (uint16_t)pm;  // the instance's exact 4x4-block mask (sorted list entry)
         }
         __syncthreads();
-        PHASE_MARK(1);
+        dg.phase(1);
         fetch_rec(hi - BB);        // records of the next batch (list entries loaded a batch ago)
         fetch_entry(hi - 2 * BB);  // list entries of the batch after it
         hi_pf = hi - BB;
@@ -426,11 +397,8 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                                                   (uint32_t)(16 * BB) | ((uint32_t)(BS * NV * 4) << 16), 16u,
                                                   (uint32_t)(NV * 4));
         const int n = sl.len, cnt = sl.cnt;
-        PHASE_MARK(2);
+        dg.phase(2);
         const int jlo16 = 16 * (hi - (int)last);  // pos = hi-1-j < last  <=>  j >= jlo  <=>  16 j >= 16 jlo
-#if GSR_STEPSTAT
-        st_batches++;
-#endif
         for (int i = 0; i < n; i += 4) {
             const uint4 gw = load_slot_group4(my_list, i);
             // this lane's entry slot (the reduction's writer lanes): the high half of its entry's word,
@@ -447,7 +415,6 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             v2f d[4];
             float G[4], araw[4], alpha[4];
             bool ok[4];
-            [[maybe_unused]] bool any = false;  // (step statistics only)
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const float4 a = rec(s_a, k), b = rec(s_b, k);
@@ -465,32 +432,13 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 araw[k] = (OPAC || ok[k]) ? ar : 0.f;
                 alpha[k] = fminf(0.99f, araw[k]);
                 if (OPAC) alpha[k] = ok[k] ? alpha[k] : 0.f;
-                any = any || ok[k];
             }
-#if GSR_STEPSTAT
-            st_steps++;
             {
-                uint64_t pads = 0, oks = 0;
+                bool pad[4];
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    pads += __popcll(__ballot(jb[k] == 16 * BB));
-                    oks += __popcll(__ballot(ok[k]));
-                }
-                st_pads += pads;
-                st_ok += oks;
-                st_csteps += __ballot(any) != 0ull;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {  // (row, entry) items: listed, and listed with no contributing pixel
-                    const uint64_t okb = __ballot(ok[k]), padb = __ballot(jb[k] == 16 * BB);
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const bool listed = ((padb >> (16 * r)) & 0xFFFFull) == 0ull;
-                        st_items += listed;
-                        st_dead += listed && ((okb >> (16 * r)) & 0xFFFFull) == 0ull;
-                    }
-                }
+                for (int k = 0; k < 4; k++) pad[k] = jb[k] == 16 * BB;
+                dg.step(pad, ok);
             }
-#endif
             // (no wave-uniform skip of steps without a contributing pair: 0.04 % of steps, and the test
             // cost 2 VALU + a branch per step; config-4 dual 396 -> 387 us without it)
             // serial part (in list order): T and A, then dL/dalpha and dchannel/dcolor
@@ -529,26 +477,39 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             // dconic = -0.5 * (hxx, hxy, hyy); both are linear in the sums (Q is per Gaussian).
             float* dst = reinterpret_cast<float*>(reinterpret_cast<char*>(s_acc) + soff);  // the (entry, block) slot
             if constexpr (MOM > 0) {  // backward_power == 2: the pair's second moments (gauss_bwd_mom_kernel)
-                float b[4][9];
+                MomIn e[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    pair_geom<true>(b[k], araw[k], dLa[k], G[k], d[k]);  // u0..u4, G dL/dalpha
-                    pair_colours<true, false, Q2>(b[k] + 6, dch[k], dp01, dp2, dq0, dq01, dq2);
+                    const float h = araw[k] * dLa[k], o = G[k] * dLa[k];
+                    const float hx = h * d[k].x, hy = h * d[k].y;
+                    e[k].m20 = hx * hx;
+                    e[k].m11 = hx * hy;
+                    e[k].m02 = hy * hy;
+                    e[k].dx = d[k].x;
+                    e[k].dy = d[k].y;
+                    e[k].xx = d[k].x * d[k].x;
+                    e[k].xy = d[k].x * d[k].y;
+                    e[k].yy = d[k].y * d[k].y;
+                    e[k].o2 = o * o;
+                    e[k].c2 = dch[k] * dch[k];
+                    const float hc = h * dch[k];
+                    e[k].hc[0] = hc * dp0;
+                    e[k].hc[1] = hc * dp1;
+                    e[k].hc[2] = hc * dp2;
                 }
-                // passes of 4 moments (the reduction's cost is per value, so the pass size only sets
-                // how many products are live at once next to the 36 base values)
-                mom_pass<MOM, 0, 4>(b, lane, dst);
-                mom_pass<MOM, 4, 4>(b, lane, dst);
-                mom_pass<MOM, 8, 4>(b, lane, dst);
-                mom_pass<MOM, 12, 4>(b, lane, dst);
+                // passes of 4 moments (the reduction's cost is per value: the pass size only sets how
+                // many products are live at once)
+                mom_pass<MOM, 0, 4>(e, mdp2, mdpp, lane, dst);
+                mom_pass<MOM, 4, 4>(e, mdp2, mdpp, lane, dst);
+                mom_pass<MOM, 8, 4>(e, mdp2, mdpp, lane, dst);
                 if constexpr (MOM == 1) {
-                    mom_pass<MOM, 16, 3>(b, lane, dst);
+                    mom_pass<MOM, 12, 4>(e, mdp2, mdpp, lane, dst);
                 } else {
-                    mom_pass<MOM, 16, 4>(b, lane, dst);
-                    mom_pass<MOM, 20, 4>(b, lane, dst);
-                    mom_pass<MOM, 24, 4>(b, lane, dst);
-                    mom_pass<MOM, 28, 4>(b, lane, dst);
-                    mom_pass<MOM, 32, 5>(b, lane, dst);
+                    mom_pass<MOM, 12, 4>(e, mdp2, mdpp, lane, dst);
+                    mom_pass<MOM, 16, 4>(e, mdp2, mdpp, lane, dst);
+                    mom_pass<MOM, 20, 4>(e, mdp2, mdpp, lane, dst);
+                    mom_pass<MOM, 24, 5>(e, mdp2, mdpp, lane, dst);
+                    mom_pass<MOM, 29, 5>(e, mdp2, mdpp, lane, dst);
                 }
             } else if constexpr (NV <= 6) {  // one reduction over all values
                 float v[4 * NV];
@@ -557,12 +518,12 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                     pair_geom<OPAC>(v + NV * k, araw[k], dLa[k], G[k], d[k]);
                     pair_colours<COL1, COL2, Q2>(v + NV * k + O_C1, dch[k], dp01, dp2, dq0, dq01, dq2);
                 }
-#if GSR_ABLATE == 1
+                if constexpr (kAblate == 1) {
 #pragma unroll
-                for (int q = 0; q < 4 * NV; q++) ablate_sink += v[q];
-#else
-                reduce_store<NV>(v, lane, dst, true);
-#endif
+                    for (int q = 0; q < 4 * NV; q++) ablate_sink += v[q];
+                } else {
+                    reduce_store<NV>(v, lane, dst, true);
+                }
             } else {  // wide variants: geometric (+ opacity), then colour sums (register pressure)
                 constexpr bool OP_A = OPAC && GSR_BWD_SPLIT6;
                 constexpr int NA = 5 + (OP_A ? 1 : 0), NB = NV - NA;
@@ -584,9 +545,9 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 }
             }
         }
-        PHASE_MARK(3);
+        dg.phase(3);
         __syncthreads();
-        PHASE_MARK(4);
+        dg.phase(4);
         // Entry totals: TPE threads per entry, thread q of an entry owns values m = q, q + TPE, ...
         // and adds the entry's consecutive block slots in ascending block order (deterministic);
         // the TPE threads store adjacent floats of the packed record.
@@ -594,7 +555,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         int t_ = tid;
         asm volatile("" : "+v"(t_));  // addresses formed here, not hoisted across the batch loop (VGPRs)
         const int e = t_ / TPE, q = t_ % TPE;
-        if (GSR_ABLATE != 2 && e < cnt) {
+        if (kAblate != 2 && e < cnt) {
             float c[NQ];
 #pragma unroll
             for (int i = 0; i < NQ; i++) c[i] = 0.f;
@@ -613,30 +574,14 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             for (int i = 0; i < NQ; i++)
                 if (q + TPE * i < RS) dst[q + TPE * i] = c[i];
         }
-        PHASE_MARK(5);
+        dg.phase(5);
         __syncthreads();
-        PHASE_MARK(6);
-#if GSR_PHASE
-        ph_acc[7]++;
-#endif
+        dg.phase(6);
+        dg.batch();
         hi -= cnt;
     }
-    PHASE_FLUSH();
-#if GSR_ABLATE == 1
-    if (ablate_sink == 1.2345f) inst[0] = ablate_sink;  // keeps the per-pair values alive (timing ablation)
-#endif
-#if GSR_STEPSTAT
-    if (lane == 0) {
-        atomicAdd(&g_stepstat[0], st_steps);
-        atomicAdd(&g_stepstat[1], st_csteps);
-        atomicAdd(&g_stepstat[2], st_ok);
-        atomicAdd(&g_stepstat[3], st_pads);
-        atomicAdd(&g_stepstat[4], st_batches);
-        atomicAdd(&g_stepstat[5], st_items);
-        atomicAdd(&g_stepstat[6], st_dead);
-    }
-#endif
-    GSR_WGTIME_MARK(true);
+    if (kAblate == 1 && ablate_sink == 1.2345f) inst[0] = ablate_sink;  // keeps the per-pair values alive
+    dg.end();
     kclock_end(clk);
 }
 
@@ -806,9 +751,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         block_sum<POSE_PARTS>(v, s_red, s_tot);
         __syncthreads();
         if (threadIdx.x < POSE_PARTS) st_agent(pf.part + POSE_PARTS * blockIdx.x + threadIdx.x, s_tot[threadIdx.x]);
-#if GSR_ABLATE == 3
-        return;  // timing ablation: no pose tail (invalid pose update)
-#endif
+        if constexpr (kAblate == 3) return;  // timing ablation: no pose tail (invalid pose update)
 #if GSR_POSE_TAIL == 1
         // One-level fixed-order sum: the last workgroup to arrive (grouped arrival counters) reads
         // all partials as one coalesced float stream (thread t: floats t, t + 256, ... = value
@@ -818,9 +761,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         {
             const int nb = gridDim.x;
             if (!last_block_arrive_grouped(reinterpret_cast<uint32_t*>(pf.part + POSE_PARTS * nb))) return;
-#if GSR_ABLATE == 4
-            return;  // timing ablation: arrival only
-#endif
+            if constexpr (kAblate == 4) return;  // timing ablation: arrival only
             static_assert(256 % POSE_PARTS == 0, "a thread keeps one value index");
             constexpr int CH = 40;
             const int total = POSE_PARTS * nb;
@@ -845,7 +786,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
                 s_tot[threadIdx.x] = t;
             }
             __syncthreads();
-            if (GSR_ABLATE != 5 && threadIdx.x == 0) {  // (5: timing ablation, no pose_fin)
+            if (kAblate != 5 && threadIdx.x == 0) {  // (5: timing ablation, no pose_fin)
                 const PoseAdam adam{pf.lr_q, pf.lr_t, pf.beta1, pf.beta2, (float)(1.0 - pf.beta1),
                                     (float)(1.0 - pf.beta2), (float)pf.eps, pf.adam_state, pf.cam_q, pf.cam_t,
                                     pf.guard, pf.cap, pf.loss, pf.best};
@@ -961,7 +902,7 @@ hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, c
 // output of a pair is linear in the pair's base values b = (u, G dL/dalpha, dch dL/dpix) with a
 // per-Gaussian coefficient row n (the chain, the conic and the NDC factor folded in), so
 //   sum_p (n . b_p)^2 = n (sum_p b_p b_p^T) n^T:
-// render_bwd forms the second moments sum_p b_p b_p^T (MOM layout, 19 or 37 sums per instance),
+// render_bwd forms the second moments sum_p b_p b_p^T (MOM layout, 16 or 34 sums per instance),
 // and this kernel applies the quadratic forms once per Gaussian, in double.
 hipError_t launch_render_bwd_moments(const Camera& cam, const uint2* ranges, const uint64_t* point_list, GeomPtrs geo,
                                      const float* final_T, const uint32_t* n_contrib, const float* dL_dpix, bool sh,
@@ -971,13 +912,13 @@ hipError_t launch_render_bwd_moments(const Camera& cam, const uint2* ranges, con
                        final_T, n_contrib, dL_dpix, nullptr, inst, guard, nullptr);
     return hipGetLastError();
 }
-int moments_record_floats(bool sh) { return sh ? 38 : 20; }
+int moments_record_floats(bool sh) { return sh ? 34 : 16; }
 
 template <int MOM>
 __global__ void __launch_bounds__(256)
 gauss_bwd_mom_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii,
                      const float* __restrict__ inst, GradsOut out, BwdGuard guard) {
-    constexpr int NV = MOM == 1 ? 19 : 37, RS = (NV + 1) & ~1;
+    constexpr int NV = MOM == 1 ? 16 : 34, RS = (NV + 1) & ~1;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= g.P) return;
     const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
@@ -1001,7 +942,7 @@ gauss_bwd_mom_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict_
         }
     }
     float Sm[9][9];
-    mom_matrix<MOM>(S, Sm, std::make_integer_sequence<int, NV>{});
+    mom_matrix<MOM>(S, Sm, std::make_integer_sequence<int, 81>{});
     float o_m2[2] = {0.f, 0.f}, o_mean[3] = {0.f, 0.f, 0.f}, o_cov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f},
           o_scale[3] = {0.f, 0.f, 0.f}, o_rot[4] = {0.f, 0.f, 0.f, 0.f}, ysq[16];
 #pragma unroll

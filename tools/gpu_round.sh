@@ -1,30 +1,84 @@
 #!/bin/bash
-# One GPU session (GPU box, repo root): any of
-#   tests    the GPU suite (pytest -m gpu)
-#   bench    the default bench line (dropin / cpu baseline off)
-#   full     the default bench line exactly as the driver runs it
-#   prof     rocprofv3 kernel trace + stats of the headline bench
-#   map      the mapping bench leg alone
-#   lock     lockstep / padding statistics of render_bwd's row lists (configs 3, 4)
-# Usage: tools/gpu_round.sh TAG step...   (stops at the first failing step)
+# The one GPU-session driver (GPU box, repo root).  Runs the listed steps in order, each under its own time
+# limit, and stops at the first failing step.  Outputs land in gpurun_out/TAG/; a summary is printed last.
+#
+# Usage: tools/gpu_round.sh TAG step...
+#   tests            the GPU suite (pytest -m gpu)
+#   smoke            __graft_entry__.smoke()
+#   bench            the bench line without the slow legs (drop-in, CPU baseline off)
+#   full             the default bench line exactly as the driver runs it
+#   map              the mapping bench leg alone (config 4)
+#   prof             rocprofv3 kernel trace + stats of the headline bench (tracking legs only)
+#   pmc              FETCH_SIZE / WRITE_SIZE passes (one rocprofv3 run per counter) of the headline bench
+#   sq               SQ issue / wait / LDS counters of the render kernels (two passes, <= 8 SQ counters each)
+#   stream           tools/micro/stream: STREAM copy / triad GB/s (the measured HBM peak)
+#   lock             render_bwd row-list lockstep statistics (tools/lockstep_stats.py, configs 3 and 4)
+#   ab=MODES=TAGS    interleaved A/B (two rounds) of tools/raster_bench.py stage times between libgsr.so and
+#                    each splatam_amd/_diag/libgsr_<tag>.so (build_variant on the CPU first);
+#                    MODES = mode:config[,mode:config...], TAGS = tag[,tag...]   e.g. ab=dual_lean:3,dual:4=ablw
+#   abbench=TAGS     interleaved A/B of the bench line (tracking + mapping values, render stage times)
 TAG=${1:-x}; shift
 ROOT=$(pwd); OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
+LIGHT="--cpu-baseline off --dropin off --fisher off --mapping off --configs off"
+lib_of() { [ "$1" = base ] && echo "$ROOT/splatam_amd/libgsr.so" || echo "$ROOT/splatam_amd/_diag/libgsr_$1.so"; }
 for s in "$@"; do
   case $s in
-    tests) timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > "$OUT/tests.log" 2>&1 \
-             || { echo "tests failed"; tail -40 "$OUT/tests.log"; exit 1; } ;;
+    tests) timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread \
+             > "$OUT/tests.log" 2>&1 || { echo "tests failed"; tail -40 "$OUT/tests.log"; exit 1; } ;;
+    smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+             || { echo "smoke failed"; tail -20 "$OUT/smoke.log"; exit 1; } ;;
     bench) timeout -k 10 300 python bench.py --dropin off --cpu-baseline off > "$OUT/bench.log" 2>&1 \
              || { echo "bench failed"; tail -30 "$OUT/bench.log"; exit 1; } ;;
-    full) timeout -k 10 400 python bench.py > "$OUT/full.log" 2>&1 || { echo "full bench failed"; tail -30 "$OUT/full.log"; exit 1; } ;;
-    prof) ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
-             --output-format csv -- python "$ROOT/bench.py" --steps 40 --warmup 20 --cpu-baseline off --dropin off \
-             --fisher off --mapping off > "$OUT/prof.log" 2>&1 ) || { echo "prof failed"; tail -20 "$OUT/prof.log"; exit 1; } ;;
+    full) timeout -k 10 500 python bench.py > "$OUT/full.log" 2>&1 || { echo "full bench failed"; tail -30 "$OUT/full.log"; exit 1; } ;;
     map) timeout -k 10 300 python bench.py --workload mapping --cpu-baseline off > "$OUT/map.log" 2>&1 \
              || { echo "map failed"; tail -30 "$OUT/map.log"; exit 1; } ;;
+    prof) ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
+             --output-format csv -- python "$ROOT/bench.py" --steps 40 --warmup 20 $LIGHT > "$OUT/prof.log" 2>&1 ) \
+             || { echo "prof failed"; tail -20 "$OUT/prof.log"; exit 1; } ;;
+    pmc) for C in FETCH_SIZE WRITE_SIZE; do
+           ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --pmc $C \
+               --kernel-include-regex 'render_|gauss_bwd|preprocess|duplicate|tile_colscan' -T -d "$OUT/pmc_$C" -o run \
+               --output-format csv -- python "$ROOT/bench.py" --steps 20 --warmup 20 $LIGHT > "$OUT/pmc_$C.log" 2>&1 ) \
+               || { echo "pmc $C failed"; tail -20 "$OUT/pmc_$C.log"; exit 1; }
+         done ;;
+    sq) G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+        G2="SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
+        i=0
+        for G in "$G1" "$G2"; do
+          i=$((i+1))
+          ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --pmc $G --kernel-include-regex 'render_' -T \
+              -d "$OUT/sq$i" -o run --output-format csv -- python "$ROOT/bench.py" --steps 20 --warmup 20 $LIGHT \
+              > "$OUT/sq$i.log" 2>&1 ) || { echo "sq pass $i failed"; tail -20 "$OUT/sq$i.log"; exit 1; }
+        done ;;
     stream) timeout -k 10 120 tools/micro/stream > "$OUT/stream.json" 2>&1 || { echo "stream failed"; exit 1; } ;;
     lock) timeout -k 10 200 python tools/lockstep_stats.py 3 128 > "$OUT/lockstep3.txt" 2>&1 && \
           timeout -k 10 200 python tools/lockstep_stats.py 4 128 > "$OUT/lockstep4.txt" 2>&1 || { echo "lock failed"; exit 1; } ;;
+    ab=*) spec=${s#ab=}; MODES=${spec%%=*}; TAGS=${spec#*=}
+          for r in 1 2; do
+            for t in base ${TAGS//,/ }; do
+              for c in ${MODES//,/ }; do
+                m=${c%%:*}; cf=${c##*:}; f="$OUT/ab_${t}_${m}_${cf}_$r.json"
+                GSR_LIB=$(lib_of $t) timeout -k 10 120 python tools/raster_bench.py --iters 60 --mode $m --config $cf \
+                    > "$f" 2>&1 || { echo "ab $t $c failed"; tail -5 "$f"; exit 1; }
+                python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['stages_us']; print('ab', sys.argv[2], sys.argv[3], 'round', sys.argv[4], 'render_fwd', s['render_fwd'], 'render_bwd', s['render_bwd'], 'gauss_bwd', s['gauss_bwd'], 'ms', round(d['ms_per_frame'], 4))" "$f" $t $c $r | tee -a "$OUT/ab.txt"
+              done
+            done
+          done ;;
+    abbench=*) TAGS=${s#abbench=}
+          for r in 1 2; do
+            for t in base ${TAGS//,/ }; do
+              f="$OUT/abbench_${t}_$r.log"
+              GSR_LIB=$(lib_of $t) timeout -k 10 300 python bench.py --cpu-baseline off --dropin off --fisher off \
+                  --configs off > "$f" 2>&1 || { echo "abbench $t failed"; tail -20 "$f"; exit 1; }
+              python - "$f" $t $r <<'PY' | tee -a "$OUT/abbench.txt"
+import json, sys
+b = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][-1]
+print("abbench", sys.argv[2], "round", sys.argv[3], "frames/s", b["value"], "render_bwd", b["roofline"]["avg_us"],
+      "render_fwd", b["stages_us"]["render_fwd"], "mapping it/s", (b.get("mapping") or {}).get("value"))
+PY
+            done
+          done ;;
     *) echo "unknown step $s"; exit 1 ;;
   esac
   echo "step $s ok"
@@ -42,11 +96,15 @@ for name in ("bench.log", "full.log", "map.log"):
         if ls:
             b = json.loads(ls[-1])
             rf = b.get("roofline", {})
-            print(name, "value", b["value"], b["unit"], "render_bwd", rf.get("avg_us"), "frac", rf.get("frac"))
-for name in ("lockstep3.txt", "lockstep4.txt", "stream.json"):
+            print(name, "value", b["value"], b["unit"], "render_bwd", rf.get("avg_us"), "frac", rf.get("frac"),
+                  "render_fwd", (b.get("stages_us") or {}).get("render_fwd"))
+            if b.get("fisher"):
+                fi = b["fisher"]
+                print("  fisher", fi.get("value"), "dropin", fi.get("dropin"))
+for name in ("lockstep3.txt", "lockstep4.txt", "stream.json", "smoke.log"):
     p = os.path.join(out, name)
     if os.path.exists(p):
-        print(open(p).read())
+        print(open(p).read().strip()[-1500:])
 t = os.path.join(out, "tests.log")
 if os.path.exists(t):
     print(open(t).read().strip().split("\n")[-1])

@@ -1,4 +1,4 @@
-"""Turns a tools/profile_round.sh output directory into the committed
+"""Turns a tools/gpu_round.sh output directory (prof/, pmc_FETCH_SIZE/, pmc_WRITE_SIZE/ steps) into the committed
 profiles/ summaries: kernel stats CSV, per-kernel PMC traffic JSON and the bench line."""
 import csv
 import glob
@@ -12,7 +12,8 @@ from collections import defaultdict
 def main(src, tag):
     dst = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
     os.makedirs(dst, exist_ok=True)
-    stats = glob.glob(f"{src}/trace/**/run_kernel_stats.csv", recursive=True)[0]
+    stats = (glob.glob(f"{src}/prof/**/run_kernel_stats.csv", recursive=True) or
+             glob.glob(f"{src}/trace/**/run_kernel_stats.csv", recursive=True))[0]
     shutil.copy(stats, f"{dst}/{tag}_kernel_stats.csv")
     rows = {r["Name"]: r for r in csv.DictReader(open(stats))}
     pmc = defaultdict(lambda: defaultdict(list))

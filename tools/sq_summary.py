@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 SQ counter passes (tools/pmc_sq.sh) per kernel: per-launch averages and derived
+"""Summarise rocprofv3 SQ counter passes (tools/gpu_round.sh sq) per kernel: per-launch averages and derived
 ratios (issued VALU per wave, wait/active fractions of wave cycles)."""
 import csv
 import glob
