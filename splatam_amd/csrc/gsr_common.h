@@ -596,6 +596,22 @@ __device__ __forceinline__ uint32_t quad_mask(float4 a, float4 b, float x0, floa
     return (mx * (my & 1u)) | ((mx * (my >> 1)) << 2);
 }
 
+// inclusive scan over the 64 lanes: six DPP adds (row_shr 1 / 2 / 4 / 8 with bank masks: the in-row prefix; row_bcast 15 / 31 carry it across
+// rows) instead of six lane shuffles through the LDS crossbar
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xe, true);   // row_shr:4 (banks 1-3)
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xc, true);   // row_shr:8 (banks 2-3)
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 (rows 1, 3)
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 (rows 2, 3)
+    return v;
+}
+// number of set bits of `mask` below this lane (v_mbcnt_lo / hi)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
 // Ordered list of the batch entries whose quadrant mask has bit `w` (one wave
 // builds its own list; ballot + popcount compaction, order preserved).
 __device__ __forceinline__ int build_wave_list(const uint8_t* s_mask, int cnt, int w, int jmin, uint16_t* list) {
@@ -622,16 +638,16 @@ template <typename MaskOf>
 __device__ __forceinline__ int build_row_lists_by(MaskOf mask_of, int cnt, int w, const int (&jmin)[4],
                                                   uint16_t* list, int stride, uint16_t pad) {
     const int lane = __lane_id();
-    const uint64_t lt = (1ull << lane) - 1ull;
     int n[4] = {0, 0, 0, 0};
     for (int c = 0; c < cnt; c += 64) {
         const int j = c + lane;
         const uint32_t m = j < cnt ? (mask_of(j) >> (4 * w)) & 0xFu : 0u;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            const bool bit = ((m >> r) & 1u) && j >= jmin[r];
-            const uint64_t bal = __ballot(bit);
-            if (bit) list[r * stride + n[r] + __popcll(bal & lt)] = (uint16_t)j;
+            // the row's lanes as an SGPR mask: its lane prefix by v_mbcnt, the store predicated on it
+            const uint64_t bal = __builtin_amdgcn_uicmp((m >> r) & 1u, 0u, 33 /* ne */) &
+                                 __builtin_amdgcn_sicmp(j, jmin[r], 39 /* sge */);
+            if (__builtin_amdgcn_inverse_ballot_w64(bal)) list[r * stride + n[r] + (int)lanes_below(bal)] = (uint16_t)j;
             n[r] += __popcll(bal);
         }
     }
@@ -676,7 +692,6 @@ __device__ __forceinline__ SlotLists build_row_slot_lists(const uint16_t* s_mask
                                                          int stride, uint32_t pad, uint32_t jmul = 1u,
                                                          uint32_t smul = 1u) {
     const int lane = __lane_id();
-    const uint64_t lt = (1ull << lane) - 1ull;
     const uint32_t below_w = (1u << (4 * w)) - 1u;  // blocks of the waves before this one
     int n[4] = {0, 0, 0, 0};
     uint32_t carry = 0;
@@ -685,29 +700,25 @@ __device__ __forceinline__ SlotLists build_row_slot_lists(const uint16_t* s_mask
         const int j = c + lane;
         const uint32_t mf = j < cmax ? (uint32_t)s_mask[j] : 0u;
         const uint32_t pc = __popc(mf);
-        // inclusive prefix of the popcounts (0..16) bit by bit: ballots + mbcnt (no lane shuffles,
-        // whose hoisted address registers spilled), the chunk total from the ballots' popcounts
-        uint32_t incl = carry, tot = 0;
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const uint64_t bk = __ballot((pc >> k) & 1u);
-            incl += (uint32_t)__popcll(bk & (lt | (1ull << lane))) << k;
-            tot += (uint32_t)__popcll(bk) << k;
-        }
+        // inclusive prefix of the popcounts over the batch (DPP scan), the chunk total from lane 63
+        const uint32_t incl = carry + wave_incl_scan(pc);
         const uint32_t base = incl - pc;
-        const bool fits = j < cmax && incl <= (uint32_t)budget;
-        cnt += __popcll(__ballot(fits));
-        carry += tot;
-        if (w == 0 && fits) s_base[j] = (uint16_t)base;
+        const uint64_t fits = __builtin_amdgcn_sicmp(j, cmax, 40 /* slt */) &
+                              __builtin_amdgcn_uicmp(incl, (uint32_t)budget, 37 /* ule */);
+        cnt += __popcll(fits);
+        carry = __builtin_amdgcn_readlane(incl, 63);
+        if (w == 0 && __builtin_amdgcn_inverse_ballot_w64(fits)) s_base[j] = (uint16_t)base;
         const uint32_t m = (mf >> (4 * w)) & 0xFu;
-        const uint32_t sb = base + __popc(mf & below_w);
+        // the entry's word for the wave's first block; block r adds the slots of blocks r' < r it reaches
+        const uint32_t w0 = __umul24((uint32_t)j, jmul) | (__umul24(base + __popc(mf & below_w), smul) << 16);
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            const bool bit = fits && ((m >> r) & 1u) && j >= jmin[r];
-            const uint64_t bal = __ballot(bit);
-            if (bit)
-                list[r * stride + n[r] + __popcll(bal & lt)] =
-                    (uint32_t)j * jmul | ((sb + __popc(m & ((1u << r) - 1u))) * smul << 16);
+            // compare masks straight from v_cmp (a __ballot of a combined bool costs a select and a compare
+            // more per row)
+            const uint64_t bal = __builtin_amdgcn_uicmp((m >> r) & 1u, 0u, 33 /* ne */) &
+                                 __builtin_amdgcn_sicmp(j, jmin[r], 39 /* sge */) & fits;
+            if (__builtin_amdgcn_inverse_ballot_w64(bal))
+                list[r * stride + n[r] + (int)lanes_below(bal)] = w0 + (__umul24(__popc(m & ((1u << r) - 1u)), smul) << 16);
             n[r] += __popcll(bal);
         }
     }
@@ -1080,16 +1091,6 @@ __device__ __forceinline__ void wave_reduce_n(const float (&v)[N], float (&r)[N 
     for (int m = 0; m < N / 4; m++) r[m] = row16_sum(swapsum16(r1[m], r1[m + N / 4]));
 }
 
-// inclusive scan over the 64 lanes
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const int lane = __lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = __shfl_up(v, o);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 

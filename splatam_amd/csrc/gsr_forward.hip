@@ -13,6 +13,7 @@
 #include <cstdlib>
 
 #include "gsr_glue_common.h"  // (includes gsr_common.h) track_xform_compute / _store: the transform-fused preprocess
+#include "gsr_diag.h"
 
 namespace gsr {
 GSR_WGTIME_TABLE
@@ -950,8 +951,9 @@ __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, E
 //                keys below it -- exact, as the keys are unique in a tile.
 // The result equals a stable (tile, depth) radix order (ids break depth ties).
 #ifndef GSR_FWD_ABLATE
-#define GSR_FWD_ABLATE 0  // timing ablations (tools/ablate.sh; results invalid): 1 no per-tile sort, 2 no walk,
-                          // 4 no tracking-loss epilogue.  0 in every real build
+#define GSR_FWD_ABLATE 0  // timing ablations (tools/gpu_round.sh ab=; results invalid except 5, 6): 1 no per-tile
+                          // sort, 2 no walk, 4 no tracking-loss epilogue, 5 bounding-box block masks, 6 no block
+                          // masks.  0 in every real build
 #endif
 __device__ __forceinline__ void tile_sort_bucket(uint64_t* __restrict__ src, uint32_t cnt,
                                                  PointEntry* __restrict__ dst, uint64_t* sk) {
@@ -1178,7 +1180,8 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
                   SpecGuard guard, unsigned long long* clk, TrackL1 l1) {
     static_assert(DUAL || !L1, "the tracking loss needs the depth / silhouette colour set");
     kclock_begin(clk);
-    GSR_WGTIME_MARK(false);
+    RenderDiag dg;  // (diagnostics builds only, gsr_diag.h): phases 0 sort, 1 staging, 2 lists, 3 walk, 4 barrier,
+    dg.begin();     // 5 epilogue
     if (guard.overflow()) {
         kclock_end(clk);
         return;
@@ -1242,6 +1245,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
     fetch_id(range.x + RENDER_BATCH);
     const uint32_t mean4 = sched_mean4(cam, guard.counters);
     const bool multi_round = sched_multi_round(cam);
+    dg.phase(0);
     for (uint32_t start = range.x; start < range.y; start += RENDER_BATCH) {
         prio_by_remaining((int)(range.y - start), mean4, multi_round);
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
@@ -1249,7 +1253,9 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         if (tid < cnt) {
             float xs = x0, ys = y0;
             asm volatile("" : "+v"(xs), "+v"(ys));  // block bounds formed here, not hoisted (VGPRs)
-            const uint32_t pm = block_mask_exact(pa, pb, xs, ys);
+            // (GSR_FWD_ABLATE 5: the bounding-box mask; 6: every block -- timing ablations)
+            const uint32_t pm = GSR_FWD_ABLATE == 5 ? block_mask(pa, pb, xs, ys)
+                              : GSR_FWD_ABLATE == 6 ? 0xFFFFu : block_mask_exact(pa, pb, xs, ys);
             s_a[tid] = pa;
             s_b[tid] = pb;
             s_c[tid] = pc;
@@ -1258,12 +1264,14 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
             point_list[start + tid] = ((PointEntry)pm << 32) | pg;  // the mask, for render_bwd
         }
         __syncthreads();
+        dg.phase(1);
         fetch_rec(start + RENDER_BATCH);      // records of the next batch (ids loaded a batch ago)
         fetch_id(start + 2 * RENDER_BATCH);   // ids of the batch after it
         const int jmin0[4] = {0, 0, 0, 0};
         const int n = build_row_lists(s_mask, cnt, w, jmin0, s_list + 4 * w * LS, LS, (uint16_t)RENDER_BATCH);
         const uint16_t* my_list = s_list + (4 * w + row) * LS;
         const uint32_t pos0 = start - range.x;
+        dg.phase(2);
         for (int i = 0; i < (GSR_FWD_ABLATE == 2 ? 0 : n); i += 4) {
             if (__ballot(!done) == 0ull) break;
             const RowGroup4 gq = load_row_group4(my_list, i);
@@ -1304,7 +1312,10 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
                 }
             }
         }
+        dg.phase(3);
         __syncthreads();
+        dg.phase(4);
+        dg.batch();
     }
     const float C0 = C01.x, C1 = C01.y, C3 = C34.x, C4 = C34.y;
     // the loss epilogue's inputs are loaded before the image stores: a load issued after a store
@@ -1394,10 +1405,19 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
             }
         }
     }
-    GSR_WGTIME_MARK(true);
+    dg.phase(5);
+    dg.end();
     kclock_end(clk);
 }
 
+#if GSR_PHASE
+extern "C" int gsr_diag_phase_fwd(unsigned long long* host) {  // copies and clears the phase cycles
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), sizeof(g_phase), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+#endif
 #if GSR_WGTIME
 extern "C" int gsr_diag_wgtime_fwd(unsigned long long* host, int n) {
     const size_t bytes = sizeof(unsigned long long) * 4 * (size_t)(n < GSR_WGTIME_MAX ? n : GSR_WGTIME_MAX);

@@ -13,6 +13,7 @@
 #   sq               SQ issue / wait / LDS counters of the render kernels (two passes, <= 8 SQ counters each)
 #   stream           tools/micro/stream: STREAM copy / triad GB/s (the measured HBM peak)
 #   lock             render_bwd row-list lockstep statistics (tools/lockstep_stats.py, configs 3 and 4)
+#   phase            render_fwd / render_bwd phase shares (tools/phase.py; needs _diag/libgsr_phase.so)
 #   ab=MODES=TAGS    interleaved A/B (two rounds) of tools/raster_bench.py stage times between libgsr.so and
 #                    each splatam_amd/_diag/libgsr_<tag>.so (build_variant on the CPU first);
 #                    MODES = mode:config[,mode:config...], TAGS = tag[,tag...]   e.g. ab=dual_lean:3,dual:4=ablw
@@ -54,6 +55,7 @@ for s in "$@"; do
     stream) timeout -k 10 120 tools/micro/stream > "$OUT/stream.json" 2>&1 || { echo "stream failed"; exit 1; } ;;
     lock) timeout -k 10 200 python tools/lockstep_stats.py 3 128 > "$OUT/lockstep3.txt" 2>&1 && \
           timeout -k 10 200 python tools/lockstep_stats.py 4 128 > "$OUT/lockstep4.txt" 2>&1 || { echo "lock failed"; exit 1; } ;;
+    phase) timeout -k 10 200 python tools/phase.py 3 10 > "$OUT/phase.json" 2>&1 || { echo "phase failed"; tail -20 "$OUT/phase.json"; exit 1; } ;;
     ab=*) spec=${s#ab=}; MODES=${spec%%=*}; TAGS=${spec#*=}
           for r in 1 2; do
             for t in base ${TAGS//,/ }; do
@@ -61,7 +63,7 @@ for s in "$@"; do
                 m=${c%%:*}; cf=${c##*:}; f="$OUT/ab_${t}_${m}_${cf}_$r.json"
                 GSR_LIB=$(lib_of $t) timeout -k 10 120 python tools/raster_bench.py --iters 60 --mode $m --config $cf \
                     > "$f" 2>&1 || { echo "ab $t $c failed"; tail -5 "$f"; exit 1; }
-                python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['stages_us']; print('ab', sys.argv[2], sys.argv[3], 'round', sys.argv[4], 'render_fwd', s['render_fwd'], 'render_bwd', s['render_bwd'], 'gauss_bwd', s['gauss_bwd'], 'ms', round(d['ms_per_frame'], 4))" "$f" $t $c $r | tee -a "$OUT/ab.txt"
+                python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['stages_us']; print('ab', sys.argv[2], sys.argv[3], 'round', sys.argv[4], 'preprocess', s['preprocess'], 'duplicate', s['duplicate'], 'render_fwd', s['render_fwd'], 'render_bwd', s['render_bwd'], 'gauss_bwd', s['gauss_bwd'], 'ms', round(d['ms_per_frame'], 4))" "$f" $t $c $r | tee -a "$OUT/ab.txt"
               done
             done
           done ;;
@@ -101,7 +103,7 @@ for name in ("bench.log", "full.log", "map.log"):
             if b.get("fisher"):
                 fi = b["fisher"]
                 print("  fisher", fi.get("value"), "dropin", fi.get("dropin"))
-for name in ("lockstep3.txt", "lockstep4.txt", "stream.json", "smoke.log"):
+for name in ("lockstep3.txt", "lockstep4.txt", "stream.json", "smoke.log", "phase.json"):
     p = os.path.join(out, name)
     if os.path.exists(p):
         print(open(p).read().strip()[-1500:])
