@@ -516,7 +516,10 @@ __device__ __forceinline__ uint32_t pe_mask(PointEntry p) { return (uint32_t)(p 
 // the right); margins cover the float32 error.  ~10 % fewer pixel-pair
 // evaluations than the box on a frame (tools/tile_balance.py).
 // The per-Gaussian half of block_mask_exact.  hx < 0: no culling (full mask);
-// hy < 0: never blended (empty mask).
+// hy < 0: never blended (empty mask).  The reciprocals, logarithm and square roots are the
+// hardware's (v_rcp / v_log / v_sqrt_f32, ~1 ulp; the correctly rounded library forms cost ~10
+// instructions each): the margins (x 1.001, + 1e-3 on tau, + 0.01 / 0.02 px) exceed their error by
+// four orders of magnitude.
 struct MaskGeom {
     float ax, ay, hx, hy, B, inv_A, twoA_tau, det, us, eps;
 };
@@ -525,57 +528,58 @@ __device__ __forceinline__ MaskGeom mask_geom(float4 a, float4 b) {
     MaskGeom g;
     g.ax = a.x;
     g.ay = a.y;
-    float hx = 0.f, hy = 0.f;
-    bool never;
-    if (!alpha_extent(a, b, hx, hy, never)) {
-        g.hx = -1.f;
-        g.hy = 0.f;
-    } else if (never) {
-        g.hx = 0.f;
-        g.hy = -1.f;
-    } else {
-        g.hx = hx;
-        g.hy = hy;
-    }
-    const float A = a.z * (1.f / K_AC), B = b.x * (1.f / K_B), C = a.w * (1.f / K_AC);
+    const float A = a.z * (1.f / K_AC), B = b.x * (1.f / K_B), C = a.w * (1.f / K_AC), o = b.y;
     const float det = A * C - B * B;
-    const float kappa = A * C / det;
-    const float tau = fmaxf(__logf(255.f * b.y), 0.f) * (1.001f + 4e-6f * kappa) + 1e-3f;  // as alpha_extent
+    const float rdet = __builtin_amdgcn_rcpf(det);
+    const float kappa = A * C * rdet;  // 1 / (1 - rho^2) >= 1
+    // anything unusual (non-finite values, a conic that is not positive definite, extreme eccentricity): no culling
+    const bool bad = !(det > 0.f) || !(A > 0.f) || !isfinite(det) || !isfinite(a.x) || !isfinite(a.y) ||
+                     !isfinite(o) || !(kappa < 1e4f);
+    const float t = 255.f * o;
+    const bool never = t < 0.999f;  // alpha <= o < 1/255: never blended
+    // tau = ln(255 o), with the margin of the float32 error of `power` (grows with kappa)
+    const float tau = fmaxf(__builtin_amdgcn_logf(t) * 0.69314718f, 0.f) * (1.001f + 4e-6f * kappa) + 1e-3f;
+    const float k2 = 2.f * tau * rdet;
+    const float hx = __builtin_amdgcn_sqrtf(k2 * C) * 1.001f + 0.01f;
+    const float hy = __builtin_amdgcn_sqrtf(k2 * A) * 1.001f + 0.01f;
+    g.hx = bad ? -1.f : (never ? 0.f : hx);
+    g.hy = bad ? 0.f : (never ? -1.f : hy);
     g.B = B;
     g.det = det;
     g.twoA_tau = 2.f * tau * A;
-    g.inv_A = 1.f / A;
-    g.us = B * sqrtf(2.f * tau / (det * C));  // uy of the leftmost point (rightmost: -us)
+    g.inv_A = __builtin_amdgcn_rcpf(A);
+    g.us = B * __builtin_amdgcn_sqrtf(k2 * __builtin_amdgcn_rcpf(C));  // uy of the leftmost point (rightmost: -us)
     g.eps = 0.02f + 0.002f * hx;
     return g;
 }
+// Block row r (pixel centres y0 + 4r .. + 3): the ellipse's x-extent over the row's y-span
+// [lo, hi] is [xmin, xmax]; the row's blocks are the columns c with x0 + 4c <= xmax and
+// xmin <= x0 + 4c + 3, i.e. c in [ceil((xmin - x0 - 3) / 4), floor((xmax - x0) / 4)] (a rounding of
+// the scaled differences can only widen that range: the mask stays conservative).
 __device__ __forceinline__ uint32_t mask_of_geom(const MaskGeom& g, float x0, float y0) {
     if (g.hx < 0.f) return 0xFFFFu;
     if (g.hy < 0.f) return 0u;
-    const float xl = g.ax - g.hx, xh = g.ax + g.hx, yl = g.ay - g.hy, yh = g.ay + g.hy;
-    uint32_t mx = 0, my = 0;
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-        mx |= (xh >= x0 + 4.f * c && xl <= x0 + 4.f * c + 3.f) ? 1u << c : 0u;
-        my |= (yh >= y0 + 4.f * c && yl <= y0 + 4.f * c + 3.f) ? 1u << c : 0u;
-    }
-    if (!mx || !my) return 0u;
+    const float dy0 = y0 - g.ay;
+    const float xa = g.ax - g.eps, xb = g.ax + g.eps;
+    const float qx = -0.25f * (x0 + 3.f), px = -0.25f * x0;
     uint32_t m = 0;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const float lo = fmaxf(y0 + 4.f * r - g.ay, -g.hy), hi = fminf(y0 + 4.f * r + 3.f - g.ay, g.hy);
-        const float ul = fminf(fmaxf(g.us, lo), hi), ur = fminf(fmaxf(-g.us, lo), hi);
-        const float wl = sqrtf(fmaxf(g.twoA_tau - g.det * ul * ul, 0.f));
-        const float wr = sqrtf(fmaxf(g.twoA_tau - g.det * ur * ur, 0.f));
-        const float xmin = g.ax + (-g.B * ul - wl) * g.inv_A - g.eps, xmax = g.ax + (-g.B * ur + wr) * g.inv_A + g.eps;
-        uint32_t cm = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) cm |= (xmax >= x0 + 4.f * c && xmin <= x0 + 4.f * c + 3.f) ? 1u << c : 0u;
-        cm &= ((my >> r) & 1u) ? mx : 0u;
+        const float ylo = dy0 + 4.f * r, yhi = ylo + 3.f;
+        const bool row = yhi >= -g.hy && ylo <= g.hy;  // the row meets the ellipse's y-span
+        const float lo = fmaxf(ylo, -g.hy), hi = fminf(yhi, g.hy);
+        const float ul = __builtin_amdgcn_fmed3f(g.us, lo, hi), ur = __builtin_amdgcn_fmed3f(-g.us, lo, hi);
+        const float wl = __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-g.det * ul, ul, g.twoA_tau), 0.f));
+        const float wr = __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-g.det * ur, ur, g.twoA_tau), 0.f));
+        const float xmin = xa - __builtin_fmaf(g.B, ul, wl) * g.inv_A;
+        const float xmax = xb + __builtin_fmaf(-g.B, ur, wr) * g.inv_A;
+        // column range, clamped to [0, 4) / [-1, 3] in float before the conversion
+        const int clo = (int)__builtin_amdgcn_fmed3f(ceilf(__builtin_fmaf(xmin, 0.25f, qx)), 0.f, 4.f);
+        const int chi = (int)__builtin_amdgcn_fmed3f(floorf(__builtin_fmaf(xmax, 0.25f, px)), -1.f, 3.f);
+        const uint32_t cm = row ? ((1u << (chi + 1)) - 1u) & ~((1u << clo) - 1u) : 0u;  // (chi + 1, clo in [0, 4])
         // block (column c, row r) -> bit 4w + rr, w = 2 (r >> 1) + (c >> 1), rr = 2 (r & 1) + (c & 1)
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-            m |= ((cm >> c) & 1u) << (4 * (2 * (r >> 1) + (c >> 1)) + 2 * (r & 1) + (c & 1));
+        const int base = 8 * (r >> 1) + 2 * (r & 1);
+        m |= ((cm & 3u) << base) | ((cm >> 2) << (base + 4));
     }
     return m;
 }
