@@ -252,17 +252,13 @@ def main():
     bytes_per_launch = 8 * Tt + 52 * I_avg + 32 * N + 56 * P
     dur_s = rb["avg_us"] * 1e-6
     achieved = bytes_per_launch / dur_s / 1e9 if dur_s > 0 else 0.0
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "render_bwd_pmc.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    # traffic: HBM bytes per launch from a separate rocprofv3 PMC pass (FETCH_SIZE / WRITE_SIZE, calibrated;
+    # counters cannot be collected inside the timed run) -- committed, so the line names where it came from
+    traffic, traffic_source = committed_traffic("render_bwd_pmc.json")
     roofline = {"kernel": "render_bwd_kernel", "bound": "hbm", "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic, "alg_bytes_per_launch": int(bytes_per_launch), "avg_us": round(rb["avg_us"], 2),
-                "num_rendered_avg": int(I_avg), "launches_timed": int(rb["launches"]),
+                "traffic": traffic, "traffic_source": traffic_source, "alg_bytes_per_launch": int(bytes_per_launch),
+                "avg_us": round(rb["avg_us"], 2), "num_rendered_avg": int(I_avg), "launches_timed": int(rb["launches"]),
                 "timing": "in-kernel wall_clock64 (first workgroup start to last workgroup end) of every launch in the timed HIP-graph replays" if tracker is not None
                 else "hipEvents around each launch"}
 
@@ -740,6 +736,22 @@ def fisher_dropin(params, cam, poses, dev):
                     "grad + im.backward(1e-3), eager, one pose at a time"}
 
 
+def committed_traffic(name):
+    """roofline.traffic: calibrated HBM bytes per launch from a separate rocprofv3 PMC pass (FETCH_SIZE /
+    WRITE_SIZE; counters cannot be collected inside the timed run), committed under profiles/ by
+    tools/make_profiles.py -- returned with where it came from (file, summary, commit of the pass)."""
+    pmc = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(pmc):
+        return None, None
+    try:
+        d = json.load(open(pmc))
+    except Exception:
+        return None, None
+    return d.get("hbm_bytes_per_launch"), {"kind": "committed PMC pass, not measured in this run",
+                                           "file": f"profiles/{name}", "summary": d.get("source"),
+                                           "commit": d.get("commit"), "kernel_avg_us_in_pass": d.get("kernel_avg_us")}
+
+
 def render_bwd_roofline(rb, I_avg, P, W, H, graph: bool):
     """SURVEY.md 8(d) algorithmic bytes of one dual render-backward launch over its measured duration."""
     Tt = ((W + 15) // 16) * ((H + 15) // 16)
@@ -826,6 +838,7 @@ def run_mapping(args, world, rank, dev):
     value = steps * world / elapsed
     nr = mapper.num_rendered()
     roofline = render_bwd_roofline(stages["render_bwd"], sum(nr) / len(nr), P, W, H, graph=True)
+    roofline["traffic"], roofline["traffic_source"] = committed_traffic("mapping_render_bwd_pmc.json")
     line = {
         "metric": f"mapping iterations/sec @{W}x{H}, {P // 1000}k anisotropic Gaussians, SH degree "
                   f"{scene.sh_degree}", "value": round(value, 3), "unit": "iterations/s", "n_gpus": world,

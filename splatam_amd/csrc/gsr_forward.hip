@@ -953,7 +953,10 @@ __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, E
 #ifndef GSR_FWD_ABLATE
 #define GSR_FWD_ABLATE 0  // timing ablations (tools/gpu_round.sh ab=; results invalid except 5, 6): 1 no per-tile
                           // sort, 2 no walk, 4 no tracking-loss epilogue, 5 bounding-box block masks, 6 no block
-                          // masks.  0 in every real build
+                          // masks, 7 masks of an earlier launch read back.  0 in every real build
+#endif
+#if GSR_FWD_ABLATE == 7
+static __device__ uint16_t g_fab_mask[1u << 23];
 #endif
 __device__ __forceinline__ void tile_sort_bucket(uint64_t* __restrict__ src, uint32_t cnt,
                                                  PointEntry* __restrict__ dst, uint64_t* sk) {
@@ -1254,8 +1257,19 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
             float xs = x0, ys = y0;
             asm volatile("" : "+v"(xs), "+v"(ys));  // block bounds formed here, not hoisted (VGPRs)
             // (GSR_FWD_ABLATE 5: the bounding-box mask; 6: every block -- timing ablations)
-            const uint32_t pm = GSR_FWD_ABLATE == 5 ? block_mask(pa, pb, xs, ys)
-                              : GSR_FWD_ABLATE == 6 ? 0xFFFFu : block_mask_exact(pa, pb, xs, ys);
+            uint32_t pm = GSR_FWD_ABLATE == 5 ? block_mask(pa, pb, xs, ys)
+                        : GSR_FWD_ABLATE == 6 ? 0xFFFFu : 0u;
+#if GSR_FWD_ABLATE == 7
+            // timing only: the exact masks of an earlier launch read back by sorted position (the bound of
+            // forming them outside this kernel; valid only while the same frame is rendered again)
+            pm = g_fab_mask[start + tid];
+            if (pm == 0u) {
+                pm = block_mask_exact(pa, pb, xs, ys);
+                g_fab_mask[start + tid] = (uint16_t)pm;
+            }
+#else
+            if (GSR_FWD_ABLATE != 5 && GSR_FWD_ABLATE != 6) pm = block_mask_exact(pa, pb, xs, ys);
+#endif
             s_a[tid] = pa;
             s_b[tid] = pb;
             s_c[tid] = pc;

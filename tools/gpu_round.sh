@@ -10,7 +10,9 @@
 #   map              the mapping bench leg alone (config 4)
 #   prof             rocprofv3 kernel trace + stats of the headline bench (tracking legs only)
 #   pmc              FETCH_SIZE / WRITE_SIZE passes (one rocprofv3 run per counter) of the headline bench
+#   mpmc             map step + FETCH_SIZE / WRITE_SIZE passes of the mapping bench (render kernels, config 4)
 #   sq               SQ issue / wait / LDS counters of the render kernels (two passes, <= 8 SQ counters each)
+#   unit             host / device split of the unchanged-caller unit (tools/raster_unit_profile.py, config 3)
 #   stream           tools/micro/stream: STREAM copy / triad GB/s (the measured HBM peak)
 #   lock             render_bwd row-list lockstep statistics (tools/lockstep_stats.py, configs 3 and 4)
 #   phase            render_fwd / render_bwd phase shares (tools/phase.py; needs _diag/libgsr_phase.so)
@@ -43,6 +45,14 @@ for s in "$@"; do
                --output-format csv -- python "$ROOT/bench.py" --steps 20 --warmup 20 $LIGHT > "$OUT/pmc_$C.log" 2>&1 ) \
                || { echo "pmc $C failed"; tail -20 "$OUT/pmc_$C.log"; exit 1; }
          done ;;
+    mpmc) timeout -k 10 300 python bench.py --workload mapping --cpu-baseline off > "$OUT/map.log" 2>&1 \
+             || { echo "map failed"; tail -30 "$OUT/map.log"; exit 1; }
+         for C in FETCH_SIZE WRITE_SIZE; do
+           ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $C \
+               --kernel-include-regex 'render_|gauss_bwd' -T -d "$OUT/pmc_map_$C" -o run --output-format csv \
+               -- python "$ROOT/bench.py" --workload mapping --steps 5 --warmup 5 --cpu-baseline off \
+               > "$OUT/pmc_map_$C.log" 2>&1 ) || { echo "pmc map $C failed"; tail -20 "$OUT/pmc_map_$C.log"; exit 1; }
+         done ;;
     sq) G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
         G2="SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
         i=0
@@ -52,6 +62,8 @@ for s in "$@"; do
               -d "$OUT/sq$i" -o run --output-format csv -- python "$ROOT/bench.py" --steps 20 --warmup 20 $LIGHT \
               > "$OUT/sq$i.log" 2>&1 ) || { echo "sq pass $i failed"; tail -20 "$OUT/sq$i.log"; exit 1; }
         done ;;
+    unit) timeout -k 10 300 python tools/raster_unit_profile.py --n 200 --out "$OUT/raster_unit_profile.txt" \
+             > "$OUT/unit.log" 2>&1 || { echo "unit failed"; tail -20 "$OUT/unit.log"; exit 1; } ;;
     stream) timeout -k 10 120 tools/micro/stream > "$OUT/stream.json" 2>&1 || { echo "stream failed"; exit 1; } ;;
     lock) timeout -k 10 200 python tools/lockstep_stats.py 3 128 > "$OUT/lockstep3.txt" 2>&1 && \
           timeout -k 10 200 python tools/lockstep_stats.py 4 128 > "$OUT/lockstep4.txt" 2>&1 || { echo "lock failed"; exit 1; } ;;

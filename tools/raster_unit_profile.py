@@ -4,9 +4,15 @@
 
 Prints, per unit: wall time; host time spent in each phase (first forward incl. its host sync,
 second forward incl. the geometry-reuse comparison, loss, backward); the device time of every kernel
-(torch.profiler) and the device-idle remainder.  Usage: python tools/raster_unit_profile.py [--n 200]"""
+(torch.profiler) and the device-idle remainder; the wall time of the same unit over a 1000-Gaussian scene at
+the same image size (the host floor: the same Python, marshalling, allocations and launches with almost no
+device work); and the top Python functions of that tiny-scene unit (cProfile, tottime).
+Usage: python tools/raster_unit_profile.py [--n 200] [--config 3] [--out file.txt]"""
 import argparse
+import cProfile
+import io
 import os
+import pstats
 import sys
 import time
 
@@ -24,7 +30,7 @@ def main():
     a = ap.parse_args()
     import diff_gaussian_rasterization as dgr
     from splatam_amd import _C
-    from splatam_amd.scenes import config_scene
+    from splatam_amd.scenes import config_scene, make_scene
     from splatam_amd.slam import camera_settings, init_tracking_params, transform_to_frame, \
         transformed_params2depthplussilhouette, transformed_params2rendervar
     dev = torch.device("cuda", 0)
@@ -92,6 +98,33 @@ def main():
     for k, (us, c) in sorted(kern.items(), key=lambda kv: -kv[1][0]):
         lines.append(f"  {us:8.1f}  x{c:4.1f}  {k[:110]}")
     lines.append(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=30))
+    # host floor: the same unit over 1000 Gaussians (same image size, same calls and allocations)
+    tiny = make_scene(1000, W, H, seed=3)
+    tp = init_tracking_params(tiny, num_frames=1, device=dev)
+    with torch.no_grad():
+        ttg = transform_to_frame(tp, 0, False, False)
+        trv1 = leaf(transformed_params2rendervar(tp, ttg))
+        trv2 = leaf(transformed_params2depthplussilhouette(tp, w2c, ttg))
+    trv2["means3D"] = trv1["means3D"]
+    rv1, rv2 = trv1, trv2  # unit() reads these names
+    for _ in range(10):
+        unit()
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    for _ in range(a.n):
+        unit()
+    torch.cuda.synchronize()
+    floor_us = 1e6 * (time.perf_counter() - t3) / a.n
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(100):
+        unit()
+    torch.cuda.synchronize()
+    pr.disable()
+    buf = io.StringIO()
+    pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(25)
+    lines.append(f"host floor (1000 Gaussians, {W}x{H}): unit wall {floor_us:.1f} us; cProfile of 100 such units:")
+    lines.append(buf.getvalue())
     txt = "\n".join(lines)
     print(txt)
     if a.out:
