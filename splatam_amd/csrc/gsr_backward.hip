@@ -400,15 +400,13 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         dg.phase(2);
         const int jlo16 = 16 * (hi - (int)last);  // pos = hi-1-j < last  <=>  j >= jlo  <=>  16 j >= 16 jlo
         for (int i = 0; i < n; i += 4) {
-            const uint4 gw = load_slot_group4(my_list, i);
-            // this lane's entry slot (the reduction's writer lanes): the high half of its entry's word,
-            // read from LDS instead of selected from gw
+            // this lane's entry slot (the reduction's writer lanes): the high half of its entry's word
             const uint32_t soff = reinterpret_cast<const uint16_t*>(my_list + i + my_e)[1];
-            int jb[4];  // byte offsets 16 j of the step's entries in s_a / s_b / s_c / s_d
-            jb[0] = (int)(gw.x & 0xFFFFu);
-            jb[1] = (int)(gw.y & 0xFFFFu);
-            jb[2] = (int)(gw.z & 0xFFFFu);
-            jb[3] = (int)(gw.w & 0xFFFFu);
+            // byte offsets 16 j of the step's entries in s_a / s_b / s_c / s_d: the low halves of the four
+            // words, one ds_read_u16 each (zero-extended by the load: no v_and per entry on the VALU)
+            int jb[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) jb[k] = (int)reinterpret_cast<const uint16_t*>(my_list + i + k)[0];
             auto rec = [&](const float4* arr, int k) {
                 return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(arr) + jb[k]);
             };

@@ -638,9 +638,10 @@ __device__ __forceinline__ int build_wave_list(const uint8_t* s_mask, int cnt, i
 // then padded with `pad` (the index of a staged dummy entry that never blends)
 // up to the returned length: the longest list rounded up to 4, so the rows of
 // a wave step through their lists in lockstep with no validity tests.
+// jmul scales the stored j (the walk may take it as an LDS byte offset; j * jmul must stay below 2^16).
 template <typename MaskOf>
 __device__ __forceinline__ int build_row_lists_by(MaskOf mask_of, int cnt, int w, const int (&jmin)[4],
-                                                  uint16_t* list, int stride, uint16_t pad) {
+                                                  uint16_t* list, int stride, uint16_t pad, uint32_t jmul = 1u) {
     const int lane = __lane_id();
     int n[4] = {0, 0, 0, 0};
     for (int c = 0; c < cnt; c += 64) {
@@ -651,7 +652,8 @@ __device__ __forceinline__ int build_row_lists_by(MaskOf mask_of, int cnt, int w
             // the row's lanes as an SGPR mask: its lane prefix by v_mbcnt, the store predicated on it
             const uint64_t bal = __builtin_amdgcn_uicmp((m >> r) & 1u, 0u, 33 /* ne */) &
                                  __builtin_amdgcn_sicmp(j, jmin[r], 39 /* sge */);
-            if (__builtin_amdgcn_inverse_ballot_w64(bal)) list[r * stride + n[r] + (int)lanes_below(bal)] = (uint16_t)j;
+            if (__builtin_amdgcn_inverse_ballot_w64(bal))
+                list[r * stride + n[r] + (int)lanes_below(bal)] = (uint16_t)((uint32_t)j * jmul);
             n[r] += __popcll(bal);
         }
     }
@@ -662,8 +664,8 @@ __device__ __forceinline__ int build_row_lists_by(MaskOf mask_of, int cnt, int w
     return len;
 }
 __device__ __forceinline__ int build_row_lists(const uint16_t* s_mask, int cnt, int w, const int (&jmin)[4],
-                                               uint16_t* list, int stride, uint16_t pad) {
-    return build_row_lists_by([&](int j) { return (uint32_t)s_mask[j]; }, cnt, w, jmin, list, stride, pad);
+                                               uint16_t* list, int stride, uint16_t pad, uint32_t jmul = 1u) {
+    return build_row_lists_by([&](int j) { return (uint32_t)s_mask[j]; }, cnt, w, jmin, list, stride, pad, jmul);
 }
 
 // Four consecutive entries of this lane's (padded) row list, per lane (VGPR).

@@ -1213,7 +1213,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
     float T = 1.f, C2 = 0.f, D = 15.0f;  // forward.cu:308 median-depth default
     float C5 = 0.f;
     v2f C01 = v2f{0.f, 0.f}, C34 = v2f{0.f, 0.f};  // channel pairs: one v_pk_fma_f32 per pair and Gaussian
-    uint32_t last = 0;
+    uint32_t last16 = 0;  // 16 x n_contrib
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pc = pa, pd = pa;
     uint32_t pg = 0, pgn = 0;  // the staged entry's Gaussian id, the id of the entry a batch later
     if (keys != nullptr) {
@@ -1282,18 +1282,27 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         fetch_rec(start + RENDER_BATCH);      // records of the next batch (ids loaded a batch ago)
         fetch_id(start + 2 * RENDER_BATCH);   // ids of the batch after it
         const int jmin0[4] = {0, 0, 0, 0};
-        const int n = build_row_lists(s_mask, cnt, w, jmin0, s_list + 4 * w * LS, LS, (uint16_t)RENDER_BATCH);
+        // list entries: LDS byte offsets 16 j of the staged records (the walk loads them with ds_read_u16)
+        static_assert(16 * RENDER_BATCH < 65536, "16-bit byte offsets");
+        const int n = build_row_lists(s_mask, cnt, w, jmin0, s_list + 4 * w * LS, LS, (uint16_t)(16 * RENDER_BATCH),
+                                      16u);
         const uint16_t* my_list = s_list + (4 * w + row) * LS;
-        const uint32_t pos0 = start - range.x;
+        const uint32_t pos16 = 16u * (start - range.x) + 16u;  // 16 (position of entry 0 + 1)
         dg.phase(2);
         for (int i = 0; i < (GSR_FWD_ABLATE == 2 ? 0 : n); i += 4) {
             if (__ballot(!done) == 0ull) break;
-            const RowGroup4 gq = load_row_group4(my_list, i);
+            int jb[4];  // byte offsets 16 j, one ds_read_u16 each (no unpacking on the VALU; volatile keeps
+#pragma unroll  // the four adjacent u16 loads from being merged into one b64 load + 4 VALU unpacks)
+            for (int k = 0; k < 4; k++)
+                jb[k] = (int)((const volatile __attribute__((address_space(3))) uint16_t*)my_list)[i + k];
+            auto rec = [&](const float4* arr, int k) {
+                return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(arr) + jb[k]);
+            };
             float alpha[4], depth[4];
             bool ok[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const float4 a = s_a[gq.j[k]], b = s_b[gq.j[k]];
+                const float4 a = rec(s_a, k), b = rec(s_b, k);
                 const float p2 = eval_p2(a, b, pix_delta(a, pix));           // log2(e) * power
                 alpha[k] = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(fminf(p2, 0.f)));
                 depth[k] = b.z;
@@ -1309,9 +1318,9 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
                 const bool term = okk && test_T < 0.0001f;
                 done = done || term;
                 const bool blend = okk && !term;
-                const float4 c = s_c[gq.j[k]];
+                const float4 c = rec(s_c, k);
                 float4 c2;
-                if (DUAL) c2 = s_d[gq.j[k]];
+                if (DUAL) c2 = rec(s_d, k);
                 if (blend) {
                     const float wgt = alpha[k] * T;
                     C01 = __builtin_elementwise_fma(v2f{c.x, c.y}, v2f{wgt, wgt}, C01);
@@ -1322,7 +1331,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
                     }
                     if (T > 0.5f && test_T < 0.5f) D = depth[k];  // median depth (forward.cu:368-372)
                     T = test_T;
-                    last = pos0 + (uint32_t)gq.j[k] + 1u;          // entries visited up to the last blend
+                    last16 = pos16 + (uint32_t)jb[k];              // 16 x entries visited up to the last blend
                 }
             }
         }
@@ -1349,7 +1358,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
         const int pid = py * cam.W + px;
         const int HW = cam.W * cam.H;
         final_T[pid] = T;
-        n_contrib[pid] = last;
+        n_contrib[pid] = last16 >> 4;
         out_color[pid] = C0 + T * cam.bg[0];
         out_color[HW + pid] = C1 + T * cam.bg[1];
         out_color[2 * HW + pid] = C2 + T * cam.bg[2];

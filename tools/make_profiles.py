@@ -13,6 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def head_commit():
+    """The commit the GPU run was made from: GSR_PROFILE_COMMIT if set (summaries made after later edits),
+    else this tree's HEAD (+dirty-csrc when the kernel sources differ from it)."""
+    if os.environ.get("GSR_PROFILE_COMMIT"):
+        return os.environ["GSR_PROFILE_COMMIT"]
     import subprocess
     r = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True, text=True)
     d = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--untracked-files=no", "splatam_amd/csrc",

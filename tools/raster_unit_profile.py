@@ -125,6 +125,36 @@ def main():
     pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(25)
     lines.append(f"host floor (1000 Gaussians, {W}x{H}): unit wall {floor_us:.1f} us; cProfile of 100 such units:")
     lines.append(buf.getvalue())
+    # host cost per call (tiny scene): the binding's backward without the autograd engine, the bare C call
+    # with pre-built arguments, and the forward (which waits for num_rendered like the reference)
+    from splatam_amd._lib import ALLOC_FN, GsrGrads, lib  # noqa: F401
+    s_ = cam
+    with torch.no_grad():
+        args = (s_.bg, trv1["means3D"], trv1["colors_precomp"], trv1["opacities"], trv1["scales"],
+                trv1["rotations"], s_.scale_modifier, torch.Tensor([]), s_.viewmatrix, s_.projmatrix, s_.tanfovx,
+                s_.tanfovy, s_.image_height, s_.image_width, torch.Tensor([]), s_.sh_degree, s_.campos,
+                s_.prefiltered)
+        nr, color, radii, gb, bb, ib, depth = _C.rasterize_gaussians(*args)
+        torch.cuda.synchronize()
+        k = 500
+        t = time.perf_counter()
+        for _ in range(k):
+            _C.rasterize_gaussians(*args)
+        fwd_us = 1e6 * (time.perf_counter() - t) / k
+        torch.cuda.synchronize()
+        bargs = (s_.bg, trv1["means3D"], radii, trv1["colors_precomp"], trv1["scales"], trv1["rotations"],
+                 s_.scale_modifier, torch.Tensor([]), s_.viewmatrix, s_.projmatrix, s_.tanfovx, s_.tanfovy, g1,
+                 torch.Tensor([]), s_.sh_degree, s_.campos, gb, nr, bb, ib)
+        t = time.perf_counter()
+        for _ in range(k):
+            _C.rasterize_gaussians_backward(*bargs)
+        bwd_host_us = 1e6 * (time.perf_counter() - t) / k
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        torch.cuda.synchronize()
+        sync_us = 1e6 * (time.perf_counter() - t)
+    lines.append(f"host cost per call (1000 Gaussians): forward {fwd_us:.1f} us (incl. its wait for num_rendered), "
+                 f"backward binding {bwd_host_us:.1f} us (host only, no sync), idle synchronize {sync_us:.1f} us")
     txt = "\n".join(lines)
     print(txt)
     if a.out:
