@@ -953,7 +953,7 @@ __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, E
 #ifndef GSR_FWD_ABLATE
 #define GSR_FWD_ABLATE 0  // timing ablations (tools/gpu_round.sh ab=; results invalid except 5, 6): 1 no per-tile
                           // sort, 2 no walk, 4 no tracking-loss epilogue, 5 bounding-box block masks, 6 no block
-                          // masks, 7 masks of an earlier launch read back.  0 in every real build
+                          // masks, 7 masks of an earlier launch read back, 8 no image stores.  0 in every real build
 #endif
 #if GSR_FWD_ABLATE == 7
 static __device__ uint16_t g_fab_mask[1u << 23];
@@ -1354,7 +1354,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
             for (int c = 0; c < 3; c++) l1_gi[c] = l1.gt_im[c * HW + pid];
         }
     }
-    if (inside) {
+    if (inside && (GSR_FWD_ABLATE != 8 || T == 1.2345f)) {  // (ablation 8: no image stores, values kept live)
         const int pid = py * cam.W + px;
         const int HW = cam.W * cam.H;
         final_T[pid] = T;
