@@ -79,6 +79,12 @@ def parse():
     ap.add_argument("--configs", choices=("auto", "on", "off"), default="auto",
                     help="BASELINE configs 1 (forward only) and 2 (fwd+bwd RGB + depth) on the GPU and the CPU "
                          "oracle beside the headline (auto: N=1 only)")
+    ap.add_argument("--fuse-render", type=int, default=1,
+                    help="tracking: 1 = the render forward and render backward of an iteration in one launch "
+                         "(render_track_kernel), 0 = separate render_fwd / render_bwd launches")
+    ap.add_argument("--unfused-leg", choices=("on", "off"), default="on",
+                    help="with --fuse-render 1 at N=1: also time a few iterations with separate render launches "
+                         "(roofline.unfused: render_bwd's own time and roofline)")
     ap.add_argument("--timing", type=int, default=1,
                     help="0: no device-clock timing of render_bwd in the graph (A/B check; no roofline)")
     return ap.parse_args()
@@ -161,7 +167,9 @@ def main():
         # HIP graph of S tracking iterations (splatam_amd/tracker.py).  Exactly `steps` iterations are
         # timed: frames of FI iterations (fresh optimizer, best-candidate write-back), the last one
         # partial when FI does not divide steps; S divides both so every frame is whole replays.
+        from splatam_amd import glue
         from splatam_amd.tracker import GraphTracker
+        glue._RENDER_FUSED = glue._RENDER_FUSED and bool(args.fuse_render)
         S = math.gcd(math.gcd(max(1, args.iters_per_graph), FI), max(1, steps))
         # warm-up: W eager tracking iterations plus one priming replay, all undone (pose restored,
         # optimizer reset) before the timed frames
@@ -249,18 +257,33 @@ def main():
         I_avg = rb["units"] / max(rb["launches"], 1)
     # SURVEY.md 8(d) per-rasterization bytes 8*Tt + 40*I + 20*N + 44*P, for the dual launch
     # (both colour sets): + colors2 gather 12*I, + dL_dpix2 12*N, + dcolors2 12*P
-    bytes_per_launch = 8 * Tt + 52 * I_avg + 32 * N + 56 * P
-    dur_s = rb["avg_us"] * 1e-6
+    bwd_bytes = 8 * Tt + 52 * I_avg + 32 * N + 56 * P
+    # render fwd 8*Tt + 44*I + 24*N per rasterization, dual: + colors2 gather 12*I, + out_color2 12*N
+    fwd_bytes = 8 * Tt + 56 * I_avg + 36 * N
+    fused = rb["launches"] == 0 and stages["render_fwd"]["launches"] > 0
+    if fused:  # render_track_kernel: the tracking forward and render backward in one launch (stage render_fwd)
+        rk, bytes_per_launch, kname = stages["render_fwd"], fwd_bytes + bwd_bytes, "render_track_kernel"
+        traffic, traffic_source = committed_traffic("render_track_pmc.json")
+    else:
+        rk, bytes_per_launch, kname = rb, bwd_bytes, "render_bwd_kernel"
+        # traffic: HBM bytes per launch from a separate rocprofv3 PMC pass (FETCH_SIZE / WRITE_SIZE,
+        # calibrated; counters cannot be collected inside the timed run) -- committed, so the line names
+        # where it came from
+        traffic, traffic_source = committed_traffic("render_bwd_pmc.json")
+    dur_s = rk["avg_us"] * 1e-6
     achieved = bytes_per_launch / dur_s / 1e9 if dur_s > 0 else 0.0
-    # traffic: HBM bytes per launch from a separate rocprofv3 PMC pass (FETCH_SIZE / WRITE_SIZE, calibrated;
-    # counters cannot be collected inside the timed run) -- committed, so the line names where it came from
-    traffic, traffic_source = committed_traffic("render_bwd_pmc.json")
-    roofline = {"kernel": "render_bwd_kernel", "bound": "hbm", "achieved": round(achieved, 2),
+    roofline = {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic, "traffic_source": traffic_source, "alg_bytes_per_launch": int(bytes_per_launch),
-                "avg_us": round(rb["avg_us"], 2), "num_rendered_avg": int(I_avg), "launches_timed": int(rb["launches"]),
+                "avg_us": round(rk["avg_us"], 2), "num_rendered_avg": int(I_avg), "launches_timed": int(rk["launches"]),
                 "timing": "in-kernel wall_clock64 (first workgroup start to last workgroup end) of every launch in the timed HIP-graph replays" if tracker is not None
                 else "hipEvents around each launch"}
+    if fused:
+        roofline["fused"] = ("the tracking iteration's render forward (+ L1 loss) and render backward in one "
+                             "launch per tile (gsr_track_forward_backward_dual_static_xf); alg bytes = SURVEY 8(d)'s "
+                             "dual render fwd + render bwd")
+        if world == 1 and args.unfused_leg == "on":
+            roofline["unfused"] = unfused_render_leg(params, curr, frame, tracker.iters, P, W, H, Tt, N)
 
     dropin = dropin_leg(args, scene, dev) if args.dropin == "on" else None
     configs = None
@@ -323,6 +346,8 @@ def main():
         # for one colour set, +9 for the second set of the dual launch (dot product, 3 products, 3 sums);
         # one dual launch evaluates each pair once for both renders (the oracle counts both renders)
         flops = 12 * evals / 2 + 54 * contrib / 2
+        if fused:  # + the forward's: F_eval 12 per evaluated pair, +14 per contributing pair (+3 for colours2)
+            flops += 12 * evals / 2 + 17 * contrib / 2
         roofline["valu"] = {"achieved_tflops": round(flops / dur_s / 1e12, 3) if dur_s > 0 else None,
                             "peak_tflops": VALU_PEAK_TFLOPS,
                             "frac": round(flops / dur_s / 1e12 / VALU_PEAK_TFLOPS, 4) if dur_s > 0 else None,
@@ -734,6 +759,44 @@ def fisher_dropin(params, cam, poses, dev):
             "path": "unchanged scripts/ros_handler.py compute_Hessian: torch glue + hessian_diff_gaussian_"
                     "rasterization_w_depth.GaussianRasterizer(backward_power=2) with every rendervar requiring "
                     "grad + im.backward(1e-3), eager, one pose at a time"}
+
+
+def unfused_render_leg(params, curr, frame, S, P, W, H, Tt, N, replays: int = 4):
+    """The same tracking iterations with render_fwd and render_bwd as separate launches
+    (GSR_TRACK_RENDER_FUSED=0's path): both kernels' in-kernel times, render_bwd's own roofline, frames/s."""
+    from splatam_amd import glue, profiling
+    from splatam_amd.tracker import GraphTracker
+    prev = glue._RENDER_FUSED
+    glue._RENDER_FUSED = False
+    try:
+        with torch.no_grad():
+            q0 = params["cam_unnorm_rots"][..., frame].clone()
+            t0 = params["cam_trans"][..., frame].clone()
+        tr = GraphTracker(params, curr, frame, iters_per_graph=S, fuse_pose=True, warmup_iters=1, prime=True)
+        profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        tr.track_frame(S * replays, check=False)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - ta
+        st = profiling.read_timing()
+        profiling.enable_timing(False)
+        overflow = tr.overflowed()
+        nr = tr.num_rendered()
+        with torch.no_grad():
+            params["cam_unnorm_rots"][..., frame] = q0
+            params["cam_trans"][..., frame] = t0
+        del tr
+    finally:
+        glue._RENDER_FUSED = prev
+    I_avg = sum(nr) / len(nr)
+    rb = st["render_bwd"]
+    alg = 8 * Tt + 52 * I_avg + 32 * N + 56 * P
+    dur = rb["avg_us"] * 1e-6
+    return {"frames_per_s": round(S * replays / el, 2), "render_fwd_us": round(st["render_fwd"]["avg_us"], 2),
+            "render_bwd_us": round(rb["avg_us"], 2), "render_bwd_alg_bytes": int(alg),
+            "render_bwd_frac": round(alg / dur / 1e9 / HBM_PEAK_GBS, 5) if dur > 0 else None,
+            "overflow": bool(overflow), "iterations": S * replays}
 
 
 def committed_traffic(name):

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 5
+#define GSR_ABI_VERSION 6
 
 /* error codes */
 #define GSR_OK 0

@@ -189,6 +189,33 @@ int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* g
                             float* dL_dcam_q, float* dL_dcam_t, float* scratch, const gsr_pose_track* track,
                             const float* log_scales, gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
+/* The tracking iteration's render forward and render backward in ONE launch (render_track_kernel):
+ * gsr_track_forward_dual_static_xf's forward + L1 loss, then in the same workgroup the back-to-front
+ * walk of gsr_track_backward_dual's render backward -- SplaTAM's tracking loss gradient is per pixel
+ * (dL/dloss is the static seed dL_dloss), so a tile's backward needs nothing from other tiles and runs
+ * from the pixel state still in registers.  inst_records: gsr_track_records_floats(capacity) floats
+ * (device), receiving the per-instance sums gsr_track_backward_dual_records reads; they equal, bit for
+ * bit, what gsr_track_backward_dual's render backward forms.  The gradient images are not formed. */
+int gsr_track_records_floats(int capacity);
+int gsr_track_forward_backward_dual_static_xf(const gsr_settings* settings, const gsr_gaussians* gaussians,
+                                              float* colors2, const gsr_track_xform* xform, int capacity,
+                                              unsigned* status, float* out_color, float* out_color2,
+                                              float* out_depth, int* radii, const float* gt_im,
+                                              const float* gt_depth, float sil_thres, float w_im, float w_depth,
+                                              const float* dL_dloss, float* loss, float* scratch,
+                                              float* inst_records, gsr_alloc_fn alloc, void* alloc_ctx,
+                                              void* stream);
+/* gsr_track_backward_dual after gsr_track_forward_backward_dual_static_xf: only the pose-fused
+ * per-Gaussian backward (the render backward's records come from inst_records). */
+int gsr_track_backward_dual_records(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
+                                    const float* colors2, int num_rendered, const void* geom_buffer,
+                                    const void* binning_buffer, const void* image_buffer, const float* means_world,
+                                    const float* unnorm_rot, int scale_cols, float* cam_q, float* cam_t, int q_stride,
+                                    const float* w2c, double lr_q, double lr_t, double beta1, double beta2,
+                                    double eps, float* adam_state, float* dL_dcam_q, float* dL_dcam_t,
+                                    float* scratch, const gsr_pose_track* track, const float* log_scales,
+                                    const float* inst_records, gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
 /* ------------------------------------------------------------------ mapping --
  * get_loss(mapping=True, do_ba=False) (scripts/splatam.py:220-353) with the
  * Replica mapping config (configs/replica/splatam.py:82-103: use_l1,

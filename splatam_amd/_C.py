@@ -451,13 +451,15 @@ def mark_visible(means3D, viewmatrix, projmatrix):
 def track_backward_dual(settings, means3D, radii, colors, colors2, scales, rotations, dL_dout_color, dL_dout_color2,
                         geomBuffer, R, binningBuffer, imageBuffer, means_world, unnorm_rot, scale_cols, cam_q_ptr,
                         cam_t_ptr, q_stride, w2c, scratch, adam=None, dq_ptr=None, dt_ptr=None, track=None,
-                        log_scales=None):
+                        log_scales=None, records=None):
     """gsr_track_backward_dual (include/gsr_glue.h): the tracking backward with the pose chain fused into
     the per-Gaussian backward.  adam = (lr_q, lr_t, beta1, beta2, eps, state tensor) applies the Adam step
     to the pose in place; otherwise the pose gradient is written at dq_ptr / dt_ptr.  track: an optional
     GsrPoseTrack (best-candidate selection; the Adam step is skipped on an overflowing forward).
     log_scales: recompute the rendervars (means3D / rotations / scales) from the world-frame map
-    instead of reading them (a forward run with store_rendervars = 0)."""
+    instead of reading them (a forward run with store_rendervars = 0).  records: the per-instance sums of
+    a fused forward (track_forward_dual_static(records=...)): gsr_track_backward_dual_records, only the
+    per-Gaussian backward runs and the gradient images are not read (may be None)."""
     device = means3D.device
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     with torch.cuda.device(device):
@@ -473,6 +475,19 @@ def track_backward_dual(settings, means3D, radii, colors, colors2, scales, rotat
         if adam is not None:
             lr_q, lr_t, b1, b2, eps, state = adam
         _begin(device)
+        if records is not None:
+            rc = lib.gsr_track_backward_dual_records(
+                ctypes.byref(s), ctypes.byref(g), radii.data_ptr(), _ptr(c2), int(R), geomBuffer.data_ptr(),
+                binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
+                means_world.data_ptr(), unnorm_rot.data_ptr(), int(scale_cols), cam_q_ptr, cam_t_ptr, int(q_stride),
+                w2c.data_ptr(), float(lr_q), float(lr_t), float(b1), float(b2), float(eps),
+                state.data_ptr() if state is not None else None, dq_ptr, dt_ptr, scratch.data_ptr(),
+                ctypes.byref(track) if track is not None else None,
+                log_scales.data_ptr() if log_scales is not None else None, records.data_ptr(), _ALLOC_CB, None,
+                _stream(device))
+            _check(rc, "track_backward_dual_records")
+            _tls.buffers = {}
+            return
         rc = lib.gsr_track_backward_dual(
             ctypes.byref(s), ctypes.byref(g), radii.data_ptr(), _ptr(c2), dpix.data_ptr(), dpix2.data_ptr(), int(R),
             geomBuffer.data_ptr(), binningBuffer.data_ptr() if binningBuffer.numel() else None,
@@ -486,14 +501,17 @@ def track_backward_dual(settings, means3D, radii, colors, colors2, scales, rotat
 
 
 def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scales, rotations, capacity, status, gt_im,
-                              gt_depth, sil_thres, w_im, w_depth, seed, scratch, xform=None):
+                              gt_depth, sil_thres, w_im, w_depth, seed, scratch, xform=None, records=None):
     """gsr_track_forward_dual_static (include/gsr_glue.h): the static dual forward with SplaTAM's
     tracking L1 loss and its gradient images formed in the render epilogue.  Returns (num_rendered=capacity,
     color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth, loss, dL_dim, dL_ddepth_sil).
     xform = (means_world, unnorm_rot, logit_opac, log_scales, scale_cols, cam_q_ptr, cam_t_ptr, q_stride, w2c,
     store): gsr_track_forward_dual_static_xf -- the tracking transform runs inside preprocess and means3D,
     colors2, opacity, scales and rotations are its OUTPUTS (preallocated contiguous float32; written only
-    when store is true)."""
+    when store is true).  records (with xform; device float32 of lib.gsr_track_records_floats(capacity)):
+    gsr_track_forward_backward_dual_static_xf -- the tracking render backward runs in the same launch
+    and leaves its per-instance sums in records (track_backward_dual(records=...)); dL_dim / dL_ddepth_sil
+    come back None (not formed)."""
     st = settings
     device = means3D.device
     P = means3D.size(0)
@@ -523,6 +541,18 @@ def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scale
             xf = GsrTrackXform(means_world=mw.data_ptr(), unnorm_rot=ur.data_ptr(), logit_opac=lo.data_ptr(),
                                log_scales=ls.data_ptr(), scale_cols=int(scols), cam_q=q_ptr, cam_t=t_ptr,
                                q_stride=int(qs), w2c=w2c.data_ptr(), store_rendervars=int(bool(store)))
+            if records is not None:
+                if (records.device != device or records.dtype != torch.float32 or not records.is_contiguous() or
+                        records.numel() < lib.gsr_track_records_floats(int(capacity))):
+                    raise RuntimeError("records: contiguous float32 of gsr_track_records_floats(capacity) on the device")
+                n = lib.gsr_track_forward_backward_dual_static_xf(
+                    ctypes.byref(s), ctypes.byref(g), _ptr(c2), ctypes.byref(xf), int(capacity), status.data_ptr(),
+                    out_color.data_ptr(), out_color2.data_ptr(), out_depth.data_ptr(), radii.data_ptr() if P else None,
+                    gi.data_ptr(), gd.data_ptr(), float(sil_thres), float(w_im), float(w_depth), sd.data_ptr(),
+                    loss.data_ptr(), scratch.data_ptr(), records.data_ptr(), _ALLOC_CB, None, _stream(device))
+                _check(n, "track_forward_backward_dual_static_xf")
+                bufs = _tls.buffers
+                return (int(n), out_color, out_color2, radii, bufs[0], bufs[1], bufs[2], out_depth, loss, None, None)
             n = lib.gsr_track_forward_dual_static_xf(
                 ctypes.byref(s), ctypes.byref(g), _ptr(c2), ctypes.byref(xf), int(capacity), status.data_ptr(),
                 out_color.data_ptr(), out_color2.data_ptr(), out_depth.data_ptr(), radii.data_ptr() if P else None,

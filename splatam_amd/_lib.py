@@ -119,6 +119,18 @@ SIGNATURES = {
                                                  c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float,
                                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ALLOC_FN, c_void_p,
                                                  c_void_p]),
+    "gsr_track_records_floats": (c_int, [c_int]),
+    "gsr_track_forward_backward_dual_static_xf": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians),
+                                                          c_void_p, ctypes.POINTER(GsrTrackXform), c_int, c_void_p,
+                                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                          c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
+                                                          c_void_p, ALLOC_FN, c_void_p, c_void_p]),
+    "gsr_track_backward_dual_records": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p,
+                                                c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                c_int, c_void_p, c_void_p, c_int, c_void_p, c_double, c_double,
+                                                c_double, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                ctypes.POINTER(GsrPoseTrack), c_void_p, c_void_p, ALLOC_FN, c_void_p,
+                                                c_void_p]),
     "gsr_backward_dual_sh_adam": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p,
                                           c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                           ctypes.POINTER(GsrGrads), c_void_p, c_int, ctypes.POINTER(GsrMapAdam),
@@ -154,15 +166,20 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         raise ImportError(f"libgsr.so not found at {path}: build it with `python -m splatam_amd.build` "
                           "(no CPU fallback exists for the rasterizer)")
     lib = ctypes.CDLL(path)
+    ab = bool(os.environ.get("GSR_LIB"))  # an A/B baseline built from an older revision (build.build_from_rev)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if ab:  # (entry points added since that revision: absent, the callers fall back)
+                continue
+            raise ImportError(f"libgsr.so lacks {name}")
         fn.restype = res
         fn.argtypes = args
     v = lib.gsr_abi_version()
-    if v != 5:
-        # an A/B baseline built from an older revision (GSR_LIB -> _diag/, build.build_from_rev) may differ in
-        # the glue structs only (ABI 4: gsr_map_adam without `halted`); the rasterizer calls are unchanged
-        if not (os.environ.get("GSR_LIB") and v == 4):
+    if v != 6:
+        # an older revision may differ in the glue structs only (ABI 4: gsr_map_adam without `halted`;
+        # ABI 5: no fused tracking render); the rasterizer calls are unchanged
+        if not (ab and v in (4, 5)):
             raise ImportError("libgsr.so ABI version mismatch")
     return lib
 

@@ -20,6 +20,7 @@
 #include "gsr_chain.h"
 #include "gsr_diag.h"
 #include "gsr_glue_common.h"
+#include "gsr_render_fwd.h"
 
 #ifndef GSR_POSE_TAIL
 #define GSR_POSE_TAIL 2  // levels of the fused pose reduction's last-workgroup sum (1 or 2)
@@ -215,6 +216,9 @@ __device__ __forceinline__ void mom_matrix(const float* S, float (&Sm)[9][9], st
 #define GSR_BWD_SPLIT6 1  // wide variants: the first reduction pass carries G dL/dalpha with the 5 geometric sums
 // (6 + 6 instead of 5 + 7 sums for mapping: 84 instead of 96 DPP adds per step, render_bwd 312 -> 303 us at config 4)
 #endif
+#ifndef GSR_NT_STORES
+#define GSR_NT_STORES 0  // render kernels' record / image stores as non-temporal (streaming) stores
+#endif
 #ifndef GSR_PACK_C
 #define GSR_PACK_C 1  // DUAL, Q2 = 1: the second colour set's one channel staged in s_c.w (no s_d array)
 #endif
@@ -223,79 +227,93 @@ constexpr int bwd_waves() {
     return MOM ? 4 : ((DUAL && Q2 == 3) ? GSR_BWD_MAP_WAVES : ((OPAC && COL1) ? GSR_BWD_WIDE_WAVES : 5));
 }
 
-template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3, int MOM = 0>
-__global__ void __launch_bounds__(TILE_PIX, (bwd_waves<DUAL, OPAC, COL1, COL2, Q2, MOM>()))
-render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry* __restrict__ point_list,
-                  const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
-                  const float* __restrict__ final_T,
-                  const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
-                  const float* __restrict__ dL_dpix2, float* __restrict__ inst, BwdGuard guard,
-                  unsigned long long* clk) {
-    static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
-    static_assert(!MOM || (!DUAL && OPAC && COL1), "the moment variants form every single-image gradient");
-    kclock_begin(clk);
-    RenderDiag dg;  // (diagnostics builds only, gsr_diag.h)
-    dg.begin();
-    if (guard.overflow()) {  // invalid forward state (static-mode overflow): touch nothing
-        kclock_end(clk);
-        return;
-    }
-    static_assert(Q2 == 1 || Q2 == 3, "Q2 is 1 or 3 channels");
-    constexpr int NV = bwd_nv<DUAL, OPAC, COL1, COL2, Q2, MOM>();
-    constexpr int O_C1 = 5 + (OPAC ? 1 : 0);
-    constexpr int BB = bwd_batch<NV, MOM>(), BS = bwd_slots<NV, MOM>();
-    constexpr int RS = (NV + 1) & ~1;  // record stride (floats)
-    constexpr int LS = BB + 4;  // row-list stride (u32)
+// A tile backward's shape and LDS layout (carved from one byte array, so a kernel that also runs the
+// forward of the same tile -- render_track_kernel -- can alias the two phases' LDS)
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2, int MOM>
+struct BwdShape {
+    static constexpr int NV = bwd_nv<DUAL, OPAC, COL1, COL2, Q2, MOM>();
+    static constexpr int BB = bwd_batch<NV, MOM>(), BS = bwd_slots<NV, MOM>();
+    static constexpr int RS = (NV + 1) & ~1;  // record stride (floats)
+    static constexpr int LS = BB + 4;          // row-list stride (u32)
     // entry BB is a dummy (opacity 0, never blends) that pads the row lists; its slot BS
     // absorbs the pad entries' (zero) sums
-    constexpr int SL = BB + 1;
+    static constexpr int SL = BB + 1;
     // PACKC: the dual render's second colour set needs only channel 0 (Q2 = 1): staged as s_c.w (the
     // tile-rect half s_c.w carried is consumed at staging), so a pair reads one colour float4, not two
-    constexpr bool PACKC = GSR_PACK_C && DUAL && Q2 == 1;
-    __shared__ float4 s_a[SL];
-    __shared__ float4 s_b[SL];
-    __shared__ float4 s_c[SL];
-    __shared__ float4 s_d[(DUAL && !PACKC) ? SL : 1];
-    __shared__ uint32_t s_u[BB];
-    __shared__ uint16_t s_mask[BB];
-    __shared__ uint16_t s_base[BB];
-    __shared__ __attribute__((aligned(16))) float s_acc[(BS + 1) * NV];
-    __shared__ uint32_t s_rmax[16];
-    __shared__ __attribute__((aligned(16))) uint32_t s_list[16 * LS];
+    static constexpr bool PACKC = GSR_PACK_C && DUAL && Q2 == 1;
+    static constexpr size_t o_a = 0, o_b = o_a + 16 * SL, o_c = o_b + 16 * SL, o_d = o_c + 16 * SL;
+    static constexpr size_t o_acc = o_d + 16 * ((DUAL && !PACKC) ? SL : 1);
+    static constexpr size_t o_list = o_acc + (4 * (BS + 1) * NV + 15) / 16 * 16;
+    static constexpr size_t o_u = o_list + 4 * 16 * LS, o_mask = o_u + 4 * BB, o_base = o_mask + 2 * BB;
+    static constexpr size_t o_rmax = (o_base + 2 * BB + 3) / 4 * 4;
+    static constexpr size_t bytes = o_rmax + 64;
+};
+
+// One thread's pixel inputs of the tile backward: the forward's final transmittance and last
+// contributor, dL/dpix of both colour sets
+struct BwdPix {
+    float T_final;
+    uint32_t last;
+    float dp0, dp1, dp2, dq0, dq1, dq2;
+};
+
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2, int MOM>
+__device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdPix& pin,
+                                         const uint2* __restrict__ ranges, const PointEntry* __restrict__ point_list,
+                                         const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
+                                         float* __restrict__ inst, const BwdGuard& guard, char* smem,
+                                         RenderDiag& dg) {
+    static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
+    static_assert(!MOM || (!DUAL && OPAC && COL1), "the moment variants form every single-image gradient");
+    static_assert(Q2 == 1 || Q2 == 3, "Q2 is 1 or 3 channels");
+    using L = BwdShape<DUAL, OPAC, COL1, COL2, Q2, MOM>;
+    constexpr int NV = L::NV;
+    constexpr int O_C1 = 5 + (OPAC ? 1 : 0);
+    constexpr int BB = L::BB, BS = L::BS, RS = L::RS, LS = L::LS;
+    constexpr bool PACKC = L::PACKC;
+    float4* const s_a = reinterpret_cast<float4*>(smem + L::o_a);
+    float4* const s_b = reinterpret_cast<float4*>(smem + L::o_b);
+    float4* const s_c = reinterpret_cast<float4*>(smem + L::o_c);
+    [[maybe_unused]] float4* const s_d = reinterpret_cast<float4*>(smem + L::o_d);
+    uint32_t* const s_u = reinterpret_cast<uint32_t*>(smem + L::o_u);
+    uint16_t* const s_mask = reinterpret_cast<uint16_t*>(smem + L::o_mask);
+    uint16_t* const s_base = reinterpret_cast<uint16_t*>(smem + L::o_base);
+    float* const s_acc = reinterpret_cast<float*>(smem + L::o_acc);
+    uint32_t* const s_rmax = reinterpret_cast<uint32_t*>(smem + L::o_rmax);
+    uint32_t* const s_list = reinterpret_cast<uint32_t*>(smem + L::o_list);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, row = (tid >> 4) & 3;
-    const int tile = sched_tile(cam), tx = tile % cam.gx, ty = tile / cam.gx;
+    const int tx = tile % cam.gx, ty = tile / cam.gx;
     const int px = tx * TILE_X + tile_px(tid);
     const int py = ty * TILE_Y + tile_py(tid);
-    const bool inside = px < cam.W && py < cam.H;
-    const int pid = py * cam.W + px;
     const float x0 = (float)(tx * TILE_X), y0 = (float)(ty * TILE_Y);
-    const int HW = cam.W * cam.H;
     const uint2 range = ranges[tile];
-    const float T_final = inside ? final_T[pid] : 0.f;
-    const uint32_t last = inside ? n_contrib[pid] : 0u;
-    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f, dq0 = 0.f, dq1 = 0.f, dq2 = 0.f;
-    if (inside) {
-        dp0 = dL_dpix[pid];
-        dp1 = dL_dpix[HW + pid];
-        dp2 = dL_dpix[2 * HW + pid];
-        if (DUAL) {
-            dq0 = dL_dpix2[pid];
-            if (Q2 == 3) {
-                dq1 = dL_dpix2[HW + pid];
-                dq2 = dL_dpix2[2 * HW + pid];
-            }
-        }
-    }
-    // per-block (row) maximum of the pixels' last contributor
-    uint32_t rmax = last;
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, o));
-    if ((lane & 15) == 0) s_rmax[4 * w + row] = rmax;
-    __syncthreads();
+    const float T_final = pin.T_final;
+    const uint32_t last = pin.last;
+    const float dp0 = pin.dp0, dp1 = pin.dp1, dp2 = pin.dp2, dq0 = pin.dq0, dq1 = pin.dq1, dq2 = pin.dq2;
+    // per-block (row) maximum of the pixels' last contributor: the forward's per-tile record (one uniform
+    // 64-B load, no reduction over n_contrib before the first list entries can be fetched), else reduced here
     uint32_t bmax = 0;
+    int rm[4];
+    if (cam.rowmax) {
+        const uint4* rp = reinterpret_cast<const uint4*>(cam.rowmax + 16 * tile);
 #pragma unroll
-    for (int b = 0; b < 16; b++) bmax = max(bmax, s_rmax[b]);
-    const int rm[4] = {(int)s_rmax[4 * w], (int)s_rmax[4 * w + 1], (int)s_rmax[4 * w + 2], (int)s_rmax[4 * w + 3]};
+        for (int b = 0; b < 4; b++) {
+            const uint4 q = rp[b];
+            bmax = max(bmax, max(max(q.x, q.y), max(q.z, q.w)));
+        }
+        const uint4 qw = rp[w];  // the wave's four blocks (a second, cached 16-B load)
+        rm[0] = (int)qw.x; rm[1] = (int)qw.y; rm[2] = (int)qw.z; rm[3] = (int)qw.w;
+    } else {
+        uint32_t rmax = last;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, o));
+        if ((lane & 15) == 0) s_rmax[4 * w + row] = rmax;
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < 16; b++) bmax = max(bmax, s_rmax[b]);
+#pragma unroll
+        for (int r = 0; r < 4; r++) rm[r] = (int)s_rmax[4 * w + r];
+    }
     // Instances behind every pixel's last contributor receive zero gradient.
     for (uint32_t k = range.x + bmax + tid; k < range.y; k += TILE_PIX) {
         const uint32_t gk = pe_id(point_list[k]);
@@ -570,7 +588,10 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
             float* dst = inst + (size_t)RS * s_u[e];  // packed record (RecLayout): the NV sums, zero pad
 #pragma unroll
             for (int i = 0; i < NQ; i++)
-                if (q + TPE * i < RS) dst[q + TPE * i] = c[i];
+                if (q + TPE * i < RS) {
+                    if (GSR_NT_STORES) __builtin_nontemporal_store(c[i], &dst[q + TPE * i]);
+                    else dst[q + TPE * i] = c[i];
+                }
         }
         dg.phase(5);
         __syncthreads();
@@ -579,8 +600,101 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
         hi -= cnt;
     }
     if (kAblate == 1 && ablate_sink == 1.2345f) inst[0] = ablate_sink;  // keeps the per-pair values alive
+}
+
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3, int MOM = 0>
+__global__ void __launch_bounds__(TILE_PIX, (bwd_waves<DUAL, OPAC, COL1, COL2, Q2, MOM>()))
+render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry* __restrict__ point_list,
+                  const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
+                  const float* __restrict__ final_T,
+                  const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
+                  const float* __restrict__ dL_dpix2, float* __restrict__ inst, BwdGuard guard,
+                  unsigned long long* clk) {
+    kclock_begin(clk);
+    RenderDiag dg;  // (diagnostics builds only, gsr_diag.h)
+    dg.begin();
+    if (guard.overflow()) {  // invalid forward state (static-mode overflow): touch nothing
+        kclock_end(clk);
+        return;
+    }
+    __shared__ __attribute__((aligned(16))) char smem[BwdShape<DUAL, OPAC, COL1, COL2, Q2, MOM>::bytes];
+    const int tid = threadIdx.x;
+    const int tile = sched_tile(cam), tx = tile % cam.gx, ty = tile / cam.gx;
+    const int px = tx * TILE_X + tile_px(tid);
+    const int py = ty * TILE_Y + tile_py(tid);
+    const bool inside = px < cam.W && py < cam.H;
+    const int pid = py * cam.W + px;
+    const int HW = cam.W * cam.H;
+    BwdPix pin{0.f, 0u, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (inside) {
+        pin.T_final = final_T[pid];
+        pin.last = n_contrib[pid];
+        pin.dp0 = dL_dpix[pid];
+        pin.dp1 = dL_dpix[HW + pid];
+        pin.dp2 = dL_dpix[2 * HW + pid];
+        if (DUAL) {
+            pin.dq0 = dL_dpix2[pid];
+            if (Q2 == 3) {
+                pin.dq1 = dL_dpix2[HW + pid];
+                pin.dq2 = dL_dpix2[2 * HW + pid];
+            }
+        }
+    }
+    bwd_tile<DUAL, OPAC, COL1, COL2, Q2, MOM>(cam, tile, pin, ranges, point_list, rr, blocksums, inst, guard, smem, dg);
     dg.end();
     kclock_end(clk);
+}
+
+// The tracking iteration's render in one launch per tile (SplaTAM get_loss(tracking=True) with a static
+// loss seed, scripts/splatam.py:220-353): the dual forward with the L1 loss epilogue, then -- in the same
+// workgroup, its LDS reused -- the back-to-front walk of the depth-channel / geometric backward
+// (render_bwd_kernel<true, false, false, true, 1>) from the pixel state still in registers.  The loss
+// gradient is per pixel, so a tile's backward needs nothing from other tiles.  Saves the second launch
+// (dispatch, drain, the end-of-kernel writeback), the backward's per-pixel reads (T, n_contrib, dL/dpix)
+// and the forward's gradient-image stores.  Results are bitwise those of render_fwd + render_bwd.
+constexpr size_t track_lds_bytes() {
+    return FwdShape<true>::bytes > BwdShape<true, false, false, true, 1, 0>::bytes
+               ? FwdShape<true>::bytes
+               : BwdShape<true, false, false, true, 1, 0>::bytes;
+}
+__global__ void __launch_bounds__(TILE_PIX, 5)
+render_track_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __restrict__ point_list,
+                    uint64_t* __restrict__ keys, const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
+                    float* __restrict__ final_T, uint32_t* __restrict__ n_contrib, float* __restrict__ out_color,
+                    float* __restrict__ out_color2, float* __restrict__ out_depth, SpecGuard guard,
+                    unsigned long long* clk, TrackL1 l1, float* __restrict__ inst) {
+    kclock_begin(clk);
+    RenderDiag dg;
+    dg.begin();
+    if (guard.overflow()) {
+        kclock_end(clk);
+        return;
+    }
+    __shared__ __attribute__((aligned(16))) char smem[track_lds_bytes()];
+    const int tile = sched_tile(cam);
+    const FwdPix f = fwd_tile<true>(cam, tile, ranges, point_list, keys, rr, guard, smem, dg);
+    float grad[4];
+    fwd_epilogue<true, true, false>(cam, tile, f, final_T, n_contrib, out_color, out_color2, out_depth, l1, grad);
+    __syncthreads();  // the forward's LDS (and its sorted point_list stores) before the backward reuses them
+    const BwdPix pin{f.T, f.last16 >> 4, grad[0], grad[1], grad[2], grad[3], 0.f, 0.f};
+    Camera cb = cam;
+    cb.rowmax = nullptr;  // the block maxima from the registers
+    bwd_tile<true, false, false, true, 1, 0>(cb, tile, pin, ranges, point_list, rr, blocksums, inst,
+                                             BwdGuard{guard.counters, guard.cap_inst}, smem, dg);
+    dg.end();
+    kclock_end(clk);
+}
+
+int track_records_stride() { return BwdShape<true, false, false, true, 1, 0>::RS; }
+
+hipError_t launch_render_track(const Camera& cam, const uint2* ranges, uint64_t* point_list, uint64_t* keys,
+                               GeomPtrs geo, float* final_T, uint32_t* n_contrib, float* out_color,
+                               float* out_color2, float* out_depth, SpecGuard guard, const TrackL1& l1, float* inst,
+                               hipStream_t s, unsigned long long* clk) {
+    hipLaunchKernelGGL(render_track_kernel, dim3(cam.gx * cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list,
+                       keys, geo.rr, geo.blocksums, final_T, n_contrib, out_color, out_color2, out_depth, guard, clk,
+                       l1, inst);
+    return hipGetLastError();
 }
 
 template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2 = 3>

@@ -300,8 +300,10 @@ size_t gsr_image_buffer_bytes(int W, int H) { return ImgLayout::make(W, H).total
 static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
                         float* out_color, float* out_color2, float* out_depth, int* radii, gsr_alloc_fn alloc,
                         void* alloc_ctx, void* stream_, int capacity = 0, uint32_t* status = nullptr,
-                        const TrackL1* l1 = nullptr, const TrackXf* xf = nullptr) {
+                        const TrackL1* l1 = nullptr, const TrackXf* xf = nullptr, float* track_inst = nullptr) {
     int rc = validate(settings, gaussians, true);
+    if (track_inst && (!l1 || !colors2 || capacity <= 0))
+        return fail(GSR_ERR_INVALID_ARG, "the fused render backward needs the static dual forward with the L1 loss");
     if (rc != GSR_OK) return rc;
     if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
     if (!out_color || !out_depth) return fail(GSR_ERR_INVALID_ARG, "output image pointers required");
@@ -330,6 +332,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     const int ntiles = cam.gx * cam.gy;
     uint32_t* order = (uint32_t*)(ib + IL.order);
     cam.tile_order = order;   // render schedule (tile_plan in the bucketed duplicate, else row-major)
+    cam.rowmax = (uint32_t*)(ib + IL.rowmax);
     cam.sched_cus = device_cus(dev);
     uint32_t* cursor = tile_count + (size_t)ntiles * TILE_CTR_STRIDE;
     hipError_t e;
@@ -446,7 +449,13 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
                 return hip_fail(e, "duplicate");
         }
         if (capacity <= 0 && scan_in_duplicate && (rc = snapshot_counters()) != GSR_OK) return rc;
-        {
+        if (track_inst) {  // forward + L1 + the tracking render backward, one launch (render_track_kernel)
+            StageTimer t(GSR_STAGE_RENDER_FWD, 0, stream, true);
+            if ((e = launch_render_track(cam, ranges, point_list, keys[0], geo, final_T, n_contrib, out_color,
+                                         out_color2, out_depth, guard, *l1, track_inst, stream, t.kclock())) !=
+                hipSuccess)
+                return hip_fail(e, "render (fused tracking forward + backward)");
+        } else {
             StageTimer t(GSR_STAGE_RENDER_FWD, 0, stream, true);
             if ((e = launch_render_fwd(cam, ranges, point_list, keys[0], geo, colors2, final_T, n_contrib,
                                        out_color, out_color2, out_depth, guard, stream, t.kclock(), l1)) !=
@@ -520,7 +529,8 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
                          int num_rendered, const void* geom_buffer, const void* binning_buffer,
                          const void* image_buffer, int power, const gsr_grads* grads, float* dcolors2,
                          int dl2_channels, gsr_alloc_fn alloc, void* alloc_ctx, void* stream_,
-                         const PoseFuse* pose = nullptr, const ShAdam* sh_adam = nullptr) {
+                         const PoseFuse* pose = nullptr, const ShAdam* sh_adam = nullptr,
+                         const float* pre_inst = nullptr) {
     int rc = validate(settings, gaussians, false);
     if (dl2_channels != 1 && dl2_channels != 3) return fail(GSR_ERR_INVALID_ARG, "dl2_channels must be 1 or 3");
     if (rc != GSR_OK) return rc;
@@ -539,6 +549,7 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
         return fail(GSR_ERR_INVALID_ARG, "missing forward state");
     // the forward's render schedule (a permutation of the tiles; any order gives the same results)
     cam.tile_order = (const uint32_t*)((const char*)image_buffer + ImgLayout::make(cam.W, cam.H).order);
+    cam.rowmax = (uint32_t*)((char*)const_cast<void*>(image_buffer) + ImgLayout::make(cam.W, cam.H).rowmax);
     cam.sched_cus = device_cus(current_device());  // (wave priority levels: one or several dispatch rounds)
     const GeomLayout GL = GeomLayout::make(P);
     cam.pre_shift = GL.shift;
@@ -658,7 +669,8 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     // staged SH backward: gauss_bwd leaves dL/dcolor in a scratch array, sh_bwd turns it into dsh and the
     // view-direction term of dL/dmeans3D (gsr_sh.hip)
     const bool shs_staged = sh_staged(cam, g);
-    const size_t rec_bytes = align_up(sizeof(float) * rec.stride * (size_t)num_rendered, 256);
+    // pre_inst: the records were formed by the fused tracking render (render_track_kernel)
+    const size_t rec_bytes = pre_inst ? 0 : align_up(sizeof(float) * rec.stride * (size_t)num_rendered, 256);
     const size_t scratch_bytes = (num_rendered > 0 ? rec_bytes : 0) + (shs_staged ? sizeof(float) * 3 * (size_t)P : 0);
     char* scratch = nullptr;
     if (scratch_bytes > 0) {
@@ -667,7 +679,11 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
         if (!scratch) return fail(GSR_ERR_ALLOC, "allocator returned NULL (backward scratch)");
     }
     float* drgb = shs_staged ? (float*)(scratch + (num_rendered > 0 ? rec_bytes : 0)) : nullptr;
-    if (num_rendered > 0) {
+    if (pre_inst) {
+        if (!pose || rec.stride != track_records_stride())
+            return fail(GSR_ERR_INVALID_ARG, "precomputed records are the pose-fused tracking backward's only");
+        inst = const_cast<float*>(pre_inst);
+    } else if (num_rendered > 0) {
         if (!binning_buffer) return fail(GSR_ERR_INVALID_ARG, "missing binning buffer");
         inst = (float*)scratch;
         const char* bb = (const char*)binning_buffer;
@@ -732,12 +748,48 @@ int gsr_track_forward_dual_static(const gsr_settings* settings, const gsr_gaussi
                         stream, capacity, status, &l1);
 }
 
+static int track_forward_xf(const gsr_settings* settings, const gsr_gaussians* gaussians, float* colors2,
+                            const gsr_track_xform* xform, int capacity, unsigned* status, float* out_color,
+                            float* out_color2, float* out_depth, int* radii, const float* gt_im, const float* gt_depth,
+                            float sil_thres, float w_im, float w_depth, const float* dL_dloss, float* loss,
+                            float* dL_dim, float* dL_ddepth_sil, float* scratch, gsr_alloc_fn alloc, void* alloc_ctx,
+                            void* stream, float* inst_records);
+
 int gsr_track_forward_dual_static_xf(const gsr_settings* settings, const gsr_gaussians* gaussians, float* colors2,
                                      const gsr_track_xform* xform, int capacity, unsigned* status, float* out_color,
                                      float* out_color2, float* out_depth, int* radii, const float* gt_im,
                                      const float* gt_depth, float sil_thres, float w_im, float w_depth,
                                      const float* dL_dloss, float* loss, float* dL_dim, float* dL_ddepth_sil,
                                      float* scratch, gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
+    return track_forward_xf(settings, gaussians, colors2, xform, capacity, status, out_color, out_color2, out_depth,
+                            radii, gt_im, gt_depth, sil_thres, w_im, w_depth, dL_dloss, loss, dL_dim, dL_ddepth_sil,
+                            scratch, alloc, alloc_ctx, stream, nullptr);
+}
+
+int gsr_track_records_floats(int capacity) { return track_records_stride() * (capacity > 1 ? capacity : 1); }
+
+int gsr_track_forward_backward_dual_static_xf(const gsr_settings* settings, const gsr_gaussians* gaussians,
+                                              float* colors2, const gsr_track_xform* xform, int capacity,
+                                              unsigned* status, float* out_color, float* out_color2,
+                                              float* out_depth, int* radii, const float* gt_im,
+                                              const float* gt_depth, float sil_thres, float w_im, float w_depth,
+                                              const float* dL_dloss, float* loss, float* scratch,
+                                              float* inst_records, gsr_alloc_fn alloc, void* alloc_ctx,
+                                              void* stream) {
+    if (!inst_records) return fail(GSR_ERR_INVALID_ARG, "track_forward_backward_dual_static_xf: null records");
+    // the gradient images are not formed (the backward runs from the registers); the L1 epilogue's
+    // pointers to them are never dereferenced
+    return track_forward_xf(settings, gaussians, colors2, xform, capacity, status, out_color, out_color2, out_depth,
+                            radii, gt_im, gt_depth, sil_thres, w_im, w_depth, dL_dloss, loss, loss, loss, scratch,
+                            alloc, alloc_ctx, stream, inst_records);
+}
+
+static int track_forward_xf(const gsr_settings* settings, const gsr_gaussians* gaussians, float* colors2,
+                            const gsr_track_xform* xform, int capacity, unsigned* status, float* out_color,
+                            float* out_color2, float* out_depth, int* radii, const float* gt_im, const float* gt_depth,
+                            float sil_thres, float w_im, float w_depth, const float* dL_dloss, float* loss,
+                            float* dL_dim, float* dL_ddepth_sil, float* scratch, gsr_alloc_fn alloc, void* alloc_ctx,
+                            void* stream, float* inst_records) {
     if (!xform || !gaussians) return fail(GSR_ERR_INVALID_ARG, "track_forward_dual_static_xf: null pointer");
     const gsr_track_xform& x = *xform;
     if ((x.scale_cols != 1 && x.scale_cols != 3) || x.q_stride < 1)
@@ -758,10 +810,19 @@ int gsr_track_forward_dual_static_xf(const gsr_settings* settings, const gsr_gau
     xf.store = x.store_rendervars != 0;
     const TrackL1 l1{gt_im, gt_depth, sil_thres, w_im, w_depth, dL_dloss, dL_dim, dL_ddepth_sil, scratch, loss};
     return forward_impl(settings, gaussians, colors2, out_color, out_color2, out_depth, radii, alloc, alloc_ctx,
-                        stream, capacity, status, &l1, &xf);
+                        stream, capacity, status, &l1, &xf, inst_records);
 }
 
 int gsr_track_backward_scratch_floats(int P) { return pose_fuse_scratch_floats(P < 1 ? 1 : P); }
+
+static int track_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
+                          const float* colors2, const float* dL_dout_color, const float* dL_dout_color2,
+                          int num_rendered, const void* geom_buffer, const void* binning_buffer,
+                          const void* image_buffer, const float* means_world, const float* unnorm_rot,
+                          int scale_cols, float* cam_q, float* cam_t, int q_stride, const float* w2c, double lr_q,
+                          double lr_t, double beta1, double beta2, double eps, float* adam_state, float* dL_dcam_q,
+                          float* dL_dcam_t, float* scratch, const gsr_pose_track* track, const float* log_scales,
+                          gsr_alloc_fn alloc, void* alloc_ctx, void* stream, const float* inst_records);
 
 int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
                             const float* colors2, const float* dL_dout_color, const float* dL_dout_color2,
@@ -771,6 +832,36 @@ int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* g
                             double lr_t, double beta1, double beta2, double eps, float* adam_state,
                             float* dL_dcam_q, float* dL_dcam_t, float* scratch, const gsr_pose_track* track,
                             const float* log_scales, gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
+    return track_backward(settings, gaussians, radii, colors2, dL_dout_color, dL_dout_color2, num_rendered,
+                          geom_buffer, binning_buffer, image_buffer, means_world, unnorm_rot, scale_cols, cam_q, cam_t,
+                          q_stride, w2c, lr_q, lr_t, beta1, beta2, eps, adam_state, dL_dcam_q, dL_dcam_t, scratch,
+                          track, log_scales, alloc, alloc_ctx, stream, nullptr);
+}
+
+int gsr_track_backward_dual_records(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
+                                    const float* colors2, int num_rendered, const void* geom_buffer,
+                                    const void* binning_buffer, const void* image_buffer, const float* means_world,
+                                    const float* unnorm_rot, int scale_cols, float* cam_q, float* cam_t, int q_stride,
+                                    const float* w2c, double lr_q, double lr_t, double beta1, double beta2,
+                                    double eps, float* adam_state, float* dL_dcam_q, float* dL_dcam_t,
+                                    float* scratch, const gsr_pose_track* track, const float* log_scales,
+                                    const float* inst_records, gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
+    if (!inst_records) return fail(GSR_ERR_INVALID_ARG, "track_backward_dual_records: null records");
+    // (the gradient images are not read: the records already hold the render backward's sums)
+    return track_backward(settings, gaussians, radii, colors2, scratch, scratch, num_rendered, geom_buffer,
+                          binning_buffer, image_buffer, means_world, unnorm_rot, scale_cols, cam_q, cam_t, q_stride,
+                          w2c, lr_q, lr_t, beta1, beta2, eps, adam_state, dL_dcam_q, dL_dcam_t, scratch, track,
+                          log_scales, alloc, alloc_ctx, stream, inst_records);
+}
+
+static int track_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,
+                          const float* colors2, const float* dL_dout_color, const float* dL_dout_color2,
+                          int num_rendered, const void* geom_buffer, const void* binning_buffer,
+                          const void* image_buffer, const float* means_world, const float* unnorm_rot,
+                          int scale_cols, float* cam_q, float* cam_t, int q_stride, const float* w2c, double lr_q,
+                          double lr_t, double beta1, double beta2, double eps, float* adam_state, float* dL_dcam_q,
+                          float* dL_dcam_t, float* scratch, const gsr_pose_track* track, const float* log_scales,
+                          gsr_alloc_fn alloc, void* alloc_ctx, void* stream, const float* inst_records) {
     if (!gaussians || (scale_cols != 1 && scale_cols != 3) || q_stride < 1)
         return fail(GSR_ERR_INVALID_ARG, "track_backward_dual: bad sizes");
     if (!colors2 || !means_world || !unnorm_rot || !cam_q || !cam_t || !w2c || !scratch ||
@@ -789,7 +880,7 @@ int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* g
     gsr_grads none{};
     return backward_impl(settings, gaussians, radii, dL_dout_color, colors2, dL_dout_color2, num_rendered,
                          geom_buffer, binning_buffer, image_buffer, 1, &none, nullptr, 1, alloc, alloc_ctx, stream,
-                         &pf);
+                         &pf, nullptr, inst_records);
 }
 
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
@@ -883,6 +974,7 @@ int gsr_forward_reuse(const gsr_settings* settings, const gsr_gaussians* gaussia
     const GeomPtrs geo = GeomPtrs::at(geom, GL);
     char* ib = (char*)image_buffer;
     cam.tile_order = (const uint32_t*)(ib + IL.order);
+    cam.rowmax = (uint32_t*)(ib + IL.rowmax);
     cam.sched_cus = device_cus(dev);
     hipError_t e;
     {

@@ -83,6 +83,7 @@ struct ImgLayout {        // per-pixel / per-tile state ("imgBuffer")
     size_t ranges;        // uint2 [tiles]  [start, end) of each tile's sorted list
     size_t order;         // u32   [tiles]  render schedule: workgroup i renders tile order[i] (tile_plan)
     size_t tile_count;    // u32   [2*tiles*TILE_CTR_STRIDE] instance counters, then bucket cursors (one memset)
+    size_t rowmax;        // u32   [tiles*16] per 4x4 block (tile_px/tile_py order): the longest n_contrib
     size_t total;
     static ImgLayout make(int W, int H) {
         ImgLayout L;
@@ -94,6 +95,7 @@ struct ImgLayout {        // per-pixel / per-tile state ("imgBuffer")
         L.ranges = o; o = align_up(o + 8 * (T ? T : 1), 256);
         L.order = o; o = align_up(o + 4 * (T ? T : 1), 256);
         L.tile_count = o; o = align_up(o + 8 * (size_t)TILE_CTR_STRIDE * (T ? T : 1), 256);
+        L.rowmax = o; o = align_up(o + 64 * (T ? T : 1), 256);
         L.total = o;
         return L;
     }
@@ -155,6 +157,9 @@ struct Camera {
     // count, the round size of the plan.
     const uint32_t* tile_order = nullptr;
     uint32_t* tile_order_out = nullptr;
+    // Per-block last-contributor maxima (ImgLayout::rowmax): written by render_fwd, read by render_bwd
+    // (its batch range and row-list bounds without a reduction over n_contrib first); nullptr = not kept
+    uint32_t* rowmax = nullptr;
     int sched_cus = 256;
     int pre_shift = 10;  // log2 Gaussians per count-matrix row (GeomLayout::shift)
 };
@@ -1197,6 +1202,13 @@ hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* p
                              float* out_color2, float* out_depth, SpecGuard guard, hipStream_t s,
                              unsigned long long* clk = nullptr, const TrackL1* l1 = nullptr);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* vis, hipStream_t s);
+// the tracking iteration's forward (+ L1) and render backward in one launch (gsr_backward.hip); inst receives
+// the pose-fused gauss_bwd's per-instance records (track_records_floats)
+hipError_t launch_render_track(const Camera& cam, const uint2* ranges, uint64_t* point_list, uint64_t* keys,
+                               GeomPtrs geo, float* final_T, uint32_t* n_contrib, float* out_color,
+                               float* out_color2, float* out_depth, SpecGuard guard, const TrackL1& l1, float* inst,
+                               hipStream_t s, unsigned long long* clk = nullptr);
+int track_records_stride();  // floats per instance record of the tracking render backward (6)
 // geometry reuse (gsr_forward_reuse): the render records' colours replaced by `colors` [P,3]
 hipError_t launch_recolour(int P, const float* colors, GeomPtrs geo, hipStream_t s);
 struct EqualPairs {

@@ -25,6 +25,10 @@ from ._lib import lib
 # tracking transform fused into the rasterizer's preprocess in the static tracking iteration
 # (gsr_track_forward_dual_static_xf); GSR_XF_FUSED=0 runs it as its own launch (A/B, parity tests)
 _XF_FUSED = os.environ.get("GSR_XF_FUSED", "1") != "0"
+# ... and with it the tracking render backward inside the forward's launch (render_track_kernel,
+# gsr_track_forward_backward_dual_static_xf); GSR_TRACK_RENDER_FUSED=0 keeps render_bwd a launch of its own
+_RENDER_FUSED = (os.environ.get("GSR_TRACK_RENDER_FUSED", "1") != "0" and
+                 hasattr(lib, "gsr_track_forward_backward_dual_static_xf"))
 # ... without storing the camera-frame rendervars (the backward recomputes them from the world-frame
 # map: gsr_track_backward_dual log_scales); True stores them (tests compare them with the separate transform)
 _XF_STORE = False
@@ -494,10 +498,14 @@ class _TrackIteration(torch.autograd.Function):
             scratch = _scratch(mw, lib.gsr_track_forward_scratch_floats(W, H))
             xform = (mw, ur, lo, ls, scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c,
                      _XF_STORE)
+            records = None
+            if _RENDER_FUSED:  # (a static seed promises the backward): the render backward in the forward's launch
+                records = torch.empty(lib.gsr_track_records_floats(capacity), **f32)
             (n, im, ds, radii, geom, binning, img, _, loss, dim, dds) = _C.track_forward_dual_static(
                 cam, means, rgb, dcol, opac, scales, rot, capacity, status, gt_im, gt_d, cfg.sil_thres, cfg.w_im,
-                cfg.w_depth, seed, scratch, xform=xform)
+                cfg.w_depth, seed, scratch, xform=xform, records=records)
             ctx.pre = (dim, dds, seed)
+            ctx.records = records
             ctx.save_for_backward(cam_rots, cam_trans, mw, ur, means, rot, dcol, scales, rgb, radii, geom, binning,
                                   img, im, ds, gt_im, gt_d, w2c)
             ctx.meta = (t, T, scols, int(n), cam, cfg)
@@ -565,9 +573,13 @@ class _TrackIteration(torch.autograd.Function):
          w2c) = ctx.saved_tensors
         t, T, scols, n, cam, cfg = ctx.meta
         nones = (None,) * 11
+        records = getattr(ctx, "records", None)
         if ctx.pre is not None and g is not None and g.data_ptr() == ctx.pre[2].data_ptr():
             dim, dds = ctx.pre[0], ctx.pre[1]
+            if records is not None:  # the render backward ran in the forward: its sums are in records
+                dim, dds = im, ds    # (placeholders of the right shape: not read)
         else:
+            records = None  # another loss seed: the render backward runs from the recomputed gradient images
             if g is None:
                 return nones
             H, W = cam.image_height, cam.image_width
@@ -586,12 +598,13 @@ class _TrackIteration(torch.autograd.Function):
                                    ur, scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c,
                                    scratch, adam=(opt.lr_q, opt.lr_t, float(opt.betas[0]), float(opt.betas[1]),
                                                   opt.eps, opt.state), track=opt.track(ctx.loss_ptr),
-                                   log_scales=ctx.log_scales)
+                                   log_scales=ctx.log_scales, records=records)
             return nones
         dq, dt = torch.zeros_like(cam_rots), torch.zeros_like(cam_trans)
         _C.track_backward_dual(cam, means, radii, rgb, dcol, scales, rot_in, dim, dds, geom, n, binning, img, mw, ur,
                                scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c, scratch,
-                               dq_ptr=dq.data_ptr() + 4 * t, dt_ptr=dt.data_ptr() + 4 * t, log_scales=ctx.log_scales)
+                               dq_ptr=dq.data_ptr() + 4 * t, dt_ptr=dt.data_ptr() + 4 * t, log_scales=ctx.log_scales,
+                               records=records)
         return (dq, dt) + (None,) * 9
 
 

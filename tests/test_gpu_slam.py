@@ -263,3 +263,32 @@ def test_transform_fused_preprocess_bitwise(cuda, aniso, store, monkeypatch):
             assert torch.equal(a, b)
     assert torch.equal(q0, q1) and torch.equal(t0, t1)
     assert float(q1[..., 1].abs().sum()) > 0.0
+
+
+@pytest.mark.parametrize("aniso", [False, True])
+def test_track_render_fused_bitwise(cuda, aniso, monkeypatch):
+    """gsr_track_forward_backward_dual_static_xf (render_track_kernel: a tile's forward + L1 loss and its
+    render backward in one workgroup) + gsr_track_backward_dual_records against the separate render_fwd /
+    render_bwd launches: loss, radii, images and the pose gradients bitwise equal."""
+    from splatam_amd import glue
+    from splatam_amd.slam import TrackingConfig
+    params, curr = _setup(cuda, aniso)
+    seed = torch.ones((), device=cuda)
+    outs = []
+    for fused in (False, True):
+        monkeypatch.setattr(glue, "_RENDER_FUSED", fused)
+        p = _pose_leaves(params)
+        status = torch.zeros(4, dtype=torch.int32, device=cuda)
+        loss, radii = glue.tracking_iteration(p, curr, 1, TrackingConfig(), capacity=400000, status=status, seed=seed)
+        saved = loss.grad_fn.saved_tensors  # (.., im, ds at 13, 14)
+        ims = [saved[13].clone(), saved[14].clone()]
+        assert (getattr(loss.grad_fn, "records", None) is not None) == fused
+        torch.autograd.backward(loss, seed)
+        outs.append((loss.detach().clone(), radii.clone(), ims, p["cam_unnorm_rots"].grad.clone(),
+                     p["cam_trans"].grad.clone()))
+        assert int(status[1]) == 0 and 0 < int(status[0]) <= 400000
+    (l0, r0, i0, q0, t0), (l1, r1, i1, q1, t1) = outs
+    assert torch.equal(l0, l1) and torch.equal(r0, r1)
+    assert torch.equal(i0[0], i1[0]) and torch.equal(i0[1], i1[1])
+    assert torch.equal(q0, q1) and torch.equal(t0, t1)
+    assert float(q1[..., 1].abs().sum()) > 0.0

@@ -20,10 +20,12 @@
 #                    each splatam_amd/_diag/libgsr_<tag>.so (build_variant on the CPU first);
 #                    MODES = mode:config[,mode:config...], TAGS = tag[,tag...]   e.g. ab=dual_lean:3,dual:4=ablw
 #   abbench=TAGS     interleaved A/B of the bench line (tracking + mapping values, render stage times)
+#   abflag=FLAG:V1,V2[,...]  interleaved A/B (two rounds) of the light bench line over the values of one bench.py
+#                    flag, e.g. abflag=--fuse-render:1,0
 TAG=${1:-x}; shift
 ROOT=$(pwd); OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
-LIGHT="--cpu-baseline off --dropin off --fisher off --mapping off --configs off"
+LIGHT="--cpu-baseline off --dropin off --fisher off --mapping off --configs off --unfused-leg off"
 lib_of() { [ "$1" = base ] && echo "$ROOT/splatam_amd/libgsr.so" || echo "$ROOT/splatam_amd/_diag/libgsr_$1.so"; }
 for s in "$@"; do
   case $s in
@@ -84,12 +86,25 @@ for s in "$@"; do
             for t in base ${TAGS//,/ }; do
               f="$OUT/abbench_${t}_$r.log"
               GSR_LIB=$(lib_of $t) timeout -k 10 300 python bench.py --cpu-baseline off --dropin off --fisher off \
-                  --configs off > "$f" 2>&1 || { echo "abbench $t failed"; tail -20 "$f"; exit 1; }
+                  --configs off --unfused-leg off > "$f" 2>&1 || { echo "abbench $t failed"; tail -20 "$f"; exit 1; }
               python - "$f" $t $r <<'PY' | tee -a "$OUT/abbench.txt"
 import json, sys
 b = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][-1]
 print("abbench", sys.argv[2], "round", sys.argv[3], "frames/s", b["value"], "render_bwd", b["roofline"]["avg_us"],
       "render_fwd", b["stages_us"]["render_fwd"], "mapping it/s", (b.get("mapping") or {}).get("value"))
+PY
+            done
+          done ;;
+    abflag=*) spec=${s#abflag=}; FL=${spec%%:*}; VALS=${spec#*:}
+          for r in 1 2; do
+            for v in ${VALS//,/ }; do
+              f="$OUT/abflag_${FL//-/}_${v}_$r.log"
+              timeout -k 10 300 python bench.py $LIGHT $FL $v > "$f" 2>&1 || { echo "abflag $FL $v failed"; tail -20 "$f"; exit 1; }
+              python - "$f" "$FL $v" $r <<'PY' | tee -a "$OUT/abflag.txt"
+import json, sys
+b = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][-1]
+print("abflag", sys.argv[2], "round", sys.argv[3], "frames/s", b["value"], "kernel", b["roofline"]["kernel"],
+      "avg_us", b["roofline"]["avg_us"], "render_fwd", b["stages_us"]["render_fwd"], "render_bwd", b["stages_us"]["render_bwd"])
 PY
             done
           done ;;

@@ -33,11 +33,13 @@ def read_pmc(src, prefix):
     return pmc
 
 
-def calibrated(fetch_kb, write_kb, inst, width, height):
+def calibrated(fetch_kb, write_kb, inst, width, height, fused=False):
     """profiles/traffic_calibration.json: 64-B record gathers are counted 1:1 by FETCH_SIZE, coalesced streams
-    at half: calibrated bytes = FETCH + streamed/2 + WRITE, the streamed reads being the sorted list entries
-    (8 B / instance) and the per-pixel inputs (final_T, n_contrib, 3 + 1 gradient channels: 24 B / pixel)."""
-    streamed = 8.0 * inst + 24.0 * width * height
+    at half: calibrated bytes = FETCH + streamed/2 + WRITE, the streamed reads being, for render_bwd, the sorted
+    list entries (8 B / instance) and the per-pixel inputs (final_T, n_contrib, 3 + 1 gradient channels:
+    24 B / pixel); for the fused tracking render (render_track_kernel) the bucket keys and the list entries
+    read by the forward and by the backward (24 B / instance) and the loss targets (16 B / pixel)."""
+    streamed = (24.0 * inst + 16.0 * width * height) if fused else (8.0 * inst + 24.0 * width * height)
     return int((fetch_kb + write_kb) * 1024 + streamed / 2), int(streamed)
 
 
@@ -88,14 +90,14 @@ def main(src, tag):
         summary[k] = {"FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write,
                       "hbm_bytes_per_launch": int((2.0 * fetch + write) * 1024),
                       "avg_duration_ns_trace": float(rows[k]["AverageNs"]) if k in rows else None}
-        if k == "render_bwd_kernel" and bench is not None and bench.get("roofline"):
+        if k == (bench or {}).get("roofline", {}).get("kernel") and bench is not None:
             # profiles/traffic_calibration.json: 64-B record gathers are counted 1:1 by FETCH_SIZE,
             # coalesced streams at half: calibrated bytes = FETCH + streamed/2 + WRITE, the streamed
             # reads being the sorted list entries (8 B / instance) and the per-pixel inputs
             # (final_T, n_contrib, 3 + 1 gradient channels: 24 B / pixel)
             cfg = bench["config"]
             cal, streamed = calibrated(fetch, write, float(bench["roofline"]["num_rendered_avg"]), cfg["width"],
-                                       cfg["height"])
+                                       cfg["height"], fused=k == "render_track_kernel")
             summary[k]["streamed_read_bytes_alg"] = streamed
             summary[k]["hbm_bytes_calibrated"] = cal
 
@@ -105,15 +107,17 @@ def main(src, tag):
                    "correction applied to everything: an upper bound); hbm_bytes_calibrated (render_bwd) = "
                    "FETCH_SIZE + streamed/2 + WRITE_SIZE per profiles/traffic_calibration.json."}
     json.dump(out, open(f"{dst}/{tag}_summary.json", "w"), indent=1)
-    rb = summary.get("render_bwd_kernel")
+    kname = (bench or {}).get("roofline", {}).get("kernel", "render_bwd_kernel")
+    rb = summary.get(kname)
     headline = bench is not None and str(bench.get("metric", "")).startswith("rasterize fwd+bwd")
     if rb and headline:  # bench.py's roofline.traffic of the headline (tracking) workload
-        json.dump({"kernel": "render_bwd_kernel", "hbm_bytes_per_launch": rb.get("hbm_bytes_calibrated",
-                                                                                 rb["hbm_bytes_per_launch"]),
+        fname = "render_track_pmc.json" if kname == "render_track_kernel" else "render_bwd_pmc.json"
+        json.dump({"kernel": kname, "hbm_bytes_per_launch": rb.get("hbm_bytes_calibrated",
+                                                                   rb["hbm_bytes_per_launch"]),
                    "uncalibrated_2fetch_plus_write": rb["hbm_bytes_per_launch"],
                    "calibration": "profiles/traffic_calibration.json",
                    "kernel_avg_us": bench["roofline"].get("avg_us"), "commit": head_commit(),
-                   "source": f"profiles/{tag}_summary.json"}, open(f"{dst}/render_bwd_pmc.json", "w"), indent=1)
+                   "source": f"profiles/{tag}_summary.json"}, open(f"{dst}/{fname}", "w"), indent=1)
     shutil.copy(blog, f"{dst}/{tag}_bench.log")
     print(json.dumps(out["kernels"], indent=1))
 
