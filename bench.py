@@ -772,7 +772,8 @@ def unfused_render_leg(params, curr, frame, S, P, W, H, Tt, N, replays: int = 4)
         with torch.no_grad():
             q0 = params["cam_unnorm_rots"][..., frame].clone()
             t0 = params["cam_trans"][..., frame].clone()
-        tr = GraphTracker(params, curr, frame, iters_per_graph=S, fuse_pose=True, warmup_iters=1, prime=True)
+        tr = GraphTracker(params, curr, frame, iters_per_graph=S, fuse_pose=True, warmup_iters=1, prime=True,
+                          timing=True)
         profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
         torch.cuda.synchronize()
         ta = time.perf_counter()
