@@ -217,7 +217,7 @@ __device__ __forceinline__ void mom_matrix(const float* S, float (&Sm)[9][9], st
 // (6 + 6 instead of 5 + 7 sums for mapping: 84 instead of 96 DPP adds per step, render_bwd 312 -> 303 us at config 4)
 #endif
 #ifndef GSR_NT_STORES
-#define GSR_NT_STORES 0  // every render record / image store non-temporal (the wide records always are)
+#define GSR_NT_STORES 0  // render kernels' record / image stores as non-temporal (streaming) stores
 #endif
 #ifndef GSR_PACK_C
 #define GSR_PACK_C 1  // DUAL, Q2 = 1: the second colour set's one channel staged in s_c.w (no s_d array)
@@ -589,9 +589,9 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
 #pragma unroll
             for (int i = 0; i < NQ; i++)
                 if (q + TPE * i < RS) {
-                    // the wide records (mapping, single-image full gradient) as streaming stores: mapping
-                    // 899-900 -> 929 it/s; the 24-B tracking records measured neutral (profiles/r4l_ab_nt.txt)
-                    if (GSR_NT_STORES || NV > 6) __builtin_nontemporal_store(c[i], &dst[q + TPE * i]);
+                    // (streaming stores measured neutral for render_bwd and 3-9 us slower for the gauss_bwd that
+                    // reads the records next: profiles/r4l_ab_nt.txt, r4m_ab_nt.txt)
+                    if (GSR_NT_STORES) __builtin_nontemporal_store(c[i], &dst[q + TPE * i]);
                     else dst[q + TPE * i] = c[i];
                 }
         }
