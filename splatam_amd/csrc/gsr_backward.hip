@@ -676,13 +676,15 @@ render_track_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __
     const int tile = sched_tile(cam);
     const FwdPix f = fwd_tile<true>(cam, tile, ranges, point_list, keys, rr, guard, smem, dg);
     float grad[4];
-    fwd_epilogue<true, true, false>(cam, tile, f, final_T, n_contrib, out_color, out_color2, out_depth, l1, grad);
+    fwd_epilogue<true, true, false, false>(cam, tile, f, final_T, n_contrib, out_color, out_color2, out_depth, l1,
+                                           grad);
     __syncthreads();  // the forward's LDS (and its sorted point_list stores) before the backward reuses them
     const BwdPix pin{f.T, f.last16 >> 4, grad[0], grad[1], grad[2], grad[3], 0.f, 0.f};
     Camera cb = cam;
     cb.rowmax = nullptr;  // the block maxima from the registers
     bwd_tile<true, false, false, true, 1, 0>(cb, tile, pin, ranges, point_list, rr, blocksums, inst,
                                              BwdGuard{guard.counters, guard.cap_inst}, smem, dg);
+    l1_finish(l1);  // the loss: arrival and the last workgroup's sum after the backward, not between the phases
     dg.end();
     kclock_end(clk);
 }
@@ -774,11 +776,20 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     gg.m = make_float3(0.f, 0.f, 0.f);
     gg.s = make_float3(0.f, 0.f, 0.f);
     gg.q = make_float4(0.f, 0.f, 0.f, 0.f);
+    // POSE: the frame's (pre-step) pose is workgroup-uniform: formed once by thread 0 (8 IEEE divisions and 2
+    // square roots per lane otherwise) and read from LDS -- the same bits
+    __shared__ Pose s_pose;
+    if constexpr (POSE) {
+        if (pf.ls || pf.scols != 1) {
+            if (threadIdx.x == 0) s_pose = make_pose(pf.cam_q, pf.cam_t, pf.qs);
+            __syncthreads();
+        }
+    }
     if (live && (POSE || radii[i] > 0)) {  // (the pose sums need every live Gaussian's mean)
         if (POSE && pf.ls) {
             TrackXf x;
             x.mw = pf.means_world; x.ur = pf.unnorm_rot; x.ls = pf.ls; x.scols = pf.scols;
-            const Pose ps = make_pose(pf.cam_q, pf.cam_t, pf.qs);
+            const Pose ps = s_pose;
             float m[3], sv[3];
             track_xform_geom(x, ps, i, m, gg.q, sv);
             gg.m = make_float3(m[0], m[1], m[2]);
@@ -853,7 +864,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         for (int k = 0; k < POSE_PARTS; k++) v[k] = 0.f;
         float c[4] = {0.f, 0.f, 0.f, 0.f};
         if (pf.scols != 1) {
-            const Pose ps = make_pose(pf.cam_q, nullptr, pf.qs);
+            const Pose ps = s_pose;  // (c only: the same normalised quaternion)
 #pragma unroll
             for (int k = 0; k < 4; k++) c[k] = ps.c[k];
         }

@@ -386,7 +386,34 @@ __device__ __forceinline__ FwdPix fwd_tile(const Camera& cam, int tile, const ui
 // tracking loss -- its per-pixel gradients (dL/dim_0..2, dL/ddepth) returned in grad and stored into
 // l1.dL_dim / l1.dL_dds when STORE_GRADS, the workgroup's loss partials published and summed by the
 // last workgroup.
-template <bool DUAL, bool L1, bool STORE_GRADS>
+// The tracking loss from the workgroups' published partials: the last workgroup to arrive adds them in
+// tile order and writes l1.loss (every thread of every workgroup calls it, after its partial store)
+__device__ __forceinline__ void l1_finish(const TrackL1& l1) {
+    __shared__ float s_fin[16];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, row4 = lane >> 4;
+    const int nb = gridDim.x * gridDim.y;
+    if (last_block_arrive_grouped(reinterpret_cast<uint32_t*>(l1.part + 2 * nb))) {
+        float v[4] = {0.f, 0.f, 0.f, 0.f}, r[1];
+        {
+            float v2[2] = {0.f, 0.f};
+            gather_partials<2, GSR_L1_CH>(l1.part, 2, nb, tid, TILE_PIX, v2);
+            v[0] = v2[0];
+            v[1] = v2[1];
+        }
+        wave_reduce_n<4>(v, r);
+        if ((lane & 15) == 0) s_fin[w * 4 + row4] = r[0];
+        __syncthreads();
+        if (tid == 0) {
+            const float s0 = (s_fin[0] + s_fin[4]) + (s_fin[8] + s_fin[12]);
+            const float s1 = (s_fin[1] + s_fin[5]) + (s_fin[9] + s_fin[13]);
+            l1.loss[0] = l1.w_im * s0 + l1.w_depth * s1;
+        }
+    }
+}
+
+// L1_FINISH: the arrival / last-workgroup sum right here (render_fwd_kernel); false: the caller calls
+// l1_finish later (render_track_kernel, after the tile's backward: no atomic round trip between its phases)
+template <bool DUAL, bool L1, bool STORE_GRADS, bool L1_FINISH = true>
 __device__ __forceinline__ void fwd_epilogue(const Camera& cam, int tile, const FwdPix& f, float* __restrict__ final_T,
                                              uint32_t* __restrict__ n_contrib, float* __restrict__ out_color,
                                              float* __restrict__ out_color2, float* __restrict__ out_depth,
@@ -485,25 +512,8 @@ __device__ __forceinline__ void fwd_epilogue(const Camera& cam, int tile, const 
         __syncthreads();
         if (tid < 4) s_tot[tid] = (s_red[tid] + s_red[4 + tid]) + (s_red[8 + tid] + s_red[12 + tid]);
         __syncthreads();
-        const int nb = gridDim.x * gridDim.y;
         if (tid < 2) st_agent(l1.part + 2 * tile + tid, s_tot[tid]);
-        if (last_block_arrive_grouped(reinterpret_cast<uint32_t*>(l1.part + 2 * nb))) {
-            v[0] = v[1] = v[2] = v[3] = 0.f;
-            {
-                float v2[2] = {0.f, 0.f};
-                gather_partials<2, GSR_L1_CH>(l1.part, 2, nb, tid, TILE_PIX, v2);
-                v[0] = v2[0];
-                v[1] = v2[1];
-            }
-            wave_reduce_n<4>(v, r);
-            if ((lane & 15) == 0) s_red[w * 4 + row4] = r[0];
-            __syncthreads();
-            if (tid == 0) {
-                const float s0 = (s_red[0] + s_red[4]) + (s_red[8] + s_red[12]);
-                const float s1 = (s_red[1] + s_red[5]) + (s_red[9] + s_red[13]);
-                l1.loss[0] = l1.w_im * s0 + l1.w_depth * s1;
-            }
-        }
+        if (L1_FINISH) l1_finish(l1);
     }
 }
 

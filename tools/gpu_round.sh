@@ -83,7 +83,9 @@ for s in "$@"; do
           done ;;
     abbench=*) TAGS=${s#abbench=}
           for r in 1 2; do
-            for t in base ${TAGS//,/ }; do
+            ORDER="base ${TAGS//,/ }"
+            [ $r = 2 ] && ORDER=$(echo $ORDER | tr ' ' '\n' | tac | tr '\n' ' ')  # round 2 in reverse order
+            for t in $ORDER; do
               f="$OUT/abbench_${t}_$r.log"
               GSR_LIB=$(lib_of $t) timeout -k 10 300 python bench.py --cpu-baseline off --dropin off --fisher off \
                   --configs off --unfused-leg off > "$f" 2>&1 || { echo "abbench $t failed"; tail -20 "$f"; exit 1; }
