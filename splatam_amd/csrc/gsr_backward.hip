@@ -676,15 +676,15 @@ render_track_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __
     const int tile = sched_tile(cam);
     const FwdPix f = fwd_tile<true>(cam, tile, ranges, point_list, keys, rr, guard, smem, dg);
     float grad[4];
-    fwd_epilogue<true, true, false, false>(cam, tile, f, final_T, n_contrib, out_color, out_color2, out_depth, l1,
-                                           grad);
+    // (the loss arrival stays here: moved after the backward it put the last workgroup's sum at the kernel's
+    // end, within noise or 0.5 us slower: profiles/r4o_ab_l1_defer.txt)
+    fwd_epilogue<true, true, false>(cam, tile, f, final_T, n_contrib, out_color, out_color2, out_depth, l1, grad);
     __syncthreads();  // the forward's LDS (and its sorted point_list stores) before the backward reuses them
     const BwdPix pin{f.T, f.last16 >> 4, grad[0], grad[1], grad[2], grad[3], 0.f, 0.f};
     Camera cb = cam;
     cb.rowmax = nullptr;  // the block maxima from the registers
     bwd_tile<true, false, false, true, 1, 0>(cb, tile, pin, ranges, point_list, rr, blocksums, inst,
                                              BwdGuard{guard.counters, guard.cap_inst}, smem, dg);
-    l1_finish(l1);  // the loss: arrival and the last workgroup's sum after the backward, not between the phases
     dg.end();
     kclock_end(clk);
 }

@@ -10,6 +10,7 @@
 #   map              the mapping bench leg alone (config 4)
 #   prof             rocprofv3 kernel trace + stats of the headline bench (tracking legs only)
 #   pmc              FETCH_SIZE / WRITE_SIZE passes (one rocprofv3 run per counter) of the headline bench
+#   mprof            rocprofv3 kernel trace + stats of the mapping bench (config 4)
 #   mpmc             map step + FETCH_SIZE / WRITE_SIZE passes of the mapping bench (render kernels, config 4)
 #   sq               SQ issue / wait / LDS counters of the render kernels (two passes, <= 8 SQ counters each)
 #   unit             host / device split of the unchanged-caller unit (tools/raster_unit_profile.py, config 3)
@@ -47,6 +48,9 @@ for s in "$@"; do
                --output-format csv -- python "$ROOT/bench.py" --steps 20 --warmup 20 $LIGHT > "$OUT/pmc_$C.log" 2>&1 ) \
                || { echo "pmc $C failed"; tail -20 "$OUT/pmc_$C.log"; exit 1; }
          done ;;
+    mprof) ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/mprof" -o run \
+             --output-format csv -- python "$ROOT/bench.py" --workload mapping --cpu-baseline off --dropin off \
+             > "$OUT/mprof.log" 2>&1 ) || { echo "mprof failed"; tail -20 "$OUT/mprof.log"; exit 1; } ;;
     mpmc) timeout -k 10 300 python bench.py --workload mapping --cpu-baseline off > "$OUT/map.log" 2>&1 \
              || { echo "map failed"; tail -30 "$OUT/map.log"; exit 1; }
          for C in FETCH_SIZE WRITE_SIZE; do
