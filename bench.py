@@ -458,6 +458,20 @@ def configs_leg(dev, want_cpu: bool):
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / n
             res[name] = {"value": round(1.0 / dt, 2), "unit": "frames/s", "ms_per_frame": round(1000 * dt, 4)}
+        # the eager calls above are host-bound (each forward waits for num_rendered, as the reference's
+        # does): the device time of the fused frame's own kernels, from hipEvents around every stage
+        from splatam_amd import profiling
+        nd = 20
+        profiling.enable_timing(True)
+        for _ in range(nd):
+            fused()
+        torch.cuda.synchronize()
+        st = profiling.read_timing()
+        profiling.enable_timing(False)
+        dev_us = sum(v["ms"] for v in st.values()) * 1000.0 / nd
+        res["fused"]["device_us_per_frame"] = round(dev_us, 2)
+        res["fused"]["device_bound_frames_per_s"] = round(1e6 / dev_us, 1) if dev_us > 0 else None
+        res["fused"]["stages_us_per_frame"] = {k: round(v["ms"] * 1000.0 / nd, 2) for k, v in st.items() if v["ms"]}
         if want_cpu:
             from oracle import oracle as orc
             c = scene.cam
