@@ -27,7 +27,6 @@
 #endif
 
 namespace gsr {
-GSR_WGTIME_TABLE
 
 // Per-pair geometric terms (hx, hy, hx dx, hx dy, hy dy[, G dL/dalpha]) with
 // h = G * dL/dG = (o * G) * dL/dalpha.
@@ -622,6 +621,7 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
     __shared__ __attribute__((aligned(16))) char smem[BwdShape<DUAL, OPAC, COL1, COL2, Q2, MOM>::bytes];
     const int tid = threadIdx.x;
     const int tile = sched_tile(cam), tx = tile % cam.gx, ty = tile / cam.gx;
+    dg.tile(tile);
     const int px = tx * TILE_X + tile_px(tid);
     const int py = ty * TILE_Y + tile_py(tid);
     const bool inside = px < cam.W && py < cam.H;
@@ -674,6 +674,7 @@ render_track_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __
     }
     __shared__ __attribute__((aligned(16))) char smem[track_lds_bytes()];
     const int tile = sched_tile(cam);
+    dg.tile(tile);
     const FwdPix f = fwd_tile<true>(cam, tile, ranges, point_list, keys, rr, guard, smem, dg);
     float grad[4];
     // (the loss arrival stays here: moved after the backward it put the last workgroup's sum at the kernel's

@@ -770,8 +770,7 @@ constexpr int KCLOCK_WORDS = 4 + 16 * KCLOCK_GROUP_STRIDE;
             g_wgtime[b_][(end_) ? 1 : 0] = wall_clock64();                                                 \
             if (!(end_)) {                                                                                 \
                 g_wgtime[b_][2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);                     \
-                g_wgtime[b_][3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) |                   \
-                                  ((unsigned long long)sched_tile(cam) << 32);                             \
+                g_wgtime[b_][3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);                    \
             }                                                                                              \
         }                                                                                                  \
     } while (0)

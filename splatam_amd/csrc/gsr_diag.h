@@ -28,6 +28,7 @@
 namespace gsr {
 
 constexpr int kAblate = GSR_ABLATE;
+GSR_WGTIME_TABLE  // (GSR_WGTIME builds: this translation unit's per-workgroup timeline table)
 
 #if GSR_STEPSTAT
 static __device__ unsigned long long g_stepstat[8];
@@ -47,6 +48,16 @@ struct RenderDiag {
         GSR_WGTIME_MARK(false);
 #if GSR_PHASE
         t = __builtin_amdgcn_s_memtime();
+#endif
+    }
+    // the workgroup's tile (GSR_WGTIME: stored beside its timeline)
+    __device__ __forceinline__ void tile(int t) {
+#if GSR_WGTIME
+        const unsigned b_ = blockIdx.y * gridDim.x + blockIdx.x;
+        if (threadIdx.x == 0 && b_ < GSR_WGTIME_MAX)
+            g_wgtime[b_][3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) | ((unsigned long long)t << 32);
+#else
+        (void)t;
 #endif
     }
     // end of phase k (GSR_PHASE); k == 7 counts a batch

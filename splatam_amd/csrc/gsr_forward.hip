@@ -17,7 +17,6 @@
 #include "gsr_render_fwd.h"
 
 namespace gsr {
-GSR_WGTIME_TABLE
 
 // ------------------------------------------------------------- preprocess --
 // LDS_HIST: per-tile instance counts go to a workgroup histogram in LDS and
@@ -1000,6 +999,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
     }
     __shared__ __attribute__((aligned(16))) char smem[FwdShape<DUAL>::bytes];
     const int tile = sched_tile(cam);
+    dg.tile(tile);
     const FwdPix f = fwd_tile<DUAL>(cam, tile, ranges, point_list, keys, rr, guard, smem, dg);
     float g[4];
     fwd_epilogue<DUAL, L1, true>(cam, tile, f, final_T, n_contrib, out_color, out_color2, out_depth, l1, g);

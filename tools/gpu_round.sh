@@ -16,6 +16,7 @@
 #   unit             host / device split of the unchanged-caller unit (tools/raster_unit_profile.py, config 3)
 #   stream           tools/micro/stream: STREAM copy / triad GB/s (the measured HBM peak)
 #   lock             render_bwd row-list lockstep statistics (tools/lockstep_stats.py, configs 3 and 4)
+#   wgtime           per-workgroup timelines of the render kernels (tools/wgtime.py; needs _diag/libgsr_wgtime.so)
 #   phase            render_fwd / render_bwd phase shares (tools/phase.py; needs _diag/libgsr_phase.so)
 #   ab=MODES=TAGS    interleaved A/B (two rounds) of tools/raster_bench.py stage times between libgsr.so and
 #                    each splatam_amd/_diag/libgsr_<tag>.so (build_variant on the CPU first);
@@ -73,6 +74,8 @@ for s in "$@"; do
     stream) timeout -k 10 120 tools/micro/stream > "$OUT/stream.json" 2>&1 || { echo "stream failed"; exit 1; } ;;
     lock) timeout -k 10 200 python tools/lockstep_stats.py 3 128 > "$OUT/lockstep3.txt" 2>&1 && \
           timeout -k 10 200 python tools/lockstep_stats.py 4 128 > "$OUT/lockstep4.txt" 2>&1 || { echo "lock failed"; exit 1; } ;;
+    wgtime) GSR_LIB=$ROOT/splatam_amd/_diag/libgsr_wgtime.so timeout -k 10 200 python tools/wgtime.py --config 3 \
+              --out "$OUT/wgtime.json" > "$OUT/wgtime.log" 2>&1 || { echo "wgtime failed"; tail -20 "$OUT/wgtime.log"; exit 1; } ;;
     phase) timeout -k 10 200 python tools/phase.py 3 10 > "$OUT/phase.json" 2>&1 || { echo "phase failed"; tail -20 "$OUT/phase.json"; exit 1; } ;;
     ab=*) spec=${s#ab=}; MODES=${spec%%=*}; TAGS=${spec#*=}
           for r in 1 2; do
