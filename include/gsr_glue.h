@@ -189,7 +189,10 @@ int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* g
                             float* dL_dcam_q, float* dL_dcam_t, float* scratch, const gsr_pose_track* track,
                             const float* log_scales, gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
-/* The tracking iteration's render forward and render backward in ONE launch (render_track_kernel):
+/* The tracking iteration's render forward and render backward in ONE launch (render_track_kernel) --
+ * what scripts/splatam.py:255-296 (get_loss(tracking=True)) + :722 (loss.backward()) run as
+ * CudaRasterizer::Rasterizer::forward (rasterizer_impl.cu:198-339) and ::backward (:343-434) per
+ * Renderer call:
  * gsr_track_forward_dual_static_xf's forward + L1 loss, then in the same workgroup the back-to-front
  * walk of gsr_track_backward_dual's render backward -- SplaTAM's tracking loss gradient is per pixel
  * (dL/dloss is the static seed dL_dloss), so a tile's backward needs nothing from other tiles and runs
