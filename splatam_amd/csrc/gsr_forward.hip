@@ -535,18 +535,25 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // tile work spread 0.81-1.18x of the mean with the row-major order, kernel span set
 // by the top; tools/wgtime.py).  tile_plan deals the tiles, in descending order of
 // list length (the render cost: 0.998 correlation with the tile's contributing
-// pairs), to workgroup slots in rounds of ncu, alternating direction (odd rounds
-// and the last, partial round reversed), so every CU's tiles add up to about the
-// same work (max/mean 1.07 on config 3).  Counting sort over length buckets of 4:
-// ties land in arbitrary order, which changes only which workgroup renders a tile,
-// never its results.
+// pairs), to workgroup slots in rounds, alternating direction, so every CU's tiles
+// add up to about the same work.  With n = q * ncu + m tiles, m CUs render q + 1
+// tiles and ncu - m render q (config 3: 176 CUs x 5, 80 x 4; the per-CU end times
+// follow the tile count first, `profiles/r4s_wgtime_fused.json`): the CUs with q
+// tiles take the q (ncu - m) longest lists, dealt over their own q rounds, and the
+// others the rest over q + 1 rounds.  Counting sort over length buckets of 4: ties
+// land in arbitrary order, which changes only which workgroup renders a tile, never
+// its results.
 constexpr int PLAN_BUCKETS = 1024, PLAN_SHIFT = 2;
 __device__ __forceinline__ uint32_t plan_bucket(uint32_t len) {  // descending length -> ascending bucket
     return (uint32_t)(PLAN_BUCKETS - 1) - min(len >> PLAN_SHIFT, (uint32_t)(PLAN_BUCKETS - 1));
 }
 __device__ __forceinline__ uint32_t plan_slot(uint32_t p, uint32_t n, uint32_t ncu) {
-    const uint32_t rd = p / ncu, k = p - rd * ncu, base = rd * ncu, m = min(ncu, n - base);
-    return base + (((rd & 1u) || m < ncu) ? m - 1u - k : k);
+    const uint32_t q = n / ncu, m = n - q * ncu, heavy = q * (ncu - m);
+    // group: CUs [g0, g0 + gs) (slot s renders on CU class s mod ncu), pp = position inside the group
+    const bool hv = p < heavy;
+    const uint32_t g0 = hv ? m : 0u, gs = hv ? ncu - m : m, pp = hv ? p : p - heavy;
+    const uint32_t rd = pp / gs, k = pp - rd * gs;
+    return rd * ncu + g0 + ((rd & 1u) ? gs - 1u - k : k);
 }
 // one workgroup of NT threads (PLAN_BUCKETS / NT consecutive buckets per thread); s_hist:
 // PLAN_BUCKETS words of LDS, s_wsum: NT / 64
