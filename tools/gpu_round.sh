@@ -12,7 +12,8 @@
 #   pmc              FETCH_SIZE / WRITE_SIZE passes (one rocprofv3 run per counter) of the headline bench
 #   mprof            rocprofv3 kernel trace + stats of the mapping bench (config 4)
 #   mpmc             map step + FETCH_SIZE / WRITE_SIZE passes of the mapping bench (render kernels, config 4)
-#   sq               SQ issue / wait / LDS counters of the render kernels (two passes, <= 8 SQ counters each)
+#   sq[=REGEX]       SQ issue / wait / LDS counters of the render kernels (or the kernels REGEX names; two
+#                    passes, <= 8 SQ counters each)
 #   unit             host / device split of the unchanged-caller unit (tools/raster_unit_profile.py, config 3)
 #   stream           tools/micro/stream: STREAM copy / triad GB/s (the measured HBM peak)
 #   lock             render_bwd row-list lockstep statistics (tools/lockstep_stats.py, configs 3 and 4)
@@ -60,12 +61,13 @@ for s in "$@"; do
                -- python "$ROOT/bench.py" --workload mapping --steps 5 --warmup 5 --cpu-baseline off \
                > "$OUT/pmc_map_$C.log" 2>&1 ) || { echo "pmc map $C failed"; tail -20 "$OUT/pmc_map_$C.log"; exit 1; }
          done ;;
-    sq) G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+    sq|sq=*) RX='render_'; [ "$s" != sq ] && RX=${s#sq=}
+        G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
         G2="SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
         i=0
         for G in "$G1" "$G2"; do
           i=$((i+1))
-          ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --pmc $G --kernel-include-regex 'render_' -T \
+          ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --pmc $G --kernel-include-regex "$RX" -T \
               -d "$OUT/sq$i" -o run --output-format csv -- python "$ROOT/bench.py" --steps 20 --warmup 20 $LIGHT \
               > "$OUT/sq$i.log" 2>&1 ) || { echo "sq pass $i failed"; tail -20 "$OUT/sq$i.log"; exit 1; }
         done ;;
