@@ -74,7 +74,14 @@ def main(src, tag):
     stats = (glob.glob(f"{src}/prof/**/run_kernel_stats.csv", recursive=True) or
              glob.glob(f"{src}/trace/**/run_kernel_stats.csv", recursive=True))[0]
     shutil.copy(stats, f"{dst}/{tag}_kernel_stats.csv")
-    rows = {r["Name"]: r for r in csv.DictReader(open(stats))}
+    # the PMC passes (-T) name kernels without namespace / template arguments: trace averages per short
+    # name, over every instantiation
+    tot = defaultdict(lambda: [0.0, 0])
+    for r in csv.DictReader(open(stats)):
+        short = r["Name"].split("(")[0].split("<")[0].split("::")[-1]
+        tot[short][0] += float(r["TotalDurationNs"])
+        tot[short][1] += int(r["Calls"])
+    rows = {k: {"AverageNs": t / max(n, 1)} for k, (t, n) in tot.items()}
     pmc = read_pmc(src, "pmc_")
     bench = None
     blog = f"{src}/bench.log" if os.path.exists(f"{src}/bench.log") else f"{src}/full.log"
