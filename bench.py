@@ -280,8 +280,10 @@ def main():
                 else "hipEvents around each launch"}
     if fused:
         roofline["fused"] = ("the tracking iteration's render forward (+ L1 loss) and render backward in one "
-                             "launch per tile (gsr_track_forward_backward_dual_static_xf); alg bytes = SURVEY 8(d)'s "
-                             "dual render fwd + render bwd")
+                             "launch per tile (gsr_track_forward_backward_dual_static_xf); the rendered images, "
+                             "final_T / n_contrib and the loss gradient images stay in registers (GraphTracker: "
+                             "images=False, nothing reads them after the launch); alg bytes = SURVEY 8(d)'s "
+                             "dual render fwd + render bwd, which count those image writes and reads")
         if world == 1 and args.unfused_leg == "on":
             roofline["unfused"] = unfused_render_leg(params, curr, frame, tracker.iters, P, W, H, Tt, N)
 

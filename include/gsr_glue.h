@@ -198,7 +198,10 @@ int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* g
  * (dL/dloss is the static seed dL_dloss), so a tile's backward needs nothing from other tiles and runs
  * from the pixel state still in registers.  inst_records: gsr_track_records_floats(capacity) floats
  * (device), receiving the per-instance sums gsr_track_backward_dual_records reads; they equal, bit for
- * bit, what gsr_track_backward_dual's render backward forms.  The gradient images are not formed. */
+ * bit, what gsr_track_backward_dual's render backward forms.  The gradient images are not formed.
+ * out_color, out_color2 and out_depth all NULL: the rendered images are not stored either (the loss and
+ * the backward consume them in registers; nor are the image buffer's final_T / n_contrib, so a render
+ * backward from another loss seed cannot follow such a call). */
 int gsr_track_records_floats(int capacity);
 int gsr_track_forward_backward_dual_static_xf(const gsr_settings* settings, const gsr_gaussians* gaussians,
                                               float* colors2, const gsr_track_xform* xform, int capacity,

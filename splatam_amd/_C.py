@@ -461,7 +461,7 @@ def track_backward_dual(settings, means3D, radii, colors, colors2, scales, rotat
     a fused forward (track_forward_dual_static(records=...)): gsr_track_backward_dual_records, only the
     per-Gaussian backward runs and the gradient images are not read (may be None)."""
     device = means3D.device
-    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    H, W = int(settings.image_height), int(settings.image_width)
     with torch.cuda.device(device):
         st = settings
         s, keep_s = _settings(st.bg, st.viewmatrix, st.projmatrix, st.campos, st.tanfovx, st.tanfovy, H, W,
@@ -501,7 +501,8 @@ def track_backward_dual(settings, means3D, radii, colors, colors2, scales, rotat
 
 
 def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scales, rotations, capacity, status, gt_im,
-                              gt_depth, sil_thres, w_im, w_depth, seed, scratch, xform=None, records=None):
+                              gt_depth, sil_thres, w_im, w_depth, seed, scratch, xform=None, records=None,
+                              images=True):
     """gsr_track_forward_dual_static (include/gsr_glue.h): the static dual forward with SplaTAM's
     tracking L1 loss and its gradient images formed in the render epilogue.  Returns (num_rendered=capacity,
     color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth, loss, dL_dim, dL_ddepth_sil).
@@ -511,7 +512,8 @@ def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scale
     when store is true).  records (with xform; device float32 of lib.gsr_track_records_floats(capacity)):
     gsr_track_forward_backward_dual_static_xf -- the tracking render backward runs in the same launch
     and leaves its per-instance sums in records (track_backward_dual(records=...)); dL_dim / dL_ddepth_sil
-    come back None (not formed)."""
+    come back None (not formed).  images=False (with records): the rendered images are not stored either
+    (color, color2 and depth come back None; the loss and the backward consume them in registers)."""
     st = settings
     device = means3D.device
     P = means3D.size(0)
@@ -524,11 +526,17 @@ def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scale
         c2 = _dev_f32(colors2, device, "colors2")
         gi, gd, sd = (_dev_f32(gt_im, device, "gt_im"), _dev_f32(gt_depth, device, "gt_depth"),
                       _dev_f32(seed, device, "seed"))
-        out_color, out_color2 = torch.empty(3, H, W, **f32), torch.empty(3, H, W, **f32)
-        out_depth = torch.empty(1, H, W, **f32)
+        if not images and (xform is None or records is None):
+            raise RuntimeError("track_forward_dual_static: images=False needs the fused render (xform and records)")
+        out_color = out_color2 = out_depth = None
+        if images:
+            out_color, out_color2 = torch.empty(3, H, W, **f32), torch.empty(3, H, W, **f32)
+            out_depth = torch.empty(1, H, W, **f32)
         radii = torch.empty(P, dtype=torch.int32, device=device)
         loss = torch.empty((), **f32)
-        dim, dds = torch.empty(3, H, W, **f32), torch.empty(3, H, W, **f32)
+        dim = dds = None
+        if records is None:
+            dim, dds = torch.empty(3, H, W, **f32), torch.empty(3, H, W, **f32)
         if status is None or status.device != device or status.numel() < 4:
             raise RuntimeError("static dual forward needs a device status tensor of 4 int32")
         _begin(device)
@@ -547,7 +555,7 @@ def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scale
                     raise RuntimeError("records: contiguous float32 of gsr_track_records_floats(capacity) on the device")
                 n = lib.gsr_track_forward_backward_dual_static_xf(
                     ctypes.byref(s), ctypes.byref(g), _ptr(c2), ctypes.byref(xf), int(capacity), status.data_ptr(),
-                    out_color.data_ptr(), out_color2.data_ptr(), out_depth.data_ptr(), radii.data_ptr() if P else None,
+                    _ptr(out_color), _ptr(out_color2), _ptr(out_depth), radii.data_ptr() if P else None,
                     gi.data_ptr(), gd.data_ptr(), float(sil_thres), float(w_im), float(w_depth), sd.data_ptr(),
                     loss.data_ptr(), scratch.data_ptr(), records.data_ptr(), _ALLOC_CB, None, _stream(device))
                 _check(n, "track_forward_backward_dual_static_xf")

@@ -659,6 +659,9 @@ constexpr size_t track_lds_bytes() {
                ? FwdShape<true>::bytes
                : BwdShape<true, false, false, true, 1, 0>::bytes;
 }
+// IMAGES = false: the images (and final_T / n_contrib / the block maxima) are not stored -- a separate
+// instantiation, so that no store (and no wait the compiler places for one) is left in the code
+template <bool IMAGES>
 __global__ void __launch_bounds__(TILE_PIX, 5)
 render_track_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __restrict__ point_list,
                     uint64_t* __restrict__ keys, const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
@@ -673,6 +676,10 @@ render_track_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __
         return;
     }
     __shared__ __attribute__((aligned(16))) char smem[track_lds_bytes()];
+    if constexpr (!IMAGES) {  // (fwd_epilogue stores nothing for a null final_T)
+        final_T = nullptr;
+        cam.rowmax = nullptr;
+    }
     const int tile = sched_tile(cam);
     dg.tile(tile);
     const FwdPix f = fwd_tile<true>(cam, tile, ranges, point_list, keys, rr, guard, smem, dg);
@@ -696,7 +703,8 @@ hipError_t launch_render_track(const Camera& cam, const uint2* ranges, uint64_t*
                                GeomPtrs geo, float* final_T, uint32_t* n_contrib, float* out_color,
                                float* out_color2, float* out_depth, SpecGuard guard, const TrackL1& l1, float* inst,
                                hipStream_t s, unsigned long long* clk) {
-    hipLaunchKernelGGL(render_track_kernel, dim3(cam.gx * cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list,
+    auto k = final_T != nullptr ? render_track_kernel<true> : render_track_kernel<false>;
+    hipLaunchKernelGGL(k, dim3(cam.gx * cam.gy), dim3(TILE_PIX), 0, s, cam, ranges, point_list,
                        keys, geo.rr, geo.blocksums, final_T, n_contrib, out_color, out_color2, out_depth, guard, clk,
                        l1, inst);
     return hipGetLastError();

@@ -306,8 +306,13 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         return fail(GSR_ERR_INVALID_ARG, "the fused render backward needs the static dual forward with the L1 loss");
     if (rc != GSR_OK) return rc;
     if (!alloc) return fail(GSR_ERR_INVALID_ARG, "allocator callback required");
-    if (!out_color || !out_depth) return fail(GSR_ERR_INVALID_ARG, "output image pointers required");
-    if (colors2 && !out_color2) return fail(GSR_ERR_INVALID_ARG, "out_color2 required with colors2");
+    // the fused tracking render may leave its images unstored (all three image pointers NULL): its loss and
+    // backward consume them in registers
+    const bool no_images = track_inst && !out_color && !out_color2 && !out_depth;
+    if (!no_images) {
+        if (!out_color || !out_depth) return fail(GSR_ERR_INVALID_ARG, "output image pointers required");
+        if (colors2 && !out_color2) return fail(GSR_ERR_INVALID_ARG, "out_color2 required with colors2");
+    }
     if (colors2 && gaussians->P > 0 && !gaussians->means3D) return fail(GSR_ERR_INVALID_ARG, "means3D is required");
     hipStream_t stream = (hipStream_t)stream_;
     const int dev = stream_device(stream);
@@ -406,6 +411,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     if (P == 0) {  // rasterize_points.cu:67-81: zero outputs, forward not run (the sticky status keeps its rows)
         void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, BinLayout::make(0, W, H).total);
         if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
+        if (no_images) return 0;
         if ((e = zero_async(out_color, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess ||
             (e = zero_async(out_depth, sizeof(float) * (size_t)W * H, stream)) != hipSuccess ||
             (colors2 && (e = zero_async(out_color2, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess))
@@ -451,7 +457,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         if (capacity <= 0 && scan_in_duplicate && (rc = snapshot_counters()) != GSR_OK) return rc;
         if (track_inst) {  // forward + L1 + the tracking render backward, one launch (render_track_kernel)
             StageTimer t(GSR_STAGE_RENDER_FWD, 0, stream, true);
-            if ((e = launch_render_track(cam, ranges, point_list, keys[0], geo, final_T, n_contrib, out_color,
+            if ((e = launch_render_track(cam, ranges, point_list, keys[0], geo, no_images ? nullptr : final_T,
+                                         n_contrib, out_color,
                                          out_color2, out_depth, guard, *l1, track_inst, stream, t.kclock())) !=
                 hipSuccess)
                 return hip_fail(e, "render (fused tracking forward + backward)");
@@ -778,7 +785,8 @@ int gsr_track_forward_backward_dual_static_xf(const gsr_settings* settings, cons
                                               void* stream) {
     if (!inst_records) return fail(GSR_ERR_INVALID_ARG, "track_forward_backward_dual_static_xf: null records");
     // the gradient images are not formed (the backward runs from the registers); the L1 epilogue's
-    // pointers to them are never dereferenced
+    // pointers to them are never dereferenced.  out_color, out_color2 and out_depth all NULL: the rendered
+    // images (and final_T / n_contrib / the block maxima of the image buffer) are not stored either
     return track_forward_xf(settings, gaussians, colors2, xform, capacity, status, out_color, out_color2, out_depth,
                             radii, gt_im, gt_depth, sil_thres, w_im, w_depth, dL_dloss, loss, loss, loss, scratch,
                             alloc, alloc_ctx, stream, inst_records);

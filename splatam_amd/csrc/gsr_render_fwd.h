@@ -448,7 +448,7 @@ __device__ __forceinline__ void fwd_epilogue(const Camera& cam, int tile, const 
             for (int c = 0; c < 3; c++) l1_gi[c] = l1.gt_im[c * HW + pid];
         }
     }
-    if (inside && (GSR_FWD_ABLATE != 8 || T == 1.2345f)) {  // (ablation 8: no image stores, values kept live)
+    if (inside && final_T != nullptr && (GSR_FWD_ABLATE != 8 || T == 1.2345f)) {  // (ablation 8: no image stores)
         const int pid = py * cam.W + px;
         const int HW = cam.W * cam.H;
         auto st = [](float* p, float v) {

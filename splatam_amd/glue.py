@@ -472,7 +472,8 @@ class _TrackIteration(torch.autograd.Function):
     the pose Adam step) fused in.  Differentiable w.r.t. the pose only, like track_transform."""
 
     @staticmethod
-    def forward(ctx, cam_rots, cam_trans, params, curr, t, cfg, pose_adam, capacity, status, means2D, seed):
+    def forward(ctx, cam_rots, cam_trans, params, curr, t, cfg, pose_adam, capacity, status, means2D, seed,
+                images=True):
         from . import _C
         cam = curr["cam"]
         cam_rots, cam_trans = _f32c(cam_rots, "cam_unnorm_rots"), _f32c(cam_trans, "cam_trans")
@@ -501,9 +502,12 @@ class _TrackIteration(torch.autograd.Function):
             records = None
             if _RENDER_FUSED:  # (a static seed promises the backward): the render backward in the forward's launch
                 records = torch.empty(lib.gsr_track_records_floats(capacity), **f32)
+            # images=False (fused render only): the rendered images stay in registers -- the loss and the
+            # render backward are in the same launch; nothing reads them afterwards unless the backward is
+            # taken from another seed, which then raises
             (n, im, ds, radii, geom, binning, img, _, loss, dim, dds) = _C.track_forward_dual_static(
                 cam, means, rgb, dcol, opac, scales, rot, capacity, status, gt_im, gt_d, cfg.sil_thres, cfg.w_im,
-                cfg.w_depth, seed, scratch, xform=xform, records=records)
+                cfg.w_depth, seed, scratch, xform=xform, records=records, images=images or records is None)
             ctx.pre = (dim, dds, seed)
             ctx.records = records
             ctx.save_for_backward(cam_rots, cam_trans, mw, ur, means, rot, dcol, scales, rgb, radii, geom, binning,
@@ -572,7 +576,7 @@ class _TrackIteration(torch.autograd.Function):
         (cam_rots, cam_trans, mw, ur, means, rot, dcol, scales, rgb, radii, geom, binning, img, im, ds, gt_im, gt_d,
          w2c) = ctx.saved_tensors
         t, T, scols, n, cam, cfg = ctx.meta
-        nones = (None,) * 11
+        nones = (None,) * 12
         records = getattr(ctx, "records", None)
         if ctx.pre is not None and g is not None and g.data_ptr() == ctx.pre[2].data_ptr():
             dim, dds = ctx.pre[0], ctx.pre[1]
@@ -582,6 +586,9 @@ class _TrackIteration(torch.autograd.Function):
             records = None  # another loss seed: the render backward runs from the recomputed gradient images
             if g is None:
                 return nones
+            if im is None:
+                raise RuntimeError("tracking_iteration(images=False) rendered without storing its images: "
+                                   "backpropagate the static loss seed it was given")
             H, W = cam.image_height, cam.image_width
             g = g.contiguous()
             dim, dds = torch.empty_like(im), torch.empty_like(ds)
@@ -605,16 +612,19 @@ class _TrackIteration(torch.autograd.Function):
                                scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c, scratch,
                                dq_ptr=dq.data_ptr() + 4 * t, dt_ptr=dt.data_ptr() + 4 * t, log_scales=ctx.log_scales,
                                records=records)
-        return (dq, dt) + (None,) * 9
+        return (dq, dt) + (None,) * 10
 
 
 def tracking_iteration(params: dict, curr: dict, time_idx: int, cfg, pose_adam: PoseAdam | None = None,
-                       capacity: int = 0, status=None, seed=None):
+                       capacity: int = 0, status=None, seed=None, images: bool = True):
     """get_loss(tracking=True) as one fused forward (transform, dual rasterization, masked L1) whose backward
     runs the render backward and the per-Gaussian backward with the pose chain (+ pose Adam) fused in:
-    no per-Gaussian gradient array, no separate pose-reduction launch.  Returns (loss, radii)."""
+    no per-Gaussian gradient array, no separate pose-reduction launch.  Returns (loss, radii).
+    images=False: with the render backward fused into the forward's launch (static mode and seed), the
+    rendered images are not stored at all (get_loss reads them only for the loss, formed in the same launch);
+    the backward must then be taken from `seed`."""
     return _TrackIteration.apply(params["cam_unnorm_rots"], params["cam_trans"], params, curr, int(time_idx), cfg,
-                                 pose_adam, int(capacity), status, None, seed)
+                                 pose_adam, int(capacity), status, None, seed, bool(images))
 
 
 class _DualRenderL1(torch.autograd.Function):

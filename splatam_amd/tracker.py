@@ -120,8 +120,11 @@ class GraphTracker:
         self.adam.status = self.status[k]  # this iteration's forward guards its Adam step
         if self.fuse_pose:
             from .glue import tracking_iteration
+            # (images=False: the replays keep the rendered images in registers -- the loss and the render
+            # backward run in the same launch and the tracker reads neither image)
             loss, _ = tracking_iteration(self.params, self.curr, self.t, self.cfg, pose_adam=self.adam,
-                                         capacity=self.capacity, status=self.status[k], seed=self.seed)
+                                         capacity=self.capacity, status=self.status[k], seed=self.seed,
+                                         images=False)
             torch.autograd.backward(loss, self.seed)
             return loss.detach()
         loss, _, _ = _get_loss_tracking_fused(self.params, self.curr, self.t, self.cfg, dual=True,

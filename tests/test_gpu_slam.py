@@ -270,28 +270,50 @@ def test_track_render_fused_bitwise(cuda, case, monkeypatch):
     """gsr_track_forward_backward_dual_static_xf (render_track_kernel: a tile's forward + L1 loss and its
     render backward in one workgroup) + gsr_track_backward_dual_records against the separate render_fwd /
     render_bwd launches: loss, radii, images and the pose gradients bitwise equal -- on small scenes and at
-    BASELINE config 3 (300 k Gaussians, 640x480: multi-batch tiles, 512- and 1024-key sorts)."""
+    BASELINE config 3 (300 k Gaussians, 640x480: multi-batch tiles, 512- and 1024-key sorts).  The fused
+    launch without image stores (images=False, GraphTracker's form) gives the same loss, radii and pose
+    gradients."""
     from splatam_amd import glue
     from splatam_amd.scenes import config_scene
     from splatam_amd.slam import TrackingConfig
     params, curr = _setup(cuda, case == "aniso", config_scene(3) if case == "config3" else None)
     seed = torch.ones((), device=cuda)
     outs = []
-    for fused in (False, True):
+    for fused, images in ((False, True), (True, True), (True, False)):
         monkeypatch.setattr(glue, "_RENDER_FUSED", fused)
         p = _pose_leaves(params)
         status = torch.zeros(4, dtype=torch.int32, device=cuda)
         loss, radii = glue.tracking_iteration(p, curr, 1, TrackingConfig(), capacity=1200000, status=status,
-                                              seed=seed)
+                                              seed=seed, images=images)
         saved = loss.grad_fn.saved_tensors  # (.., im, ds at 13, 14)
-        ims = [saved[13].clone(), saved[14].clone()]
+        ims = [saved[13].clone(), saved[14].clone()] if images else None
+        if not images:
+            assert saved[13] is None and saved[14] is None
         assert (getattr(loss.grad_fn, "records", None) is not None) == fused
         torch.autograd.backward(loss, seed)
         outs.append((loss.detach().clone(), radii.clone(), ims, p["cam_unnorm_rots"].grad.clone(),
                      p["cam_trans"].grad.clone()))
         assert int(status[1]) == 0 and 0 < int(status[0]) <= 1200000
-    (l0, r0, i0, q0, t0), (l1, r1, i1, q1, t1) = outs
+    (l0, r0, i0, q0, t0), (l1, r1, i1, q1, t1), (l2, r2, _, q2, t2) = outs
     assert torch.equal(l0, l1) and torch.equal(r0, r1)
     assert torch.equal(i0[0], i1[0]) and torch.equal(i0[1], i1[1])
     assert torch.equal(q0, q1) and torch.equal(t0, t1)
+    assert torch.equal(l1, l2) and torch.equal(r1, r2) and torch.equal(q1, q2) and torch.equal(t1, t2)
     assert float(q1[..., 1].abs().sum()) > 0.0
+
+
+def test_track_render_no_images_needs_its_seed(cuda):
+    """tracking_iteration(images=False) stores no images: a backward from another loss seed (which would
+    recompute the gradient images from them) raises instead of reading unwritten memory."""
+    from splatam_amd import glue
+    from splatam_amd.slam import TrackingConfig
+    if not glue._RENDER_FUSED:
+        pytest.skip("fused tracking render disabled (GSR_TRACK_RENDER_FUSED=0)")
+    params, curr = _setup(cuda, False, None)
+    seed = torch.ones((), device=cuda)
+    p = _pose_leaves(params)
+    status = torch.zeros(4, dtype=torch.int32, device=cuda)
+    loss, _ = glue.tracking_iteration(p, curr, 1, TrackingConfig(), capacity=400000, status=status, seed=seed,
+                                      images=False)
+    with pytest.raises(RuntimeError, match="images=False"):
+        torch.autograd.backward(loss, 2.0 * seed)
