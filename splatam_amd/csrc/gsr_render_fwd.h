@@ -284,6 +284,7 @@ __device__ __forceinline__ FwdPix fwd_tile(const Camera& cam, int tile, const ui
         prio_by_remaining((int)(range.y - start), mean4, multi_round);
         if (__syncthreads_and(done)) break;  // forward.cu:314-316
         const int cnt = (int)min((uint32_t)RENDER_BATCH, range.y - start);
+        PointEntry ent = 0;
         if (tid < cnt) {
             float xs = x0, ys = y0;
             asm volatile("" : "+v"(xs), "+v"(ys));  // block bounds formed here, not hoisted (VGPRs)
@@ -306,12 +307,15 @@ __device__ __forceinline__ FwdPix fwd_tile(const Camera& cam, int tile, const ui
             s_c[tid] = pc;
             if (DUAL) s_d[tid] = pd;
             s_mask[tid] = (uint16_t)pm;
-            point_list[start + tid] = ((PointEntry)pm << 32) | pg;  // the mask, for render_bwd
+            ent = ((PointEntry)pm << 32) | pg;  // the mask, for render_bwd (stored below)
         }
         __syncthreads();
         dg.phase(1);
         fetch_rec(start + RENDER_BATCH);      // records of the next batch (ids loaded a batch ago)
         fetch_id(start + 2 * RENDER_BATCH);   // ids of the batch after it
+        // the entry's store after those loads: a load issued behind a store waits for the store too
+        // (vmcnt counts both), so the other order put this store's latency in front of every gather
+        if (tid < cnt) point_list[start + tid] = ent;
         const int jmin0[4] = {0, 0, 0, 0};
         // list entries: LDS byte offsets 16 j of the staged records (the walk loads them with ds_read_u16)
         static_assert(16 * RENDER_BATCH < 65536, "16-bit byte offsets");
