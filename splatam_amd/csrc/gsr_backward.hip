@@ -786,7 +786,20 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     gg.s = make_float3(0.f, 0.f, 0.f);
     gg.q = make_float4(0.f, 0.f, 0.f, 0.f);
     // POSE: the frame's (pre-step) pose is workgroup-uniform: formed once by thread 0 (8 IEEE divisions and 2
-    // square roots per lane otherwise) and read from LDS -- the same bits
+    // square roots per lane otherwise) and read from LDS -- the same bits.  The Gaussian's own inputs (radius,
+    // record range, the world-frame transform inputs) are loaded ahead of that barrier: loads issued after a
+    // __syncthreads would wait for thread 0's pose chain (its loads and the make_pose arithmetic)
+    const int rad = live ? radii[i] : 0;
+    const bool xf_geom = POSE && pf.ls;
+    TrackXf x;
+    x.mw = pf.means_world; x.ur = pf.unnorm_rot; x.ls = pf.ls; x.scols = pf.scols;
+    XfRaw xr{};
+    if (xf_geom && live) xr = track_xform_load(x, i, false);
+    uint32_t off = 0, cnt = 0;
+    if (POSE && live && rad > 0) {
+        off = geo.offsets[i];
+        cnt = geo.tiles[i];
+    }
     __shared__ Pose s_pose;
     if constexpr (POSE) {
         if (pf.ls || pf.scols != 1) {
@@ -794,21 +807,22 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
             __syncthreads();
         }
     }
-    if (live && (POSE || radii[i] > 0)) {  // (the pose sums need every live Gaussian's mean)
-        if (POSE && pf.ls) {
-            TrackXf x;
-            x.mw = pf.means_world; x.ur = pf.unnorm_rot; x.ls = pf.ls; x.scols = pf.scols;
+    if (live && (POSE || rad > 0)) {  // (the pose sums need every live Gaussian's mean)
+        if (xf_geom) {
             const Pose ps = s_pose;
             float m[3], sv[3];
-            track_xform_geom(x, ps, i, m, gg.q, sv);
+            track_xform_geom_raw(xr, x.scols, ps, m, gg.q, sv);
             gg.m = make_float3(m[0], m[1], m[2]);
             gg.s = make_float3(sv[0], sv[1], sv[2]);
         } else {
             gg = load_geom(g, i);
         }
     }
-    if (live && radii[i] > 0 && !guard.overflow()) {  // overflow: zero gradients, no record reads
-        const uint32_t off = geo.offsets[i], cnt = geo.tiles[i];
+    if (live && rad > 0 && !guard.overflow()) {  // overflow: zero gradients, no record reads
+        if (!POSE) {
+            off = geo.offsets[i];
+            cnt = geo.tiles[i];
+        }
         // fixed-order sum of the Gaussian's instance records (deterministic)
         float acc[INST_REC_MAX];
 #pragma unroll

@@ -23,6 +23,8 @@
 #                    each splatam_amd/_diag/libgsr_<tag>.so (build_variant on the CPU first);
 #                    MODES = mode:config[,mode:config...], TAGS = tag[,tag...]   e.g. ab=dual_lean:3,dual:4=ablw
 #   abbench=TAGS     interleaved A/B of the bench line (tracking + mapping values, render stage times)
+#   abprof=TAGS      interleaved A/B (two rounds) of rocprofv3 kernel-trace averages of the headline bench's
+#                    tracking kernels between libgsr.so and each _diag/libgsr_<tag>.so
 #   abflag=FLAG:V1,V2[,...]  interleaved A/B (two rounds) of the light bench line over the values of one bench.py
 #                    flag, e.g. abflag=--fuse-render:1,0
 TAG=${1:-x}; shift
@@ -90,6 +92,25 @@ for s in "$@"; do
               done
             done
           done ;;
+    abprof=*) TAGS=${s#abprof=}
+         for r in 1 2; do
+           L="base ${TAGS//,/ }"; [ $r = 2 ] && L="$(echo $L | tr ' ' '\n' | tac | tr '\n' ' ')"
+           for t in $L; do
+             d="$OUT/abprof_${t}_$r"
+             ( cd /tmp && export TMPDIR=/tmp && GSR_LIB=$(lib_of $t) timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+                 -d "$d" -o run --output-format csv -- python "$ROOT/bench.py" --steps 40 --warmup 20 $LIGHT \
+                 > "$d.log" 2>&1 ) || { echo "abprof $t failed"; tail -20 "$d.log"; exit 1; }
+             python - "$d" $t $r <<'PY' | tee -a "$OUT/abprof.txt"
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)[0]
+ks = {}
+for row in csv.DictReader(open(f)):
+    if int(row["Calls"]) >= 40:
+        ks[row["Name"].split("(")[0].split("<")[0].split("::")[-1]] = float(row["AverageNs"]) / 1000
+print("abprof", sys.argv[2], "round", sys.argv[3], " ".join(f"{k} {v:.2f}" for k, v in sorted(ks.items())))
+PY
+           done
+         done ;;
     abbench=*) TAGS=${s#abbench=}
           for r in 1 2; do
             ORDER="base ${TAGS//,/ }"
