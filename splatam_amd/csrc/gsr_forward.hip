@@ -673,11 +673,14 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
             cv[k] = ok ? cursor[(size_t)b * ntiles + t0 + k] : 0u;
         }
         uint32_t pre = 0, all = 0, viol = 0, vmax = 0;
-        for (uint32_t k = tid; k < nb; k += DUP_T) {
-            const uint32_t v = geo.wgsum[k];
-            viol |= v >> 31;
-            all += v & 0x7fffffffu;
-            pre += k < b ? (v & 0x7fffffffu) : 0u;
+        // two workgroup sums per trip, both loads issued before either is used (config 3: 586 rows, so some
+        // lanes read two -- one memory round trip instead of two ahead of the workgroup's first barrier)
+        for (uint32_t k = tid; k < nb; k += 2 * DUP_T) {
+            const uint32_t k2 = k + DUP_T;
+            const uint32_t v = geo.wgsum[k], v2 = k2 < nb ? geo.wgsum[k2] : 0u;
+            viol |= (v | v2) >> 31;
+            all += (v & 0x7fffffffu) + (v2 & 0x7fffffffu);
+            pre += (k < b ? (v & 0x7fffffffu) : 0u) + (k2 < b ? (v2 & 0x7fffffffu) : 0u);
         }
         uint32_t csum = 0;
         if (in_regs) {
