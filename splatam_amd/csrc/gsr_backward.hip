@@ -874,7 +874,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         g2[2] *= -0.5f;
         g2[3] *= -0.5f;
         g2[4] *= -0.5f;
-        const unsigned clamped = geo.clamp[i];
+        const unsigned clamped = g.shs ? geo.clamp[i] : 0u;  // (SH colour clamping; not stored without SH)
         gauss_chain(cam, g, gg, i, g2, clamped, dmean, dcov, dscale, drot, dsh, nsh);
     }
     if constexpr (POSE) {

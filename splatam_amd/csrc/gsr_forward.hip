@@ -150,7 +150,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                 }
                 q1 = make_float4(K_B * cb, XF ? xop : pre_op, pv.z, 0.f);  // .w: workgroup-local instance offset, below
                 geo.bin[i] = make_uint4(rlo, rhi, __float_as_uint(pv.z), tiles);
-                if (!g.sh_staged) geo.clamp[i] = clamped;
+                if (!g.sh_staged && !g.colors) geo.clamp[i] = clamped;  // (read only by the SH backward)
                 for (int ty = y0; ty < y1; ty++)  // per-tile instance counts -> bucket ranges
                     for (int tx = x0; tx < x1; tx++) {
                         if (LDS_HIST) atomicAdd(&s_hist[ty * cam.gx + tx], 1u);
