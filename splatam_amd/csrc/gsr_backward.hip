@@ -875,7 +875,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         g2[3] *= -0.5f;
         g2[4] *= -0.5f;
         const unsigned clamped = g.shs ? geo.clamp[i] : 0u;  // (SH colour clamping; not stored without SH)
-        gauss_chain(cam, g, gg, i, g2, clamped, dmean, dcov, dscale, drot, dsh, nsh);
+        gauss_chain(cam, g, gg, i, g2, clamped, dmean, dcov, dscale, drot, dsh, nsh, !POSE || pf.scols != 1);
     }
     if constexpr (POSE) {
         // tracking: the pose sums of this Gaussian (track_transform_bwd_kernel's, gsr_glue.hip), then

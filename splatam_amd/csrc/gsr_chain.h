@@ -114,9 +114,11 @@ __device__ __forceinline__ void sh_chain_bwd(const Camera& cam, float3 m, const 
 // ------------------------------------------------------ per-Gaussian chain --
 // g2: [0..1] dL/dmean2D (NDC units), [2..4] dL/dconic (A, B/2, C), [5] dL/dopacity,
 // [6..8] dL/dcolor.  Outputs: dmean3D[3], dcov3D[6], dscale[3], drot[4], dsh[3*nsh].
+// want_rs = false: dscale / drot are not wanted (left zero) -- the pose-fused tracking backward of an
+// isotropic map, whose pose sums read neither
 __device__ inline void gauss_chain(const Camera& cam, const GaussIn& g, const GaussGeom& gg, int i, const float g2[9],
                                    unsigned clamped, float dmean[3], float dcov[6], float dscale[3], float drot[4],
-                                   float* dsh_out, int nsh) {
+                                   float* dsh_out, int nsh, bool want_rs = true) {
     const float fx = cam.focal_x, fy = cam.focal_y;
     const float3 m = gg.m;
     float c3[6];
@@ -189,7 +191,7 @@ __device__ inline void gauss_chain(const Camera& cam, const GaussIn& g, const Ga
     for (int k = 0; k < 3; k++) dscale[k] = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; k++) drot[k] = 0.f;
-    if (g.scales) {
+    if (g.scales && want_rs) {
         const float4 q = gg.q;
         const float r = q.x, x = q.y, y = q.z, z = q.w;
         float R[3][3];
