@@ -865,8 +865,9 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         // instance records hold (hx, hy, hxx, hxy, hyy, dopacity, dcolor) sums (render_bwd_kernel);
         // the conic is recomputed exactly as preprocess computed it (the render record keeps
         // only its exp2-scaled form)
-        float ca, cb, cc;
-        gaussian_conic(cam, g, gg, i, ca, cb, cc);
+        float ca, cb, cc, c3[6];
+        Proj pj;
+        gaussian_conic(cam, g, gg, i, ca, cb, cc, &pj, c3);
         const float ddelx = (float)(0.5 * cam.W), ddely = (float)(0.5 * cam.H);  // backward.cu:935-936
         const float hx = g2[0], hy = g2[1];
         g2[0] = -(ca * hx + cb * hy) * ddelx;
@@ -875,7 +876,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         g2[3] *= -0.5f;
         g2[4] *= -0.5f;
         const unsigned clamped = g.shs ? geo.clamp[i] : 0u;  // (SH colour clamping; not stored without SH)
-        gauss_chain(cam, g, gg, i, g2, clamped, dmean, dcov, dscale, drot, dsh, nsh, !POSE || pf.scols != 1);
+        gauss_chain(cam, g, gg, i, g2, clamped, dmean, dcov, dscale, drot, dsh, nsh, !POSE || pf.scols != 1, &pj, c3);
     }
     if constexpr (POSE) {
         // tracking: the pose sums of this Gaussian (track_transform_bwd_kernel's, gsr_glue.hip), then

@@ -26,8 +26,9 @@ __device__ __forceinline__ GaussGeom load_geom(const GaussIn& g, int i) {
 }
 
 // Conic of Gaussian i as preprocess computed it (same helpers, same inputs).
+// (pj_out / c3_out: the projection and 3D covariance it formed, for gauss_chain to reuse)
 __device__ inline void gaussian_conic(const Camera& cam, const GaussIn& g, const GaussGeom& gg, int i, float& ca,
-                                      float& cb, float& cc) {
+                                      float& cb, float& cc, Proj* pj_out = nullptr, float* c3_out = nullptr) {
     const float3 m = gg.m;
     float c3[6];
     if (g.cov3D) {
@@ -39,6 +40,10 @@ __device__ inline void gaussian_conic(const Camera& cam, const GaussIn& g, const
     Proj pj;
     cov2d_fwd(m, cam.focal_x, cam.focal_y, cam.tan_fovx, cam.tan_fovy, c3, cam.view, pj);
     (void)conic_of(pj, ca, cb, cc);
+    if (pj_out) *pj_out = pj;
+    if (c3_out)
+#pragma unroll
+        for (int k = 0; k < 6; k++) c3_out[k] = c3[k];
 }
 __device__ inline void gaussian_conic(const Camera& cam, const GaussIn& g, int i, float& ca, float& cb, float& cc) {
     gaussian_conic(cam, g, load_geom(g, i), i, ca, cb, cc);
@@ -118,19 +123,26 @@ __device__ __forceinline__ void sh_chain_bwd(const Camera& cam, float3 m, const 
 // isotropic map, whose pose sums read neither
 __device__ inline void gauss_chain(const Camera& cam, const GaussIn& g, const GaussGeom& gg, int i, const float g2[9],
                                    unsigned clamped, float dmean[3], float dcov[6], float dscale[3], float drot[4],
-                                   float* dsh_out, int nsh, bool want_rs = true) {
+                                   float* dsh_out, int nsh, bool want_rs = true, const Proj* pj_in = nullptr,
+                                   const float* c3_in = nullptr) {
     const float fx = cam.focal_x, fy = cam.focal_y;
     const float3 m = gg.m;
     float c3[6];
-    if (g.cov3D) {
-#pragma unroll
-        for (int k = 0; k < 6; k++) c3[k] = g.cov3D[6 * i + k];
-    } else {
-        cov3d_fwd(gg.s, cam.scale_modifier, gg.q, c3);
-    }
-    // computeCov2DCUDA (backward.cu:144-274)
     Proj pj;
-    cov2d_fwd(m, fx, fy, cam.tan_fovx, cam.tan_fovy, c3, cam.view, pj);
+    if (pj_in) {  // gaussian_conic's (the same expressions on the same inputs)
+        pj = *pj_in;
+#pragma unroll
+        for (int k = 0; k < 6; k++) c3[k] = c3_in[k];
+    } else {
+        if (g.cov3D) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) c3[k] = g.cov3D[6 * i + k];
+        } else {
+            cov3d_fwd(gg.s, cam.scale_modifier, gg.q, c3);
+        }
+        // computeCov2DCUDA (backward.cu:144-274)
+        cov2d_fwd(m, fx, fy, cam.tan_fovx, cam.tan_fovy, c3, cam.view, pj);
+    }
     const float a = pj.a, b = pj.b, c = pj.c;
     const float gA = g2[2], gBh = g2[3], gC = g2[4];
     const float denom = a * c - b * b;
