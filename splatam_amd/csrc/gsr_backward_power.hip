@@ -365,23 +365,26 @@ gauss_bwd_power_kernel(GaussIn g, GeomPtrs geo, const int* __restrict__ radii, c
 // 16-B record per (tile, Gaussian) instance at its unsorted slot.
 constexpr int MPACK_F4 = 4;  // M (15 floats, row-major) + 1 pad
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 5)  // (5 workgroups per CU: a frame's ~1200 in one round)
 gauss_mpack_kernel(Camera cam, GaussIn g, const int* __restrict__ radii, float4* __restrict__ mp) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= g.P || radii[i] <= 0) return;
     const GaussGeom gg = load_geom(g, i);
+    // the conic, projection and 3D covariance once; the five chain evaluations reuse them and skip the
+    // rotation / scale terms (only dmean3D is tabulated)
+    float ca, cb, cc, c3[6];
+    Proj pj;
+    gaussian_conic(cam, g, gg, i, ca, cb, cc, &pj, c3);
     float J[3][5];
 #pragma unroll 1
     for (int kk = 0; kk < 5; kk++) {  // column kk <- unit dmean2D.x/.y, dconic.A/.B/.C
         float g2[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         g2[kk] = 1.f;
         float dmean[3], dcov[6], dscale[3], drot[4], dsh[48];
-        gauss_chain(cam, g, gg, i, g2, 0u, dmean, dcov, dscale, drot, dsh, 0);
+        gauss_chain(cam, g, gg, i, g2, 0u, dmean, dcov, dscale, drot, dsh, 0, false, &pj, c3);
 #pragma unroll
         for (int r = 0; r < 3; r++) J[r][kk] = dmean[r];
     }
-    float ca, cb, cc;
-    gaussian_conic(cam, g, gg, i, ca, cb, cc);
     const float ddelx = (float)(0.5 * cam.W), ddely = (float)(0.5 * cam.H);  // backward.cu:935-936
     float M[16];
 #pragma unroll
