@@ -1120,8 +1120,9 @@ gauss_bwd_mom_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict_
     };
     if (live) {
         const GaussGeom gg = load_geom(g, i);
-        float ca, cb, cc;
-        gaussian_conic(cam, g, gg, i, ca, cb, cc);
+        float ca, cb, cc, c3[6];
+        Proj pj;  // (with c3: reused by the unit chain evaluations below)
+        gaussian_conic(cam, g, gg, i, ca, cb, cc, &pj, c3);
         const float ddx = (float)(0.5 * cam.W), ddy = (float)(0.5 * cam.H);  // backward.cu:935-936
         // chain input g2 = Lm u: dmean2D (NDC units) from (hx, hy), dconic = -u_conic / 2 (backward.cu:1020-1038)
         const float L0[2] = {-ca * ddx, -cb * ddx}, L1[2] = {-cb * ddy, -cc * ddy};
@@ -1145,7 +1146,7 @@ gauss_bwd_mom_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict_
             float g2[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             g2[in] = 1.f;
             float dmean[3], dcov[6], dscale[3], drot[4], dsh[48];
-            gauss_chain(cam, g, gg, i, g2, 0u, dmean, dcov, dscale, drot, dsh, nsh);
+            gauss_chain(cam, g, gg, i, g2, 0u, dmean, dcov, dscale, drot, dsh, nsh, true, &pj, c3);
             // (selects with constant indices: no dynamic register-array indexing)
 #pragma unroll
             for (int b = 0; b < 5; b++) {

@@ -59,13 +59,19 @@ gauss_jac_kernel(Camera cam, GaussIn g, const int* __restrict__ radii, float* __
     if (i >= g.P || radii[i] <= 0) return;
     const int nsh = g.shs ? (cam.sh_degree + 1) * (cam.sh_degree + 1) : 0;
     float* J = jac + (size_t)JAC_FLOATS * i;
+    // the geometry, conic, projection and 3D covariance once (as preprocess computed the conic); the
+    // eight unit chain evaluations reuse them
+    const GaussGeom gg = load_geom(g, i);
+    float ca, cb, cc, c3[6];
+    Proj pj;
+    gaussian_conic(cam, g, gg, i, ca, cb, cc, &pj, c3);
     // column kk <- unit input g2[kin[kk]] (opacity, input 5, reaches no chained output)
     for (int kk = 0; kk < 8; kk++) {
         const int in = kk < 5 ? kk : kk + 1;
         float g2[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         g2[in] = 1.f;
         float dmean[3], dcov[6], dscale[3], drot[4], dsh[48];
-        gauss_chain(cam, g, i, g2, 0u, dmean, dcov, dscale, drot, dsh, nsh);
+        gauss_chain(cam, g, gg, i, g2, 0u, dmean, dcov, dscale, drot, dsh, nsh, true, &pj, c3);
         for (int r = 0; r < 3; r++) J[r * 8 + kk] = dmean[r];
         if (in >= 2 && in <= 4) {
             const int c = in - 2;
@@ -77,7 +83,9 @@ gauss_jac_kernel(Camera cam, GaussIn g, const int* __restrict__ radii, float* __
             for (int k = 0; k < 16; k++) J[63 + k] = k < nsh ? dsh[3 * k] : 0.f;
     }
     J[79] = 0.f;
-    gaussian_conic(cam, g, i, J[JAC_CONIC], J[JAC_CONIC + 1], J[JAC_CONIC + 2]);  // as preprocess computed it
+    J[JAC_CONIC] = ca;
+    J[JAC_CONIC + 1] = cb;
+    J[JAC_CONIC + 2] = cc;
     J[JAC_CONIC + 3] = 0.f;
 }
 
