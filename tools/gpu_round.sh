@@ -25,6 +25,7 @@
 #   abbench=TAGS     interleaved A/B of the bench line (tracking + mapping values, render stage times)
 #   abprof=TAGS      interleaved A/B (two rounds) of rocprofv3 kernel-trace averages of the headline bench's
 #                    tracking kernels between libgsr.so and each _diag/libgsr_<tag>.so
+#   abfisher=TAGS    interleaved A/B (two rounds) of the Fisher leg: poses/s and its kernels' rocprofv3 averages
 #   abflag=FLAG:V1,V2[,...]  interleaved A/B (two rounds) of the light bench line over the values of one bench.py
 #                    flag, e.g. abflag=--fuse-render:1,0
 TAG=${1:-x}; shift
@@ -108,6 +109,25 @@ for row in csv.DictReader(open(f)):
     if int(row["Calls"]) >= 40:
         ks[row["Name"].split("(")[0].split("<")[0].split("::")[-1]] = float(row["AverageNs"]) / 1000
 print("abprof", sys.argv[2], "round", sys.argv[3], " ".join(f"{k} {v:.2f}" for k, v in sorted(ks.items())))
+PY
+           done
+         done ;;
+    abfisher=*) TAGS=${s#abfisher=}
+         for r in 1 2; do
+           L="base ${TAGS//,/ }"; [ $r = 2 ] && L="$(echo $L | tr ' ' '\n' | tac | tr '\n' ' ')"
+           for t in $L; do
+             d="$OUT/abfisher_${t}_$r"
+             ( cd /tmp && export TMPDIR=/tmp && GSR_LIB=$(lib_of $t) timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+                 -d "$d" -o run --output-format csv -- python "$ROOT/bench.py" --steps 20 --warmup 5 --cpu-baseline off \
+                 --dropin off --mapping off --configs off --unfused-leg off > "$d.log" 2>&1 ) \
+                 || { echo "abfisher $t failed"; tail -20 "$d.log"; exit 1; }
+             python - "$d" $t $r <<'PY' | tee -a "$OUT/abfisher.txt"
+import csv, glob, json, sys
+f = glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)[0]
+ks = {r["Name"].split("(")[0].split("<")[0].split("::")[-1]: float(r["AverageNs"]) / 1000 for r in csv.DictReader(open(f))}
+d = json.loads([l for l in open(sys.argv[1] + ".log") if l.startswith("{")][-1])
+print("abfisher", sys.argv[2], "round", sys.argv[3], "poses/s", d["fisher"]["value"], " ".join(
+    f"{k} {ks[k]:.2f}" for k in ("gauss_mpack_kernel", "render_bwd_fisher_kernel", "gauss_bwd_fisher_kernel") if k in ks))
 PY
            done
          done ;;
