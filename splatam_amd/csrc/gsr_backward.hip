@@ -760,14 +760,11 @@ hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint6
 // SHL: per-lane SH chain (g.shs may be set).  Without it (colours precomputed, or SH handled by
 // the staged sh_bwd_kernel) g.shs is NULL at compile time, and the 48-float dsh array and the SH
 // chain drop out of the kernel (mapping variant: 142 -> fewer VGPRs, more waves per SIMD).
-#ifndef GSR_GB_WAVES5
-#define GSR_GB_WAVES5 0  // timing experiment: gauss_bwd capped at 5 waves per SIMD
-#endif
+// at most 5 waves per SIMD: at 78-80 VGPRs the kernel would run 6, and the sixth wave measured slower for the
+// mapping variant (1 M anisotropic Gaussians: 65.0 -> 64.0 us capped) and no faster for tracking
+// (profiles/r5z_ab_gauss_bwd_waves.txt)
 template <bool POSE, bool SHL>
-__global__ void __launch_bounds__(256)
-#if GSR_GB_WAVES5
-__attribute__((amdgpu_waves_per_eu(1, 5)))
-#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 5)))
 gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float* __restrict__ inst,
                  RecLayout rec, GradsOut out, BwdGuard guard, PoseFuse pf) {
     if constexpr (!SHL) {
