@@ -104,6 +104,34 @@ static inline real rmax(real a, real b) { return a > b ? a : b; }
 #define RPOW(x, p) powf((x), (p))
 #endif
 
+/* forward.cu:341,349 / backward.cu:681-684: power = -0.5 (A dx^2 + C dy^2) - B dx dy, G = exp(power).
+ * GSR_ORACLE_ALPHA_FORM (float32 experiment builds only, tools/alpha_forms.py; never the oracle the tests
+ * use) evaluates it the way a GPU render-record variant does instead: the conic prescaled by -log2(e)/2,
+ * -log2(e) in float, power as log2(e) * power in the variant's FMA order, G = exp2f. */
+#if defined(GSR_ORACLE_ALPHA_FORM) && !defined(REAL_IS_DOUBLE)
+static inline float alpha_power(const float* co, float dx, float dy)
+{
+    const float l2e = 1.4426950408889634f, kac = -0.5f * l2e, kb = -l2e;
+    const float A = kac * co[0], B = kb * co[1], C = kac * co[2];
+    (void)A; (void)B; (void)C;
+#if GSR_ORACLE_ALPHA_FORM == 1 /* dx (A' dx + B' dy) + C' dy^2 */
+    return fmaf(fmaf(B, dy, A * dx), dx, (C * dy) * dy);
+#elif GSR_ORACLE_ALPHA_FORM == 3 /* (B' dx) dy + (A' dx dx + C' dy dy) */
+    return fmaf(B * dx, dy, fmaf(A * dx, dx, (C * dy) * dy));
+#elif GSR_ORACLE_ALPHA_FORM == 5 /* the reference order with the exact -1/2 folded, times log2(e) */
+    const float a = -0.5f * co[0], c = -0.5f * co[2], b = -co[1];
+    return (((a * dx) * dx + (c * dy) * dy) + (b * dx) * dy) * l2e;
+#else
+#error unknown GSR_ORACLE_ALPHA_FORM
+#endif
+}
+#define POWER_OF(co, dx, dy) alpha_power((co), (dx), (dy))
+#define GEXP(p) exp2f(p)
+#else
+#define POWER_OF(co, dx, dy) ((real)-0.5 * ((co)[0] * (dx) * (dx) + (co)[2] * (dy) * (dy)) - (co)[1] * (dx) * (dy))
+#define GEXP(p) REXP(p)
+#endif
+
 /* auxiliary.h:41-44: evaluated in double because of the 1.0 / 0.5 literals */
 static inline real ndc2pix(real v, int S) { return (real)((((double)v + 1.0) * S - 1.0) * 0.5); }
 
@@ -353,9 +381,9 @@ static long long render_tile(const oracle_in* in, oracle_fwd_out* o, int tx, int
                 int g = o->point_list[k];
                 real dx = o->means2D[2 * g] - (real)px, dy = o->means2D[2 * g + 1] - (real)py;
                 const real* co = o->conic_opacity + 4 * g;
-                real power = (real)-0.5 * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                real power = POWER_OF(co, dx, dy);
                 if (power > (real)0) continue;
-                real alpha = rmin((real)0.99, co[3] * REXP(power));
+                real alpha = rmin((real)0.99, co[3] * GEXP(power));
                 if (fabs((double)alpha * 255.0 - 1.0) <= ALPHA_BAND) near = 1;
                 if (alpha < (real)1 / (real)255) continue;
                 real test_T = T * ((real)1 - alpha);
@@ -718,9 +746,9 @@ int oracle_backward(const oracle_in* in, const oracle_fwd_out* fo, const real* d
                         int g = fo->point_list[k];
                         real dx = fo->means2D[2 * g] - (real)px, dy = fo->means2D[2 * g + 1] - (real)py;
                         const real* co = fo->conic_opacity + 4 * g;
-                        real power_ = (real)-0.5 * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                        real power_ = POWER_OF(co, dx, dy);
                         if (power_ > (real)0) continue;
-                        real G = REXP(power_);
+                        real G = GEXP(power_);
                         real alpha = rmin((real)0.99, co[3] * G);
                         if (alpha < (real)1 / (real)255) continue;
                         ct++;

@@ -183,11 +183,12 @@ def check_grad_accuracy(gpu_grads, ref32, ref64, stable):
     relative L2 error against float64 is at most max(1e-4, 2x) the float32 oracle's, over all
     Gaussians and over the stable ones; per element (stable Gaussians, away from every alpha / T /
     clamp threshold), the 99.99 % quantile of r is at most max(2e-3, 3x) the float32 oracle's, no
-    element exceeds r = max(0.1, 3x the float32 oracle's maximum), and at most max(10, 3x the
-    oracle's) elements exceed r = 1e-3.  (r is relative to the element's float32 error scale: a
-    float32 rasterizer whose exp / conic rounding differs from the oracle's moves the few
-    cancellation-dominated elements by a fraction of that scale -- config 4's dscales: 0.127 with the
-    round-4 p2 evaluation order, against the float32 oracle's own 0.051.)
+    element exceeds r = 0.1, and at most max(10, 3x the oracle's) elements exceed r = 1e-3.  (r is
+    relative to the element's float32 error scale; the fixed 0.1 is a tenth of it.  The worst element
+    is a cancellation-dominated near-zero gradient whose r moves with any ulp of the alpha arithmetic:
+    config 4's dscales[553617, 0] = -2.9e-9 at a scale of 2.9e-8 reads 0.05-0.32 across float32
+    evaluation orders of forward.cu:341; the reference-order float32 oracle itself reads 0.05 on the GPU
+    box's host and 0.18 in the build container -- tools/alpha_forms.py, profiles/r7_alpha_forms_cpu.txt.)
     Returns (gpu stats, oracle stats); raises AssertionError with both on failure."""
     g = grad_accuracy(gpu_grads, ref64, stable)
     o = grad_accuracy({k: ref32[k].reshape(v.shape) for k, v in gpu_grads.items() if k in ref32}, ref64, stable)
@@ -201,7 +202,7 @@ def check_grad_accuracy(gpu_grads, ref32, ref64, stable):
             why.append("rel_l2_stable")
         if a["q9999"] > max(2e-3, 3 * b["q9999"]):
             why.append("q9999")
-        if a["max"] > max(0.1, 3 * b["max"]):
+        if a["max"] > 0.1:
             why.append("max")
         if a["n_over_1e3"] > max(10, 3 * b["n_over_1e3"]):
             why.append("n_over_1e3")

@@ -53,6 +53,8 @@ def _lib(dtype):
     if key not in _libs:
         name = {"float32": "libgsr_oracle_f32.so", "float64": "libgsr_oracle_f64.so"}[key]
         path = os.path.join(_BUILD, name)
+        if key == "float32" and os.environ.get("GSR_ORACLE_F32_LIB"):  # tools/alpha_forms.py experiment builds
+            path = os.environ["GSR_ORACLE_F32_LIB"]
         if not os.path.exists(path):
             build()
         lib = ctypes.CDLL(path)

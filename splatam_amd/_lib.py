@@ -1,7 +1,9 @@
 """Loads libgsr.so (the C ABI of include/gsr.h) with ctypes.
 
 Fails loudly: there is no CPU or eager-PyTorch fallback for the rasterizer.
-Set GSR_LIB to load a library from another path.
+Set GSR_LIB to load a library from another path (same strict symbol / ABI checks).  GSR_LIB_AB=1 in
+addition relaxes them for an A/B baseline built from an older revision (build.build_from_rev): entry
+points added since that revision may be absent and ABI versions 4 / 5 are accepted.
 """
 from __future__ import annotations
 
@@ -166,7 +168,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         raise ImportError(f"libgsr.so not found at {path}: build it with `python -m splatam_amd.build` "
                           "(no CPU fallback exists for the rasterizer)")
     lib = ctypes.CDLL(path)
-    ab = bool(os.environ.get("GSR_LIB"))  # an A/B baseline built from an older revision (build.build_from_rev)
+    # an A/B baseline built from an older revision (build.build_from_rev): explicit opt-in only
+    ab = os.environ.get("GSR_LIB_AB") == "1" and bool(os.environ.get("GSR_LIB"))
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name, None)
         if fn is None:

@@ -109,33 +109,37 @@ def build_from_rev(rev: str, tag: str) -> str:
     """A/B baseline without macros in the sources: libgsr built from the csrc/ and include/ trees of git
     revision `rev` (exported to a scratch directory) into splatam_amd/_diag/libgsr_<tag>.so, which
     tools/gpu_round.sh's ab= / abbench= steps load through GSR_LIB."""
+    import io
+    import tarfile
     import tempfile
     work = tempfile.mkdtemp(prefix=f"gsr_{tag}_")
-    for sub in ("splatam_amd/csrc", "include"):
-        r = subprocess.run(f"git -C {ROOT} archive {rev} {sub} | tar -x -C {work}", shell=True,
+    try:
+        for sub in ("splatam_amd/csrc", "include"):
+            r = subprocess.run(["git", "-C", ROOT, "archive", rev, sub], capture_output=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"git archive {rev} {sub} failed: {r.stderr.decode(errors='replace')}")
+            with tarfile.open(fileobj=io.BytesIO(r.stdout)) as tf:
+                tf.extractall(work)
+        csrc, inc = os.path.join(work, "splatam_amd", "csrc"), os.path.join(work, "include")
+        objs = []
+        for src in SOURCES:
+            obj = os.path.join(work, os.path.splitext(src)[0] + ".o")
+            base = flags()
+            base = [f for i, f in enumerate(base) if f != "-I" and (i == 0 or base[i - 1] != "-I")]  # (drop -I pairs)
+            cmd = [hipcc(), *base, "-I", inc, "-I", csrc, "-c", os.path.join(csrc, src), "-o", obj]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed for {src} at {rev}:\n{r.stderr}")
+            objs.append(obj)
+        os.makedirs(DIAG, exist_ok=True)
+        lib = os.path.join(DIAG, f"libgsr_{tag}.so")
+        r = subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs],
                            capture_output=True, text=True)
         if r.returncode != 0:
-            raise RuntimeError(f"git archive {rev} {sub} failed: {r.stderr}")
-    csrc, inc = os.path.join(work, "splatam_amd", "csrc"), os.path.join(work, "include")
-    objs = []
-    for src in SOURCES:
-        obj = os.path.join(work, os.path.splitext(src)[0] + ".o")
-        base = flags()
-        base = [f for i, f in enumerate(base) if f != "-I" and (i == 0 or base[i - 1] != "-I")]  # (drop -I pairs)
-        cmd = [hipcc(), *base, "-I", inc, "-I", csrc, "-c", os.path.join(csrc, src), "-o", obj]
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"hipcc failed for {src} at {rev}:\n{r.stderr}")
-        objs.append(obj)
-    os.makedirs(DIAG, exist_ok=True)
-    lib = os.path.join(DIAG, f"libgsr_{tag}.so")
-    r = subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs],
-                       capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"link failed:\n{r.stderr}")
-    shutil.rmtree(work, ignore_errors=True)
-    return lib
-
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+        return lib
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
 
 if __name__ == "__main__":
     if "--from-rev" in sys.argv:  # python -m splatam_amd.build --from-rev REV TAG

@@ -686,7 +686,12 @@ render_track_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __
     float grad[4];
     // (the loss arrival stays here: moved after the backward it put the last workgroup's sum at the kernel's
     // end, within noise or 0.5 us slower: profiles/r4o_ab_l1_defer.txt)
-    fwd_epilogue<true, true, false>(cam, tile, f, final_T, n_contrib, out_color, out_color2, out_depth, l1, grad);
+    // STORE_GRADS = false: the gradient images are not formed here, and the C entry passes l1.dL_dim /
+    // l1.dL_dds as NULL (a variant that stores them needs real image pointers from gsr_capi.hip)
+    constexpr bool kStoreGrads = false;
+    static_assert(!kStoreGrads, "render_track_kernel's callers pass no gradient images");
+    fwd_epilogue<true, true, kStoreGrads>(cam, tile, f, final_T, n_contrib, out_color, out_color2, out_depth, l1,
+                                          grad);
     __syncthreads();  // the forward's LDS (and its sorted point_list stores) before the backward reuses them
     const BwdPix pin{f.T, f.last16 >> 4, grad[0], grad[1], grad[2], grad[3], 0.f, 0.f};
     Camera cb = cam;

@@ -411,6 +411,13 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     if (P == 0) {  // rasterize_points.cu:67-81: zero outputs, forward not run (the sticky status keeps its rows)
         void* bin = obtain(alloc, alloc_ctx, GSR_BUF_BINNING, BinLayout::make(0, W, H).total);
         if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
+        if (l1) {  // the zero silhouette masks every pixel: loss 0 and zero gradient images, as get_loss gives
+            const size_t img3 = sizeof(float) * 3 * (size_t)W * H;
+            if ((e = zero_async(l1->loss, sizeof(float), stream)) != hipSuccess ||
+                (l1->dL_dim && (e = zero_async(l1->dL_dim, img3, stream)) != hipSuccess) ||
+                (l1->dL_dds && (e = zero_async(l1->dL_dds, img3, stream)) != hipSuccess))
+                return hip_fail(e, "zero loss");
+        }
         if (no_images) return 0;
         if ((e = zero_async(out_color, sizeof(float) * 3 * (size_t)W * H, stream)) != hipSuccess ||
             (e = zero_async(out_depth, sizeof(float) * (size_t)W * H, stream)) != hipSuccess ||
@@ -541,7 +548,8 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     int rc = validate(settings, gaussians, false);
     if (dl2_channels != 1 && dl2_channels != 3) return fail(GSR_ERR_INVALID_ARG, "dl2_channels must be 1 or 3");
     if (rc != GSR_OK) return rc;
-    if (colors2 && !dL_dout_color2) return fail(GSR_ERR_INVALID_ARG, "dual backward needs dL_dout_color2");
+    // (with pre-formed records -- the fused tracking render's -- the gradient images are not read)
+    if (colors2 && !dL_dout_color2 && !pre_inst) return fail(GSR_ERR_INVALID_ARG, "dual backward needs dL_dout_color2");
     if (colors2 && power != 1) return fail(GSR_ERR_INVALID_ARG, "dual render supports backward_power == 1 only");
     if (!grads) return fail(GSR_ERR_INVALID_ARG, "grads required");
     if (num_rendered < 0) return fail(GSR_ERR_INVALID_ARG, "num_rendered must be >= 0");
@@ -552,7 +560,7 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
         return fail(GSR_ERR_INVALID_ARG, "sh_adam needs staged SH colours (M == (D+1)^2) and power 1");
     const int P = g.P;
     if (P == 0) return GSR_OK;
-    if (!geom_buffer || !image_buffer || !radii || !dL_dout_color)
+    if (!geom_buffer || !image_buffer || !radii || (!dL_dout_color && !pre_inst))
         return fail(GSR_ERR_INVALID_ARG, "missing forward state");
     // the forward's render schedule (a permutation of the tiles; any order gives the same results)
     cam.tile_order = (const uint32_t*)((const char*)image_buffer + ImgLayout::make(cam.W, cam.H).order);
@@ -788,8 +796,8 @@ int gsr_track_forward_backward_dual_static_xf(const gsr_settings* settings, cons
     // pointers to them are never dereferenced.  out_color, out_color2 and out_depth all NULL: the rendered
     // images (and final_T / n_contrib / the block maxima of the image buffer) are not stored either
     return track_forward_xf(settings, gaussians, colors2, xform, capacity, status, out_color, out_color2, out_depth,
-                            radii, gt_im, gt_depth, sil_thres, w_im, w_depth, dL_dloss, loss, loss, loss, scratch,
-                            alloc, alloc_ctx, stream, inst_records);
+                            radii, gt_im, gt_depth, sil_thres, w_im, w_depth, dL_dloss, loss, nullptr, nullptr,
+                            scratch, alloc, alloc_ctx, stream, inst_records);
 }
 
 static int track_forward_xf(const gsr_settings* settings, const gsr_gaussians* gaussians, float* colors2,
@@ -810,7 +818,8 @@ static int track_forward_xf(const gsr_settings* settings, const gsr_gaussians* g
         return fail(GSR_ERR_INVALID_ARG, "track_forward_dual_static_xf: precomputed colours, scales / rotations only");
     if (!colors2) return fail(GSR_ERR_INVALID_ARG, "colors2 required");
     if (capacity <= 0 || !status) return fail(GSR_ERR_INVALID_ARG, "static mode needs capacity > 0 and status");
-    if (!gt_im || !gt_depth || !dL_dloss || !loss || !dL_dim || !dL_ddepth_sil || !scratch)
+    // (the fused forward + backward, inst_records set, forms no gradient images: dL_dim / dL_ddepth_sil NULL)
+    if (!gt_im || !gt_depth || !dL_dloss || !loss || (!inst_records && (!dL_dim || !dL_ddepth_sil)) || !scratch)
         return fail(GSR_ERR_INVALID_ARG, "track_forward_dual_static_xf: null pointer");
     TrackXf xf;
     xf.mw = x.means_world; xf.ur = x.unnorm_rot; xf.lo = x.logit_opac; xf.ls = x.log_scales;
@@ -856,7 +865,7 @@ int gsr_track_backward_dual_records(const gsr_settings* settings, const gsr_gaus
                                     const float* inst_records, gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
     if (!inst_records) return fail(GSR_ERR_INVALID_ARG, "track_backward_dual_records: null records");
     // (the gradient images are not read: the records already hold the render backward's sums)
-    return track_backward(settings, gaussians, radii, colors2, scratch, scratch, num_rendered, geom_buffer,
+    return track_backward(settings, gaussians, radii, colors2, nullptr, nullptr, num_rendered, geom_buffer,
                           binning_buffer, image_buffer, means_world, unnorm_rot, scale_cols, cam_q, cam_t, q_stride,
                           w2c, lr_q, lr_t, beta1, beta2, eps, adam_state, dL_dcam_q, dL_dcam_t, scratch, track,
                           log_scales, alloc, alloc_ctx, stream, inst_records);

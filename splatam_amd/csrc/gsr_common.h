@@ -435,13 +435,16 @@ __device__ __forceinline__ v2f pix_delta(float4 sa, v2f pix) {
 #pragma clang fp contract(off)
     return v2f{sa.x, sa.y} - pix;
 }
-// p2 = dx (A' dx + B' dy) + C' dy^2: one packed multiply and three single ops (v_pk_mul, 2 fma, mul)
-// after the packed delta; the forward and the backward evaluate the same expression, so their
-// alpha decisions agree bit for bit.
+// p2 = (A' dx) dx + (C' dy) dy, then + (B' dx) dy: forward.cu:341's order (the two square terms, of one
+// sign, summed first; the cross term last), as FMAs on the packed (A' dx, C' dy).  The forward and the
+// backward evaluate the same expression, so their alpha decisions agree bit for bit.  (Round 4 evaluated
+// dx (A' dx + B' dy) + C' dy^2, one VALU less; its per-element gradient errors moved away from the
+// float32 reference arithmetic's: config 4's worst dscales element 0.127 of its float32 error scale against
+// 0.05 -- tools/alpha_forms.py replays both orders in the CPU oracle, profiles/r7_alpha_forms_cpu.txt.)
 __device__ __forceinline__ float eval_p2(float4 sa, float4 sb, v2f d) {
 #pragma clang fp contract(off)
     const v2f t = v2f{sa.z, sa.w} * d;  // (A' dx, C' dy)
-    return __builtin_fmaf(__builtin_fmaf(sb.x, d.y, t.x), d.x, t.y * d.y);
+    return __builtin_fmaf(sb.x * d.x, d.y, __builtin_fmaf(t.x, d.x, t.y * d.y));
 }
 
 // Pixel of thread tid within its 16x16 tile: wave w covers the 8x8 quadrant

@@ -95,7 +95,9 @@ def test_fisher_selective_path(cuda, power, aniso, bg):
         r_full = harness.rel_l2(sel["grads"][k], full["grads"][k])
         r_ref = harness.rel_l2(sel["grads"][k], ref[k].reshape(sel["grads"][k].shape))
         print(f"power {power} {k}: rel L2 vs full path {r_full:.2e}, vs oracle {r_ref:.2e}")
-        assert r_full <= 2e-5, (k, r_full)  # (power 2: the full path sums second moments; see config 3)
+        # power 2: the full path sums per-instance second moments (a different float order than the
+        # selective path's per-pair squares); other powers take the per-pair powf path on both sides
+        assert r_full <= (2e-5 if power == 2 else 2e-6), (k, r_full)
         assert r_ref <= 1e-4, (k, r_ref)
     if power % 2 == 0:
         assert (sel["grads"]["dmeans3D"] >= 0).all() and (sel["grads"]["dopacity"] >= 0).all()

@@ -26,6 +26,9 @@
 #   abprof=TAGS      interleaved A/B (two rounds) of rocprofv3 kernel-trace averages of the headline bench's
 #                    tracking kernels between libgsr.so and each _diag/libgsr_<tag>.so
 #   abfisher=TAGS    interleaved A/B (two rounds) of the Fisher leg: poses/s and its kernels' rocprofv3 averages
+#   configs          tests/test_gpu_configs.py with -s (per-config parity statistics in configs.log)
+#   drv              the driver's bench command (--steps 20 --warmup 5) and 100/10, interleaved, two rounds
+#   drift            per-launch render_track durations over 5 frames of 40 iterations (tools/drift.py)
 #   abflag=FLAG:V1,V2[,...]  interleaved A/B (two rounds) of the light bench line over the values of one bench.py
 #                    flag, e.g. abflag=--fuse-render:1,0
 TAG=${1:-x}; shift
@@ -87,7 +90,7 @@ for s in "$@"; do
             for t in base ${TAGS//,/ }; do
               for c in ${MODES//,/ }; do
                 m=${c%%:*}; cf=${c##*:}; f="$OUT/ab_${t}_${m}_${cf}_$r.json"
-                GSR_LIB=$(lib_of $t) timeout -k 10 120 python tools/raster_bench.py --iters 60 --mode $m --config $cf \
+                GSR_LIB_AB=1 GSR_LIB=$(lib_of $t) timeout -k 10 120 python tools/raster_bench.py --iters 60 --mode $m --config $cf \
                     > "$f" 2>&1 || { echo "ab $t $c failed"; tail -5 "$f"; exit 1; }
                 python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['stages_us']; print('ab', sys.argv[2], sys.argv[3], 'round', sys.argv[4], 'preprocess', s['preprocess'], 'duplicate', s['duplicate'], 'render_fwd', s['render_fwd'], 'render_bwd', s['render_bwd'], 'gauss_bwd', s['gauss_bwd'], 'ms', round(d['ms_per_frame'], 4))" "$f" $t $c $r | tee -a "$OUT/ab.txt"
               done
@@ -98,7 +101,7 @@ for s in "$@"; do
            L="base ${TAGS//,/ }"; [ $r = 2 ] && L="$(echo $L | tr ' ' '\n' | tac | tr '\n' ' ')"
            for t in $L; do
              d="$OUT/abprof_${t}_$r"
-             ( cd /tmp && export TMPDIR=/tmp && GSR_LIB=$(lib_of $t) timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+             ( cd /tmp && export TMPDIR=/tmp && GSR_LIB_AB=1 GSR_LIB=$(lib_of $t) timeout -k 10 300 rocprofv3 --kernel-trace --stats \
                  -d "$d" -o run --output-format csv -- python "$ROOT/bench.py" --steps 40 --warmup 20 $LIGHT \
                  > "$d.log" 2>&1 ) || { echo "abprof $t failed"; tail -20 "$d.log"; exit 1; }
              python - "$d" $t $r <<'PY' | tee -a "$OUT/abprof.txt"
@@ -117,7 +120,7 @@ PY
            L="base ${TAGS//,/ }"; [ $r = 2 ] && L="$(echo $L | tr ' ' '\n' | tac | tr '\n' ' ')"
            for t in $L; do
              d="$OUT/abfisher_${t}_$r"
-             ( cd /tmp && export TMPDIR=/tmp && GSR_LIB=$(lib_of $t) timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+             ( cd /tmp && export TMPDIR=/tmp && GSR_LIB_AB=1 GSR_LIB=$(lib_of $t) timeout -k 10 300 rocprofv3 --kernel-trace --stats \
                  -d "$d" -o run --output-format csv -- python "$ROOT/bench.py" --steps 20 --warmup 5 --cpu-baseline off \
                  --dropin off --mapping off --configs off --unfused-leg off > "$d.log" 2>&1 ) \
                  || { echo "abfisher $t failed"; tail -20 "$d.log"; exit 1; }
@@ -137,7 +140,7 @@ PY
             [ $r = 2 ] && ORDER=$(echo $ORDER | tr ' ' '\n' | tac | tr '\n' ' ')  # round 2 in reverse order
             for t in $ORDER; do
               f="$OUT/abbench_${t}_$r.log"
-              GSR_LIB=$(lib_of $t) timeout -k 10 300 python bench.py --cpu-baseline off --dropin off --fisher off \
+              GSR_LIB_AB=1 GSR_LIB=$(lib_of $t) timeout -k 10 300 python bench.py --cpu-baseline off --dropin off --fisher off \
                   --configs off --unfused-leg off > "$f" 2>&1 || { echo "abbench $t failed"; tail -20 "$f"; exit 1; }
               python - "$f" $t $r <<'PY' | tee -a "$OUT/abbench.txt"
 import json, sys
@@ -160,6 +163,25 @@ print("abflag", sys.argv[2], "round", sys.argv[3], "frames/s", b["value"], "kern
 PY
             done
           done ;;
+    configs) timeout -k 10 900 python -u -m pytest tests/test_gpu_configs.py -s -v -m gpu --timeout 400 \
+             --timeout-method thread > "$OUT/configs.log" 2>&1 || { echo "configs failed"; tail -40 "$OUT/configs.log"; exit 1; } ;;
+    drv) for r in 1 2; do  # the driver's own bench command against the builder's 100/10 runs, interleaved
+           for sw in "20 5" "100 10"; do
+             set -- $sw; f="$OUT/drv_s$1_w$2_$r.log"
+             timeout -k 10 300 python bench.py --gpus 1 --steps $1 --warmup $2 > "$f" 2>&1 \
+               || { echo "drv $sw failed"; tail -20 "$f"; exit 1; }
+             python - "$f" "$1/$2" $r <<'PY' | tee -a "$OUT/drv.txt"
+import json, sys
+b = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][-1]
+print("drv steps/warmup", sys.argv[2], "round", sys.argv[3], "frames/s", b["value"], "kernel_us", b["roofline"]["avg_us"],
+      "launches", b["roofline"].get("launches_timed"))
+PY
+           done
+         done ;;
+    drift) ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/drift" -o run \
+             --output-format csv -- python "$ROOT/bench.py" --steps 200 --warmup 5 $LIGHT > "$OUT/drift.log" 2>&1 ) \
+             || { echo "drift failed"; tail -20 "$OUT/drift.log"; exit 1; }
+           python tools/drift.py "$OUT/drift" --skip 25 | tee "$OUT/drift.txt" ;;
     *) echo "unknown step $s"; exit 1 ;;
   esac
   echo "step $s ok"
