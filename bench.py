@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=("auto", "on", "off"), default="auto")
     ap.add_argument("--graph", type=int, default=1, help="1: replay the tracking iterations as a HIP graph")
     ap.add_argument("--iters-per-graph", type=int, default=20)
+    ap.add_argument("--settle-ms", type=float, default=50.0,
+                    help="tracking: untimed priming replays (undone) until this much wall time has passed, so "
+                         "the timed region does not start on the GPU's clock ramp (0: one priming replay)")
     ap.add_argument("--frame-iters", type=int, default=40,
                     help="tracking iterations per frame (configs/replica/splatam.py:15); the timed loop runs whole "
                          "frames: fresh optimizer, replays, best-candidate pose written back")
@@ -174,7 +177,8 @@ def main():
         # warm-up: W eager tracking iterations plus one priming replay, all undone (pose restored,
         # optimizer reset) before the timed frames
         tracker = GraphTracker(params, curr, frame, iters_per_graph=S, timing=bool(args.timing),
-                               fuse_pose=bool(args.fuse_pose), warmup_iters=max(1, args.warmup), prime=True)
+                               fuse_pose=bool(args.fuse_pose), warmup_iters=max(1, args.warmup), prime=True,
+                               prime_ms=args.settle_ms)
     else:
         for _ in range(args.warmup):
             step()
@@ -362,8 +366,10 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "execution": (f"{steps} timed tracking iterations in frames of up to {FI} (fresh optimizer per "
                           f"frame, best-candidate pose written back): HIP graph of {tracker.iters} iterations "
-                          f"replayed {-(-steps // tracker.iters)}x; warm-up {args.warmup} eager iterations + one "
-                          f"priming replay, undone; binning capacity {tracker.capacity}, no overflow"
+                          f"replayed {-(-steps // tracker.iters)}x; warm-up {args.warmup} eager iterations + "
+                          f"{tracker.prime_replays} priming replays ({tracker.prime_ms:.0f} ms: graph upload and "
+                          f"GPU clock settle, --settle-ms {args.settle_ms:g}), undone; binning capacity "
+                          f"{tracker.capacity}, no overflow"
                           if tracker is not None else "eager"),
             "data": "synthetic (SURVEY.md 8(d) seeded scene; targets rendered at the unperturbed pose)",
             "config": {"workload": f"config {args.config}: {P} isotropic Gaussians, {W}x{H}, SplaTAM tracking "

@@ -60,7 +60,7 @@ class GraphTracker:
     def __init__(self, params: dict, curr_data: dict, time_idx: int, iters_per_graph: int = 20,
                  cfg: TrackingConfig = TrackingConfig(), lrs=(0.0004, 0.002), headroom: float = 1.5,
                  warmup_iters: int = 3, min_extra: int = 65536, timing: bool = False, fuse_pose: bool = False,
-                 prime: bool = False):
+                 prime: bool = False, prime_ms: float = 0.0):
         if not fused_eligible(params, curr_data, cfg):
             raise RuntimeError("GraphTracker needs the fused tracking configuration (only the pose requires grad)")
         self.params, self.curr, self.t, self.cfg = params, curr_data, time_idx, cfg
@@ -104,8 +104,21 @@ class GraphTracker:
         with torch.cuda.graph(self.graph, stream=side):  # capture on the warm-up stream (autograd nodes live there)
             for k in range(self.iters):
                 self.loss = self._iteration(k)
+        self.prime_replays, self.prime_ms = 0, 0.0
         if prime:  # one replay (graph upload, first-launch costs), undone like the warm-up iterations
-            self.graph.replay()
+            # prime_ms: further replays until that much wall time has passed since the first one -- the
+            # GPU's clock ramps up over the first ~25 ms of sustained work (GRBM_COUNT per microsecond of the
+            # fused render rises ~9 % over its first ~50 launches, profiles/r7c_clk.txt), so a short timed
+            # region right behind a short warm-up would time the ramp, not the kernel
+            import time
+            t0p = time.perf_counter()
+            while True:
+                self.graph.replay()
+                self.prime_replays += 1
+                torch.cuda.synchronize(dev)
+                self.prime_ms = 1000.0 * (time.perf_counter() - t0p)
+                if self.prime_ms >= prime_ms:
+                    break
             with torch.no_grad():
                 rots[..., time_idx] = q0
                 trans[..., time_idx] = t0

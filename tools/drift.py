@@ -6,6 +6,9 @@ ramping: later frames faster at the same iteration index).
     python tools/drift.py TRACE_DIR [--kernel render_track] [--frame-iters 40] [--skip N]
 
 --skip: launches before the timed region (eager warm-up iterations + the priming replay).
+--counters: the trace is a rocprofv3 --pmc GRBM_COUNT GRBM_GUI_ACTIVE pass (counter_collection.csv, one row
+per dispatch and counter): also prints GRBM_COUNT / duration per frame, the GPU clock the launch ran at
+(summed over the XCDs' GRBM instances, so in units of MHz x instances; the trend is what matters).
 """
 from __future__ import annotations
 
@@ -21,13 +24,30 @@ def main():
     ap.add_argument("--kernel", default="render_track")
     ap.add_argument("--frame-iters", type=int, default=40)
     ap.add_argument("--skip", type=int, default=0)
+    ap.add_argument("--counters", action="store_true")
     a = ap.parse_args()
-    f = glob.glob(a.trace_dir + "/**/*kernel_trace.csv", recursive=True)[0]
-    rows = [r for r in csv.DictReader(open(f)) if a.kernel in r["Kernel_Name"]]
+    cnt = {}
+    if a.counters:
+        f = glob.glob(a.trace_dir + "/**/*counter_collection.csv", recursive=True)[0]
+        by = {}
+        for r in csv.DictReader(open(f)):
+            if a.kernel in r["Kernel_Name"]:
+                by.setdefault(r["Dispatch_Id"], dict(r))[r["Counter_Name"]] = float(r["Counter_Value"])
+        rows = list(by.values())
+    else:
+        f = glob.glob(a.trace_dir + "/**/*kernel_trace.csv", recursive=True)[0]
+        rows = [r for r in csv.DictReader(open(f)) if a.kernel in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000 for r in rows]
     t = [(int(r["Start_Timestamp"]) - int(rows[0]["Start_Timestamp"])) / 1e6 for r in rows]
     print(f"{len(d)} launches of {a.kernel}; untimed (skipped) {a.skip}: mean {statistics.mean(d[:a.skip]) if a.skip else 0:.2f} us")
+    if a.counters:
+        mhz = [r.get("GRBM_COUNT", 0.0) / x for r, x in zip(rows, d)]
+        busy = [r.get("GRBM_GUI_ACTIVE", 0.0) / max(r.get("GRBM_COUNT", 1.0), 1.0) for r in rows]
+        print("GRBM_COUNT / us by launch (untimed then timed, 5-launch means):",
+              " ".join(f"{statistics.mean(mhz[i:i + 5]):.0f}" for i in range(0, len(mhz), 5)))
+        print("GRBM_GUI_ACTIVE / GRBM_COUNT (5-launch means):",
+              " ".join(f"{statistics.mean(busy[i:i + 5]):.3f}" for i in range(0, len(busy), 5)))
     d, t = d[a.skip:], t[a.skip:]
     FI = a.frame_iters
     nf = len(d) // FI

@@ -29,6 +29,7 @@
 #   configs          tests/test_gpu_configs.py with -s (per-config parity statistics in configs.log)
 #   drv              the driver's bench command (--steps 20 --warmup 5) and 100/10, interleaved, two rounds
 #   drift            per-launch render_track durations over 5 frames of 40 iterations (tools/drift.py)
+#   clk              GRBM_COUNT / GRBM_GUI_ACTIVE per render_track launch over the drift run (clock per launch)
 #   abflag=FLAG:V1,V2[,...]  interleaved A/B (two rounds) of the light bench line over the values of one bench.py
 #                    flag, e.g. abflag=--fuse-render:1,0
 TAG=${1:-x}; shift
@@ -179,9 +180,14 @@ PY
            done
          done ;;
     drift) ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/drift" -o run \
-             --output-format csv -- python "$ROOT/bench.py" --steps 200 --warmup 5 $LIGHT > "$OUT/drift.log" 2>&1 ) \
+             --output-format csv -- python "$ROOT/bench.py" --steps 200 --warmup 5 --settle-ms 0 $LIGHT > "$OUT/drift.log" 2>&1 ) \
              || { echo "drift failed"; tail -20 "$OUT/drift.log"; exit 1; }
            python tools/drift.py "$OUT/drift" --skip 25 | tee "$OUT/drift.txt" ;;
+    clk) ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --pmc GRBM_COUNT GRBM_GUI_ACTIVE \
+             --kernel-include-regex render_track -T -d "$OUT/clk" -o run --output-format csv \
+             -- python "$ROOT/bench.py" --steps 200 --warmup 5 --settle-ms 0 $LIGHT > "$OUT/clk.log" 2>&1 ) \
+             || { echo "clk failed"; tail -20 "$OUT/clk.log"; exit 1; }
+         python tools/drift.py "$OUT/clk" --skip 25 --counters | tee "$OUT/clk.txt" ;;
     *) echo "unknown step $s"; exit 1 ;;
   esac
   echo "step $s ok"
