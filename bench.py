@@ -77,7 +77,11 @@ def parse():
                     help="also time the batched Fisher / EIG view scoring (backward_power 2) on the same map")
     ap.add_argument("--mapping", choices=("auto", "on", "off"), default="auto",
                     help="also time the mapping workload (config 4) into a 'mapping' object (auto: N=1 only)")
-    ap.add_argument("--mapping-steps", type=int, default=100, help="mapping leg: timed iterations")
+    ap.add_argument("--mapping-steps", type=int, default=120, help="mapping leg: timed iterations (whole frames)")
+    ap.add_argument("--map-frame-iters", type=int, default=60,
+                    help="mapping: iterations per frame = per HIP graph (configs/replica/splatam.py:16: 60)")
+    ap.add_argument("--map-prune", type=int, default=1,
+                    help="mapping: prune_gaussians inside the frame (configs/replica/splatam.py:101-111), 0: off")
     ap.add_argument("--fisher-k", type=int, default=16, help="fisher: poses per HIP-graph launch")
     ap.add_argument("--configs", choices=("auto", "on", "off"), default="auto",
                     help="BASELINE configs 1 (forward only) and 2 (fwd+bwd RGB + depth) on the GPU and the CPU "
@@ -136,7 +140,9 @@ def main():
     scene = config_scene(args.config)
     P, W, H = scene.P, scene.cam.W, scene.cam.H
     params = init_tracking_params(scene, num_frames=max(world, 1), device=dev)
-    sd.broadcast_map(params)                    # canonical Gaussian map from rank 0
+    fm = sd.FlatMap(params)                     # the map as one contiguous buffer: one collective per broadcast
+    sd.broadcast_flat(fm)                       # canonical Gaussian map from rank 0
+    bc = sd.MapBroadcaster(fm)                  # double-buffered broadcast, overlapped with the frames' replays
     frame = sd.frames_for_rank(world)[0] if world > 1 else 0  # frame sharding: rank r tracks frame r
     cam = camera_settings(scene.cam, dev)
     w2c = torch.eye(4, device=dev)
@@ -196,13 +202,15 @@ def main():
         done, f, n_bcast = 0, 0, 0
         while done < steps:
             if world > 1 and per_bcast and f % per_bcast == 0:
-                sd.broadcast_map(params)       # map update -> RCCL broadcast over xGMI
+                bc.finish()                    # the map version broadcast at the last boundary goes live
+                bc.start()                     # map update -> one RCCL broadcast over xGMI, side stream
                 n_bcast += 1
             n = min(FI, steps - done)
             tracker.track_frame(n, check=False)  # one frame: fresh optimizer, replays, best pose written back
             #   (overflow checked once after the timed loop, below)
             done += n
             f += 1
+        bc.finish()
     else:
         for i in range(steps):
             if world > 1 and args.bcast_every > 0 and i % args.bcast_every == 0:
@@ -239,7 +247,7 @@ def main():
         torch.cuda.synchronize()
         tc0 = time.perf_counter()
         for _ in range(nb):
-            sd.broadcast_map(params)
+            sd.broadcast_flat(fm)
         torch.cuda.synchronize()
         dist.barrier()
         el_b = sd.max_over_ranks(time.perf_counter() - tc0, device=dev)
@@ -247,8 +255,11 @@ def main():
             raise SystemExit("binning capacity overflow during the no-broadcast replays: measurement invalid")
         bcast_split = {"value_no_broadcast": round(frames / el_nb, 3), "ms_per_step_no_broadcast":
                        round(1000.0 * el_nb / steps, 4), "broadcast_ms": round(1000.0 * el_b / nb, 4),
-                       "broadcasts_in_timed_region": n_bcast,
-                       "broadcast_bytes": int(sum(params[k].numel() * params[k].element_size() for k in sd.MAP_KEYS))}
+                       "broadcasts_in_timed_region": n_bcast, "broadcast_bytes": int(fm.nbytes),
+                       "broadcast_path": "one RCCL broadcast of the flat map buffer (splatam_amd.dist.FlatMap) "
+                                         "per map update, on a side stream overlapped with the next frame's "
+                                         "replays (MapBroadcaster, double-buffered); broadcast_ms: the blocking "
+                                         "single call alone"}
 
     # ---- roofline of the dominant kernel (render backward) ------------------
     rb = stages["render_bwd"]
@@ -299,7 +310,7 @@ def main():
         if stream:
             roofline["peak_measured"] = {"copy_gbs": stream["copy_gbs"], "triad_gbs": stream["triad_gbs"],
                                          "source": "tools/micro/stream (1 GiB float4 streams, best of 20)"}
-    fisher = fisher_leg(args, scene, dev) if args.fisher == "on" else None
+    fisher = fisher_leg(args, scene, dev, world=world, rank=rank) if args.fisher == "on" else None
     mapping = None
     if args.mapping == "on" or (args.mapping == "auto" and world == 1):
         mapping = mapping_leg(args, dev)
@@ -639,7 +650,7 @@ def mapping_keyframes(params, cam, K, rank, dev):
     return kfs
 
 
-def dropin_mapping_leg(args, dev, iters: int = 20):
+def dropin_mapping_leg(args, dev, iters: int = 60):
     """The unchanged mapping loop (scripts/splatam.py:841-905) at config 4: every parameter an
     nn.Parameter, a fresh torch.optim.Adam per frame over every group (eps 1e-15), per iteration a random
     keyframe, the literal get_loss(mapping=True) with two diff_gaussian_rasterization.GaussianRasterizer
@@ -659,6 +670,7 @@ def dropin_mapping_leg(args, dev, iters: int = 20):
     params = as_parameters(base)
     del base
     variables = tracking_variables(P, dev)
+    variables["scene_radius"] = torch.max(kfs[0]["depth"]) / 3.0  # initialize_first_timestep (splatam.py:212)
     cfg = MappingConfig()
     rng = np.random.RandomState(0)
     map_frame_literal(params, variables, kfs, 3, cfg, renderer=dgr.GaussianRasterizer, rng=rng)  # warm-up
@@ -667,6 +679,7 @@ def dropin_mapping_leg(args, dev, iters: int = 20):
     map_frame_literal(params, variables, kfs, iters, cfg, renderer=dgr.GaussianRasterizer, rng=rng)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    survivors = int(params["means3D"].shape[0])
     del params, variables, kfs
     torch.cuda.empty_cache()
     return {"value": round(iters / dt, 3), "unit": "iterations/s", "ms_per_step": round(1000 * dt / iters, 4),
@@ -674,15 +687,21 @@ def dropin_mapping_leg(args, dev, iters: int = 20):
             "path": f"unchanged scripts/splatam.py mapping loop body at config 4 ({P} Gaussians, SH degree "
                     f"{scene.sh_degree}, {W}x{H}, {K} keyframes): literal get_loss(mapping=True) with 2x "
                     "diff_gaussian_rasterization.GaussianRasterizer, torch L1 + calc_ssim + masked depth L1, "
-                    "loss.backward(), torch.optim.Adam over every group (fresh per frame), eager; pruning and "
-                    "densification off"}
+                    "loss.backward(), prune_gaussians at iterations 0 and 20 (configs/replica/splatam.py:101-111, "
+                    "remove_points on the optimizer), torch.optim.Adam over every group (fresh per frame), eager; "
+                    f"one {iters}-iteration frame; GS densification off (the config's default)",
+            "survivors": survivors}
 
 
-def fisher_leg(args, scene, dev, launches: int = 6):
+def fisher_leg(args, scene, dev, launches: int = 6, world: int = 1, rank: int = 0):
     """Fisher / EIG view scoring (scripts/ros_handler.py:807-902) on the bench map:
     the visited-pose Hessian sum H = sum_k [dL/dmeans_cam, dL/dopacity] of backward_power=2 renders seeded
-    with 1e-3, K poses per HIP-graph launch (fisher.BatchedFisher), against the per-pose eager path."""
+    with 1e-3, K poses per HIP-graph launch (fisher.BatchedFisher), against the per-pose eager path.
+    N > 1: the visited poses shard over the ranks (rank r scores poses rK .. rK + K - 1 of the ring, weak
+    scaling) and the ranks' H sums meet in one all-reduce (compute_H_visited_inv's sum,
+    ros_handler.py:807-829), inside the timed region; value = all ranks' poses / max-over-ranks time."""
     import math
+    from splatam_amd import dist as sd
     from splatam_amd.fisher import BatchedFisher, FisherScorer
     from splatam_amd.slam import camera_settings, init_tracking_params
     params = init_tracking_params(scene, num_frames=1, device=dev)
@@ -697,16 +716,24 @@ def fisher_leg(args, scene, dev, launches: int = 6):
         w[:3, 3] = torch.tensor([0.01 * math.sin(k), 0.01 * math.cos(k), 0.0], device=dev)
         return w
 
-    poses = [pose(k) for k in range(K)]
+    poses = [pose(k + rank * K) for k in range(K)]  # this rank's share of the visited poses
     bf = BatchedFisher(sc, K, mode="sum", probe_w2cs=poses)
     bf.hessian_sum(poses)
+    H = torch.zeros_like(bf.out)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(launches):
-        if bf.hessian_sum(poses) is None:  # the default (checked) call: one host sync per launch
+        h = bf.hessian_sum(poses)  # the default (checked) call: one host sync per launch
+        if h is None:
             return {"error": "binning capacity overflow"}
+        H.add_(h)
+    sd.all_reduce_sum_(H)  # the visited-pose sum over all ranks' shares
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    dt = sd.max_over_ranks(time.perf_counter() - t0, device=dev)
     sc.hessian(poses[0])
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -715,8 +742,9 @@ def fisher_leg(args, scene, dev, launches: int = 6):
     torch.cuda.synchronize()
     de = (time.perf_counter() - t1) / 4
     dropin = fisher_dropin(params, cam, poses, dev)
-    return {"value": round(K * launches / dt, 2), "unit": "poses/s", "poses_per_launch": K,
-            "ms_per_pose": round(1000 * dt / (K * launches), 4), "eager_ms_per_pose": round(1000 * de, 4),
+    return {"value": round(K * launches * world / dt, 2), "unit": "poses/s", "poses_per_launch": K,
+            "ranks": world, "ms_per_pose": round(1000 * dt / (K * launches), 4),
+            "eager_ms_per_pose": round(1000 * de, 4),
             "dropin": dropin,
             "workload": f"H_train of {K} visited poses per HIP-graph launch over the {scene.P}-Gaussian "
                         f"{scene.cam.W}x{scene.cam.H} map: static forward + backward_power=2 per pose, "
@@ -868,10 +896,10 @@ def mapping_leg(args, dev):
     records it too: the same measurement as `--workload mapping` (rank 0, N=1 only)."""
     import copy
     a = copy.copy(args)
-    a.config, a.steps, a.warmup = 4, max(20, args.mapping_steps), 20
+    a.config, a.steps, a.warmup = 4, max(1, args.mapping_steps), args.map_frame_iters
     line = run_mapping(a, 1, 0, dev)
     keep = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "execution", "config", "roofline",
-            "stages_us")
+            "stages_us", "pruning")
     return {k: line[k] for k in keep}
 
 
@@ -898,9 +926,13 @@ def run_mapping(args, world, rank, dev):
     kfs = mapping_keyframes(params, cam, K, rank, dev)  # keyframe targets: the map with perturbed colours
     for k in ("means3D", "unnorm_rotations", "logit_opacities", "log_scales", key):
         params[k].requires_grad_(True)
-    steps = max(1, args.steps)
-    S = math.gcd(max(1, args.iters_per_graph), steps)  # exactly `steps` timed iterations, whole replays
-    mapper = GraphMapper(params, kfs, iters_per_graph=S, cfg=MappingConfig(), timing=bool(args.timing))
+    # one replay = one frame of --map-frame-iters iterations (fresh Adam, prune_gaussians at the iterations
+    # pruning_dict names: 0 and 20 of 60); exactly `steps` timed iterations, rounded up to whole frames
+    S = max(1, args.map_frame_iters)
+    steps = S * max(1, -(-max(1, args.steps) // S))
+    scene_radius = torch.max(kfs[0]["depth"]) / 3.0  # initialize_first_timestep (splatam.py:212), ratio 3 (replica)
+    mapper = GraphMapper(params, kfs, iters_per_graph=S, cfg=MappingConfig(), timing=bool(args.timing),
+                         prune=bool(args.map_prune), scene_radius=scene_radius)
     for _ in range(max(1, -(-args.warmup // S))):  # >= W untimed iterations (whole replays)
         mapper.run()  # checked: raises on an overflow
     torch.cuda.synchronize()
@@ -922,6 +954,7 @@ def run_mapping(args, world, rank, dev):
                          "measurement invalid")
     elapsed = sd.max_over_ranks(t1 - t0, device=dev)
     value = steps * world / elapsed
+    survivors = int(mapper.survivors().sum().item())
     nr = mapper.num_rendered()
     roofline = render_bwd_roofline(stages["render_bwd"], sum(nr) / len(nr), P, W, H, graph=True)
     roofline["traffic"], roofline["traffic_source"] = committed_traffic("mapping_render_bwd_pmc.json")
@@ -930,8 +963,14 @@ def run_mapping(args, world, rank, dev):
                   f"{scene.sh_degree}", "value": round(value, 3), "unit": "iterations/s", "n_gpus": world,
         "steps": steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "execution": f"HIP graph of {S} mapping iterations (one frame, fresh Adam), replayed; binning "
-                     f"capacity {mapper.capacity}, no overflow",
+        "execution": f"HIP graph of {S} mapping iterations (one frame, fresh Adam), replayed "
+                     f"{steps // S}x; binning capacity {mapper.capacity}, no overflow",
+        "pruning": ({"iterations": sorted(mapper.prune_at), "survivors": survivors, "gaussians": P,
+                     "path": "prune_gaussians inside the frame (scripts/splatam.py:876-878, configs/replica/"
+                             "splatam.py:101-111): device alive mask (gsr_map_prune), pruned Gaussians culled by "
+                             "the static forward; a pruning iteration is its loss forward only (the reference's "
+                             "optimizer.step() updates no Gaussian there: remove_points drops every .grad)"}
+                    if mapper.prune_at else None),
         "data": f"synthetic (SURVEY.md 8(d) seeded scene; {K} keyframe targets rendered from a perturbed map)",
         "config": {"workload": f"config {args.config}: {P} Gaussians, {W}x{H}, SplaTAM mapping iteration "
                                "(SH colour + depth/silhouette render fwd+bwd, L1 + SSIM + depth L1, Adam on "

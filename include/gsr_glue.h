@@ -309,6 +309,23 @@ int gsr_map_transform_bwd_adam(int P, float* means_world, float* unnorm_rot, flo
                                const float* dL_dscales, const float* dL_dcolors, const gsr_map_adam* adam,
                                void* stream);
 
+/* SplaTAM's pruning inside a captured mapping frame (prune_gaussians, utils/slam_external.py:167-188, with
+ * scripts/splatam.py:876-878 calling it between loss.backward() and optimizer.step()) without changing P:
+ *   gsr_map_prune: alive[i] (uint8, 1 = kept) is cleared where the reference's remove_points would drop
+ *     Gaussian i: sigmoid(logit_opac[i]) < opac_thr, or (remove_big) max_j exp(log_scales[i, j]) > big_thr
+ *     (big_thr = 0.1 * scene_radius as the caller's float32 tensor holds it); each value formed as torch
+ *     forms it (1 / (1 + exp(-x)), exp) so the decision is the reference's.  Already cleared entries stay.
+ *   gsr_forward_dual_static_alive: gsr_forward_dual_static (include/gsr.h) where a Gaussian with
+ *     alive[i] == 0 is culled like one behind the camera (radius 0, no instances, zero gradients); the
+ *     others' images, binning order, gradients and optimizer steps are exactly those of the compacted
+ *     set (the per-tile (depth, id) order of the survivors does not depend on the removed ids). */
+int gsr_map_prune(int P, const float* logit_opac, const float* log_scales, int scale_cols, float opac_thr,
+                  float big_thr, int remove_big, unsigned char* alive, void* stream);
+int gsr_forward_dual_static_alive(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
+                                  int capacity, unsigned* status, float* out_color, float* out_color2,
+                                  float* out_depth, int* radii, const unsigned char* alive, gsr_alloc_fn alloc,
+                                  void* alloc_ctx, void* stream);
+
 /* torch.optim.Adam (foreach implementation, no weight decay / amsgrad /
  * maximize) over up to 16 float32 tensors in one launch; every tensor shares
  * `step` (>= 1, already incremented) and has its own lr. */

@@ -335,12 +335,13 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
 
 def rasterize_gaussians_dual(background, means3D, colors, colors2, opacity, scales, rotations, scale_modifier,
                              cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh,
-                             degree, campos, prefiltered, capacity=0, status=None):
+                             degree, campos, prefiltered, capacity=0, status=None, alive=None):
     """gsr_forward_dual: rasterize_gaussians with a second precomputed colour set
     composited in the same pass.  Returns (num_rendered, color, color2, radii,
     geomBuffer, binningBuffer, imgBuffer, depth).  capacity > 0 selects
     gsr_forward_dual_static (no host synchronisation; `status` is a device int32[4]
-    receiving the counters, and num_rendered is the capacity)."""
+    receiving the counters, and num_rendered is the capacity).  alive (static mode only): a
+    device uint8 [P] mask, 0 = pruned (gsr_forward_dual_static_alive: culled, radius 0)."""
     device = means3D.device
     if device.type != "cuda":
         raise RuntimeError("splatam_amd rasterizer runs on ROCm devices only (no CPU fallback); "
@@ -363,11 +364,23 @@ def rasterize_gaussians_dual(background, means3D, colors, colors2, opacity, scal
         if capacity > 0:
             if status is None or status.device != device or status.numel() < 4:
                 raise RuntimeError("static dual forward needs a device status tensor of 4 int32")
-            n = lib.gsr_forward_dual_static(ctypes.byref(s), ctypes.byref(g), _ptr(c2), int(capacity),
-                                            status.data_ptr(), out_color.data_ptr(), out_color2.data_ptr(),
-                                            out_depth.data_ptr(), radii.data_ptr() if P else None, _ALLOC_CB, None,
-                                            _stream(device))
+            if alive is not None:
+                if alive.device != device or alive.dtype != torch.uint8 or alive.numel() != P or \
+                        not alive.is_contiguous():
+                    raise RuntimeError("alive must be a contiguous uint8 tensor of P entries on the render device")
+                n = lib.gsr_forward_dual_static_alive(ctypes.byref(s), ctypes.byref(g), _ptr(c2), int(capacity),
+                                                      status.data_ptr(), out_color.data_ptr(), out_color2.data_ptr(),
+                                                      out_depth.data_ptr(), radii.data_ptr() if P else None,
+                                                      alive.data_ptr() if P else None, _ALLOC_CB, None,
+                                                      _stream(device))
+            else:
+                n = lib.gsr_forward_dual_static(ctypes.byref(s), ctypes.byref(g), _ptr(c2), int(capacity),
+                                                status.data_ptr(), out_color.data_ptr(), out_color2.data_ptr(),
+                                                out_depth.data_ptr(), radii.data_ptr() if P else None, _ALLOC_CB,
+                                                None, _stream(device))
         else:
+            if alive is not None:
+                raise RuntimeError("the alive mask needs the static (capacity > 0) forward")
             n = lib.gsr_forward_dual(ctypes.byref(s), ctypes.byref(g), _ptr(c2), out_color.data_ptr(),
                                      out_color2.data_ptr(), out_depth.data_ptr(), radii.data_ptr() if P else None,
                                      _ALLOC_CB, None, _stream(device))

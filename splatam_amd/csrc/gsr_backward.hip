@@ -410,9 +410,14 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
         const int jmin[4] = {hi - rm[0], hi - rm[1], hi - rm[2], hi - rm[3]};
         // list words: (LDS byte offset of entry j's staged record, 16 j) | (byte offset of its slot) << 16
         static_assert(16 * BB < 65536 && (BS + 1) * NV * 4 < 65536, "list words hold 16-bit byte offsets");
-        const SlotLists sl = build_row_slot_lists(s_mask, s_base, cmax, BS, w, jmin, s_list + 4 * w * LS, LS,
-                                                  (uint32_t)(16 * BB) | ((uint32_t)(BS * NV * 4) << 16), 16u,
-                                                  (uint32_t)(NV * 4));
+        SlotLists sl = build_row_slot_lists(s_mask, s_base, cmax, BS, w, jmin, s_list + 4 * w * LS, LS,
+                                            (uint32_t)(16 * BB) | ((uint32_t)(BS * NV * 4) << 16), 16u,
+                                            (uint32_t)(NV * 4));
+        if constexpr (kDupPhase == 3) {  // (VALU census only: the same lists again)
+            asm volatile("" ::: "memory");
+            sl = build_row_slot_lists(s_mask, s_base, cmax, BS, w, jmin, s_list + 4 * w * LS, LS,
+                                      (uint32_t)(16 * BB) | ((uint32_t)(BS * NV * 4) << 16), 16u, (uint32_t)(NV * 4));
+        }
         const int n = sl.len, cnt = sl.cnt;
         dg.phase(2);
         const int jlo16 = 16 * (hi - (int)last);  // pos = hi-1-j < last  <=>  j >= jlo  <=>  16 j >= 16 jlo

@@ -115,6 +115,7 @@ GaussIn make_gauss(const gsr_gaussians* g) {
     o.cov3D = g->cov3D_precomp;
     o.colors2 = nullptr;
     o.sh_staged = 0;
+    o.alive = nullptr;
     return o;
 }
 
@@ -300,7 +301,8 @@ size_t gsr_image_buffer_bytes(int W, int H) { return ImgLayout::make(W, H).total
 static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
                         float* out_color, float* out_color2, float* out_depth, int* radii, gsr_alloc_fn alloc,
                         void* alloc_ctx, void* stream_, int capacity = 0, uint32_t* status = nullptr,
-                        const TrackL1* l1 = nullptr, const TrackXf* xf = nullptr, float* track_inst = nullptr) {
+                        const TrackL1* l1 = nullptr, const TrackXf* xf = nullptr, float* track_inst = nullptr,
+                        const uint8_t* alive = nullptr) {
     int rc = validate(settings, gaussians, true);
     if (track_inst && (!l1 || !colors2 || capacity <= 0))
         return fail(GSR_ERR_INVALID_ARG, "the fused render backward needs the static dual forward with the L1 loss");
@@ -320,6 +322,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     Camera cam = make_camera(settings);
     GaussIn g = make_gauss(gaussians);
     g.colors2 = colors2;  // packed into the render records by preprocess (dual render)
+    g.alive = alive;
     if (xf) g.xf = *xf;   // tracking transform fused into preprocess (g's arrays are then its outputs)
     const int P = g.P, W = cam.W, H = cam.H;
     const GeomLayout GL = GeomLayout::make(P);
@@ -1055,6 +1058,17 @@ int gsr_forward_dual_static(const gsr_settings* settings, const gsr_gaussians* g
     if (capacity <= 0 || !status) return fail(GSR_ERR_INVALID_ARG, "static mode needs capacity > 0 and status");
     return forward_impl(settings, gaussians, colors2, out_color, out_color2, out_depth, radii, alloc, alloc_ctx,
                         stream, capacity, status);
+}
+
+int gsr_forward_dual_static_alive(const gsr_settings* settings, const gsr_gaussians* gaussians, const float* colors2,
+                                  int capacity, unsigned* status, float* out_color, float* out_color2,
+                                  float* out_depth, int* radii, const unsigned char* alive, gsr_alloc_fn alloc,
+                                  void* alloc_ctx, void* stream) {
+    if (!colors2) return fail(GSR_ERR_INVALID_ARG, "colors2 required");
+    if (capacity <= 0 || !status) return fail(GSR_ERR_INVALID_ARG, "static mode needs capacity > 0 and status");
+    if (!alive && gaussians && gaussians->P > 0) return fail(GSR_ERR_INVALID_ARG, "alive mask required");
+    return forward_impl(settings, gaussians, colors2, out_color, out_color2, out_depth, radii, alloc, alloc_ctx,
+                        stream, capacity, status, nullptr, nullptr, nullptr, alive);
 }
 
 int gsr_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,

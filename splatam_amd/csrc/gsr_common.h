@@ -223,6 +223,7 @@ struct GaussIn {
     const float* cov3D;
     const float* colors2;  // second precomputed colour set of a dual render (else nullptr)
     int sh_staged;         // SH colours already in bin[i].xyz / clamp (sh_eval_kernel, gsr_sh.hip)
+    const uint8_t* alive = nullptr;  // optional per-Gaussian mask, 0 = pruned (gsr_forward_dual_static_alive)
 };
 
 struct GeomPtrs {

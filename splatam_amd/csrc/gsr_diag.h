@@ -28,6 +28,11 @@
 namespace gsr {
 
 constexpr int kAblate = GSR_ABLATE;
+#ifndef GSR_DUP_PHASE
+#define GSR_DUP_PHASE 0  // VALU census by SQ counters (tools/gpu_round.sh sqab=): one render phase run twice (1 the
+                         // tile sort, 2 the forward row lists, 3 the backward slot lists); results unchanged
+#endif
+constexpr int kDupPhase = GSR_DUP_PHASE;
 GSR_WGTIME_TABLE  // (GSR_WGTIME builds: this translation unit's per-workgroup timeline table)
 
 #if GSR_STEPSTAT

@@ -93,6 +93,10 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
         float3 pv = xform4x3(p, cam.view);
         bool ok = pv.z > 0.001f;  // auxiliary.h:154 (the 1.3 NDC test is commented out)
         if (!ok && cam.prefiltered) violation = true;
+        // a pruned Gaussian (alive mask, prune_gaussians inside a captured mapping frame) is culled like one
+        // behind the camera: radius 0, no instances, zero gradients -- the survivors render and
+        // differentiate exactly as after remove_points (utils/slam_external.py:141-163)
+        if (g.alive != nullptr && g.alive[i] == 0) ok = false;
         float cov3[6];
         Proj pj;
         float det = 0.f, ca = 0.f, cb = 0.f, cc = 0.f;

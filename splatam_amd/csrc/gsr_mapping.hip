@@ -573,6 +573,27 @@ void fill_adam_common(double beta1, double beta2, double eps, int step, float& w
     e = (float)eps;
 }
 
+// prune_gaussians' removal test (utils/slam_external.py:174-181) as an in-place mask update: one lane per
+// Gaussian; sigmoid and exp formed the way torch's elementwise kernels form them (ATen: 1 / (1 + exp(-x)) in
+// float, expf), max over the scale columns with torch.max's NaN propagation
+__global__ void map_prune_kernel(int P, const float* __restrict__ logit_opac, const float* __restrict__ log_scales,
+                                 int scols, float opac_thr, float big_thr, int remove_big, uint8_t* __restrict__ alive) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P || alive[i] == 0) return;
+    const float op = 1.0f / (1.0f + expf(-logit_opac[i]));
+    bool rm = op < opac_thr;
+    if (remove_big) {
+        float m = expf(log_scales[(size_t)scols * i]);
+        for (int k = 1; k < scols; k++) {
+            const float v = expf(log_scales[(size_t)scols * i + k]);
+            m = (v > m || isnan(v)) && !isnan(m) ? v : m;
+        }
+        rm = rm || m > big_thr;
+    }
+    if (rm) alive[i] = 0;
+}
+
 }  // namespace
 }  // namespace gsr
 
@@ -669,6 +690,17 @@ int gsr_map_transform_bwd_adam(int P, float* means_world, float* unnorm_rot, flo
                        nullptr, nullptr, nullptr, dL_dcolors, color_cols, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GSR_OK : hip_fail(e, "map_transform_bwd_adam");
+}
+
+int gsr_map_prune(int P, const float* logit_opac, const float* log_scales, int scale_cols, float opac_thr,
+                  float big_thr, int remove_big, unsigned char* alive, void* stream) {
+    if (P < 0 || scale_cols < 1) return fail(GSR_ERR_INVALID_ARG, "map_prune: bad sizes");
+    if (P == 0) return GSR_OK;
+    if (!logit_opac || !alive || (remove_big && !log_scales)) return fail(GSR_ERR_INVALID_ARG, "map_prune: null pointer");
+    hipLaunchKernelGGL(map_prune_kernel, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, P, logit_opac,
+                       log_scales, scale_cols, opac_thr, big_thr, remove_big, alive);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? GSR_OK : hip_fail(e, "map_prune");
 }
 
 int gsr_adam_step(int n_tensors, const gsr_adam_tensor* tensors, int step, double beta1, double beta2, double eps,

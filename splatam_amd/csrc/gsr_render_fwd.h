@@ -253,6 +253,11 @@ __device__ __forceinline__ FwdPix fwd_tile(const Camera& cam, int tile, const ui
         tile_sort_bucket(keys + range.x, range.y - range.x, point_list + range.x,
                          reinterpret_cast<uint64_t*>(s_ab));
         __syncthreads();
+        if constexpr (kDupPhase == 1) {  // (VALU census only: the same sort again, same result)
+            tile_sort_bucket(keys + range.x, range.y - range.x, point_list + range.x,
+                             reinterpret_cast<uint64_t*>(s_ab));
+            __syncthreads();
+        }
     }
     if (tid == 0) {
         s_a[RENDER_BATCH] = pa;
@@ -319,8 +324,11 @@ __device__ __forceinline__ FwdPix fwd_tile(const Camera& cam, int tile, const ui
         const int jmin0[4] = {0, 0, 0, 0};
         // list entries: LDS byte offsets 16 j of the staged records (the walk loads them with ds_read_u16)
         static_assert(16 * RENDER_BATCH < 65536, "16-bit byte offsets");
-        const int n = build_row_lists(s_mask, cnt, w, jmin0, s_list + 4 * w * LS, LS, (uint16_t)(16 * RENDER_BATCH),
-                                      16u);
+        int n = build_row_lists(s_mask, cnt, w, jmin0, s_list + 4 * w * LS, LS, (uint16_t)(16 * RENDER_BATCH), 16u);
+        if constexpr (kDupPhase == 2) {  // (VALU census only: the same lists again)
+            asm volatile("" ::: "memory");
+            n = build_row_lists(s_mask, cnt, w, jmin0, s_list + 4 * w * LS, LS, (uint16_t)(16 * RENDER_BATCH), 16u);
+        }
         const uint16_t* my_list = s_list + (4 * w + row) * LS;
         const uint32_t pos16 = 16u * (start - range.x) + 16u;  // 16 (position of entry 0 + 1)
         dg.phase(2);

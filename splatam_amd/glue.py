@@ -367,6 +367,31 @@ class _MapTransform(torch.autograd.Function):
         return (dm if need[0] else None), du, dl, ds, (g_col if need[4] else None), None, None, None, None, None
 
 
+def prune_step(it: int, prune_dict: dict):
+    """What prune_gaussians (utils/slam_external.py:167-188) does at mapping iteration `it`:
+    (remove, opacity threshold, remove_big, reset_opacities)."""
+    pd = prune_dict
+    remove = it <= pd["stop_after"] and it >= pd["start_after"] and it % pd["prune_every"] == 0
+    thr = pd["final_removal_opacity_threshold"] if it == pd["stop_after"] else pd["removal_opacity_threshold"]
+    big = remove and it >= pd["remove_big_after"]
+    reset = it <= pd["stop_after"] and it > 0 and it % pd["reset_opacities_every"] == 0 and bool(pd["reset_opacities"])
+    return remove, float(thr), big, reset
+
+
+def map_prune(params: dict, alive: torch.Tensor, opac_thr: float, big_thr: float | None):
+    """gsr_map_prune: clear alive[i] where remove_points would drop Gaussian i (slam_external.py:174-181):
+    sigmoid(logit_opacities) < opac_thr, or (big_thr given) max exp(log_scales) > big_thr -- big_thr the
+    float32 value of 0.1 * variables['scene_radius'].  In place, no host sync (capturable)."""
+    lo, ls = _f32c(params["logit_opacities"], "logit_opacities"), _f32c(params["log_scales"], "log_scales")
+    P = lo.shape[0]
+    if alive.dtype != torch.uint8 or alive.numel() != P or alive.device != lo.device or not alive.is_contiguous():
+        raise RuntimeError("alive must be a contiguous uint8 tensor of P entries on the parameters' device")
+    rc = lib.gsr_map_prune(P, lo.data_ptr(), ls.data_ptr(), ls.shape[1], float(opac_thr),
+                           float(big_thr) if big_thr is not None else 0.0, 1 if big_thr is not None else 0,
+                           alive.data_ptr(), _stream(lo))
+    _check(rc, "map_prune")
+
+
 def map_transform(params: dict, time_idx: int, w2c: torch.Tensor, color_key: str = "rgb_colors",
                   adam: MapAdam | None = None):
     """transform_to_frame(params, t, gaussians_grad=True, camera_grad=False) (slam_helpers.py:252-304)

@@ -20,8 +20,23 @@ one w2c and one image size -- otherwise the sequence drawn at construction is ba
 into the graph, `redraw` False).  `sequence` is the last replay's draw.
 Each replay is one frame's mapping.  An iteration whose forward overflows the
 binning capacity skips its Adam step on the device (its status row, sticky
-across replays, reports it).  Densification / pruning (which change P)
-are outside the graph, as they are outside the reference's inner loop body.
+across replays, reports it).
+
+Pruning runs inside the frame, where the reference runs it: scripts/splatam.py:876-878 calls
+prune_gaussians between loss.backward() and optimizer.step() of every mapping iteration, and with
+configs/replica/splatam.py:101-111 (prune_every = stop_after = 20) it removes Gaussians at iterations
+0 and 20 of each frame.  P cannot change inside a captured graph, so the removal is a device mask:
+at a pruning iteration gsr_map_prune clears alive[i] for the Gaussians remove_points would drop
+(utils/slam_external.py:174-181), and every later forward of the frame culls them
+(gsr_forward_dual_static_alive: radius 0, no instances, zero gradients), so the survivors render,
+differentiate and step exactly as the compacted set does.  At a pruning iteration the reference's
+optimizer.step() updates no Gaussian parameter at all -- remove_points replaced every one of them by a
+new tensor without .grad, so torch.optim.Adam skips them and their state["step"] does not advance --
+hence that iteration is captured as its loss forward plus the mask update, with no backward and no
+Adam step (the fused steps' step counts follow: 1..19, then 20..58 for a 60-iteration frame).
+compact() then removes the pruned Gaussians from the parameters and the Adam state for real
+(remove_points) after the replay.  Densification (GS-style, off in the default configs) changes P and
+stays outside the graph.
 """
 from __future__ import annotations
 
@@ -56,7 +71,8 @@ def probe_num_rendered(params, curr_data, time_idx) -> tuple[int, int]:
 
 class GraphMapper:
     def __init__(self, params: dict, keyframes: list, iters_per_graph: int = 60, cfg: MappingConfig = MappingConfig(),
-                 headroom: float = 1.5, min_extra: int = 65536, seed: int | None = None, timing: bool = False):
+                 headroom: float = 1.5, min_extra: int = 65536, seed: int | None = None, timing: bool = False,
+                 prune: bool | None = None, scene_radius=None):
         if not keyframes:
             raise RuntimeError("GraphMapper needs at least one keyframe")
         for kf in keyframes:
@@ -69,6 +85,8 @@ class GraphMapper:
                 raise RuntimeError(f"params[{k!r}] must be a leaf tensor requiring grad")
         self.params, self.keyframes, self.cfg = params, keyframes, cfg
         dev = params["means3D"].device
+        self._setup_pruning(cfg if prune is None else None, bool(prune), scene_radius, int(iters_per_graph),
+                            params["means3D"].shape[0], dev)
         probes = [probe_num_rendered(params, kf, kf["id"]) for kf in keyframes]
         longest = max(p[1] for p in probes)
         if longest > TILE_SORT_CAP:
@@ -100,6 +118,7 @@ class GraphMapper:
                 for k, v in snapshot.items():
                     params[k].copy_(v)
             self.status.zero_()
+            self.alive.fill_(1)
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         del snapshot
@@ -110,8 +129,32 @@ class GraphMapper:
         self.stream = side
         with torch.cuda.graph(self.graph, stream=side):
             self.adam.reset()          # initialize_optimizer per frame: zero moments, step 0
+            self.alive.fill_(1)        # every Gaussian of the frame's map is live until a pruning iteration
             for k in range(self.iters):
                 self.loss = self._iteration(k)
+        self.stale = False
+
+    def _setup_pruning(self, cfg, prune, scene_radius, iters, P, dev):
+        """The frame's pruning iterations (glue.prune_step over 0..iters-1) and the alive mask."""
+        from .glue import prune_step
+        on = cfg.prune_gaussians if cfg is not None else prune
+        pd = self.cfg.pruning_dict
+        self.prune_at = {}
+        if on:
+            for k in range(iters):
+                remove, thr, big, reset = prune_step(k, pd)
+                if reset:
+                    raise ValueError("reset_opacities inside a captured frame would need per-group Adam step "
+                                     "counts (update_params_and_optimizer skips one group's step): map eagerly")
+                if remove:
+                    self.prune_at[k] = (thr, big)
+        self.big_thr = None
+        if any(big for _, big in self.prune_at.values()):
+            if scene_radius is None:
+                raise ValueError("pruning big Gaussians needs variables['scene_radius'] (scene_radius=)")
+            r = scene_radius if torch.is_tensor(scene_radius) else torch.tensor(float(scene_radius))
+            self.big_thr = float((0.1 * r.to(device=dev, dtype=torch.float32)).item())  # as the reference forms it
+        self.alive = torch.ones(P, dtype=torch.uint8, device=dev)
 
     def _make_slots(self, params, keyframes, dev):
         """Per-iteration keyframe slots read by the captured iterations: target image / depth, and the
@@ -158,10 +201,38 @@ class GraphMapper:
             kf = self.keyframes[self.sequence[k]]
             params, t = self.params, kf["id"]
         self.adam.status = self.status[k]  # this iteration's forward guards its Adam step
+        alive = self.alive if self.prune_at else None
         loss, _, _ = _get_loss_mapping_fused(params, kf, t, self.cfg, adam=self.adam, capacity=self.capacity,
-                                             status=self.status[k], means2D=self.means2D)
+                                             status=self.status[k], means2D=self.means2D, alive=alive)
+        if k in self.prune_at:
+            # prune_gaussians after loss.backward(): the gradients of this iteration reach no parameter (every
+            # Gaussian tensor is replaced by remove_points, so optimizer.step() skips them), so no backward runs
+            from .glue import map_prune
+            thr, big = self.prune_at[k]
+            map_prune(self.params, self.alive, thr, self.big_thr if big else None)
+            return loss.detach()
         torch.autograd.backward(loss, self.seed)
         return loss.detach()
+
+    def survivors(self) -> torch.Tensor:
+        """Boolean [P] mask of the Gaussians the last replay kept."""
+        return self.alive.bool()
+
+    def compact(self):
+        """After a replay, remove the pruned Gaussians for real: remove_points (utils/slam_external.py:141-163)
+        on the parameters and the frame's Adam moments.  Returns (params, exp_avg, exp_avg_sq): a new params
+        dict (the Gaussian tensors compacted, new leaves requiring grad; the camera tensors as they were) and
+        the moments by parameter name.  P changes, so this mapper is stale afterwards (run() raises): build
+        the next frame's mapper on the returned parameters."""
+        keep = self.survivors()
+        out = dict(self.params)
+        m, v = {}, {}
+        with torch.no_grad():
+            for k, em, ev in zip(self.adam.keys, self.adam.exp_avg, self.adam.exp_avg_sq):
+                out[k] = self.params[k].detach()[keep].clone().requires_grad_(True)
+                m[k], v[k] = em[keep].clone(), ev[keep].clone()
+        self.stale = True
+        return out, m, v
 
     def run(self, check: bool = True, sequence=None):
         """Enqueue one frame's mapping (one graph launch).  With `redraw` the keyframe of every iteration
@@ -172,6 +243,8 @@ class GraphMapper:
         with one host sync and raises on an overflow, so the caller can rebuild with more headroom and
         re-map the frame; check=False (timing loops) enqueues without a sync -- read overflowed()
         afterwards."""
+        if self.stale:
+            raise RuntimeError("this mapper was compacted (P changed): build a new one for the next frame")
         if self.redraw:
             n = len(self.keyframes)
             seq = [int(self.rng.randint(0, n)) for _ in range(self.iters)] if sequence is None else \

@@ -264,6 +264,19 @@ class MappingConfig:
     # densification statistics read means2D.grad of the RGB render alone (splatam.py:256,
     # slam_external.py:100-104), which one dual rasterization does not provide
     use_gaussian_splatting_densification: bool = False
+    # configs/replica/splatam.py:101-111: prune_gaussians (utils/slam_external.py:167-188) between
+    # loss.backward() and optimizer.step() of every mapping iteration (scripts/splatam.py:876-878)
+    prune_gaussians: bool = True
+    pruning_dict: dict = field(default_factory=lambda: dict(start_after=0, remove_big_after=0, stop_after=20,
+                                                           prune_every=20, removal_opacity_threshold=0.005,
+                                                           final_removal_opacity_threshold=0.005,
+                                                           reset_opacities=False, reset_opacities_every=500))
+    # configs/replica/splatam.py:113-123 (used when use_gaussian_splatting_densification)
+    densify_dict: dict = field(default_factory=lambda: dict(start_after=500, remove_big_after=3000, stop_after=5000,
+                                                           densify_every=100, grad_thresh=0.0002,
+                                                           num_to_split_into=2, removal_opacity_threshold=0.005,
+                                                           final_removal_opacity_threshold=0.005,
+                                                           reset_opacities_every=3000))
 
 
 def _gaussian(window_size, sigma):
@@ -327,9 +340,10 @@ _SH_ADAM_FUSED = True  # False: the colour step in gsr_map_transform_bwd_adam (A
 
 
 def _get_loss_mapping_fused(params, curr_data, iter_time_idx, cfg: MappingConfig, adam=None, capacity=0, status=None,
-                            means2D=None):
+                            means2D=None, alive=None):
     """The fused mapping iteration; capacity > 0: static-capacity rasterization (HIP-graph capturable),
-    means2D: optional caller-owned [P,3] tensor (the mapper passes a static one without grad)."""
+    means2D: optional caller-owned [P,3] tensor (the mapper passes a static one without grad), alive: the
+    static forward's pruning mask (GraphMapper's in-frame prune_gaussians)."""
     from .glue import map_transform, mapping_loss
     key = color_key(params)
     means, rots, dcol, opac, scales, col = map_transform(params, iter_time_idx, curr_data["w2c"], key, adam)
@@ -341,7 +355,7 @@ def _get_loss_mapping_fused(params, curr_data, iter_time_idx, cfg: MappingConfig
     sh_adam = adam if (adam is not None and sh is not None and _SH_ADAM_FUSED) else None
     im, depth_sil, radius, _ = rasterize_gaussians_dual(means, means2D, sh, colors, dcol, opac, scales, rots, None,
                                                         curr_data["cam"], capacity, status, grad2_channels=1,
-                                                        sh_adam=sh_adam, guard_sink=adam)
+                                                        sh_adam=sh_adam, guard_sink=adam, alive=alive)
     loss = mapping_loss(im, depth_sil, curr_data["im"], curr_data["depth"], cfg.w_im, cfg.w_depth)
     return loss, radius, means2D
 
@@ -390,21 +404,28 @@ def get_loss_mapping(params, curr_data, iter_time_idx, cfg: MappingConfig = Mapp
 
 def map_frame_literal(params, variables, keyframes, num_iters, cfg: MappingConfig = MappingConfig(), optimizer=None,
                       renderer=None, rng=None, losses_out=None):
-    """The unchanged mapping loop body of scripts/splatam.py:841-905 for one frame (prune_gaussians and
-    densification off, no progress reports): a fresh torch Adam over every parameter group
-    (initialize_optimizer, :842), then per iteration a keyframe drawn with np.random.randint (:851),
-    get_loss(mapping=True) through two GaussianRasterizer calls, loss.backward(), optimizer.step(),
-    zero_grad.  keyframes: dicts with cam / im / depth / w2c / id.  Returns the optimizer."""
+    """The unchanged mapping loop body of scripts/splatam.py:841-905 for one frame (no progress reports): a
+    fresh torch Adam over every parameter group (initialize_optimizer, :842), then per iteration a keyframe
+    drawn with np.random.randint (:851), get_loss(mapping=True) through two GaussianRasterizer calls,
+    loss.backward(), then (:876-884) prune_gaussians when cfg.prune_gaussians and densify when
+    cfg.use_gaussian_splatting_densification (surgery.py restatements; both replace tensors of `params` and
+    need variables["scene_radius"]), optimizer.step(), zero_grad.  keyframes: dicts with cam / im / depth /
+    w2c / id.  `params` is updated in place (entries replaced when P changes).  Returns the optimizer."""
     import numpy as np
+    from . import surgery
     rng = np.random if rng is None else rng
     if optimizer is None:
         optimizer = mapping_optimizer(params, cfg, fused=False)
-    for _ in range(num_iters):
+    for it in range(num_iters):
         kf = keyframes[int(rng.randint(0, len(keyframes)))]
         loss, _radius, _m2d = get_loss_mapping(params, kf, kf["id"], cfg, fused=False, variables=variables,
                                                renderer=renderer)
         loss.backward()
         with torch.no_grad():
+            if cfg.prune_gaussians:
+                surgery.prune_gaussians(params, variables, optimizer, it, cfg.pruning_dict)
+            if cfg.use_gaussian_splatting_densification:
+                surgery.densify(params, variables, optimizer, it, cfg.densify_dict)
             optimizer.step()
             optimizer.zero_grad(set_to_none=True)
         if losses_out is not None:

@@ -1,7 +1,7 @@
 """Gaussian-set surgery on the parameters and the optimizer state.
 
-Restates utils/slam_external.py:107-178 (update_params_and_optimizer,
-cat_params_to_optimizer, remove_points, prune_gaussians) operating on any
+Restates utils/slam_external.py:100-243 (accumulate_mean2d_gradient, update_params_and_optimizer,
+cat_params_to_optimizer, remove_points, prune_gaussians, densify) operating on any
 optimizer that keeps torch.optim.Adam's state layout -- torch.optim.Adam itself
 or splatam_amd.glue.FusedAdam, whose state uses the same keys ("step",
 "exp_avg", "exp_avg_sq"), so these functions (and the reference's own) work on
@@ -85,6 +85,63 @@ def prune_gaussians(params, variables, optimizer, iter, prune_dict):
                 to_remove = torch.logical_or(to_remove, big)
             params, variables = remove_points(to_remove, params, variables, optimizer)
         if iter > 0 and iter % prune_dict["reset_opacities_every"] == 0 and prune_dict["reset_opacities"]:
+            new = {"logit_opacities": inverse_sigmoid(torch.ones_like(params["logit_opacities"]) * 0.01)}
+            params = update_params_and_optimizer(new, params, optimizer)
+    return params, variables
+
+
+def accumulate_mean2d_gradient(variables):
+    """slam_external.py:100-104: the densification statistic from the RGB render's own means2D.grad."""
+    seen = variables["seen"]
+    variables["means2D_gradient_accum"][seen] += torch.norm(variables["means2D"].grad[seen, :2], dim=-1)
+    variables["denom"][seen] += 1
+    return variables
+
+
+def densify(params, variables, optimizer, iter, densify_dict):
+    """slam_external.py:191-243 (Gaussian-Splatting-style clone / split / prune).  The split samples come
+    from torch.normal on the current CUDA generator, like the reference's."""
+    from .slam import build_rotation
+    if iter <= densify_dict["stop_after"]:
+        variables = accumulate_mean2d_gradient(variables)
+        grad_thresh = densify_dict["grad_thresh"]
+        if iter >= densify_dict["start_after"] and iter % densify_dict["densify_every"] == 0:
+            grads = variables["means2D_gradient_accum"] / variables["denom"]
+            grads[grads.isnan()] = 0.0
+            to_clone = torch.logical_and(grads >= grad_thresh, torch.max(torch.exp(params["log_scales"]), dim=1).values
+                                         <= 0.01 * variables["scene_radius"])
+            new_params = {k: v[to_clone] for k, v in params.items() if k not in CAM_KEYS}
+            params = cat_params_to_optimizer(new_params, params, optimizer)
+            num_pts = params["means3D"].shape[0]
+            padded_grad = torch.zeros(num_pts, device=grads.device)
+            padded_grad[:grads.shape[0]] = grads
+            to_split = torch.logical_and(padded_grad >= grad_thresh,
+                                         torch.max(torch.exp(params["log_scales"]), dim=1).values
+                                         > 0.01 * variables["scene_radius"])
+            n = densify_dict["num_to_split_into"]
+            new_params = {k: v[to_split].repeat(n, 1) for k, v in params.items() if k not in CAM_KEYS}
+            stds = torch.exp(params["log_scales"])[to_split].repeat(n, 3)
+            means = torch.zeros((stds.size(0), 3), device=stds.device)
+            samples = torch.normal(mean=means, std=stds)
+            rots = build_rotation(params["unnorm_rotations"][to_split]).repeat(n, 1, 1)
+            new_params["means3D"] += torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1)
+            new_params["log_scales"] = torch.log(torch.exp(new_params["log_scales"]) / (0.8 * n))
+            params = cat_params_to_optimizer(new_params, params, optimizer)
+            num_pts = params["means3D"].shape[0]
+            variables["means2D_gradient_accum"] = torch.zeros(num_pts, device=grads.device)
+            variables["denom"] = torch.zeros(num_pts, device=grads.device)
+            variables["max_2D_radius"] = torch.zeros(num_pts, device=grads.device)
+            to_remove = torch.cat((to_split, torch.zeros(n * int(to_split.sum()), dtype=torch.bool,
+                                                         device=grads.device)))
+            params, variables = remove_points(to_remove, params, variables, optimizer)
+            thr = (densify_dict["final_removal_opacity_threshold"] if iter == densify_dict["stop_after"]
+                   else densify_dict["removal_opacity_threshold"])
+            to_remove = (torch.sigmoid(params["logit_opacities"]) < thr).squeeze()
+            if iter >= densify_dict["remove_big_after"]:
+                big = torch.exp(params["log_scales"]).max(dim=1).values > 0.1 * variables["scene_radius"]
+                to_remove = torch.logical_or(to_remove, big)
+            params, variables = remove_points(to_remove, params, variables, optimizer)
+        if iter > 0 and iter % densify_dict["reset_opacities_every"] == 0 and densify_dict["reset_opacities"]:
             new = {"logit_opacities": inverse_sigmoid(torch.ones_like(params["logit_opacities"]) * 0.01)}
             params = update_params_and_optimizer(new, params, optimizer)
     return params, variables

@@ -109,3 +109,55 @@ def test_fisher_scoring_sharded_world2():
     for _, h, s in res:
         assert torch.allclose(torch.tensor(h, dtype=hinv.dtype), hinv) and torch.allclose(torch.tensor(s, dtype=scores.dtype), scores)
     assert bool((scores[1:] > scores[:-1]).all())
+
+
+def _flat_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from splatam_amd import dist as sd
+    from splatam_amd.scenes import make_scene
+    from splatam_amd.slam import init_tracking_params
+    params = init_tracking_params(make_scene(100, 32, 32, seed=rank), num_frames=4, device="cpu")
+    objs = {k: params[k] for k in sd.MAP_KEYS}
+    fm = sd.FlatMap(params)
+    seated = all(params[k] is objs[k] for k in sd.MAP_KEYS) and fm.check()  # same tensor objects, new storage
+    sent = sd.broadcast_flat(fm)  # one collective: rank 1 now holds rank 0's map
+    ref0 = init_tracking_params(make_scene(100, 32, 32, seed=0), num_frames=4, device="cpu")
+    same = all(torch.equal(params[k], ref0[k]) for k in sd.MAP_KEYS)
+    # double-buffered: rank 0 updates its map, starts the broadcast, keeps updating; rank 1 keeps the old
+    # version until finish(), then holds exactly the version rank 0 had at start()
+    bc = sd.MapBroadcaster(fm)
+    if rank == 0:
+        with torch.no_grad():
+            params["means3D"].add_(1.0)
+    v1 = params["means3D"].clone() if rank == 0 else None
+    bc.start()
+    stale = torch.equal(params["means3D"], ref0["means3D"]) if rank == 1 else True
+    if rank == 0:
+        with torch.no_grad():
+            params["means3D"].add_(5.0)  # after start(): not part of this broadcast
+    bc.finish()
+    got = params["means3D"].clone()
+    dist.broadcast(v1 if rank == 0 else (v1 := torch.empty_like(got)), src=0)  # rank 0's start() version
+    fresh = torch.equal(got, v1) if rank == 1 else torch.equal(got, v1 + 5.0)
+    q.put((rank, seated, sent, same, stale, fresh))
+    dist.destroy_process_group()
+
+
+def test_flat_map_broadcast_world2():
+    """FlatMap re-seats the map tensors as views of one buffer (the same tensor objects) and broadcast_flat
+    moves the whole map in one collective; MapBroadcaster's double buffer leaves the receiving rank on the
+    old map until finish(), then on exactly the version the source had at start() (bitwise)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_flat_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, seated, sent, same, stale, fresh in res:
+        assert seated and same and stale and fresh, (rank, seated, same, stale, fresh)
+        assert sent == 100 * (3 + 3 + 4 + 1 + 1) * 4

@@ -287,7 +287,7 @@ def test_graph_mapper_matches_eager_iterations(cuda, sh):
     for k in keys:
         g_p[k].requires_grad_(True)
         e_p[k].requires_grad_(True)
-    mapper = GraphMapper(g_p, kfs, iters_per_graph=6, seed=7)
+    mapper = GraphMapper(g_p, kfs, iters_per_graph=6, seed=7, prune=False)
     assert mapper.redraw
     for k in keys:  # construction (warm-up) leaves the parameters untouched
         assert torch.equal(g_p[k].detach(), params[k]), k
@@ -327,7 +327,7 @@ def test_graph_mapper_overflow_halts_and_raises(cuda):
     p = {k: v.clone() for k, v in params.items()}
     for k in keys:
         p[k].requires_grad_(True)
-    mapper = GraphMapper(p, kfs, iters_per_graph=4, seed=3, headroom=1.0, min_extra=0)
+    mapper = GraphMapper(p, kfs, iters_per_graph=4, seed=3, headroom=1.0, min_extra=0, prune=False)
     with torch.no_grad():
         p["log_scales"].add_(1.0)  # 2.7x larger footprints: far more tile instances than the capacity
     before = {k: p[k].detach().clone() for k in keys}

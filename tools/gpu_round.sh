@@ -30,6 +30,8 @@
 #   drv              the driver's bench command (--steps 20 --warmup 5) and 100/10, interleaved, two rounds
 #   drift            per-launch render_track durations over 5 frames of 40 iterations (tools/drift.py)
 #   clk              GRBM_COUNT / GRBM_GUI_ACTIVE per render_track launch over the drift run (clock per launch)
+#   sqab=TAGS        SQ instruction counts (VALU / SALU / LDS per launch) of render_track (SQRX: another kernel
+#                    regex) for libgsr.so and each _diag/libgsr_<tag>.so
 #   abflag=FLAG:V1,V2[,...]  interleaved A/B (two rounds) of the light bench line over the values of one bench.py
 #                    flag, e.g. abflag=--fuse-render:1,0
 TAG=${1:-x}; shift
@@ -188,6 +190,24 @@ PY
              -- python "$ROOT/bench.py" --steps 200 --warmup 5 --settle-ms 0 $LIGHT > "$OUT/clk.log" 2>&1 ) \
              || { echo "clk failed"; tail -20 "$OUT/clk.log"; exit 1; }
          python tools/drift.py "$OUT/clk" --skip 25 --counters | tee "$OUT/clk.txt" ;;
+    sqab=*) TAGS=${s#sqab=}  # SQ instruction counts of the fused tracking render per library (VALU census by variants)
+         for t in base ${TAGS//,/ }; do
+           d="$OUT/sqab_$t"
+           ( cd /tmp && export TMPDIR=/tmp && GSR_LIB_AB=1 GSR_LIB=$(lib_of $t) timeout -s KILL 200 rocprofv3 --pmc \
+               SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_BRANCH \
+               --kernel-include-regex "${SQRX:-render_track}" -T -d "$d" -o run --output-format csv \
+               -- python "$ROOT/bench.py" --steps 20 --warmup 5 $LIGHT > "$d.log" 2>&1 ) \
+               || { echo "sqab $t failed"; tail -20 "$d.log"; exit 1; }
+           python - "$d" $t <<'PY' | tee -a "$OUT/sqab.txt"
+import csv, glob, sys, collections
+f = glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)[0]
+acc = collections.defaultdict(list)
+for r in csv.DictReader(open(f)):
+    acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+print("sqab", sys.argv[2], " ".join(f"{k} {sum(v) / len(v) / 1e6:.3f}M" for k, v in sorted(acc.items())), "launches",
+      len(acc.get("SQ_INSTS_VALU", [])))
+PY
+         done ;;
     *) echo "unknown step $s"; exit 1 ;;
   esac
   echo "step $s ok"
