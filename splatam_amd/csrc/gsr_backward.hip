@@ -41,17 +41,20 @@ __device__ __forceinline__ void pair_geom(float* vk, float araw, float dLa, floa
     vk[4] = hv.y * d.y;
     if (OPAC) vk[5] = G * dLa;
 }
-// Per-pair colour terms dch * dL/dpix (COL1, 3) and dch * dL/dpix2 (COL2, Q2 channels).
-template <bool COL1, bool COL2, int Q2>
+// Per-pair colour terms dch * dL/dpix (COL1: C1 = 3 channels, or 1 on a tile whose dL/dpix channels 1 and
+// 2 are zero) and dch * dL/dpix2 (COL2, Q2 channels).
+template <bool COL1, bool COL2, int Q2, int C1 = 3>
 __device__ __forceinline__ void pair_colours(float* vk, float dch, v2f dp01, float dp2, float dq0, v2f dq01,
                                              float dq2) {
-    if (COL1) {
+    if (COL1 && C1 == 1) {
+        vk[0] = dch * dp01.x;
+    } else if (COL1) {
         const v2f t = dch * dp01;
         vk[0] = t.x;
         vk[1] = t.y;
         vk[2] = dch * dp2;
     }
-    float* v2 = vk + (COL1 ? 3 : 0);
+    float* v2 = vk + (COL1 ? C1 : 0);
     if (COL2 && Q2 == 1) {
         v2[0] = dch * dq0;
     } else if (COL2) {
@@ -135,8 +138,8 @@ constexpr int bwd_slots() { return MOM == 1 ? 256 : (MOM == 2 ? 128 : (NV <= 6 ?
 //   MOM 1 (colours precomputed, 16 sums): [13, 16) sum (dch dL/dpix_c)^2
 //   MOM 2 (SH colours, 34 sums): [13, 19) sum dch^2 dL/dpix_c dL/dpix_d (c <= d, row-major),
 //                                [19, 34) sum u_i dch dL/dpix_c (i-major)
-template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2, int MOM = 0>
-constexpr int bwd_nv() { return MOM == 1 ? 16 : (MOM == 2 ? 34 : 5 + (OPAC ? 1 : 0) + (COL1 ? 3 : 0) + (COL2 ? Q2 : 0)); }
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2, int MOM = 0, int C1 = 3>
+constexpr int bwd_nv() { return MOM == 1 ? 16 : (MOM == 2 ? 34 : 5 + (OPAC ? 1 : 0) + (COL1 ? C1 : 0) + (COL2 ? Q2 : 0)); }
 __host__ __device__ constexpr int mono_t(int a, int b) {  // monomial index of dx^a dy^b, a + b in {2, 3, 4}
     return a + b == 2 ? 2 - a : (a + b == 3 ? 3 + (3 - a) : 7 + (4 - a));
 }
@@ -228,11 +231,16 @@ constexpr int bwd_waves() {
 
 // A tile backward's shape and LDS layout (carved from one byte array, so a kernel that also runs the
 // forward of the same tile -- render_track_kernel -- can alias the two phases' LDS)
-template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2, int MOM>
+// C1 = 1: the single-image colour sums of a tile whose dL/dpix channels 1 and 2 are zero (SplaTAM's
+// depth/silhouette render: its loss differentiates the depth channel only) -- one colour sum instead of
+// three; the batch shape and the record layout stay those of the C1 = 3 variant (the two missing sums are
+// stored as zeros), so both serve the same launch.
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2, int MOM, int C1 = 3>
 struct BwdShape {
-    static constexpr int NV = bwd_nv<DUAL, OPAC, COL1, COL2, Q2, MOM>();
-    static constexpr int BB = bwd_batch<NV, MOM>(), BS = bwd_slots<NV, MOM>();
-    static constexpr int RS = (NV + 1) & ~1;  // record stride (floats)
+    static constexpr int NV = bwd_nv<DUAL, OPAC, COL1, COL2, Q2, MOM, C1>();
+    static constexpr int NV3 = bwd_nv<DUAL, OPAC, COL1, COL2, Q2, MOM, 3>();
+    static constexpr int BB = bwd_batch<NV3, MOM>(), BS = bwd_slots<NV3, MOM>();
+    static constexpr int RS = (NV3 + 1) & ~1;  // record stride (floats)
     static constexpr int LS = BB + 4;          // row-list stride (u32)
     // entry BB is a dummy (opacity 0, never blends) that pads the row lists; its slot BS
     // absorbs the pad entries' (zero) sums
@@ -256,7 +264,7 @@ struct BwdPix {
     float dp0, dp1, dp2, dq0, dq1, dq2;
 };
 
-template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2, int MOM>
+template <bool DUAL, bool OPAC, bool COL1, bool COL2, int Q2, int MOM, int C1 = 3>
 __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdPix& pin,
                                          const uint2* __restrict__ ranges, const PointEntry* __restrict__ point_list,
                                          const float4* __restrict__ rr, const uint32_t* __restrict__ blocksums,
@@ -265,7 +273,8 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
     static_assert(DUAL || !COL2, "COL2 needs the dual colour set");
     static_assert(!MOM || (!DUAL && OPAC && COL1), "the moment variants form every single-image gradient");
     static_assert(Q2 == 1 || Q2 == 3, "Q2 is 1 or 3 channels");
-    using L = BwdShape<DUAL, OPAC, COL1, COL2, Q2, MOM>;
+    static_assert(C1 == 3 || (C1 == 1 && COL1 && !DUAL && !MOM), "one colour sum: single-image colour variants only");
+    using L = BwdShape<DUAL, OPAC, COL1, COL2, Q2, MOM, C1>;
     constexpr int NV = L::NV;
     constexpr int O_C1 = 5 + (OPAC ? 1 : 0);
     constexpr int BB = L::BB, BS = L::BS, RS = L::RS, LS = L::LS;
@@ -478,6 +487,8 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
                     const float4 c2 = rec(s_d, k);
                     const v2f t = v2f{c.x, c.y} * dp01 + v2f{c2.x, c2.y} * dq01;
                     cd = __builtin_fmaf(c.z, dp2, __builtin_fmaf(c2.z, dq2, t.x + t.y));
+                } else if (C1 == 1) {  // dL/dpix channels 1, 2 zero on this tile: the same value (up to a zero's sign)
+                    cd = c.x * dp0;
                 } else {
                     const v2f t = v2f{c.x, c.y} * dp01;
                     cd = __builtin_fmaf(c.z, dp2, t.x + t.y);
@@ -536,7 +547,7 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     pair_geom<OPAC>(v + NV * k, araw[k], dLa[k], G[k], d[k]);
-                    pair_colours<COL1, COL2, Q2>(v + NV * k + O_C1, dch[k], dp01, dp2, dq0, dq01, dq2);
+                    pair_colours<COL1, COL2, Q2, C1>(v + NV * k + O_C1, dch[k], dp01, dp2, dq0, dq01, dq2);
                 }
                 if constexpr (kAblate == 1) {
 #pragma unroll
@@ -559,7 +570,7 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
                         if (OB) v[NB * k] = G[k] * dLa[k];
-                        pair_colours<COL1, COL2, Q2>(v + NB * k + OB, dch[k], dp01, dp2, dq0, dq01, dq2);
+                        pair_colours<COL1, COL2, Q2, C1>(v + NB * k + OB, dch[k], dp01, dp2, dq0, dq01, dq2);
                     }
                     reduce_store<NB>(v, lane, dst + NA, true);
                 }
@@ -571,7 +582,7 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
         // Entry totals: TPE threads per entry, thread q of an entry owns values m = q, q + TPE, ...
         // and adds the entry's consecutive block slots in ascending block order (deterministic);
         // the TPE threads store adjacent floats of the packed record.
-        constexpr int TPE = TILE_PIX / BB, NQ = (RS + TPE - 1) / TPE;
+        constexpr int TPE = TILE_PIX / BB, NQ = (NV + TPE - 1) / TPE, NQR = (RS + TPE - 1) / TPE;
         int t_ = tid;
         asm volatile("" : "+v"(t_));  // addresses formed here, not hoisted across the batch loop (VGPRs)
         const int e = t_ / TPE, q = t_ % TPE;
@@ -591,12 +602,13 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
             }
             float* dst = inst + (size_t)RS * s_u[e];  // packed record (RecLayout): the NV sums, zero pad
 #pragma unroll
-            for (int i = 0; i < NQ; i++)
+            for (int i = 0; i < NQR; i++)
                 if (q + TPE * i < RS) {
                     // (streaming stores measured neutral for render_bwd and 3-9 us slower for the gauss_bwd that
                     // reads the records next: profiles/r4l_ab_nt.txt, r4m_ab_nt.txt)
-                    if (GSR_NT_STORES) __builtin_nontemporal_store(c[i], &dst[q + TPE * i]);
-                    else dst[q + TPE * i] = c[i];
+                    const float val = i < NQ ? c[i] : 0.f;  // (C1 = 1: the two absent colour sums are zero)
+                    if (GSR_NT_STORES) __builtin_nontemporal_store(val, &dst[q + TPE * i]);
+                    else dst[q + TPE * i] = val;
                 }
         }
         dg.phase(5);
@@ -645,6 +657,18 @@ render_bwd_kernel(Camera cam, const uint2* __restrict__ ranges, const PointEntry
                 pin.dq1 = dL_dpix2[HW + pid];
                 pin.dq2 = dL_dpix2[2 * HW + pid];
             }
+        }
+    }
+    if constexpr (!DUAL && COL1 && MOM == 0) {
+        // a tile whose incoming gradient has zero channels 1 and 2 everywhere (SplaTAM's depth/silhouette
+        // render: get_loss differentiates only its depth channel, scripts/splatam.py:262-270) forms one colour
+        // sum per pair instead of three; the others are exactly zero (records identical up to a zero's sign)
+        if (!__syncthreads_or(pin.dp1 != 0.f || pin.dp2 != 0.f)) {
+            bwd_tile<DUAL, OPAC, COL1, COL2, Q2, MOM, 1>(cam, tile, pin, ranges, point_list, rr, blocksums, inst, guard,
+                                                         smem, dg);
+            dg.end();
+            kclock_end(clk);
+            return;
         }
     }
     bwd_tile<DUAL, OPAC, COL1, COL2, Q2, MOM>(cam, tile, pin, ranges, point_list, rr, blocksums, inst, guard, smem, dg);

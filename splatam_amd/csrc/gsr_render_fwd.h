@@ -347,7 +347,9 @@ __device__ __forceinline__ FwdPix fwd_tile(const Camera& cam, int tile, const ui
             for (int k = 0; k < 4; k++) {
                 const float4 a = rec(s_a, k), b = rec(s_b, k);
                 const float p2 = eval_p2(a, b, pix_delta(a, pix));           // log2(e) * power
-                alpha[k] = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(fminf(p2, 0.f)));
+                // (no clamp of p2: a pair with p2 > 0 -- exp2 up to inf, alpha then 0.99 -- is excluded by ok[k],
+                // as forward.cu:342 skips it; a NaN p2 fails p2 <= 0 too)
+                alpha[k] = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(p2));
                 depth[k] = b.z;
                 ok[k] = p2 <= 0.0f && alpha[k] >= 1.0f / 255.0f;  // the pad entry has alpha 0
             }
