@@ -159,3 +159,22 @@ def test_alias_packages():
     assert list(inspect.signature(fork.GaussianRasterizer.__init__).parameters) == ["self", "raster_settings",
                                                                                     "backward_power"]
     assert hasattr(upstream, "_C") and hasattr(fork._C, "rasterize_gaussians_backward")
+
+
+def test_gsr_lib_override_stays_strict(tmp_path):
+    """GSR_LIB alone loads another library under the full symbol / ABI checks; only GSR_LIB_AB=1 (an A/B
+    baseline from an older revision) relaxes them (a stale ABI-4 build must not load silently)."""
+    import subprocess
+    import sys
+    src = tmp_path / "stale.c"
+    src.write_text("int gsr_abi_version(void) { return 4; }\n")
+    so = tmp_path / "libstale.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    code = "import splatam_amd._lib"
+    base = {k: v for k, v in os.environ.items() if k not in ("GSR_LIB", "GSR_LIB_AB")}
+    strict = subprocess.run([sys.executable, "-c", code], env=dict(base, GSR_LIB=str(so)), capture_output=True,
+                            text=True, cwd=ROOT)
+    assert strict.returncode != 0 and "lacks" in strict.stderr, strict.stderr[-500:]
+    relaxed = subprocess.run([sys.executable, "-c", code], env=dict(base, GSR_LIB=str(so), GSR_LIB_AB="1"),
+                             capture_output=True, text=True, cwd=ROOT)
+    assert relaxed.returncode == 0, relaxed.stderr[-500:]
