@@ -832,10 +832,11 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
     x.mw = pf.means_world; x.ur = pf.unnorm_rot; x.ls = pf.ls; x.scols = pf.scols;
     XfRaw xr{};
     if (xf_geom && live) xr = track_xform_load(x, i, false);
-    uint32_t off = 0, cnt = 0;
+    uint32_t off = 0, cnt = 0, tl = 0xFFFFFFFFu;  // tl: live-tile mask (Camera::cull: culled slots are unwritten)
     if (POSE && live && rad > 0) {
         off = geo.offsets[i];
         cnt = geo.tiles[i];
+        tl = reinterpret_cast<const uint32_t*>(geo.bin)[4 * (size_t)i + 3];
     }
     __shared__ Pose s_pose;
     if constexpr (POSE) {
@@ -875,11 +876,11 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
                 const float2* r = reinterpret_cast<const float2*>(inst + (size_t)rec.stride * (off + e0 + k));
 #pragma unroll
                 for (int m = 0; m < INST_REC_MAX / 2; m++)
-                    v[k][m] = (m < np && e0 + k < cnt) ? r[m] : make_float2(0.f, 0.f);
+                    v[k][m] = (m < np && e0 + k < cnt && tile_live(tl, e0 + k)) ? r[m] : make_float2(0.f, 0.f);
             }
 #pragma unroll
             for (int k = 0; k < RU; k++)
-                if (e0 + k < cnt) {
+                if (e0 + k < cnt && tile_live(tl, e0 + k)) {  // (a culled slot's record would be +0: skipped exactly)
 #pragma unroll
                     for (int m = 0; m < INST_REC_MAX / 2; m++)
                         if (m < np) {

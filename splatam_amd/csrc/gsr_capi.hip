@@ -19,6 +19,9 @@
 #include "../../include/gsr_glue.h"
 #include "gsr_common.h"
 
+#ifndef GSR_TRACK_CULL
+#define GSR_TRACK_CULL 1  // Camera::cull in the fused tracking forward (0: timing A/B)
+#endif
 using namespace gsr;
 
 namespace {
@@ -358,6 +361,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     }
     static const bool force_radix_env = getenv("GSR_FORCE_RADIX") && atoi(getenv("GSR_FORCE_RADIX")) != 0;
     const bool force_radix = force_radix_env && capacity <= 0;
+    // tile culling in the fused tracking forward (static mode: the speculative bucketed path is final)
+    cam.cull = (GSR_TRACK_CULL && xf && capacity > 0 && lds_hist) ? 1 : 0;
     // the bucketed duplicate's workgroup 0 writes the render schedule (tile_plan); the other paths
     // render in row-major order
     Camera cplan = cam;

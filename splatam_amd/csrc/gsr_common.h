@@ -162,7 +162,17 @@ struct Camera {
     uint32_t* rowmax = nullptr;
     int sched_cus = 256;
     int pre_shift = 10;  // log2 Gaussians per count-matrix row (GeomLayout::shift)
+    // Tile culling (the fused tracking forward, static mode): a (Gaussian, tile) instance whose alpha >= 1/255
+    // ellipse reaches no 4x4 block of the tile (block_mask_exact == 0, conservative) is left out of the tile's
+    // bucket -- it would be sorted and staged but never evaluated, and its record would be zero.  Its record
+    // slot stays (slots are rect-indexed); bin[i].w carries the Gaussian's live-tile mask, which gauss_bwd
+    // reads to skip the unwritten slots.  Results are bitwise those of the unculled lists; num_rendered
+    // (the record count) is unchanged, the tile ranges are shorter.
+    int cull = 0;
 };
+// bin[i].w: bit k set = rect tile k (row-major in the rect) has an instance in its bucket; all ones when
+// nothing is culled (or the rect has more than 32 tiles)
+__device__ __forceinline__ bool tile_live(uint32_t live, uint32_t k) { return k >= 32u || ((live >> k) & 1u); }
 // Wave priority by remaining work (GSR_PRIO_SCHED): the instruction arbiter favours older
 // waves, so on a CU the last-dispatched tile used to run alone at the end at one wave per
 // SIMD; raising the priority of the waves with the most work left keeps the CU's tiles
@@ -591,6 +601,25 @@ __device__ __forceinline__ uint32_t mask_of_geom(const MaskGeom& g, float x0, fl
         m |= ((cm & 3u) << base) | ((cm >> 2) << (base + 4));
     }
     return m;
+}
+// Whether the ellipse can reach the tile at all (Camera::cull): mask_of_geom's test with the tile's whole
+// pixel-centre span [y0, y0 + 15] as one row and [x0, x0 + 15] as one column -- a superset of the union of its
+// sixteen block tests (it also admits the unit gaps between block rows / columns), so conservative like them
+#ifndef GSR_CULL_EXACT
+#define GSR_CULL_EXACT 0  // 1: the sixteen block tests (block_mask_exact != 0) instead
+#endif
+__device__ __forceinline__ bool tile_reached(const MaskGeom& g, float x0, float y0) {
+    if (g.hx < 0.f) return true;
+    if (g.hy < 0.f) return false;
+    const float ylo = y0 - g.ay, yhi = ylo + 15.f;
+    if (!(yhi >= -g.hy && ylo <= g.hy)) return false;
+    const float lo = fmaxf(ylo, -g.hy), hi = fminf(yhi, g.hy);
+    const float ul = __builtin_amdgcn_fmed3f(g.us, lo, hi), ur = __builtin_amdgcn_fmed3f(-g.us, lo, hi);
+    const float wl = __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-g.det * ul, ul, g.twoA_tau), 0.f));
+    const float wr = __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-g.det * ur, ur, g.twoA_tau), 0.f));
+    const float xmin = (g.ax - g.eps) - __builtin_fmaf(g.B, ul, wl) * g.inv_A;
+    const float xmax = (g.ax + g.eps) + __builtin_fmaf(-g.B, ur, wr) * g.inv_A;
+    return xmax >= x0 && xmin <= x0 + 15.f;
 }
 __device__ __forceinline__ uint32_t block_mask_exact(float4 a, float4 b, float x0, float y0) {
     return mask_of_geom(mask_geom(a, b), x0, y0);

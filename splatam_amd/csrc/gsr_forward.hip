@@ -153,10 +153,22 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                     rr[3] = q3;
                 }
                 q1 = make_float4(K_B * cb, XF ? xop : pre_op, pv.z, 0.f);  // .w: workgroup-local instance offset, below
-                geo.bin[i] = make_uint4(rlo, rhi, __float_as_uint(pv.z), tiles);
+                // live-tile mask (Camera::cull): the render's own conservative block-mask test per rect tile
+                uint32_t live = 0xFFFFFFFFu;
+                if (cam.cull && tiles <= 32u) {
+                    const MaskGeom mg = mask_geom(q0, q1);
+                    live = 0u;
+                    for (int ty = y0, k = 0; ty < y1; ty++)
+                        for (int tx = x0; tx < x1; tx++, k++)
+                            live |= (GSR_CULL_EXACT ? mask_of_geom(mg, (float)(tx * TILE_X), (float)(ty * TILE_Y)) != 0u
+                                                    : tile_reached(mg, (float)(tx * TILE_X), (float)(ty * TILE_Y)))
+                                        ? 1u << k : 0u;
+                }
+                geo.bin[i] = make_uint4(rlo, rhi, __float_as_uint(pv.z), live);
                 if (!g.sh_staged && !g.colors) geo.clamp[i] = clamped;  // (read only by the SH backward)
-                for (int ty = y0; ty < y1; ty++)  // per-tile instance counts -> bucket ranges
-                    for (int tx = x0; tx < x1; tx++) {
+                for (int ty = y0, k = 0; ty < y1; ty++)  // per-tile instance counts -> bucket ranges
+                    for (int tx = x0; tx < x1; tx++, k++) {
+                        if (!tile_live(live, (uint32_t)k)) continue;
                         if (LDS_HIST) atomicAdd(&s_hist[ty * cam.gx + tx], 1u);
                         else atomicAdd(&counts[(ty * cam.gx + tx) * TILE_CTR_STRIDE], 1u);
                     }
@@ -644,7 +656,7 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
     constexpr int ROW = DUP_G * DUP_T;  // Gaussians per count-matrix row (1 << cam.pre_shift)
     extern __shared__ uint32_t s_cur[];
     __shared__ uint32_t s_incl[ROW];
-    __shared__ uint32_t s_x0[ROW], s_y0[ROW], s_w[ROW], s_depth[ROW];
+    __shared__ uint32_t s_x0[ROW], s_y0[ROW], s_w[ROW], s_depth[ROW], s_live[ROW];
     __shared__ uint32_t wsum[DUP_T / 64], s_tmax[DUP_T / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int i0 = blockIdx.x * ROW + DUP_G * tid;  // this lane's Gaussians i0 .. i0 + DUP_G - 1
@@ -780,6 +792,7 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
             s_y0[q] = r[g].x >> 16;
             s_w[q] = (r[g].y & 0xFFFFu) - (r[g].x & 0xFFFFu);
             s_depth[q] = r[g].z;
+            s_live[q] = r[g].w;
         }
     }
     uint32_t incl = wave_incl_scan(tsum);
@@ -809,6 +822,7 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
             const uint32_t x0 = r[g].x & 0xFFFFu, y0 = r[g].x >> 16, wdt = (r[g].y & 0xFFFFu) - x0;
             const uint32_t gi = (uint32_t)(i0 + g);
             for (uint32_t k = 0; k < t[g]; k++) {
+                if (!tile_live(r[g].w, k)) continue;  // culled (Camera::cull): not in the bucket
                 const uint32_t tile = (y0 + k / wdt) * (uint32_t)cam.gx + x0 + k % wdt;
                 const uint32_t pos = LDS_HIST ? atomicAdd(&s_cur[tile], 1u)
                                               : ranges[tile].x + atomicAdd(&cursor[tile * TILE_CTR_STRIDE], 1u);
@@ -826,6 +840,7 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
             if (s_incl[mid] > e) hi = mid; else lo = mid + 1;
         }
         const uint32_t local = e - ((lo == 0) ? 0u : s_incl[lo - 1]);
+        if (!tile_live(s_live[lo], local)) continue;  // culled (Camera::cull)
         const uint32_t wdt = s_w[lo];
         const uint32_t tile = (s_y0[lo] + local / wdt) * (uint32_t)cam.gx + s_x0[lo] + local % wdt;
         const uint32_t pos = LDS_HIST ? atomicAdd(&s_cur[tile], 1u)
