@@ -121,6 +121,9 @@ __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, E
 //                for every other chunk (staged in LDS), the number of that chunk's
 //                keys below it -- exact, as the keys are unique in a tile.
 // The result equals a stable (tile, depth) radix order (ids break depth ties).
+#ifndef GSR_FWD_DONE_EXIT
+#define GSR_FWD_DONE_EXIT 1  // forward walk: done lanes exit the loop (0: a wave-uniform ballot test per step)
+#endif
 #ifndef GSR_FWD_ABLATE
 #define GSR_FWD_ABLATE 0  // timing ablations (tools/gpu_round.sh ab=; results invalid except 5, 6): 1 no per-tile
                           // sort, 2 no walk, 4 no tracking-loss epilogue, 5 bounding-box block masks, 6 no block
@@ -333,7 +336,9 @@ __device__ __forceinline__ FwdPix fwd_tile(const Camera& cam, int tile, const ui
         const uint32_t pos16 = 16u * (start - range.x) + 16u;  // 16 (position of entry 0 + 1)
         dg.phase(2);
         for (int i = 0; i < (GSR_FWD_ABLATE == 2 ? 0 : n); i += 4) {
-            if (__ballot(!done) == 0ull) break;
+            // a lane whose pixel is done leaves the walk (the wave's loop ends when every lane has: exec-mask
+            // bookkeeping on the scalar unit -- a __ballot(!done) test cost 2 VALU per step)
+            if (GSR_FWD_DONE_EXIT ? done : __ballot(!done) == 0ull) break;
             int jb[4];  // byte offsets 16 j, one ds_read_u16 each (no unpacking on the VALU; volatile keeps
 #pragma unroll  // the four adjacent u16 loads from being merged into one b64 load + 4 VALU unpacks)
             for (int k = 0; k < 4; k++)
