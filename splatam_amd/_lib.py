@@ -93,6 +93,7 @@ SIGNATURES = {
     "gsr_abi_version": (c_int, []),
     "gsr_selftest_reduce9": (c_int, [c_void_p, c_void_p, c_void_p]),
     "gsr_timing_enable": (c_int, [c_int]),
+    "gsr_tile_cull": (c_int, [c_int]),
     "gsr_timing_read": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
     # include/gsr_glue.h: fused SplaTAM tracking glue
     "gsr_track_scratch_floats": (c_int, [c_int]),

@@ -860,6 +860,7 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         if (!POSE) {
             off = geo.offsets[i];
             cnt = geo.tiles[i];
+            tl = reinterpret_cast<const uint32_t*>(geo.bin)[4 * (size_t)i + 3];
         }
         // fixed-order sum of the Gaussian's instance records (deterministic)
         float acc[INST_REC_MAX];
@@ -1115,7 +1116,9 @@ gauss_bwd_mom_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict_
     const bool live = radii[i] > 0 && !guard.overflow();
     if (live) {  // fixed-order sum of the Gaussian's instance records (deterministic)
         const uint32_t off = geo.offsets[i], cnt = geo.tiles[i];
+        const uint32_t tl = reinterpret_cast<const uint32_t*>(geo.bin)[4 * (size_t)i + 3];  // (Camera::cull)
         for (uint32_t e = 0; e < cnt; e++) {
+            if (!tile_live(tl, e)) continue;
             const float2* r = reinterpret_cast<const float2*>(inst + (size_t)RS * (off + e));
             float2 v[RS / 2];
 #pragma unroll

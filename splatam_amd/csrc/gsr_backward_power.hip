@@ -327,7 +327,9 @@ gauss_bwd_power_kernel(GaussIn g, GeomPtrs geo, const int* __restrict__ radii, c
     for (int m = 0; m < NVP; m++) s[m] = 0.f;
     if (radii[i] > 0 && !guard.overflow()) {
         const uint32_t off = geo.offsets[i], cnt = geo.tiles[i];
+        const uint32_t tl = reinterpret_cast<const uint32_t*>(geo.bin)[4 * (size_t)i + 3];  // (Camera::cull)
         for (uint32_t e = 0; e < cnt; e++) {
+            if (!tile_live(tl, e)) continue;
             const float4* r = rec + (size_t)(off + e) * (NVP / 4);
 #pragma unroll
             for (int m = 0; m < NVP / 4; m++) {
@@ -683,14 +685,16 @@ gauss_bwd_fisher_kernel(int P, GeomPtrs geo, const int* __restrict__ radii, cons
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     if (radii[i] > 0 && !guard.overflow()) {
         const uint32_t off = geo.offsets[i], cnt = geo.tiles[i];
+        const uint32_t tl = reinterpret_cast<const uint32_t*>(geo.bin)[4 * (size_t)i + 3];  // (Camera::cull)
         constexpr int RU = 4;  // RU records' loads per memory round trip, added in instance order
         for (uint32_t e0 = 0; e0 < cnt; e0 += RU) {
             float4 v[RU];
 #pragma unroll
-            for (int k = 0; k < RU; k++) v[k] = e0 + k < cnt ? rec[off + e0 + k] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int k = 0; k < RU; k++)
+                v[k] = (e0 + k < cnt && tile_live(tl, e0 + k)) ? rec[off + e0 + k] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int k = 0; k < RU; k++)
-                if (e0 + k < cnt) {
+                if (e0 + k < cnt && tile_live(tl, e0 + k)) {
                     s.x += v[k].x;
                     s.y += v[k].y;
                     s.z += v[k].z;

@@ -267,37 +267,46 @@ def test_transform_fused_preprocess_bitwise(cuda, aniso, store, monkeypatch):
 
 @pytest.mark.parametrize("case", ["aniso", "config3"])
 def test_track_tile_cull_bitwise(cuda, case, monkeypatch):
-    """Tile culling (Camera::cull, the fused tracking forward in static mode): instances whose alpha >= 1/255
-    ellipse reaches no 4x4 block of their tile are left out of the tile lists.  Against the unculled lists
-    (the separate transform + gsr_track_forward_dual_static): loss, radii and pose gradients bitwise equal,
-    num_rendered (the record count) equal, and the longest tile list shorter at config 3."""
+    """Tile culling (gsr_tile_cull, every static-mode forward): instances whose alpha >= 1/255 ellipse reaches
+    no 4x4 block of their tile are left out of the tile lists.  Against the same static iterations with
+    culling off: loss, radii and pose gradients bitwise equal (transform fused or not, render backward fused
+    or not), num_rendered (the record count) equal, the longest tile list shorter at config 3."""
     from splatam_amd import glue
+    from splatam_amd._lib import lib
     from splatam_amd.scenes import config_scene
     from splatam_amd.slam import TrackingConfig
     params, curr = _setup(cuda, case == "aniso", config_scene(3) if case == "config3" else None)
     seed = torch.ones((), device=cuda)
-    outs = []
-    for fused in (False, True):  # fused: the transform inside preprocess (XF), which culls
-        for rfused in (False, True):  # separate render launches / render_track_kernel
-            monkeypatch.setattr(glue, "_XF_FUSED", fused)
-            monkeypatch.setattr(glue, "_RENDER_FUSED", rfused and fused)
-            p = _pose_leaves(params)
-            status = torch.zeros(4, dtype=torch.int32, device=cuda)
-            loss, radii = glue.tracking_iteration(p, curr, 1, TrackingConfig(), capacity=1200000, status=status,
-                                                  seed=seed)
-            torch.autograd.backward(loss, seed)
-            outs.append((loss.detach().clone(), radii.clone(), p["cam_unnorm_rots"].grad.clone(),
-                         p["cam_trans"].grad.clone(), status.clone()))
-            assert int(status[1]) == 0
-    l0, r0, q0, t0, s0 = outs[0]
-    for l1, r1, q1, t1, s1 in outs[2:]:
-        assert torch.equal(l0, l1) and torch.equal(r0, r1)
-        assert torch.equal(q0, q1) and torch.equal(t0, t1)
+    outs = {}
+    prev = lib.gsr_tile_cull(-1)
+    assert prev == 2
+    try:
+        for mode in (0, 2):
+            lib.gsr_tile_cull(mode)
+            for fused, rfused in ((False, False), (True, False), (True, True)):
+                monkeypatch.setattr(glue, "_XF_FUSED", fused)
+                monkeypatch.setattr(glue, "_RENDER_FUSED", rfused)
+                p = _pose_leaves(params)
+                status = torch.zeros(4, dtype=torch.int32, device=cuda)
+                loss, radii = glue.tracking_iteration(p, curr, 1, TrackingConfig(), capacity=1200000, status=status,
+                                                      seed=seed)
+                torch.autograd.backward(loss, seed)
+                outs[mode, fused, rfused] = (loss.detach().clone(), radii.clone(), p["cam_unnorm_rots"].grad.clone(),
+                                             p["cam_trans"].grad.clone(), status.clone())
+                assert int(status[1]) == 0
+    finally:
+        lib.gsr_tile_cull(prev)
+    l0, r0, q0, t0, s0 = outs[0, False, False]
+    for (mode, fused, rfused), (l1, r1, q1, t1, s1) in outs.items():
+        assert torch.equal(l0, l1) and torch.equal(r0, r1), (mode, fused, rfused)
+        assert torch.equal(q0, q1) and torch.equal(t0, t1), (mode, fused, rfused)
         assert int(s1[0]) == int(s0[0])
-        assert int(s1[2]) <= int(s0[2])
+        assert int(s1[2]) == int(outs[mode, False, False][4][2])
+    longest = {m: int(outs[m, True, True][4][2]) for m in (0, 2)}
+    print("longest tile list unculled / culled:", longest[0], longest[2])
+    assert longest[2] <= longest[0]
     if case == "config3":
-        print("longest tile list unculled / culled:", int(s0[2]), int(outs[2][4][2]))
-        assert int(outs[2][4][2]) < int(s0[2])
+        assert longest[2] < 0.85 * longest[0]
 
 
 @pytest.mark.parametrize("case", ["iso", "aniso", "config3"])
