@@ -137,10 +137,11 @@ def binning_gpu(scene, device="cuda:0", use_sh=False):
     e = torch.Tensor([])
     sh = scene.shs.to(dev) if use_sh else e
     col = e if use_sh else scene.colors.to(dev)
-    out = _C.rasterize_gaussians(torch.zeros(3, device=dev), scene.means3D.to(dev), col, scene.opacities.to(dev),
-                                 scene.scales.to(dev), scene.rotations.to(dev), 1.0, e, c.viewmatrix.to(dev),
-                                 c.projmatrix.to(dev), c.tanfovx, c.tanfovy, c.H, c.W, sh,
-                                 scene.sh_degree if use_sh else 0, c.campos.to(dev), False)
+    with _C.reference_binning():  # the reference's lists (tile culling would drop never-evaluated instances)
+        out = _C.rasterize_gaussians(torch.zeros(3, device=dev), scene.means3D.to(dev), col,
+                                     scene.opacities.to(dev), scene.scales.to(dev), scene.rotations.to(dev), 1.0, e,
+                                     c.viewmatrix.to(dev), c.projmatrix.to(dev), c.tanfovx, c.tanfovy, c.H, c.W, sh,
+                                     scene.sh_degree if use_sh else 0, c.campos.to(dev), False)
     n, color, radii, geom, binning, img, depth = out
     v = views(img, binning, c.W, c.H, n)
     res = {k: t.cpu().numpy() for k, t in v.items()}

@@ -445,6 +445,30 @@ def rasterize_gaussians_dual_backward(background, means3D, radii, colors, colors
         return (out[0], out[1], dcolors2, *out[2:])
 
 
+TILE_CULL_EVERY, TILE_CULL_STATIC, TILE_CULL_TRACK, TILE_CULL_NONE = 3, 2, 1, 0
+
+
+def tile_cull(mode: int | None = None) -> int:
+    """gsr_tile_cull (include/gsr_glue.h): the process-wide tile-culling mode -- 3 every forward (default),
+    2 the static-mode forwards only (the dynamic drop-in forward then builds the reference's binning), 1 the
+    fused tracking forward only, 0 none.  Returns the previous mode (mode None: only queries)."""
+    return int(lib.gsr_tile_cull(-1 if mode is None else int(mode)))
+
+
+class reference_binning:
+    """Context: the dynamic forward builds the reference's binning (rasterizer_impl.cu's num_rendered, ranges
+    and (tile, depth, id) point list, every instance of every rect tile) -- tile culling limited to the
+    static-mode forwards.  Outputs and gradients are the same bits either way; the oracle tests compare lists."""
+
+    def __enter__(self):
+        self.prev = tile_cull(TILE_CULL_STATIC)
+        return self
+
+    def __exit__(self, *exc):
+        tile_cull(self.prev)
+        return False
+
+
 def mark_visible(means3D, viewmatrix, projmatrix):
     """markVisible (rasterize_points.cu:198-216): bool[P], view_z > 0.001."""
     device = means3D.device

@@ -20,7 +20,7 @@
 #include "gsr_common.h"
 
 #ifndef GSR_TILE_CULL
-#define GSR_TILE_CULL 2  // Camera::cull: 2 = every static-mode forward, 1 = the fused tracking forward only, 0 = none
+#define GSR_TILE_CULL 3  // Camera::cull: 3 = every forward, 2 = the static-mode ones, 1 = the fused tracking one, 0 = none
 #endif
 #include <atomic>
 static std::atomic<int> g_tile_cull{GSR_TILE_CULL};  // gsr_tile_cull
@@ -363,10 +363,9 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     }
     static const bool force_radix_env = getenv("GSR_FORCE_RADIX") && atoi(getenv("GSR_FORCE_RADIX")) != 0;
     const bool force_radix = force_radix_env && capacity <= 0;
-    // tile culling in the static-mode forwards (the speculative bucketed path is final there; the dynamic
-    // drop-in forward keeps the reference's binning: its exact re-launch may take the radix path)
+    // tile culling (gsr_tile_cull): mode 3 every forward, 2 the static-mode ones, 1 the fused tracking one
     const int cull_mode = g_tile_cull.load(std::memory_order_relaxed);
-    cam.cull = ((cull_mode >= 2 || (cull_mode == 1 && xf)) && capacity > 0 && lds_hist) ? 1 : 0;
+    cam.cull = (cull_mode >= 3 || (cull_mode == 2 && capacity > 0) || (cull_mode == 1 && xf && capacity > 0)) ? 1 : 0;
     // the bucketed duplicate's workgroup 0 writes the render schedule (tile_plan); the other paths
     // render in row-major order
     Camera cplan = cam;
@@ -924,7 +923,7 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
 }
 
 int gsr_tile_cull(int mode) {
-    return mode < 0 ? g_tile_cull.load() : g_tile_cull.exchange(mode > 2 ? 2 : mode);
+    return mode < 0 ? g_tile_cull.load() : g_tile_cull.exchange(mode > 3 ? 3 : mode);
 }
 
 int gsr_timing_enable(int on) {

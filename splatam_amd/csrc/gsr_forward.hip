@@ -479,7 +479,7 @@ hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, 
 __global__ void __launch_bounds__(PRE_BLOCK)
 duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, uint32_t* __restrict__ gid) {
     __shared__ uint32_t s_incl[PRE_BLOCK];   // inclusive scan of tiles touched
-    __shared__ uint32_t s_x0[PRE_BLOCK], s_y0[PRE_BLOCK], s_w[PRE_BLOCK], s_depth[PRE_BLOCK];
+    __shared__ uint32_t s_x0[PRE_BLOCK], s_y0[PRE_BLOCK], s_w[PRE_BLOCK], s_depth[PRE_BLOCK], s_live[PRE_BLOCK];
     __shared__ uint32_t wsum[PRE_BLOCK / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, R = (int)blockDim.x;  // R = 1 << pre_shift
     const int i = (blockIdx.x << cam.pre_shift) + tid;
@@ -492,6 +492,7 @@ duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, u
         s_y0[tid] = r.x >> 16;
         s_w[tid] = (r.y & 0xFFFFu) - (r.x & 0xFFFFu);
         s_depth[tid] = r.z;
+        s_live[tid] = r.w;
     }
     __syncthreads();
     uint32_t woff = 0;
@@ -516,7 +517,10 @@ duplicate_kernel(Camera cam, int P, GeomPtrs geo, uint64_t* __restrict__ keys, u
         const uint32_t tx = s_x0[lo] + local % wdt;
         const uint32_t u = base + e;
         const uint32_t gi = (blockIdx.x << cam.pre_shift) + lo;
-        keys[u] = ((uint64_t)(ty * (uint32_t)cam.gx + tx) << 32) | (uint64_t)s_depth[lo];
+        // a culled instance (Camera::cull) sorts behind every tile (tile id gx * gy, within the sorted bits), so
+        // the live ones take the positions the culled tile counts' ranges give them
+        const uint32_t tkey = tile_live(s_live[lo], local) ? ty * (uint32_t)cam.gx + tx : (uint32_t)(cam.gx * cam.gy);
+        keys[u] = ((uint64_t)tkey << 32) | (uint64_t)s_depth[lo];
         gid[u] = gi;
     }
 }

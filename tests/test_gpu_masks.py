@@ -62,10 +62,11 @@ def test_block_masks_conservative_and_tight(cuda, which):
     s = config_scene(1) if which == "config1" else make_scene(6000, 192, 144, seed=5, anisotropic=True)
     c = s.cam
     e = torch.Tensor([])
-    out = _C.rasterize_gaussians(torch.zeros(3, device=cuda), s.means3D.to(cuda), s.colors.to(cuda),
-                                 s.opacities.to(cuda), s.scales.to(cuda), s.rotations.to(cuda), 1.0, e,
-                                 c.viewmatrix.to(cuda), c.projmatrix.to(cuda), c.tanfovx, c.tanfovy, c.H, c.W, e,
-                                 0, c.campos.to(cuda), False)
+    with _C.reference_binning():  # the oracle's lists, entry for entry
+        out = _C.rasterize_gaussians(torch.zeros(3, device=cuda), s.means3D.to(cuda), s.colors.to(cuda),
+                                     s.opacities.to(cuda), s.scales.to(cuda), s.rotations.to(cuda), 1.0, e,
+                                     c.viewmatrix.to(cuda), c.projmatrix.to(cuda), c.tanfovx, c.tanfovy, c.H, c.W,
+                                     e, 0, c.campos.to(cuda), False)
     n, img, binning = out[0], out[5], out[4]
     v = views(img, binning, c.W, c.H, n)
     torch.cuda.synchronize()

@@ -107,17 +107,25 @@ def test_bitwise_deterministic_backward(cuda):
         assert np.array_equal(a["grads"][k], b["grads"][k]), k
 
 
-def _binning_gpu(scene, cuda):
+def _binning_gpu(scene, cuda, mode=2):
+    """The dynamic forward's binning; mode (gsr_tile_cull) 2: the reference's lists, 3: tile-culled lists."""
     from splatam_amd import _C
     from splatam_amd.layout import views
     c = scene.cam
-    out = _C.rasterize_gaussians(torch.zeros(3, device=cuda), scene.means3D.to(cuda), scene.colors.to(cuda),
-                                 scene.opacities.to(cuda), scene.scales.to(cuda), scene.rotations.to(cuda), 1.0,
-                                 torch.Tensor([]), c.viewmatrix.to(cuda), c.projmatrix.to(cuda), c.tanfovx,
-                                 c.tanfovy, c.H, c.W, torch.Tensor([]), 0, c.campos.to(cuda), False)
+    prev = _C.tile_cull(mode)
+    try:
+        out = _C.rasterize_gaussians(torch.zeros(3, device=cuda), scene.means3D.to(cuda), scene.colors.to(cuda),
+                                     scene.opacities.to(cuda), scene.scales.to(cuda), scene.rotations.to(cuda), 1.0,
+                                     torch.Tensor([]), c.viewmatrix.to(cuda), c.projmatrix.to(cuda), c.tanfovx,
+                                     c.tanfovy, c.H, c.W, torch.Tensor([]), 0, c.campos.to(cuda), False)
+    finally:
+        _C.tile_cull(prev)
     n, color, radii, geom, binning, img, depth = out
     v = views(img, binning, c.W, c.H, n)
-    return n, {k: t.cpu().numpy() for k, t in v.items()}
+    res = {k: t.cpu().numpy() for k, t in v.items()}
+    res["radii"] = radii.cpu().numpy()
+    res["color"], res["depth"] = color.cpu().numpy(), depth.cpu().numpy()
+    return n, res
 
 
 BIN_CASES = [
@@ -152,6 +160,59 @@ def test_binning_bit_exact(cuda, case):
         assert cnt_ref.max() <= 4096
         for lo, hi in ((1024, 2048), (2048, 3072), (3072, 4096)):
             assert ((cnt_ref > lo) & (cnt_ref <= hi)).any(), (lo, hi)
+
+
+@pytest.mark.parametrize("case", BIN_CASES, ids=[c["name"] for c in BIN_CASES])
+def test_tile_cull_drops_only_unreached_instances(cuda, case):
+    """Tile culling in the dynamic drop-in forward (gsr_tile_cull mode 3, every binning path: bucketed,
+    chunked, radix fallback with the culled instances keyed behind every tile, global-atomic counts): every
+    tile list is an order-preserving subsequence of the reference's list (mode 2), an instance is dropped only
+    where no pixel of its tile reaches alpha >= 1/255 (float64, margin), num_rendered, radii, images and every
+    gradient are bitwise those of the reference's lists."""
+    from splatam_amd import _C
+    scene = make_scene(case["P"], case["W"], case["H"], seed=13, anisotropic=case["aniso"],
+                       z_range=(0.5, 1.0) if case.get("near") else (0.5, 5.0))
+    scene.scales *= case.get("scale", 1.0)
+    c = scene.cam
+    fr, _ = harness.run_oracle(scene, backward=False)
+    n2, v2 = _binning_gpu(scene, cuda, mode=2)
+    n3, v3 = _binning_gpu(scene, cuda, mode=3)
+    assert n2 == n3 == fr.num_rendered
+    for k in ("radii", "color", "depth"):
+        assert np.array_equal(v2[k], v3[k]), k
+    gx = (c.W + 15) // 16
+    m2, co = fr.means2D.astype(np.float64), fr.conic_opacity.astype(np.float64)
+    ly, lx = np.meshgrid(np.arange(16), np.arange(16), indexing="ij")
+    dropped = 0
+    for t in range(len(v2["ranges"])):
+        a2, b2 = (int(x) for x in v2["ranges"][t])
+        a3, b3 = (int(x) for x in v3["ranges"][t])
+        full = v2["point_list"][a2:b2].astype(np.int64) if b2 > a2 else np.zeros(0, np.int64)
+        kept = v3["point_list"][a3:b3].astype(np.int64) if b3 > a3 else np.zeros(0, np.int64)
+        sel = np.isin(full, kept)
+        np.testing.assert_array_equal(full[sel], kept)  # an order-preserving subsequence
+        gone = full[~sel].astype(np.int64)
+        dropped += len(gone)
+        if len(gone):
+            X, Y = (t % gx) * 16 + lx.ravel(), (t // gx) * 16 + ly.ravel()
+            inside = (X < c.W) & (Y < c.H)
+            dx, dy = m2[gone, 0][:, None] - X[None], m2[gone, 1][:, None] - Y[None]
+            A, B, C, o = (co[gone, k][:, None] for k in range(4))
+            power = -0.5 * (A * dx * dx + C * dy * dy) - B * dx * dy
+            alpha = o * np.exp(np.minimum(power, 0.0))
+            assert not ((power <= 0) & (alpha >= 0.99 / 255.0) & inside[None]).any(), t
+    print(f"{case['name']}: {dropped} of {n2} instances culled")
+    if case["name"] not in ("many_tiles", "long_lists"):  # (long_lists: every Gaussian reaches all six tiles)
+        assert dropped > 0
+    dpix = np.random.RandomState(3).randn(3, c.H, c.W).astype(np.float32)
+    prev = _C.tile_cull(2)
+    try:
+        a = harness.run_gpu(scene, dpix)
+    finally:
+        _C.tile_cull(prev)
+    b = harness.run_gpu(scene, dpix)
+    for k in a["grads"]:
+        assert np.array_equal(a["grads"][k], b["grads"][k]), k
 
 
 POWER_CASES = [
@@ -358,8 +419,11 @@ def test_block_masks_are_conservative(cuda, aniso):
     rng = v["ranges"].long()
     gx = (c.W + 15) // 16
     tile_of = torch.repeat_interleave(torch.arange(rng.shape[0], device=dev), (rng[:, 1] - rng[:, 0]).clamp(min=0))
-    gid = v["point_list"].long()[:n]
-    mask = v["block_masks"].long()[:n] & 0xFFFF
+    # the listed entries: the ranges' total (num_rendered counts record slots, culled instances included)
+    nl = int((rng[:, 1] - rng[:, 0]).clamp(min=0).sum())
+    assert nl <= n
+    gid = v["point_list"].long()[:nl]
+    mask = v["block_masks"].long()[:nl] & 0xFFFF
     ty, tx = tile_of // gx, tile_of % gx
     ly, lx = torch.meshgrid(torch.arange(16, device=dev), torch.arange(16, device=dev), indexing="ij")
     px = (tx * 16)[:, None, None] + lx[None]
@@ -370,7 +434,7 @@ def test_block_masks_are_conservative(cuda, aniso):
     ok = (pw <= 0) & (al >= 1.0 / 255.0 * 0.999) & (px < c.W) & (py < c.H)
     # block (cx, cy) of the tile -> mask bit 4 (2 (cy >> 1) + (cx >> 1)) + 2 (cy & 1) + (cx & 1)
     blk = ok.reshape(-1, 4, 4, 4, 4).any(4).any(2)  # [inst, cy, cx]
-    bits = torch.zeros(n, dtype=torch.long, device=dev)
+    bits = torch.zeros(nl, dtype=torch.long, device=dev)
     for cy in range(4):
         for cx in range(4):
             bit = 4 * (2 * (cy >> 1) + (cx >> 1)) + 2 * (cy & 1) + (cx & 1)
@@ -380,7 +444,7 @@ def test_block_masks_are_conservative(cuda, aniso):
     nc = v["n_contrib"].reshape(c.H, c.W).long()
     nc = torch.nn.functional.pad(nc, (0, gx * 16 - c.W, 0, ((c.H + 15) // 16) * 16 - c.H))
     tile_last = nc.reshape((c.H + 15) // 16, 16, gx, 16).amax(dim=(1, 3)).reshape(-1)
-    pos = torch.arange(n, device=dev) - rng[tile_of, 0]
+    pos = torch.arange(nl, device=dev) - rng[tile_of, 0]
     staged = pos < tile_last[tile_of]
     missed = ((bits & ~mask) != 0) & staged
     assert int(staged.sum()) > 0

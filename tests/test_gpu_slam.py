@@ -267,7 +267,7 @@ def test_transform_fused_preprocess_bitwise(cuda, aniso, store, monkeypatch):
 
 @pytest.mark.parametrize("case", ["aniso", "config3"])
 def test_track_tile_cull_bitwise(cuda, case, monkeypatch):
-    """Tile culling (gsr_tile_cull, every static-mode forward): instances whose alpha >= 1/255 ellipse reaches
+    """Tile culling (gsr_tile_cull, every forward): instances whose alpha >= 1/255 ellipse reaches
     no 4x4 block of their tile are left out of the tile lists.  Against the same static iterations with
     culling off: loss, radii and pose gradients bitwise equal (transform fused or not, render backward fused
     or not), num_rendered (the record count) equal, the longest tile list shorter at config 3."""
@@ -279,7 +279,7 @@ def test_track_tile_cull_bitwise(cuda, case, monkeypatch):
     seed = torch.ones((), device=cuda)
     outs = {}
     prev = lib.gsr_tile_cull(-1)
-    assert prev == 2
+    assert prev == 3  # the default: every forward culls
     try:
         for mode in (0, 2):
             lib.gsr_tile_cull(mode)

@@ -32,6 +32,8 @@
 #   clk              GRBM_COUNT / GRBM_GUI_ACTIVE per render_track launch over the drift run (clock per launch)
 #   sqab=TAGS        SQ instruction counts (VALU / SALU / LDS per launch) of render_track (SQRX: another kernel
 #                    regex) for libgsr.so and each _diag/libgsr_<tag>.so
+#   abdropin=TAGS    interleaved A/B (two rounds) of the bench line with the drop-in legs (unchanged-caller tracking loop,
+#                    raster unit, their render stage times)
 #   abflag=FLAG:V1,V2[,...]  interleaved A/B (two rounds) of the light bench line over the values of one bench.py
 #                    flag, e.g. abflag=--fuse-render:1,0
 TAG=${1:-x}; shift
@@ -150,6 +152,23 @@ import json, sys
 b = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][-1]
 print("abbench", sys.argv[2], "round", sys.argv[3], "frames/s", b["value"], "render_bwd", b["roofline"]["avg_us"],
       "render_fwd", b["stages_us"]["render_fwd"], "mapping it/s", (b.get("mapping") or {}).get("value"))
+PY
+            done
+          done ;;
+    abdropin=*) TAGS=${s#abdropin=}
+          for r in 1 2; do
+            ORDER="base ${TAGS//,/ }"
+            [ $r = 2 ] && ORDER=$(echo $ORDER | tr ' ' '\n' | tac | tr '\n' ' ')
+            for t in $ORDER; do
+              f="$OUT/abdropin_${t}_$r.log"
+              GSR_LIB_AB=1 GSR_LIB=$(lib_of $t) timeout -k 10 400 python bench.py --cpu-baseline off --fisher off --mapping off \
+                  --configs off --unfused-leg off > "$f" 2>&1 || { echo "abdropin $t failed"; tail -20 "$f"; exit 1; }
+              python - "$f" $t $r <<'PY' | tee -a "$OUT/abdropin.txt"
+import json, sys
+b = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][-1]
+d = b["dropin"]
+print("abdropin", sys.argv[2], "round", sys.argv[3], "frames/s", b["value"], "dropin", d["value"], "raster_unit",
+      d["raster_unit"]["value"], "render_bwd", d["render_bwd"]["avg_us"], "stages", d["stages_us"])
 PY
             done
           done ;;

@@ -129,7 +129,7 @@ def main():
     s = config_scene(int(sys.argv[1]) if len(sys.argv) > 1 else 3)
     params = init_tracking_params(s, 1, dev)
     cam = camera_settings(s.cam, dev)
-    with torch.no_grad():
+    with torch.no_grad(), _C.reference_binning():  # every rect instance listed (the statistic is about them)
         tg = transform_to_frame(params, 0, False, False)
         rv = transformed_params2rendervar(params, tg)
         W, H = s.cam.W, s.cam.H
