@@ -123,3 +123,31 @@ def test_fisher_selective_config3(cuda):
         r_ref = harness.rel_l2(sel["grads"][k], ref[k].reshape(sel["grads"][k].shape))
         print(f"config 3 {k}: rel L2 vs full path {r_full:.2e}, vs oracle {r_ref:.2e}")
         assert r_full <= 2e-5 and r_ref <= 1e-4, (k, r_full, r_ref)
+
+
+def test_batched_fisher_tile_cull_bitwise(cuda):
+    """Tile culling in the Fisher launches (static forwards + backward_power=2 moments): the visited-pose
+    Hessian sum and the candidate scores are bitwise those with culling off."""
+    from splatam_amd import _C
+    from splatam_amd.fisher import BatchedFisher
+    scene = make_scene(3000, 96, 72, seed=22)
+    params = init_tracking_params(scene, num_frames=1, device=cuda)
+    cam = camera_settings(scene.cam, cuda)
+    sc = FisherScorer(params, cam)
+    poses = [_pose(d, [0.01 * d, -0.005 * d, 0.02]).to(cuda) for d in (-4.0, -2.0, 0.0, 1.5)]
+    out = {}
+    prev = _C.tile_cull()
+    try:
+        for mode in (0, 3):
+            _C.tile_cull(mode)
+            bs = BatchedFisher(sc, 4, mode="sum", probe_w2cs=poses)
+            h = bs.hessian_sum(poses).clone()
+            sc.fit_visited(poses, batch=bs)
+            bsc = BatchedFisher(sc, 4, mode="scores", probe_w2cs=poses)
+            s = sc.eig_scores(poses, batch=bsc).clone()
+            torch.cuda.synchronize()
+            out[mode] = (h, s)
+    finally:
+        _C.tile_cull(prev)
+    assert float(out[0][0].abs().sum()) > 0
+    assert torch.equal(out[0][0], out[3][0]) and torch.equal(out[0][1], out[3][1])

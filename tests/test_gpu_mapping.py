@@ -422,3 +422,35 @@ def test_sh_colour_adam_fused_bitwise(cuda, monkeypatch):
         assert float((p1[k] - params[k]).abs().max()) > 0.0, k
     for a, b in zip(s0, s1):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("sh", [False, True])
+def test_graph_mapper_tile_cull_bitwise(cuda, sh):
+    """Tile culling (gsr_tile_cull, every forward by default) in the captured mapping frame: parameters after
+    two 6-iteration replays are bitwise those of the same frame with culling off (static dual forward, SH or
+    RGB colours, the 10-sum render backward, gauss_bwd skipping the culled record slots)."""
+    from splatam_amd import _C
+    from splatam_amd.mapper import GraphMapper
+    _, params, cam = _map_params(cuda, True, sh)
+    kfs = _keyframes(params, cam, cuda)
+    key = slam.color_key(params)
+    keys = GAUSS_KEYS + (key,)
+    res = {}
+    prev = _C.tile_cull()
+    try:
+        for mode in (0, 3):
+            _C.tile_cull(mode)
+            p = {k: v.clone() for k, v in params.items()}
+            for k in keys:
+                p[k].requires_grad_(True)
+            mapper = GraphMapper(p, kfs, iters_per_graph=6, seed=7, prune=False)
+            for _ in range(2):
+                mapper.run()
+            torch.cuda.synchronize()
+            assert not mapper.overflowed()
+            res[mode] = {k: p[k].detach().clone() for k in keys}
+    finally:
+        _C.tile_cull(prev)
+    for k in keys:
+        assert float((res[3][k] - params[k]).abs().max()) > 0.0, k
+        assert torch.equal(res[0][k], res[3][k]), k
