@@ -22,7 +22,8 @@
 #define GSR_PHASE 0
 #endif
 #ifndef GSR_ABLATE
-#define GSR_ABLATE 0  // render_bwd / gauss_bwd timing ablations (1 no row reduction, 2 no entry totals, 3-5 pose tail)
+#define GSR_ABLATE 0  // render_bwd / gauss_bwd timing ablations (1 no row reduction, 2 no entry totals, 3-5 pose tail,
+                      // 6 no tracking-loss arrival / sum)
 #endif
 
 namespace gsr {

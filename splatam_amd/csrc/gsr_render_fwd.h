@@ -408,6 +408,7 @@ __device__ __forceinline__ FwdPix fwd_tile(const Camera& cam, int tile, const ui
 // The tracking loss from the workgroups' published partials: the last workgroup to arrive adds them in
 // tile order and writes l1.loss (every thread of every workgroup calls it, after its partial store)
 __device__ __forceinline__ void l1_finish(const TrackL1& l1) {
+    if constexpr (kAblate == 6) return;  // timing ablation: no loss arrival / sum (loss invalid)
     __shared__ float s_fin[16];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, row4 = lane >> 4;
     const int nb = gridDim.x * gridDim.y;
