@@ -121,6 +121,9 @@ __device__ void tile_sort_regs(const uint64_t* __restrict__ src, uint32_t cnt, E
 //                for every other chunk (staged in LDS), the number of that chunk's
 //                keys below it -- exact, as the keys are unique in a tile.
 // The result equals a stable (tile, depth) radix order (ids break depth ties).
+#ifndef GSR_FWD_PAIR25
+#define GSR_FWD_PAIR25 1  // dual forward walk: channels 2 and 5 blended by one v_pk_fma (0: two v_fmac)
+#endif
 #ifndef GSR_FWD_DONE_EXIT
 #define GSR_FWD_DONE_EXIT 1  // forward walk: done lanes exit the loop (0: a wave-uniform ballot test per step)
 #endif
@@ -312,7 +315,9 @@ __device__ __forceinline__ FwdPix fwd_tile(const Camera& cam, int tile, const ui
 #endif
             s_a[tid] = pa;
             s_b[tid] = pb;
-            s_c[tid] = pc;
+            // (DUAL: the second set's third channel rides in s_c.w -- the walk blends channels (0, 1), (2, 5)
+            // and (3, 4) as three pairs -- and the rect half it replaces is not read after staging)
+            s_c[tid] = (DUAL && GSR_FWD_PAIR25) ? make_float4(pc.x, pc.y, pc.z, pd.z) : pc;
             if (DUAL) s_d[tid] = pd;
             s_mask[tid] = (uint16_t)pm;
             ent = ((PointEntry)pm << 32) | pg;  // the mask, for render_bwd (stored below)
@@ -374,10 +379,17 @@ __device__ __forceinline__ FwdPix fwd_tile(const Camera& cam, int tile, const ui
                 if (blend) {
                     const float wgt = alpha[k] * T;
                     C01 = __builtin_elementwise_fma(v2f{c.x, c.y}, v2f{wgt, wgt}, C01);
-                    C2 += c.z * wgt;
-                    if (DUAL) {
+                    if (DUAL && GSR_FWD_PAIR25) {  // the same fused products per channel, two per instruction
+                        const v2f c25 = __builtin_elementwise_fma(v2f{c.z, c.w}, v2f{wgt, wgt}, v2f{C2, C5});
+                        C2 = c25.x;
+                        C5 = c25.y;
                         C34 = __builtin_elementwise_fma(v2f{c2.x, c2.y}, v2f{wgt, wgt}, C34);
-                        C5 += c2.z * wgt;
+                    } else {
+                        C2 += c.z * wgt;
+                        if (DUAL) {
+                            C34 = __builtin_elementwise_fma(v2f{c2.x, c2.y}, v2f{wgt, wgt}, C34);
+                            C5 += c2.z * wgt;
+                        }
                     }
                     if (T > 0.5f && test_T < 0.5f) D = depth[k];  // median depth (forward.cu:368-372)
                     T = test_T;
