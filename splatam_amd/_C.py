@@ -38,6 +38,28 @@ def _alloc(ctx, kind, nbytes):  # called from C, under the GIL
 
 _ALLOC_CB = ALLOC_FN(_alloc)
 
+# The native torch binding (csrc/gsr_torch.cpp, built in-tree by splatam_amd.build next to libgsr.so) takes
+# the drop-in path's per-iteration calls -- rasterize_gaussians in dynamic mode and
+# rasterize_gaussians_backward -- at a fraction of this module's Python host cost; the same library
+# calls, so the same bits.  GSR_NATIVE_BINDING=0 keeps them on ctypes (A/B, tests).
+_NATIVE_ON = os.environ.get("GSR_NATIVE_BINDING", "1") != "0"
+_native_mod = None
+
+
+def _native():
+    global _native_mod
+    if _native_mod is None:
+        from . import _gsr_torch  # noqa: F401  (ImportError: run `python -m splatam_amd.build`)
+        _native_mod = _gsr_torch
+    return _native_mod
+
+
+_EMPTY = torch.Tensor([])
+
+
+def _t(x):  # None -> the empty tensor the reference passes for an absent input
+    return _EMPTY if x is None else x
+
 
 def _begin(device):
     _tls.device = device
@@ -228,6 +250,11 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     capacity > 0 selects gsr_forward_static (no host synchronisation, HIP-graph capturable; `status` is a
     device int32[4] receiving the sticky counters, and num_rendered is the capacity).
     """
+    if _NATIVE_ON and capacity <= 0 and not _GEOM_CACHE:
+        return _native().rasterize_gaussians(
+            _t(background), means3D, _t(colors), _t(opacity), _t(scales), _t(rotations), float(scale_modifier),
+            _t(cov3D_precomp), _t(viewmatrix), _t(projmatrix), float(tan_fovx), float(tan_fovy), int(image_height),
+            int(image_width), _t(sh), int(degree), _t(campos), bool(prefiltered))
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     device = means3D.device
@@ -298,6 +325,12 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     precomputed colours (scripts/ros_handler.py:884-889 reads no other gradient) -- which runs the
     4-value-per-pair kernel; any other power != 1 request forms every gradient.
     """
+    if _NATIVE_ON:
+        return tuple(_native().rasterize_gaussians_backward(
+            _t(background), means3D, radii, _t(colors), _t(scales), _t(rotations), float(scale_modifier),
+            _t(cov3D_precomp), _t(viewmatrix), _t(projmatrix), float(tan_fovx), float(tan_fovy), dL_dout_color, _t(sh),
+            int(degree), _t(campos), geomBuffer, int(R), binningBuffer, imageBuffer, int(power),
+            [] if needs is None else [bool(x) for x in needs]))
     device = means3D.device
     P = means3D.size(0)
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))

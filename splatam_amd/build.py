@@ -63,7 +63,40 @@ def build(force: bool = False) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    build_torch_binding()
     return LIB
+
+
+TORCH_SRC = os.path.join(CSRC, "gsr_torch.cpp")
+
+
+def torch_binding_path() -> str:
+    import sysconfig
+    return os.path.join(HERE, "_gsr_torch" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_torch_binding() -> str:
+    """The native torch binding of the drop-in path's per-iteration calls (csrc/gsr_torch.cpp): a host-only
+    pybind11 module over libgsr.so (linked with an $ORIGIN rpath), in-tree so it travels with libgsr.so."""
+    import sysconfig
+
+    import torch
+    from torch.utils import cpp_extension as ce
+    out = torch_binding_path()
+    deps = [TORCH_SRC, os.path.join(ROOT, "include", "gsr.h")]  # (libgsr.so is resolved at load time)
+    if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
+        return out
+    inc = ce.include_paths() + [sysconfig.get_paths()["include"], os.path.join(ROOT, "include"), "/opt/rocm/include"]
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = [hipcc(), "-x", "c++", "-std=c++17", "-O2", "-fPIC", "-shared", "-w", "-D__HIP_PLATFORM_AMD__=1",
+           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_gsr_torch", "-DTORCH_API_INCLUDE_EXTENSION_H",
+           *[f"-I{d}" for d in inc], TORCH_SRC, "-o", out, f"-L{tlib}", f"-L{HERE}", "-lgsr", "-lc10", "-lc10_hip",
+           "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{tlib}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"torch binding build failed:\n{r.stdout[-4000:]}\n{r.stderr[-4000:]}")
+    return out
 
 
 def build_diag() -> str:
