@@ -81,10 +81,11 @@ at::Tensor cam_f32(const at::Tensor& t, const at::Device& dev, const char* name,
         if (p.get() == impl && e.version == t._version() && e.stream == s && e.copy.device() == dev) return e.copy;
     }
     at::Tensor c = dev_f32(t, dev, name);
-    if (g_cam.size() >= 64) {
+    if (g_cam.size() >= 64) {  // drop the dead entries; still full: drop the oldest half (bounded either way)
         std::vector<CamEntry> live;
         for (auto& e : g_cam)
             if (!e.src.expired()) live.push_back(e);
+        if (live.size() >= 64) live.erase(live.begin(), live.begin() + 32);
         g_cam.swap(live);
     }
     g_cam.push_back(CamEntry{c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>(t.getIntrusivePtr()),
