@@ -108,9 +108,12 @@ def _cam_f32(t: torch.Tensor, device, name: str, stream: int) -> torch.Tensor | 
     if e is not None and e[0]() is t and e[1] == t._version and e[2] == stream and e[3].device == device:
         return e[3]
     c = _dev_f32(t, device, name)
-    if len(cache) >= 64:
+    if len(cache) >= 64:  # drop the dead entries; still full: the oldest half (bounded either way)
         for k in [k for k, v in cache.items() if v[0]() is None]:
             del cache[k]
+        if len(cache) >= 64:
+            for k in list(cache)[:32]:
+                del cache[k]
     cache[id(t)] = (weakref.ref(t), t._version, stream, c)
     return c
 
