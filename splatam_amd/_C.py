@@ -41,8 +41,9 @@ _ALLOC_CB = ALLOC_FN(_alloc)
 # The native torch binding (csrc/gsr_torch.cpp, built in-tree by splatam_amd.build next to libgsr.so) takes
 # the drop-in path's per-iteration calls -- rasterize_gaussians in dynamic mode and
 # rasterize_gaussians_backward -- at a fraction of this module's Python host cost; the same library
-# calls, so the same bits.  GSR_NATIVE_BINDING=0 keeps them on ctypes (A/B, tests).
-_NATIVE_ON = os.environ.get("GSR_NATIVE_BINDING", "1") != "0"
+# calls, so the same bits.  GSR_NATIVE_BINDING=0 keeps them on ctypes (A/B, tests).  The binding links the
+# in-tree libgsr.so, so a library loaded from another path (GSR_LIB: A/B builds) keeps every call on ctypes.
+_NATIVE_ON = os.environ.get("GSR_NATIVE_BINDING", "1") != "0" and not os.environ.get("GSR_LIB")
 _native_mod = None
 
 

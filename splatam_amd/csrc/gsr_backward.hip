@@ -22,6 +22,9 @@
 #include "gsr_glue_common.h"
 #include "gsr_render_fwd.h"
 
+#ifndef GSR_PK_XD
+#define GSR_PK_XD 1  // the tile walk's e Tn and alpha Tn as one packed multiply
+#endif
 #ifndef GSR_POSE_TAIL
 #define GSR_POSE_TAIL 2  // levels of the fused pose reduction's last-workgroup sum (1 or 2)
 #endif
@@ -32,6 +35,20 @@ namespace gsr {
 // h = G * dL/dG = (o * G) * dL/dalpha.
 template <bool OPAC>
 __device__ __forceinline__ void pair_geom(float* vk, float araw, float dLa, float G, v2f d) {
+#if GSR_PK_XD
+    if constexpr (OPAC) {  // (araw dLa, G dLa): one v_pk_mul_f32, the same two products
+        const v2f ho = v2f{araw, G} * dLa;
+        const v2f hv = ho.x * d;
+        const v2f hh = hv.x * d;
+        vk[0] = hv.x;
+        vk[1] = hv.y;
+        vk[2] = hh.x;
+        vk[3] = hh.y;
+        vk[4] = hv.y * d.y;
+        vk[5] = ho.y;
+        return;
+    }
+#endif
     const v2f hv = (araw * dLa) * d;  // (hx, hy)
     const v2f hh = hv.x * d;          // (hx dx, hx dy)
     vk[0] = hv.x;
@@ -496,9 +513,15 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
                 const float inv = __builtin_amdgcn_rcpf(1.f - alpha[k]);   // v_rcp_f32 (~1 ulp)
                 const float Tn = T * inv;                                   // T / (1 - alpha), backward.cu:978
                 const float e = cd - A;
+#if GSR_PK_XD
+                const v2f xd = v2f{e, alpha[k]} * Tn;  // (e Tn, alpha Tn): one v_pk_mul_f32, the same two products
+                const float x = xd.x;
+                dch[k] = xd.y;                          // 0 when masked
+#else
                 const float x = e * Tn;
-                dLa[k] = (OPAC && !ok[k]) ? 0.f : x;    // (without OPAC: h = araw dLa is 0 when masked)
                 dch[k] = alpha[k] * Tn;                 // 0 when masked
+#endif
+                dLa[k] = (OPAC && !ok[k]) ? 0.f : x;    // (without OPAC: h = araw dLa is 0 when masked)
                 T = Tn;  // masked pairs: alpha = 0 and v_rcp_f32(1) == 1 exactly (tools/micro/rcp_one.hip)
                 A = __builtin_fmaf(alpha[k], e, A);     // unchanged when masked
             }
@@ -511,7 +534,12 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
                 MomIn e[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
+#if GSR_PK_XD
+                    const v2f ho = v2f{araw[k], G[k]} * dLa[k];
+                    const float h = ho.x, o = ho.y;
+#else
                     const float h = araw[k] * dLa[k], o = G[k] * dLa[k];
+#endif
                     const float hx = h * d[k].x, hy = h * d[k].y;
                     e[k].m20 = hx * hx;
                     e[k].m11 = hx * hy;

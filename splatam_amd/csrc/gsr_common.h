@@ -1035,6 +1035,9 @@ __device__ __forceinline__ void wave_reduce2x9(const float (&v)[18], float (&r)[
 #ifndef GSR_DPP_BANKMASK
 #define GSR_DPP_BANKMASK 1
 #endif
+#ifndef GSR_REDUCE_PIN
+#define GSR_REDUCE_PIN 1
+#endif
 template <int NV>
 struct RowReduce {
     static constexpr int V = 4 * NV;
@@ -1113,6 +1116,13 @@ __device__ __forceinline__ void row_reduce(const float (&v)[4 * NV], float (&r)[
         row_tstep<V / 4, 0x4E>(b, c, lane & 2);
         row_tstep<V / 8, 0xB1>(c, r, lane & 1);
     }
+#if GSR_REDUCE_PIN
+    // the totals formed here, in every lane: otherwise the compiler sinks the plain steps' adds into the
+    // caller's writer-lane branch, where a DPP read of a disabled lane is invalid, so each step becomes
+    // v_mov_b32_dpp (outside) + v_add_f32 (inside) instead of one v_add_f32_dpp (same operands, same sum)
+#pragma unroll
+    for (int i = 0; i < RR::R; i++) asm volatile("" : "+v"(r[i]));
+#endif
 }
 __device__ __forceinline__ int row_entry(int lane) { return 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1); }
 template <int NV>
