@@ -2,8 +2,9 @@
 (python -c "from splatam_amd import build; build.build_variant('phase', ['GSR_PHASE=1'])"), runs the
 tracking-style dual rasterization (config 3; grads for means3D + the depth colour) and reports the share of
 per-wave shader-clock cycles in each phase of render_fwd_kernel and render_bwd_kernel (gsr_diag.h).  The
-s_memtime stamps wait for outstanding LDS operations, so the shares are indicative, not exact.
-Usage: python tools/phase.py [config] [reps]"""
+s_memtime stamps wait for outstanding LDS operations, so the shares are indicative, not exact.  With `full`
+every Gaussian input requires grad (the mapping-style variant: opacity and colour sums as well).
+Usage: python tools/phase.py [config] [reps] [full]"""
 import ctypes
 import json
 import os
@@ -27,6 +28,7 @@ NAMES = {"bwd": ["prologue", "staging+barrier", "list_build", "row_walk", "barri
 def main():
     cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    full = len(sys.argv) > 3 and sys.argv[3] == "full"
     dev = torch.device("cuda:0")
     s = config_scene(cfg)
     cam = camera_settings(s.cam, dev)
@@ -46,8 +48,9 @@ def main():
     for r in range(reps + 1):
         for f in fns.values():
             f(buf)  # clear
-        im, im2, _, _ = rasterize_gaussians_dual(m3, m2, None, s.colors.to(dev), ds, s.opacities.to(dev),
-                                                 s.scales.to(dev), s.rotations.to(dev), None, cam, grad2_channels=1)
+        leaf = (lambda t: t.to(dev).requires_grad_(True)) if full else (lambda t: t.to(dev))  # noqa: E731
+        im, im2, _, _ = rasterize_gaussians_dual(m3, m2, None, leaf(s.colors), ds, leaf(s.opacities),
+                                                 leaf(s.scales), leaf(s.rotations), None, cam, grad2_channels=1)
         torch.autograd.backward([im, im2], [g, g2])
         torch.cuda.synchronize()
         for k, f in fns.items():
@@ -55,7 +58,7 @@ def main():
             if r:  # the first repetition warms up
                 for q in range(8):
                     tot[k][q] += int(buf[q])
-    out = {"config": cfg, "reps": reps}
+    out = {"config": cfg, "reps": reps, "full": full}
     for k, t in tot.items():
         n = len(NAMES[k])
         cyc = sum(t[:n])
