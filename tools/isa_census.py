@@ -19,7 +19,7 @@ def main():
     src, name = sys.argv[1], sys.argv[2]
     extra = sys.argv[3:]
     out = os.path.join(tempfile.gettempdir(), "gsr_census.s")
-    cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", "--offload-arch=gfx950", "-fno-slp-vectorize",
+    cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", "--offload-arch=gfx950", *([] if os.environ.get("CENSUS_SLP") else ["-fno-slp-vectorize"]),
            "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "splatam_amd", "csrc"),
            "--cuda-device-only", "-S", "-o", out, src, *extra]
     subprocess.run(cmd, check=True, capture_output=True)
