@@ -178,3 +178,18 @@ def test_gsr_lib_override_stays_strict(tmp_path):
     relaxed = subprocess.run([sys.executable, "-c", code], env=dict(base, GSR_LIB=str(so), GSR_LIB_AB="1"),
                              capture_output=True, text=True, cwd=ROOT)
     assert relaxed.returncode == 0, relaxed.stderr[-500:]
+
+
+def test_gsr_lib_override_keeps_calls_on_ctypes():
+    """The native binding links the in-tree libgsr.so, so a library selected through GSR_LIB (A/B builds) must
+    take every call, the drop-in path's two included: _C then keeps them on ctypes."""
+    import subprocess
+    import sys
+    code = "from splatam_amd import _C; print(_C._NATIVE_ON)"
+    base = {k: v for k, v in os.environ.items() if k not in ("GSR_LIB", "GSR_LIB_AB", "GSR_NATIVE_BINDING")}
+    lib = os.path.join(ROOT, "splatam_amd", "libgsr.so")
+    default = subprocess.run([sys.executable, "-c", code], env=base, capture_output=True, text=True, cwd=ROOT)
+    override = subprocess.run([sys.executable, "-c", code], env=dict(base, GSR_LIB=lib), capture_output=True,
+                              text=True, cwd=ROOT)
+    assert default.returncode == 0 and default.stdout.strip() == "True", default.stderr[-500:]
+    assert override.returncode == 0 and override.stdout.strip() == "False", override.stderr[-500:]
