@@ -25,10 +25,17 @@ constexpr uint32_t TILE_SORT_REGS = 1024;  // longest list sorted in registers (
 // (the runtime-loop ds_bpermute version spent most of its time in SALU/branch
 // overhead and LDS-permute latency: 32 us on the config-3 buckets,
 // tools/micro/sort_bench.hip).  Lane mappings checked by tools/micro/lane_xor.hip.
+#ifndef GSR_SORT_SWIZZLE
+#define GSR_SORT_SWIZZLE 0  // lane exchanges of distance <= 16 by ds_swizzle (LDS pipe) instead of DPP / permlane (VALU):
+                            // 779 static VALU fewer, bitwise the same order, the fused kernel unchanged (r8s_ab_sort_swizzle)
+#endif
 template <int M>
 __device__ __forceinline__ uint32_t lane_xor(uint32_t x) {
     static_assert(M == 1 || M == 2 || M == 4 || M == 8 || M == 16 || M == 32, "lane xor distance");
-    if constexpr (M == 1) {
+    if constexpr (GSR_SORT_SWIZZLE && M <= 16) {
+        // bit-mode swizzle inside each 32-lane half: lane' = (lane & 0x1F) ^ M
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (M << 10) | 0x1F);
+    } else if constexpr (M == 1) {
         return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
     } else if constexpr (M == 2) {
         return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
