@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 6
+#define GSR_ABI_VERSION 7
 
 /* error codes */
 #define GSR_OK 0
@@ -67,7 +67,20 @@ typedef struct gsr_settings {
     int sh_degree;
     const float* campos;      /* [3] */
     int prefiltered;
+    /* Not in the reference's settings (its binning is internal to the forward / backward pair); a
+     * per-call choice, no process-wide state.  GSR_BINNING_CULLED (0, the default of a zero-initialised
+     * struct): a (Gaussian, tile) instance whose alpha >= 1/255 ellipse reaches no 4x4 block of the tile
+     * is left out of the tile's sorted list -- it would be staged but never evaluated.  Images, radii,
+     * num_rendered and gradients are bitwise those of the reference's lists.  GSR_BINNING_REFERENCE (1):
+     * every rect instance listed, rasterizer_impl.cu:290-315 entry for entry.  Either way the binning
+     * buffer's point list holds num_rendered valid entries: point_list[0, L) are the tiles' sorted lists
+     * (L = the ranges' total) and point_list[L, num_rendered) the culled instances (Gaussian id, empty
+     * block mask), so its ids are the reference's multiset (Gaussian i appears tiles_touched(i) times). */
+    int binning;
 } gsr_settings;
+
+#define GSR_BINNING_CULLED 0
+#define GSR_BINNING_REFERENCE 1
 
 /* Per-Gaussian inputs (rasterize_points.cu:36-54 argument list) */
 typedef struct gsr_gaussians {

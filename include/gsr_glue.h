@@ -204,13 +204,6 @@ int gsr_track_backward_dual(const gsr_settings* settings, const gsr_gaussians* g
  * backward from another loss seed cannot follow such a call). */
 int gsr_track_records_floats(int capacity);
 
-/* Tile culling (no reference counterpart: the binning is internal to the forward / backward pair).  mode 3:
- * every forward (default), 2: the static-mode forwards only (the dynamic drop-in forward keeps the reference's
- * binning), 1: the fused tracking forward only, 0: none; a negative mode only queries.  Returns the previous
- * mode.  A culled (Gaussian, tile) instance -- one whose alpha >= 1/255 ellipse reaches no 4x4 block of the
- * tile -- is left out of the tile's list; its record slot is kept (num_rendered is unchanged) and never written,
- * and the images, radii and gradients are bitwise those of the unculled lists. */
-int gsr_tile_cull(int mode);
 int gsr_track_forward_backward_dual_static_xf(const gsr_settings* settings, const gsr_gaussians* gaussians,
                                               float* colors2, const gsr_track_xform* xform, int capacity,
                                               unsigned* status, float* out_color, float* out_color2,

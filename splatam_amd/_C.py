@@ -48,9 +48,18 @@ _native_mod = None
 
 
 def _native():
-    global _native_mod
+    """The native binding module, or None when it cannot be imported (stale or missing build): a warning once,
+    and every call stays on the ctypes binding of the same libgsr.so."""
+    global _native_mod, _NATIVE_ON
     if _native_mod is None:
-        from . import _gsr_torch  # noqa: F401  (ImportError: run `python -m splatam_amd.build`)
+        try:
+            from . import _gsr_torch  # noqa: F401  (run `python -m splatam_amd.build` to rebuild it)
+        except ImportError as exc:
+            import warnings
+            warnings.warn(f"splatam_amd: native torch binding unavailable ({exc}); using the ctypes binding of "
+                          "libgsr.so", RuntimeWarning)
+            _NATIVE_ON = False
+            return None
         _native_mod = _gsr_torch
     return _native_mod
 
@@ -136,7 +145,7 @@ def _settings(bg, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, scal
     s = GsrSettings(image_height=int(H), image_width=int(W), tan_fovx=float(tan_fovx), tan_fovy=float(tan_fovy),
                     bg=_ptr(keep[0]), scale_modifier=float(scale_modifier), viewmatrix=_ptr(keep[1]),
                     projmatrix=_ptr(keep[2]), sh_degree=int(degree), campos=_ptr(keep[3]),
-                    prefiltered=int(bool(prefiltered)))
+                    prefiltered=int(bool(prefiltered)), binning=binning_mode())
     return s, keep
 
 
@@ -254,7 +263,8 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     capacity > 0 selects gsr_forward_static (no host synchronisation, HIP-graph capturable; `status` is a
     device int32[4] receiving the sticky counters, and num_rendered is the capacity).
     """
-    if _NATIVE_ON and capacity <= 0 and not _GEOM_CACHE:
+    if (_NATIVE_ON and capacity <= 0 and not _GEOM_CACHE and binning_mode() == BINNING_CULLED and
+            _native() is not None):
         return _native().rasterize_gaussians(
             _t(background), means3D, _t(colors), _t(opacity), _t(scales), _t(rotations), float(scale_modifier),
             _t(cov3D_precomp), _t(viewmatrix), _t(projmatrix), float(tan_fovx), float(tan_fovy), int(image_height),
@@ -329,7 +339,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     precomputed colours (scripts/ros_handler.py:884-889 reads no other gradient) -- which runs the
     4-value-per-pair kernel; any other power != 1 request forms every gradient.
     """
-    if _NATIVE_ON:
+    if _NATIVE_ON and _native() is not None:
         return tuple(_native().rasterize_gaussians_backward(
             _t(background), means3D, radii, _t(colors), _t(scales), _t(rotations), float(scale_modifier),
             _t(cov3D_precomp), _t(viewmatrix), _t(projmatrix), float(tan_fovx), float(tan_fovy), dL_dout_color, _t(sh),
@@ -482,27 +492,29 @@ def rasterize_gaussians_dual_backward(background, means3D, radii, colors, colors
         return (out[0], out[1], dcolors2, *out[2:])
 
 
-TILE_CULL_EVERY, TILE_CULL_STATIC, TILE_CULL_TRACK, TILE_CULL_NONE = 3, 2, 1, 0
+BINNING_CULLED, BINNING_REFERENCE = 0, 1  # gsr_settings.binning (include/gsr.h)
 
 
-def tile_cull(mode: int | None = None) -> int:
-    """gsr_tile_cull (include/gsr_glue.h): the process-wide tile-culling mode -- 3 every forward (default),
-    2 the static-mode forwards only (the dynamic drop-in forward then builds the reference's binning), 1 the
-    fused tracking forward only, 0 none.  Returns the previous mode (mode None: only queries)."""
-    return int(lib.gsr_tile_cull(-1 if mode is None else int(mode)))
+def binning_mode() -> int:
+    """The calling thread's gsr_settings.binning for the calls it makes: BINNING_CULLED (default) or
+    BINNING_REFERENCE inside `reference_binning()`.  Per thread and per call -- the library keeps no mode."""
+    return getattr(_tls, "binning", BINNING_CULLED)
 
 
 class reference_binning:
-    """Context: the dynamic forward builds the reference's binning (rasterizer_impl.cu's num_rendered, ranges
-    and (tile, depth, id) point list, every instance of every rect tile) -- tile culling limited to the
-    static-mode forwards.  Outputs and gradients are the same bits either way; the oracle tests compare lists."""
+    """Context (this thread only): the forwards built here -- eager, static or captured in a HIP graph -- list
+    every rect instance, i.e. rasterizer_impl.cu's num_rendered, ranges and (tile, depth, id) point list entry
+    for entry (gsr_settings.binning = GSR_BINNING_REFERENCE).  Outside it the tile lists leave out the instances
+    that reach no pixel of their tile.  Images, radii, num_rendered and gradients are the same bits either way;
+    the oracle tests compare the lists themselves."""
 
     def __enter__(self):
-        self.prev = tile_cull(TILE_CULL_STATIC)
+        self.prev = binning_mode()
+        _tls.binning = BINNING_REFERENCE
         return self
 
     def __exit__(self, *exc):
-        tile_cull(self.prev)
+        _tls.binning = self.prev
         return False
 
 

@@ -21,7 +21,7 @@ class GsrSettings(ctypes.Structure):
     """gsr_settings (include/gsr.h)."""
     _fields_ = [("image_height", c_int), ("image_width", c_int), ("tan_fovx", c_float), ("tan_fovy", c_float),
                 ("bg", c_void_p), ("scale_modifier", c_float), ("viewmatrix", c_void_p), ("projmatrix", c_void_p),
-                ("sh_degree", c_int), ("campos", c_void_p), ("prefiltered", c_int)]
+                ("sh_degree", c_int), ("campos", c_void_p), ("prefiltered", c_int), ("binning", c_int)]
 
 
 class GsrGaussians(ctypes.Structure):
@@ -93,7 +93,6 @@ SIGNATURES = {
     "gsr_abi_version": (c_int, []),
     "gsr_selftest_reduce9": (c_int, [c_void_p, c_void_p, c_void_p]),
     "gsr_timing_enable": (c_int, [c_int]),
-    "gsr_tile_cull": (c_int, [c_int]),
     "gsr_timing_read": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
     # include/gsr_glue.h: fused SplaTAM tracking glue
     "gsr_track_scratch_floats": (c_int, [c_int]),
@@ -184,10 +183,11 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     v = lib.gsr_abi_version()
-    if v != 6:
+    if v != 7:
         # an older revision may differ in the glue structs only (ABI 4: gsr_map_adam without `halted`;
-        # ABI 5: no fused tracking render); the rasterizer calls are unchanged
-        if not (ab and v in (4, 5)):
+        # ABI 5: no fused tracking render; ABI 6: gsr_settings without `binning`, which such a library does
+        # not read); the rasterizer calls are unchanged
+        if not (ab and v in (4, 5, 6)):
             raise ImportError("libgsr.so ABI version mismatch")
     return lib
 

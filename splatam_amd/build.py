@@ -63,7 +63,7 @@ def build(force: bool = False) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    build_torch_binding()
+    build_torch_binding(force=force)
     return LIB
 
 
@@ -75,16 +75,22 @@ def torch_binding_path() -> str:
     return os.path.join(HERE, "_gsr_torch" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
-def build_torch_binding() -> str:
+def build_torch_binding(force: bool = False) -> str:
     """The native torch binding of the drop-in path's per-iteration calls (csrc/gsr_torch.cpp): a host-only
-    pybind11 module over libgsr.so (linked with an $ORIGIN rpath), in-tree so it travels with libgsr.so."""
+    pybind11 module over libgsr.so (linked with an $ORIGIN rpath), in-tree so it travels with libgsr.so.
+    Rebuilt when its sources are newer, when `force`, or when the torch it was built against (version, C++ ABI:
+    the stamp file next to it) is not the one importing it now."""
     import sysconfig
 
     import torch
     from torch.utils import cpp_extension as ce
     out = torch_binding_path()
+    stamp_file = out + ".stamp"
+    stamp = f"{torch.__version__} abi={int(torch._C._GLIBCXX_USE_CXX11_ABI)}"
     deps = [TORCH_SRC, os.path.join(ROOT, "include", "gsr.h")]  # (libgsr.so is resolved at load time)
-    if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
+    same_torch = os.path.exists(stamp_file) and open(stamp_file).read().strip() == stamp
+    if (not force and same_torch and os.path.exists(out) and
+            os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps)):
         return out
     inc = ce.include_paths() + [sysconfig.get_paths()["include"], os.path.join(ROOT, "include"), "/opt/rocm/include"]
     tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
@@ -96,6 +102,8 @@ def build_torch_binding() -> str:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"torch binding build failed:\n{r.stdout[-4000:]}\n{r.stderr[-4000:]}")
+    with open(stamp_file, "w") as f:
+        f.write(stamp + "\n")
     return out
 
 

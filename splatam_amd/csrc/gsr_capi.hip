@@ -20,10 +20,8 @@
 #include "gsr_common.h"
 
 #ifndef GSR_TILE_CULL
-#define GSR_TILE_CULL 3  // Camera::cull: 3 = every forward, 2 = the static-mode ones, 1 = the fused tracking one, 0 = none
+#define GSR_TILE_CULL 1  // Camera::cull for gsr_settings.binning == GSR_BINNING_CULLED (0: A/B builds without culling)
 #endif
-#include <atomic>
-static std::atomic<int> g_tile_cull{GSR_TILE_CULL};  // gsr_tile_cull
 using namespace gsr;
 
 namespace {
@@ -127,6 +125,8 @@ GaussIn make_gauss(const gsr_gaussians* g) {
 int validate(const gsr_settings* s, const gsr_gaussians* g, bool forward) {
     if (!s || !g) return fail(GSR_ERR_INVALID_ARG, "null settings or gaussians");
     if (g->P < 0) return fail(GSR_ERR_INVALID_ARG, "P must be >= 0");
+    if (s->binning != GSR_BINNING_CULLED && s->binning != GSR_BINNING_REFERENCE)
+        return fail(GSR_ERR_INVALID_ARG, "settings.binning must be GSR_BINNING_CULLED or GSR_BINNING_REFERENCE");
     if (s->image_width <= 0 || s->image_height <= 0) return fail(GSR_ERR_INVALID_ARG, "image size must be positive");
     if (s->image_width > 16 * 65535 || s->image_height > 16 * 65535)
         return fail(GSR_ERR_INVALID_ARG, "image too large for 16-bit tile coordinates");
@@ -363,9 +363,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     }
     static const bool force_radix_env = getenv("GSR_FORCE_RADIX") && atoi(getenv("GSR_FORCE_RADIX")) != 0;
     const bool force_radix = force_radix_env && capacity <= 0;
-    // tile culling (gsr_tile_cull): mode 3 every forward, 2 the static-mode ones, 1 the fused tracking one
-    const int cull_mode = g_tile_cull.load(std::memory_order_relaxed);
-    cam.cull = (cull_mode >= 3 || (cull_mode == 2 && capacity > 0) || (cull_mode == 1 && xf && capacity > 0)) ? 1 : 0;
+    // tile culling: a per-call choice (gsr_settings.binning), no process-wide mode
+    cam.cull = (GSR_TILE_CULL && settings->binning != GSR_BINNING_REFERENCE) ? 1 : 0;
     // the bucketed duplicate's workgroup 0 writes the render schedule (tile_plan); the other paths
     // render in row-major order
     Camera cplan = cam;
@@ -468,7 +467,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
             if ((e = launch_duplicate_bucket(cplan, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
-                                             ntiles, keys[0], GL.nb, guard, capacity > 0 ? status : nullptr,
+                                             ntiles, keys[0], point_list, GL.nb, guard,
+                                             capacity > 0 ? status : nullptr,
                                              stream)) != hipSuccess)
                 return hip_fail(e, "duplicate");
         }
@@ -516,7 +516,8 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
             if ((e = launch_duplicate_bucket(cplan, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
-                                             ntiles, keys[0], GL.nb, none, nullptr, stream)) != hipSuccess)
+                                             ntiles, keys[0], point_list, GL.nb, none, nullptr, stream)) !=
+                hipSuccess)
                 return hip_fail(e, "duplicate");
         }
     } else if (I > 0) {
@@ -922,9 +923,6 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
     return GSR_OK;
 }
 
-int gsr_tile_cull(int mode) {
-    return mode < 0 ? g_tile_cull.load() : g_tile_cull.exchange(mode > 3 ? 3 : mode);
-}
 
 int gsr_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_timing_mu);

@@ -53,6 +53,7 @@ struct GeomLayout {       // per-Gaussian state ("geomBuffer")
     size_t offsets;       // u32    [P]  exclusive instance offset (also in q1.w)
     size_t blocksums;     // u32    [nb] exclusive scan of the per-workgroup instance totals
     size_t wgsum;         // u32    [nb] per-workgroup instance totals (bit 31: prefiltered violation)
+    size_t wgcull;        // u32    [nb] per-workgroup culled-instance totals (Camera::cull; point_list's tail)
     size_t counters;      // u32    [8]  [0]=num_rendered [1]=prefiltered violation [2]=longest tile list
                           //             [3]=sort cap [4]=colscan arrival counter
     size_t total;
@@ -71,6 +72,7 @@ struct GeomLayout {       // per-Gaussian state ("geomBuffer")
         L.offsets = o; o = align_up(o + 4 * p, 256);
         L.blocksums = o; o = align_up(o + 4 * (size_t)(L.nb > 0 ? L.nb : 1), 256);
         L.wgsum = o; o = align_up(o + 4 * (size_t)(L.nb > 0 ? L.nb : 1), 256);
+        L.wgcull = o; o = align_up(o + 4 * (size_t)(L.nb > 0 ? L.nb : 1), 256);
         L.counters = o; o = align_up(o + 32, 256);
         L.total = o;
         return L;
@@ -173,6 +175,11 @@ struct Camera {
 // bin[i].w: bit k set = rect tile k (row-major in the rect) has an instance in its bucket; all ones when
 // nothing is culled (or the rect has more than 32 tiles)
 __device__ __forceinline__ bool tile_live(uint32_t live, uint32_t k) { return k >= 32u || ((live >> k) & 1u); }
+// culled instances among rect tiles [0, k) (k <= the Gaussian's tile count): positions in point_list's tail
+__device__ __forceinline__ uint32_t culled_below(uint32_t live, uint32_t k) {
+    const uint32_t m = k >= 32u ? 0xFFFFFFFFu : ((1u << k) - 1u);
+    return (uint32_t)__popc(~live & m);
+}
 // Wave priority by remaining work (GSR_PRIO_SCHED): the instruction arbiter favours older
 // waves, so on a CU the last-dispatched tile used to run alone at the end at one wave per
 // SIMD; raising the priority of the waves with the most work left keeps the CU's tiles
@@ -245,11 +252,12 @@ struct GeomPtrs {
     uint32_t* blocksums;
     uint32_t* counters;
     uint32_t* wgsum;
+    uint32_t* wgcull;
     static GeomPtrs at(void* base, const GeomLayout& L) {
         char* b = (char*)base;
         return {(float4*)(b + L.rr), (uint32_t*)(b + L.clamp), (uint4*)(b + L.bin), (uint32_t*)(b + L.tiles),
                 (uint32_t*)(b + L.offsets), (uint32_t*)(b + L.blocksums), (uint32_t*)(b + L.counters),
-                (uint32_t*)(b + L.wgsum)};
+                (uint32_t*)(b + L.wgsum), (uint32_t*)(b + L.wgcull)};
     }
 };
 
@@ -1215,8 +1223,8 @@ __device__ __forceinline__ void status_merge(uint32_t* st, uint32_t n, uint32_t 
 // Row-major render schedule (the paths that do not run tile_plan).
 hipError_t launch_identity_order(uint32_t* order, int ntiles, hipStream_t s);
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2* ranges, const uint32_t* tot,
-                                   uint32_t* cursor, bool lds_hist, int ntiles, uint64_t* keys, int nb,
-                                   SpecGuard guard, uint32_t* status, hipStream_t s);
+                                   uint32_t* cursor, bool lds_hist, int ntiles, uint64_t* keys, uint64_t* point_list,
+                                   int nb, SpecGuard guard, uint32_t* status, hipStream_t s);
 hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t n, int nsb, int npass,
                              hipStream_t s);
 hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint64_t* point_list, uint32_t n,

@@ -66,7 +66,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
         for (int t = threadIdx.x; t < ntiles; t += blockDim.x) s_hist[t] = 0u;
     if (LDS_HIST || XF) __syncthreads();
     if (i == 0) geo.counters[4] = 0u;  // tile_colscan_kernel's arrival counter (next launch)
-    uint32_t tiles = 0;
+    uint32_t tiles = 0, culled = 0;  // culled: rect tiles left out of the lists (Camera::cull)
     bool violation = false;  // prefiltered set but the point is culled (auxiliary.h:154-160)
     float4 q0, q1, q2, q3;
     if (i < g.P) {
@@ -164,6 +164,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                                                     : tile_reached(mg, (float)(tx * TILE_X), (float)(ty * TILE_Y)))
                                         ? 1u << k : 0u;
                 }
+                culled = culled_below(live, tiles);
                 geo.bin[i] = make_uint4(rlo, rhi, __float_as_uint(pv.z), live);
                 if (!g.sh_staged && !g.colors) geo.clamp[i] = clamped;  // (read only by the SH backward)
                 for (int ty = y0, k = 0; ty < y1; ty++)  // per-tile instance counts -> bucket ranges
@@ -187,10 +188,14 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     // workgroup scan of tiles touched: the local instance offset goes into the render
     // record (q1.w; the render kernels add the scanned workgroup base, blocksums[i >> pre_shift]),
     // the workgroup total into wgsum (input of the two-level scan)
-    __shared__ uint32_t wsum[PRE_BLOCK / 64];
+    __shared__ uint32_t wsum[PRE_BLOCK / 64], wcul[PRE_BLOCK / 64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t incl = wave_incl_scan(tiles);
     if (lane == 63) wsum[wv] = incl;
+    if (cam.cull) {  // the workgroup's culled instances: duplicate places them in point_list's tail
+        const uint32_t cincl = wave_incl_scan(culled);
+        if (lane == 63) wcul[wv] = cincl;
+    }
     __syncthreads();
     uint32_t woff = 0;
     for (int k = 0; k < wv; k++) woff += wsum[k];
@@ -206,7 +211,13 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     }
     // top bit: prefiltered violation anywhere in the workgroup (folded into counters[1] by the scan)
     const bool viol = __syncthreads_or(violation);
-    if (threadIdx.x == blockDim.x - 1) geo.wgsum[blockIdx.x] = (woff + incl) | (viol ? 0x80000000u : 0u);
+    if (threadIdx.x == blockDim.x - 1) {
+        geo.wgsum[blockIdx.x] = (woff + incl) | (viol ? 0x80000000u : 0u);
+        uint32_t cw = 0;
+        if (cam.cull)
+            for (int k = 0; k < (int)(blockDim.x >> 6); k++) cw += wcul[k];
+        geo.wgcull[blockIdx.x] = cw;
+    }
     if (LDS_HIST)
         for (int t = threadIdx.x; t < ntiles; t += blockDim.x) counts[(size_t)blockIdx.x * ntiles + t] = s_hist[t];
 }
@@ -654,14 +665,19 @@ template <bool LDS_HIST, int DUP_G>
 __global__ void __launch_bounds__(DUP_T)
 duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges, const uint32_t* __restrict__ tot,
                         uint32_t* __restrict__ cursor, int ntiles, uint64_t* __restrict__ keys,
-                        SpecGuard guard, uint32_t sort_cap, uint32_t* __restrict__ status) {
+                        uint64_t* __restrict__ point_list, SpecGuard guard, uint32_t sort_cap,
+                        uint32_t* __restrict__ status) {
     // LDS_HIST: cursor = the column-scanned count matrix; this workgroup's
     // instances of tile t go to start[t] + cursor[block][t] + (LDS rank)
+    // Culled instances (Camera::cull) are in no bucket: they fill point_list's tail [L, num_rendered)
+    // (L = the buckets' total) in (Gaussian, rect tile) order, as PointEntry (empty block mask << 32 | id), so
+    // every one of the num_rendered entries the forward returns is a valid Gaussian id.
     constexpr int ROW = DUP_G * DUP_T;  // Gaussians per count-matrix row (1 << cam.pre_shift)
     extern __shared__ uint32_t s_cur[];
     __shared__ uint32_t s_incl[ROW];
-    __shared__ uint32_t s_x0[ROW], s_y0[ROW], s_w[ROW], s_depth[ROW], s_live[ROW];
-    __shared__ uint32_t wsum[DUP_T / 64], s_tmax[DUP_T / 64];
+    __shared__ uint32_t s_x0[ROW], s_y0[ROW], s_w[ROW], s_depth[ROW], s_live[ROW], s_cx[ROW];
+    __shared__ uint32_t wsum[DUP_T / 64], s_tmax[DUP_T / 64], s_cws[DUP_T / 64];
+    __shared__ uint32_t s_cred[2][DUP_T / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int i0 = blockIdx.x * ROW + DUP_G * tid;  // this lane's Gaussians i0 .. i0 + DUP_G - 1
     // the Gaussians' tile counts and rects, loaded ahead of the prologue's loads (one round trip)
@@ -672,7 +688,7 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         t[g] = (i0 + g < P) ? geo.tiles[i0 + g] : 0u;
         r[g] = (i0 + g < P) ? geo.bin[i0 + g] : make_uint4(0u, 0u, 0u, 0u);  // (rect lo, rect hi, depth bits, tiles)
     }
-    uint32_t base;
+    uint32_t base, ctail = 0;
     if (LDS_HIST) {
         // The scans of scan_counts_body, redone by every workgroup (the inputs are
         // a few KB, L2-resident): this workgroup's instance base from the raw
@@ -692,15 +708,18 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
             tv[k] = ok ? tot[t0 + k] : 0u;
             cv[k] = ok ? cursor[(size_t)b * ntiles + t0 + k] : 0u;
         }
-        uint32_t pre = 0, all = 0, viol = 0, vmax = 0;
+        uint32_t pre = 0, all = 0, viol = 0, vmax = 0, cpre = 0, call = 0;
         // two workgroup sums per trip, both loads issued before either is used (config 3: 586 rows, so some
         // lanes read two -- one memory round trip instead of two ahead of the workgroup's first barrier)
         for (uint32_t k = tid; k < nb; k += 2 * DUP_T) {
             const uint32_t k2 = k + DUP_T;
             const uint32_t v = geo.wgsum[k], v2 = k2 < nb ? geo.wgsum[k2] : 0u;
+            const uint32_t c = cam.cull ? geo.wgcull[k] : 0u, c2 = (cam.cull && k2 < nb) ? geo.wgcull[k2] : 0u;
             viol |= (v | v2) >> 31;
             all += (v & 0x7fffffffu) + (v2 & 0x7fffffffu);
             pre += (k < b ? (v & 0x7fffffffu) : 0u) + (k2 < b ? (v2 & 0x7fffffffu) : 0u);
+            call += c + c2;
+            cpre += (k < b ? c : 0u) + (k2 < b ? c2 : 0u);
         }
         uint32_t csum = 0;
         if (in_regs) {
@@ -722,16 +741,22 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         all = wave_sum_u32(all);
         viol = wave_max_u32(viol);
         vmax = wave_max_u32(vmax);
+        if (cam.cull) {
+            cpre = wave_sum_u32(cpre);
+            call = wave_sum_u32(call);
+        }
         if (lane == 0) {
             s_red[0][w] = pre;
             s_red[1][w] = all;
             s_red[2][w] = viol;
             s_red[3][w] = vmax;
+            s_cred[0][w] = cpre;
+            s_cred[1][w] = call;
         }
         if (lane == 63) s_red[4][w] = cincl;
         __syncthreads();
         uint32_t woff = 0;
-        pre = all = viol = vmax = 0;
+        pre = all = viol = vmax = cpre = call = 0;
 #pragma unroll
         for (int k = 0; k < DUP_T / 64; k++) {
             pre += s_red[0][k];
@@ -739,7 +764,10 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
             viol |= s_red[2][k];
             vmax = max(vmax, s_red[3][k]);
             woff += k < w ? s_red[4][k] : 0u;
+            cpre += s_cred[0][k];
+            call += s_cred[1][k];
         }
+        ctail = all - call + cpre;  // this workgroup's first culled instance in point_list
         uint32_t run = woff + cincl - csum;  // bucket start of this thread's first tile
         if (in_regs) {
 #pragma unroll
@@ -784,12 +812,37 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
     } else {
         if (guard.overflow()) return;
         base = geo.blocksums[blockIdx.x];
+        if (cam.cull) {  // (the global-atomic path, > MAX_LDS_TILES tiles) the culled totals' prefix, here
+            const uint32_t b = blockIdx.x, nb = gridDim.x;
+            uint32_t cpre = 0, call = 0;
+            for (uint32_t k = tid; k < nb; k += DUP_T) {
+                const uint32_t c = geo.wgcull[k];
+                call += c;
+                cpre += k < b ? c : 0u;
+            }
+            cpre = wave_sum_u32(cpre);
+            call = wave_sum_u32(call);
+            if (lane == 0) {
+                s_cred[0][w] = cpre;
+                s_cred[1][w] = call;
+            }
+            __syncthreads();
+            cpre = call = 0;
+#pragma unroll
+            for (int k = 0; k < DUP_T / 64; k++) {
+                cpre += s_cred[0][k];
+                call += s_cred[1][k];
+            }
+            ctail = geo.counters[0] - call + cpre;
+        }
     }
-    uint32_t tsum = 0, tmax = 0;
+    uint32_t tsum = 0, tmax = 0, cg[DUP_G], csum = 0;
 #pragma unroll
     for (int g = 0; g < DUP_G; g++) {
         tsum += t[g];
         tmax = max(tmax, t[g]);
+        cg[g] = (cam.cull && t[g]) ? culled_below(r[g].w, t[g]) : 0u;
+        csum += cg[g];
         const int q = DUP_G * tid + g;
         if (t[g]) {
             s_x0[q] = r[g].x & 0xFFFFu;
@@ -800,13 +853,20 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         }
     }
     uint32_t incl = wave_incl_scan(tsum);
+    const uint32_t cincl = cam.cull ? wave_incl_scan(csum) : 0u;
     tmax = wave_max_u32(tmax);
     __syncthreads();  // (wsum is also tile_plan's scratch)
-    if (lane == 63) wsum[w] = incl;
+    if (lane == 63) {
+        wsum[w] = incl;
+        s_cws[w] = cincl;
+    }
     if (lane == 0) s_tmax[w] = tmax;
     __syncthreads();
-    uint32_t run = incl - tsum;
-    for (int k = 0; k < w; k++) run += wsum[k];
+    uint32_t run = incl - tsum, crun = ctail + cincl - csum;
+    for (int k = 0; k < w; k++) {
+        run += wsum[k];
+        crun += s_cws[k];
+    }
 #pragma unroll
     for (int k = 0; k < DUP_T / 64; k++) tmax = max(tmax, s_tmax[k]);
 #pragma unroll
@@ -814,6 +874,8 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         if (i0 + g < P) geo.offsets[i0 + g] = base + run;
         run += t[g];
         s_incl[DUP_G * tid + g] = run;
+        s_cx[DUP_G * tid + g] = crun;  // the Gaussian's first slot in point_list's culled tail
+        crun += cg[g];
     }
     if (tmax <= (uint32_t)GSR_DUP_LOOP_MAX) {
         // few tiles per Gaussian in this row (config 3: at most 4; mapping duplicate 50.4 -> 48.1 us at 16 or
@@ -825,8 +887,12 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         for (int g = 0; g < DUP_G; g++) {
             const uint32_t x0 = r[g].x & 0xFFFFu, y0 = r[g].x >> 16, wdt = (r[g].y & 0xFFFFu) - x0;
             const uint32_t gi = (uint32_t)(i0 + g);
+            uint32_t ct = s_cx[DUP_G * tid + g];
             for (uint32_t k = 0; k < t[g]; k++) {
-                if (!tile_live(r[g].w, k)) continue;  // culled (Camera::cull): not in the bucket
+                if (!tile_live(r[g].w, k)) {  // culled (Camera::cull): not in the bucket, in the tail
+                    point_list[ct++] = (uint64_t)gi;
+                    continue;
+                }
                 const uint32_t tile = (y0 + k / wdt) * (uint32_t)cam.gx + x0 + k % wdt;
                 const uint32_t pos = LDS_HIST ? atomicAdd(&s_cur[tile], 1u)
                                               : ranges[tile].x + atomicAdd(&cursor[tile * TILE_CTR_STRIDE], 1u);
@@ -844,7 +910,10 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
             if (s_incl[mid] > e) hi = mid; else lo = mid + 1;
         }
         const uint32_t local = e - ((lo == 0) ? 0u : s_incl[lo - 1]);
-        if (!tile_live(s_live[lo], local)) continue;  // culled (Camera::cull)
+        if (!tile_live(s_live[lo], local)) {  // culled (Camera::cull): in point_list's tail
+            point_list[s_cx[lo] + culled_below(s_live[lo], local)] = (uint64_t)(blockIdx.x * ROW + lo);
+            continue;
+        }
         const uint32_t wdt = s_w[lo];
         const uint32_t tile = (s_y0[lo] + local / wdt) * (uint32_t)cam.gx + s_x0[lo] + local % wdt;
         const uint32_t pos = LDS_HIST ? atomicAdd(&s_cur[tile], 1u)
@@ -855,14 +924,14 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
 }
 
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2* ranges, const uint32_t* tot,
-                                   uint32_t* cursor, bool lds_hist, int ntiles, uint64_t* keys, int nb,
-                                   SpecGuard guard, uint32_t* status, hipStream_t s) {
+                                   uint32_t* cursor, bool lds_hist, int ntiles, uint64_t* keys, uint64_t* point_list,
+                                   int nb, SpecGuard guard, uint32_t* status, hipStream_t s) {
     if (nb == 0) return hipSuccess;
     const bool g2 = cam.pre_shift == 10;  // rows of 1024: two Gaussians per lane; of 512: one
     auto k = lds_hist ? (g2 ? duplicate_bucket_kernel<true, 2> : duplicate_bucket_kernel<true, 1>)
                       : (g2 ? duplicate_bucket_kernel<false, 2> : duplicate_bucket_kernel<false, 1>);
     hipLaunchKernelGGL(k, dim3(nb), dim3(DUP_T), lds_hist ? sizeof(uint32_t) * ntiles : 0, s, cam, P, geo, ranges,
-                       tot, cursor, ntiles, keys, guard, (uint32_t)TILE_SORT_CAP, status);
+                       tot, cursor, ntiles, keys, point_list, guard, (uint32_t)TILE_SORT_CAP, status);
     return hipGetLastError();
 }
 

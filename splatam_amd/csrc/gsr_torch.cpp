@@ -8,6 +8,7 @@
 // backward per SplaTAM iteration, host-bound -- pays in full.  Here the same checks, error messages,
 // buffers and results cost a few microseconds.  Semantics mirror _C.rasterize_gaussians (dynamic mode,
 // capacity 0) and _C.rasterize_gaussians_backward exactly; _C.py dispatches to this module for them.
+#include <cstdlib>
 #include <torch/extension.h>
 
 #include <c10/hip/HIPStream.h>
@@ -62,6 +63,11 @@ at::Tensor dev_f32(const at::Tensor& t, const at::Device& dev, const char* name)
 // _C._cam_f32: the camera tensors are the same objects on every call of an iteration and SplaTAM passes
 // the matrices as transposed views, so the contiguous copy is reused while the source tensor is alive and
 // unmodified (weak reference + version counter), on the same stream, never during stream capture.
+// GSR_CAM_CACHE=0 disables it, as for the ctypes path (_C._CAM_CACHE).
+const bool g_cam_cache_on = [] {
+    const char* v = std::getenv("GSR_CAM_CACHE");
+    return !(v && std::string(v) == "0");
+}();
 struct CamEntry {
     c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl> src;
     int64_t version;
@@ -73,6 +79,7 @@ thread_local std::vector<CamEntry> g_cam;
 at::Tensor cam_f32(const at::Tensor& t, const at::Device& dev, const char* name, hipStream_t s) {
     if (!t.defined() || t.numel() == 0) return at::Tensor();
     if (t.scalar_type() == at::kFloat && t.device() == dev && t.is_contiguous()) return t;
+    if (!g_cam_cache_on) return dev_f32(t, dev, name);
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return dev_f32(t, dev, name);
     const c10::TensorImpl* impl = t.unsafeGetTensorImpl();

@@ -34,8 +34,9 @@ optimizer.step() updates no Gaussian parameter at all -- remove_points replaced 
 new tensor without .grad, so torch.optim.Adam skips them and their state["step"] does not advance --
 hence that iteration is captured as its loss forward plus the mask update, with no backward and no
 Adam step (the fused steps' step counts follow: 1..19, then 20..58 for a 60-iteration frame).
-compact() then removes the pruned Gaussians from the parameters and the Adam state for real
-(remove_points) after the replay.  Densification (GS-style, off in the default configs) changes P and
+The mask persists across replays: a Gaussian pruned in one replay stays removed in the next, as after the
+reference's remove_points.  compact() then removes the pruned Gaussians from the parameters, the Adam state
+and SplaTAM's per-Gaussian variables for real (remove_points).  Densification (GS-style, off in the default configs) changes P and
 stays outside the graph.
 """
 from __future__ import annotations
@@ -129,7 +130,9 @@ class GraphMapper:
         self.stream = side
         with torch.cuda.graph(self.graph, stream=side):
             self.adam.reset()          # initialize_optimizer per frame: zero moments, step 0
-            self.alive.fill_(1)        # every Gaussian of the frame's map is live until a pruning iteration
+            # (the alive mask is NOT reset per replay: a Gaussian pruned in one replay stays removed in the next,
+            # as remove_points removes it for good -- its parameters drift under their moments with zero
+            # gradient for the rest of that frame, but it is never rendered again; compact() drops it)
             for k in range(self.iters):
                 self.loss = self._iteration(k)
         self.stale = False
@@ -215,22 +218,39 @@ class GraphMapper:
         return loss.detach()
 
     def survivors(self) -> torch.Tensor:
-        """Boolean [P] mask of the Gaussians the last replay kept."""
+        """Boolean [P] mask of the Gaussians every replay so far kept (the mask persists across replays)."""
         return self.alive.bool()
 
-    def compact(self):
+    VARIABLE_KEYS = ("means2D_gradient_accum", "denom", "max_2D_radius", "timestep")
+
+    def compact(self, variables: dict | None = None):
         """After a replay, remove the pruned Gaussians for real: remove_points (utils/slam_external.py:141-163)
-        on the parameters and the frame's Adam moments.  Returns (params, exp_avg, exp_avg_sq): a new params
-        dict (the Gaussian tensors compacted, new leaves requiring grad; the camera tensors as they were) and
-        the moments by parameter name.  P changes, so this mapper is stale afterwards (run() raises): build
-        the next frame's mapper on the returned parameters."""
+        on the parameters, the frame's Adam moments and -- when `variables` is given -- the per-Gaussian
+        SplaTAM variables remove_points compacts too (means2D_gradient_accum, denom, max_2D_radius and, when
+        present, timestep; assigned into the caller's dict as remove_points does, so get_loss's
+        `variables['max_2D_radius'][seen]` and the saved params['timestep'] keep lining up with means3D).
+        Returns (params, exp_avg, exp_avg_sq): a new params dict (every per-Gaussian tensor compacted, new
+        leaves requiring grad; the camera tensors as they were) and the moments by parameter name.  P changes,
+        so this mapper is stale afterwards (run() raises): build the next frame's mapper on the returned
+        parameters."""
         keep = self.survivors()
+        P = keep.shape[0]
         out = dict(self.params)
         m, v = {}, {}
         with torch.no_grad():
             for k, em, ev in zip(self.adam.keys, self.adam.exp_avg, self.adam.exp_avg_sq):
                 out[k] = self.params[k].detach()[keep].clone().requires_grad_(True)
                 m[k], v[k] = em[keep].clone(), ev[keep].clone()
+            for k, t in self.params.items():  # any other per-Gaussian parameter (remove_points: every non-camera key)
+                if k in m or k in ("cam_unnorm_rots", "cam_trans") or not torch.is_tensor(t) or t.dim() == 0:
+                    continue
+                if t.shape[0] == P:
+                    out[k] = t.detach()[keep].clone().requires_grad_(t.requires_grad)
+            if variables is not None:
+                for k in self.VARIABLE_KEYS:
+                    t = variables.get(k)
+                    if torch.is_tensor(t) and t.dim() > 0 and t.shape[0] == P:
+                        variables[k] = t[keep.to(t.device)]
         self.stale = True
         return out, m, v
 

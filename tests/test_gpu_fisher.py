@@ -1,6 +1,7 @@
 """Fisher / EIG view scoring (splatam_amd.fisher, ros_handler.py:807-902) on the GPU:
 the per-pose Hessian H = [dL/dmeans_cam, dL/dopacity] of the backward_power=2 render
 seeded with 1e-3 against the float32 C oracle's fused-mode (per-pair powf) backward."""
+import contextlib
 import math
 
 import numpy as np
@@ -136,10 +137,8 @@ def test_batched_fisher_tile_cull_bitwise(cuda):
     sc = FisherScorer(params, cam)
     poses = [_pose(d, [0.01 * d, -0.005 * d, 0.02]).to(cuda) for d in (-4.0, -2.0, 0.0, 1.5)]
     out = {}
-    prev = _C.tile_cull()
-    try:
-        for mode in (0, 3):
-            _C.tile_cull(mode)
+    for mode in (0, 3):  # 0: the reference's lists (reference_binning, captured with the graphs), 3: culled
+        with (_C.reference_binning() if mode == 0 else contextlib.nullcontext()):
             bs = BatchedFisher(sc, 4, mode="sum", probe_w2cs=poses)
             h = bs.hessian_sum(poses).clone()
             sc.fit_visited(poses, batch=bs)
@@ -147,7 +146,5 @@ def test_batched_fisher_tile_cull_bitwise(cuda):
             s = sc.eig_scores(poses, batch=bsc).clone()
             torch.cuda.synchronize()
             out[mode] = (h, s)
-    finally:
-        _C.tile_cull(prev)
     assert float(out[0][0].abs().sum()) > 0
     assert torch.equal(out[0][0], out[3][0]) and torch.equal(out[0][1], out[3][1])

@@ -3,6 +3,7 @@ the fused SSIM/L1 loss kernels, the mapping transform backward, the fused Adam
 step and the whole fused iteration against the literal restatement of
 scripts/splatam.py:220-353 (mapping=True) in splatam_amd.slam, whose torch glue
 is itself pinned to the reference's utils/*.py by tests/test_glue_cpu.py."""
+import contextlib
 import numpy as np
 import pytest
 import torch
@@ -426,7 +427,7 @@ def test_sh_colour_adam_fused_bitwise(cuda, monkeypatch):
 
 @pytest.mark.parametrize("sh", [False, True])
 def test_graph_mapper_tile_cull_bitwise(cuda, sh):
-    """Tile culling (gsr_tile_cull, every forward by default) in the captured mapping frame: parameters after
+    """Tile culling (gsr_settings.binning, culled by default) in the captured mapping frame: parameters after
     two 6-iteration replays are bitwise those of the same frame with culling off (static dual forward, SH or
     RGB colours, the 10-sum render backward, gauss_bwd skipping the culled record slots)."""
     from splatam_amd import _C
@@ -436,21 +437,17 @@ def test_graph_mapper_tile_cull_bitwise(cuda, sh):
     key = slam.color_key(params)
     keys = GAUSS_KEYS + (key,)
     res = {}
-    prev = _C.tile_cull()
-    try:
-        for mode in (0, 3):
-            _C.tile_cull(mode)
+    for mode in (0, 3):  # 0: the reference's lists (reference_binning), 3: culled (the default)
+        with (_C.reference_binning() if mode == 0 else contextlib.nullcontext()):
             p = {k: v.clone() for k, v in params.items()}
             for k in keys:
                 p[k].requires_grad_(True)
             mapper = GraphMapper(p, kfs, iters_per_graph=6, seed=7, prune=False)
-            for _ in range(2):
-                mapper.run()
-            torch.cuda.synchronize()
-            assert not mapper.overflowed()
-            res[mode] = {k: p[k].detach().clone() for k in keys}
-    finally:
-        _C.tile_cull(prev)
+        for _ in range(2):
+            mapper.run()
+        torch.cuda.synchronize()
+        assert not mapper.overflowed()
+        res[mode] = {k: p[k].detach().clone() for k in keys}
     for k in keys:
         assert float((res[3][k] - params[k]).abs().max()) > 0.0, k
         assert torch.equal(res[0][k], res[3][k]), k

@@ -10,6 +10,7 @@ Tolerances (north star: 1e-4 relative):
   * median depth: exact on >= 99.5 % of pixels (T ~ 0.5 crossings excepted);
   * gradients: relative L2 <= 1e-4 per tensor against the float32 oracle.
 """
+import contextlib
 import dataclasses
 
 import numpy as np
@@ -108,18 +109,16 @@ def test_bitwise_deterministic_backward(cuda):
 
 
 def _binning_gpu(scene, cuda, mode=2):
-    """The dynamic forward's binning; mode (gsr_tile_cull) 2: the reference's lists, 3: tile-culled lists."""
+    """The dynamic forward's binning; mode 2: the reference's lists (gsr_settings.binning = REFERENCE), 3: the
+    tile-culled lists (the default)."""
     from splatam_amd import _C
     from splatam_amd.layout import views
     c = scene.cam
-    prev = _C.tile_cull(mode)
-    try:
+    with (_C.reference_binning() if mode == 2 else contextlib.nullcontext()):
         out = _C.rasterize_gaussians(torch.zeros(3, device=cuda), scene.means3D.to(cuda), scene.colors.to(cuda),
                                      scene.opacities.to(cuda), scene.scales.to(cuda), scene.rotations.to(cuda), 1.0,
                                      torch.Tensor([]), c.viewmatrix.to(cuda), c.projmatrix.to(cuda), c.tanfovx,
                                      c.tanfovy, c.H, c.W, torch.Tensor([]), 0, c.campos.to(cuda), False)
-    finally:
-        _C.tile_cull(prev)
     n, color, radii, geom, binning, img, depth = out
     v = views(img, binning, c.W, c.H, n)
     res = {k: t.cpu().numpy() for k, t in v.items()}
@@ -164,7 +163,7 @@ def test_binning_bit_exact(cuda, case):
 
 @pytest.mark.parametrize("case", BIN_CASES, ids=[c["name"] for c in BIN_CASES])
 def test_tile_cull_drops_only_unreached_instances(cuda, case):
-    """Tile culling in the dynamic drop-in forward (gsr_tile_cull mode 3, every binning path: bucketed,
+    """Tile culling in the dynamic drop-in forward (the default gsr_settings.binning, every binning path: bucketed,
     chunked, radix fallback with the culled instances keyed behind every tile, global-atomic counts): every
     tile list is an order-preserving subsequence of the reference's list (mode 2), an instance is dropped only
     where no pixel of its tile reaches alpha >= 1/255 (float64, margin), num_rendered, radii, images and every
@@ -205,14 +204,95 @@ def test_tile_cull_drops_only_unreached_instances(cuda, case):
     if case["name"] not in ("many_tiles", "long_lists"):  # (long_lists: every Gaussian reaches all six tiles)
         assert dropped > 0
     dpix = np.random.RandomState(3).randn(3, c.H, c.W).astype(np.float32)
-    prev = _C.tile_cull(2)
-    try:
+    with _C.reference_binning():
         a = harness.run_gpu(scene, dpix)
-    finally:
-        _C.tile_cull(prev)
     b = harness.run_gpu(scene, dpix)
     for k in a["grads"]:
         assert np.array_equal(a["grads"][k], b["grads"][k]), k
+
+
+@pytest.mark.parametrize("case", BIN_CASES, ids=[c["name"] for c in BIN_CASES])
+def test_point_list_holds_num_rendered_valid_ids(cuda, case):
+    """The binning buffer's contract (rasterizer_impl.cu:290-315 walks num_rendered entries): with culling on
+    (the default) and off, every one of the num_rendered point-list entries is a Gaussian id in [0, P), and
+    their multiset is the reference's (Gaussian i listed tiles_touched(i) times).  Culled instances sit in
+    the tail [L, num_rendered) (L = the ranges' total) with an empty block mask.  The r7s abort came from
+    reading that tail before the library wrote it."""
+    scene = make_scene(case["P"], case["W"], case["H"], seed=13, anisotropic=case["aniso"],
+                       z_range=(0.5, 1.0) if case.get("near") else (0.5, 5.0))
+    scene.scales *= case.get("scale", 1.0)
+    fr, _ = harness.run_oracle(scene, backward=False)
+    want = np.bincount(fr.point_list.astype(np.int64), minlength=scene.P)
+    for mode in (2, 3):
+        n, v = _binning_gpu(scene, cuda, mode=mode)
+        assert n == fr.num_rendered
+        ids = v["point_list"][:n].astype(np.int64)
+        assert ids.min() >= 0 and ids.max() < scene.P, mode
+        np.testing.assert_array_equal(np.bincount(ids, minlength=scene.P), want)
+        L = int((v["ranges"][:, 1] - v["ranges"][:, 0]).clip(min=0).sum())
+        assert L <= n
+        if mode == 2:
+            assert L == n
+        assert not (v["block_masks"][L:n] & 0xFFFF).any(), mode
+        print(f"{case['name']} mode {mode}: {n - L} of {n} entries in the culled tail")
+
+
+def test_point_list_valid_in_static_mode(cuda):
+    """The static (capacity) forward: the first status[0] = num_rendered entries are valid ids, culled or not."""
+    from splatam_amd import _C
+    from splatam_amd.layout import views
+    scene = make_scene(20000, 320, 240, seed=3)
+    c = scene.cam
+    dev = torch.device(cuda)
+    e = torch.Tensor([])
+    for mode in (2, 3):
+        status = torch.zeros(4, dtype=torch.int32, device=dev)
+        with (_C.reference_binning() if mode == 2 else contextlib.nullcontext()):
+            out = _C.rasterize_gaussians(torch.zeros(3, device=dev), scene.means3D.to(dev), scene.colors.to(dev),
+                                         scene.opacities.to(dev), scene.scales.to(dev), scene.rotations.to(dev), 1.0,
+                                         e, c.viewmatrix.to(dev), c.projmatrix.to(dev), c.tanfovx, c.tanfovy, c.H, c.W,
+                                         e, 0, c.campos.to(dev), False, capacity=200000, status=status)
+        torch.cuda.synchronize()
+        n = int(status[0])
+        assert 0 < n <= 200000
+        v = views(out[5], out[4], c.W, c.H, n)
+        ids = v["point_list"][:n].long()
+        assert int(ids.min()) >= 0 and int(ids.max()) < scene.P
+        counts = torch.bincount(ids, minlength=scene.P)
+        # tiles_touched per Gaussian: the rect of its radius (radii > 0 <=> listed at least once)
+        assert torch.equal(counts > 0, out[2] > 0)
+
+
+def test_binning_mode_is_per_call_across_threads(cuda):
+    """gsr_settings.binning is a per-call argument (no process-wide mode): two threads, each with its own
+    stream, one forwarding with the reference's lists and one with culled lists, interleaved, each get their
+    own lists -- bitwise those of a single-threaded call."""
+    import threading
+    scene = make_scene(8000, 160, 120, seed=19)
+    ref = {m: _binning_gpu(scene, cuda, mode=m) for m in (2, 3)}
+    assert ref[2][0] == ref[3][0]
+    assert not np.array_equal(ref[2][1]["ranges"], ref[3][1]["ranges"])  # the modes differ on this scene
+    errors = []
+
+    def worker(mode):
+        try:
+            s = torch.cuda.Stream(device=cuda)
+            with torch.cuda.stream(s):
+                for _ in range(12):
+                    n, v = _binning_gpu(scene, cuda, mode=mode)
+                    for k in ("ranges", "point_list"):
+                        if not np.array_equal(v[k], ref[mode][1][k]):
+                            errors.append((mode, k))
+        except Exception as exc:  # pragma: no cover - reported below
+            errors.append((mode, repr(exc)))
+
+    ts = [threading.Thread(target=worker, args=(m,)) for m in (2, 3, 2, 3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors[:4]
 
 
 POWER_CASES = [

@@ -173,7 +173,21 @@ def test_graph_mapper_pruning_follows_literal_frame(cuda):
     mapper.run()
     torch.cuda.synchronize()
     seq = list(mapper.sequence)
-    c_p, _, _ = mapper.compact()
+    P0 = params["means3D"].shape[0]
+    g_vars = slam.tracking_variables(P0, cuda)
+    g_vars["max_2D_radius"] += torch.arange(P0, device=cuda, dtype=torch.float32)  # row identity
+    keep = mapper.survivors()
+    c_p, _, _ = mapper.compact(g_vars)
+    # remove_points compacts the per-Gaussian variables too (slam_external.py:155-159): they line up with
+    # the compacted map, and the reference's eager get_loss updates max_2D_radius[seen] on them
+    Pk = c_p["means3D"].shape[0]
+    for k in ("max_2D_radius", "means2D_gradient_accum", "denom", "timestep"):
+        assert g_vars[k].shape[0] == Pk, k
+    assert torch.equal(g_vars["max_2D_radius"], torch.arange(P0, device=cuda, dtype=torch.float32)[keep])
+    loss_after, radius_after, _ = slam.get_loss_mapping(c_p, kfs[0], kfs[0]["id"], cfg, fused=False,
+                                                        variables=g_vars)
+    assert torch.isfinite(loss_after) and radius_after.shape[0] == Pk
+    assert bool(g_vars["seen"].any())
     lit = slam.as_parameters(params)
     variables = slam.tracking_variables(params["means3D"].shape[0], cuda)
     variables["scene_radius"] = r

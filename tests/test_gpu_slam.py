@@ -2,6 +2,7 @@
 (get_loss_tracking(fast=True, fused=False)) and the fused HIP glue
 (include/gsr_glue.h, fused=True) equal the literal restatement of
 scripts/splatam.py:220-353 (fast=False) in loss and pose gradients."""
+import contextlib
 import pytest
 import torch
 
@@ -267,22 +268,19 @@ def test_transform_fused_preprocess_bitwise(cuda, aniso, store, monkeypatch):
 
 @pytest.mark.parametrize("case", ["aniso", "config3"])
 def test_track_tile_cull_bitwise(cuda, case, monkeypatch):
-    """Tile culling (gsr_tile_cull, every forward): instances whose alpha >= 1/255 ellipse reaches
+    """Tile culling (gsr_settings.binning, culled by default): instances whose alpha >= 1/255 ellipse reaches
     no 4x4 block of their tile are left out of the tile lists.  Against the same static iterations with
     culling off: loss, radii and pose gradients bitwise equal (transform fused or not, render backward fused
     or not), num_rendered (the record count) equal, the longest tile list shorter at config 3."""
     from splatam_amd import glue
-    from splatam_amd._lib import lib
+    from splatam_amd import _C
     from splatam_amd.scenes import config_scene
     from splatam_amd.slam import TrackingConfig
     params, curr = _setup(cuda, case == "aniso", config_scene(3) if case == "config3" else None)
     seed = torch.ones((), device=cuda)
     outs = {}
-    prev = lib.gsr_tile_cull(-1)
-    assert prev == 3  # the default: every forward culls
-    try:
-        for mode in (0, 2):
-            lib.gsr_tile_cull(mode)
+    for mode in (0, 2):  # 0: the reference's lists (reference_binning), 2: culled (the default)
+        with (_C.reference_binning() if mode == 0 else contextlib.nullcontext()):
             for fused, rfused in ((False, False), (True, False), (True, True)):
                 monkeypatch.setattr(glue, "_XF_FUSED", fused)
                 monkeypatch.setattr(glue, "_RENDER_FUSED", rfused)
@@ -294,8 +292,6 @@ def test_track_tile_cull_bitwise(cuda, case, monkeypatch):
                 outs[mode, fused, rfused] = (loss.detach().clone(), radii.clone(), p["cam_unnorm_rots"].grad.clone(),
                                              p["cam_trans"].grad.clone(), status.clone())
                 assert int(status[1]) == 0
-    finally:
-        lib.gsr_tile_cull(prev)
     l0, r0, q0, t0, s0 = outs[0, False, False]
     for (mode, fused, rfused), (l1, r1, q1, t1, s1) in outs.items():
         assert torch.equal(l0, l1) and torch.equal(r0, r1), (mode, fused, rfused)
