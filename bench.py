@@ -82,6 +82,9 @@ def parse():
                     help="mapping: iterations per frame = per HIP graph (configs/replica/splatam.py:16: 60)")
     ap.add_argument("--map-prune", type=int, default=1,
                     help="mapping: prune_gaussians inside the frame (configs/replica/splatam.py:101-111), 0: off")
+    ap.add_argument("--map-prunable", type=float, default=0.02,
+                    help="mapping: fraction of the map's Gaussians given opacities under prune_gaussians' 0.005 "
+                         "threshold (removed at the frame's first pruning iteration, as faded Gaussians are)")
     ap.add_argument("--fisher-k", type=int, default=16, help="fisher: poses per HIP-graph launch")
     ap.add_argument("--configs", choices=("auto", "on", "off"), default="auto",
                     help="BASELINE configs 1 (forward only) and 2 (fwd+bwd RGB + depth) on the GPU and the CPU "
@@ -139,23 +142,15 @@ def main():
     from splatam_amd import dist as sd
     scene = config_scene(args.config)
     P, W, H = scene.P, scene.cam.W, scene.cam.H
-    params = init_tracking_params(scene, num_frames=max(world, 1), device=dev)
+    from splatam_amd.workloads import tracking_frame
+    frame = sd.frames_for_rank(world)[0] if world > 1 else 0  # frame sharding: rank r tracks frame r
+    # the map of init_tracking_params and the frame's target rendered at the unperturbed pose -- the workload
+    # tests/test_gpu_pinned.py compares with the literal get_loss loop at this size
+    params, curr = tracking_frame(scene, dev, num_frames=max(world, 1), frame=frame)
     fm = sd.FlatMap(params)                     # the map as one contiguous buffer: one collective per broadcast
     sd.broadcast_flat(fm)                       # canonical Gaussian map from rank 0
     bc = sd.MapBroadcaster(fm)                  # double-buffered broadcast, overlapped with the frames' replays
-    frame = sd.frames_for_rank(world)[0] if world > 1 else 0  # frame sharding: rank r tracks frame r
-    cam = camera_settings(scene.cam, dev)
-    w2c = torch.eye(4, device=dev)
-    # targets: renders at the unperturbed pose (ground truth of the synthetic frame)
-    with torch.no_grad():
-        gt = dict(params)
-        gt["cam_unnorm_rots"] = torch.zeros_like(params["cam_unnorm_rots"])
-        gt["cam_unnorm_rots"][0, 0] = 1.0
-        gt["cam_trans"] = torch.zeros_like(params["cam_trans"])
-        tg = transform_to_frame(gt, frame, False, False)
-        im, _, _ = GaussianRasterizer(cam)(**transformed_params2rendervar(gt, tg))
-        ds, _, _ = GaussianRasterizer(cam)(**transformed_params2depthplussilhouette(gt, w2c, tg))
-    curr = {"cam": cam, "w2c": w2c, "im": im.clone(), "depth": ds[0:1].clone()}
+    cam, w2c = curr["cam"], curr["w2c"]
     params["cam_unnorm_rots"].requires_grad_(True)
     params["cam_trans"].requires_grad_(True)
     # configs/replica/splatam.py:71-80 tracking learning rates; torch's fused (single-kernel) Adam
@@ -194,7 +189,7 @@ def main():
     if tracker is None:
         profiling.enable_timing(True)
     else:  # reset the device-clock accumulators the captured stamps add to
-        profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
+        profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if tracker is not None:
@@ -390,7 +385,9 @@ def main():
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items()},
+            # per launch, from the in-kernel stage clocks of every launch in the timed replays (the per-tile sort runs
+            # inside render_fwd / render_track: no "sort" stage; "ranges" is the tile-count column scan)
+            "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items() if v["launches"]},
             "dropin": dropin,
             "fisher": fisher,
             "mapping": mapping,
@@ -628,28 +625,6 @@ def dropin_leg(args, scene, dev, iters_per_frame: int = 40):
                                     "to ms_per_step is the caller's torch glue"}}
 
 
-def mapping_keyframes(params, cam, K, rank, dev):
-    """K keyframe targets (cam / im / depth / w2c / id): the map with perturbed colours rendered at each
-    keyframe's pose (the synthetic stand-in for the dataset frames the reference maps against)."""
-    from splatam_amd.rasterizer import GaussianRasterizer
-    from splatam_amd.slam import _rendervar_colors, color_key, transform_to_frame, \
-        transformed_params2depthplussilhouette, transformed_params2rendervar
-    key = color_key(params)
-    w2c = torch.eye(4, device=dev)
-    g = torch.Generator().manual_seed(1234)
-    kfs = []
-    with torch.no_grad():
-        truth = dict(params)
-        truth[key] = params[key] * 0.9 + 0.05 * torch.rand(params[key].shape, generator=g).to(dev)
-        for j in range(K):
-            t = rank * K + j
-            tg = transform_to_frame(truth, t, False, False)
-            im, _, _ = GaussianRasterizer(cam)(**_rendervar_colors(truth, transformed_params2rendervar(truth, tg)))
-            ds, _, _ = GaussianRasterizer(cam)(**transformed_params2depthplussilhouette(truth, w2c, tg))
-            kfs.append({"cam": cam, "w2c": w2c, "im": im.clamp(0, 1), "depth": ds[0:1].clone(), "id": t})
-    return kfs
-
-
 def dropin_mapping_leg(args, dev, iters: int = 60):
     """The unchanged mapping loop (scripts/splatam.py:841-905) at config 4: every parameter an
     nn.Parameter, a fresh torch.optim.Adam per frame over every group (eps 1e-15), per iteration a random
@@ -659,14 +634,12 @@ def dropin_mapping_leg(args, dev, iters: int = 60):
     import numpy as np
     import diff_gaussian_rasterization as dgr
     from splatam_amd.scenes import config_scene
-    from splatam_amd.slam import MappingConfig, as_parameters, camera_settings, init_mapping_params, \
-        map_frame_literal, tracking_variables
+    from splatam_amd.slam import MappingConfig, as_parameters, map_frame_literal, tracking_variables
+    from splatam_amd.workloads import mapping_workload
     scene = config_scene(4)
     P, W, H = scene.P, scene.cam.W, scene.cam.H
     K = max(1, args.keyframes)
-    base = init_mapping_params(scene, num_frames=K, device=dev)
-    cam = camera_settings(scene.cam, dev, sh_degree=scene.sh_degree)
-    kfs = mapping_keyframes(base, cam, K, 0, dev)
+    base, cam, kfs = mapping_workload(scene, K, dev, prunable=args.map_prunable)  # the HIP-graph leg's window
     params = as_parameters(base)
     del base
     variables = tracking_variables(P, dev)
@@ -824,7 +797,7 @@ def unfused_render_leg(params, curr, frame, S, P, W, H, Tt, N, replays: int = 4)
             t0 = params["cam_trans"][..., frame].clone()
         tr = GraphTracker(params, curr, frame, iters_per_graph=S, fuse_pose=True, warmup_iters=1, prime=True,
                           timing=True)
-        profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
+        profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)
         torch.cuda.synchronize()
         ta = time.perf_counter()
         tr.track_frame(S * replays, check=False)
@@ -913,17 +886,18 @@ def run_mapping(args, world, rank, dev):
     from splatam_amd import profiling
     from splatam_amd.mapper import GraphMapper
     from splatam_amd.scenes import config_scene
-    from splatam_amd.slam import MappingConfig, camera_settings, color_key, init_mapping_params
+    from splatam_amd.slam import MappingConfig, color_key
+    from splatam_amd.workloads import mapping_workload
 
     scene = config_scene(args.config)
     P, W, H = scene.P, scene.cam.W, scene.cam.H
     K = max(1, args.keyframes)
-    params = init_mapping_params(scene, num_frames=K * max(world, 1), device=dev)
+    # keyframe targets: the map with perturbed colours; --map-prunable of the Gaussians faded under
+    # prune_gaussians' 0.005 opacity threshold, so the frame's pruning iterations remove them
+    params, cam, kfs = mapping_workload(scene, K, dev, rank=rank, world=world, prunable=args.map_prunable)
     sd.broadcast_map(params, keys=tuple(k for k in params))
-    cam = camera_settings(scene.cam, dev, sh_degree=scene.sh_degree)
     w2c = torch.eye(4, device=dev)
     key = color_key(params)
-    kfs = mapping_keyframes(params, cam, K, rank, dev)  # keyframe targets: the map with perturbed colours
     for k in ("means3D", "unnorm_rotations", "logit_opacities", "log_scales", key):
         params[k].requires_grad_(True)
     # one replay = one frame of --map-frame-iters iterations (fresh Adam, prune_gaussians at the iterations
@@ -938,7 +912,7 @@ def run_mapping(args, world, rank, dev):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
+    profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps // S):
@@ -977,7 +951,7 @@ def run_mapping(args, world, rank, dev):
                                "all Gaussian parameters)", "gaussians": P, "width": W, "height": H,
                    "keyframes": K, "parallelism": f"frame-sharded x{world}"},
         "roofline": roofline,
-        "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items()},
+        "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items() if v["launches"]},
     }
     del mapper, params, kfs
     torch.cuda.empty_cache()

@@ -826,9 +826,9 @@ hipError_t launch_render_bwd(const Camera& cam, const uint2* ranges, const uint6
 // mapping variant (1 M anisotropic Gaussians: 65.0 -> 64.0 us capped) and no faster for tracking
 // (profiles/r5z_ab_gauss_bwd_waves.txt)
 template <bool POSE, bool SHL>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 5)))
-gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float* __restrict__ inst,
-                 RecLayout rec, GradsOut out, BwdGuard guard, PoseFuse pf) {
+__device__ __forceinline__ void gauss_bwd_body(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii,
+                                               const float* __restrict__ inst, RecLayout rec, GradsOut out,
+                                               BwdGuard guard, PoseFuse pf) {
     if constexpr (!SHL) {
         g.shs = nullptr;
         g.M = 0;
@@ -1098,18 +1098,27 @@ gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ ra
         for (int k = 48; k < 3 * g.M; k++) d[k] = 0.f;
     }
 }
+template <bool POSE, bool SHL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 5)))
+gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float* __restrict__ inst,
+                 RecLayout rec, GradsOut out, BwdGuard guard, PoseFuse pf, unsigned long long* clk) {
+    kclock_begin(clk);
+    gauss_bwd_body<POSE, SHL>(cam, g, geo, radii, inst, rec, out, guard, pf);
+    kclock_end(clk);
+}
 
 // workgroup partials, arrival counters, the 16 group sums
 int pose_fuse_scratch_floats(int P) { return POSE_PARTS * ((P + 255) / 256) + ARRIVE_GROUPED_WORDS + 16 * POSE_PARTS; }
 
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* inst,
-                            RecLayout rec, const GradsOut& out, BwdGuard guard, hipStream_t s, const PoseFuse* pose) {
+                            RecLayout rec, const GradsOut& out, BwdGuard guard, hipStream_t s, const PoseFuse* pose,
+                            unsigned long long* clk) {
     if (g.P == 0) return hipSuccess;
     const bool shl = g.shs != nullptr;
     auto k = pose ? (shl ? gauss_bwd_kernel<true, true> : gauss_bwd_kernel<true, false>)
                   : (shl ? gauss_bwd_kernel<false, true> : gauss_bwd_kernel<false, false>);
     hipLaunchKernelGGL(k, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii, inst, rec, out, guard,
-                       pose ? *pose : PoseFuse{});
+                       pose ? *pose : PoseFuse{}, clk);
     return hipGetLastError();
 }
 

@@ -395,18 +395,23 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     if (P > 0) {
         if (!radii) return fail(GSR_ERR_INVALID_ARG, "radii output required");
         {
-            StageTimer t(GSR_STAGE_PREPROCESS, P, stream);
+            // (stage clocks in the device-clock mode: preprocess_kernel stamps itself; sh_eval is not timed)
+            StageTimer t(GSR_STAGE_PREPROCESS, P, stream, true);
             if (sh_staged(cam, g)) {  // SH colours with coalesced coefficient reads, ahead of preprocess
                 if ((e = launch_sh_eval(cam, g, geo, stream)) != hipSuccess) return hip_fail(e, "sh_eval");
                 g.sh_staged = 1;
             }
             if ((e = launch_preprocess(cam, g, geo, radii, lds_hist ? cmat : tile_count, lds_hist, ntiles, GL.nb,
-                                       stream)) != hipSuccess)
+                                       stream, t.kclock())) != hipSuccess)
                 return hip_fail(e, "preprocess");
+        }
+        {
+            // the tile-count scans that give the ranges (the "ranges" stage of the bucketed path)
+            StageTimer t(GSR_STAGE_RANGES, ntiles, stream, lds_hist);
             if (lds_hist) {  // column scan (+ instance / tile scans in the same launch unless scan_in_duplicate)
                 if ((e = launch_tile_colscan(cmat, GL.nb, ntiles, tile_tot, geo, ranges,
-                                             capacity > 0 ? status : nullptr, !scan_in_duplicate, stream)) !=
-                    hipSuccess)
+                                             capacity > 0 ? status : nullptr, !scan_in_duplicate, stream,
+                                             t.kclock())) != hipSuccess)
                     return hip_fail(e, "tile count scan");
             } else if ((e = launch_scan_counts(geo, GL.nb, tile_count, TILE_CTR_STRIDE, ntiles, ranges,
                                                capacity > 0 ? status : nullptr, stream)) != hipSuccess) {
@@ -465,11 +470,11 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         bin_ptrs(bin, SL, keys, vals, gid, point_list, hist);
         const SpecGuard guard{geo.counters, cap, (uint32_t)TILE_SORT_CAP};
         {
-            StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
+            StageTimer t(GSR_STAGE_DUPLICATE, P, stream, true);
             if ((e = launch_duplicate_bucket(cplan, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
                                              ntiles, keys[0], point_list, GL.nb, guard,
                                              capacity > 0 ? status : nullptr,
-                                             stream)) != hipSuccess)
+                                             stream, t.kclock())) != hipSuccess)
                 return hip_fail(e, "duplicate");
         }
         if (capacity <= 0 && scan_in_duplicate && (rc = snapshot_counters()) != GSR_OK) return rc;
@@ -514,9 +519,10 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     const bool tile_sorted = I > 0 && longest <= (uint32_t)TILE_SORT_CAP && !force_radix;
     if (tile_sorted) {
         {
-            StageTimer t(GSR_STAGE_DUPLICATE, P, stream);
+            StageTimer t(GSR_STAGE_DUPLICATE, P, stream, true);
             if ((e = launch_duplicate_bucket(cplan, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
-                                             ntiles, keys[0], point_list, GL.nb, none, nullptr, stream)) !=
+                                             ntiles, keys[0], point_list, GL.nb, none, nullptr, stream,
+                                             t.kclock())) !=
                 hipSuccess)
                 return hip_fail(e, "duplicate");
         }
@@ -723,7 +729,8 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
     }
     out.dcolors2 = dcolors2;
     {
-        StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream);
+        // (device-clock mode: gauss_bwd_kernel stamps itself; a staged sh_bwd after it is not timed)
+        StageTimer t(GSR_STAGE_GAUSS_BWD, P, stream, true);
         const BwdGuard guard{geo.counters, (uint32_t)num_rendered};
         GaussIn gc = g;
         GradsOut oc = out;
@@ -738,8 +745,8 @@ static int backward_impl(const gsr_settings* settings, const gsr_gaussians* gaus
             pc = *pose;
             pc.guard = geo.counters;
         }
-        if ((e = launch_gauss_bwd(cam, gc, geo, radii, inst, rec, oc, guard, stream, pose ? &pc : nullptr)) !=
-            hipSuccess)
+        if ((e = launch_gauss_bwd(cam, gc, geo, radii, inst, rec, oc, guard, stream, pose ? &pc : nullptr,
+                                  t.kclock())) != hipSuccess)
             return hip_fail(e, "gaussian backward");
         // the colour step guards on this call's own forward counters (not a sticky status row: an
         // overflow in an earlier replay must not skip the steps of later valid iterations)

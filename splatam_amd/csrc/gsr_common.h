@@ -1175,9 +1175,9 @@ __device__ __forceinline__ uint32_t instance_slot(uint2 rect, uint32_t off, uint
 
 // ------------------------------------------------------- kernel launchers --
 hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* counts,
-                             bool lds_hist, int ntiles, int nb, hipStream_t s);
+                             bool lds_hist, int ntiles, int nb, hipStream_t s, unsigned long long* clk = nullptr);
 hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, GeomPtrs geo, uint2* ranges,
-                               uint32_t* status, bool tail, hipStream_t s);
+                               uint32_t* status, bool tail, hipStream_t s, unsigned long long* clk = nullptr);
 hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hipStream_t s);
 hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
                               uint2* ranges, uint32_t* status, hipStream_t s);
@@ -1224,7 +1224,7 @@ __device__ __forceinline__ void status_merge(uint32_t* st, uint32_t n, uint32_t 
 hipError_t launch_identity_order(uint32_t* order, int ntiles, hipStream_t s);
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2* ranges, const uint32_t* tot,
                                    uint32_t* cursor, bool lds_hist, int ntiles, uint64_t* keys, uint64_t* point_list,
-                                   int nb, SpecGuard guard, uint32_t* status, hipStream_t s);
+                                   int nb, SpecGuard guard, uint32_t* status, hipStream_t s, unsigned long long* clk = nullptr);
 hipError_t launch_radix_sort(uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t n, int nsb, int npass,
                              hipStream_t s);
 hipError_t launch_gather_ids(const uint32_t* vals, const uint32_t* gid, uint64_t* point_list, uint32_t n,
@@ -1323,7 +1323,7 @@ struct PoseFuse {
 int pose_fuse_scratch_floats(int P);
 hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* inst,
                             RecLayout rec, const GradsOut& out, BwdGuard guard, hipStream_t s,
-                            const PoseFuse* pose = nullptr);
+                            const PoseFuse* pose = nullptr, unsigned long long* clk = nullptr);
 hipError_t launch_selftest_reduce9(const float* in, float* out, hipStream_t s);
 // gsr_sh.hip: SH colour stages with LDS-staged, coalesced coefficient traffic
 bool sh_staged(const Camera& cam, const GaussIn& g);

@@ -28,8 +28,10 @@ namespace gsr {
 // formed here from the world-frame map and the pose, and stored to g's arrays for the backward.
 template <bool LDS_HIST, bool XF>
 __global__ void __launch_bounds__(PRE_BLOCK)
-preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __restrict__ counts, int ntiles) {
+preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __restrict__ counts, int ntiles,
+                  unsigned long long* clk) {
 #pragma clang fp contract(off)
+    kclock_begin(clk);  // (stage clock: first workgroup's start to the last one's end; nullptr = off)
     extern __shared__ uint32_t s_hist[];
     __shared__ float s_pose[16];  // XF: the frame's pose (R 9, t 3, F.normalize(q) 4), formed once by wave 0
     const int i = (blockIdx.x << cam.pre_shift) + threadIdx.x;  // blockDim.x = 1 << pre_shift
@@ -220,16 +222,17 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     }
     if (LDS_HIST)
         for (int t = threadIdx.x; t < ntiles; t += blockDim.x) counts[(size_t)blockIdx.x * ntiles + t] = s_hist[t];
+    kclock_end(clk);
 }
 
 hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* counts,
-                             bool lds_hist, int ntiles, int nb, hipStream_t s) {
+                             bool lds_hist, int ntiles, int nb, hipStream_t s, unsigned long long* clk) {
     if (nb == 0) return hipSuccess;
     const bool xf = g.xf.mw != nullptr;
     auto k = lds_hist ? (xf ? preprocess_kernel<true, true> : preprocess_kernel<true, false>)
                       : (xf ? preprocess_kernel<false, true> : preprocess_kernel<false, false>);
     hipLaunchKernelGGL(k, dim3(nb), dim3(1 << cam.pre_shift), lds_hist ? sizeof(uint32_t) * ntiles : 0, s, cam, g,
-                       geo, radii, counts, ntiles);
+                       geo, radii, counts, ntiles, clk);
     return hipGetLastError();
 }
 
@@ -267,9 +270,9 @@ constexpr int SCAN_ITEMS = 4;
 // prologue, which removes this launch's serial tail (arrival + one-workgroup
 // scan: ~10 us of latency at config 3).
 template <bool TAIL, int CT>
-__global__ void __launch_bounds__(CS_THREADS)
-tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t* __restrict__ tot, GeomPtrs geo,
-                    uint2* __restrict__ ranges, uint32_t sort_cap, uint32_t* __restrict__ status) {
+__device__ __forceinline__ void tile_colscan_body(uint32_t* __restrict__ counts, int nb, int ntiles,
+                                                  uint32_t* __restrict__ tot, GeomPtrs geo, uint2* __restrict__ ranges,
+                                                  uint32_t sort_cap, uint32_t* __restrict__ status) {
     constexpr int CS_TILES = ColscanShape<CT>::TILES, CS_PARTS = ColscanShape<CT>::PARTS, CS_RQ = ColscanShape<CT>::RQ;
     __shared__ uint32_t s_part[CS_PARTS][CS_TILES];
     const int tl = threadIdx.x % CS_TILES, q = threadIdx.x / CS_TILES;
@@ -334,15 +337,24 @@ tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t*
     scan_counts_body<true>(geo.wgsum, geo.blocksums, (uint32_t)nb, tot, 1u, (uint32_t)ntiles, ranges, geo.counters,
                            sort_cap, status);
 }
+template <bool TAIL, int CT>
+__global__ void __launch_bounds__(CS_THREADS)
+tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t* __restrict__ tot, GeomPtrs geo,
+                    uint2* __restrict__ ranges, uint32_t sort_cap, uint32_t* __restrict__ status,
+                    unsigned long long* clk) {
+    kclock_begin(clk);
+    tile_colscan_body<TAIL, CT>(counts, nb, ntiles, tot, geo, ranges, sort_cap, status);
+    kclock_end(clk);
+}
 
 hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, GeomPtrs geo, uint2* ranges,
-                               uint32_t* status, bool tail, hipStream_t s) {
+                               uint32_t* status, bool tail, hipStream_t s, unsigned long long* clk) {
     static_assert(CS_THREADS == SCAN_THREADS, "the last colscan workgroup runs the scan body");
     const int ct = nb <= CS_ROWS_SMALL ? 16 : 32;
     auto k = tail ? (ct == 16 ? tile_colscan_kernel<true, 16> : tile_colscan_kernel<true, 32>)
                   : (ct == 16 ? tile_colscan_kernel<false, 16> : tile_colscan_kernel<false, 32>);
     hipLaunchKernelGGL(k, dim3((ntiles + ct - 1) / ct), dim3(CS_THREADS), 0, s, counts, nb, ntiles, tot, geo, ranges,
-                       (uint32_t)TILE_SORT_CAP, status);
+                       (uint32_t)TILE_SORT_CAP, status, clk);
     return hipGetLastError();
 }
 
@@ -662,18 +674,18 @@ constexpr int DUP_T = 512;
 #define GSR_NO_PLAN 0  // timing experiment: row-major render order instead of tile_plan
 #endif
 template <bool LDS_HIST, int DUP_G>
-__global__ void __launch_bounds__(DUP_T)
-duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges, const uint32_t* __restrict__ tot,
-                        uint32_t* __restrict__ cursor, int ntiles, uint64_t* __restrict__ keys,
-                        uint64_t* __restrict__ point_list, SpecGuard guard, uint32_t sort_cap,
-                        uint32_t* __restrict__ status) {
+__device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges,
+                                                      const uint32_t* __restrict__ tot, uint32_t* __restrict__ cursor,
+                                                      int ntiles, uint64_t* __restrict__ keys,
+                                                      uint64_t* __restrict__ point_list, SpecGuard guard,
+                                                      uint32_t sort_cap, uint32_t* __restrict__ status,
+                                                      uint32_t* __restrict__ s_cur) {
     // LDS_HIST: cursor = the column-scanned count matrix; this workgroup's
     // instances of tile t go to start[t] + cursor[block][t] + (LDS rank)
     // Culled instances (Camera::cull) are in no bucket: they fill point_list's tail [L, num_rendered)
     // (L = the buckets' total) in (Gaussian, rect tile) order, as PointEntry (empty block mask << 32 | id), so
     // every one of the num_rendered entries the forward returns is a valid Gaussian id.
     constexpr int ROW = DUP_G * DUP_T;  // Gaussians per count-matrix row (1 << cam.pre_shift)
-    extern __shared__ uint32_t s_cur[];
     __shared__ uint32_t s_incl[ROW];
     __shared__ uint32_t s_x0[ROW], s_y0[ROW], s_w[ROW], s_depth[ROW], s_live[ROW], s_cx[ROW];
     __shared__ uint32_t wsum[DUP_T / 64], s_tmax[DUP_T / 64], s_cws[DUP_T / 64];
@@ -922,16 +934,28 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
         keys[pos] = ((uint64_t)s_depth[lo] << 32) | (uint64_t)gi;
     }
 }
+template <bool LDS_HIST, int DUP_G>
+__global__ void __launch_bounds__(DUP_T)
+duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges, const uint32_t* __restrict__ tot,
+                        uint32_t* __restrict__ cursor, int ntiles, uint64_t* __restrict__ keys,
+                        uint64_t* __restrict__ point_list, SpecGuard guard, uint32_t sort_cap,
+                        uint32_t* __restrict__ status, unsigned long long* clk) {
+    extern __shared__ uint32_t s_cur[];
+    kclock_begin(clk);
+    duplicate_bucket_body<LDS_HIST, DUP_G>(cam, P, geo, ranges, tot, cursor, ntiles, keys, point_list, guard, sort_cap,
+                                           status, s_cur);
+    kclock_end(clk);
+}
 
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2* ranges, const uint32_t* tot,
                                    uint32_t* cursor, bool lds_hist, int ntiles, uint64_t* keys, uint64_t* point_list,
-                                   int nb, SpecGuard guard, uint32_t* status, hipStream_t s) {
+                                   int nb, SpecGuard guard, uint32_t* status, hipStream_t s, unsigned long long* clk) {
     if (nb == 0) return hipSuccess;
     const bool g2 = cam.pre_shift == 10;  // rows of 1024: two Gaussians per lane; of 512: one
     auto k = lds_hist ? (g2 ? duplicate_bucket_kernel<true, 2> : duplicate_bucket_kernel<true, 1>)
                       : (g2 ? duplicate_bucket_kernel<false, 2> : duplicate_bucket_kernel<false, 1>);
     hipLaunchKernelGGL(k, dim3(nb), dim3(DUP_T), lds_hist ? sizeof(uint32_t) * ntiles : 0, s, cam, P, geo, ranges,
-                       tot, cursor, ntiles, keys, point_list, guard, (uint32_t)TILE_SORT_CAP, status);
+                       tot, cursor, ntiles, keys, point_list, guard, (uint32_t)TILE_SORT_CAP, status, clk);
     return hipGetLastError();
 }
 

@@ -125,7 +125,7 @@ class GraphMapper:
         del snapshot
         if timing:
             from . import profiling
-            profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
+            profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)
         self.graph = torch.cuda.CUDAGraph()
         self.stream = side
         with torch.cuda.graph(self.graph, stream=side):

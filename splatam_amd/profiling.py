@@ -7,6 +7,10 @@ import ctypes
 from ._lib import lib
 
 STAGES = ("preprocess", "duplicate", "sort", "ranges", "render_fwd", "render_bwd", "gauss_bwd")
+# the stages whose kernels stamp themselves in the device-clock mode (first workgroup's start to the last
+# workgroup's end, no extra launches): every kernel of a captured tracking / mapping iteration except sh_eval /
+# sh_bwd and the radix fallback
+CLOCK_STAGES = ("preprocess", "ranges", "duplicate", "render_fwd", "render_bwd", "gauss_bwd")
 
 
 GSR_TIMING_CLOCK = 0x100

@@ -403,14 +403,15 @@ def get_loss_mapping(params, curr_data, iter_time_idx, cfg: MappingConfig = Mapp
 
 
 def map_frame_literal(params, variables, keyframes, num_iters, cfg: MappingConfig = MappingConfig(), optimizer=None,
-                      renderer=None, rng=None, losses_out=None):
+                      renderer=None, rng=None, losses_out=None, loss_dtype=None):
     """The unchanged mapping loop body of scripts/splatam.py:841-905 for one frame (no progress reports): a
     fresh torch Adam over every parameter group (initialize_optimizer, :842), then per iteration a keyframe
     drawn with np.random.randint (:851), get_loss(mapping=True) through two GaussianRasterizer calls,
     loss.backward(), then (:876-884) prune_gaussians when cfg.prune_gaussians and densify when
     cfg.use_gaussian_splatting_densification (surgery.py restatements; both replace tensors of `params` and
     need variables["scene_radius"]), optimizer.step(), zero_grad.  keyframes: dicts with cam / im / depth /
-    w2c / id.  `params` is updated in place (entries replaced when P changes).  Returns the optimizer."""
+    w2c / id.  `params` is updated in place (entries replaced when P changes).  loss_dtype: the loss terms in
+    that precision (torch.float64: a tighter test reference).  Returns the optimizer."""
     import numpy as np
     from . import surgery
     rng = np.random if rng is None else rng
@@ -419,7 +420,7 @@ def map_frame_literal(params, variables, keyframes, num_iters, cfg: MappingConfi
     for it in range(num_iters):
         kf = keyframes[int(rng.randint(0, len(keyframes)))]
         loss, _radius, _m2d = get_loss_mapping(params, kf, kf["id"], cfg, fused=False, variables=variables,
-                                               renderer=renderer)
+                                               renderer=renderer, loss_dtype=loss_dtype)
         loss.backward()
         with torch.no_grad():
             if cfg.prune_gaussians:

@@ -98,7 +98,7 @@ class GraphTracker:
         if timing:  # device-clock stamps of render_bwd / render_fwd (in-kernel) (accumulate over replays)
             from . import profiling
             torch.cuda.synchronize(dev)
-            profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
+            profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)
         self.graph = torch.cuda.CUDAGraph()
         self.stream = side
         with torch.cuda.graph(self.graph, stream=side):  # capture on the warm-up stream (autograd nodes live there)
@@ -127,7 +127,7 @@ class GraphTracker:
             torch.cuda.synchronize(dev)
             if timing:
                 from . import profiling
-                profiling.enable_timing(clock_stages=("render_bwd", "render_fwd"))
+                profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)
 
     def _iteration(self, k: int):
         self.adam.status = self.status[k]  # this iteration's forward guards its Adam step
