@@ -95,6 +95,10 @@ def parse():
     ap.add_argument("--unfused-leg", choices=("on", "off"), default="on",
                     help="with --fuse-render 1 at N=1: also time a few iterations with separate render launches "
                          "(roofline.unfused: render_bwd's own time and roofline)")
+    ap.add_argument("--stage-clocks", choices=("all", "render"), default="render",
+                    help="tracking: the kernels whose in-kernel stage clocks run in the timed replays (render: the "
+                         "render kernel only, stages_us from a separate pass with every clock on; all: every stage "
+                         "in the timed replays, ~5 us per iteration of stamps)")
     ap.add_argument("--timing", type=int, default=1,
                     help="0: no device-clock timing of render_bwd in the graph (A/B check; no roofline)")
     return ap.parse_args()
@@ -177,9 +181,10 @@ def main():
         S = math.gcd(math.gcd(max(1, args.iters_per_graph), FI), max(1, steps))
         # warm-up: W eager tracking iterations plus one priming replay, all undone (pose restored,
         # optimizer reset) before the timed frames
+        clock_stages = profiling.CLOCK_STAGES if args.stage_clocks == "all" else ("render_fwd", "render_bwd")
         tracker = GraphTracker(params, curr, frame, iters_per_graph=S, timing=bool(args.timing),
                                fuse_pose=bool(args.fuse_pose), warmup_iters=max(1, args.warmup), prime=True,
-                               prime_ms=args.settle_ms)
+                               prime_ms=args.settle_ms, clock_stages=clock_stages)
     else:
         for _ in range(args.warmup):
             step()
@@ -189,7 +194,7 @@ def main():
     if tracker is None:
         profiling.enable_timing(True)
     else:  # reset the device-clock accumulators the captured stamps add to
-        profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)
+        profiling.enable_timing(clock_stages=tracker.clock_stages)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if tracker is not None:
@@ -223,6 +228,30 @@ def main():
     elapsed = sd.max_over_ranks(t1 - t0, device=dev)
     frames = steps * world
     value = frames / elapsed
+    # Per-stage breakdown: every kernel's in-kernel clock on, in a separate pass of the same frames after the
+    # timed region (the stamps cost ~5 us per iteration -- 6510 vs 6290 frames/s interleaved,
+    # profiles/r9i_ab_stage_clocks.txt -- so the timed replays clock the render kernel only)
+    stages_timed = {k: round(v["avg_us"], 2) for k, v in stages.items() if v["launches"]}
+    stages_breakdown, stages_source = stages_timed, "the timed replays' in-kernel stage clocks"
+    if tracker is not None and args.timing and args.stage_clocks == "render":
+        bt = GraphTracker(params, curr, frame, iters_per_graph=S, timing=True, fuse_pose=bool(args.fuse_pose),
+                          warmup_iters=1, prime=True, prime_ms=args.settle_ms, clock_stages=profiling.CLOCK_STAGES)
+        profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)
+        done = 0
+        while done < steps:
+            n = min(FI, steps - done)
+            bt.track_frame(n, check=False)
+            done += n
+        torch.cuda.synchronize()
+        stages_breakdown = {k: round(v["avg_us"], 2) for k, v in profiling.read_timing().items() if v["launches"]}
+        profiling.enable_timing(False)
+        if bt.overflowed():
+            raise SystemExit("binning capacity overflow in the stage-breakdown pass")
+        stages_source = (f"a separate pass of the same {steps} iterations after the timed region with every "
+                         "kernel's in-kernel stage clock on (the timed replays clock the render kernel only)")
+        del bt
+    if stages["render_bwd"]["launches"] == 0 and stages["render_fwd"]["launches"] > 0:  # fused: render_track
+        stages_breakdown = {("render_track" if k == "render_fwd" else k): v for k, v in stages_breakdown.items()}
     # the same timed frames without the broadcast, and the broadcast alone
     bcast_split = None
     if world > 1 and tracker is not None:
@@ -385,9 +414,9 @@ def main():
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
-            # per launch, from the in-kernel stage clocks of every launch in the timed replays (the per-tile sort runs
-            # inside render_fwd / render_track: no "sort" stage; "ranges" is the tile-count column scan)
-            "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items() if v["launches"]},
+            # per launch, from in-kernel stage clocks (the per-tile sort runs inside render_fwd / render_track: no
+            # "sort" stage; "ranges" is the tile-count column scan)
+            "stages_us": stages_breakdown, "stages_source": stages_source,
             "dropin": dropin,
             "fisher": fisher,
             "mapping": mapping,

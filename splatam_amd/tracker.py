@@ -60,7 +60,7 @@ class GraphTracker:
     def __init__(self, params: dict, curr_data: dict, time_idx: int, iters_per_graph: int = 20,
                  cfg: TrackingConfig = TrackingConfig(), lrs=(0.0004, 0.002), headroom: float = 1.5,
                  warmup_iters: int = 3, min_extra: int = 65536, timing: bool = False, fuse_pose: bool = False,
-                 prime: bool = False, prime_ms: float = 0.0):
+                 prime: bool = False, prime_ms: float = 0.0, clock_stages=None):
         if not fused_eligible(params, curr_data, cfg):
             raise RuntimeError("GraphTracker needs the fused tracking configuration (only the pose requires grad)")
         self.params, self.curr, self.t, self.cfg = params, curr_data, time_idx, cfg
@@ -95,10 +95,11 @@ class GraphTracker:
             self.status.zero_()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
-        if timing:  # device-clock stamps of render_bwd / render_fwd (in-kernel) (accumulate over replays)
-            from . import profiling
+        from . import profiling
+        self.clock_stages = tuple(clock_stages) if clock_stages is not None else profiling.CLOCK_STAGES
+        if timing:  # in-kernel device-clock stamps of the captured stages (accumulate over replays)
             torch.cuda.synchronize(dev)
-            profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)
+            profiling.enable_timing(clock_stages=self.clock_stages)
         self.graph = torch.cuda.CUDAGraph()
         self.stream = side
         with torch.cuda.graph(self.graph, stream=side):  # capture on the warm-up stream (autograd nodes live there)
@@ -126,8 +127,7 @@ class GraphTracker:
             self.status.zero_()
             torch.cuda.synchronize(dev)
             if timing:
-                from . import profiling
-                profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)
+                profiling.enable_timing(clock_stages=self.clock_stages)
 
     def _iteration(self, k: int):
         self.adam.status = self.status[k]  # this iteration's forward guards its Adam step

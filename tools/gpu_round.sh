@@ -181,7 +181,7 @@ PY
 import json, sys
 b = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][-1]
 print("abflag", sys.argv[2], "round", sys.argv[3], "frames/s", b["value"], "kernel", b["roofline"]["kernel"],
-      "avg_us", b["roofline"]["avg_us"], "render_fwd", b["stages_us"]["render_fwd"], "render_bwd", b["stages_us"]["render_bwd"])
+      "avg_us", b["roofline"]["avg_us"], "stages_us", b["stages_us"])
 PY
             done
           done ;;
