@@ -99,6 +99,9 @@ def parse():
                     help="tracking: the kernels whose in-kernel stage clocks run in the timed replays (render: the "
                          "render kernel only, stages_us from a separate pass with every clock on; all: every stage "
                          "in the timed replays, ~5 us per iteration of stamps)")
+    ap.add_argument("--stage-breakdown", choices=("on", "off"), default="on",
+                    help="tracking: the separate all-clocks pass after the timed region that gives stages_us (off: "
+                         "profiling runs, whose kernel averages it would mix with the clocked launches)")
     ap.add_argument("--timing", type=int, default=1,
                     help="0: no device-clock timing of render_bwd in the graph (A/B check; no roofline)")
     return ap.parse_args()
@@ -233,7 +236,7 @@ def main():
     # profiles/r9i_ab_stage_clocks.txt -- so the timed replays clock the render kernel only)
     stages_timed = {k: round(v["avg_us"], 2) for k, v in stages.items() if v["launches"]}
     stages_breakdown, stages_source = stages_timed, "the timed replays' in-kernel stage clocks"
-    if tracker is not None and args.timing and args.stage_clocks == "render":
+    if tracker is not None and args.timing and args.stage_clocks == "render" and args.stage_breakdown == "on":
         bt = GraphTracker(params, curr, frame, iters_per_graph=S, timing=True, fuse_pose=bool(args.fuse_pose),
                           warmup_iters=1, prime=True, prime_ms=args.settle_ms, clock_stages=profiling.CLOCK_STAGES)
         profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)

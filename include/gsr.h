@@ -74,8 +74,11 @@ typedef struct gsr_settings {
      * num_rendered and gradients are bitwise those of the reference's lists.  GSR_BINNING_REFERENCE (1):
      * every rect instance listed, rasterizer_impl.cu:290-315 entry for entry.  Either way the binning
      * buffer's point list holds num_rendered valid entries: point_list[0, L) are the tiles' sorted lists
-     * (L = the ranges' total) and point_list[L, num_rendered) the culled instances (Gaussian id, empty
-     * block mask), so its ids are the reference's multiset (Gaussian i appears tiles_touched(i) times). */
+     * (L = the ranges' total) and point_list[L, num_rendered) has an empty block mask and a valid Gaussian
+     * id -- in gsr_forward / gsr_forward_dual (the buffers a caller reads like the reference's) the culled
+     * instances themselves, so the ids are the reference's multiset (Gaussian i appears tiles_touched(i)
+     * times); in the static-capacity forwards, whose buffers only this library reads, padding (the Gaussian
+     * owning each of the last rect instance slots), which costs the binning nothing. */
     int binning;
 } gsr_settings;
 

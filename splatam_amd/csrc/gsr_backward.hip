@@ -364,9 +364,8 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
     float T = T_final, A = bg_dot;
     [[maybe_unused]] float ablate_sink = 0.f;  // (timing ablation 1)
     const int my_e = row_entry(lane);
-    // Slots start zero; after every batch the entry totals re-zero exactly the slots they read
-    // (every slot a row list can have written), and the pad slot only ever receives zeros, so no
-    // per-batch clear is needed.
+    // Slots start zero; after every batch the used slots (those of the batch's entries, every slot a row
+    // list can have written) are cleared, and the pad slot only ever receives zeros.
     for (int q = tid; q < (BS + 1) * NV; q += TILE_PIX) s_acc[q] = 0.f;
     const uint32_t* my_list = s_list + (4 * w + row) * LS;
     if (tid == 0) {
@@ -619,14 +618,11 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
 #pragma unroll
             for (int i = 0; i < NQ; i++) c[i] = 0.f;
             const int nb = __popc((uint32_t)s_mask[e]);
-            float* src = s_acc + (int)s_base[e] * NV;
+            const float* src = s_acc + (int)s_base[e] * NV;
             for (int b = 0; b < nb; b++, src += NV) {
 #pragma unroll
                 for (int i = 0; i < NQ; i++)
-                    if (q + TPE * i < NV) {
-                        c[i] += src[q + TPE * i];
-                        src[q + TPE * i] = 0.f;
-                    }
+                    if (q + TPE * i < NV) c[i] += src[q + TPE * i];
             }
             float* dst = inst + (size_t)RS * s_u[e];  // packed record (RecLayout): the NV sums, zero pad
 #pragma unroll
@@ -641,6 +637,16 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
         }
         dg.phase(5);
         __syncthreads();
+        // The batch's slots back to zero for the next batch's reduction: the used range [0, slots of entries
+        // < cnt) as contiguous float4 stores (the next batch's staging barrier orders them before its walk).
+        // Re-zeroing each slot right after reading it cost bank-conflicted scattered stores in the totals
+        // (slot stride NV = 6 words: entries whose slot bases differ by 16 share banks)
+        {
+            const int used = cnt > 0 ? (int)s_base[cnt - 1] + __popc((uint32_t)s_mask[cnt - 1]) : 0;
+            float4* const a4 = reinterpret_cast<float4*>(s_acc);
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int q4 = tid; q4 < (used * NV + 3) / 4; q4 += TILE_PIX) a4[q4] = z;
+        }
         dg.phase(6);
         dg.batch();
         hi -= cnt;
@@ -1098,13 +1104,13 @@ __device__ __forceinline__ void gauss_bwd_body(Camera cam, GaussIn g, GeomPtrs g
         for (int k = 48; k < 3 * g.M; k++) d[k] = 0.f;
     }
 }
-template <bool POSE, bool SHL>
+template <bool POSE, bool SHL, bool CLK>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 5)))
 gauss_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float* __restrict__ inst,
                  RecLayout rec, GradsOut out, BwdGuard guard, PoseFuse pf, unsigned long long* clk) {
-    kclock_begin(clk);
+    if constexpr (CLK) kclock_begin(clk);
     gauss_bwd_body<POSE, SHL>(cam, g, geo, radii, inst, rec, out, guard, pf);
-    kclock_end(clk);
+    if constexpr (CLK) kclock_end(clk);
 }
 
 // workgroup partials, arrival counters, the 16 group sums
@@ -1115,8 +1121,10 @@ hipError_t launch_gauss_bwd(const Camera& cam, const GaussIn& g, GeomPtrs geo, c
                             unsigned long long* clk) {
     if (g.P == 0) return hipSuccess;
     const bool shl = g.shs != nullptr;
-    auto k = pose ? (shl ? gauss_bwd_kernel<true, true> : gauss_bwd_kernel<true, false>)
-                  : (shl ? gauss_bwd_kernel<false, true> : gauss_bwd_kernel<false, false>);
+    auto k = clk ? (pose ? (shl ? gauss_bwd_kernel<true, true, true> : gauss_bwd_kernel<true, false, true>)
+                         : (shl ? gauss_bwd_kernel<false, true, true> : gauss_bwd_kernel<false, false, true>))
+                 : (pose ? (shl ? gauss_bwd_kernel<true, true, false> : gauss_bwd_kernel<true, false, false>)
+                         : (shl ? gauss_bwd_kernel<false, true, false> : gauss_bwd_kernel<false, false, false>));
     hipLaunchKernelGGL(k, dim3((g.P + 255) / 256), dim3(256), 0, s, cam, g, geo, radii, inst, rec, out, guard,
                        pose ? *pose : PoseFuse{}, clk);
     return hipGetLastError();

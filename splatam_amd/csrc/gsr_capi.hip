@@ -365,6 +365,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     const bool force_radix = force_radix_env && capacity <= 0;
     // tile culling: a per-call choice (gsr_settings.binning), no process-wide mode
     cam.cull = (GSR_TILE_CULL && settings->binning != GSR_BINNING_REFERENCE) ? 1 : 0;
+    cam.tail_exact = capacity <= 0 ? 1 : 0;  // (include/gsr.h: the culled instances, or padding in static mode)
     // the bucketed duplicate's workgroup 0 writes the render schedule (tile_plan); the other paths
     // render in row-major order
     Camera cplan = cam;

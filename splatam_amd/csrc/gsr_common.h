@@ -171,6 +171,9 @@ struct Camera {
     // reads to skip the unwritten slots.  Results are bitwise those of the unculled lists; num_rendered
     // (the record count) is unchanged, the tile ranges are shorter.
     int cull = 0;
+    // point_list's tail [L, num_rendered) of a culled binning: 1 the culled instances themselves (the dynamic
+    // forward, whose buffers the caller reads like the reference's), 0 padding ids (static mode)
+    int tail_exact = 0;
 };
 // bin[i].w: bit k set = rect tile k (row-major in the rect) has an instance in its bucket; all ones when
 // nothing is culled (or the rect has more than 32 tiles)

@@ -16,7 +16,14 @@
 #include "gsr_diag.h"
 #include "gsr_render_fwd.h"
 
+#ifndef GSR_CULL_TAIL
+#define GSR_CULL_TAIL 1  // culled instances written to point_list's tail (0: timing experiments only)
+#endif
+
 namespace gsr {
+
+constexpr bool kCullTail = GSR_CULL_TAIL != 0;
+
 
 // ------------------------------------------------------------- preprocess --
 // LDS_HIST: per-tile instance counts go to a workgroup histogram in LDS and
@@ -26,12 +33,13 @@ namespace gsr {
 // per-tile counters (fallback for > MAX_LDS_TILES tiles).
 // XF: SplaTAM's tracking transform fused in (g.xf, TrackXf): the camera-frame rendervars are
 // formed here from the world-frame map and the pose, and stored to g's arrays for the backward.
-template <bool LDS_HIST, bool XF>
+// CLK: the in-kernel stage clock (a separate instantiation: the production launches carry none of it)
+template <bool LDS_HIST, bool XF, bool CLK>
 __global__ void __launch_bounds__(PRE_BLOCK)
 preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __restrict__ counts, int ntiles,
                   unsigned long long* clk) {
 #pragma clang fp contract(off)
-    kclock_begin(clk);  // (stage clock: first workgroup's start to the last one's end; nullptr = off)
+    if constexpr (CLK) kclock_begin(clk);  // (stage clock: first workgroup's start to the last one's end)
     extern __shared__ uint32_t s_hist[];
     __shared__ float s_pose[16];  // XF: the frame's pose (R 9, t 3, F.normalize(q) 4), formed once by wave 0
     const int i = (blockIdx.x << cam.pre_shift) + threadIdx.x;  // blockDim.x = 1 << pre_shift
@@ -166,7 +174,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                                                     : tile_reached(mg, (float)(tx * TILE_X), (float)(ty * TILE_Y)))
                                         ? 1u << k : 0u;
                 }
-                culled = culled_below(live, tiles);
+                if (kCullTail && cam.tail_exact) culled = culled_below(live, tiles);
                 geo.bin[i] = make_uint4(rlo, rhi, __float_as_uint(pv.z), live);
                 if (!g.sh_staged && !g.colors) geo.clamp[i] = clamped;  // (read only by the SH backward)
                 for (int ty = y0, k = 0; ty < y1; ty++)  // per-tile instance counts -> bucket ranges
@@ -194,7 +202,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t incl = wave_incl_scan(tiles);
     if (lane == 63) wsum[wv] = incl;
-    if (cam.cull) {  // the workgroup's culled instances: duplicate places them in point_list's tail
+    if (kCullTail && cam.cull && cam.tail_exact) {  // the workgroup's culled instances (the exact tail, duplicate)
         const uint32_t cincl = wave_incl_scan(culled);
         if (lane == 63) wcul[wv] = cincl;
     }
@@ -216,21 +224,23 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     if (threadIdx.x == blockDim.x - 1) {
         geo.wgsum[blockIdx.x] = (woff + incl) | (viol ? 0x80000000u : 0u);
         uint32_t cw = 0;
-        if (cam.cull)
+        if (kCullTail && cam.cull && cam.tail_exact)
             for (int k = 0; k < (int)(blockDim.x >> 6); k++) cw += wcul[k];
-        geo.wgcull[blockIdx.x] = cw;
+        if (kCullTail) geo.wgcull[blockIdx.x] = cw;
     }
     if (LDS_HIST)
         for (int t = threadIdx.x; t < ntiles; t += blockDim.x) counts[(size_t)blockIdx.x * ntiles + t] = s_hist[t];
-    kclock_end(clk);
+    if constexpr (CLK) kclock_end(clk);
 }
 
 hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* counts,
                              bool lds_hist, int ntiles, int nb, hipStream_t s, unsigned long long* clk) {
     if (nb == 0) return hipSuccess;
     const bool xf = g.xf.mw != nullptr;
-    auto k = lds_hist ? (xf ? preprocess_kernel<true, true> : preprocess_kernel<true, false>)
-                      : (xf ? preprocess_kernel<false, true> : preprocess_kernel<false, false>);
+    auto k = clk ? (lds_hist ? (xf ? preprocess_kernel<true, true, true> : preprocess_kernel<true, false, true>)
+                             : (xf ? preprocess_kernel<false, true, true> : preprocess_kernel<false, false, true>))
+                 : (lds_hist ? (xf ? preprocess_kernel<true, true, false> : preprocess_kernel<true, false, false>)
+                             : (xf ? preprocess_kernel<false, true, false> : preprocess_kernel<false, false, false>));
     hipLaunchKernelGGL(k, dim3(nb), dim3(1 << cam.pre_shift), lds_hist ? sizeof(uint32_t) * ntiles : 0, s, cam, g,
                        geo, radii, counts, ntiles, clk);
     return hipGetLastError();
@@ -337,22 +347,24 @@ __device__ __forceinline__ void tile_colscan_body(uint32_t* __restrict__ counts,
     scan_counts_body<true>(geo.wgsum, geo.blocksums, (uint32_t)nb, tot, 1u, (uint32_t)ntiles, ranges, geo.counters,
                            sort_cap, status);
 }
-template <bool TAIL, int CT>
+template <bool TAIL, int CT, bool CLK>
 __global__ void __launch_bounds__(CS_THREADS)
 tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t* __restrict__ tot, GeomPtrs geo,
                     uint2* __restrict__ ranges, uint32_t sort_cap, uint32_t* __restrict__ status,
                     unsigned long long* clk) {
-    kclock_begin(clk);
+    if constexpr (CLK) kclock_begin(clk);
     tile_colscan_body<TAIL, CT>(counts, nb, ntiles, tot, geo, ranges, sort_cap, status);
-    kclock_end(clk);
+    if constexpr (CLK) kclock_end(clk);
 }
 
 hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, GeomPtrs geo, uint2* ranges,
                                uint32_t* status, bool tail, hipStream_t s, unsigned long long* clk) {
     static_assert(CS_THREADS == SCAN_THREADS, "the last colscan workgroup runs the scan body");
     const int ct = nb <= CS_ROWS_SMALL ? 16 : 32;
-    auto k = tail ? (ct == 16 ? tile_colscan_kernel<true, 16> : tile_colscan_kernel<true, 32>)
-                  : (ct == 16 ? tile_colscan_kernel<false, 16> : tile_colscan_kernel<false, 32>);
+    auto k = clk ? (tail ? (ct == 16 ? tile_colscan_kernel<true, 16, true> : tile_colscan_kernel<true, 32, true>)
+                         : (ct == 16 ? tile_colscan_kernel<false, 16, true> : tile_colscan_kernel<false, 32, true>))
+                 : (tail ? (ct == 16 ? tile_colscan_kernel<true, 16, false> : tile_colscan_kernel<true, 32, false>)
+                         : (ct == 16 ? tile_colscan_kernel<false, 16, false> : tile_colscan_kernel<false, 32, false>));
     hipLaunchKernelGGL(k, dim3((ntiles + ct - 1) / ct), dim3(CS_THREADS), 0, s, counts, nb, ntiles, tot, geo, ranges,
                        (uint32_t)TILE_SORT_CAP, status, clk);
     return hipGetLastError();
@@ -673,7 +685,7 @@ constexpr int DUP_T = 512;
 #ifndef GSR_NO_PLAN
 #define GSR_NO_PLAN 0  // timing experiment: row-major render order instead of tile_plan
 #endif
-template <bool LDS_HIST, int DUP_G>
+template <bool LDS_HIST, int DUP_G, bool EXACT>
 __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges,
                                                       const uint32_t* __restrict__ tot, uint32_t* __restrict__ cursor,
                                                       int ntiles, uint64_t* __restrict__ keys,
@@ -682,12 +694,19 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
                                                       uint32_t* __restrict__ s_cur) {
     // LDS_HIST: cursor = the column-scanned count matrix; this workgroup's
     // instances of tile t go to start[t] + cursor[block][t] + (LDS rank)
-    // Culled instances (Camera::cull) are in no bucket: they fill point_list's tail [L, num_rendered)
-    // (L = the buckets' total) in (Gaussian, rect tile) order, as PointEntry (empty block mask << 32 | id), so
-    // every one of the num_rendered entries the forward returns is a valid Gaussian id.
+    // Culled instances (Camera::cull) are in no bucket, so the tile lists fill point_list[0, L) with L <
+    // num_rendered; the tail [L, num_rendered) is written too, so every one of the num_rendered entries the
+    // forward returns is a valid Gaussian id with an empty block mask (PointEntry = mask << 32 | id):
+    //   EXACT (the dynamic, drop-in forward): the culled instances themselves, in (Gaussian, rect tile) order --
+    //     the ids are then the reference's multiset (Gaussian i listed tiles_touched(i) times);
+    //   else (static mode: the library is the only reader): padding -- slot u of the tail holds the Gaussian
+    //     owning rect instance slot u (offsets[i] <= u < offsets[i] + tiles[i]), which needs no global prefix of
+    //     the culled counts (that bookkeeping cost the kernel 16 VGPRs and a second dispatch round).
+    constexpr bool TAIL = kCullTail;
     constexpr int ROW = DUP_G * DUP_T;  // Gaussians per count-matrix row (1 << cam.pre_shift)
     __shared__ uint32_t s_incl[ROW];
-    __shared__ uint32_t s_x0[ROW], s_y0[ROW], s_w[ROW], s_depth[ROW], s_live[ROW], s_cx[ROW];
+    __shared__ uint32_t s_x0[ROW], s_y0[ROW], s_w[ROW], s_depth[ROW], s_live[ROW];
+    __shared__ uint32_t s_cx[EXACT ? ROW : 1];
     __shared__ uint32_t wsum[DUP_T / 64], s_tmax[DUP_T / 64], s_cws[DUP_T / 64];
     __shared__ uint32_t s_cred[2][DUP_T / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -700,7 +719,7 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
         t[g] = (i0 + g < P) ? geo.tiles[i0 + g] : 0u;
         r[g] = (i0 + g < P) ? geo.bin[i0 + g] : make_uint4(0u, 0u, 0u, 0u);  // (rect lo, rect hi, depth bits, tiles)
     }
-    uint32_t base, ctail = 0;
+    uint32_t base, ctail = 0, ltot = 0xFFFFFFFFu;  // ltot: L, the lists' total (padding tail)
     if (LDS_HIST) {
         // The scans of scan_counts_body, redone by every workgroup (the inputs are
         // a few KB, L2-resident): this workgroup's instance base from the raw
@@ -726,12 +745,15 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
         for (uint32_t k = tid; k < nb; k += 2 * DUP_T) {
             const uint32_t k2 = k + DUP_T;
             const uint32_t v = geo.wgsum[k], v2 = k2 < nb ? geo.wgsum[k2] : 0u;
-            const uint32_t c = cam.cull ? geo.wgcull[k] : 0u, c2 = (cam.cull && k2 < nb) ? geo.wgcull[k2] : 0u;
+            // (EXACT: preprocess wrote wgcull; loaded unconditionally, with the workgroup sums)
+            const uint32_t c = (TAIL && EXACT) ? geo.wgcull[k] : 0u, c2 = (TAIL && EXACT && k2 < nb) ? geo.wgcull[k2] : 0u;
             viol |= (v | v2) >> 31;
             all += (v & 0x7fffffffu) + (v2 & 0x7fffffffu);
             pre += (k < b ? (v & 0x7fffffffu) : 0u) + (k2 < b ? (v2 & 0x7fffffffu) : 0u);
-            call += c + c2;
-            cpre += (k < b ? c : 0u) + (k2 < b ? c2 : 0u);
+            if (TAIL && EXACT) {
+                call += c + c2;
+                cpre += (k < b ? c : 0u) + (k2 < b ? c2 : 0u);
+            }
         }
         uint32_t csum = 0;
         if (in_regs) {
@@ -753,7 +775,7 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
         all = wave_sum_u32(all);
         viol = wave_max_u32(viol);
         vmax = wave_max_u32(vmax);
-        if (cam.cull) {
+        if (TAIL && EXACT && cam.cull) {
             cpre = wave_sum_u32(cpre);
             call = wave_sum_u32(call);
         }
@@ -762,12 +784,14 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
             s_red[1][w] = all;
             s_red[2][w] = viol;
             s_red[3][w] = vmax;
-            s_cred[0][w] = cpre;
-            s_cred[1][w] = call;
+            if (TAIL && EXACT) {
+                s_cred[0][w] = cpre;
+                s_cred[1][w] = call;
+            }
         }
         if (lane == 63) s_red[4][w] = cincl;
         __syncthreads();
-        uint32_t woff = 0;
+        uint32_t woff = 0, lsum = 0;
         pre = all = viol = vmax = cpre = call = 0;
 #pragma unroll
         for (int k = 0; k < DUP_T / 64; k++) {
@@ -776,10 +800,14 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
             viol |= s_red[2][k];
             vmax = max(vmax, s_red[3][k]);
             woff += k < w ? s_red[4][k] : 0u;
-            cpre += s_cred[0][k];
-            call += s_cred[1][k];
+            if (TAIL && !EXACT) lsum += s_red[4][k];
+            if (TAIL && EXACT) {
+                cpre += s_cred[0][k];
+                call += s_cred[1][k];
+            }
         }
-        ctail = all - call + cpre;  // this workgroup's first culled instance in point_list
+        if (TAIL && EXACT) ctail = all - call + cpre;  // this workgroup's first culled instance in point_list
+        if (TAIL && !EXACT) ltot = lsum;
         uint32_t run = woff + cincl - csum;  // bucket start of this thread's first tile
         if (in_regs) {
 #pragma unroll
@@ -824,7 +852,8 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
     } else {
         if (guard.overflow()) return;
         base = geo.blocksums[blockIdx.x];
-        if (cam.cull) {  // (the global-atomic path, > MAX_LDS_TILES tiles) the culled totals' prefix, here
+        if (TAIL && !EXACT && ntiles > 0) ltot = ranges[ntiles - 1].y;  // (the scan launch wrote the ranges)
+        if (TAIL && EXACT && cam.cull) {  // (the global-atomic path, > MAX_LDS_TILES tiles) the culled totals' prefix
             const uint32_t b = blockIdx.x, nb = gridDim.x;
             uint32_t cpre = 0, call = 0;
             for (uint32_t k = tid; k < nb; k += DUP_T) {
@@ -853,7 +882,7 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
     for (int g = 0; g < DUP_G; g++) {
         tsum += t[g];
         tmax = max(tmax, t[g]);
-        cg[g] = (cam.cull && t[g]) ? culled_below(r[g].w, t[g]) : 0u;
+        cg[g] = (TAIL && EXACT && cam.cull && t[g]) ? culled_below(r[g].w, t[g]) : 0u;
         csum += cg[g];
         const int q = DUP_G * tid + g;
         if (t[g]) {
@@ -865,28 +894,33 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
         }
     }
     uint32_t incl = wave_incl_scan(tsum);
-    const uint32_t cincl = cam.cull ? wave_incl_scan(csum) : 0u;
+    const uint32_t cincl = (TAIL && EXACT && cam.cull) ? wave_incl_scan(csum) : 0u;
     tmax = wave_max_u32(tmax);
     __syncthreads();  // (wsum is also tile_plan's scratch)
     if (lane == 63) {
         wsum[w] = incl;
-        s_cws[w] = cincl;
+        if (TAIL && EXACT) s_cws[w] = cincl;
     }
     if (lane == 0) s_tmax[w] = tmax;
     __syncthreads();
     uint32_t run = incl - tsum, crun = ctail + cincl - csum;
     for (int k = 0; k < w; k++) {
         run += wsum[k];
-        crun += s_cws[k];
+        if (TAIL && EXACT) crun += s_cws[k];
     }
 #pragma unroll
     for (int k = 0; k < DUP_T / 64; k++) tmax = max(tmax, s_tmax[k]);
+    uint32_t cx[DUP_G];  // (EXACT) the Gaussians' first slots in point_list's culled tail
 #pragma unroll
     for (int g = 0; g < DUP_G; g++) {  // Gaussian order: the workgroup-local instance offsets of preprocess
-        if (i0 + g < P) geo.offsets[i0 + g] = base + run;
+        const uint32_t off = base + run;
+        if (i0 + g < P) geo.offsets[i0 + g] = off;
+        if (TAIL && !EXACT && off + t[g] > ltot)  // padding tail: the owner of each rect slot >= L
+            for (uint32_t u = max(off, ltot); u < off + t[g]; u++) point_list[u] = (uint64_t)(i0 + g);
         run += t[g];
         s_incl[DUP_G * tid + g] = run;
-        s_cx[DUP_G * tid + g] = crun;  // the Gaussian's first slot in point_list's culled tail
+        cx[g] = crun;
+        if (TAIL && EXACT) s_cx[DUP_G * tid + g] = crun;  // (read by the load-balanced path)
         crun += cg[g];
     }
     if (tmax <= (uint32_t)GSR_DUP_LOOP_MAX) {
@@ -899,10 +933,10 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
         for (int g = 0; g < DUP_G; g++) {
             const uint32_t x0 = r[g].x & 0xFFFFu, y0 = r[g].x >> 16, wdt = (r[g].y & 0xFFFFu) - x0;
             const uint32_t gi = (uint32_t)(i0 + g);
-            uint32_t ct = s_cx[DUP_G * tid + g];
+            uint32_t ct = cx[g];
             for (uint32_t k = 0; k < t[g]; k++) {
-                if (!tile_live(r[g].w, k)) {  // culled (Camera::cull): not in the bucket, in the tail
-                    point_list[ct++] = (uint64_t)gi;
+                if (!tile_live(r[g].w, k)) {  // culled (Camera::cull): not in the bucket (EXACT: in the tail)
+                    if (TAIL && EXACT) point_list[ct++] = (uint64_t)gi;
                     continue;
                 }
                 const uint32_t tile = (y0 + k / wdt) * (uint32_t)cam.gx + x0 + k % wdt;
@@ -922,8 +956,9 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
             if (s_incl[mid] > e) hi = mid; else lo = mid + 1;
         }
         const uint32_t local = e - ((lo == 0) ? 0u : s_incl[lo - 1]);
-        if (!tile_live(s_live[lo], local)) {  // culled (Camera::cull): in point_list's tail
-            point_list[s_cx[lo] + culled_below(s_live[lo], local)] = (uint64_t)(blockIdx.x * ROW + lo);
+        if (!tile_live(s_live[lo], local)) {  // culled (Camera::cull): not in the bucket (EXACT: in the tail)
+            if (TAIL && EXACT)
+                point_list[s_cx[lo] + culled_below(s_live[lo], local)] = (uint64_t)(blockIdx.x * ROW + lo);
             continue;
         }
         const uint32_t wdt = s_w[lo];
@@ -934,17 +969,26 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
         keys[pos] = ((uint64_t)s_depth[lo] << 32) | (uint64_t)gi;
     }
 }
-template <bool LDS_HIST, int DUP_G>
-__global__ void __launch_bounds__(DUP_T)
+// EXACT instantiations: at most 80 VGPRs (6 waves per SIMD), three 512-lane workgroups per CU, so config 3's 586
+// count-matrix rows run in one dispatch round on 256 CUs (that bookkeeping took the kernel to 88 VGPRs: two
+// workgroups per CU, a second round, 10.8 -> 14.5 us); the padding ones stay at 72-79 VGPRs by themselves
+template <bool LDS_HIST, int DUP_G, bool CLK, bool EXACT>
+__global__ void __launch_bounds__(DUP_T) __attribute__((amdgpu_waves_per_eu(6, 8)))
 duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges, const uint32_t* __restrict__ tot,
                         uint32_t* __restrict__ cursor, int ntiles, uint64_t* __restrict__ keys,
                         uint64_t* __restrict__ point_list, SpecGuard guard, uint32_t sort_cap,
                         uint32_t* __restrict__ status, unsigned long long* clk) {
     extern __shared__ uint32_t s_cur[];
-    kclock_begin(clk);
-    duplicate_bucket_body<LDS_HIST, DUP_G>(cam, P, geo, ranges, tot, cursor, ntiles, keys, point_list, guard, sort_cap,
-                                           status, s_cur);
-    kclock_end(clk);
+    if constexpr (CLK) kclock_begin(clk);
+    duplicate_bucket_body<LDS_HIST, DUP_G, EXACT>(cam, P, geo, ranges, tot, cursor, ntiles, keys, point_list, guard,
+                                                  sort_cap, status, s_cur);
+    if constexpr (CLK) kclock_end(clk);
+}
+
+template <bool CLK, bool EXACT>
+static auto duplicate_bucket_variant(bool lds_hist, bool g2) {
+    return lds_hist ? (g2 ? duplicate_bucket_kernel<true, 2, CLK, EXACT> : duplicate_bucket_kernel<true, 1, CLK, EXACT>)
+                    : (g2 ? duplicate_bucket_kernel<false, 2, CLK, EXACT> : duplicate_bucket_kernel<false, 1, CLK, EXACT>);
 }
 
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2* ranges, const uint32_t* tot,
@@ -952,8 +996,11 @@ hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2
                                    int nb, SpecGuard guard, uint32_t* status, hipStream_t s, unsigned long long* clk) {
     if (nb == 0) return hipSuccess;
     const bool g2 = cam.pre_shift == 10;  // rows of 1024: two Gaussians per lane; of 512: one
-    auto k = lds_hist ? (g2 ? duplicate_bucket_kernel<true, 2> : duplicate_bucket_kernel<true, 1>)
-                      : (g2 ? duplicate_bucket_kernel<false, 2> : duplicate_bucket_kernel<false, 1>);
+    const bool exact = cam.tail_exact != 0;
+    auto k = clk ? (exact ? duplicate_bucket_variant<true, true>(lds_hist, g2)
+                          : duplicate_bucket_variant<true, false>(lds_hist, g2))
+                 : (exact ? duplicate_bucket_variant<false, true>(lds_hist, g2)
+                          : duplicate_bucket_variant<false, false>(lds_hist, g2));
     hipLaunchKernelGGL(k, dim3(nb), dim3(DUP_T), lds_hist ? sizeof(uint32_t) * ntiles : 0, s, cam, P, geo, ranges,
                        tot, cursor, ntiles, keys, point_list, guard, (uint32_t)TILE_SORT_CAP, status, clk);
     return hipGetLastError();

@@ -238,7 +238,9 @@ def test_point_list_holds_num_rendered_valid_ids(cuda, case):
 
 
 def test_point_list_valid_in_static_mode(cuda):
-    """The static (capacity) forward: the first status[0] = num_rendered entries are valid ids, culled or not."""
+    """The static (capacity) forward: the first status[0] = num_rendered entries are valid ids, culled or not:
+    the tile lists, then (culled) padding entries -- the owners of the last rect instance slots -- with empty
+    block masks (include/gsr.h: the exact culled instances are written by the dynamic forward only)."""
     from splatam_amd import _C
     from splatam_amd.layout import views
     scene = make_scene(20000, 320, 240, seed=3)
@@ -258,9 +260,11 @@ def test_point_list_valid_in_static_mode(cuda):
         v = views(out[5], out[4], c.W, c.H, n)
         ids = v["point_list"][:n].long()
         assert int(ids.min()) >= 0 and int(ids.max()) < scene.P
-        counts = torch.bincount(ids, minlength=scene.P)
-        # tiles_touched per Gaussian: the rect of its radius (radii > 0 <=> listed at least once)
-        assert torch.equal(counts > 0, out[2] > 0)
+        rng = v["ranges"].long()
+        L = int((rng[:, 1] - rng[:, 0]).clamp(min=0).sum())
+        assert (L == n) if mode == 2 else (L < n)
+        assert not bool((v["block_masks"][L:n] & 0xFFFF).any())
+        assert bool((out[2][ids] > 0).all())  # every listed or padding id has a rect (radius > 0)
 
 
 def test_binning_mode_is_per_call_across_threads(cuda):

@@ -39,7 +39,7 @@
 TAG=${1:-x}; shift
 ROOT=$(pwd); OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
-LIGHT="--cpu-baseline off --dropin off --fisher off --mapping off --configs off --unfused-leg off"
+LIGHT="--cpu-baseline off --dropin off --fisher off --mapping off --configs off --unfused-leg off --stage-breakdown off"
 lib_of() { [ "$1" = base ] && echo "$ROOT/splatam_amd/libgsr.so" || echo "$ROOT/splatam_amd/_diag/libgsr_$1.so"; }
 for s in "$@"; do
   case $s in
@@ -209,6 +209,25 @@ PY
              -- python "$ROOT/bench.py" --steps 200 --warmup 5 --settle-ms 0 $LIGHT > "$OUT/clk.log" 2>&1 ) \
              || { echo "clk failed"; tail -20 "$OUT/clk.log"; exit 1; }
          python tools/drift.py "$OUT/clk" --skip 25 --counters | tee "$OUT/clk.txt" ;;
+    sqlds=*) TAGS=${s#sqlds=}  # LDS bank-conflict census of the fused tracking render per library (duplicated phases)
+         for t in base ${TAGS//,/ }; do
+           d="$OUT/sqlds_$t"
+           ( cd /tmp && export TMPDIR=/tmp && GSR_LIB_AB=1 GSR_LIB=$(lib_of $t) timeout -s KILL 200 rocprofv3 --pmc \
+               SQ_WAVES SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS \
+               --kernel-include-regex "${SQRX:-render_track}" -T -d "$d" -o run --output-format csv \
+               -- python "$ROOT/bench.py" --steps 20 --warmup 5 $LIGHT > "$d.log" 2>&1 ) \
+               || { echo "sqlds $t failed"; tail -20 "$d.log"; exit 1; }
+           python - "$d" $t <<'PY' | tee -a "$OUT/sqlds.txt"
+import csv, glob, sys, collections
+f = glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)[0]
+acc = collections.defaultdict(list)
+for r in csv.DictReader(open(f)):
+    acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+n = max(len(v) for v in acc.values()) // 1
+launches = len(set(r["Dispatch_Id"] for r in csv.DictReader(open(f))))
+print("sqlds", sys.argv[2], "launches", launches, " ".join(f"{k} {sum(v) / max(launches, 1):.4g}" for k, v in sorted(acc.items())))
+PY
+         done ;;
     sqab=*) TAGS=${s#sqab=}  # SQ instruction counts of the fused tracking render per library (VALU census by variants)
          for t in base ${TAGS//,/ }; do
            d="$OUT/sqab_$t"
