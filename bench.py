@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--map-prunable", type=float, default=0.02,
                     help="mapping: fraction of the map's Gaussians given opacities under prune_gaussians' 0.005 "
                          "threshold (removed at the frame's first pruning iteration, as faded Gaussians are)")
+    ap.add_argument("--sequence", choices=("auto", "on", "off"), default="auto",
+                    help="SLAM sequence leg (splatam_amd.sequence) at config 3 (auto: N=1 only)")
+    ap.add_argument("--seq-frames", type=int, default=4, help="sequence: timed frames (after frame 0)")
     ap.add_argument("--fisher-k", type=int, default=16, help="fisher: poses per HIP-graph launch")
     ap.add_argument("--configs", choices=("auto", "on", "off"), default="auto",
                     help="BASELINE configs 1 (forward only) and 2 (fwd+bwd RGB + depth) on the GPU and the CPU "
@@ -335,14 +338,23 @@ def main():
         configs = configs_leg(dev, want_cpu=rank == 0 and args.cpu_baseline != "off")
         stream = hbm_stream_gbs()
         if stream:
-            roofline["peak_measured"] = {"copy_gbs": stream["copy_gbs"], "triad_gbs": stream["triad_gbs"],
-                                         "source": "tools/micro/stream (1 GiB float4 streams, best of 20)"}
+            # not a peak: the rate plain copies reach on this box (the roofline's `peak` stays the 8 TB/s spec)
+            roofline["stream_measured"] = {
+                "copy_gbs": stream["copy_gbs"], "triad_gbs": stream["triad_gbs"],
+                "copy_tile_gbs": stream.get("copy_tile_gbs"), "copy_tile_form": stream.get("copy_tile_form"),
+                "source": "tools/micro/stream (1 GiB float4 arrays, best of 20 launches): grid-stride "
+                          "copy / triad, and block-tile copies with 4-16 loads in flight per thread "
+                          "(plain or nontemporal)"}
     fisher = fisher_leg(args, scene, dev, world=world, rank=rank) if args.fisher == "on" else None
     mapping = None
     if args.mapping == "on" or (args.mapping == "auto" and world == 1):
         mapping = mapping_leg(args, dev)
         if args.dropin == "on":
             mapping["dropin"] = dropin_mapping_leg(args, dev)
+
+    sequence = None
+    if args.sequence == "on" or (args.sequence == "auto" and world == 1):
+        sequence = sequence_leg(args, dev)
 
     # ---- CPU baseline: the float32 C oracle on one frame (rank 0, N=1) ------
     cpu = None
@@ -423,6 +435,7 @@ def main():
             "dropin": dropin,
             "fisher": fisher,
             "mapping": mapping,
+            "sequence": sequence,
             "configs": configs,
             "broadcast": bcast_split,
         }
@@ -886,6 +899,81 @@ def render_bwd_roofline(rb, I_avg, P, W, H, graph: bool):
             "num_rendered_avg": int(I_avg), "launches_timed": int(rb["launches"]),
             "timing": "in-kernel wall_clock64 (first workgroup start to last workgroup end) of every launch in "
                       "the timed HIP-graph replays" if graph else "hipEvents around each launch"}
+
+
+def sequence_leg(args, dev):
+    """SplaTAM's per-frame loop (scripts/splatam.py:697-929) at config 3's scene: --seq-frames frames, each
+    40 tracking iterations (constant-velocity start, best candidate written back), add_new_gaussians and 60
+    mapping iterations over the keyframe window (prune_gaussians at 0 and 20).  `value`: frames/s of
+    SlamSequence (capacity-padded map, one GraphTracker + one GraphMapper for the whole sequence, densification
+    on the device without a host sync); `per_frame`: the same frames with a fresh GraphTracker and GraphMapper
+    per frame (probe + warm-up + capture each, torch.cat densification, compaction after pruning) -- everything
+    a shape-changing map costs, inside the timed region.  Frame 0 (mapping only) and construction untimed."""
+    from splatam_amd.scenes import config_scene
+    from splatam_amd.sequence import PerFrameSlam, SlamSequence
+    from splatam_amd.tracker import probe_num_rendered
+    from splatam_amd.workloads import sequence_workload
+
+    K = max(1, args.seq_frames)
+    scene = config_scene(3)
+    P, W, H = scene.P, scene.cam.W, scene.cam.H
+    params, frames, cam, w2c, intr, (q_gt, t_gt) = sequence_workload(scene, K + 1, dev, prunable=args.map_prunable)
+    P0 = params["means3D"].shape[0]
+    n, _ = probe_num_rendered(params, {"cam": cam, "w2c": w2c, **frames[0]}, 0)
+    capacity, bin_cap = P0 + (K + 1) * W * H, 2 * n + 2_000_000
+    t0 = time.perf_counter()
+    seq = SlamSequence(params, frames, cam, w2c, intr, capacity=capacity, bin_capacity=bin_cap, seed=0)
+    seq.frame(0)
+    seq.check()
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t0
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j, t in enumerate(range(1, K + 1)):
+        ev[j][0].record()
+        seq.track(t)
+        ev[j][1].record()
+        seq.densify(t)
+        ev[j][2].record()
+        seq.map(t)
+        ev[j][3].record()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    seq.check()
+    phases = {name: round(sum(e[i].elapsed_time(e[i + 1]) for e in ev) / K, 3)
+              for i, name in enumerate(("tracking_ms", "densify_ms", "mapping_ms"))}
+    n_live = int(seq.n_live.item())
+    live = int(seq.alive.sum().item())
+    te = float((seq.params["cam_trans"][..., 1:K + 1] - t_gt[..., 1:K + 1]).norm(dim=1).max())
+    # the per-frame form on the same frames and keyframe draws (its own probes; checked runs)
+    ref = PerFrameSlam(params, frames, cam, w2c, intr)
+    ref.frame(0, seq.draws[0])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(1, K + 1):
+        ref.frame(t, seq.draws[t])
+    torch.cuda.synchronize()
+    elapsed_ref = time.perf_counter() - t0
+    dpose = float((seq.params["cam_trans"] - ref.p["cam_trans"]).abs().max())
+    out = {"metric": "SLAM frames/sec (40 tracking + densification + 60 mapping iterations per frame)",
+           "value": round(K / elapsed, 3), "unit": "frames/s", "ms_per_frame": round(1000.0 * elapsed / K, 3),
+           "frames": K, "phases_ms": phases,
+           "per_frame": {"value": round(K / elapsed_ref, 3), "ms_per_frame": round(1000.0 * elapsed_ref / K, 3),
+                         "form": "fresh GraphTracker + GraphMapper per frame (probe, warm-up, capture), torch.cat "
+                                 "densification, compact() after pruning",
+                         "max_pose_diff_m": dpose, "gaussians": int(ref.p["means3D"].shape[0])},
+           "map": {"initial": P0, "appended": n_live - P0, "live": live, "capacity": capacity,
+                   "binning_capacity": bin_cap},
+           "pose_error_m": round(te, 5), "setup_s": round(t_build, 3),
+           "config": {"workload": f"config 3 scene ({P} isotropic Gaussians, {W}x{H}); the map starts without "
+                                  f"the left 20 % of frame 0 (densified), {args.map_prunable:g} of it prunable; "
+                                  "camera 2 cm + 0.3 deg per frame", "gaussians": P, "width": W, "height": H},
+           "data": "synthetic (splatam_amd.workloads.sequence_workload: targets rendered from the full scene "
+                   "along the trajectory, 1 % depth noise)"}
+    del seq, ref
+    torch.cuda.empty_cache()
+    return out
 
 
 def main_mapping(args, world, rank, dev):

@@ -151,6 +151,9 @@ typedef struct gsr_track_xform {
     const float* w2c;          /* [4,4] row-major: depth colours */
     int store_rendervars;      /* 1: write the rendervars (outputs below); 0: do not -- the
                                   backward then recomputes them (gsr_track_backward_dual log_scales) */
+    const uint8_t* alive;      /* (ABI 7) [P] or NULL: alive[i] == 0 culls Gaussian i like one behind the
+                                  camera (radius 0, no instances, zero gradients) -- a capacity-padded map's
+                                  free and pruned slots (splatam_amd.sequence) */
 } gsr_track_xform;
 
 int gsr_track_forward_dual_static_xf(const gsr_settings* settings, const gsr_gaussians* gaussians, float* colors2,

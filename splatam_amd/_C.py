@@ -593,7 +593,7 @@ def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scale
     tracking L1 loss and its gradient images formed in the render epilogue.  Returns (num_rendered=capacity,
     color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth, loss, dL_dim, dL_ddepth_sil).
     xform = (means_world, unnorm_rot, logit_opac, log_scales, scale_cols, cam_q_ptr, cam_t_ptr, q_stride, w2c,
-    store): gsr_track_forward_dual_static_xf -- the tracking transform runs inside preprocess and means3D,
+    store[, alive]): gsr_track_forward_dual_static_xf -- the tracking transform runs inside preprocess and means3D,
     colors2, opacity, scales and rotations are its OUTPUTS (preallocated contiguous float32; written only
     when store is true).  records (with xform; device float32 of lib.gsr_track_records_floats(capacity)):
     gsr_track_forward_backward_dual_static_xf -- the tracking render backward runs in the same launch
@@ -631,10 +631,15 @@ def track_forward_dual_static(settings, means3D, colors, colors2, opacity, scale
             if any(t is None or not t.is_contiguous() or t.dtype != torch.float32 or t.device != device for t in outs):
                 raise RuntimeError("track_forward_dual_static_xf: the rendervar outputs must be contiguous float32 "
                                    "tensors on the device")
-            mw, ur, lo, ls, scols, q_ptr, t_ptr, qs, w2c, store = xform
+            mw, ur, lo, ls, scols, q_ptr, t_ptr, qs, w2c, store = xform[:10]
+            alive = xform[10] if len(xform) > 10 else None
+            if alive is not None and (alive.dtype != torch.uint8 or alive.numel() != P or alive.device != device
+                                      or not alive.is_contiguous()):
+                raise RuntimeError("alive: contiguous uint8 of P entries on the device")
             xf = GsrTrackXform(means_world=mw.data_ptr(), unnorm_rot=ur.data_ptr(), logit_opac=lo.data_ptr(),
                                log_scales=ls.data_ptr(), scale_cols=int(scols), cam_q=q_ptr, cam_t=t_ptr,
-                               q_stride=int(qs), w2c=w2c.data_ptr(), store_rendervars=int(bool(store)))
+                               q_stride=int(qs), w2c=w2c.data_ptr(), store_rendervars=int(bool(store)),
+                               alive=_ptr(alive))
             if records is not None:
                 if (records.device != device or records.dtype != torch.float32 or not records.is_contiguous() or
                         records.numel() < lib.gsr_track_records_floats(int(capacity))):

@@ -47,7 +47,7 @@ class GsrTrackXform(ctypes.Structure):
     """gsr_track_xform (include/gsr_glue.h)."""
     _fields_ = [("means_world", c_void_p), ("unnorm_rot", c_void_p), ("logit_opac", c_void_p),
                 ("log_scales", c_void_p), ("scale_cols", c_int), ("cam_q", c_void_p), ("cam_t", c_void_p),
-                ("q_stride", c_int), ("w2c", c_void_p), ("store_rendervars", c_int)]
+                ("q_stride", c_int), ("w2c", c_void_p), ("store_rendervars", c_int), ("alive", c_void_p)]
 
 
 class GsrPoseTrack(ctypes.Structure):

@@ -847,7 +847,7 @@ static int track_forward_xf(const gsr_settings* settings, const gsr_gaussians* g
     xf.store = x.store_rendervars != 0;
     const TrackL1 l1{gt_im, gt_depth, sil_thres, w_im, w_depth, dL_dloss, dL_dim, dL_ddepth_sil, scratch, loss};
     return forward_impl(settings, gaussians, colors2, out_color, out_color2, out_depth, radii, alloc, alloc_ctx,
-                        stream, capacity, status, &l1, &xf, inst_records);
+                        stream, capacity, status, &l1, &xf, inst_records, x.alive);
 }
 
 int gsr_track_backward_scratch_floats(int P) { return pose_fuse_scratch_floats(P < 1 ? 1 : P); }

@@ -498,7 +498,7 @@ class _TrackIteration(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, cam_rots, cam_trans, params, curr, t, cfg, pose_adam, capacity, status, means2D, seed,
-                images=True):
+                images=True, alive=None):
         from . import _C
         cam = curr["cam"]
         cam_rots, cam_trans = _f32c(cam_rots, "cam_unnorm_rots"), _f32c(cam_trans, "cam_trans")
@@ -517,13 +517,16 @@ class _TrackIteration(torch.autograd.Function):
         gt_im, gt_d = _f32c(curr["im"], "gt_im"), _f32c(curr["depth"], "gt_depth")
         H, W = cam.image_height, cam.image_width
         ctx.pre = None
+        if alive is not None and not (seed is not None and capacity > 0 and _XF_FUSED):
+            raise RuntimeError("tracking_iteration: an alive mask needs the static, transform-fused form "
+                               "(capacity > 0, a static seed)")
         if seed is not None and capacity > 0 and _XF_FUSED:
             # static mode, static seed: the transform inside preprocess (gsr_track_forward_dual_static_xf),
             # loss + gradient images in the render epilogue
             seed = _f32c(seed, "seed")
             scratch = _scratch(mw, lib.gsr_track_forward_scratch_floats(W, H))
             xform = (mw, ur, lo, ls, scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c,
-                     _XF_STORE)
+                     _XF_STORE, alive)
             records = None
             if _RENDER_FUSED:  # (a static seed promises the backward): the render backward in the forward's launch
                 records = torch.empty(lib.gsr_track_records_floats(capacity), **f32)
@@ -601,7 +604,7 @@ class _TrackIteration(torch.autograd.Function):
         (cam_rots, cam_trans, mw, ur, means, rot, dcol, scales, rgb, radii, geom, binning, img, im, ds, gt_im, gt_d,
          w2c) = ctx.saved_tensors
         t, T, scols, n, cam, cfg = ctx.meta
-        nones = (None,) * 12
+        nones = (None,) * 13
         records = getattr(ctx, "records", None)
         if ctx.pre is not None and g is not None and g.data_ptr() == ctx.pre[2].data_ptr():
             dim, dds = ctx.pre[0], ctx.pre[1]
@@ -637,19 +640,20 @@ class _TrackIteration(torch.autograd.Function):
                                scols, cam_rots.data_ptr() + 4 * t, cam_trans.data_ptr() + 4 * t, T, w2c, scratch,
                                dq_ptr=dq.data_ptr() + 4 * t, dt_ptr=dt.data_ptr() + 4 * t, log_scales=ctx.log_scales,
                                records=records)
-        return (dq, dt) + (None,) * 10
+        return (dq, dt) + (None,) * 11
 
 
 def tracking_iteration(params: dict, curr: dict, time_idx: int, cfg, pose_adam: PoseAdam | None = None,
-                       capacity: int = 0, status=None, seed=None, images: bool = True):
+                       capacity: int = 0, status=None, seed=None, images: bool = True, alive=None):
     """get_loss(tracking=True) as one fused forward (transform, dual rasterization, masked L1) whose backward
     runs the render backward and the per-Gaussian backward with the pose chain (+ pose Adam) fused in:
     no per-Gaussian gradient array, no separate pose-reduction launch.  Returns (loss, radii).
     images=False: with the render backward fused into the forward's launch (static mode and seed), the
     rendered images are not stored at all (get_loss reads them only for the loss, formed in the same launch);
-    the backward must then be taken from `seed`."""
+    the backward must then be taken from `seed`.  alive (uint8 [P], static form only): the Gaussians with
+    alive[i] == 0 are culled (a capacity-padded map's free and pruned slots)."""
     return _TrackIteration.apply(params["cam_unnorm_rots"], params["cam_trans"], params, curr, int(time_idx), cfg,
-                                 pose_adam, int(capacity), status, None, seed, bool(images))
+                                 pose_adam, int(capacity), status, None, seed, bool(images), alive)
 
 
 class _DualRenderL1(torch.autograd.Function):

@@ -73,7 +73,7 @@ def probe_num_rendered(params, curr_data, time_idx) -> tuple[int, int]:
 class GraphMapper:
     def __init__(self, params: dict, keyframes: list, iters_per_graph: int = 60, cfg: MappingConfig = MappingConfig(),
                  headroom: float = 1.5, min_extra: int = 65536, seed: int | None = None, timing: bool = False,
-                 prune: bool | None = None, scene_radius=None):
+                 prune: bool | None = None, scene_radius=None, alive=None, capacity: int | None = None):
         if not keyframes:
             raise RuntimeError("GraphMapper needs at least one keyframe")
         for kf in keyframes:
@@ -88,11 +88,20 @@ class GraphMapper:
         dev = params["means3D"].device
         self._setup_pruning(cfg if prune is None else None, bool(prune), scene_radius, int(iters_per_graph),
                             params["means3D"].shape[0], dev)
-        probes = [probe_num_rendered(params, kf, kf["id"]) for kf in keyframes]
-        longest = max(p[1] for p in probes)
-        if longest > TILE_SORT_CAP:
-            raise RuntimeError(f"a tile list of {longest} > {TILE_SORT_CAP}: use the eager (synchronous) path")
-        self.capacity = max(1, int(headroom * max(p[0] for p in probes)) + int(min_extra))
+        # alive: an external uint8 [P] mask (a capacity-padded map's live slots, splatam_amd.sequence): every
+        # forward culls the cleared slots and the in-frame pruning clears more
+        self.external_alive = alive is not None
+        if alive is not None:
+            if alive.dtype != torch.uint8 or alive.numel() != params["means3D"].shape[0] or alive.device != dev:
+                raise RuntimeError("alive: uint8 [P] on the parameters' device")
+            self.alive = alive
+        if capacity is None:
+            probes = [probe_num_rendered(params, kf, kf["id"]) for kf in keyframes]
+            longest = max(p[1] for p in probes)
+            if longest > TILE_SORT_CAP:
+                raise RuntimeError(f"a tile list of {longest} > {TILE_SORT_CAP}: use the eager (synchronous) path")
+            capacity = max(1, int(headroom * max(p[0] for p in probes)) + int(min_extra))
+        self.capacity = int(capacity)
         self.iters = int(iters_per_graph)
         self.rng = np.random if seed is None else np.random.RandomState(seed)
         kf0 = keyframes[0]
@@ -112,6 +121,7 @@ class GraphMapper:
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         snapshot = {k: params[k].detach().clone() for k in GAUSS_KEYS + (key,)}
+        alive0 = self.alive.clone()
         with torch.cuda.stream(side):  # warm-up iterations outside the capture, then the state is restored
             for k in range(min(2, self.iters)):
                 self._iteration(k)
@@ -119,7 +129,7 @@ class GraphMapper:
                 for k, v in snapshot.items():
                     params[k].copy_(v)
             self.status.zero_()
-            self.alive.fill_(1)
+            self.alive.copy_(alive0)
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         del snapshot
@@ -204,7 +214,7 @@ class GraphMapper:
             kf = self.keyframes[self.sequence[k]]
             params, t = self.params, kf["id"]
         self.adam.status = self.status[k]  # this iteration's forward guards its Adam step
-        alive = self.alive if self.prune_at else None
+        alive = self.alive if (self.prune_at or self.external_alive) else None
         loss, _, _ = _get_loss_mapping_fused(params, kf, t, self.cfg, adam=self.adam, capacity=self.capacity,
                                              status=self.status[k], means2D=self.means2D, alive=alive)
         if k in self.prune_at:
@@ -216,6 +226,22 @@ class GraphMapper:
             return loss.detach()
         torch.autograd.backward(loss, self.seed)
         return loss.detach()
+
+    def set_keyframes(self, keyframes: list):
+        """A new keyframe window for the next replays (SplaTAM selects one per mapped frame, scripts/splatam.py:
+        820-836): the captured iterations read per-iteration slots that run() fills from this window, so the
+        graph is not re-captured.  Needs the redraw form; the keyframes must share the camera settings object,
+        the w2c and the image size of the ones the mapper was built with."""
+        if not self.redraw:
+            raise RuntimeError("set_keyframes needs the redraw form (keyframes sharing cam / w2c / image size)")
+        kf0 = self._slot_kfs[0]
+        for kf in keyframes:
+            if kf["cam"] is not kf0["cam"] or kf["w2c"] is not kf0["w2c"] or kf["im"].shape != self._slot_im.shape[1:]:
+                raise RuntimeError("set_keyframes: every keyframe must share the mapper's camera, w2c and image size")
+        self.keyframes = list(keyframes)
+        self._kf_im = torch.stack([kf["im"] for kf in keyframes]).contiguous()
+        self._kf_depth = torch.stack([kf["depth"] for kf in keyframes]).contiguous()
+        self._kf_ids = [int(kf["id"]) for kf in keyframes]
 
     def survivors(self) -> torch.Tensor:
         """Boolean [P] mask of the Gaussians every replay so far kept (the mask persists across replays)."""

@@ -60,16 +60,23 @@ class GraphTracker:
     def __init__(self, params: dict, curr_data: dict, time_idx: int, iters_per_graph: int = 20,
                  cfg: TrackingConfig = TrackingConfig(), lrs=(0.0004, 0.002), headroom: float = 1.5,
                  warmup_iters: int = 3, min_extra: int = 65536, timing: bool = False, fuse_pose: bool = False,
-                 prime: bool = False, prime_ms: float = 0.0, clock_stages=None):
+                 prime: bool = False, prime_ms: float = 0.0, clock_stages=None, alive=None,
+                 capacity: int | None = None):
         if not fused_eligible(params, curr_data, cfg):
             raise RuntimeError("GraphTracker needs the fused tracking configuration (only the pose requires grad)")
         self.params, self.curr, self.t, self.cfg = params, curr_data, time_idx, cfg
         self.fuse_pose = fuse_pose  # pose chain + Adam inside the rasterizer's per-Gaussian backward
+        # alive: uint8 [P] mask of a capacity-padded map (splatam_amd.sequence), read by every replay
+        if alive is not None and not fuse_pose:
+            raise RuntimeError("GraphTracker: an alive mask needs fuse_pose=True")
+        self.alive = alive
         dev = params["means3D"].device
-        n, longest = probe_num_rendered(params, curr_data, time_idx)
-        if longest > TILE_SORT_CAP:
-            raise RuntimeError(f"a tile list of {longest} > {TILE_SORT_CAP}: use the eager (synchronous) path")
-        self.capacity = max(1, int(headroom * n) + int(min_extra))
+        if capacity is None:  # (capacity: the binning capacity given, e.g. for a map that grows between frames)
+            n, longest = probe_num_rendered(params, curr_data, time_idx)
+            if longest > TILE_SORT_CAP:
+                raise RuntimeError(f"a tile list of {longest} > {TILE_SORT_CAP}: use the eager (synchronous) path")
+            capacity = max(1, int(headroom * n) + int(min_extra))
+        self.capacity = int(capacity)
         self.iters = int(iters_per_graph)
         self.status = torch.zeros(self.iters, 4, dtype=torch.int32, device=dev)
         rots, trans = params["cam_unnorm_rots"], params["cam_trans"]
@@ -137,7 +144,7 @@ class GraphTracker:
             # backward run in the same launch and the tracker reads neither image)
             loss, _ = tracking_iteration(self.params, self.curr, self.t, self.cfg, pose_adam=self.adam,
                                          capacity=self.capacity, status=self.status[k], seed=self.seed,
-                                         images=False)
+                                         images=False, alive=self.alive)
             torch.autograd.backward(loss, self.seed)
             return loss.detach()
         loss, _, _ = _get_loss_tracking_fused(self.params, self.curr, self.t, self.cfg, dual=True,

@@ -9,6 +9,8 @@ the GPU parity tests pin (tests/test_gpu_pinned.py) -- the same map, pose pertur
   Gaussians get opacities under prune_gaussians' removal threshold (configs/replica/splatam.py:101-111:
   0.005), so the mapping frame's pruning iterations (0 and 20) remove Gaussians the way a real sequence's
   faded Gaussians are removed.
+* sequence_workload: a synthetic capture (frames along a trajectory, a map with a hole to densify) for the
+  SLAM sequence leg (splatam_amd.sequence).
 """
 from __future__ import annotations
 
@@ -91,3 +93,42 @@ def mapping_workload(scene: Scene, K: int, dev, rank: int = 0, world: int = 1, p
     if prunable > 0:
         make_prunable(params, prunable)
     return params, cam, kfs
+
+
+def sequence_workload(scene: Scene, num_frames: int, dev, hole: float = 0.2, step=(0.02, 0.3),
+                      prunable: float = 0.0):
+    """(params, frames, cam, w2c, intrinsics, gt_poses): a synthetic capture for splatam_amd.sequence.
+
+    The scene (camera frame of frame 0) is the truth; frame t's camera has moved by t * step = (metres along
+    x, degrees about y) and its target image / depth are the truth rendered there (depth with 1 % seeded
+    noise, as mapping_keyframes).  The map SplaTAM starts from is the truth without the Gaussians whose
+    projection in frame 0 falls in the left `hole` fraction of the image (the part the first frames must add
+    by densification) and with pose columns t > 0 left at init_tracking_params' perturbed values (the
+    sequence overwrites them from the constant-velocity model); `prunable` as make_prunable."""
+    truth = init_tracking_params(scene, num_frames=max(1, num_frames), device=dev)
+    cam = camera_settings(scene.cam, dev)
+    w2c = torch.eye(4, device=dev)
+    gt = dict(truth)
+    q = torch.zeros(1, 4, num_frames, device=dev)
+    tr = torch.zeros(1, 3, num_frames, device=dev)
+    for t in range(num_frames):
+        a = torch.deg2rad(torch.tensor(step[1] * t, dtype=torch.float64))
+        q[0, 0, t], q[0, 2, t] = float(torch.cos(a / 2)), float(torch.sin(a / 2))
+        tr[0, 0, t] = step[0] * t
+    gt["cam_unnorm_rots"], gt["cam_trans"] = q, tr
+    g = torch.Generator().manual_seed(99)
+    frames = []
+    for t in range(num_frames):
+        im, depth = render_targets(truth, cam, w2c, t, perturb=gt)
+        depth = depth * (1.0 + 0.01 * torch.randn(depth.shape, generator=g).to(dev))
+        frames.append({"im": im.clamp(0, 1).contiguous(), "depth": depth.contiguous()})
+    c = scene.cam
+    u = truth["means3D"][:, 0] / truth["means3D"][:, 2] * c.fx + c.cx
+    keep = u >= hole * c.W
+    params = {k: (v[keep].contiguous() if v.shape[0] == keep.shape[0] and k not in ("cam_unnorm_rots", "cam_trans")
+                  else v.clone()) for k, v in truth.items()}
+    params["cam_unnorm_rots"][..., 0] = q[..., 0]
+    params["cam_trans"][..., 0] = tr[..., 0]
+    if prunable > 0:
+        make_prunable(params, prunable)
+    return params, frames, cam, w2c, (c.fx, c.fy, c.cx, c.cy), (q, tr)

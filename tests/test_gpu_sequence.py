@@ -1,0 +1,75 @@
+"""SLAM sequence on one HIP-graph tracker and one HIP-graph mapper (splatam_amd.sequence) against the
+per-frame loop of fresh GraphTrackers / GraphMappers on an unpadded map that grows by torch.cat
+(add_new_gaussians_literal) -- the form in which P changes every frame, scripts/splatam.py:697-929.
+
+The capacity-padded map keeps dead rows (culled by the alive mask) and appends the densified Gaussians at
+n_live + rank; its live rows, in slot order, are the literal map's rows.  Without pruning both forms run the
+same kernels on the same live Gaussians in the same order, so the poses and the map agree bitwise.  With the
+in-frame pruning the pruned rows stay in place (dead) in the padded map, which moves the later rows' block
+assignment in the pose reduction: the poses agree to float32 rounding, not bitwise."""
+import pytest
+import torch
+
+from splatam_amd.mapper import GAUSS_KEYS
+from splatam_amd.scenes import make_scene
+from splatam_amd.sequence import PerFrameSlam, SlamSequence
+from splatam_amd.workloads import sequence_workload
+
+pytestmark = pytest.mark.gpu
+
+N_FRAMES = 3
+
+
+@pytest.fixture(scope="module")
+def capture(cuda):
+    scene = make_scene(20_000, 320, 240, seed=7)
+    return sequence_workload(scene, N_FRAMES, torch.device(cuda))
+
+
+def _literal(params0, frames, cam, w2c, intr, draws, bin_cap, prune):
+    ref = PerFrameSlam(params0, frames, cam, w2c, intr, prune=prune, bin_capacity=bin_cap)
+    for t in range(N_FRAMES):
+        ref.frame(t, draws[t])
+    torch.cuda.synchronize()
+    return ref.p
+
+
+def _run_sequence(capture, prune):
+    params, frames, cam, w2c, intr, _ = capture
+    from splatam_amd.tracker import probe_num_rendered
+    n, _ = probe_num_rendered(params, {"cam": cam, "w2c": w2c, "im": frames[0]["im"], "depth": frames[0]["depth"]}, 0)
+    bin_cap = 4 * n + 400_000
+    seq = SlamSequence(params, frames, cam, w2c, intr, capacity=params["means3D"].shape[0] + 2 * 320 * 240,
+                       bin_capacity=bin_cap, prune=prune, seed=0)
+    for t in range(N_FRAMES):
+        seq.frame(t)
+    seq.check()
+    torch.cuda.synchronize()
+    return seq, bin_cap
+
+
+@pytest.mark.parametrize("prune", [False, True])
+def test_sequence_equals_per_frame_loop(cuda, capture, prune):
+    params, frames, cam, w2c, intr, (q_gt, t_gt) = capture
+    seq, bin_cap = _run_sequence(capture, prune)
+    ref = _literal(params, frames, cam, w2c, intr, seq.draws, bin_cap, prune)
+    live = seq.live_params()
+    P0, Pn = params["means3D"].shape[0], live["means3D"].shape[0]
+    added = int(seq.n_live.item()) - P0
+    print(f"prune={prune}: P0 {P0}, appended {added}, live {Pn}, literal {ref['means3D'].shape[0]}")
+    assert added > 1000  # the hole was densified
+    assert Pn == ref["means3D"].shape[0]
+    dq = float((seq.params["cam_unnorm_rots"] - ref["cam_unnorm_rots"]).abs().max())
+    dt = float((seq.params["cam_trans"] - ref["cam_trans"]).abs().max())
+    errs = {k: float((live[k] - ref[k]).abs().max()) for k in GAUSS_KEYS + ("rgb_colors",)}
+    print(f"  pose max |d| q {dq:.3e} t {dt:.3e}; map {errs}")
+    # tracking reached the trajectory (1 cm / 0.3 deg per frame)
+    assert float((seq.params["cam_trans"][..., 1:] - t_gt[..., 1:]).abs().max()) < 5e-3
+    if not prune:
+        assert dq == 0.0 and dt == 0.0
+        assert all(e == 0.0 for e in errs.values())
+    else:
+        assert dq <= 1e-5 and dt <= 1e-5
+        # the map: the mapping frames start from the densified Gaussians of slightly different poses
+        for k, e in errs.items():
+            assert e <= 1e-3 * max(1.0, float(ref[k].abs().max())), (k, e)

@@ -22,6 +22,32 @@ __global__ void __launch_bounds__(256) k_copy(const float4* __restrict__ a, floa
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) c[i] = a[i];
 }
+// one-shot block tiles: every thread issues U float4 loads (strided by the block size, so each load
+// instruction covers 1 KiB contiguous per wave... 4 KiB per block) before its U stores; NT: nontemporal
+// loads/stores (streaming data that is never re-read)
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) k_copy_tile(const float4* __restrict__ a4, float4* __restrict__ c4, size_t n) {
+    const f4v* __restrict__ a = reinterpret_cast<const f4v*>(a4);
+    f4v* __restrict__ c = reinterpret_cast<f4v*>(c4);
+    const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+    f4v v[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const size_t i = base + (size_t)j * 256;
+        if (i < n) v[j] = NT ? __builtin_nontemporal_load(a + i) : a[i];
+    }
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+        const size_t i = base + (size_t)j * 256;
+        if (i < n) {
+            if (NT)
+                __builtin_nontemporal_store(v[j], c + i);
+            else
+                c[i] = v[j];
+        }
+    }
+}
 __global__ void __launch_bounds__(256) k_scale(const float4* __restrict__ a, float4* __restrict__ c, float s,
                                                 size_t n) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -93,7 +119,41 @@ int main() {
             }
         }
     }
-    printf("{\"array_bytes\": %zu, \"cus\": %d", bytes, cus);
+    // the block-tile copies (U float4 per thread, plain or nontemporal): the best of them is copy_tile_gbs
+    const char* tnames[6] = {"u4", "u8", "u16", "u4nt", "u8nt", "u16nt"};
+    double tbest[6] = {0, 0, 0, 0, 0, 0};
+    for (int v = 0; v < 6; v++) {
+        const int U = (v % 3 == 0) ? 4 : (v % 3 == 1) ? 8 : 16;
+        const dim3 grid((unsigned)((n + 256 * U - 1) / (256 * U))), block(256);
+        auto launch = [&]() {
+            switch (v) {
+                case 0: hipLaunchKernelGGL((k_copy_tile<4, false>), grid, block, 0, 0, a, c, n); break;
+                case 1: hipLaunchKernelGGL((k_copy_tile<8, false>), grid, block, 0, 0, a, c, n); break;
+                case 2: hipLaunchKernelGGL((k_copy_tile<16, false>), grid, block, 0, 0, a, c, n); break;
+                case 3: hipLaunchKernelGGL((k_copy_tile<4, true>), grid, block, 0, 0, a, c, n); break;
+                case 4: hipLaunchKernelGGL((k_copy_tile<8, true>), grid, block, 0, 0, a, c, n); break;
+                default: hipLaunchKernelGGL((k_copy_tile<16, true>), grid, block, 0, 0, a, c, n); break;
+            }
+        };
+        for (int w = 0; w < 3; w++) launch();
+        CHECK(hipDeviceSynchronize());
+        for (int r = 0; r < 20; r++) {
+            CHECK(hipEventRecord(e0, 0));
+            launch();
+            CHECK(hipEventRecord(e1, 0));
+            CHECK(hipEventSynchronize(e1));
+            float ms = 0.f;
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
+            const double gbs = 2.0 * bytes / (ms * 1e-3) / 1e9;
+            if (gbs > tbest[v]) tbest[v] = gbs;
+        }
+    }
+    int tb = 0;
+    for (int v = 1; v < 6; v++)
+        if (tbest[v] > tbest[tb]) tb = v;
+    printf("{\"array_bytes\": %zu, \"cus\": %d, \"copy_tile_gbs\": %.1f, \"copy_tile_form\": \"%s\"", bytes, cus,
+           tbest[tb], tnames[tb]);
+    for (int v = 0; v < 6; v++) printf(", \"copy_tile_%s_gbs\": %.1f", tnames[v], tbest[v]);
     for (int k = 0; k < 4; k++) printf(", \"%s_gbs\": %.1f, \"%s_grid\": %d", names[k], best[k], names[k], best_grid[k]);
     printf("}\n");
     CHECK(hipFree(a));
