@@ -82,6 +82,9 @@ def parse():
                     help="mapping: iterations per frame = per HIP graph (configs/replica/splatam.py:16: 60)")
     ap.add_argument("--map-prune", type=int, default=1,
                     help="mapping: prune_gaussians inside the frame (configs/replica/splatam.py:101-111), 0: off")
+    ap.add_argument("--map-binning", choices=("culled", "reference"), default="culled",
+                    help="mapping: tile lists without the culled instances (default) or the reference's lists "
+                         "(A/B of the tile cull's effect on the mapping kernels)")
     ap.add_argument("--map-prunable", type=float, default=0.02,
                     help="mapping: fraction of the map's Gaussians given opacities under prune_gaussians' 0.005 "
                          "threshold (removed at the frame's first pruning iteration, as faded Gaussians are)")
@@ -908,7 +911,8 @@ def sequence_leg(args, dev):
     SlamSequence (capacity-padded map, one GraphTracker + one GraphMapper for the whole sequence, densification
     on the device without a host sync); `per_frame`: the same frames with a fresh GraphTracker and GraphMapper
     per frame (probe + warm-up + capture each, torch.cat densification, compaction after pruning) -- everything
-    a shape-changing map costs, inside the timed region.  Frame 0 (mapping only) and construction untimed."""
+    a shape-changing map costs, inside the timed region.  Construction and frames 0 (mapping only) and 1 (the
+    first densification) untimed, for both forms; the timed frames are 2 .. K + 1."""
     from splatam_amd.scenes import config_scene
     from splatam_amd.sequence import PerFrameSlam, SlamSequence
     from splatam_amd.tracker import probe_num_rendered
@@ -917,20 +921,22 @@ def sequence_leg(args, dev):
     K = max(1, args.seq_frames)
     scene = config_scene(3)
     P, W, H = scene.P, scene.cam.W, scene.cam.H
-    params, frames, cam, w2c, intr, (q_gt, t_gt) = sequence_workload(scene, K + 1, dev, prunable=args.map_prunable)
+    params, frames, cam, w2c, intr, (q_gt, t_gt) = sequence_workload(scene, K + 2, dev, prunable=args.map_prunable)
     P0 = params["means3D"].shape[0]
     n, _ = probe_num_rendered(params, {"cam": cam, "w2c": w2c, **frames[0]}, 0)
-    capacity, bin_cap = P0 + (K + 1) * W * H, 2 * n + 2_000_000
+    capacity, bin_cap = P0 + (K + 2) * W * H, 2 * n + 2_000_000
     t0 = time.perf_counter()
     seq = SlamSequence(params, frames, cam, w2c, intr, capacity=capacity, bin_capacity=bin_cap, seed=0)
-    seq.frame(0)
-    seq.check()
     torch.cuda.synchronize()
     t_build = time.perf_counter() - t0
+    W0 = 2  # untimed warm-up frames: 0 (mapping only) and 1 (the first densification: allocator, kernels)
+    for t in range(W0):
+        seq.frame(t)
+    seq.check()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for j, t in enumerate(range(1, K + 1)):
+    for j, t in enumerate(range(W0, W0 + K)):
         ev[j][0].record()
         seq.track(t)
         ev[j][1].record()
@@ -945,13 +951,14 @@ def sequence_leg(args, dev):
               for i, name in enumerate(("tracking_ms", "densify_ms", "mapping_ms"))}
     n_live = int(seq.n_live.item())
     live = int(seq.alive.sum().item())
-    te = float((seq.params["cam_trans"][..., 1:K + 1] - t_gt[..., 1:K + 1]).norm(dim=1).max())
+    te = float((seq.params["cam_trans"][..., 1:W0 + K] - t_gt[..., 1:W0 + K]).norm(dim=1).max())
     # the per-frame form on the same frames and keyframe draws (its own probes; checked runs)
     ref = PerFrameSlam(params, frames, cam, w2c, intr)
-    ref.frame(0, seq.draws[0])
+    for t in range(W0):
+        ref.frame(t, seq.draws[t])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for t in range(1, K + 1):
+    for t in range(W0, W0 + K):
         ref.frame(t, seq.draws[t])
     torch.cuda.synchronize()
     elapsed_ref = time.perf_counter() - t0
@@ -1025,8 +1032,13 @@ def run_mapping(args, world, rank, dev):
     S = max(1, args.map_frame_iters)
     steps = S * max(1, -(-max(1, args.steps) // S))
     scene_radius = torch.max(kfs[0]["depth"]) / 3.0  # initialize_first_timestep (splatam.py:212), ratio 3 (replica)
-    mapper = GraphMapper(params, kfs, iters_per_graph=S, cfg=MappingConfig(), timing=bool(args.timing),
-                         prune=bool(args.map_prune), scene_radius=scene_radius)
+    import contextlib
+    from splatam_amd import _C
+    binning = _C.reference_binning() if getattr(args, "map_binning", "culled") == "reference" else \
+        contextlib.nullcontext()
+    with binning:  # (captured into the graph: every replay bins this way)
+        mapper = GraphMapper(params, kfs, iters_per_graph=S, cfg=MappingConfig(), timing=bool(args.timing),
+                             prune=bool(args.map_prune), scene_radius=scene_radius)
     for _ in range(max(1, -(-args.warmup // S))):  # >= W untimed iterations (whole replays)
         mapper.run()  # checked: raises on an overflow
     torch.cuda.synchronize()
@@ -1069,7 +1081,8 @@ def run_mapping(args, world, rank, dev):
         "config": {"workload": f"config {args.config}: {P} Gaussians, {W}x{H}, SplaTAM mapping iteration "
                                "(SH colour + depth/silhouette render fwd+bwd, L1 + SSIM + depth L1, Adam on "
                                "all Gaussian parameters)", "gaussians": P, "width": W, "height": H,
-                   "keyframes": K, "parallelism": f"frame-sharded x{world}"},
+                   "keyframes": K, "parallelism": f"frame-sharded x{world}",
+                   "binning": getattr(args, "map_binning", "culled")},
         "roofline": roofline,
         "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items() if v["launches"]},
     }

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 7
+#define GSR_ABI_VERSION 8
 
 /* error codes */
 #define GSR_OK 0
@@ -183,6 +183,26 @@ int gsr_forward_reuse(const gsr_settings* settings, const gsr_gaussians* gaussia
                       const void* prev_geom, void* binning_buffer, void* image_buffer, const int* prev_radii,
                       float* out_color, float* out_depth, int* radii,
                       gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
+/* gsr_forward with the geometry reuse decided on the device (SplaTAM's second
+ * Renderer call of an iteration, scripts/splatam.py:255,259): the `npairs`
+ * (<= 8) float arrays a[k] / b[k] of n[k] elements -- this call's and the
+ * previous call's rotations / opacities / scales -- are compared bitwise on the
+ * device, and both forms are enqueued, each launch gated on the result: equal
+ * -> the gsr_forward_reuse form (the previous call's geometry with this call's
+ * colours, its sorted lists; *reused = 1, num_rendered = prev_num_rendered, and
+ * the binning and image buffers the backward must get are prev_binning /
+ * prev_image, whose final_T / n_contrib are rewritten with the same values);
+ * different -> the full gsr_forward (*reused = 0, this call's own buffers).
+ * The host waits once, on the counter copy gsr_forward waits on anyway.  The
+ * caller guarantees what gsr_forward_reuse requires of everything else (same
+ * means3D, camera and settings; colors_precomp, no SH; the previous call's
+ * buffers alive).  Returns num_rendered or a negative error. */
+int gsr_forward_reuse_if_equal(const gsr_settings* settings, const gsr_gaussians* gaussians, int npairs,
+                               const float* const* a, const float* const* b, const long long* n,
+                               int prev_num_rendered, const void* prev_geom, void* prev_binning, void* prev_image,
+                               const int* prev_radii, float* out_color, float* out_depth, int* radii, int* reused,
+                               gsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
 /* Zeroes *flag (device int) and sets it to non-zero when any of the
  * `npairs` (<= 8) float arrays a[k][0..n[k]) and b[k][0..n[k]) differ bitwise.

@@ -167,19 +167,40 @@ def _gaussians(means3D, sh, colors, opacity, scales, rotations, cov3D_precomp, d
 # renders RGB and then the depth/silhouette image of the same Gaussians from the same camera
 # (scripts/splatam.py:255,259), two RasterizeGaussiansCUDA calls whose preprocess, binning and
 # tile sort are identical.  The second call reuses the first call's geometry / binning / image
-# buffers (gsr_forward_reuse) when
+# buffers when
 #   * means3D and the camera tensors are the same storage at the same version, the scalar
 #     settings and P are equal, the colours are precomputed (no SH) and no cov3D is given,
 #   * the first call's buffers and its rotations / opacities / scales are still alive and
 #     unmodified (weak references + tensor versions), and
-#   * this call's rotations / opacities / scales equal the first call's bitwise (one device
-#     comparison, gsr_bitwise_equal, read back with the host sync the reference also makes).
-# Off by default (GSR_GEOM_CACHE=1 enables it): it saves ~60 us of device work per pair of calls, but
-# its comparison read-back is a second host synchronisation per pair, and the unchanged caller is
-# host-bound -- SURVEY 8(d)'s unit took 0.65-0.68 ms with it against 0.48-0.55 ms without on the same
-# box (profiles/r3_unit_ab.txt).
-_GEOM_CACHE = os.environ.get("GSR_GEOM_CACHE", "0") == "1"
-REUSE_STATS = {"hits": 0, "misses": 0}  # eligible calls that did / did not reuse (diagnostics, tests)
+#   * this call's rotations / opacities / scales equal the first call's bitwise -- compared on the
+#     device by gsr_forward_reuse_if_equal, which enqueues the reuse and the full forward each gated on
+#     the comparison, so the host waits once, on the counter copy every dynamic forward waits on.
+# On by default (GSR_GEOM_CACHE=0 or set_geom_cache(False) disables it); the native binding
+# (gsr_torch.cpp) applies the same rules.  (Until ABI 8 the comparison was read back by a second host
+# synchronisation, which made the reuse slower than two full calls: profiles/r3_unit_ab.txt.)
+_GEOM_CACHE = os.environ.get("GSR_GEOM_CACHE", "1") != "0"
+REUSE_STATS = {"hits": 0, "misses": 0}  # eligible calls that did / did not reuse (ctypes path)
+
+
+def set_geom_cache(on: bool):
+    """Geometry reuse on / off for both bindings (tests, A/B runs)."""
+    global _GEOM_CACHE
+    _GEOM_CACHE = bool(on)
+    nat = _native()
+    if nat is not None:
+        nat.set_geom_cache(bool(on))
+
+
+def reuse_stats() -> dict:
+    """Hits / misses of the geometry reuse over both bindings ("content": misses on the device comparison)."""
+    out = dict(REUSE_STATS)
+    nat = _native() if _NATIVE_ON else None
+    if nat is not None:
+        h, m, c = nat.reuse_stats()
+        out["hits"] = out.get("hits", 0) + int(h)
+        out["misses"] = out.get("misses", 0) + int(m)
+        out["content"] = out.get("content", 0) + int(c)
+    return out
 
 
 class _Prev:
@@ -189,7 +210,7 @@ class _Prev:
 
 
 def _try_reuse(key, shared, others, P):
-    """The previous call's state if this call may reuse it (host checks + one device comparison).
+    """The previous call's state if this call may reuse it (the host checks; the device compares the rest).
     key: device, stream and scalar settings; shared: tensors that must be the very same objects
     (means3D, bg, viewmatrix, projmatrix, campos) at the same versions."""
     prev = getattr(_tls, "prev", {}).get(key[0])
@@ -213,29 +234,12 @@ def _try_reuse(key, shared, others, P):
         return _miss("version")  # (radii: copied into this call's, so an in-place edit must miss)
     if any(a is None or a.shape != b.shape for a, b in zip(others, po)):
         return _miss("shape")
-    flag = _flag(key[0])  # (zeroed by gsr_bitwise_equal)
-    arr_a = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in others])
-    arr_b = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in po])
-    arr_n = (ctypes.c_longlong * 3)(*[t.numel() for t in others])
-    _check(lib.gsr_bitwise_equal(3, arr_a, arr_b, arr_n, flag.data_ptr(), key[1]), "bitwise_equal")
-    if int(flag.item()) != 0:
-        return _miss("content")
-    return prev, bufs, radii
+    return prev, bufs, radii, po
 
 
 def _miss(reason):
     REUSE_STATS[reason] = REUSE_STATS.get(reason, 0) + 1
     return None
-
-
-def _flag(device):
-    flags = getattr(_tls, "flags", None)
-    if flags is None:
-        flags = _tls.flags = {}
-    f = flags.get(device)
-    if f is None:
-        f = flags[device] = torch.zeros(1, dtype=torch.int32, device=device)
-    return f
 
 
 def _remember(key, shared, others, bufs, radii, num_rendered):
@@ -263,8 +267,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     capacity > 0 selects gsr_forward_static (no host synchronisation, HIP-graph capturable; `status` is a
     device int32[4] receiving the sticky counters, and num_rendered is the capacity).
     """
-    if (_NATIVE_ON and capacity <= 0 and not _GEOM_CACHE and binning_mode() == BINNING_CULLED and
-            _native() is not None):
+    if (_NATIVE_ON and capacity <= 0 and binning_mode() == BINNING_CULLED and _native() is not None):
         return _native().rasterize_gaussians(
             _t(background), means3D, _t(colors), _t(opacity), _t(scales), _t(rotations), float(scale_modifier),
             _t(cov3D_precomp), _t(viewmatrix), _t(projmatrix), float(tan_fovx), float(tan_fovy), int(image_height),
@@ -300,16 +303,28 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
             key = (device, stream, P, H, W, float(tan_fovx), float(tan_fovy), float(scale_modifier), int(degree),
                    bool(prefiltered))
             hit = _try_reuse(key, shared, others, P)
-            REUSE_STATS["hits" if hit is not None else "misses"] += 1
             if hit is not None:
-                prev, bufs, prev_radii = hit
+                prev, bufs, prev_radii, po = hit
                 _begin(device)
-                n = lib.gsr_forward_reuse(ctypes.byref(s), ctypes.byref(g), int(prev.num_rendered), bufs[0].data_ptr(),
-                                          bufs[1].data_ptr(), bufs[2].data_ptr(), prev_radii.data_ptr(),
-                                          out_color.data_ptr(), out_depth.data_ptr(), radii.data_ptr(), _ALLOC_CB, None,
-                                          stream)
+                arr_a = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in others])
+                arr_b = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in po])
+                arr_n = (ctypes.c_longlong * 3)(*[t.numel() for t in others])
+                reused = ctypes.c_int(0)
+                n = lib.gsr_forward_reuse_if_equal(
+                    ctypes.byref(s), ctypes.byref(g), 3, arr_a, arr_b, arr_n, int(prev.num_rendered),
+                    bufs[0].data_ptr(), bufs[1].data_ptr(), bufs[2].data_ptr(), prev_radii.data_ptr(),
+                    out_color.data_ptr(), out_depth.data_ptr(), radii.data_ptr(), ctypes.byref(reused), _ALLOC_CB,
+                    None, stream)
                 _check(n, "rasterize_gaussians (geometry reuse)")
-                return (int(n), out_color, radii, _tls.buffers[0], bufs[1], bufs[2], out_depth)
+                if reused.value:
+                    REUSE_STATS["hits"] += 1
+                    return (int(n), out_color, radii, _tls.buffers[0], bufs[1], bufs[2], out_depth)
+                _miss("content")  # a full forward ran: this call's own buffers
+                REUSE_STATS["misses"] += 1
+                bufs = _tls.buffers
+                _remember(key, shared, others, (bufs[0], bufs[1], bufs[2]), radii, int(n))
+                return (int(n), out_color, radii, bufs[0], bufs[1], bufs[2], out_depth)
+            REUSE_STATS["misses"] += 1
         _begin(device)
         if capacity > 0:
             if status is None or status.device != device or status.numel() < 4:

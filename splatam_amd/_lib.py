@@ -83,6 +83,10 @@ SIGNATURES = {
     "gsr_forward_reuse": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_int, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ALLOC_FN, c_void_p,
                                   c_void_p]),
+    "gsr_forward_reuse_if_equal": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_int,
+                                           c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ALLOC_FN, c_void_p,
+                                           c_void_p]),
     "gsr_bitwise_equal": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gsr_mark_visible": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gsr_geom_buffer_bytes": (c_size_t, [c_int]),
@@ -183,11 +187,11 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     v = lib.gsr_abi_version()
-    if v != 7:
+    if v != 8:
         # an older revision may differ in the glue structs only (ABI 4: gsr_map_adam without `halted`;
         # ABI 5: no fused tracking render; ABI 6: gsr_settings without `binning`, which such a library does
-        # not read); the rasterizer calls are unchanged
-        if not (ab and v in (4, 5, 6)):
+        # not read; ABI 7: no gsr_forward_reuse_if_equal); the rasterizer calls are unchanged
+        if not (ab and v in (4, 5, 6, 7)):
             raise ImportError("libgsr.so ABI version mismatch")
     return lib
 

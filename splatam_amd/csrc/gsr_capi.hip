@@ -299,6 +299,17 @@ size_t gsr_geom_counters_offset(int P) { return GeomLayout::make(P).counters; }
 size_t gsr_binning_buffer_bytes(int num_rendered, int W, int H) { return BinLayout::make(num_rendered, W, H).total; }
 size_t gsr_image_buffer_bytes(int W, int H) { return ImgLayout::make(W, H).total; }
 
+// gsr_forward_reuse_if_equal's inputs: the device comparison and the previous call's state
+struct ReuseIn {
+    EqualPairs pairs;
+    int prev_num_rendered;
+    const void* prev_geom;
+    void* prev_binning;
+    void* prev_image;
+    const int* prev_radii;
+    int* reused;
+};
+
 // colors2 != NULL: dual render (second colour set composited in the same pass, out_color2)
 // capacity > 0: static mode -- binning buffer of `capacity` instances, no host
 // synchronisation at all (graph-capturable); the device counters are copied to
@@ -307,7 +318,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
                         float* out_color, float* out_color2, float* out_depth, int* radii, gsr_alloc_fn alloc,
                         void* alloc_ctx, void* stream_, int capacity = 0, uint32_t* status = nullptr,
                         const TrackL1* l1 = nullptr, const TrackXf* xf = nullptr, float* track_inst = nullptr,
-                        const uint8_t* alive = nullptr) {
+                        const uint8_t* alive = nullptr, const ReuseIn* reuse = nullptr) {
     int rc = validate(settings, gaussians, true);
     if (track_inst && (!l1 || !colors2 || capacity <= 0))
         return fail(GSR_ERR_INVALID_ARG, "the fused render backward needs the static dual forward with the L1 loss");
@@ -366,6 +377,25 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     // tile culling: a per-call choice (gsr_settings.binning), no process-wide mode
     cam.cull = (GSR_TILE_CULL && settings->binning != GSR_BINNING_REFERENCE) ? 1 : 0;
     cam.tail_exact = capacity <= 0 ? 1 : 0;  // (include/gsr.h: the culled instances, or padding in static mode)
+    // gated geometry reuse (gsr_forward_reuse_if_equal): the device compares this call's geometry with the
+    // previous call's, both forms are enqueued with every launch gated on the result (counters[5]), and the
+    // host learns which one ran from the counter copy it waits on anyway -- no second synchronisation
+    const bool gated = reuse && capacity <= 0 && !colors2 && !track_inst && !l1 && !xf && lds_hist && !force_radix &&
+                       P > 0 && !sh_staged(cam, g);
+    if (reuse && reuse->reused) *reuse->reused = 0;
+    Gate eq_gate;
+    if (gated) {
+        uint32_t* flag = geo.counters + 5;
+        if ((e = zero_async(flag, sizeof(uint32_t), stream)) != hipSuccess ||
+            (e = launch_bitwise_equal(reuse->pairs, (int*)flag, stream)) != hipSuccess)
+            return hip_fail(e, "geometry comparison");
+        cam.gate = Gate{flag, 1u};  // the full forward runs when the geometry differs ...
+        eq_gate = Gate{flag, 0u};   // ... the reuse form when it is equal
+        if ((e = launch_reuse_copy(eq_gate, reuse->prev_geom, geom, GL.counters, reuse->prev_radii, radii, P, stream)) !=
+                hipSuccess ||
+            (e = launch_recolour(P, g.colors, geo, stream, eq_gate)) != hipSuccess)
+            return hip_fail(e, "geometry reuse");
+    }
     // the bucketed duplicate's workgroup 0 writes the render schedule (tile_plan); the other paths
     // render in row-major order
     Camera cplan = cam;
@@ -377,7 +407,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     const bool scan_in_duplicate = lds_hist && !force_radix;
     auto snapshot_counters = [&]() -> int {  // num_rendered & co. to pinned host memory (eager mode)
         if (!pin.p) {
-            if ((e = hipHostMalloc((void**)&pin.p, 16, hipHostMallocDefault)) != hipSuccess)
+            if ((e = hipHostMalloc((void**)&pin.p, 32, hipHostMallocDefault)) != hipSuccess)
                 return hip_fail(e, "hipHostMalloc");
         }
         if (!pin.ev) {  // created on the stream's device (the caller's current device is that device)
@@ -388,7 +418,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
             if (cur != dev) (void)hipSetDevice(cur);
             if (e != hipSuccess) return hip_fail(e, "hipEventCreate");
         }
-        if ((e = hipMemcpyAsync(pin.p, geo.counters, 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+        if ((e = hipMemcpyAsync(pin.p, geo.counters, gated ? 32 : 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
             return hip_fail(e, "copy num_rendered");
         if ((e = hipEventRecord(pin.ev, stream)) != hipSuccess) return hip_fail(e, "record num_rendered");
         return GSR_OK;
@@ -412,7 +442,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
             if (lds_hist) {  // column scan (+ instance / tile scans in the same launch unless scan_in_duplicate)
                 if ((e = launch_tile_colscan(cmat, GL.nb, ntiles, tile_tot, geo, ranges,
                                              capacity > 0 ? status : nullptr, !scan_in_duplicate, stream,
-                                             t.kclock())) != hipSuccess)
+                                             t.kclock(), cam.gate)) != hipSuccess)
                     return hip_fail(e, "tile count scan");
             } else if ((e = launch_scan_counts(geo, GL.nb, tile_count, TILE_CTR_STRIDE, ntiles, ranges,
                                                capacity > 0 ? status : nullptr, stream)) != hipSuccess) {
@@ -493,12 +523,28 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
                 hipSuccess)
                 return hip_fail(e, "render");
         }
+        if (gated) {  // the reuse form's render: the previous call's sorted lists (no sort) and image buffer
+            Camera cr = cam;
+            cr.gate = eq_gate;
+            char* pib = (char*)reuse->prev_image;
+            cr.tile_order = (const uint32_t*)(pib + IL.order);
+            cr.rowmax = (uint32_t*)(pib + IL.rowmax);
+            const SpecGuard rg{geo.counters, (uint32_t)reuse->prev_num_rendered, 0xFFFFFFFFu};
+            if ((e = launch_render_fwd(cr, (const uint2*)(pib + IL.ranges), (uint64_t*)reuse->prev_binning, nullptr,
+                                       geo, nullptr, (float*)(pib + IL.final_T), (uint32_t*)(pib + IL.n_contrib),
+                                       out_color, nullptr, out_depth, rg, stream)) != hipSuccess)
+                return hip_fail(e, "render (geometry reuse)");
+        }
         speculated = true;
     }
     if (capacity > 0) {  // static mode: report, never wait (an overflow shows in status, outputs invalid)
         return (int)cap;
     }
     if ((e = hipEventSynchronize(pin.ev)) != hipSuccess) return hip_fail(e, "sync num_rendered");
+    if (gated && pin.p[5] == 0u) {  // equal geometry: the reuse form ran (num_rendered is the previous call's)
+        *reuse->reused = 1;
+        return reuse->prev_num_rendered;
+    }
     const uint32_t I = pin.p[0];
     const uint32_t longest = pin.p[2];
     if (pin.p[1] != 0)
@@ -1033,6 +1079,36 @@ int gsr_forward_reuse(const gsr_settings* settings, const gsr_gaussians* gaussia
             return hip_fail(e, "render");
     }
     return num_rendered;
+}
+
+int gsr_forward_reuse_if_equal(const gsr_settings* settings, const gsr_gaussians* gaussians, int npairs,
+                               const float* const* a, const float* const* b, const long long* n,
+                               int prev_num_rendered, const void* prev_geom, void* prev_binning, void* prev_image,
+                               const int* prev_radii, float* out_color, float* out_depth, int* radii, int* reused,
+                               gsr_alloc_fn alloc, void* alloc_ctx, void* stream) {
+    if (!gaussians || !gaussians->colors_precomp || (gaussians->shs && gaussians->M > 0) || gaussians->cov3D_precomp)
+        return fail(GSR_ERR_INVALID_ARG, "geometry reuse needs precomputed colours (no SH, no cov3D)");
+    if (npairs < 1 || npairs > 8 || !a || !b || !n || !reused)
+        return fail(GSR_ERR_INVALID_ARG, "gsr_forward_reuse_if_equal: 1..8 pairs and `reused`");
+    if (prev_num_rendered < 0 || !prev_geom || !prev_binning || !prev_image || !prev_radii)
+        return fail(GSR_ERR_INVALID_ARG, "geometry reuse needs the previous call's state");
+    ReuseIn r{};
+    r.pairs.npairs = npairs;
+    for (int k = 0; k < npairs; k++) {
+        if (n[k] < 0 || (n[k] > 0 && (!a[k] || !b[k])))
+            return fail(GSR_ERR_INVALID_ARG, "gsr_forward_reuse_if_equal: pair");
+        r.pairs.a[k] = a[k];
+        r.pairs.b[k] = b[k];
+        r.pairs.n[k] = n[k];
+    }
+    r.prev_num_rendered = prev_num_rendered;
+    r.prev_geom = prev_geom;
+    r.prev_binning = prev_binning;
+    r.prev_image = prev_image;
+    r.prev_radii = prev_radii;
+    r.reused = reused;
+    return forward_impl(settings, gaussians, nullptr, out_color, nullptr, out_depth, radii, alloc, alloc_ctx, stream,
+                        0, nullptr, nullptr, nullptr, nullptr, nullptr, &r);
 }
 
 int gsr_bitwise_equal(int npairs, const float* const* a, const float* const* b, const long long* n, int* flag,

@@ -143,6 +143,14 @@ struct BinLayout {        // per-instance state ("binningBuffer")
 };
 
 // ------------------------------------------------------------ parameters --
+// A launch's device-side switch (the gated geometry reuse of gsr_forward_reuse_if_equal): the kernel runs
+// iff (*p != 0) == run; p == nullptr: always runs.  Read once per workgroup, before anything else.
+struct Gate {
+    const uint32_t* p = nullptr;
+    uint32_t run = 1;
+    __device__ __forceinline__ bool off() const { return p != nullptr && ((*p != 0u) != (run != 0u)); }
+};
+
 struct Camera {
     int W, H;
     float tan_fovx, tan_fovy, focal_x, focal_y;
@@ -174,6 +182,7 @@ struct Camera {
     // point_list's tail [L, num_rendered) of a culled binning: 1 the culled instances themselves (the dynamic
     // forward, whose buffers the caller reads like the reference's), 0 padding ids (static mode)
     int tail_exact = 0;
+    Gate gate;  // (preprocess, duplicate_bucket and render_fwd return at once when it is off)
 };
 // bin[i].w: bit k set = rect tile k (row-major in the rect) has an instance in its bucket; all ones when
 // nothing is culled (or the rect has more than 32 tiles)
@@ -1180,7 +1189,8 @@ __device__ __forceinline__ uint32_t instance_slot(uint2 rect, uint32_t off, uint
 hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, int* radii, uint32_t* counts,
                              bool lds_hist, int ntiles, int nb, hipStream_t s, unsigned long long* clk = nullptr);
 hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, GeomPtrs geo, uint2* ranges,
-                               uint32_t* status, bool tail, hipStream_t s, unsigned long long* clk = nullptr);
+                               uint32_t* status, bool tail, hipStream_t s, unsigned long long* clk = nullptr,
+                               Gate gate = Gate{});
 hipError_t launch_exclusive_scan(uint32_t* data, uint32_t n, uint32_t* total, hipStream_t s);
 hipError_t launch_scan_counts(GeomPtrs geo, int nb, const uint32_t* tile_count, int tile_stride, int ntiles,
                               uint2* ranges, uint32_t* status, hipStream_t s);
@@ -1263,7 +1273,10 @@ hipError_t launch_render_track(const Camera& cam, const uint2* ranges, uint64_t*
                                hipStream_t s, unsigned long long* clk = nullptr);
 int track_records_stride();  // floats per instance record of the tracking render backward (6)
 // geometry reuse (gsr_forward_reuse): the render records' colours replaced by `colors` [P,3]
-hipError_t launch_recolour(int P, const float* colors, GeomPtrs geo, hipStream_t s);
+hipError_t launch_recolour(int P, const float* colors, GeomPtrs geo, hipStream_t s, Gate gate = Gate{});
+// gated geometry reuse: geom [0, counters) + counters[0..3] and the radii from the previous call
+hipError_t launch_reuse_copy(Gate gate, const void* prev_geom, void* geom, size_t geom_bytes, const int* prev_radii,
+                             int* radii, int P, hipStream_t s);
 struct EqualPairs {
     int npairs;
     const float* a[8];

@@ -39,6 +39,7 @@ __global__ void __launch_bounds__(PRE_BLOCK)
 preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __restrict__ counts, int ntiles,
                   unsigned long long* clk) {
 #pragma clang fp contract(off)
+    if (cam.gate.off()) return;
     if constexpr (CLK) kclock_begin(clk);  // (stage clock: first workgroup's start to the last one's end)
     extern __shared__ uint32_t s_hist[];
     __shared__ float s_pose[16];  // XF: the frame's pose (R 9, t 3, F.normalize(q) 4), formed once by wave 0
@@ -351,14 +352,15 @@ template <bool TAIL, int CT, bool CLK>
 __global__ void __launch_bounds__(CS_THREADS)
 tile_colscan_kernel(uint32_t* __restrict__ counts, int nb, int ntiles, uint32_t* __restrict__ tot, GeomPtrs geo,
                     uint2* __restrict__ ranges, uint32_t sort_cap, uint32_t* __restrict__ status,
-                    unsigned long long* clk) {
+                    unsigned long long* clk, Gate gate) {
+    if (gate.off()) return;
     if constexpr (CLK) kclock_begin(clk);
     tile_colscan_body<TAIL, CT>(counts, nb, ntiles, tot, geo, ranges, sort_cap, status);
     if constexpr (CLK) kclock_end(clk);
 }
 
 hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* tot, GeomPtrs geo, uint2* ranges,
-                               uint32_t* status, bool tail, hipStream_t s, unsigned long long* clk) {
+                               uint32_t* status, bool tail, hipStream_t s, unsigned long long* clk, Gate gate) {
     static_assert(CS_THREADS == SCAN_THREADS, "the last colscan workgroup runs the scan body");
     const int ct = nb <= CS_ROWS_SMALL ? 16 : 32;
     auto k = clk ? (tail ? (ct == 16 ? tile_colscan_kernel<true, 16, true> : tile_colscan_kernel<true, 32, true>)
@@ -366,7 +368,7 @@ hipError_t launch_tile_colscan(uint32_t* counts, int nb, int ntiles, uint32_t* t
                  : (tail ? (ct == 16 ? tile_colscan_kernel<true, 16, false> : tile_colscan_kernel<true, 32, false>)
                          : (ct == 16 ? tile_colscan_kernel<false, 16, false> : tile_colscan_kernel<false, 32, false>));
     hipLaunchKernelGGL(k, dim3((ntiles + ct - 1) / ct), dim3(CS_THREADS), 0, s, counts, nb, ntiles, tot, geo, ranges,
-                       (uint32_t)TILE_SORT_CAP, status, clk);
+                       (uint32_t)TILE_SORT_CAP, status, clk, gate);
     return hipGetLastError();
 }
 
@@ -979,6 +981,7 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
                         uint64_t* __restrict__ point_list, SpecGuard guard, uint32_t sort_cap,
                         uint32_t* __restrict__ status, unsigned long long* clk) {
     extern __shared__ uint32_t s_cur[];
+    if (cam.gate.off()) return;
     if constexpr (CLK) kclock_begin(clk);
     duplicate_bucket_body<LDS_HIST, DUP_G, EXACT>(cam, P, geo, ranges, tot, cursor, ntiles, keys, point_list, guard,
                                                   sort_cap, status, s_cur);
@@ -1163,6 +1166,7 @@ render_fwd_kernel(Camera cam, const uint2* __restrict__ ranges, PointEntry* __re
                   float* __restrict__ out_color, float* __restrict__ out_color2, float* __restrict__ out_depth,
                   SpecGuard guard, unsigned long long* clk, TrackL1 l1) {
     static_assert(DUAL || !L1, "the tracking loss needs the depth / silhouette colour set");
+    if (cam.gate.off()) return;
     kclock_begin(clk);
     RenderDiag dg;  // (diagnostics builds only, gsr_diag.h): phases 0 sort, 1 staging, 2 lists, 3 walk, 4 barrier,
     dg.begin();     // 5 epilogue
@@ -1215,16 +1219,38 @@ hipError_t launch_render_fwd(const Camera& cam, const uint2* ranges, uint64_t* p
 // gsr_forward_reuse: the copied render records get this call's colours (preprocess writes the
 // colours only for Gaussians that touch a tile: the same condition here, tiles[i] != 0)
 __global__ void recolour_kernel(int P, const float* __restrict__ colors, float4* __restrict__ rr,
-                                const uint32_t* __restrict__ tiles) {
+                                const uint32_t* __restrict__ tiles, Gate gate) {
+    if (gate.off()) return;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P || tiles[i] == 0u) return;
     float4* q2 = rr + (size_t)RR_F4 * i + 2;
     const float4 old = *q2;
     *q2 = make_float4(colors[3 * i], colors[3 * i + 1], colors[3 * i + 2], old.w);
 }
-hipError_t launch_recolour(int P, const float* colors, GeomPtrs geo, hipStream_t s) {
+hipError_t launch_recolour(int P, const float* colors, GeomPtrs geo, hipStream_t s, Gate gate) {
     if (P <= 0) return hipSuccess;
-    hipLaunchKernelGGL(recolour_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, colors, geo.rr, geo.tiles);
+    hipLaunchKernelGGL(recolour_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, colors, geo.rr, geo.tiles, gate);
+    return hipGetLastError();
+}
+// gsr_forward_reuse_if_equal's copy of the previous call's state (runs only when the gate says "equal"): the
+// geometry buffer up to its counters block plus counters[0..3] (num_rendered, prefiltered flag, longest list,
+// sort cap: counters[4..7] stay this call's -- [5] holds the gate itself) and the radii.  (The image and
+// binning buffers are the previous call's, as in gsr_forward_reuse: the render writes the same final_T /
+// n_contrib into them.)  16-B grid-stride streams (the geometry layout is 256-B aligned).
+__global__ void __launch_bounds__(256) reuse_copy_kernel(Gate gate, const uint4* __restrict__ pg, uint4* __restrict__ g,
+                                                         size_t ng16, const int* __restrict__ prad, int* __restrict__ rad,
+                                                         int P) {
+    if (gate.off()) return;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (size_t k = t0; k <= ng16; k += stride) g[k] = pg[k];  // (k == ng16: counters[0..3])
+    for (size_t k = t0; k < (size_t)P; k += stride) rad[k] = prad[k];
+}
+hipError_t launch_reuse_copy(Gate gate, const void* prev_geom, void* geom, size_t geom_bytes, const int* prev_radii,
+                             int* radii, int P, hipStream_t s) {
+    if (geom_bytes & 15) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(reuse_copy_kernel, dim3(2048), dim3(256), 0, s, gate, (const uint4*)prev_geom, (uint4*)geom,
+                       geom_bytes / 16, prev_radii, radii, P);
     return hipGetLastError();
 }
 // flag |= 1 when a[k][i] != b[k][i] bitwise for any pair k (grid-stride over the pairs' elements)

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -152,6 +153,59 @@ Gauss gaussians(const at::Tensor& means3D, const at::Tensor& sh, const at::Tenso
     return r;
 }
 
+// Geometry reuse across consecutive calls (_C.py's rules, here for the native path): SplaTAM renders RGB and
+// then depth / silhouette of the same Gaussians from the same camera (scripts/splatam.py:255,259).  When the
+// host checks pass -- means3D and the camera tensors the very same objects at the same versions, equal scalar
+// settings, precomputed colours, no SH / cov3D, the previous call's rotations / opacities / scales and buffers
+// alive and unmodified -- the call goes through gsr_forward_reuse_if_equal, which compares this call's
+// rotations / opacities / scales with the previous call's on the device and gates the reuse and the full
+// forward on the result, with the one host wait gsr_forward makes anyway.  GSR_GEOM_CACHE=0 (or
+// set_geom_cache(False)) disables it.
+using WeakT = c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>;
+bool g_geom_cache = [] {
+    const char* v = std::getenv("GSR_GEOM_CACHE");
+    return !(v && std::string(v) == "0");
+}();
+std::array<int64_t, 3> g_reuse_stats{0, 0, 0};  // hits, misses, misses on content (device comparison)
+
+struct Ref {  // a weak reference + the version it had
+    std::optional<WeakT> w;
+    int64_t version = 0;
+    static Ref of(const at::Tensor& t) {
+        Ref r;
+        if (t.defined()) {
+            r.w.emplace(t.getIntrusivePtr());
+            r.version = t._version();
+        }
+        return r;
+    }
+    bool same(const at::Tensor& t) const {  // the same object, unmodified (both undefined: same)
+        if (!t.defined() || !w) return !t.defined() && !w;
+        auto p = w->lock();
+        return p.get() == t.unsafeGetTensorImpl() && t._version() == version;
+    }
+    at::Tensor get() const {  // the referenced tensor at its recorded version, or undefined
+        if (!w) return at::Tensor();
+        auto p = w->lock();
+        if (!p) return at::Tensor();
+        at::Tensor t(std::move(p));
+        return t._version() == version ? t : at::Tensor();
+    }
+};
+struct PrevCall {
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    int64_t P = 0, H = 0, W = 0, degree = 0;
+    double tanfovx = 0, tanfovy = 0, scale_modifier = 0;
+    bool prefiltered = false;
+    std::array<Ref, 5> shared;  // means3D, bg, viewmatrix, projmatrix, campos (the caller's objects)
+    std::array<Ref, 3> others;  // rotations, opacities, scales as passed down
+    std::array<Ref, 3> bufs;    // geom, binning, image
+    Ref radii;
+    int num_rendered = 0;
+};
+thread_local std::vector<PrevCall> g_prev;
+
 // _C.rasterize_gaussians, dynamic mode
 std::tuple<int64_t, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> rasterize_gaussians(
     const at::Tensor& background, const at::Tensor& means3D, const at::Tensor& colors, const at::Tensor& opacity,
@@ -181,11 +235,81 @@ std::tuple<int64_t, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, 
     at::Tensor radii = at::empty({P}, at::TensorOptions().dtype(at::kInt).device(dev));
     Bufs b;
     b.dev = dev;
-    const int n = gsr_forward(&c.s, &g.g, out_color.data_ptr<float>(), out_depth.data_ptr<float>(),
-                              radii.data_ptr<int>(), alloc_cb, &b, st);
-    if (n < 0) raise_rc("rasterize_gaussians");
+    const bool reusable = g_geom_cache && g.g.colors_precomp && g.g.M == 0 && !g.g.cov3D_precomp && g.g.opacities &&
+                          g.g.scales && g.g.rotations;
+    if (!reusable) {
+        const int n = gsr_forward(&c.s, &g.g, out_color.data_ptr<float>(), out_depth.data_ptr<float>(),
+                                  radii.data_ptr<int>(), alloc_cb, &b, st);
+        if (n < 0) raise_rc("rasterize_gaussians");
+        return {(int64_t)n, out_color, radii, b.t[GSR_BUF_GEOM], b.t[GSR_BUF_BINNING], b.t[GSR_BUF_IMAGE], out_depth};
+    }
+    const std::array<const at::Tensor*, 5> shared = {&means3D, &background, &viewmatrix, &projmatrix, &campos};
+    const std::array<at::Tensor, 3> others = {g.keep[5], g.keep[3], g.keep[4]};
+    PrevCall* pc = nullptr;
+    for (auto& e : g_prev)
+        if (e.dev == dev.index()) pc = &e;
+    bool hit = pc && pc->stream == st && pc->P == P && pc->H == H && pc->W == W && pc->degree == degree &&
+               pc->tanfovx == tan_fovx && pc->tanfovy == tan_fovy && pc->scale_modifier == scale_modifier &&
+               pc->prefiltered == prefiltered;
+    for (int k = 0; hit && k < 5; k++) hit = pc->shared[k].same(*shared[k]);
+    std::array<at::Tensor, 3> po, pb;
+    at::Tensor prad;
+    for (int k = 0; hit && k < 3; k++) {
+        po[k] = pc->others[k].get();
+        pb[k] = pc->bufs[k].get();
+        hit = po[k].defined() && pb[k].defined() && po[k].sizes() == others[k].sizes();
+    }
+    if (hit) {
+        prad = pc->radii.get();
+        hit = prad.defined();
+    }
+    int n;
+    if (hit) {
+        const float* pa[3];
+        const float* pbp[3];
+        long long pn[3];
+        for (int k = 0; k < 3; k++) {
+            pa[k] = others[k].data_ptr<float>();
+            pbp[k] = po[k].data_ptr<float>();
+            pn[k] = (long long)others[k].numel();
+        }
+        int reused = 0;
+        n = gsr_forward_reuse_if_equal(&c.s, &g.g, 3, pa, pbp, pn, pc->num_rendered, pb[0].data_ptr(), pb[1].data_ptr(),
+                                       pb[2].data_ptr(), prad.data_ptr<int>(), out_color.data_ptr<float>(),
+                                       out_depth.data_ptr<float>(), radii.data_ptr<int>(), &reused, alloc_cb, &b, st);
+        if (n < 0) raise_rc("rasterize_gaussians (geometry reuse)");
+        if (reused) {  // this call's geometry buffer; the previous call's binning and image buffers
+            g_reuse_stats[0]++;
+            return {(int64_t)n, out_color, radii, b.t[GSR_BUF_GEOM], pb[1], pb[2], out_depth};
+        }
+        g_reuse_stats[1]++;
+        g_reuse_stats[2]++;
+    } else {
+        g_reuse_stats[1]++;
+        n = gsr_forward(&c.s, &g.g, out_color.data_ptr<float>(), out_depth.data_ptr<float>(), radii.data_ptr<int>(),
+                        alloc_cb, &b, st);
+        if (n < 0) raise_rc("rasterize_gaussians");
+    }
+    if (!pc) {
+        g_prev.emplace_back();
+        pc = &g_prev.back();
+    }
+    PrevCall& r = *pc;
+    r.dev = dev.index();
+    r.stream = st;
+    r.P = P, r.H = H, r.W = W, r.degree = degree;
+    r.tanfovx = tan_fovx, r.tanfovy = tan_fovy, r.scale_modifier = scale_modifier;
+    r.prefiltered = prefiltered;
+    for (int k = 0; k < 5; k++) r.shared[k] = Ref::of(*shared[k]);
+    for (int k = 0; k < 3; k++) r.others[k] = Ref::of(others[k]);
+    r.bufs = {Ref::of(b.t[GSR_BUF_GEOM]), Ref::of(b.t[GSR_BUF_BINNING]), Ref::of(b.t[GSR_BUF_IMAGE])};
+    r.radii = Ref::of(radii);
+    r.num_rendered = n;
     return {(int64_t)n, out_color, radii, b.t[GSR_BUF_GEOM], b.t[GSR_BUF_BINNING], b.t[GSR_BUF_IMAGE], out_depth};
 }
+
+void set_geom_cache(bool on) { g_geom_cache = on; }
+std::vector<int64_t> reuse_stats() { return {g_reuse_stats[0], g_reuse_stats[1], g_reuse_stats[2]}; }
 
 // _C.rasterize_gaussians_backward (needs: 8 flags or an empty list = every gradient)
 std::vector<at::Tensor> rasterize_gaussians_backward(
@@ -238,4 +362,6 @@ PYBIND11_MODULE(_gsr_torch, m) {
     m.doc() = "native torch binding of gsr_forward / gsr_backward (the drop-in path's per-iteration calls)";
     m.def("rasterize_gaussians", &rasterize_gaussians);
     m.def("rasterize_gaussians_backward", &rasterize_gaussians_backward);
+    m.def("set_geom_cache", &set_geom_cache);
+    m.def("reuse_stats", &reuse_stats);
 }

@@ -13,7 +13,9 @@ Here the map lives in a capacity-padded buffer: every per-Gaussian tensor has `c
 instances, zero gradients), and `n_live` (device) counts the appended rows.  add_new_gaussians becomes
 `densify_static`: the silhouette render, the masks and the point cloud of every pixel on the device, the new
 rows scattered to n_live + (their rank among the selected pixels) -- no host synchronisation, no reallocation.
-Pruned rows stay dead (append-only; the sequence raises when the capacity is exhausted).  The tracker renders
+After a frame's pruning, compact_static moves the live rows to the front in order (remove_points without
+a reallocation), so the padded map's live rows are always the reference map's rows in its order; the sequence
+raises (check()) when the capacity is exhausted.  The tracker renders
 from a one-column pose slot and slot targets that each frame fills; the mapper draws from a keyframe window
 set per frame (GraphMapper.set_keyframes).  Keyframe selection is the window of the last `window - 1` keyframes
 plus the current frame (keyframe_selection_overlap, :820-836, ranks keyframes by the overlap of a random
@@ -78,8 +80,7 @@ def frame_pointcloud(params: dict, curr: dict, t: int, intrinsics) -> dict:
     """get_pointcloud + initialize_new_params (scripts/splatam.py:73-124,356-381; projective scales, isotropic)
     for EVERY pixel of the frame: the new Gaussian each pixel would add (world-frame mean from the depth and the
     pose of column t, the pixel's colour, log_scale = log(sqrt((z / mean focal)^2)), opacity logit 0, identity
-    rotation).  c2w is the rigid transform's inverse formed by torch.linalg.inv_ex (the reference's
-    torch.inverse, without its host-synchronising error check)."""
+    rotation)."""
     im, depth = curr["im"], curr["depth"]
     H, W = im.shape[1], im.shape[2]
     fx, fy, cx, cy = intrinsics
@@ -89,7 +90,12 @@ def frame_pointcloud(params: dict, curr: dict, t: int, intrinsics) -> dict:
         w2c = torch.eye(4, device=dev, dtype=torch.float32)
         w2c[:3, :3] = build_rotation(rot)
         w2c[:3, 3] = params["cam_trans"][..., t].detach()
-        c2w = torch.linalg.inv_ex(w2c)[0]
+        # c2w: the rigid transform's closed-form inverse [R^T, -R^T t] (the reference's torch.inverse forms the
+        # same matrix by LU; both SplaTAM forms here use this one)
+        c2w = torch.eye(4, device=dev, dtype=torch.float32)
+        rt = w2c[:3, :3].transpose(0, 1)
+        c2w[:3, :3] = rt
+        c2w[:3, 3] = -(rt @ w2c[:3, 3])
         xg, yg = torch.meshgrid(torch.arange(W, device=dev).float(), torch.arange(H, device=dev).float(), indexing="xy")
         xx, yy = ((xg - cx) / fx).reshape(-1), ((yg - cy) / fy).reshape(-1)
         z = depth[0].reshape(-1)
@@ -163,6 +169,26 @@ def densify_static(params: dict, alive: torch.Tensor, n_live: torch.Tensor, over
         total = n_live + incl[-1:]
         overflow.logical_or_(total > capacity)
         n_live.copy_(torch.clamp(total, max=capacity))
+
+
+def compact_static(params: dict, alive: torch.Tensor, n_live: torch.Tensor, capacity: int):
+    """remove_points (utils/slam_external.py:141-163) on a capacity-padded map, without a host
+    synchronisation or a reallocation: the live rows move, in order, to the front (their rank among the live
+    rows; the dead ones to the sink row), alive becomes the prefix [0, count), n_live the count.  The map's
+    rows are then those of the compacted reference map, in the same order, so the next frame's densified
+    rows land where torch.cat puts them."""
+    with torch.no_grad():
+        keep = alive.bool()
+        rank = torch.cumsum(keep.to(torch.int64), 0) - 1
+        dest = torch.where(keep, rank, torch.full_like(rank, capacity))
+        for k, v in params.items():
+            if k in ("cam_unnorm_rots", "cam_trans") or not torch.is_tensor(v) or v.dim() == 0 or \
+                    v.shape[0] != capacity + 1:
+                continue
+            v.data.index_put_((dest,), v.detach().clone())
+        count = rank[-1:] + 1
+        alive.copy_((torch.arange(capacity + 1, device=alive.device) < count).to(torch.uint8))
+        n_live.copy_(count)
 
 
 class SlamSequence:
@@ -241,6 +267,8 @@ class SlamSequence:
         seq = [int(self.rng.randint(0, len(win))) for _ in range(self.mapping_iters)] if sequence is None else sequence
         self.draws.append(seq)
         self.mapper.run(check=False, sequence=seq)
+        if self.mapper.prune_at:  # the frame's pruned Gaussians removed for good (in place, no sync)
+            compact_static(self.params, self.alive, self.n_live, self.capacity)
         # keyframes: frame 0 and every keyframe_every-th frame (scripts/splatam.py:907-913)
         if t > 0 and (t + 1) % self.keyframe_every == 0:
             self.keyframes.append(self._kf(t))

@@ -100,7 +100,8 @@ def sequence_workload(scene: Scene, num_frames: int, dev, hole: float = 0.2, ste
     """(params, frames, cam, w2c, intrinsics, gt_poses): a synthetic capture for splatam_amd.sequence.
 
     The scene (camera frame of frame 0) is the truth; frame t's camera has moved by t * step = (metres along
-    x, degrees about y) and its target image / depth are the truth rendered there (depth with 1 % seeded
+    x, degrees about y) and its target image / depth are the truth rendered there (the depth as a sensor
+    reports it -- rendered depth / silhouette where the silhouette exceeds 0.5, else 0 -- with 1 % seeded
     noise, as mapping_keyframes).  The map SplaTAM starts from is the truth without the Gaussians whose
     projection in frame 0 falls in the left `hole` fraction of the image (the part the first frames must add
     by densification) and with pose columns t > 0 left at init_tracking_params' perturbed values (the
@@ -119,7 +120,12 @@ def sequence_workload(scene: Scene, num_frames: int, dev, hole: float = 0.2, ste
     g = torch.Generator().manual_seed(99)
     frames = []
     for t in range(num_frames):
-        im, depth = render_targets(truth, cam, w2c, t, perturb=gt)
+        im, _ = render_targets(truth, cam, w2c, t, perturb=gt)
+        with torch.no_grad():  # sensor-like depth: the surface depth (rendered depth / silhouette), 0 where uncovered
+            tg = transform_to_frame(gt, t, False, False)
+            ds, _, _ = GaussianRasterizer(cam)(**transformed_params2depthplussilhouette(gt, w2c, tg))
+            sil = ds[1:2]
+            depth = torch.where(sil > 0.5, ds[0:1] / sil.clamp_min(1e-6), torch.zeros_like(sil))
         depth = depth * (1.0 + 0.01 * torch.randn(depth.shape, generator=g).to(dev))
         frames.append({"im": im.clamp(0, 1).contiguous(), "depth": depth.contiguous()})
     c = scene.cam

@@ -43,7 +43,7 @@ def test_library_exports_every_header_symbol():
     missing = [f for f in fns if not hasattr(lib, f)]
     assert not missing, missing
     assert set(fns) == set(_lib.SIGNATURES), "ctypes signature table out of sync with include/*.h"
-    assert lib.gsr_abi_version() == 7
+    assert lib.gsr_abi_version() == 8
 
 
 @pytest.mark.parametrize("cname,pyname", [("gsr_settings", "GsrSettings"), ("gsr_gaussians", "GsrGaussians"),

@@ -575,7 +575,7 @@ def _geom_pair(cuda, seed, perturb_second=False, cache=True):
     g1 = torch.as_tensor(rs.randn(3, 120, 160).astype(np.float32), device=cuda)
     g2 = torch.as_tensor(rs.randn(3, 120, 160).astype(np.float32), device=cuda)
     old = _C._GEOM_CACHE
-    _C._GEOM_CACHE = cache
+    _C.set_geom_cache(cache)
     try:
         m3 = scene.means3D.to(cuda).requires_grad_(True)
         u_rot = scene.rotations.to(cuda).requires_grad_(True)
@@ -598,27 +598,48 @@ def _geom_pair(cuda, seed, perturb_second=False, cache=True):
         res += [t.grad.cpu() for t in (m3, u_rot, lo, ls, col)]
         return res
     finally:
-        _C._GEOM_CACHE = old
+        _C.set_geom_cache(old)
 
 
-def test_geometry_reuse_matches_two_full_calls(cuda):
+@pytest.mark.parametrize("native", [True, False])
+def test_geometry_reuse_matches_two_full_calls(cuda, native):
     """The second of two calls on identical geometry reuses the first call's preprocess / binning
-    (gsr_forward_reuse): images, radii, depth and every gradient bitwise those of two full calls."""
+    (gsr_forward_reuse_if_equal, comparison and gating on the device): images, radii, depth and every
+    gradient bitwise those of two full calls -- through the native binding and the ctypes one."""
     from splatam_amd import _C
-    hits = _C.REUSE_STATS["hits"]
-    a = _geom_pair(cuda, 41, cache=True)
-    assert _C.REUSE_STATS["hits"] == hits + 1, _C.REUSE_STATS  # the second call took the reuse path
-    b = _geom_pair(cuda, 41, cache=False)
+    with _binding(native):
+        hits = _C.reuse_stats()["hits"]
+        a = _geom_pair(cuda, 41, cache=True)
+        assert _C.reuse_stats()["hits"] == hits + 1, _C.reuse_stats()  # the second call took the reuse form
+        b = _geom_pair(cuda, 41, cache=False)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
 
 
-def test_geometry_reuse_refused_on_changed_geometry(cuda):
-    """Scales differing in the second call (bitwise comparison on the device) -> full forward."""
+@pytest.mark.parametrize("native", [True, False])
+def test_geometry_reuse_refused_on_changed_geometry(cuda, native):
+    """Scales differing in the second call (bitwise comparison on the device) -> the full forward ran."""
     from splatam_amd import _C
-    hits, content = _C.REUSE_STATS["hits"], _C.REUSE_STATS.get("content", 0)
-    a = _geom_pair(cuda, 43, perturb_second=True, cache=True)
-    assert _C.REUSE_STATS["hits"] == hits and _C.REUSE_STATS["content"] == content + 1, _C.REUSE_STATS
-    b = _geom_pair(cuda, 43, perturb_second=True, cache=False)
+    with _binding(native):
+        st = _C.reuse_stats()
+        hits, content = st["hits"], st.get("content", 0)
+        a = _geom_pair(cuda, 43, perturb_second=True, cache=True)
+        st = _C.reuse_stats()
+        assert st["hits"] == hits and st["content"] == content + 1, st
+        b = _geom_pair(cuda, 43, perturb_second=True, cache=False)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+@contextlib.contextmanager
+def _binding(native):
+    """The native torch binding (the default for the dynamic forward) or the ctypes path."""
+    from splatam_amd import _C
+    old = _C._NATIVE_ON
+    if native and _C._native() is None:
+        pytest.fail("the native torch binding did not load")
+    _C._NATIVE_ON = bool(native)
+    try:
+        yield
+    finally:
+        _C._NATIVE_ON = old

@@ -2,11 +2,10 @@
 per-frame loop of fresh GraphTrackers / GraphMappers on an unpadded map that grows by torch.cat
 (add_new_gaussians_literal) -- the form in which P changes every frame, scripts/splatam.py:697-929.
 
-The capacity-padded map keeps dead rows (culled by the alive mask) and appends the densified Gaussians at
-n_live + rank; its live rows, in slot order, are the literal map's rows.  Without pruning both forms run the
-same kernels on the same live Gaussians in the same order, so the poses and the map agree bitwise.  With the
-in-frame pruning the pruned rows stay in place (dead) in the padded map, which moves the later rows' block
-assignment in the pose reduction: the poses agree to float32 rounding, not bitwise."""
+The capacity-padded map keeps its free rows dead (culled by the alive mask), appends the densified Gaussians
+at n_live + rank and, after a frame's pruning, moves the live rows to the front in order (compact_static); its
+live rows are then the literal map's rows in the literal map's order, both forms run the same kernels on the
+same Gaussians in the same order, and the poses and the map agree bitwise -- with and without pruning."""
 import pytest
 import torch
 
@@ -63,13 +62,9 @@ def test_sequence_equals_per_frame_loop(cuda, capture, prune):
     dt = float((seq.params["cam_trans"] - ref["cam_trans"]).abs().max())
     errs = {k: float((live[k] - ref[k]).abs().max()) for k in GAUSS_KEYS + ("rgb_colors",)}
     print(f"  pose max |d| q {dq:.3e} t {dt:.3e}; map {errs}")
-    # tracking reached the trajectory (1 cm / 0.3 deg per frame)
-    assert float((seq.params["cam_trans"][..., 1:] - t_gt[..., 1:]).abs().max()) < 5e-3
-    if not prune:
-        assert dq == 0.0 and dt == 0.0
-        assert all(e == 0.0 for e in errs.values())
-    else:
-        assert dq <= 1e-5 and dt <= 1e-5
-        # the map: the mapping frames start from the densified Gaussians of slightly different poses
-        for k, e in errs.items():
-            assert e <= 1e-3 * max(1.0, float(ref[k].abs().max())), (k, e)
+    # tracking follows the trajectory (2 cm / 0.3 deg per frame)
+    te = float((seq.params["cam_trans"][..., 1:] - t_gt[..., 1:]).abs().max())
+    print(f"  translation error {te:.4f} m")
+    assert te < 1e-2
+    assert dq == 0.0 and dt == 0.0
+    assert all(e == 0.0 for e in errs.values())

@@ -12,8 +12,10 @@
 #   pmc              FETCH_SIZE / WRITE_SIZE passes (one rocprofv3 run per counter) of the headline bench
 #   mprof            rocprofv3 kernel trace + stats of the mapping bench (config 4)
 #   mpmc             map step + FETCH_SIZE / WRITE_SIZE passes of the mapping bench (render kernels, config 4)
+#   mpmcab           mpmc for the culled and the reference tile lists (--map-binning culled / reference)
 #   sq[=REGEX]       SQ issue / wait / LDS counters of the render kernels (or the kernels REGEX names; two
 #                    passes, <= 8 SQ counters each)
+#   squnit           SQ + FETCH / WRITE passes and the kernel trace of the drop-in unit's single-image render_bwd
 #   unit             host / device split of the unchanged-caller unit (tools/raster_unit_profile.py, config 3)
 #   stream           tools/micro/stream: STREAM copy / triad GB/s (the measured HBM peak)
 #   lock             render_bwd row-list lockstep statistics (tools/lockstep_stats.py, configs 3 and 4)
@@ -72,6 +74,30 @@ for s in "$@"; do
                -- python "$ROOT/bench.py" --workload mapping --steps 5 --warmup 5 --cpu-baseline off \
                > "$OUT/pmc_map_$C.log" 2>&1 ) || { echo "pmc map $C failed"; tail -20 "$OUT/pmc_map_$C.log"; exit 1; }
          done ;;
+    mpmcab) for B in culled reference; do  # tile cull A/B of the mapping kernels: times + FETCH / WRITE bytes
+           timeout -k 10 300 python bench.py --workload mapping --cpu-baseline off --map-binning $B \
+               > "$OUT/map_$B.log" 2>&1 || { echo "map $B failed"; tail -30 "$OUT/map_$B.log"; exit 1; }
+           for C in FETCH_SIZE WRITE_SIZE; do
+             ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $C \
+                 --kernel-include-regex 'render_|gauss_bwd' -T -d "$OUT/pmc_map_${B}_$C" -o run --output-format csv \
+                 -- python "$ROOT/bench.py" --workload mapping --steps 5 --warmup 5 --cpu-baseline off --map-binning $B \
+                 > "$OUT/pmc_map_${B}_$C.log" 2>&1 ) || { echo "pmc map $B $C failed"; tail -20 "$OUT/pmc_map_${B}_$C.log"; exit 1; }
+           done
+         done ;;
+    squnit) # the drop-in unit's single-image render_bwd (tools/raster_bench.py --mode single, config 3): SQ issue /
+            # wait / LDS counters, FETCH / WRITE bytes and the kernel trace, one rocprofv3 run each
+        G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+        G2="SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
+        i=0
+        for G in "$G1" "$G2" FETCH_SIZE WRITE_SIZE; do
+          i=$((i+1))
+          ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --pmc $G --kernel-include-regex 'render_bwd' -T \
+              -d "$OUT/squnit$i" -o run --output-format csv -- python "$ROOT/tools/raster_bench.py" --mode single \
+              --iters 40 --warmup 10 > "$OUT/squnit$i.log" 2>&1 ) || { echo "squnit pass $i failed"; tail -20 "$OUT/squnit$i.log"; exit 1; }
+        done
+        ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/squnit_trace" -o run \
+            --output-format csv -- python "$ROOT/tools/raster_bench.py" --mode single --iters 40 --warmup 10 \
+            > "$OUT/squnit_trace.log" 2>&1 ) || { echo "squnit trace failed"; tail -20 "$OUT/squnit_trace.log"; exit 1; } ;;
     sq|sq=*) RX='render_'; [ "$s" != sq ] && RX=${s#sq=}
         G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
         G2="SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
