@@ -90,7 +90,10 @@ def parse():
                          "threshold (removed at the frame's first pruning iteration, as faded Gaussians are)")
     ap.add_argument("--sequence", choices=("auto", "on", "off"), default="auto",
                     help="SLAM sequence leg (splatam_amd.sequence) at config 3 (auto: N=1 only)")
-    ap.add_argument("--seq-frames", type=int, default=4, help="sequence: timed frames (after frame 0)")
+    ap.add_argument("--seq-frames", type=int, default=4, help="sequence: timed frames (after frames 0 and 1)")
+    ap.add_argument("--seq-headroom", type=int, default=None,
+                    help="sequence: map capacity beyond the initial map, in Gaussians (default W*H/3); every "
+                         "per-Gaussian launch covers the whole capacity")
     ap.add_argument("--fisher-k", type=int, default=16, help="fisher: poses per HIP-graph launch")
     ap.add_argument("--configs", choices=("auto", "on", "off"), default="auto",
                     help="BASELINE configs 1 (forward only) and 2 (fwd+bwd RGB + depth) on the GPU and the CPU "
@@ -289,6 +292,9 @@ def main():
         bcast_split = {"value_no_broadcast": round(frames / el_nb, 3), "ms_per_step_no_broadcast":
                        round(1000.0 * el_nb / steps, 4), "broadcast_ms": round(1000.0 * el_b / nb, 4),
                        "broadcasts_in_timed_region": n_bcast, "broadcast_bytes": int(fm.nbytes),
+                       # the receiving ranks track against the map of the previous broadcast boundary (the
+                       # double-buffered broadcast goes live one boundary after it starts)
+                       "map_staleness_boundaries": 1,
                        "broadcast_path": "one RCCL broadcast of the flat map buffer (splatam_amd.dist.FlatMap) "
                                          "per map update, on a side stream overlapped with the next frame's "
                                          "replays (MapBroadcaster, double-buffered); broadcast_ms: the blocking "
@@ -924,7 +930,8 @@ def sequence_leg(args, dev):
     params, frames, cam, w2c, intr, (q_gt, t_gt) = sequence_workload(scene, K + 2, dev, prunable=args.map_prunable)
     P0 = params["means3D"].shape[0]
     n, _ = probe_num_rendered(params, {"cam": cam, "w2c": w2c, **frames[0]}, 0)
-    capacity, bin_cap = P0 + (K + 2) * W * H, 2 * n + 2_000_000
+    headroom = args.seq_headroom if args.seq_headroom is not None else W * H // 3
+    capacity, bin_cap = P0 + headroom, 2 * n + 2_000_000
     t0 = time.perf_counter()
     seq = SlamSequence(params, frames, cam, w2c, intr, capacity=capacity, bin_capacity=bin_cap, seed=0)
     torch.cuda.synchronize()

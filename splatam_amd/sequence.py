@@ -207,14 +207,27 @@ class SlamSequence:
             raise ValueError("SlamSequence: SplaTAM's isotropic rgb map (the tracking fast path's form)")
         if tracking_iters % track_replay:
             raise ValueError("tracking_iters must be a multiple of track_replay")
-        dev = params["means3D"].device
         self.frames, self.cam, self.w2c, self.intrinsics = frames, cam, w2c, intrinsics
-        self.capacity, self.bin_capacity = int(capacity), int(bin_capacity)
+        self.bin_capacity = int(bin_capacity)
         self.tracking_iters, self.mapping_iters, self.window = tracking_iters, mapping_iters, window
         self.keyframe_every, self.sil_thres = keyframe_every, sil_thres
-        self.params, self.alive, self.n_live = pad_map(params, self.capacity)
+        self.track_replay, self.track_cfg, self.map_cfg, self.prune, self.seed = \
+            track_replay, track_cfg, map_cfg, prune, seed
+        if scene_radius is None:  # initialize_first_timestep: max depth / scene_radius_depth_ratio (3, the config's)
+            scene_radius = frames[0]["depth"].max() / 3.0
+        self.scene_radius = scene_radius
+        self.keyframes = [self._kf(0)]
+        self.rng = np.random.RandomState(seed)
+        self.draws = []  # the mapper's keyframe draws per frame (window indices)
+        dev = params["means3D"].device
         self.overflow = torch.zeros(1, dtype=torch.bool, device=dev)
         self.dstatus = torch.zeros(4, dtype=torch.int32, device=dev)
+        self._build(params, int(capacity))
+
+    def _build(self, params: dict, capacity: int):
+        """The padded map of `params` (its per-Gaussian rows live) and the tracker / mapper graphs over it."""
+        self.capacity = capacity
+        self.params, self.alive, self.n_live = pad_map(params, self.capacity)
         for k in GAUSS_KEYS + ("rgb_colors",):
             self.params[k].requires_grad_(True)
         q, tr = params["cam_unnorm_rots"], params["cam_trans"]
@@ -225,17 +238,26 @@ class SlamSequence:
         self.slot = {k: (v.detach() if k in GAUSS_KEYS + ("rgb_colors",) else v) for k, v in self.params.items()}
         self.slot["cam_unnorm_rots"] = q[..., :1].detach().clone().requires_grad_(True)
         self.slot["cam_trans"] = tr[..., :1].detach().clone().requires_grad_(True)
-        self.slot_curr = {"cam": cam, "w2c": w2c, "im": frames[0]["im"].clone(), "depth": frames[0]["depth"].clone()}
-        self.tracker = GraphTracker(self.slot, self.slot_curr, 0, iters_per_graph=track_replay, cfg=track_cfg,
-                                    warmup_iters=1, fuse_pose=True, alive=self.alive, capacity=self.bin_capacity)
-        self.keyframes = [self._kf(0)]
-        self.rng = np.random.RandomState(seed)
-        if scene_radius is None:  # initialize_first_timestep: max depth / scene_radius_depth_ratio (3, the config's)
-            scene_radius = frames[0]["depth"].max() / 3.0
-        self.mapper = GraphMapper(self.params, self.keyframes, iters_per_graph=mapping_iters, cfg=map_cfg, seed=seed,
-                                  prune=prune, scene_radius=scene_radius, alive=self.alive,
-                                  capacity=self.bin_capacity)
-        self.draws = []  # the mapper's keyframe draws per frame (window indices)
+        f0 = self.frames[0]
+        self.slot_curr = {"cam": self.cam, "w2c": self.w2c, "im": f0["im"].clone(), "depth": f0["depth"].clone()}
+        self.tracker = GraphTracker(self.slot, self.slot_curr, 0, iters_per_graph=self.track_replay,
+                                    cfg=self.track_cfg, warmup_iters=1, fuse_pose=True, alive=self.alive,
+                                    capacity=self.bin_capacity)
+        self.mapper = GraphMapper(self.params, self.keyframes, iters_per_graph=self.mapping_iters, cfg=self.map_cfg,
+                                  seed=self.seed, prune=self.prune, scene_radius=self.scene_radius,
+                                  alive=self.alive, capacity=self.bin_capacity)
+
+    def ensure_headroom(self, free: int) -> bool:
+        """One host read of n_live: when fewer than `free` rows are left, move the map into a larger buffer
+        (max(2 x capacity, n_live + free) rows) and rebuild the two graphs -- the live rows and their order
+        unchanged, so the results are the same bits.  Every per-Gaussian launch covers the whole capacity
+        (bench.py's sequence leg: 45.6 frames/s at 342 k rows, 27.1 at 1.84 M for the same 293 k live
+        Gaussians), so size it to the map and grow on demand.  Returns True when it grew."""
+        n = int(self.n_live.item())
+        if self.capacity - n >= free:
+            return False
+        self._build(self.live_params(), max(2 * self.capacity, n + int(free)))
+        return True
 
     def _kf(self, t: int) -> dict:
         return {"cam": self.cam, "w2c": self.w2c, "im": self.frames[t]["im"], "depth": self.frames[t]["depth"], "id": t}

@@ -5,7 +5,8 @@ per-frame loop of fresh GraphTrackers / GraphMappers on an unpadded map that gro
 The capacity-padded map keeps its free rows dead (culled by the alive mask), appends the densified Gaussians
 at n_live + rank and, after a frame's pruning, moves the live rows to the front in order (compact_static); its
 live rows are then the literal map's rows in the literal map's order, both forms run the same kernels on the
-same Gaussians in the same order, and the poses and the map agree bitwise -- with and without pruning."""
+same Gaussians in the same order, and the poses and the map agree bitwise -- with and without pruning, and
+when the map outgrows its buffer mid-sequence (ensure_headroom: a larger buffer, the graphs rebuilt)."""
 import pytest
 import torch
 
@@ -33,24 +34,30 @@ def _literal(params0, frames, cam, w2c, intr, draws, bin_cap, prune):
     return ref.p
 
 
-def _run_sequence(capture, prune):
+def _run_sequence(capture, prune, grow=False):
     params, frames, cam, w2c, intr, _ = capture
     from splatam_amd.tracker import probe_num_rendered
     n, _ = probe_num_rendered(params, {"cam": cam, "w2c": w2c, "im": frames[0]["im"], "depth": frames[0]["depth"]}, 0)
     bin_cap = 4 * n + 400_000
-    seq = SlamSequence(params, frames, cam, w2c, intr, capacity=params["means3D"].shape[0] + 2 * 320 * 240,
+    P0 = params["means3D"].shape[0]
+    seq = SlamSequence(params, frames, cam, w2c, intr, capacity=P0 + (1000 if grow else 2 * 320 * 240),
                        bin_capacity=bin_cap, prune=prune, seed=0)
+    grew = 0
     for t in range(N_FRAMES):
+        if grow:  # the capacity runs out after frame 0: the map moves to a larger buffer, graphs rebuilt
+            grew += seq.ensure_headroom(320 * 240)
         seq.frame(t)
+    if grow:
+        assert grew >= 1 and seq.capacity > P0 + 1000
     seq.check()
     torch.cuda.synchronize()
     return seq, bin_cap
 
 
-@pytest.mark.parametrize("prune", [False, True])
-def test_sequence_equals_per_frame_loop(cuda, capture, prune):
+@pytest.mark.parametrize("prune,grow", [(False, False), (True, False), (True, True)])
+def test_sequence_equals_per_frame_loop(cuda, capture, prune, grow):
     params, frames, cam, w2c, intr, (q_gt, t_gt) = capture
-    seq, bin_cap = _run_sequence(capture, prune)
+    seq, bin_cap = _run_sequence(capture, prune, grow)
     ref = _literal(params, frames, cam, w2c, intr, seq.draws, bin_cap, prune)
     live = seq.live_params()
     P0, Pn = params["means3D"].shape[0], live["means3D"].shape[0]
