@@ -1006,7 +1006,7 @@ def mapping_leg(args, dev):
     a.config, a.steps, a.warmup = 4, max(1, args.mapping_steps), args.map_frame_iters
     line = run_mapping(a, 1, 0, dev)
     keep = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "execution", "config", "roofline",
-            "stages_us", "pruning")
+            "stages_us", "stages_source", "pruning")
     return {k: line[k] for k in keep}
 
 
@@ -1043,9 +1043,14 @@ def run_mapping(args, world, rank, dev):
     from splatam_amd import _C
     binning = _C.reference_binning() if getattr(args, "map_binning", "culled") == "reference" else \
         contextlib.nullcontext()
+    snap = {k: params[k].detach().clone() for k in ("means3D", "unnorm_rotations", "logit_opacities", "log_scales",
+                                                     key)}  # (the stage-breakdown pass starts from the same map)
     with binning:  # (captured into the graph: every replay bins this way)
+        # the timed replays clock the render kernels only (each clocked launch pays its workgroups' clock
+        # atomics); the other stages come from a separate all-clocks mapper after the timed region
         mapper = GraphMapper(params, kfs, iters_per_graph=S, cfg=MappingConfig(), timing=bool(args.timing),
-                             prune=bool(args.map_prune), scene_radius=scene_radius)
+                             prune=bool(args.map_prune), scene_radius=scene_radius,
+                             clock_stages=("render_fwd", "render_bwd"))
     for _ in range(max(1, -(-args.warmup // S))):  # >= W untimed iterations (whole replays)
         mapper.run()  # checked: raises on an overflow
     torch.cuda.synchronize()
@@ -1065,10 +1070,27 @@ def run_mapping(args, world, rank, dev):
     if mapper.overflowed():
         raise SystemExit(f"binning capacity overflow during the timed replays (capacity {mapper.capacity}): "
                          "measurement invalid")
-    elapsed = sd.max_over_ranks(t1 - t0, device=dev)
-    value = steps * world / elapsed
     survivors = int(mapper.survivors().sum().item())
     nr = mapper.num_rendered()
+    stages_all = None
+    if args.timing and getattr(args, "stage_breakdown", "on") == "on":  # every stage clocked, one untimed frame
+        mcap = mapper.capacity
+        del mapper
+        with torch.no_grad():
+            for k, v in snap.items():
+                params[k].copy_(v)
+        with binning:
+            mb = GraphMapper(params, kfs, iters_per_graph=S, cfg=MappingConfig(), timing=True,
+                             prune=bool(args.map_prune), scene_radius=scene_radius, capacity=mcap)
+        profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)
+        mb.run(check=False)
+        torch.cuda.synchronize()
+        stages_all = profiling.read_timing()
+        profiling.enable_timing(False)
+        del mb
+    del snap
+    elapsed = sd.max_over_ranks(t1 - t0, device=dev)
+    value = steps * world / elapsed
     roofline = render_bwd_roofline(stages["render_bwd"], sum(nr) / len(nr), P, W, H, graph=True)
     roofline["traffic"], roofline["traffic_source"] = committed_traffic("mapping_render_bwd_pmc.json")
     line = {
@@ -1091,9 +1113,12 @@ def run_mapping(args, world, rank, dev):
                    "keyframes": K, "parallelism": f"frame-sharded x{world}",
                    "binning": getattr(args, "map_binning", "culled")},
         "roofline": roofline,
-        "stages_us": {k: round(v["avg_us"], 2) for k, v in stages.items() if v["launches"]},
+        "stages_us": {k: round(v["avg_us"], 2) for k, v in (stages_all or stages).items() if v["launches"]},
+        "stages_source": ("a separate untimed frame with every kernel's in-kernel stage clock on (the timed "
+                          "replays clock the render kernels only)" if stages_all else
+                          "the timed replays' in-kernel stage clocks (render kernels)"),
     }
-    del mapper, params, kfs
+    del params, kfs
     torch.cuda.empty_cache()
     return line
 

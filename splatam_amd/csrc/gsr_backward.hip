@@ -366,6 +366,7 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
     const int my_e = row_entry(lane);
     // Slots start zero; after every batch the used slots (those of the batch's entries, every slot a row
     // list can have written) are cleared, and the pad slot only ever receives zeros.
+    constexpr bool kBulkClear = !OPAC;
     for (int q = tid; q < (BS + 1) * NV; q += TILE_PIX) s_acc[q] = 0.f;
     const uint32_t* my_list = s_list + (4 * w + row) * LS;
     if (tid == 0) {
@@ -618,11 +619,14 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
 #pragma unroll
             for (int i = 0; i < NQ; i++) c[i] = 0.f;
             const int nb = __popc((uint32_t)s_mask[e]);
-            const float* src = s_acc + (int)s_base[e] * NV;
+            float* src = s_acc + (int)s_base[e] * NV;
             for (int b = 0; b < nb; b++, src += NV) {
 #pragma unroll
                 for (int i = 0; i < NQ; i++)
-                    if (q + TPE * i < NV) c[i] += src[q + TPE * i];
+                    if (q + TPE * i < NV) {
+                        c[i] += src[q + TPE * i];
+                        if constexpr (!kBulkClear) src[q + TPE * i] = 0.f;
+                    }
             }
             float* dst = inst + (size_t)RS * s_u[e];  // packed record (RecLayout): the NV sums, zero pad
 #pragma unroll
@@ -640,8 +644,11 @@ __device__ __forceinline__ void bwd_tile(const Camera& cam, int tile, const BwdP
         // The batch's slots back to zero for the next batch's reduction: the used range [0, slots of entries
         // < cnt) as contiguous float4 stores (the next batch's staging barrier orders them before its walk).
         // Re-zeroing each slot right after reading it cost bank-conflicted scattered stores in the totals
-        // (slot stride NV = 6 words: entries whose slot bases differ by 16 share banks)
-        {
+        // (slot stride NV = 6 words: entries whose slot bases differ by 16 share banks).  Only in the lean
+        // variants (no opacity gradient: the tracking render): the full-gradient ones are at their VGPR
+        // bound, where the sweep's bookkeeping spilled (render_bwd<1,1,1,1,1,0>: 16 B of scratch, +10 us at
+        // config 4), so they keep re-zeroing in the totals
+        if constexpr (kBulkClear) {
             const int used = cnt > 0 ? (int)s_base[cnt - 1] + __popc((uint32_t)s_mask[cnt - 1]) : 0;
             float4* const a4 = reinterpret_cast<float4*>(s_acc);
             const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);

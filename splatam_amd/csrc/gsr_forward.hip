@@ -987,11 +987,33 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
                                                   sort_cap, status, s_cur);
     if constexpr (CLK) kclock_end(clk);
 }
+// The exact-tail form (the dynamic forward) needs ~88 VGPRs: at the 80-VGPR cap above it spills 80 B per
+// lane; GSR_DUP_EXACT_WAVES sets its own occupancy target
+#ifndef GSR_DUP_EXACT_WAVES
+#define GSR_DUP_EXACT_WAVES 6
+#endif
+template <bool LDS_HIST, int DUP_G, bool CLK>
+__global__ void __launch_bounds__(DUP_T) __attribute__((amdgpu_waves_per_eu(GSR_DUP_EXACT_WAVES, 8)))
+duplicate_bucket_exact_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges,
+                              const uint32_t* __restrict__ tot, uint32_t* __restrict__ cursor, int ntiles,
+                              uint64_t* __restrict__ keys, uint64_t* __restrict__ point_list, SpecGuard guard,
+                              uint32_t sort_cap, uint32_t* __restrict__ status, unsigned long long* clk) {
+    extern __shared__ uint32_t s_cur[];
+    if (cam.gate.off()) return;
+    if constexpr (CLK) kclock_begin(clk);
+    duplicate_bucket_body<LDS_HIST, DUP_G, true>(cam, P, geo, ranges, tot, cursor, ntiles, keys, point_list, guard,
+                                                 sort_cap, status, s_cur);
+    if constexpr (CLK) kclock_end(clk);
+}
 
 template <bool CLK, bool EXACT>
 static auto duplicate_bucket_variant(bool lds_hist, bool g2) {
-    return lds_hist ? (g2 ? duplicate_bucket_kernel<true, 2, CLK, EXACT> : duplicate_bucket_kernel<true, 1, CLK, EXACT>)
-                    : (g2 ? duplicate_bucket_kernel<false, 2, CLK, EXACT> : duplicate_bucket_kernel<false, 1, CLK, EXACT>);
+    if constexpr (EXACT)
+        return lds_hist ? (g2 ? duplicate_bucket_exact_kernel<true, 2, CLK> : duplicate_bucket_exact_kernel<true, 1, CLK>)
+                        : (g2 ? duplicate_bucket_exact_kernel<false, 2, CLK> : duplicate_bucket_exact_kernel<false, 1, CLK>);
+    else
+        return lds_hist ? (g2 ? duplicate_bucket_kernel<true, 2, CLK, false> : duplicate_bucket_kernel<true, 1, CLK, false>)
+                        : (g2 ? duplicate_bucket_kernel<false, 2, CLK, false> : duplicate_bucket_kernel<false, 1, CLK, false>);
 }
 
 hipError_t launch_duplicate_bucket(const Camera& cam, int P, GeomPtrs geo, uint2* ranges, const uint32_t* tot,

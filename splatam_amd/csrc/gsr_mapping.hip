@@ -346,15 +346,16 @@ __global__ void __launch_bounds__(ADAM_BLOCK) adam_step_kernel(AdamArgs a) {
         for (int k = 0; k < 4; k++) {
             const long long i = base + 4 * ((long long)k * ADAM_BLOCK + threadIdx.x);
             if (i + 3 < n) {
-                float4 P4 = *reinterpret_cast<const float4*>(p + i), G4 = *reinterpret_cast<const float4*>(g + i);
-                float4 M4 = *reinterpret_cast<const float4*>(m + i), V4 = *reinterpret_cast<const float4*>(v + i);
+                float4 P4 = *reinterpret_cast<const float4*>(p + i), G4 = ld_stream(reinterpret_cast<const float4*>(g + i));
+                float4 M4 = ld_stream(reinterpret_cast<const float4*>(m + i));
+                float4 V4 = ld_stream(reinterpret_cast<const float4*>(v + i));
                 adam_elem(P4.x, G4.x, M4.x, V4.x, ss, a);
                 adam_elem(P4.y, G4.y, M4.y, V4.y, ss, a);
                 adam_elem(P4.z, G4.z, M4.z, V4.z, ss, a);
                 adam_elem(P4.w, G4.w, M4.w, V4.w, ss, a);
-                *reinterpret_cast<float4*>(p + i) = P4;
-                *reinterpret_cast<float4*>(m + i) = M4;
-                *reinterpret_cast<float4*>(v + i) = V4;
+                st_stream(reinterpret_cast<float4*>(p + i), P4);
+                st_stream(reinterpret_cast<float4*>(m + i), M4);
+                st_stream(reinterpret_cast<float4*>(v + i), V4);
             } else {
                 for (long long e = i; e < n; e++) adam_elem(p[e], g[e], m[e], v[e], ss, a);
             }
@@ -380,11 +381,11 @@ struct MapAdam {  // the mapping optimizer's state, applied in place (NULL p: wr
 };
 
 __device__ __forceinline__ float adam_apply(float* p, float g, float* m, float* v, float ss, const MapAdam& a) {
-    float mm = *m, vv = *v;
+    float mm = ld_stream(m), vv = ld_stream(v);
     const float np = adam_update_elem(*p, g, mm, vv, ss, a.w1, a.beta2, a.omb2, a.bc2_sqrt, a.eps);
-    *m = mm;
-    *v = vv;
-    *p = np;
+    st_stream(m, mm);
+    st_stream(v, vv);
+    st_stream(p, np);
     return np;
 }
 
@@ -398,16 +399,16 @@ __device__ __forceinline__ void adam_apply_n(float* p, const float* g, float* m,
 #pragma unroll
     for (int k = 0; k < N; k++) {
         pv[k] = p[k * stride];
-        mv[k] = m[k * stride];
-        vv[k] = v[k * stride];
+        mv[k] = ld_stream(m + k * stride);
+        vv[k] = ld_stream(v + k * stride);
     }
 #pragma unroll
     for (int k = 0; k < N; k++) {
         float mm = mv[k], v2 = vv[k];
         const float np = adam_update_elem(pv[k], g[k], mm, v2, ss, a.w1, a.beta2, a.omb2, a.bc2_sqrt, a.eps);
-        m[k * stride] = mm;
-        v[k * stride] = v2;
-        p[k * stride] = np;
+        st_stream(m + k * stride, mm);
+        st_stream(v + k * stride, v2);
+        st_stream(p + k * stride, np);
     }
 }
 
@@ -513,16 +514,18 @@ map_transform_bwd_kernel(int P, const float* ur, const float* lo, const float* l
     float* const v2 = adam.v[2] + i;
     float* const v3 = adam.v[3] + scols * i;
 #pragma unroll
-    for (int k = 0; k < 3; k++) { pv[k] = p0[k]; mv[k] = m0[k]; vv[k] = v0[k]; gv[k] = dp[k]; }
+    for (int k = 0; k < 3; k++) { pv[k] = p0[k]; mv[k] = ld_stream(m0 + k); vv[k] = ld_stream(v0 + k); gv[k] = dp[k]; }
 #pragma unroll
-    for (int k = 0; k < 4; k++) { pv[3 + k] = p1[k]; mv[3 + k] = m1[k]; vv[3 + k] = v1[k]; gv[3 + k] = duv[k]; }
-    pv[7] = *p2; mv[7] = *m2; vv[7] = *v2; gv[7] = dl;
+    for (int k = 0; k < 4; k++) {
+        pv[3 + k] = p1[k]; mv[3 + k] = ld_stream(m1 + k); vv[3 + k] = ld_stream(v1 + k); gv[3 + k] = duv[k];
+    }
+    pv[7] = *p2; mv[7] = ld_stream(m2); vv[7] = ld_stream(v2); gv[7] = dl;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         const bool on = k < scols;
         pv[8 + k] = on ? p3[k] : 0.f;
-        mv[8 + k] = on ? m3[k] : 0.f;
-        vv[8 + k] = on ? v3[k] : 0.f;
+        mv[8 + k] = on ? ld_stream(m3 + k) : 0.f;
+        vv[8 + k] = on ? ld_stream(v3 + k) : 0.f;
         gv[8 + k] = dsc[k];
     }
 #pragma unroll
@@ -534,27 +537,27 @@ map_transform_bwd_kernel(int P, const float* ur, const float* lo, const float* l
     // stores grouped by array (adjacent elements of one array in a row), so they merge into
     // dwordx3 / dwordx4 stores: interleaving p / m / v stores (possibly aliasing) kept them dwords
 #pragma unroll
-    for (int k = 0; k < 3; k++) p0[k] = pv[k];
+    for (int k = 0; k < 3; k++) st_stream(p0 + k, pv[k]);
 #pragma unroll
-    for (int k = 0; k < 3; k++) m0[k] = mv[k];
+    for (int k = 0; k < 3; k++) st_stream(m0 + k, mv[k]);
 #pragma unroll
-    for (int k = 0; k < 3; k++) v0[k] = vv[k];
+    for (int k = 0; k < 3; k++) st_stream(v0 + k, vv[k]);
 #pragma unroll
-    for (int k = 0; k < 4; k++) p1[k] = pv[3 + k];
+    for (int k = 0; k < 4; k++) st_stream(p1 + k, pv[3 + k]);
 #pragma unroll
-    for (int k = 0; k < 4; k++) m1[k] = mv[3 + k];
+    for (int k = 0; k < 4; k++) st_stream(m1 + k, mv[3 + k]);
 #pragma unroll
-    for (int k = 0; k < 4; k++) v1[k] = vv[3 + k];
-    *p2 = pv[7]; *m2 = mv[7]; *v2 = vv[7];
+    for (int k = 0; k < 4; k++) st_stream(v1 + k, vv[3 + k]);
+    st_stream(p2, pv[7]); st_stream(m2, mv[7]); st_stream(v2, vv[7]);
     if (scols == 3) {
 #pragma unroll
-        for (int k = 0; k < 3; k++) p3[k] = pv[8 + k];
+        for (int k = 0; k < 3; k++) st_stream(p3 + k, pv[8 + k]);
 #pragma unroll
-        for (int k = 0; k < 3; k++) m3[k] = mv[8 + k];
+        for (int k = 0; k < 3; k++) st_stream(m3 + k, mv[8 + k]);
 #pragma unroll
-        for (int k = 0; k < 3; k++) v3[k] = vv[8 + k];
+        for (int k = 0; k < 3; k++) st_stream(v3 + k, vv[8 + k]);
     } else {
-        *p3 = pv[8]; *m3 = mv[8]; *v3 = vv[8];
+        st_stream(p3, pv[8]); st_stream(m3, mv[8]); st_stream(v3, vv[8]);
     }
 }
 

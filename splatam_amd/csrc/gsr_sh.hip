@@ -20,6 +20,13 @@ namespace gsr {
 namespace {
 
 constexpr int SH_BLOCK = 256;
+#ifndef GSR_SH_SPLIT
+#define GSR_SH_SPLIT 1  // sh_bwd_split_kernel for the fused colour Adam step (config 4: 205 -> 195 us)
+#endif
+constexpr int SH_SPLIT_BLOCK = 128;
+#ifndef GSR_SH_BWD_NT
+#define GSR_SH_BWD_NT 0  // sh_bwd's coefficient staging with nontemporal loads (its Adam step re-reads them)
+#endif
 // sh_eval: one wave per workgroup (12.5 KB of LDS at D = 3): the waves of a CU stage and evaluate
 // independently instead of in barrier-coupled groups of four
 
@@ -30,7 +37,9 @@ struct ShTile {
 };
 
 // Global [n x ROW] block (contiguous: M == NSH) -> LDS rows.
-template <int NSH, int BLK = SH_BLOCK>
+// NT: nontemporal loads (sh_eval's coefficient stream, read once there; sh_bwd's staging keeps the plain
+// loads: its colour Adam step re-reads the same coefficients right after)
+template <int NSH, int BLK = SH_BLOCK, bool NT = false>
 __device__ __forceinline__ void stage_rows(float* s, const float* __restrict__ src, int n, int tix = -1) {
     const int tt = tix < 0 ? (int)threadIdx.x : tix;  // the staging thread's index among BLK
     using T = ShTile<NSH>;
@@ -41,7 +50,7 @@ __device__ __forceinline__ void stage_rows(float* s, const float* __restrict__ s
             constexpr int IT = T::ROW / 4 > 0 ? T::ROW / 4 : 1;  // float4 per lane (ROW % 4 == 0 here)
             float4 v[IT];
 #pragma unroll
-            for (int k = 0; k < IT; k++) v[k] = s4[tt + k * BLK];
+            for (int k = 0; k < IT; k++) v[k] = NT ? ld_stream(s4 + tt + k * BLK) : s4[tt + k * BLK];
 #pragma unroll
             for (int k = 0; k < IT; k++) {
                 const int e = 4 * (tt + k * BLK), r = e / T::ROW, c = e - r * T::ROW;
@@ -106,9 +115,9 @@ __device__ __forceinline__ void adam_rows(float* p, float* m, float* v, const fl
             float4 pv[U], mv[U], vv[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                pv[u] = p4[e4 + u * SH_BLOCK];
-                mv[u] = m4[e4 + u * SH_BLOCK];
-                vv[u] = v4[e4 + u * SH_BLOCK];
+                pv[u] = GSR_SH_BWD_NT ? ld_stream(p4 + e4 + u * SH_BLOCK) : p4[e4 + u * SH_BLOCK];
+                mv[u] = ld_stream(m4 + e4 + u * SH_BLOCK);
+                vv[u] = ld_stream(v4 + e4 + u * SH_BLOCK);
             }
 #pragma unroll
             for (int u = 0; u < U; u++) {
@@ -121,22 +130,22 @@ __device__ __forceinline__ void adam_rows(float* p, float* m, float* v, const fl
             }
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                m4[e4 + u * SH_BLOCK] = mv[u];
-                v4[e4 + u * SH_BLOCK] = vv[u];
-                p4[e4 + u * SH_BLOCK] = pv[u];
+                st_stream(m4 + e4 + u * SH_BLOCK, mv[u]);
+                st_stream(v4 + e4 + u * SH_BLOCK, vv[u]);
+                st_stream(p4 + e4 + u * SH_BLOCK, pv[u]);
             }
         }
         for (; 4 * e4 < total; e4 += SH_BLOCK) {
             const int e = 4 * e4, r = e / T::ROW, c = e - r * T::ROW;
             const float* q = s + r * T::PITCH + c;
-            float4 pv = p4[e4], mv = m4[e4], vv = v4[e4];
+            float4 pv = p4[e4], mv = ld_stream(m4 + e4), vv = ld_stream(v4 + e4);
             elem(pv.x, q[0], mv.x, vv.x);
             elem(pv.y, q[1], mv.y, vv.y);
             elem(pv.z, q[2], mv.z, vv.z);
             elem(pv.w, q[3], mv.w, vv.w);
-            m4[e4] = mv;
-            v4[e4] = vv;
-            p4[e4] = pv;
+            st_stream(m4 + e4, mv);
+            st_stream(v4 + e4, vv);
+            st_stream(p4 + e4, pv);
         }
     } else {
         for (int e = threadIdx.x; e < total; e += SH_BLOCK) {
@@ -147,6 +156,62 @@ __device__ __forceinline__ void adam_rows(float* p, float* m, float* v, const fl
             v[e] = vv;
             p[e] = pv;
         }
+    }
+}
+
+// adam_rows with the parameters taken from the workgroup's own LDS copy (s_p, the staged coefficients)
+// instead of re-reading them from HBM: only exp_avg / exp_avg_sq are read (the same bits: s_p holds what
+// the block staged).  BLK lanes, gradients in s_g.
+template <int NSH, int BLK>
+__device__ __forceinline__ void adam_rows_lds(float* p, float* m, float* v, const float* s_p, const float* s_g, int n,
+                                              const ShAdam& a) {
+    using T = ShTile<NSH>;
+    const int total = n * T::ROW;
+    auto elem = [&](float& pp, float g, float& mm_, float& vv_) {
+        pp = adam_update_elem(pp, g, mm_, vv_, a.ss, a.w1, a.beta2, a.omb2, a.bc2_sqrt, a.eps);
+    };
+    float4* p4 = reinterpret_cast<float4*>(p);
+    float4* m4 = reinterpret_cast<float4*>(m);
+    float4* v4 = reinterpret_cast<float4*>(v);
+    constexpr int U = 4;
+    int e4 = threadIdx.x;
+    for (; 4 * (e4 + (U - 1) * BLK) < total; e4 += U * BLK) {
+        float4 pv[U], mv[U], vv[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            mv[u] = ld_stream(m4 + e4 + u * BLK);
+            vv[u] = ld_stream(v4 + e4 + u * BLK);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int e = 4 * (e4 + u * BLK), r = e / T::ROW, c = e - r * T::ROW;
+            const float* q = s_g + r * T::PITCH + c;
+            const float* pp = s_p + r * T::PITCH + c;
+            pv[u] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+            elem(pv[u].x, q[0], mv[u].x, vv[u].x);
+            elem(pv[u].y, q[1], mv[u].y, vv[u].y);
+            elem(pv[u].z, q[2], mv[u].z, vv[u].z);
+            elem(pv[u].w, q[3], mv[u].w, vv[u].w);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            st_stream(m4 + e4 + u * BLK, mv[u]);
+            st_stream(v4 + e4 + u * BLK, vv[u]);
+            st_stream(p4 + e4 + u * BLK, pv[u]);
+        }
+    }
+    for (; 4 * e4 < total; e4 += BLK) {
+        const int e = 4 * e4, r = e / T::ROW, c = e - r * T::ROW;
+        const float* q = s_g + r * T::PITCH + c;
+        const float* pp = s_p + r * T::PITCH + c;
+        float4 pv = make_float4(pp[0], pp[1], pp[2], pp[3]), mv = ld_stream(m4 + e4), vv = ld_stream(v4 + e4);
+        elem(pv.x, q[0], mv.x, vv.x);
+        elem(pv.y, q[1], mv.y, vv.y);
+        elem(pv.z, q[2], mv.z, vv.z);
+        elem(pv.w, q[3], mv.w, vv.w);
+        st_stream(m4 + e4, mv);
+        st_stream(v4 + e4, vv);
+        st_stream(p4 + e4, pv);
     }
 }
 
@@ -163,7 +228,7 @@ __global__ void __launch_bounds__(64) sh_eval_kernel(Camera cam, GaussIn g, Geom
     // the lane's mean is loaded with the staging stream, not after it
     const float3 p = act ? make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2])
                          : make_float3(0.f, 0.f, 0.f);
-    stage_rows<NSH, 64>(s_sh, g.shs + (size_t)T::ROW * base, n);
+    stage_rows<NSH, 64, true>(s_sh, g.shs + (size_t)T::ROW * base, n);
     __syncthreads();
     if (!act) return;
     float rgb[3];
@@ -185,7 +250,7 @@ sh_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii
     __shared__ float s_sh[SH_BLOCK * T::PITCH];
     const int base = blockIdx.x * SH_BLOCK;
     const int n = min(SH_BLOCK, g.P - base);
-    stage_rows<NSH>(s_sh, g.shs + (size_t)T::ROW * base, n);
+    stage_rows<NSH, SH_BLOCK, GSR_SH_BWD_NT != 0>(s_sh, g.shs + (size_t)T::ROW * base, n);
     __syncthreads();
     if ((int)threadIdx.x < n) {
         const int i = base + threadIdx.x;
@@ -215,6 +280,55 @@ sh_bwd_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii
     }
 }
 
+// sh_bwd with the colour Adam step reading the coefficients from LDS: the gradient rows go to a second LDS
+// array (two 128-Gaussian blocks of rows, 50 KB at D = 3), so the staged coefficients survive the chain
+// and the step reads only the two moments from HBM (192 MB less per config-4 iteration than re-reading the
+// coefficients).  Same element update, same bits.
+template <int NSH>
+__global__ void __launch_bounds__(SH_SPLIT_BLOCK)
+sh_bwd_split_kernel(Camera cam, GaussIn g, GeomPtrs geo, const int* __restrict__ radii, const float* __restrict__ drgb,
+                    float* __restrict__ dmeans3D, float* __restrict__ dsh, BwdGuard guard, ShAdam sa) {
+    using T = ShTile<NSH>;
+    constexpr int BLK = SH_SPLIT_BLOCK;
+    __shared__ float s_sh[BLK * T::PITCH];
+    __shared__ float s_g[BLK * T::PITCH];
+    const int base = blockIdx.x * BLK;
+    const int n = min(BLK, g.P - base);
+    stage_rows<NSH, BLK>(s_sh, g.shs + (size_t)T::ROW * base, n);
+    __syncthreads();
+    if ((int)threadIdx.x < n) {
+        const int i = base + threadIdx.x;
+        const float* row = s_sh + threadIdx.x * T::PITCH;
+        float* grow = s_g + threadIdx.x * T::PITCH;
+        if (radii[i] > 0 && !guard.overflow()) {
+            const float3 m = make_float3(g.means3D[3 * i], g.means3D[3 * i + 1], g.means3D[3 * i + 2]);
+            const float d[3] = {drgb[3 * i], drgb[3 * i + 1], drgb[3 * i + 2]};
+            float dmean[3] = {dmeans3D[3 * i], dmeans3D[3 * i + 1], dmeans3D[3 * i + 2]};
+            float dsh_r[T::ROW];
+            sh_chain_bwd(cam, m, row, d, geo.clamp[i], dsh_r, dmean);
+#pragma unroll
+            for (int k = 0; k < T::ROW; k++) grow[k] = dsh_r[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) dmeans3D[3 * i + k] = dmean[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < T::ROW; k++) grow[k] = 0.f;
+        }
+    }
+    __syncthreads();
+    if (sa.m) {
+        if (fused_step_skipped(sa.guard, sa.cap, sa.halted)) return;
+        const size_t o = (size_t)T::ROW * base;
+        adam_rows_lds<NSH, BLK>(const_cast<float*>(g.shs) + o, sa.m + o, sa.v + o, s_sh, s_g, n, sa);
+    } else if (dsh) {
+        const int total = n * T::ROW;
+        for (int e = threadIdx.x; e < total; e += BLK) {
+            const int r = e / T::ROW, c = e - r * T::ROW;
+            dsh[(size_t)T::ROW * base + e] = s_g[r * T::PITCH + c];
+        }
+    }
+}
+
 template <int NSH>
 hipError_t launch_sh_eval_t(const Camera& cam, const GaussIn& g, GeomPtrs geo, hipStream_t s) {
     constexpr int per = 64;
@@ -225,6 +339,14 @@ hipError_t launch_sh_eval_t(const Camera& cam, const GaussIn& g, GeomPtrs geo, h
 template <int NSH>
 hipError_t launch_sh_bwd_t(const Camera& cam, const GaussIn& g, GeomPtrs geo, const int* radii, const float* drgb,
                            float* dmeans3D, float* dsh, BwdGuard guard, hipStream_t s, const ShAdam& sa) {
+    using T = ShTile<NSH>;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(g.shs) | reinterpret_cast<uintptr_t>(sa.m) |
+                           reinterpret_cast<uintptr_t>(sa.v)) & 15u) == 0;
+    if (GSR_SH_SPLIT && sa.m && T::ROW % 4 == 0 && aligned) {  // (the float4 form of adam_rows_lds)
+        hipLaunchKernelGGL(sh_bwd_split_kernel<NSH>, dim3((g.P + SH_SPLIT_BLOCK - 1) / SH_SPLIT_BLOCK),
+                           dim3(SH_SPLIT_BLOCK), 0, s, cam, g, geo, radii, drgb, dmeans3D, dsh, guard, sa);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(sh_bwd_kernel<NSH>, dim3((g.P + SH_BLOCK - 1) / SH_BLOCK), dim3(SH_BLOCK), 0, s, cam, g, geo,
                        radii, drgb, dmeans3D, dsh, guard, sa);
     return hipGetLastError();

@@ -73,7 +73,8 @@ def probe_num_rendered(params, curr_data, time_idx) -> tuple[int, int]:
 class GraphMapper:
     def __init__(self, params: dict, keyframes: list, iters_per_graph: int = 60, cfg: MappingConfig = MappingConfig(),
                  headroom: float = 1.5, min_extra: int = 65536, seed: int | None = None, timing: bool = False,
-                 prune: bool | None = None, scene_radius=None, alive=None, capacity: int | None = None):
+                 prune: bool | None = None, scene_radius=None, alive=None, capacity: int | None = None,
+                 clock_stages=None):
         if not keyframes:
             raise RuntimeError("GraphMapper needs at least one keyframe")
         for kf in keyframes:
@@ -133,9 +134,11 @@ class GraphMapper:
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         del snapshot
-        if timing:
+        if timing:  # in-kernel stage clocks captured into the graph (clock_stages: which; default every stage --
+            # each clocked launch pays its workgroups' clock atomics, ~15 us for config 4's preprocess)
             from . import profiling
-            profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES)
+            profiling.enable_timing(clock_stages=profiling.CLOCK_STAGES if clock_stages is None else
+                                    tuple(clock_stages))
         self.graph = torch.cuda.CUDAGraph()
         self.stream = side
         with torch.cuda.graph(self.graph, stream=side):

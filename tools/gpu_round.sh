@@ -16,6 +16,7 @@
 #   sq[=REGEX]       SQ issue / wait / LDS counters of the render kernels (or the kernels REGEX names; two
 #                    passes, <= 8 SQ counters each)
 #   squnit           SQ + FETCH / WRITE passes and the kernel trace of the drop-in unit's single-image render_bwd
+#   msq=REGEX        SQ + FETCH / WRITE passes of the mapping bench's kernels matching REGEX
 #   unit             host / device split of the unchanged-caller unit (tools/raster_unit_profile.py, config 3)
 #   stream           tools/micro/stream: STREAM copy / triad GB/s (the measured HBM peak)
 #   lock             render_bwd row-list lockstep statistics (tools/lockstep_stats.py, configs 3 and 4)
@@ -27,6 +28,8 @@
 #   abbench=TAGS     interleaved A/B of the bench line (tracking + mapping values, render stage times)
 #   abprof=TAGS      interleaved A/B (two rounds) of rocprofv3 kernel-trace averages of the headline bench's
 #                    tracking kernels between libgsr.so and each _diag/libgsr_<tag>.so
+#   mabprof=TAGS     interleaved A/B (two rounds) of the mapping bench's rocprofv3 kernel averages and it/s
+#   seqab=TAGS       interleaved A/B (two rounds) of the bench's sequence leg
 #   abfisher=TAGS    interleaved A/B (two rounds) of the Fisher leg: poses/s and its kernels' rocprofv3 averages
 #   configs          tests/test_gpu_configs.py with -s (per-config parity statistics in configs.log)
 #   drv              the driver's bench command (--steps 20 --warmup 5) and 100/10, interleaved, two rounds
@@ -41,7 +44,7 @@
 TAG=${1:-x}; shift
 ROOT=$(pwd); OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
-LIGHT="--cpu-baseline off --dropin off --fisher off --mapping off --configs off --unfused-leg off --stage-breakdown off"
+LIGHT="--cpu-baseline off --dropin off --fisher off --mapping off --configs off --unfused-leg off --stage-breakdown off --sequence off"
 lib_of() { [ "$1" = base ] && echo "$ROOT/splatam_amd/libgsr.so" || echo "$ROOT/splatam_amd/_diag/libgsr_$1.so"; }
 for s in "$@"; do
   case $s in
@@ -98,6 +101,16 @@ for s in "$@"; do
         ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/squnit_trace" -o run \
             --output-format csv -- python "$ROOT/tools/raster_bench.py" --mode single --iters 40 --warmup 10 \
             > "$OUT/squnit_trace.log" 2>&1 ) || { echo "squnit trace failed"; tail -20 "$OUT/squnit_trace.log"; exit 1; } ;;
+    msq=*) RX=${s#msq=}  # SQ issue / wait counters + FETCH / WRITE of the mapping bench's kernels that RX names
+        G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+        G2="SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM"
+        i=0
+        for G in "$G1" "$G2" FETCH_SIZE WRITE_SIZE; do
+          i=$((i+1))
+          ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $G --kernel-include-regex "$RX" -T \
+              -d "$OUT/msq$i" -o run --output-format csv -- python "$ROOT/bench.py" --workload mapping --steps 5 --warmup 5 \
+              --cpu-baseline off > "$OUT/msq$i.log" 2>&1 ) || { echo "msq pass $i failed"; tail -20 "$OUT/msq$i.log"; exit 1; }
+        done ;;
     sq|sq=*) RX='render_'; [ "$s" != sq ] && RX=${s#sq=}
         G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
         G2="SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
@@ -144,6 +157,36 @@ for row in csv.DictReader(open(f)):
         ks[row["Name"].split("(")[0].split("<")[0].split("::")[-1]] = float(row["AverageNs"]) / 1000
 print("abprof", sys.argv[2], "round", sys.argv[3], " ".join(f"{k} {v:.2f}" for k, v in sorted(ks.items())))
 PY
+           done
+         done ;;
+    mabprof=*) TAGS=${s#mabprof=}  # interleaved A/B (two rounds) of the mapping bench's kernel averages
+         for r in 1 2; do
+           L="base ${TAGS//,/ }"; [ $r = 2 ] && L="$(echo $L | tr ' ' '\n' | tac | tr '\n' ' ')"
+           for t in $L; do
+             d="$OUT/mabprof_${t}_$r"
+             ( cd /tmp && export TMPDIR=/tmp && GSR_LIB_AB=1 GSR_LIB=$(lib_of $t) timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+                 -d "$d" -o run --output-format csv -- python "$ROOT/bench.py" --workload mapping --steps 120 --warmup 60 \
+                 --cpu-baseline off > "$d.log" 2>&1 ) || { echo "mabprof $t failed"; tail -20 "$d.log"; exit 1; }
+             python - "$d" $t $r <<'PY' | tee -a "$OUT/mabprof.txt"
+import csv, glob, json, sys
+f = glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)[0]
+ks = {}
+for row in csv.DictReader(open(f)):
+    if int(row["Calls"]) >= 100:
+        ks[row["Name"].split("(")[0].split("<")[0].split("::")[-1]] = float(row["AverageNs"]) / 1000
+d = json.loads([l for l in open(sys.argv[1] + ".log") if l.startswith("{")][-1])
+print("mabprof", sys.argv[2], "round", sys.argv[3], "it/s", d["value"], " ".join(f"{k} {v:.2f}" for k, v in sorted(ks.items())))
+PY
+           done
+         done ;;
+    seqab=*) TAGS=${s#seqab=}  # interleaved A/B (two rounds) of the sequence leg (config 3 SLAM frames)
+         for r in 1 2; do
+           L="base ${TAGS//,/ }"; [ $r = 2 ] && L="$(echo $L | tr ' ' '\n' | tac | tr '\n' ' ')"
+           for t in $L; do
+             f="$OUT/seqab_${t}_$r.log"
+             GSR_LIB_AB=1 GSR_LIB=$(lib_of $t) timeout -k 10 300 python bench.py $LIGHT --sequence on > "$f" 2>&1 \
+                 || { echo "seqab $t failed"; tail -20 "$f"; exit 1; }
+             python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])['sequence']; print('seqab', sys.argv[2], 'round', sys.argv[3], 'frames/s', d['value'], 'phases', d['phases_ms'], 'per_frame', d['per_frame']['value'])" "$f" $t $r | tee -a "$OUT/seqab.txt"
            done
          done ;;
     abfisher=*) TAGS=${s#abfisher=}
