@@ -1072,9 +1072,9 @@ def run_mapping(args, world, rank, dev):
                          "measurement invalid")
     survivors = int(mapper.survivors().sum().item())
     nr = mapper.num_rendered()
+    mcap, prune_iters = mapper.capacity, sorted(mapper.prune_at)
     stages_all = None
     if args.timing and getattr(args, "stage_breakdown", "on") == "on":  # every stage clocked, one untimed frame
-        mcap = mapper.capacity
         del mapper
         with torch.no_grad():
             for k, v in snap.items():
@@ -1099,13 +1099,13 @@ def run_mapping(args, world, rank, dev):
         "steps": steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "execution": f"HIP graph of {S} mapping iterations (one frame, fresh Adam), replayed "
-                     f"{steps // S}x; binning capacity {mapper.capacity}, no overflow",
-        "pruning": ({"iterations": sorted(mapper.prune_at), "survivors": survivors, "gaussians": P,
+                     f"{steps // S}x; binning capacity {mcap}, no overflow",
+        "pruning": ({"iterations": prune_iters, "survivors": survivors, "gaussians": P,
                      "path": "prune_gaussians inside the frame (scripts/splatam.py:876-878, configs/replica/"
                              "splatam.py:101-111): device alive mask (gsr_map_prune), pruned Gaussians culled by "
                              "the static forward; a pruning iteration is its loss forward only (the reference's "
                              "optimizer.step() updates no Gaussian there: remove_points drops every .grad)"}
-                    if mapper.prune_at else None),
+                    if prune_iters else None),
         "data": f"synthetic (SURVEY.md 8(d) seeded scene; {K} keyframe targets rendered from a perturbed map)",
         "config": {"workload": f"config {args.config}: {P} Gaussians, {W}x{H}, SplaTAM mapping iteration "
                                "(SH colour + depth/silhouette render fwd+bwd, L1 + SSIM + depth L1, Adam on "

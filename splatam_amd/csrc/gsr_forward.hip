@@ -34,7 +34,10 @@ constexpr bool kCullTail = GSR_CULL_TAIL != 0;
 // XF: SplaTAM's tracking transform fused in (g.xf, TrackXf): the camera-frame rendervars are
 // formed here from the world-frame map and the pose, and stored to g's arrays for the backward.
 // CLK: the in-kernel stage clock (a separate instantiation: the production launches carry none of it)
-template <bool LDS_HIST, bool XF, bool CLK>
+// EXACT: the per-workgroup culled-instance counts of the dynamic forward's exact list tail (Camera::tail_exact);
+// a separate instantiation because the bookkeeping, even skipped at run time, cost the static mapping
+// preprocess 45 -> 58 us in code generation (profiles/r9y_ab_preprocess_tail.txt)
+template <bool LDS_HIST, bool XF, bool CLK, bool EXACT>
 __global__ void __launch_bounds__(PRE_BLOCK)
 preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __restrict__ counts, int ntiles,
                   unsigned long long* clk) {
@@ -175,7 +178,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
                                                     : tile_reached(mg, (float)(tx * TILE_X), (float)(ty * TILE_Y)))
                                         ? 1u << k : 0u;
                 }
-                if (kCullTail && cam.tail_exact) culled = culled_below(live, tiles);
+                if constexpr (kCullTail && EXACT) culled = culled_below(live, tiles);
                 geo.bin[i] = make_uint4(rlo, rhi, __float_as_uint(pv.z), live);
                 if (!g.sh_staged && !g.colors) geo.clamp[i] = clamped;  // (read only by the SH backward)
                 for (int ty = y0, k = 0; ty < y1; ty++)  // per-tile instance counts -> bucket ranges
@@ -203,7 +206,7 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t incl = wave_incl_scan(tiles);
     if (lane == 63) wsum[wv] = incl;
-    if (kCullTail && cam.cull && cam.tail_exact) {  // the workgroup's culled instances (the exact tail, duplicate)
+    if constexpr (kCullTail && EXACT) {  // the workgroup's culled instances (the exact tail, duplicate)
         const uint32_t cincl = wave_incl_scan(culled);
         if (lane == 63) wcul[wv] = cincl;
     }
@@ -224,10 +227,11 @@ preprocess_kernel(Camera cam, GaussIn g, GeomPtrs geo, int* radii, uint32_t* __r
     const bool viol = __syncthreads_or(violation);
     if (threadIdx.x == blockDim.x - 1) {
         geo.wgsum[blockIdx.x] = (woff + incl) | (viol ? 0x80000000u : 0u);
-        uint32_t cw = 0;
-        if (kCullTail && cam.cull && cam.tail_exact)
+        if constexpr (kCullTail && EXACT) {
+            uint32_t cw = 0;
             for (int k = 0; k < (int)(blockDim.x >> 6); k++) cw += wcul[k];
-        if (kCullTail) geo.wgcull[blockIdx.x] = cw;
+            geo.wgcull[blockIdx.x] = cw;
+        }
     }
     if (LDS_HIST)
         for (int t = threadIdx.x; t < ntiles; t += blockDim.x) counts[(size_t)blockIdx.x * ntiles + t] = s_hist[t];
@@ -238,10 +242,19 @@ hipError_t launch_preprocess(const Camera& cam, const GaussIn& g, GeomPtrs geo, 
                              bool lds_hist, int ntiles, int nb, hipStream_t s, unsigned long long* clk) {
     if (nb == 0) return hipSuccess;
     const bool xf = g.xf.mw != nullptr;
-    auto k = clk ? (lds_hist ? (xf ? preprocess_kernel<true, true, true> : preprocess_kernel<true, false, true>)
-                             : (xf ? preprocess_kernel<false, true, true> : preprocess_kernel<false, false, true>))
-                 : (lds_hist ? (xf ? preprocess_kernel<true, true, false> : preprocess_kernel<true, false, false>)
-                             : (xf ? preprocess_kernel<false, true, false> : preprocess_kernel<false, false, false>));
+    const bool exact = cam.tail_exact && cam.cull && !xf;  // (the transform-fused form is static-only)
+    auto k = clk ? (lds_hist ? (xf ? preprocess_kernel<true, true, true, false>
+                                   : (exact ? preprocess_kernel<true, false, true, true>
+                                            : preprocess_kernel<true, false, true, false>))
+                             : (xf ? preprocess_kernel<false, true, true, false>
+                                   : (exact ? preprocess_kernel<false, false, true, true>
+                                            : preprocess_kernel<false, false, true, false>)))
+                 : (lds_hist ? (xf ? preprocess_kernel<true, true, false, false>
+                                   : (exact ? preprocess_kernel<true, false, false, true>
+                                            : preprocess_kernel<true, false, false, false>))
+                             : (xf ? preprocess_kernel<false, true, false, false>
+                                   : (exact ? preprocess_kernel<false, false, false, true>
+                                            : preprocess_kernel<false, false, false, false>)));
     hipLaunchKernelGGL(k, dim3(nb), dim3(1 << cam.pre_shift), lds_hist ? sizeof(uint32_t) * ntiles : 0, s, cam, g,
                        geo, radii, counts, ntiles, clk);
     return hipGetLastError();
