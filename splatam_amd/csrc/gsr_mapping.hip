@@ -369,6 +369,9 @@ __global__ void __launch_bounds__(ADAM_BLOCK) adam_step_kernel(AdamArgs a) {
 }
 
 // ---------------------------------------------------- mapping transform bwd --
+#ifndef GSR_NT_GRADS
+#define GSR_NT_GRADS 1  // (config 4: map_transform_bwd 66.5 -> 61.8 us, profiles/r9z_ab_nt_grads.txt)
+#endif
 struct MapAdam {  // the mapping optimizer's state, applied in place (NULL p: write gradients instead)
     float* p[5];          // means3D, unnorm_rotations, logit_opacities, log_scales, colours
     float* m[5];
@@ -446,10 +449,12 @@ map_transform_bwd_kernel(int P, const float* ur, const float* lo, const float* l
     }
     if (i >= P) return;
     const Pose ps = make_pose(cq, nullptr, qs);
-    float g0 = gm ? gm[3 * i] : 0.f, g1 = gm ? gm[3 * i + 1] : 0.f, g2 = gm ? gm[3 * i + 2] : 0.f;
+    // (the incoming gradients and camera-frame means are read once: GSR_NT_GRADS streams them nontemporally)
+    auto ldg = [](const float* q) { return GSR_NT_GRADS ? ld_stream(q) : *q; };
+    float g0 = gm ? ldg(gm + 3 * i) : 0.f, g1 = gm ? ldg(gm + 3 * i + 1) : 0.f, g2 = gm ? ldg(gm + 3 * i + 2) : 0.f;
     if (gd) {  // colours [z, 1, z^2]: dz = dc0 + 2 z dc2
-        const float z = w2c[8] * mc[3 * i] + w2c[9] * mc[3 * i + 1] + w2c[10] * mc[3 * i + 2] + w2c[11];
-        const float dz = gd[3 * i] + 2.f * z * gd[3 * i + 2];
+        const float z = w2c[8] * ldg(mc + 3 * i) + w2c[9] * ldg(mc + 3 * i + 1) + w2c[10] * ldg(mc + 3 * i + 2) + w2c[11];
+        const float dz = ldg(gd + 3 * i) + 2.f * z * ldg(gd + 3 * i + 2);
         g0 += dz * w2c[8]; g1 += dz * w2c[9]; g2 += dz * w2c[10];
     }
     // m = R p + t  ->  dp = R^T g
@@ -460,7 +465,7 @@ map_transform_bwd_kernel(int P, const float* ur, const float* lo, const float* l
     if (gr) {
         float un_norm;
         const float4 u = normalize4(load4(ur + 4 * i), un_norm);
-        float4 d = load4(gr + 4 * i);
+        float4 d = make_float4(ldg(gr + 4 * i), ldg(gr + 4 * i + 1), ldg(gr + 4 * i + 2), ldg(gr + 4 * i + 3));
         if (scols != 1) {  // rot = normalize(o), o = quat_mult(c, u): do -> du = quat_mult(c, .)^T do
             float o_norm;
             const float4 o = quat_mult(ps.c, u);
@@ -477,16 +482,16 @@ map_transform_bwd_kernel(int P, const float* ur, const float* lo, const float* l
     float dl = 0.f;
     if (go) {  // sigmoid backward: g * (1 - y) * y
         const float y = 1.f / (1.f + expf(-lo[i]));
-        dl = go[i] * ((1.f - y) * y);
+        dl = ldg(go + i) * ((1.f - y) * y);
     }
     float dsc[3] = {0.f, 0.f, 0.f};
     if (gs) {  // exp backward: g * exp(x); tile backward sums the three columns
         if (scols == 1) {
             const float e = expf(ls[i]);
-            dsc[0] = gs[3 * i] * e + gs[3 * i + 1] * e + gs[3 * i + 2] * e;
+            dsc[0] = ldg(gs + 3 * i) * e + ldg(gs + 3 * i + 1) * e + ldg(gs + 3 * i + 2) * e;
         } else {
 #pragma unroll
-            for (int k = 0; k < 3; k++) dsc[k] = gs[3 * i + k] * expf(ls[3 * i + k]);
+            for (int k = 0; k < 3; k++) dsc[k] = ldg(gs + 3 * i + k) * expf(ls[3 * i + k]);
         }
     }
     if (!step) {
