@@ -384,16 +384,19 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
                        P > 0 && !sh_staged(cam, g);
     if (reuse && reuse->reused) *reuse->reused = 0;
     Gate eq_gate;
+    uint32_t epoch = 0;
     if (gated) {
-        uint32_t* flag = geo.counters + 5;
-        if ((e = zero_async(flag, sizeof(uint32_t), stream)) != hipSuccess ||
-            (e = launch_bitwise_equal(reuse->pairs, (int*)flag, stream)) != hipSuccess)
+        // the gate word is counters[5] of this call's geometry buffer, not cleared: the comparison stores this
+        // call's epoch there on a difference, and no earlier content can equal the epoch (unique per call)
+        static std::atomic<uint32_t> g_epoch{0};
+        do epoch = g_epoch.fetch_add(1u, std::memory_order_relaxed) + 1u; while (epoch == 0u);
+        uint32_t* word = geo.counters + 5;
+        if ((e = launch_epoch_mismatch(reuse->pairs, word, epoch, stream)) != hipSuccess)
             return hip_fail(e, "geometry comparison");
-        cam.gate = Gate{flag, 1u};  // the full forward runs when the geometry differs ...
-        eq_gate = Gate{flag, 0u};   // ... the reuse form when it is equal
-        if ((e = launch_reuse_copy(eq_gate, reuse->prev_geom, geom, GL.counters, reuse->prev_radii, radii, P, stream)) !=
-                hipSuccess ||
-            (e = launch_recolour(P, g.colors, geo, stream, eq_gate)) != hipSuccess)
+        cam.gate = Gate{word, epoch, 1u};  // the full forward runs when the geometry differs ...
+        eq_gate = Gate{word, epoch, 0u};   // ... the reuse form when it is equal
+        if ((e = launch_reuse_copy(eq_gate, reuse->prev_geom, geom, GL.counters, GL.tiles, g.colors,
+                                   reuse->prev_radii, radii, P, stream)) != hipSuccess)
             return hip_fail(e, "geometry reuse");
     }
     // the bucketed duplicate's workgroup 0 writes the render schedule (tile_plan); the other paths
@@ -541,7 +544,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         return (int)cap;
     }
     if ((e = hipEventSynchronize(pin.ev)) != hipSuccess) return hip_fail(e, "sync num_rendered");
-    if (gated && pin.p[5] == 0u) {  // equal geometry: the reuse form ran (num_rendered is the previous call's)
+    if (gated && pin.p[5] != epoch) {  // equal geometry: the reuse form ran (num_rendered is the previous call's)
         *reuse->reused = 1;
         return reuse->prev_num_rendered;
     }

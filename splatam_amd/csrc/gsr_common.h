@@ -143,12 +143,16 @@ struct BinLayout {        // per-instance state ("binningBuffer")
 };
 
 // ------------------------------------------------------------ parameters --
-// A launch's device-side switch (the gated geometry reuse of gsr_forward_reuse_if_equal): the kernel runs
-// iff (*p != 0) == run; p == nullptr: always runs.  Read once per workgroup, before anything else.
+// A launch's device-side switch (the gated geometry reuse of gsr_forward_reuse_if_equal): the comparison
+// kernel stores the call's epoch e into *p when the geometry differs; the kernel runs iff (*p == e) == run.
+// The word is not cleared first: whatever it held is not e (epochs are unique per call), which reads as
+// "equal" only if the comparison found no difference.  p == nullptr: always runs.  Read once per
+// workgroup, before anything else.
 struct Gate {
     const uint32_t* p = nullptr;
+    uint32_t e = 0;
     uint32_t run = 1;
-    __device__ __forceinline__ bool off() const { return p != nullptr && ((*p != 0u) != (run != 0u)); }
+    __device__ __forceinline__ bool off() const { return p != nullptr && ((*p == e) != (run != 0u)); }
 };
 
 struct Camera {
@@ -1274,9 +1278,12 @@ hipError_t launch_render_track(const Camera& cam, const uint2* ranges, uint64_t*
 int track_records_stride();  // floats per instance record of the tracking render backward (6)
 // geometry reuse (gsr_forward_reuse): the render records' colours replaced by `colors` [P,3]
 hipError_t launch_recolour(int P, const float* colors, GeomPtrs geo, hipStream_t s, Gate gate = Gate{});
-// gated geometry reuse: geom [0, counters) + counters[0..3] and the radii from the previous call
-hipError_t launch_reuse_copy(Gate gate, const void* prev_geom, void* geom, size_t geom_bytes, const int* prev_radii,
-                             int* radii, int P, hipStream_t s);
+// gated geometry reuse: geom [0, counters) + counters[0..3] and the radii from the previous call, the render
+// records' colour quarter replaced by this call's colours (recolour fused into the copy)
+hipError_t launch_reuse_copy(Gate gate, const void* prev_geom, void* geom, size_t geom_bytes, size_t tiles_offset,
+                             const float* colors, const int* prev_radii, int* radii, int P, hipStream_t s);
+// *word = e when any pair differs bitwise (word not cleared: see Gate)
+hipError_t launch_epoch_mismatch(const struct EqualPairs& q, uint32_t* word, uint32_t e, hipStream_t s);
 struct EqualPairs {
     int npairs;
     const float* a[8];

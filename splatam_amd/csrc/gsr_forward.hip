@@ -1269,23 +1269,67 @@ hipError_t launch_recolour(int P, const float* colors, GeomPtrs geo, hipStream_t
 }
 // gsr_forward_reuse_if_equal's copy of the previous call's state (runs only when the gate says "equal"): the
 // geometry buffer up to its counters block plus counters[0..3] (num_rendered, prefiltered flag, longest list,
-// sort cap: counters[4..7] stay this call's -- [5] holds the gate itself) and the radii.  (The image and
-// binning buffers are the previous call's, as in gsr_forward_reuse: the render writes the same final_T /
-// n_contrib into them.)  16-B grid-stride streams (the geometry layout is 256-B aligned).
+// sort cap: counters[4..7] stay this call's -- [5] holds the gate itself) and the radii; the render records'
+// colour quarter (rr[i][2].xyz) of every Gaussian that touches a tile gets this call's colours on the way
+// (recolour_kernel's condition and values, fused into the copy).  (The image and binning buffers are the
+// previous call's, as in gsr_forward_reuse: the render writes the same final_T / n_contrib into them.)
+// 16-B grid-stride streams (the geometry layout is 256-B aligned, the records at offset 0).
 __global__ void __launch_bounds__(256) reuse_copy_kernel(Gate gate, const uint4* __restrict__ pg, uint4* __restrict__ g,
-                                                         size_t ng16, const int* __restrict__ prad, int* __restrict__ rad,
-                                                         int P) {
+                                                         size_t ng16, const uint32_t* __restrict__ ptiles,
+                                                         const float* __restrict__ colors, const int* __restrict__ prad,
+                                                         int* __restrict__ rad, int P) {
     if (gate.off()) return;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (size_t k = t0; k <= ng16; k += stride) g[k] = pg[k];  // (k == ng16: counters[0..3])
+    const size_t nrr = (size_t)RR_F4 * P;
+    for (size_t k = t0; k <= ng16; k += stride) {  // (k == ng16: counters[0..3])
+        uint4 v = pg[k];
+        if (k < nrr && (k % RR_F4) == 2) {
+            const size_t i = k / RR_F4;
+            if (ptiles[i] != 0u) {
+                v.x = __float_as_uint(colors[3 * i]);
+                v.y = __float_as_uint(colors[3 * i + 1]);
+                v.z = __float_as_uint(colors[3 * i + 2]);
+            }
+        }
+        g[k] = v;
+    }
     for (size_t k = t0; k < (size_t)P; k += stride) rad[k] = prad[k];
 }
-hipError_t launch_reuse_copy(Gate gate, const void* prev_geom, void* geom, size_t geom_bytes, const int* prev_radii,
-                             int* radii, int P, hipStream_t s) {
+hipError_t launch_reuse_copy(Gate gate, const void* prev_geom, void* geom, size_t geom_bytes, size_t tiles_offset,
+                             const float* colors, const int* prev_radii, int* radii, int P, hipStream_t s) {
     if (geom_bytes & 15) return hipErrorInvalidValue;
     hipLaunchKernelGGL(reuse_copy_kernel, dim3(2048), dim3(256), 0, s, gate, (const uint4*)prev_geom, (uint4*)geom,
-                       geom_bytes / 16, prev_radii, radii, P);
+                       geom_bytes / 16, (const uint32_t*)((const char*)prev_geom + tiles_offset), colors, prev_radii,
+                       radii, P);
+    return hipGetLastError();
+}
+// *word = e when a[k] and b[k] differ bitwise anywhere (16-B loads where both arrays allow them)
+__global__ void __launch_bounds__(256) epoch_mismatch_kernel(EqualPairs q, uint32_t* word, uint32_t e) {
+    bool diff = false;
+    const long long t0 = (long long)blockIdx.x * blockDim.x + threadIdx.x, stride = (long long)gridDim.x * blockDim.x;
+    for (int k = 0; k < q.npairs; k++) {
+        const float* a = q.a[k];
+        const float* b = q.b[k];
+        long long head = 0;
+        if ((((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15u) == 0)) {
+            const uint4* a4 = reinterpret_cast<const uint4*>(a);
+            const uint4* b4 = reinterpret_cast<const uint4*>(b);
+            const long long n4 = q.n[k] / 4;
+            for (long long i = t0; i < n4; i += stride) {
+                const uint4 x = a4[i], y = b4[i];
+                diff = diff || x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w;
+            }
+            head = 4 * n4;
+        }
+        const uint32_t* au = reinterpret_cast<const uint32_t*>(a);
+        const uint32_t* bu = reinterpret_cast<const uint32_t*>(b);
+        for (long long i = head + t0; i < q.n[k]; i += stride) diff = diff || au[i] != bu[i];
+    }
+    if (__ballot(diff) != 0ull && __lane_id() == 0) atomicExch(word, e);
+}
+hipError_t launch_epoch_mismatch(const EqualPairs& q, uint32_t* word, uint32_t e, hipStream_t s) {
+    hipLaunchKernelGGL(epoch_mismatch_kernel, dim3(1024), dim3(256), 0, s, q, word, e);
     return hipGetLastError();
 }
 // flag |= 1 when a[k][i] != b[k][i] bitwise for any pair k (grid-stride over the pairs' elements)
