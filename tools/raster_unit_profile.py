@@ -93,7 +93,7 @@ def main():
     lines = [f"config {a.config}: unit wall {1e6 * (t2 - t0) / a.n:.1f} us, host (loop, no final sync) "
              f"{1e6 * (t1 - t0) / a.n:.1f} us, device busy {dev_us:.1f} us per unit",
              "host per phase (us/unit): " + ", ".join(f"{k} {1e6 * v / a.n:.1f}" for k, v in acc.items()),
-             f"geometry reuse: {_C.REUSE_STATS}",
+             f"geometry reuse: {_C.reuse_stats()}",
              "device per unit (us, launches):"]
     for k, (us, c) in sorted(kern.items(), key=lambda kv: -kv[1][0]):
         lines.append(f"  {us:8.1f}  x{c:4.1f}  {k[:110]}")
