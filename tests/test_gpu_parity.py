@@ -575,7 +575,8 @@ def _geom_pair(cuda, seed, perturb_second=False, cache=True):
     g1 = torch.as_tensor(rs.randn(3, 120, 160).astype(np.float32), device=cuda)
     g2 = torch.as_tensor(rs.randn(3, 120, 160).astype(np.float32), device=cuda)
     old = _C._GEOM_CACHE
-    _C.set_geom_cache(cache)
+    if cache is not None:  # (None: leave the current setting -- callers on several threads)
+        _C.set_geom_cache(cache)
     try:
         m3 = scene.means3D.to(cuda).requires_grad_(True)
         u_rot = scene.rotations.to(cuda).requires_grad_(True)
@@ -598,7 +599,8 @@ def _geom_pair(cuda, seed, perturb_second=False, cache=True):
         res += [t.grad.cpu() for t in (m3, u_rot, lo, ls, col)]
         return res
     finally:
-        _C.set_geom_cache(old)
+        if cache is not None:
+            _C.set_geom_cache(old)
 
 
 @pytest.mark.parametrize("native", [True, False])
@@ -629,6 +631,44 @@ def test_geometry_reuse_refused_on_changed_geometry(cuda, native):
         b = _geom_pair(cuda, 43, perturb_second=True, cache=False)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+def test_geometry_reuse_concurrent_threads(cuda):
+    """Two threads, each on its own stream, running RGB / depth pairs with the reuse on: every image, radius
+    and gradient bitwise that of the same pair with the reuse off (the gate word lives in each call's own
+    geometry buffer, the previous-call state is per thread)."""
+    import threading
+    from splatam_amd import _C
+    seeds = [(61, 62), (63, 64)]
+    ref = {sd: _geom_pair(cuda, sd, cache=False) for pair in seeds for sd in pair}
+    old = _C._GEOM_CACHE
+    _C.set_geom_cache(True)
+    hits = _C.reuse_stats()["hits"]
+    out, errs = {}, []
+
+    def worker(pair):
+        try:
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                for sd in pair:
+                    out[sd] = _geom_pair(cuda, sd, cache=None)
+            st.synchronize()
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(e)
+
+    try:
+        th = [threading.Thread(target=worker, args=(pair,)) for pair in seeds]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+    finally:
+        _C.set_geom_cache(old)
+    assert not errs, errs
+    assert _C.reuse_stats()["hits"] >= hits + 4, _C.reuse_stats()
+    for sd, r in ref.items():
+        for x, y in zip(out[sd], r):
+            assert torch.equal(x, y), sd
 
 
 @contextlib.contextmanager
