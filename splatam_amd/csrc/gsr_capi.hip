@@ -310,6 +310,21 @@ struct ReuseIn {
     int* reused;
 };
 
+// the reuse form's render: the previous call's sorted lists (no sort), ranges, schedule and image buffer (its
+// final_T / n_contrib rewritten with the same values), this call's records (the copied geometry)
+static hipError_t launch_reuse_render(const Camera& cam, Gate gate, const ImgLayout& IL, const ReuseIn* reuse,
+                                      const GeomPtrs& geo, float* out_color, float* out_depth, hipStream_t stream) {
+    Camera cr = cam;
+    cr.gate = gate;
+    char* pib = (char*)reuse->prev_image;
+    cr.tile_order = (const uint32_t*)(pib + IL.order);
+    cr.rowmax = (uint32_t*)(pib + IL.rowmax);
+    const SpecGuard rg{geo.counters, (uint32_t)reuse->prev_num_rendered, 0xFFFFFFFFu};
+    return launch_render_fwd(cr, (const uint2*)(pib + IL.ranges), (uint64_t*)reuse->prev_binning, nullptr, geo,
+                             nullptr, (float*)(pib + IL.final_T), (uint32_t*)(pib + IL.n_contrib), out_color, nullptr,
+                             out_depth, rg, stream);
+}
+
 // colors2 != NULL: dual render (second colour set composited in the same pass, out_color2)
 // capacity > 0: static mode -- binning buffer of `capacity` instances, no host
 // synchronisation at all (graph-capturable); the device counters are copied to
@@ -377,17 +392,39 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     // tile culling: a per-call choice (gsr_settings.binning), no process-wide mode
     cam.cull = (GSR_TILE_CULL && settings->binning != GSR_BINNING_REFERENCE) ? 1 : 0;
     cam.tail_exact = capacity <= 0 ? 1 : 0;  // (include/gsr.h: the culled instances, or padding in static mode)
+    auto snapshot_counters = [&]() -> int {  // num_rendered & co. to pinned host memory (eager mode)
+        if (!pin.p) {
+            if ((e = hipHostMalloc((void**)&pin.p, 32, hipHostMallocDefault)) != hipSuccess)
+                return hip_fail(e, "hipHostMalloc");
+        }
+        if (!pin.ev) {  // created on the stream's device (the caller's current device is that device)
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            if (cur != dev) (void)hipSetDevice(dev);
+            e = hipEventCreateWithFlags(&pin.ev, hipEventDisableTiming);
+            if (cur != dev) (void)hipSetDevice(cur);
+            if (e != hipSuccess) return hip_fail(e, "hipEventCreate");
+        }
+        if ((e = hipMemcpyAsync(pin.p, geo.counters, 32, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+            return hip_fail(e, "copy num_rendered");
+        if ((e = hipEventRecord(pin.ev, stream)) != hipSuccess) return hip_fail(e, "record num_rendered");
+        return GSR_OK;
+    };
     // gated geometry reuse (gsr_forward_reuse_if_equal): the device compares this call's geometry with the
     // previous call's, both forms are enqueued with every launch gated on the result (counters[5]), and the
-    // host learns which one ran from the counter copy it waits on anyway -- no second synchronisation
-    const bool gated = reuse && capacity <= 0 && !colors2 && !track_inst && !l1 && !xf && lds_hist && !force_radix &&
-                       P > 0 && !sh_staged(cam, g);
+    // host learns which one ran from the counter copy it waits on anyway -- no second synchronisation.  (A
+    // speculative form -- the reuse enqueued unconditionally, the host waiting on the comparison right after
+    // it, the full forward only on a difference -- measured slower on the unchanged caller: its early wait
+    // stalls the host before the call's render is enqueued, profiles/r10i_unit_reuse_forms.txt)
+    const bool can_reuse = reuse && capacity <= 0 && !colors2 && !track_inst && !l1 && !xf && lds_hist &&
+                           !force_radix && P > 0 && !sh_staged(cam, g);
+    const bool gated = can_reuse;
     if (reuse && reuse->reused) *reuse->reused = 0;
     Gate eq_gate;
     uint32_t epoch = 0;
     if (gated) {
-        // the gate word is counters[5] of this call's geometry buffer, not cleared: the comparison stores this
-        // call's epoch there on a difference, and no earlier content can equal the epoch (unique per call)
+        // the comparison word is counters[5] of this call's geometry buffer, not cleared: the comparison stores
+        // this call's epoch there on a difference, and no earlier content can equal the epoch (unique per call)
         static std::atomic<uint32_t> g_epoch{0};
         do epoch = g_epoch.fetch_add(1u, std::memory_order_relaxed) + 1u; while (epoch == 0u);
         uint32_t* word = geo.counters + 5;
@@ -408,24 +445,6 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     // the bucketed duplicate does the instance / tile scans itself (lds_hist); otherwise a
     // scan launch does them, and the counters are final right after it
     const bool scan_in_duplicate = lds_hist && !force_radix;
-    auto snapshot_counters = [&]() -> int {  // num_rendered & co. to pinned host memory (eager mode)
-        if (!pin.p) {
-            if ((e = hipHostMalloc((void**)&pin.p, 32, hipHostMallocDefault)) != hipSuccess)
-                return hip_fail(e, "hipHostMalloc");
-        }
-        if (!pin.ev) {  // created on the stream's device (the caller's current device is that device)
-            int cur = 0;
-            (void)hipGetDevice(&cur);
-            if (cur != dev) (void)hipSetDevice(dev);
-            e = hipEventCreateWithFlags(&pin.ev, hipEventDisableTiming);
-            if (cur != dev) (void)hipSetDevice(cur);
-            if (e != hipSuccess) return hip_fail(e, "hipEventCreate");
-        }
-        if ((e = hipMemcpyAsync(pin.p, geo.counters, gated ? 32 : 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-            return hip_fail(e, "copy num_rendered");
-        if ((e = hipEventRecord(pin.ev, stream)) != hipSuccess) return hip_fail(e, "record num_rendered");
-        return GSR_OK;
-    };
     if (P > 0) {
         if (!radii) return fail(GSR_ERR_INVALID_ARG, "radii output required");
         {
@@ -527,15 +546,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
                 return hip_fail(e, "render");
         }
         if (gated) {  // the reuse form's render: the previous call's sorted lists (no sort) and image buffer
-            Camera cr = cam;
-            cr.gate = eq_gate;
-            char* pib = (char*)reuse->prev_image;
-            cr.tile_order = (const uint32_t*)(pib + IL.order);
-            cr.rowmax = (uint32_t*)(pib + IL.rowmax);
-            const SpecGuard rg{geo.counters, (uint32_t)reuse->prev_num_rendered, 0xFFFFFFFFu};
-            if ((e = launch_render_fwd(cr, (const uint2*)(pib + IL.ranges), (uint64_t*)reuse->prev_binning, nullptr,
-                                       geo, nullptr, (float*)(pib + IL.final_T), (uint32_t*)(pib + IL.n_contrib),
-                                       out_color, nullptr, out_depth, rg, stream)) != hipSuccess)
+            if ((e = launch_reuse_render(cam, eq_gate, IL, reuse, geo, out_color, out_depth, stream)) != hipSuccess)
                 return hip_fail(e, "render (geometry reuse)");
         }
         speculated = true;
