@@ -42,7 +42,8 @@ int hip_fail(hipError_t e, const char* where) {
 namespace {
 
 struct Pinned {  // per-thread staging of the device counters + the event after the scan
-    uint32_t* p = nullptr;
+    uint32_t* p = nullptr;   // (mapped, coherent: the bucketed duplicate stores into it, Camera::host_snap)
+    uint32_t* dp = nullptr;  // its device address
     hipEvent_t ev = nullptr;
     ~Pinned() {
         if (p) (void)hipHostFree(p);
@@ -71,6 +72,8 @@ int current_device() {
     return d;
 }
 thread_local Pinned g_pinned[kMaxDevices];
+// GSR_SNAP_COPY=1: the counters reach the host by a copy launched after the duplicate (A/B switch of Camera::host_snap)
+const bool g_snap_copy = getenv("GSR_SNAP_COPY") && atoi(getenv("GSR_SNAP_COPY")) != 0;
 struct RatioHint {
     std::atomic<double> v{3.0};  // last num_rendered / P (binning capacity hint)
 };
@@ -392,10 +395,12 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     // tile culling: a per-call choice (gsr_settings.binning), no process-wide mode
     cam.cull = (GSR_TILE_CULL && settings->binning != GSR_BINNING_REFERENCE) ? 1 : 0;
     cam.tail_exact = capacity <= 0 ? 1 : 0;  // (include/gsr.h: the culled instances, or padding in static mode)
-    auto snapshot_counters = [&]() -> int {  // num_rendered & co. to pinned host memory (eager mode)
+    auto ensure_pinned = [&]() -> int {
         if (!pin.p) {
-            if ((e = hipHostMalloc((void**)&pin.p, 32, hipHostMallocDefault)) != hipSuccess)
+            if ((e = hipHostMalloc((void**)&pin.p, 32, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
                 return hip_fail(e, "hipHostMalloc");
+            if ((e = hipHostGetDevicePointer((void**)&pin.dp, pin.p, 0)) != hipSuccess)
+                return hip_fail(e, "hipHostGetDevicePointer");
         }
         if (!pin.ev) {  // created on the stream's device (the caller's current device is that device)
             int cur = 0;
@@ -405,7 +410,14 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
             if (cur != dev) (void)hipSetDevice(cur);
             if (e != hipSuccess) return hip_fail(e, "hipEventCreate");
         }
-        if ((e = hipMemcpyAsync(pin.p, geo.counters, 32, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+        return GSR_OK;
+    };
+    // num_rendered & co. to pinned host memory (eager mode): copied here, or (stored_by_kernel) already stored by
+    // the launch just enqueued (Camera::host_snap)
+    auto snapshot_counters = [&](bool stored_by_kernel) -> int {
+        if (int r = ensure_pinned(); r != GSR_OK) return r;
+        if (!stored_by_kernel &&
+            (e = hipMemcpyAsync(pin.p, geo.counters, 32, hipMemcpyDeviceToHost, stream)) != hipSuccess)
             return hip_fail(e, "copy num_rendered");
         if ((e = hipEventRecord(pin.ev, stream)) != hipSuccess) return hip_fail(e, "record num_rendered");
         return GSR_OK;
@@ -471,7 +483,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
                 return hip_fail(e, "scan");
             }
         }
-        if (capacity <= 0 && !scan_in_duplicate && (rc = snapshot_counters()) != GSR_OK) return rc;
+        if (capacity <= 0 && !scan_in_duplicate && (rc = snapshot_counters(false)) != GSR_OK) return rc;
     } else {
         if ((e = zero_async(ranges, sizeof(uint2) * (size_t)ntiles, stream)) != hipSuccess)
             return hip_fail(e, "memset ranges");
@@ -522,6 +534,11 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
         if (!bin) return fail(GSR_ERR_ALLOC, "allocator returned NULL (binning buffer)");
         bin_ptrs(bin, SL, keys, vals, gid, point_list, hist);
         const SpecGuard guard{geo.counters, cap, (uint32_t)TILE_SORT_CAP};
+        const bool dup_snap = capacity <= 0 && scan_in_duplicate && !g_snap_copy;
+        if (dup_snap) {
+            if ((rc = ensure_pinned()) != GSR_OK) return rc;
+            cplan.host_snap = pin.dp;
+        }
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream, true);
             if ((e = launch_duplicate_bucket(cplan, P, geo, ranges, tile_tot, lds_hist ? cmat : cursor, lds_hist,
@@ -530,7 +547,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
                                              stream, t.kclock())) != hipSuccess)
                 return hip_fail(e, "duplicate");
         }
-        if (capacity <= 0 && scan_in_duplicate && (rc = snapshot_counters()) != GSR_OK) return rc;
+        if (capacity <= 0 && scan_in_duplicate && (rc = snapshot_counters(dup_snap)) != GSR_OK) return rc;
         if (track_inst) {  // forward + L1 + the tracking render backward, one launch (render_track_kernel)
             StageTimer t(GSR_STAGE_RENDER_FWD, 0, stream, true);
             if ((e = launch_render_track(cam, ranges, point_list, keys[0], geo, no_images ? nullptr : final_T,

@@ -187,6 +187,10 @@ struct Camera {
     // forward, whose buffers the caller reads like the reference's), 0 padding ids (static mode)
     int tail_exact = 0;
     Gate gate;  // (preprocess, duplicate_bucket and render_fwd return at once when it is off)
+    // Host snapshot (the dynamic forward's bucketed binning only): the duplicate's workgroup 0 stores counters[0..7]
+    // into this mapped, coherent pinned host buffer once they are final -- in place of a 32-B device-to-host copy
+    // launched behind it (4 us of the stream per forward) -- and the host's event follows the duplicate
+    uint32_t* host_snap = nullptr;
 };
 // bin[i].w: bit k set = rect tile k (row-major in the rect) has an instance in its bucket; all ones when
 // nothing is culled (or the rect has more than 32 tiles)

@@ -700,6 +700,19 @@ constexpr int DUP_T = 512;
 #ifndef GSR_NO_PLAN
 #define GSR_NO_PLAN 0  // timing experiment: row-major render order instead of tile_plan
 #endif
+// the snapshot the host reads after the duplicate (Camera::host_snap): two 16-B vector stores to the coherent
+// pinned buffer, made visible to the host by the kernel's end-of-kernel release
+__device__ __forceinline__ void store_host_snap(uint32_t* snap, uint4 lo, uint4 hi) {
+    reinterpret_cast<uint4*>(snap)[0] = lo;
+    reinterpret_cast<uint4*>(snap)[1] = hi;
+}
+// gated geometry reuse, equal geometry: the duplicate is skipped, and its workgroup 0 hands the counters the reuse
+// copy wrote (the previous call's [0..3], this call's [4..7]) to the host instead
+__device__ __forceinline__ void dup_gate_off_snap(const Camera& cam, const GeomPtrs& geo) {
+    if (cam.host_snap && blockIdx.x == 0 && threadIdx.x == 0)
+        store_host_snap(cam.host_snap, *reinterpret_cast<const uint4*>(geo.counters),
+                        *reinterpret_cast<const uint4*>(geo.counters + 4));
+}
 template <bool LDS_HIST, int DUP_G, bool EXACT>
 __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ranges,
                                                       const uint32_t* __restrict__ tot, uint32_t* __restrict__ cursor,
@@ -849,6 +862,9 @@ __device__ __forceinline__ void duplicate_bucket_body(Camera cam, int P, GeomPtr
                 geo.counters[2] = vmax;
                 geo.counters[3] = sort_cap;
                 if (status) status_merge(status, all, viol, vmax, sort_cap);
+                if (cam.host_snap)  // (Camera::host_snap; [4..7] were final before this launch)
+                    store_host_snap(cam.host_snap, make_uint4(all, viol, vmax, sort_cap),
+                                    *reinterpret_cast<const uint4*>(geo.counters + 4));
             }
         }
         if (b == 0 && cam.tile_order_out) {
@@ -994,7 +1010,10 @@ duplicate_bucket_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict__ ran
                         uint64_t* __restrict__ point_list, SpecGuard guard, uint32_t sort_cap,
                         uint32_t* __restrict__ status, unsigned long long* clk) {
     extern __shared__ uint32_t s_cur[];
-    if (cam.gate.off()) return;
+    if (cam.gate.off()) {
+        dup_gate_off_snap(cam, geo);
+        return;
+    }
     if constexpr (CLK) kclock_begin(clk);
     duplicate_bucket_body<LDS_HIST, DUP_G, EXACT>(cam, P, geo, ranges, tot, cursor, ntiles, keys, point_list, guard,
                                                   sort_cap, status, s_cur);
@@ -1012,7 +1031,10 @@ duplicate_bucket_exact_kernel(Camera cam, int P, GeomPtrs geo, uint2* __restrict
                               uint64_t* __restrict__ keys, uint64_t* __restrict__ point_list, SpecGuard guard,
                               uint32_t sort_cap, uint32_t* __restrict__ status, unsigned long long* clk) {
     extern __shared__ uint32_t s_cur[];
-    if (cam.gate.off()) return;
+    if (cam.gate.off()) {
+        dup_gate_off_snap(cam, geo);
+        return;
+    }
     if constexpr (CLK) kclock_begin(clk);
     duplicate_bucket_body<LDS_HIST, DUP_G, true>(cam, P, geo, ranges, tot, cursor, ntiles, keys, point_list, guard,
                                                  sort_cap, status, s_cur);

@@ -56,6 +56,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.backward_power = backward_power
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
                               binningBuffer, imgBuffer)
+        # the gradients of radii and depth are ignored: no zero tensors materialised for them (two fill
+        # launches per call otherwise); the depth output keeps requires_grad, as the reference's does
+        ctx.set_materialize_grads(False)
         return color, radii, depth
 
     @staticmethod
@@ -63,6 +66,8 @@ class _RasterizeGaussians(torch.autograd.Function):
         s = ctx.raster_settings
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer,
          imgBuffer) = ctx.saved_tensors
+        if grad_out_color is None:  # (a loss that reads only the depth output: what materialisation gave)
+            grad_out_color = torch.zeros(3, s.image_height, s.image_width, device=means3D.device)
         # inputs: (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, ...);
         # outputs of the binding: (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drotations)
         n = ctx.needs_input_grad

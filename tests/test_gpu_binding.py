@@ -64,3 +64,33 @@ def test_native_binding_errors_and_empty(cuda):
     n, color, radii, geom, binning, img, depth = nat.rasterize_gaussians(
         *args(torch.zeros(0, 3, device=dev), torch.zeros(0, 3, device=dev)))
     assert n == 0 and color.shape == (3, 32, 32) and float(color.abs().sum()) == 0 and radii.numel() == 0
+
+
+def test_dropin_depth_only_loss(cuda):
+    """The drop-in Function does not materialise the ignored radii / depth gradients; a loss that reads only
+    the depth output (whose gradient the reference ignores, __init__.py:92) still back-propagates, with the
+    gradients a zero colour gradient gives, and depth keeps requires_grad as in the reference."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    dev = torch.device(cuda)
+    scene = make_scene(3000, 96, 72, seed=12)
+    c = scene.cam
+    st = GaussianRasterizationSettings(image_height=c.H, image_width=c.W, tanfovx=c.tanfovx, tanfovy=c.tanfovy,
+                                       bg=torch.zeros(3, device=dev), scale_modifier=1.0,
+                                       viewmatrix=c.viewmatrix.to(dev), projmatrix=c.projmatrix.to(dev), sh_degree=0,
+                                       campos=c.campos.to(dev), prefiltered=False)
+
+    def run(depth_only):
+        leaf = {k: getattr(scene, k).to(dev).requires_grad_(True)
+                for k in ("means3D", "colors", "opacities", "scales", "rotations")}
+        m2 = torch.zeros_like(leaf["means3D"], requires_grad=True)
+        im, radii, depth = GaussianRasterizer(st)(means3D=leaf["means3D"], means2D=m2, colors_precomp=leaf["colors"],
+                                                  opacities=leaf["opacities"], scales=leaf["scales"],
+                                                  rotations=leaf["rotations"])
+        assert depth.requires_grad and not radii.requires_grad
+        (depth.sum() if depth_only else im.sum() * 0.0 + depth.sum()).backward()
+        return {k: v.grad for k, v in leaf.items()} | {"means2D": m2.grad}
+
+    a, b = run(True), run(False)
+    for k in a:
+        assert a[k] is not None and torch.equal(a[k], b[k]), k
+        assert float(a[k].abs().sum()) == 0.0, k
