@@ -595,6 +595,7 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     bin_ptrs(bin, BL, keys, vals, gid, point_list, hist);
     const SpecGuard none{geo.counters, 0xffffffffu, 0xffffffffu};
     const bool tile_sorted = I > 0 && longest <= (uint32_t)TILE_SORT_CAP && !force_radix;
+    cplan.host_snap = nullptr;  // (the host has read this call's counters: nothing may store into them later)
     if (tile_sorted) {
         {
             StageTimer t(GSR_STAGE_DUPLICATE, P, stream, true);

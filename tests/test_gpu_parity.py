@@ -683,3 +683,35 @@ def _binding(native):
         yield
     finally:
         _C._NATIVE_ON = old
+
+
+def test_speculation_overflow_relaunch(cuda):
+    """The dynamic forward sizes its binning from the last calls' instances per Gaussian and enqueues the
+    render before it knows num_rendered; a call with far more instances per Gaussian than the last overflows
+    that capacity and re-runs the duplicate and render at the exact size.  That re-launch gives bitwise the
+    outputs of the same call made once the size hint has caught up, and the counters the host reads (after
+    the duplicate stored them into the pinned snapshot) are this call's."""
+    from splatam_amd import _C
+    dev = torch.device(cuda)
+    e = torch.Tensor([])
+    small = make_scene(20000, 320, 240, seed=5)
+    big = make_scene(20000, 320, 240, seed=6)
+    big.scales = big.scales * 6.0  # many more tiles per Gaussian than the small scene's
+
+    def call(s):
+        c = s.cam
+        out = _C.rasterize_gaussians(torch.zeros(3, device=dev), s.means3D.to(dev), s.colors.to(dev),
+                                     s.opacities.to(dev), s.scales.to(dev), s.rotations.to(dev), 1.0, e,
+                                     c.viewmatrix.to(dev), c.projmatrix.to(dev), c.tanfovx, c.tanfovy, c.H, c.W, e, 0,
+                                     c.campos.to(dev), False)
+        torch.cuda.synchronize()
+        return out[0], out[1].cpu(), out[2].cpu(), out[6].cpu()
+
+    n_small = call(small)[0]
+    for _ in range(3):
+        call(small)  # the hint: the small scene's instances per Gaussian
+    first = call(big)  # beyond 1.5x that hint: the re-launch
+    again = call(big)  # the hint now matches
+    assert first[0] == again[0] and first[0] > 1.5 * n_small * 1.2, (first[0], n_small)
+    for a, b in zip(first[1:], again[1:]):
+        assert torch.equal(a, b)
