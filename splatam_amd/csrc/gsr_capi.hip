@@ -289,6 +289,7 @@ void timing_drain(Timing& T) {  // caller holds g_timing_mu
 
 namespace gsr {
 int geom_pre_shift(int P) { return pre_shift_for(P, device_cus(current_device())); }
+int current_device_cus() { return device_cus(current_device()); }
 }  // namespace gsr
 
 extern "C" {

@@ -25,6 +25,7 @@ constexpr int TILE_PIX = TILE_X * TILE_Y;
 constexpr int PRE_BLOCK = 1024;  // the largest row (workgroup size bound, LDS arrays)
 __host__ __device__ inline int pre_shift_for(int P, int cus) { return ((P + 1023) >> 10) < 2 * cus ? 9 : 10; }
 int geom_pre_shift(int P);  // pre_shift_for(P, CU count of the current device) (gsr_capi.hip)
+int current_device_cus();   // the current device's CU count (gsr_capi.hip)
 constexpr int MAX_LDS_TILES = 16384; // tile histogram in LDS up to 64 KB; global atomics beyond
 constexpr int SORT_THREADS = 256;
 constexpr int SORT_ITEMS = 8;        // keys per thread per radix pass

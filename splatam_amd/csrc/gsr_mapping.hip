@@ -79,9 +79,10 @@ __device__ __forceinline__ float sgn(float x) { return x > 0.f ? 1.f : (x < 0.f 
 // zero outside the image (conv2d zero padding).
 // Every load of the thread's elements is issued before the first LDS store: a load-then-store
 // loop waits one HBM round trip per element (the halo phase set the kernels' time).
-template <int NM>
-__device__ __forceinline__ void load_halo(float (*dst)[SS_IH][SS_IW], const float* const (&src)[NM], int H, int W,
-                                          int x0, int y0) {
+template <int TH, int NM>
+__device__ __forceinline__ void load_halo(float (*dst)[TH + 2 * SS_R][SS_IW], const float* const (&src)[NM], int H,
+                                          int W, int x0, int y0) {
+    constexpr int SS_IH = TH + 2 * SS_R;
     constexpr int NE = (SS_IH * SS_IW + SS_BLOCK - 1) / SS_BLOCK;
     float v[NE][NM];
 #pragma unroll
@@ -106,9 +107,10 @@ __device__ __forceinline__ void load_halo(float (*dst)[SS_IH][SS_IW], const floa
 
 // Separable window: horizontal pass over the halo rows into hs, then each
 // thread forms the vertical pass for SS_ROWS_PER_THREAD output rows of one column.
-template <int NI, int NO, typename F>
-__device__ __forceinline__ void horizontal_pass(const float (*src)[SS_IH][SS_IW], float (*hs)[SS_IH][SS_TW],
-                                                const Window& win, F moments) {
+template <int TH, int NI, int NO, typename F>
+__device__ __forceinline__ void horizontal_pass(const float (*src)[TH + 2 * SS_R][SS_IW],
+                                                float (*hs)[TH + 2 * SS_R][SS_TW], const Window& win, F moments) {
+    constexpr int SS_IH = TH + 2 * SS_R;
     for (int e = threadIdx.x; e < SS_IH * SS_TW; e += SS_BLOCK) {
         const int r = e / SS_TW, cc = e - r * SS_TW;
         float acc[NO];
@@ -129,9 +131,10 @@ __device__ __forceinline__ void horizontal_pass(const float (*src)[SS_IH][SS_IW]
     }
 }
 
-template <int NO>
-__device__ __forceinline__ void vertical_pass(const float (*hs)[SS_IH][SS_TW], const Window& win, int col, int r0,
-                                              float (&out)[SS_ROWS_PER_THREAD][NO]) {
+template <int TH, int NO>
+__device__ __forceinline__ void vertical_pass(const float (*hs)[TH + 2 * SS_R][SS_TW], const Window& win, int col,
+                                              int r0, float (&out)[TH / (SS_BLOCK / SS_TW)][NO]) {
+    constexpr int SS_ROWS_PER_THREAD = TH / (SS_BLOCK / SS_TW);
 #pragma unroll
     for (int j = 0; j < SS_ROWS_PER_THREAD; j++)
 #pragma unroll
@@ -153,11 +156,13 @@ __device__ __forceinline__ void vertical_pass(const float (*hs)[SS_IH][SS_TW], c
 
 // gmap: 3 partial maps x 3 channels x HW floats; part: MAP_PARTS * nblocks
 // partials then the arrival counters; out: [0] depth mask count (read by the backward).
+template <int TH>
 __global__ void __launch_bounds__(SS_BLOCK)
 map_loss_fwd_kernel(int H, int W, const float* __restrict__ im, const float* __restrict__ ds,
                     const float* __restrict__ gt_im, const float* __restrict__ gt_d, float w_im, float w_depth,
                     Window win, float* __restrict__ gmap, float* __restrict__ part, float* __restrict__ out,
                     float* __restrict__ loss) {
+    constexpr int SS_TH = TH, SS_IH = TH + 2 * SS_R, SS_ROWS_PER_THREAD = TH / (SS_BLOCK / SS_TW);
     __shared__ float s_in[2][SS_IH][SS_IW];
     __shared__ float s_h[5][SS_IH][SS_TW];
     __shared__ float s_red[4 * MAP_PARTS];
@@ -181,14 +186,14 @@ map_loss_fwd_kernel(int H, int W, const float* __restrict__ im, const float* __r
             pgd[j] = gt_d[pid];
         }
     }
-    load_halo<2>(s_in, src, H, W, x0, y0);
+    load_halo<TH, 2>(s_in, src, H, W, x0, y0);
     __syncthreads();
-    horizontal_pass<2, 5>(s_in, s_h, win, [](const float (&i)[2], float (&o)[5]) {
+    horizontal_pass<TH, 2, 5>(s_in, s_h, win, [](const float (&i)[2], float (&o)[5]) {
         o[0] = i[0]; o[1] = i[1]; o[2] = i[0] * i[0]; o[3] = i[1] * i[1]; o[4] = i[0] * i[1];
     });
     __syncthreads();
     float mo[SS_ROWS_PER_THREAD][5];
-    vertical_pass<5>(s_h, win, col, r0, mo);
+    vertical_pass<TH, 5>(s_h, win, col, r0, mo);
     float v[MAP_PARTS] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < SS_ROWS_PER_THREAD; j++) {
@@ -239,11 +244,13 @@ map_loss_fwd_kernel(int H, int W, const float* __restrict__ im, const float* __r
     }
 }
 
+template <int TH>
 __global__ void __launch_bounds__(SS_BLOCK)
 map_loss_bwd_kernel(int H, int W, const float* __restrict__ im, const float* __restrict__ ds,
                     const float* __restrict__ gt_im, const float* __restrict__ gt_d, float w_im, float w_depth,
                     Window win, const float* __restrict__ gmap, const float* __restrict__ fwd_out,
                     const float* __restrict__ dloss, float* __restrict__ dim, float* __restrict__ dds) {
+    constexpr int SS_TH = TH, SS_IH = TH + 2 * SS_R, SS_ROWS_PER_THREAD = TH / (SS_BLOCK / SS_TW);
     __shared__ float s_in[3][SS_IH][SS_IW];
     __shared__ float s_h[3][SS_IH][SS_TW];
     const int HW = H * W, c = blockIdx.z;
@@ -270,14 +277,14 @@ map_loss_bwd_kernel(int H, int W, const float* __restrict__ im, const float* __r
             }
         }
     }
-    load_halo<3>(s_in, src, H, W, x0, y0);
+    load_halo<TH, 3>(s_in, src, H, W, x0, y0);
     __syncthreads();
-    horizontal_pass<3, 3>(s_in, s_h, win, [](const float (&i)[3], float (&o)[3]) {
+    horizontal_pass<TH, 3, 3>(s_in, s_h, win, [](const float (&i)[3], float (&o)[3]) {
         o[0] = i[0]; o[1] = i[1]; o[2] = i[2];
     });
     __syncthreads();
     float bl[SS_ROWS_PER_THREAD][3];
-    vertical_pass<3>(s_h, win, col, r0, bl);
+    vertical_pass<TH, 3>(s_h, win, col, r0, bl);
     const float g = dloss[0];
     const float n = 3.f * (float)HW;
     const float g_ssim = g * w_im * (-0.2f / n);  // d/dS of w_im * 0.2 * (1 - mean(S))
@@ -566,8 +573,18 @@ map_transform_bwd_kernel(int P, const float* ur, const float* lo, const float* l
     }
 }
 
-int map_loss_blocks(int H, int W, dim3& grid) {
-    grid = dim3((W + SS_TW - 1) / SS_TW, (H + SS_TH - 1) / SS_TH, 3);
+// The SSIM tile height: 16 rows (3 workgroups per CU by their LDS), or 32 (2 per CU) when that takes the frame's
+// tiles into one dispatch round and 16 rows would not -- config 3's 640x480: 900 -> 450 workgroups on 256 CUs
+// (mapping 14.68 -> 14.45-14.50 ms per 60-iteration frame, profiles/r10q_seq_ssim_rows.txt); at 1200x680 the
+// 32-row tiles measured slower (GSR_SS_TH timing builds)
+int map_loss_rows(int H, int W) {
+    if (SS_TH != 16) return SS_TH;  // (a timing build's fixed height)
+    const long cols = (W + SS_TW - 1) / SS_TW, cus = current_device_cus();
+    const long b16 = 3 * cols * ((H + 15) / 16), b32 = 3 * cols * ((H + 31) / 32);
+    return (b16 > 3 * cus && b32 <= 2 * cus) ? 32 : 16;
+}
+int map_loss_blocks(int H, int W, dim3& grid, int rows) {
+    grid = dim3((W + SS_TW - 1) / SS_TW, (H + rows - 1) / rows, 3);
     return (int)(grid.x * grid.y * grid.z);
 }
 
@@ -610,8 +627,8 @@ using namespace gsr;
 extern "C" {
 
 int gsr_map_loss_scratch_floats(int H, int W) {
-    dim3 grid;
-    return MAP_PARTS * map_loss_blocks(H, W, grid) + ARRIVE_GROUPED_WORDS;
+    dim3 grid;  // (sized for the smaller row count: at least as many workgroups as the height chosen)
+    return MAP_PARTS * map_loss_blocks(H, W, grid, std::min(SS_TH, 16)) + ARRIVE_GROUPED_WORDS;
 }
 
 int gsr_map_loss_state_floats(int H, int W) { return 9 * H * W + 4; }
@@ -622,9 +639,10 @@ int gsr_map_loss_fwd(int H, int W, const float* im, const float* depth_sil, cons
     if (!im || !depth_sil || !gt_im || !gt_depth || !loss || !state || !scratch)
         return fail(GSR_ERR_INVALID_ARG, "map_loss_fwd: null pointer");
     dim3 grid;
-    map_loss_blocks(H, W, grid);
+    const int rows = map_loss_rows(H, W);
+    map_loss_blocks(H, W, grid, rows);
     float* out = state + 9 * (size_t)H * W;
-    hipLaunchKernelGGL(map_loss_fwd_kernel, grid, dim3(SS_BLOCK), 0, (hipStream_t)stream, H, W, im, depth_sil, gt_im,
+    hipLaunchKernelGGL(rows == 32 ? map_loss_fwd_kernel<32> : map_loss_fwd_kernel<SS_TH>, grid, dim3(SS_BLOCK), 0, (hipStream_t)stream, H, W, im, depth_sil, gt_im,
                        gt_depth, w_im, w_depth, make_window(), state, scratch, out, loss);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GSR_OK : hip_fail(e, "map_loss_fwd");
@@ -637,8 +655,9 @@ int gsr_map_loss_bwd(int H, int W, const float* im, const float* depth_sil, cons
     if (!im || !depth_sil || !gt_im || !gt_depth || !dL_dloss || !state || !dL_dim || !dL_ddepth_sil)
         return fail(GSR_ERR_INVALID_ARG, "map_loss_bwd: null pointer");
     dim3 grid;
-    map_loss_blocks(H, W, grid);
-    hipLaunchKernelGGL(map_loss_bwd_kernel, grid, dim3(SS_BLOCK), 0, (hipStream_t)stream, H, W, im, depth_sil, gt_im,
+    const int rows = map_loss_rows(H, W);
+    map_loss_blocks(H, W, grid, rows);
+    hipLaunchKernelGGL(rows == 32 ? map_loss_bwd_kernel<32> : map_loss_bwd_kernel<SS_TH>, grid, dim3(SS_BLOCK), 0, (hipStream_t)stream, H, W, im, depth_sil, gt_im,
                        gt_depth, w_im, w_depth, make_window(), state, state + 9 * (size_t)H * W, dL_dloss, dL_dim,
                        dL_ddepth_sil);
     const hipError_t e = hipGetLastError();
