@@ -330,6 +330,18 @@ int gsr_forward_dual_static_alive(const gsr_settings* settings, const gsr_gaussi
                                   float* out_depth, int* radii, const unsigned char* alive, gsr_alloc_fn alloc,
                                   void* alloc_ctx, void* stream);
 
+/* The mapping iteration's transform fused into its forward (as
+ * gsr_track_forward_dual_static_xf for tracking): gsr_track_transform_fwd(xform -> gaussians->means3D,
+ * ->rotations, colors2, ->opacities, ->scales) followed by gsr_forward_dual_static_alive(..., xform->alive)
+ * with those arrays, in one pass of preprocess -- the same results bit for bit, without the transform's
+ * launch.  The five arrays are OUTPUTS (xform->store_rendervars must be 1: the mapping backward reads
+ * them); gaussians->colors_precomp the RGB colours [P,3] (input); shs and cov3D_precomp must be NULL
+ * (SH colours are evaluated ahead of preprocess, from the camera-frame means). */
+int gsr_forward_dual_static_xf(const gsr_settings* settings, const gsr_gaussians* gaussians, float* colors2,
+                               const gsr_track_xform* xform, int capacity, unsigned* status, float* out_color,
+                               float* out_color2, float* out_depth, int* radii, gsr_alloc_fn alloc, void* alloc_ctx,
+                               void* stream);
+
 /* torch.optim.Adam (foreach implementation, no weight decay / amsgrad /
  * maximize) over up to 16 float32 tensors in one launch; every tensor shares
  * `step` (>= 1, already incremented) and has its own lr. */

@@ -397,13 +397,16 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
 
 def rasterize_gaussians_dual(background, means3D, colors, colors2, opacity, scales, rotations, scale_modifier,
                              cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh,
-                             degree, campos, prefiltered, capacity=0, status=None, alive=None):
+                             degree, campos, prefiltered, capacity=0, status=None, alive=None, xform=None):
     """gsr_forward_dual: rasterize_gaussians with a second precomputed colour set
     composited in the same pass.  Returns (num_rendered, color, color2, radii,
     geomBuffer, binningBuffer, imgBuffer, depth).  capacity > 0 selects
     gsr_forward_dual_static (no host synchronisation; `status` is a device int32[4]
     receiving the counters, and num_rendered is the capacity).  alive (static mode only): a
-    device uint8 [P] mask, 0 = pruned (gsr_forward_dual_static_alive: culled, radius 0)."""
+    device uint8 [P] mask, 0 = pruned (gsr_forward_dual_static_alive: culled, radius 0).
+    xform (static mode only): (means_world, unnorm_rot, logit_opac, log_scales, scale_cols, cam_q ptr, cam_t ptr,
+    q_stride, w2c) -- the mapping transform inside preprocess (gsr_forward_dual_static_xf): means3D, rotations,
+    colors2, opacity and scales are then its outputs."""
     device = means3D.device
     if device.type != "cuda":
         raise RuntimeError("splatam_amd rasterizer runs on ROCm devices only (no CPU fallback); "
@@ -430,6 +433,20 @@ def rasterize_gaussians_dual(background, means3D, colors, colors2, opacity, scal
                 if alive.device != device or alive.dtype != torch.uint8 or alive.numel() != P or \
                         not alive.is_contiguous():
                     raise RuntimeError("alive must be a contiguous uint8 tensor of P entries on the render device")
+            if xform is not None:
+                outs = (means3D, colors2, opacity, scales, rotations)
+                if any(not t.is_contiguous() or t.dtype != torch.float32 or t.device != device for t in outs):
+                    raise RuntimeError("forward_dual_static_xf: the rendervar outputs must be contiguous float32 "
+                                       "tensors on the device")
+                mw, ur, lo, ls, scols, q_ptr, t_ptr, qs, w2c = xform[:9]
+                xf = GsrTrackXform(means_world=mw.data_ptr(), unnorm_rot=ur.data_ptr(), logit_opac=lo.data_ptr(),
+                                   log_scales=ls.data_ptr(), scale_cols=int(scols), cam_q=q_ptr, cam_t=t_ptr,
+                                   q_stride=int(qs), w2c=w2c.data_ptr(), store_rendervars=1, alive=_ptr(alive))
+                n = lib.gsr_forward_dual_static_xf(ctypes.byref(s), ctypes.byref(g), _ptr(c2), ctypes.byref(xf),
+                                                   int(capacity), status.data_ptr(), out_color.data_ptr(),
+                                                   out_color2.data_ptr(), out_depth.data_ptr(),
+                                                   radii.data_ptr() if P else None, _ALLOC_CB, None, _stream(device))
+            elif alive is not None:
                 n = lib.gsr_forward_dual_static_alive(ctypes.byref(s), ctypes.byref(g), _ptr(c2), int(capacity),
                                                       status.data_ptr(), out_color.data_ptr(), out_color2.data_ptr(),
                                                       out_depth.data_ptr(), radii.data_ptr() if P else None,
@@ -441,8 +458,8 @@ def rasterize_gaussians_dual(background, means3D, colors, colors2, opacity, scal
                                                 out_depth.data_ptr(), radii.data_ptr() if P else None, _ALLOC_CB,
                                                 None, _stream(device))
         else:
-            if alive is not None:
-                raise RuntimeError("the alive mask needs the static (capacity > 0) forward")
+            if alive is not None or xform is not None:
+                raise RuntimeError("the alive mask and the fused transform need the static (capacity > 0) forward")
             n = lib.gsr_forward_dual(ctypes.byref(s), ctypes.byref(g), _ptr(c2), out_color.data_ptr(),
                                      out_color2.data_ptr(), out_depth.data_ptr(), radii.data_ptr() if P else None,
                                      _ALLOC_CB, None, _stream(device))

@@ -165,6 +165,9 @@ SIGNATURES = {
     "gsr_forward_dual_static_alive": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p,
                                               c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                               ALLOC_FN, c_void_p, c_void_p]),
+    "gsr_forward_dual_static_xf": (c_int, [ctypes.POINTER(GsrSettings), ctypes.POINTER(GsrGaussians), c_void_p,
+                                           ctypes.POINTER(GsrTrackXform), c_int, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, ALLOC_FN, c_void_p, c_void_p]),
     # include/gsr_glue.h: Fisher scoring glue
     "gsr_points_to_camera": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gsr_fisher_accumulate": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

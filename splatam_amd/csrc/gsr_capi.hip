@@ -929,6 +929,31 @@ static int track_forward_xf(const gsr_settings* settings, const gsr_gaussians* g
                         stream, capacity, status, &l1, &xf, inst_records, x.alive);
 }
 
+int gsr_forward_dual_static_xf(const gsr_settings* settings, const gsr_gaussians* gaussians, float* colors2,
+                               const gsr_track_xform* xform, int capacity, unsigned* status, float* out_color,
+                               float* out_color2, float* out_depth, int* radii, gsr_alloc_fn alloc, void* alloc_ctx,
+                               void* stream) {
+    if (!xform || !gaussians) return fail(GSR_ERR_INVALID_ARG, "forward_dual_static_xf: null pointer");
+    const gsr_track_xform& x = *xform;
+    if ((x.scale_cols != 1 && x.scale_cols != 3) || x.q_stride < 1)
+        return fail(GSR_ERR_INVALID_ARG, "forward_dual_static_xf: bad sizes");
+    if (!x.store_rendervars) return fail(GSR_ERR_INVALID_ARG, "forward_dual_static_xf: store_rendervars must be 1");
+    if (gaussians->P > 0 && (!x.means_world || !x.unnorm_rot || !x.logit_opac || !x.log_scales || !x.cam_q ||
+                             !x.cam_t || !x.w2c || !gaussians->means3D || !gaussians->rotations ||
+                             !gaussians->opacities || !gaussians->scales || !gaussians->colors_precomp))
+        return fail(GSR_ERR_INVALID_ARG, "forward_dual_static_xf: null pointer");
+    if (gaussians->shs || gaussians->cov3D_precomp)
+        return fail(GSR_ERR_INVALID_ARG, "forward_dual_static_xf: precomputed colours, scales / rotations only");
+    if (!colors2) return fail(GSR_ERR_INVALID_ARG, "colors2 required");
+    if (capacity <= 0 || !status) return fail(GSR_ERR_INVALID_ARG, "static mode needs capacity > 0 and status");
+    TrackXf xf;
+    xf.mw = x.means_world; xf.ur = x.unnorm_rot; xf.lo = x.logit_opac; xf.ls = x.log_scales;
+    xf.scols = x.scale_cols; xf.cq = x.cam_q; xf.ct = x.cam_t; xf.qs = x.q_stride; xf.w2c = x.w2c;
+    xf.store = true;
+    return forward_impl(settings, gaussians, colors2, out_color, out_color2, out_depth, radii, alloc, alloc_ctx,
+                        stream, capacity, status, nullptr, &xf, nullptr, x.alive);
+}
+
 int gsr_track_backward_scratch_floats(int P) { return pose_fuse_scratch_floats(P < 1 ? 1 : P); }
 
 static int track_backward(const gsr_settings* settings, const gsr_gaussians* gaussians, const int* radii,

@@ -304,7 +304,7 @@ class MapAdam:
 class _MapTransform(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means_world, unnorm_rot, logit_opac, log_scales, colors, cam_rots, cam_trans, w2c, time_idx,
-                adam=None):
+                adam=None, defer=None):
         cam_rots, cam_trans = _f32c(cam_rots, "cam_unnorm_rots"), _f32c(cam_trans, "cam_trans")
         means_world, unnorm_rot = _f32c(means_world, "means3D"), _f32c(unnorm_rot, "unnorm_rotations")
         logit_opac, log_scales = _f32c(logit_opac, "logit_opacities"), _f32c(log_scales, "log_scales")
@@ -320,12 +320,16 @@ class _MapTransform(torch.autograd.Function):
         f32 = dict(dtype=torch.float32, device=means_world.device)
         means_cam, rot, dcol = torch.empty(P, 3, **f32), torch.empty(P, 4, **f32), torch.empty(P, 3, **f32)
         opac, scales = torch.empty(P, 1, **f32), torch.empty(P, 3, **f32)
-        rc = lib.gsr_track_transform_fwd(P, means_world.data_ptr(), unnorm_rot.data_ptr(), logit_opac.data_ptr(),
-                                         log_scales.data_ptr(), scols, cam_rots.data_ptr() + 4 * t,
-                                         cam_trans.data_ptr() + 4 * t, T, w2c.data_ptr(), means_cam.data_ptr(),
-                                         rot.data_ptr(), dcol.data_ptr(), opac.data_ptr(), scales.data_ptr(),
-                                         _stream(means_world))
-        _check(rc, "map_transform_fwd")
+        if defer is None:
+            rc = lib.gsr_track_transform_fwd(P, means_world.data_ptr(), unnorm_rot.data_ptr(), logit_opac.data_ptr(),
+                                             log_scales.data_ptr(), scols, cam_rots.data_ptr() + 4 * t,
+                                             cam_trans.data_ptr() + 4 * t, T, w2c.data_ptr(), means_cam.data_ptr(),
+                                             rot.data_ptr(), dcol.data_ptr(), opac.data_ptr(), scales.data_ptr(),
+                                             _stream(means_world))
+            _check(rc, "map_transform_fwd")
+        else:  # the next forward (rasterize_gaussians_dual(xform=...)) forms and writes the five outputs
+            defer.append((means_world, unnorm_rot, logit_opac, log_scales, scols, cam_rots.data_ptr() + 4 * t,
+                          cam_trans.data_ptr() + 4 * t, T, w2c, (cam_rots, cam_trans)))
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(means_world, unnorm_rot, logit_opac, log_scales, colors, cam_rots, means_cam, w2c)
         ctx.meta = (t, T, scols)
@@ -353,7 +357,7 @@ class _MapTransform(torch.autograd.Function):
                 g_means.data_ptr(), p(g_rot), p(g_dcol), p(g_opac), p(g_scales), p(g_col), ctypes.byref(st),
                 _stream(means_world))
             _check(rc, "map_transform_bwd_adam")
-            return (None,) * 10
+            return (None,) * 11
         need = ctx.needs_input_grad
         dm = torch.empty_like(means_world)
         du = torch.empty_like(unnorm_rot) if need[1] else None
@@ -364,7 +368,7 @@ class _MapTransform(torch.autograd.Function):
                                        g_means.data_ptr(), p(g_rot), p(g_dcol), p(g_opac), p(g_scales), dm.data_ptr(),
                                        p(du), p(dl), p(ds), _stream(means_world))
         _check(rc, "map_transform_bwd")
-        return (dm if need[0] else None), du, dl, ds, (g_col if need[4] else None), None, None, None, None, None
+        return (dm if need[0] else None), du, dl, ds, (g_col if need[4] else None), None, None, None, None, None, None
 
 
 def prune_step(it: int, prune_dict: dict):
@@ -393,18 +397,21 @@ def map_prune(params: dict, alive: torch.Tensor, opac_thr: float, big_thr: float
 
 
 def map_transform(params: dict, time_idx: int, w2c: torch.Tensor, color_key: str = "rgb_colors",
-                  adam: MapAdam | None = None):
+                  adam: MapAdam | None = None, defer: list | None = None):
     """transform_to_frame(params, t, gaussians_grad=True, camera_grad=False) (slam_helpers.py:252-304)
     + the rendervar builders (slam_helpers.py:124-139, 196-213, 234-249) for the mapping iteration.
     Returns (means3D_cam, rotations, depth_colors [z,1,z^2], opacities, scales, colours); differentiable
     w.r.t. the Gaussian parameters.  With `adam` the backward applies the mapping optimizer's step in
-    place (no .grad is produced); the parameters must then require grad, or autograd never calls it."""
+    place (no .grad is produced); the parameters must then require grad, or autograd never calls it.
+    defer (a list): no launch -- the transform's inputs are appended to it and the next
+    rasterize_gaussians_dual(xform=defer[0]) forms the five outputs inside its preprocess (static mode,
+    precomputed colours); nothing may read them before that forward."""
     if adam is not None and not params["means3D"].requires_grad:
         raise RuntimeError("map_transform: the fused optimizer step runs in the backward; the Gaussian "
                            "parameters must require grad")
     return _MapTransform.apply(params["means3D"], params["unnorm_rotations"], params["logit_opacities"],
                                params["log_scales"], params[color_key], params["cam_unnorm_rots"].detach(),
-                               params["cam_trans"].detach(), w2c, int(time_idx), adam)
+                               params["cam_trans"].detach(), w2c, int(time_idx), adam, defer)
 
 
 class _MappingLoss(torch.autograd.Function):

@@ -85,7 +85,7 @@ class _RasterizeGaussians(torch.autograd.Function):
 
 def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations,
                              cov3Ds_precomp, raster_settings, capacity=0, status=None, grad2_channels=3,
-                             means2D_grad_sum=False, sh_adam=None, guard_sink=None, alive=None):
+                             means2D_grad_sum=False, sh_adam=None, guard_sink=None, alive=None, xform=None):
     """Two GaussianRasterizer calls on identical geometry fused into one
     rasterization: SplaTAM renders RGB and the [z, 1, z^2]
     depth/silhouette image from the same means / scales / rotations / opacities
@@ -106,7 +106,10 @@ def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opac
     backward (gsr_backward_dual_sh_adam); `sh` then receives no gradient (the caller's own colour step,
     gsr_map_transform_bwd_adam, sees none and leaves the colours to this one).
     alive: uint8 [P] pruning mask for the static mode (0 = removed: culled, zero gradients; GraphMapper's
-    in-frame prune_gaussians)."""
+    in-frame prune_gaussians).
+    xform: the mapping transform deferred into this forward (glue.map_transform(defer=...)): preprocess forms
+    means3D / rotations / colors2 / opacities / scales from the world-frame map and writes them
+    (gsr_forward_dual_static_xf; static mode, precomputed colours)."""
     empty = torch.Tensor([])
     return _RasterizeGaussiansDual.apply(means3D, means2D, empty if sh is None else sh,
                                          empty if colors_precomp is None else colors_precomp, colors2, opacities,
@@ -114,19 +117,19 @@ def rasterize_gaussians_dual(means3D, means2D, sh, colors_precomp, colors2, opac
                                          empty if rotations is None else rotations,
                                          empty if cov3Ds_precomp is None else cov3Ds_precomp, raster_settings,
                                          capacity, status, grad2_channels, bool(means2D_grad_sum), sh_adam,
-                                         guard_sink, alive)
+                                         guard_sink, alive, xform)
 
 
 class _RasterizeGaussiansDual(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, colors2, opacities, scales, rotations, cov3Ds_precomp,
                 raster_settings, capacity, status, grad2_channels, means2D_grad_sum, sh_adam=None, guard_sink=None,
-                alive=None):
+                alive=None, xform=None):
         s = raster_settings
         num_rendered, color, color2, radii, geomBuffer, binningBuffer, imgBuffer, depth = _C.rasterize_gaussians_dual(
             s.bg, means3D, colors_precomp, colors2, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
-            s.campos, s.prefiltered, capacity=capacity, status=status, alive=alive)
+            s.campos, s.prefiltered, capacity=capacity, status=status, alive=alive, xform=xform)
         if guard_sink is not None:
             if capacity > 0:
                 # the fused optimizer steps of this iteration guard on this forward's own counters
@@ -172,7 +175,8 @@ class _RasterizeGaussiansDual(torch.autograd.Function):
             dl2_channels=ctx.grad2_channels if grad_color2 is not None else 3, sh_adam=sa)
         if not n[0]:
             g_m3 = None
-        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None, None, None, None, None, None, None, None
+        return g_m3, g_m2, g_sh, g_col, g_col2, g_op, g_sc, g_rot, g_cov, None, None, None, None, None, None, None, None, \
+            None
 
 
 class GaussianRasterizer(nn.Module):

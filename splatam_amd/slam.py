@@ -12,6 +12,7 @@ itself is splatam_amd.rasterizer (HIP).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -337,6 +338,9 @@ def fused_mapping_eligible(params, curr_data, cfg: MappingConfig) -> bool:
 
 
 _SH_ADAM_FUSED = True  # False: the colour step in gsr_map_transform_bwd_adam (A/B, parity tests)
+# the static mapping forward with precomputed colours forms the transform inside its preprocess
+# (gsr_forward_dual_static_xf); GSR_MAP_XF_FUSED=0 / False: the transform as its own launch (A/B, parity tests)
+_MAP_XF_FUSED = os.environ.get("GSR_MAP_XF_FUSED", "1") != "0"
 
 
 def _get_loss_mapping_fused(params, curr_data, iter_time_idx, cfg: MappingConfig, adam=None, capacity=0, status=None,
@@ -346,7 +350,8 @@ def _get_loss_mapping_fused(params, curr_data, iter_time_idx, cfg: MappingConfig
     static forward's pruning mask (GraphMapper's in-frame prune_gaussians)."""
     from .glue import map_transform, mapping_loss
     key = color_key(params)
-    means, rots, dcol, opac, scales, col = map_transform(params, iter_time_idx, curr_data["w2c"], key, adam)
+    defer = [] if (_MAP_XF_FUSED and capacity > 0 and key != "shs") else None
+    means, rots, dcol, opac, scales, col = map_transform(params, iter_time_idx, curr_data["w2c"], key, adam, defer)
     if means2D is None:
         means2D = torch.zeros(means.shape[0], 3, device=means.device, requires_grad=True)
     sh, colors = (col, None) if key == "shs" else (None, col)
@@ -355,7 +360,8 @@ def _get_loss_mapping_fused(params, curr_data, iter_time_idx, cfg: MappingConfig
     sh_adam = adam if (adam is not None and sh is not None and _SH_ADAM_FUSED) else None
     im, depth_sil, radius, _ = rasterize_gaussians_dual(means, means2D, sh, colors, dcol, opac, scales, rots, None,
                                                         curr_data["cam"], capacity, status, grad2_channels=1,
-                                                        sh_adam=sh_adam, guard_sink=adam, alive=alive)
+                                                        sh_adam=sh_adam, guard_sink=adam, alive=alive,
+                                                        xform=defer[0] if defer else None)
     loss = mapping_loss(im, depth_sil, curr_data["im"], curr_data["depth"], cfg.w_im, cfg.w_depth)
     return loss, radius, means2D
 

@@ -451,3 +451,33 @@ def test_graph_mapper_tile_cull_bitwise(cuda, sh):
     for k in keys:
         assert float((res[3][k] - params[k]).abs().max()) > 0.0, k
         assert torch.equal(res[0][k], res[3][k]), k
+
+
+@pytest.mark.parametrize("prune", [False, True])
+def test_graph_mapper_transform_in_preprocess_bitwise(cuda, monkeypatch, prune):
+    """The mapping transform formed inside the static forward's preprocess (gsr_forward_dual_static_xf, RGB
+    colours) against its own launch (gsr_track_transform_fwd) ahead of gsr_forward_dual_static(_alive): after two
+    6-iteration replays (with in-frame pruning: the alive mask culls inside the fused preprocess too) the
+    parameters are bitwise equal."""
+    from splatam_amd.mapper import GraphMapper
+    _, params, cam = _map_params(cuda, True, False)
+    kfs = _keyframes(params, cam, cuda)
+    key = slam.color_key(params)
+    assert key != "shs"
+    keys = GAUSS_KEYS + (key,)
+    res = {}
+    for fused in (False, True):
+        monkeypatch.setattr(slam, "_MAP_XF_FUSED", fused)
+        p = {k: v.clone() for k, v in params.items()}
+        for k in keys:
+            p[k].requires_grad_(True)
+        mapper = GraphMapper(p, kfs, iters_per_graph=6, seed=7, prune=prune, scene_radius=2.0)
+        for _ in range(2):
+            mapper.run()
+        torch.cuda.synchronize()
+        assert not mapper.overflowed()
+        res[fused] = ({k: p[k].detach().clone() for k in keys}, mapper.alive.clone())
+    for k in keys:
+        assert float((res[True][0][k] - params[k]).abs().max()) > 0.0, k
+        assert torch.equal(res[False][0][k], res[True][0][k]), k
+    assert torch.equal(res[False][1], res[True][1])
