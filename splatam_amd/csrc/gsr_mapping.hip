@@ -43,9 +43,7 @@ constexpr int SS_TW = 64;                 // output tile width (one wave per row
 constexpr int SS_TH = GSR_SS_TH;          // output tile height
 constexpr int SS_R = 5;                   // window radius (window_size 11)
 constexpr int SS_IW = SS_TW + 2 * SS_R;   // 74
-constexpr int SS_IH = SS_TH + 2 * SS_R;   // 26 at 16 rows
 constexpr int SS_BLOCK = 256;
-constexpr int SS_ROWS_PER_THREAD = SS_TH / (SS_BLOCK / SS_TW);  // 4 at 16 rows
 constexpr float SS_C1 = 0.01f * 0.01f;
 constexpr float SS_C2 = 0.03f * 0.03f;
 constexpr int MAP_PARTS = 4;  // sum ssim, sum |x - y|, sum masked |d - gt|, mask count
