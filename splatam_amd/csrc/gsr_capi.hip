@@ -938,12 +938,12 @@ int gsr_forward_dual_static_xf(const gsr_settings* settings, const gsr_gaussians
     if ((x.scale_cols != 1 && x.scale_cols != 3) || x.q_stride < 1)
         return fail(GSR_ERR_INVALID_ARG, "forward_dual_static_xf: bad sizes");
     if (!x.store_rendervars) return fail(GSR_ERR_INVALID_ARG, "forward_dual_static_xf: store_rendervars must be 1");
+    if (gaussians->shs || gaussians->cov3D_precomp)
+        return fail(GSR_ERR_INVALID_ARG, "forward_dual_static_xf: precomputed colours, scales / rotations only");
     if (gaussians->P > 0 && (!x.means_world || !x.unnorm_rot || !x.logit_opac || !x.log_scales || !x.cam_q ||
                              !x.cam_t || !x.w2c || !gaussians->means3D || !gaussians->rotations ||
                              !gaussians->opacities || !gaussians->scales || !gaussians->colors_precomp))
         return fail(GSR_ERR_INVALID_ARG, "forward_dual_static_xf: null pointer");
-    if (gaussians->shs || gaussians->cov3D_precomp)
-        return fail(GSR_ERR_INVALID_ARG, "forward_dual_static_xf: precomputed colours, scales / rotations only");
     if (!colors2) return fail(GSR_ERR_INVALID_ARG, "colors2 required");
     if (capacity <= 0 || !status) return fail(GSR_ERR_INVALID_ARG, "static mode needs capacity > 0 and status");
     TrackXf xf;
