@@ -398,7 +398,9 @@ static int forward_impl(const gsr_settings* settings, const gsr_gaussians* gauss
     cam.tail_exact = capacity <= 0 ? 1 : 0;  // (include/gsr.h: the culled instances, or padding in static mode)
     auto ensure_pinned = [&]() -> int {
         if (!pin.p) {
-            if ((e = hipHostMalloc((void**)&pin.p, 32, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+            // (portable: the buffer serves the launches on device `dev`, whatever device is current here)
+            if ((e = hipHostMalloc((void**)&pin.p, 32,
+                                   hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable)) != hipSuccess)
                 return hip_fail(e, "hipHostMalloc");
             if ((e = hipHostGetDevicePointer((void**)&pin.dp, pin.p, 0)) != hipSuccess)
                 return hip_fail(e, "hipHostGetDevicePointer");
